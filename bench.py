@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: DSSM two-tower training step, query-doc pairs/sec (fwd+bwd+Adam).
+
+Workload (BASELINE.json configs[1]): TRIGRAM_D=30000, widths 300/300/128, BS=1024 queries per
+GPU, NEG=4, bf16 compute (fp32 master weights and Adam state).  A step = one
+sess.run(train_step) of the reference (new_dssm.py:267): forward with batch-stat BN + EMA
+update, backward, dense Adam over all 9.13M parameters (+ one RCCL gradient all-reduce when
+N > 1).  Pairs per step = BS*(NEG+1) per GPU.  Synthetic batches are generated
+on the host and staged in HBM before the timed region; each step just points the plan at the
+next staged batch (no copy).
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+   N>1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+           --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+D, WIDTHS, BS, NEG = 30000, (300, 300, 128), 1024, 4
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batches", type=int, default=8, help="distinct staged batches per rank")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--allreduce", default="torch", choices=["torch", "rccl"])
+    return ap.parse_args()
+
+
+def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int) -> int:
+    """indptr + (index, value) per nnz + one gathered W1 row (n1*s_w) per nnz
+    + fp32 Z1 output row per input row."""
+    return 4 * (rows + 1) + nnz * (4 + 4) + nnz * n1 * s_w + rows * n1 * 4
+
+
+def adam_alg_bytes(n_params: int, shadow_elems: int) -> int:
+    """p, m, v read+write, g read (28 B/param) + bf16 shadow writes."""
+    return 28 * n_params + 2 * shadow_elems
+
+
+def cpu_baseline(seconds: float):
+    """Time the CPU port of the step (oracle/, test infrastructure) on a bounded sample."""
+    from oracle import cpu_port
+    return cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dssm_amd import _lib
+    from dssm_amd.model import DSSM
+    from dssm_amd.data import ZipfColumns, synth_batch
+
+    model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
+    comm = None
+    if world > 1 and args.allreduce == "rccl":
+        from dssm_amd.dist import RcclComm
+        comm = RcclComm(rank, world)
+
+    cols = ZipfColumns(D)
+    staged = []
+    nnzs = []
+    for b in range(args.batches):
+        hb = synth_batch(D, BS, NEG, seed=1000 + rank * 100003 + b, cols=cols)
+        nnzs.append(hb.nnz)
+        staged.append((torch.from_numpy(hb.indptr).to(dev),
+                       torch.from_numpy(hb.indices).to(dev),
+                       torch.from_numpy(hb.values).to(dev)))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+
+    def step(i):
+        ip, ix, vv = staged[i % len(staged)]
+        model.set_batch(indptr=ip, indices=ix, values=vv)
+        model.forward(True)
+        model.backward()
+        if world > 1:
+            if comm is not None:
+                comm.allreduce_(model.grads)
+            else:
+                dist.all_reduce(model.grads)
+        model.apply_adam(1.0 / world)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    for pid in (_lib.PROBE_SPMM_FWD, _lib.PROBE_ADAM, _lib.PROBE_DW1, _lib.PROBE_CSC):
+        model.probe_enable(pid, args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss, acc = model.loss_accuracy()
+
+    probes = {}
+    for name, pid in (("spmm_fwd", _lib.PROBE_SPMM_FWD), ("adam", _lib.PROBE_ADAM),
+                      ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC)):
+        tot, cnt = model.probe_read(pid)
+        probes[name] = tot / max(cnt, 1)  # ms per launch
+    ms_per_step = 1e3 * elapsed / args.steps
+    pairs = world * BS * (NEG + 1) * args.steps
+    value = pairs / elapsed
+
+    # roofline of the dominant HBM-bound kernels (algorithmic bytes / measured avg duration)
+    rows = BS * (2 + NEG)
+    nnz_avg = int(np.mean([nnzs[(args.warmup + i) % len(nnzs)] for i in range(args.steps)]))
+    s_w = 2 if args.dtype == "bf16" else 4
+    n_params = int(model.params.numel())
+    shadow = sum((D if l == 0 else WIDTHS[l - 1]) * WIDTHS[l] for l in range(len(WIDTHS))) if args.dtype == "bf16" else 0
+    kern = {
+        "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes["spmm_fwd"]),
+        "adam": (adam_alg_bytes(n_params, shadow), probes["adam"]),
+    }
+    rl = {}
+    for k, (byt, ms) in kern.items():
+        gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        rl[k] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": byt,
+                 "avg_ms": round(ms, 5), "traffic": None}
+    dominant = max(kern, key=lambda k: kern[k][1])
+
+    out = {
+        "metric": "query-doc pairs/sec (fwd+bwd), TRIGRAM_D=30k NEG=4, 1/2/4/8 MI355X",
+        "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+        "config": {"workload": "dssm C2: TRIGRAM_D=30000, widths 300/300/128, NEG=4, "
+                               "Zipf(1.1) trigram batches ~32 nnz/row, fwd+bwd+dense Adam",
+                   "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
+                   "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
+                   "avg_nnz_per_step": nnz_avg},
+        "roofline": dict(rl[dominant], kernel=dominant),
+        "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
+        "rooflines": rl,
+        "final_loss": round(loss, 5), "final_accuracy": round(acc, 4),
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.destroy()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+"""ctypes binding of libdssm.so (include/dssm.h).
+
+torch is imported first on purpose: the torch wheel bundles its own libamdhip64.so.7; loading
+it before libdssm.so makes the dynamic loader resolve our NEEDED libamdhip64.so.7 to that same
+runtime instance, so torch-allocated device pointers and torch stream handles are valid in our
+kernels.  There is no fallback: if the library is missing every device call raises."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the library load, see module doc)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdssm.so")
+
+DSSM_ABI_VERSION = 1
+DSSM_MAX_LAYERS = 8
+DSSM_F32, DSSM_BF16 = 0, 1
+(BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
+ BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
+PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
+
+
+class DssmError(RuntimeError):
+    pass
+
+
+class dssm_config(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int), ("trigram_d", C.c_int), ("n_layers", C.c_int),
+        ("widths", C.c_int * DSSM_MAX_LAYERS), ("query_bs", C.c_int), ("neg", C.c_int),
+        ("max_nnz", C.c_int), ("compute_dtype", C.c_int), ("gamma", C.c_float),
+        ("bn_eps", C.c_float), ("ema_decay", C.c_float), ("lr", C.c_float), ("beta1", C.c_float),
+        ("beta2", C.c_float), ("adam_eps", C.c_float),
+    ]
+
+
+class dssm_segment(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("offset", C.c_int64), ("rows", C.c_int64),
+                ("cols", C.c_int64)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "dssm_abi_version": (C.c_int, []),
+    "dssm_last_error": (C.c_char_p, []),
+    "dssm_config_check": (C.c_int, [C.POINTER(dssm_config)]),
+    "dssm_param_count": (C.c_int64, [C.POINTER(dssm_config)]),
+    "dssm_param_layout": (C.c_int, [C.POINTER(dssm_config), C.POINTER(dssm_segment), C.c_int]),
+    "dssm_ema_count": (C.c_int64, [C.POINTER(dssm_config)]),
+    "dssm_workspace_bytes": (C.c_size_t, [C.POINTER(dssm_config)]),
+    "dssm_plan_create": (C.c_int, [C.POINTER(dssm_config), _P, C.c_size_t, _P, _P, _P, _P, _P,
+                                   C.POINTER(_P)]),
+    "dssm_plan_destroy": (C.c_int, [_P]),
+    "dssm_plan_buffer": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(_P), C.POINTER(C.c_size_t)]),
+    "dssm_plan_set_batch": (C.c_int, [_P, _P, _P, _P]),
+    "dssm_plan_sync_shadows": (C.c_int, [_P, _P]),
+    "dssm_plan_forward": (C.c_int, [_P, C.c_int, _P]),
+    "dssm_plan_backward": (C.c_int, [_P, _P]),
+    "dssm_plan_adam": (C.c_int, [_P, C.c_float, C.c_float, C.c_float, _P]),
+    "dssm_plan_train_step": (C.c_int, [_P, C.c_float, C.c_float, _P]),
+    "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),
+    "dssm_plan_probe_read": (C.c_int, [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
+    "dssm_spmm_csr_fwd": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,
+                                    C.c_int, _P]),
+    "dssm_dense_fwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
+                                 _P, C.c_int, _P]),
+    "dssm_bn_ws_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "dssm_bn_relu_fwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float,
+                                   C.c_float, C.c_int, C.c_int, _P, C.c_int, _P, _P, _P, _P]),
+    "dssm_cosine_softmax_loss": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, _P,
+                                           _P, _P, _P, _P, _P, _P, _P]),
+    "dssm_comm_unique_id": (C.c_int, [_P]),
+    "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
+    "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),
+    "dssm_comm_destroy": (C.c_int, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libdssm.so (once).  Raises DssmError when it is missing — no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DssmError(f"{path} not found: build it with `python -m dssm_amd.build` "
+                        "(the HIP path has no CPU fallback)")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.dssm_abi_version() != DSSM_ABI_VERSION:
+        raise DssmError("libdssm.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load().dssm_last_error().decode(errors="replace")
+        raise DssmError(f"{what or 'dssm call'} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream

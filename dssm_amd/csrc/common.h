@@ -1,0 +1,78 @@
+// Shared device helpers for the gfx950 DSSM kernels (wave64, bf16 storage = uint16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define DSSM_WAVE 64
+
+__device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned)h) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Broadcast lane j's value (j wave-uniform) -> scalar register.
+__device__ __forceinline__ int bcast_i(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ float bcast_f(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// ---- 8-column vector loads/stores (lane owns 8 consecutive columns) ------------------------
+// nvalid in {4, 8}: widths are multiples of 4, so a lane's group is either full or half.
+__device__ __forceinline__ void load8(const float* p, int nvalid, float (&x)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  if (nvalid > 4) {
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+    x[4] = x[5] = x[6] = x[7] = 0.f;
+  }
+}
+// bf16 rows are padded to ldp(n) (multiple of 8) with zero pads: always a full 16-B load.
+__device__ __forceinline__ void load8(const u16* p, int /*nvalid*/, float (&x)[8]) {
+  uint4 a = *reinterpret_cast<const uint4*>(p);
+  x[0] = __uint_as_float(a.x << 16); x[1] = __uint_as_float(a.x & 0xffff0000u);
+  x[2] = __uint_as_float(a.y << 16); x[3] = __uint_as_float(a.y & 0xffff0000u);
+  x[4] = __uint_as_float(a.z << 16); x[5] = __uint_as_float(a.z & 0xffff0000u);
+  x[6] = __uint_as_float(a.w << 16); x[7] = __uint_as_float(a.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ void store8(float* p, const float (&x)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+}
+__device__ __forceinline__ unsigned pack2bf(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+__device__ __forceinline__ void store8(u16* p, const float (&x)[8]) {
+  uint4 a;
+  a.x = pack2bf(x[0], x[1]); a.y = pack2bf(x[2], x[3]);
+  a.z = pack2bf(x[4], x[5]); a.w = pack2bf(x[6], x[7]);
+  *reinterpret_cast<uint4*>(p) = a;
+}
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<u16>(u16 v) { return bf2f(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ u16 from_f<u16>(float v) { return f2bf(v); }
+
+// BatchNorm affine exactly as tf.nn.batch_normalization: x*inv + (beta - mean*inv).
+// The forward and the backward's ReLU mask both call this, so the mask is bit-identical.
+__device__ __forceinline__ float bn_affine(float z, float inv, float shift) {
+  return __fmaf_rn(z, inv, shift);
+}
+
+__host__ __device__ inline int ldp8(int n) { return (n + 7) & ~7; }
+__host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }

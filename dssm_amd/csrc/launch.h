@@ -1,0 +1,79 @@
+// Host-side launchers for the DSSM kernels (one per .hip translation unit).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dssm {
+
+// ---- sparse (spmm.hip) ----
+// FC1 forward: Z = X*W + b, one wave per CSR row, lane owns 8 output columns.
+hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
+                           const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
+                           int ldz, hipStream_t s);
+// CSR -> CSC transpose of X with a virtual all-ones column D appended (its dW row = db1).
+// cnt: int[D+1] scratch, col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
+hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
+                            int D, int max_nnz, int* cnt, int* col_ptr, int* csc_row,
+                            float* csc_val, int* csc_col, hipStream_t s);
+// dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).
+hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
+                      const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
+                      bool dz_bf16, int lddz, int n, float* G, hipStream_t s);
+
+// ---- dense GEMM (gemm.hip) ----
+enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
+// FWD: C[M x ldc] = A[M x K] * B[K x N] + bias (cols >= N written 0)
+// DA : C[M x ldc] = A[M x K] * B^T where B is [N x K] (ld ldb)
+// DW : C[M x N] += A^T * B, A is [K x M] (ld lda) with a virtual ones row at m == M-1 when
+//      ones_row != 0; B is [K x N]; split-K over the K (rows) dimension with fp32 atomics.
+hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
+                       const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
+                       hipStream_t s);
+
+// ---- batch norm (bn.hip) ----
+struct BnTowers {
+  int row_split;   // rows [0,row_split) tower 0 (query), [row_split, rows) tower 1 (doc)
+  int rows;
+};
+size_t bn_partial_floats(int rows, int ldz, int row_split);
+// Forward statistics + EMA + affine coefficients for both towers.
+// coef layout (floats): [4][2][ldz] = mean_used, rstd, inv, shift per tower.
+hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const float* gamma_q,
+                               const float* beta_q, const float* gamma_d, const float* beta_d,
+                               float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
+                               float* ema_d_var, float eps, float decay, bool train,
+                               float* batch_mean /*[2*n] or null*/, float* batch_var,
+                               float* partial, float* coef, hipStream_t s);
+// out = relu?(Z*inv + shift) in out dtype; pads zero.
+hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
+                           bool relu, void* out, bool out_bf16, hipStream_t s);
+// Backward: dY = dA*(y>0); dgamma/dbeta per tower into grad slots; dZ (out dtype).
+hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
+                         const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
+                         float* dbeta_d, float* partial, float* bcoef, void* dZ, bool dz_bf16,
+                         hipStream_t s);
+
+// ---- cosine / loss (cosine.hip) ----
+hipError_t launch_cosine_loss(const float* y, int ld, int n, int bs, int neg, float gamma,
+                              float* cos_raw, float* cos_sim, float* prob, float* qnorm,
+                              float* loss_j, float* correct_j, float* loss_out, float* dy,
+                              hipStream_t s);
+
+// ---- optimizer (adam.hip) ----
+struct ShadowSeg {
+  int64_t offset;  // arena element offset of the weight block
+  int64_t rows;    // weight rows (bias row excluded)
+  int cols;        // == arena row length
+  int ld;          // shadow leading dimension
+  uint16_t* ptr;   // bf16 shadow
+};
+struct ShadowList {
+  int count;
+  ShadowSeg seg[8];
+};
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float alpha,
+                       float beta1, float beta2, float eps, float grad_scale, ShadowList sh,
+                       hipStream_t s);
+hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
+
+}  // namespace dssm

@@ -1,0 +1,561 @@
+// C-ABI of libdssm.so (include/dssm.h): layout of the parameter arena and the workspace, the
+// training-step plan that sequences the HIP kernels on one stream, the functional entry points
+// behind the Python add_layer / batch_normalization / cosine API, and the RCCL communicator.
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dssm.h"
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(DSSM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Layout {
+  int L = 0, D = 0, BS = 0, NEG = 0, R = 0;
+  bool bf16 = false;
+  int n[DSSM_MAX_LAYERS] = {}, ldp[DSSM_MAX_LAYERS] = {}, in_dim[DSSM_MAX_LAYERS] = {};
+  // parameter arena (fp32 elements)
+  int64_t fc_off[DSSM_MAX_LAYERS] = {};      // [W_l; b_l] as (in+1) x n
+  int64_t bn_off[DSSM_MAX_LAYERS][4] = {};  // q_gamma, q_beta, d_gamma, d_beta
+  int64_t total = 0;
+  int64_t ema_off[DSSM_MAX_LAYERS] = {};     // q_mean, q_var, d_mean, d_var (each n)
+  int64_t ema_total = 0;
+  // workspace (bytes)
+  size_t Z[DSSM_MAX_LAYERS], A[DSSM_MAX_LAYERS], dA[DSSM_MAX_LAYERS], dZ[DSSM_MAX_LAYERS];
+  size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
+      bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS];
+  size_t partial, cos_raw, cos_sim, prob, qnorm, loss_j, correct_j, loss;
+  size_t cnt, col_ptr, csc_row, csc_val, csc_col;
+  size_t ws = 0;
+  int max_nnz = 0;
+};
+
+int check_cfg(const dssm_config* c) {
+  if (!c) return fail(DSSM_E_INVALID, "null config");
+  if (c->abi_version != DSSM_ABI_VERSION) return fail(DSSM_E_INVALID, "abi_version mismatch");
+  if (c->trigram_d < 1) return fail(DSSM_E_INVALID, "trigram_d must be >= 1");
+  if (c->n_layers < 1 || c->n_layers > DSSM_MAX_LAYERS)
+    return fail(DSSM_E_INVALID, "n_layers must be in [1, 8]");
+  for (int l = 0; l < c->n_layers; ++l) {
+    const int w = c->widths[l];
+    if (w < 4 || w > 4096 || (w % 4))
+      return fail(DSSM_E_UNSUPPORTED, "layer widths must be multiples of 4 in [4, 4096]");
+  }
+  if (c->widths[c->n_layers - 1] > 512)
+    return fail(DSSM_E_UNSUPPORTED, "embedding (last) width must be <= 512");
+  if (c->query_bs < 1) return fail(DSSM_E_INVALID, "query_bs must be >= 1");
+  if (c->neg < 1 || c->neg > 15) return fail(DSSM_E_UNSUPPORTED, "NEG must be in [1, 15]");
+  if (c->max_nnz < 0) return fail(DSSM_E_INVALID, "max_nnz must be >= 0");
+  if ((int64_t)c->query_bs * (2 + c->neg) > (1 << 26)) return fail(DSSM_E_UNSUPPORTED, "too many rows");
+  if (c->compute_dtype != DSSM_F32 && c->compute_dtype != DSSM_BF16)
+    return fail(DSSM_E_INVALID, "compute_dtype must be DSSM_F32 or DSSM_BF16");
+  return DSSM_OK;
+}
+
+void make_layout(const dssm_config* c, Layout& Lt) {
+  Lt.L = c->n_layers;
+  Lt.D = c->trigram_d;
+  Lt.BS = c->query_bs;
+  Lt.NEG = c->neg;
+  Lt.R = c->query_bs * (2 + c->neg);
+  Lt.bf16 = c->compute_dtype == DSSM_BF16;
+  Lt.max_nnz = c->max_nnz;
+  int64_t off = 0;
+  for (int l = 0; l < Lt.L; ++l) {
+    Lt.n[l] = c->widths[l];
+    Lt.ldp[l] = ldp8(c->widths[l]);
+    Lt.in_dim[l] = l == 0 ? c->trigram_d : c->widths[l - 1];
+    Lt.fc_off[l] = off;
+    off = align64(off + (int64_t)(Lt.in_dim[l] + 1) * Lt.n[l]);
+  }
+  for (int l = 0; l < Lt.L; ++l)
+    for (int k = 0; k < 4; ++k) {
+      Lt.bn_off[l][k] = off;
+      off = align64(off + Lt.n[l]);
+    }
+  Lt.total = off;
+  int64_t e = 0;
+  for (int l = 0; l < Lt.L; ++l) {
+    Lt.ema_off[l] = e;
+    e += 4 * (int64_t)Lt.n[l];
+  }
+  Lt.ema_total = e;
+
+  size_t w = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = w;
+    w = align256(w + bytes);
+    return o;
+  };
+  const size_t R = Lt.R;
+  const size_t act = Lt.bf16 ? 2 : 4;
+  size_t max_part = 0;
+  for (int l = 0; l < Lt.L; ++l) {
+    const size_t ld = Lt.ldp[l];
+    Lt.Z[l] = take(R * ld * 4);
+    Lt.A[l] = take(R * ld * (l == Lt.L - 1 ? 4 : act));
+    Lt.dA[l] = take(R * ld * 4);
+    Lt.dZ[l] = take(R * ld * act);
+    Lt.coef[l] = take(4 * 2 * ld * 4);
+    Lt.bcoef[l] = take(2 * 2 * ld * 4);
+    Lt.bmean[l] = take(2 * Lt.n[l] * 4);
+    Lt.bvar[l] = take(2 * Lt.n[l] * 4);
+    Lt.shadow[l] = Lt.bf16 ? take((size_t)Lt.in_dim[l] * ld * 2) : 0;
+    max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
+  }
+  Lt.partial = take(max_part * 4);
+  const size_t K = Lt.NEG + 1;
+  Lt.cos_raw = take(K * Lt.BS * 4);
+  Lt.cos_sim = take(K * Lt.BS * 4);
+  Lt.prob = take(K * Lt.BS * 4);
+  Lt.qnorm = take(Lt.BS * 4);
+  Lt.loss_j = take(Lt.BS * 4);
+  Lt.correct_j = take(Lt.BS * 4);
+  Lt.loss = take(2 * 4);
+  Lt.cnt = take((size_t)(Lt.D + 1) * 4);
+  Lt.col_ptr = take((size_t)(Lt.D + 2) * 4);
+  const size_t ent = (size_t)Lt.max_nnz + R;
+  Lt.csc_row = take(ent * 4);
+  Lt.csc_val = take(ent * 4);
+  Lt.csc_col = take(ent * 4);
+  Lt.ws = w;
+}
+
+}  // namespace
+
+struct dssm_plan {
+  dssm_config cfg;
+  Layout Lt;
+  char* ws;
+  float *p, *g, *m, *v, *ema;
+  const int32_t* indptr = nullptr;
+  const int32_t* indices = nullptr;
+  const float* values = nullptr;
+  bool fwd_train_done = false;
+  // Kernel timing probes: HIP events recorded on the launch stream around one kernel family.
+  struct Probe {
+    bool on = false;
+    std::vector<hipEvent_t> ev;  // start/stop pairs
+    int next = 0;
+  } probe[DSSM_PROBE_COUNT];
+
+  void probe_begin(int id, hipStream_t s) {
+    Probe& p = probe[id];
+    if (p.on && p.next + 1 < (int)p.ev.size()) hipEventRecord(p.ev[p.next], s);
+  }
+  void probe_end(int id, hipStream_t s) {
+    Probe& p = probe[id];
+    if (p.on && p.next + 1 < (int)p.ev.size()) {
+      hipEventRecord(p.ev[p.next + 1], s);
+      p.next += 2;
+    }
+  }
+
+  template <typename T> T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+  const void* weight(int l) const {  // what the kernels read for W_l
+    return Lt.bf16 ? (const void*)at<u16>(Lt.shadow[l]) : (const void*)(p + Lt.fc_off[l]);
+  }
+  int weight_ld(int l) const { return Lt.bf16 ? Lt.ldp[l] : Lt.n[l]; }
+  const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
+  dssm::ShadowList shadows() {
+    dssm::ShadowList s;
+    s.count = 0;
+    if (!Lt.bf16) return s;
+    for (int l = 0; l < Lt.L; ++l) {
+      dssm::ShadowSeg& g = s.seg[s.count++];
+      g.offset = Lt.fc_off[l];
+      g.rows = Lt.in_dim[l];
+      g.cols = Lt.n[l];
+      g.ld = Lt.ldp[l];
+      g.ptr = at<uint16_t>(Lt.shadow[l]);
+    }
+    return s;
+  }
+};
+
+extern "C" {
+
+int dssm_abi_version(void) { return DSSM_ABI_VERSION; }
+const char* dssm_last_error(void) { return g_err.c_str(); }
+
+int dssm_config_check(const dssm_config* cfg) { return check_cfg(cfg); }
+
+int64_t dssm_param_count(const dssm_config* cfg) {
+  if (check_cfg(cfg)) return -1;
+  Layout Lt;
+  make_layout(cfg, Lt);
+  return Lt.total;
+}
+
+int64_t dssm_ema_count(const dssm_config* cfg) {
+  if (check_cfg(cfg)) return -1;
+  Layout Lt;
+  make_layout(cfg, Lt);
+  return Lt.ema_total;
+}
+
+int dssm_param_layout(const dssm_config* cfg, dssm_segment* segs, int max_segs) {
+  if (int rc = check_cfg(cfg)) return rc;
+  Layout Lt;
+  make_layout(cfg, Lt);
+  int k = 0;
+  auto put = [&](const char* name, int64_t off, int64_t rows, int64_t cols) {
+    if (segs && k < max_segs) {
+      std::snprintf(segs[k].name, sizeof(segs[k].name), "%s", name);
+      segs[k].offset = off;
+      segs[k].rows = rows;
+      segs[k].cols = cols;
+    }
+    ++k;
+  };
+  char nm[32];
+  for (int l = 0; l < Lt.L; ++l) {
+    std::snprintf(nm, sizeof nm, "fc%d", l + 1);
+    put(nm, Lt.fc_off[l], Lt.in_dim[l] + 1, Lt.n[l]);
+  }
+  static const char* bnn[4] = {"q_gamma", "q_beta", "d_gamma", "d_beta"};
+  for (int l = 0; l < Lt.L; ++l)
+    for (int j = 0; j < 4; ++j) {
+      std::snprintf(nm, sizeof nm, "bn%d_%s", l + 1, bnn[j]);
+      put(nm, Lt.bn_off[l][j], 1, Lt.n[l]);
+    }
+  return k;
+}
+
+size_t dssm_workspace_bytes(const dssm_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  Layout Lt;
+  make_layout(cfg, Lt);
+  return Lt.ws;
+}
+
+int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_bytes, float* params,
+                     float* grads, float* adam_m, float* adam_v, float* ema, dssm_plan** out) {
+  if (int rc = check_cfg(cfg)) return rc;
+  if (!out || !workspace || !params || !grads || !adam_m || !adam_v || !ema)
+    return fail(DSSM_E_INVALID, "null buffer passed to dssm_plan_create");
+  dssm_plan* P = new dssm_plan();
+  P->cfg = *cfg;
+  make_layout(cfg, P->Lt);
+  if (workspace_bytes < P->Lt.ws) {
+    delete P;
+    return fail(DSSM_E_INVALID, "workspace too small");
+  }
+  if ((reinterpret_cast<uintptr_t>(workspace) & 255) || (reinterpret_cast<uintptr_t>(params) & 15)) {
+    delete P;
+    return fail(DSSM_E_INVALID, "workspace must be 256-B aligned and arenas 16-B aligned");
+  }
+  P->ws = static_cast<char*>(workspace);
+  P->p = params;
+  P->g = grads;
+  P->m = adam_m;
+  P->v = adam_v;
+  P->ema = ema;
+  *out = P;
+  return DSSM_OK;
+}
+
+int dssm_plan_destroy(dssm_plan* plan) {
+  if (plan)
+    for (auto& p : plan->probe)
+      for (hipEvent_t e : p.ev) hipEventDestroy(e);
+  delete plan;
+  return DSSM_OK;
+}
+
+int dssm_plan_probe_enable(dssm_plan* P, int id, int max_samples) {
+  if (!P || id < 0 || id >= DSSM_PROBE_COUNT || max_samples < 0)
+    return fail(DSSM_E_INVALID, "bad probe arguments");
+  auto& p = P->probe[id];
+  for (hipEvent_t e : p.ev) hipEventDestroy(e);
+  p.ev.clear();
+  p.next = 0;
+  p.on = max_samples > 0;
+  for (int i = 0; i < 2 * max_samples; ++i) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    p.ev.push_back(e);
+  }
+  return DSSM_OK;
+}
+
+int dssm_plan_probe_read(dssm_plan* P, int id, float* total_ms, int* count) {
+  if (!P || id < 0 || id >= DSSM_PROBE_COUNT || !total_ms || !count)
+    return fail(DSSM_E_INVALID, "bad probe arguments");
+  auto& p = P->probe[id];
+  float tot = 0.f;
+  int n = 0;
+  for (int i = 0; i + 1 < p.next; i += 2) {
+    HIP_TRY(hipEventSynchronize(p.ev[i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, p.ev[i], p.ev[i + 1]));
+    tot += ms;
+    ++n;
+  }
+  *total_ms = tot;
+  *count = n;
+  return DSSM_OK;
+}
+
+int dssm_plan_buffer(const dssm_plan* P, int id, int layer, void** ptr, size_t* bytes) {
+  if (!P || !ptr) return fail(DSSM_E_INVALID, "null plan/ptr");
+  const Layout& Lt = P->Lt;
+  const int K = Lt.NEG + 1;
+  if (layer < 0 || layer >= Lt.L) layer = Lt.L - 1;
+  size_t off = 0, n = 0;
+  switch (id) {
+    case DSSM_BUF_LOSS: off = Lt.loss; n = 8; break;
+    case DSSM_BUF_COS_SIM_RAW: off = Lt.cos_raw; n = (size_t)K * Lt.BS * 4; break;
+    case DSSM_BUF_COS_SIM: off = Lt.cos_sim; n = (size_t)K * Lt.BS * 4; break;
+    case DSSM_BUF_PROB: off = Lt.prob; n = (size_t)K * Lt.BS * 4; break;
+    case DSSM_BUF_QUERY_NORM: off = Lt.qnorm; n = (size_t)Lt.BS * 4; break;
+    case DSSM_BUF_EMBED: off = Lt.A[Lt.L - 1]; n = (size_t)Lt.R * Lt.ldp[Lt.L - 1] * 4; break;
+    case DSSM_BUF_Z: off = Lt.Z[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * 4; break;
+    case DSSM_BUF_BATCH_MEAN: off = Lt.bmean[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
+    case DSSM_BUF_BATCH_VAR: off = Lt.bvar[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
+    case DSSM_BUF_DZ: off = Lt.dZ[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * (Lt.bf16 ? 2 : 4); break;
+    default: return fail(DSSM_E_INVALID, "unknown buffer id");
+  }
+  *ptr = P->ws + off;
+  if (bytes) *bytes = n;
+  return DSSM_OK;
+}
+
+int dssm_plan_set_batch(dssm_plan* P, const int32_t* indptr, const int32_t* indices,
+                        const float* values) {
+  if (!P || !indptr || (!indices && P->Lt.max_nnz) || (!values && P->Lt.max_nnz))
+    return fail(DSSM_E_INVALID, "null batch pointer");
+  P->indptr = indptr;
+  P->indices = indices;
+  P->values = values;
+  return DSSM_OK;
+}
+
+int dssm_plan_sync_shadows(dssm_plan* P, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!P->Lt.bf16) return DSSM_OK;
+  HIP_TRY(dssm::launch_shadow_sync(P->p, P->shadows(), (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!P->indptr) return fail(DSSM_E_INVALID, "no batch set (dssm_plan_set_batch)");
+  hipStream_t s = (hipStream_t)stream;
+  const Layout& Lt = P->Lt;
+  const dssm_config& c = P->cfg;
+  const dssm::BnTowers tw{Lt.BS, Lt.R};
+  P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
+  HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
+                                P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
+                                Lt.ldp[0], s));
+  P->probe_end(DSSM_PROBE_SPMM_FWD, s);
+  for (int l = 0; l < Lt.L; ++l) {
+    float* ema = P->ema + Lt.ema_off[l];
+    const int n = Lt.n[l];
+    HIP_TRY(dssm::launch_bn_fwd_stats(
+        P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
+        P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
+        c.bn_eps, c.ema_decay, train != 0, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
+        P->at<float>(Lt.partial), P->at<float>(Lt.coef[l]), s));
+    const bool last = l == Lt.L - 1;
+    HIP_TRY(dssm::launch_bn_apply(P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw,
+                                  P->at<float>(Lt.coef[l]), true, P->ws + Lt.A[l],
+                                  Lt.bf16 && !last, s));
+    if (!last)
+      HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, Lt.bf16, Lt.R, Lt.n[l + 1], n, P->ws + Lt.A[l],
+                                Lt.ldp[l], P->weight(l + 1), P->weight_ld(l + 1),
+                                P->at<float>(Lt.Z[l + 1]), Lt.ldp[l + 1], P->bias(l + 1), false, s));
+  }
+  const int lL = Lt.L - 1;
+  HIP_TRY(dssm::launch_cosine_loss(
+      P->at<float>(Lt.A[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG, c.gamma,
+      P->at<float>(Lt.cos_raw), P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob),
+      P->at<float>(Lt.qnorm), P->at<float>(Lt.loss_j), P->at<float>(Lt.correct_j),
+      P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]), s));
+  P->fwd_train_done = train != 0;
+  return DSSM_OK;
+}
+
+int dssm_plan_backward(dssm_plan* P, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!P->fwd_train_done) return fail(DSSM_E_INVALID, "backward needs a train-mode forward first");
+  hipStream_t s = (hipStream_t)stream;
+  const Layout& Lt = P->Lt;
+  const dssm::BnTowers tw{Lt.BS, Lt.R};
+  P->probe_begin(DSSM_PROBE_CSC, s);
+  HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
+                                 P->at<int>(Lt.cnt), P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
+                                 P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s));
+  P->probe_end(DSSM_PROBE_CSC, s);
+  for (int l = Lt.L - 1; l >= 0; --l) {
+    const int n = Lt.n[l];
+    HIP_TRY(dssm::launch_bn_bwd(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), Lt.ldp[l], n, tw,
+                                P->at<float>(Lt.coef[l]), P->g + Lt.bn_off[l][0],
+                                P->g + Lt.bn_off[l][1], P->g + Lt.bn_off[l][2],
+                                P->g + Lt.bn_off[l][3], P->at<float>(Lt.partial),
+                                P->at<float>(Lt.bcoef[l]), P->ws + Lt.dZ[l], Lt.bf16, s));
+    if (l > 0) {
+      const int kin = Lt.in_dim[l];
+      float* gw = P->g + Lt.fc_off[l];
+      HIP_TRY(hipMemsetAsync(gw, 0, sizeof(float) * (size_t)(kin + 1) * n, s));
+      HIP_TRY(dssm::launch_gemm(dssm::GEMM_DW, Lt.bf16, kin + 1, n, Lt.R, P->ws + Lt.A[l - 1],
+                                Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true, s));
+      HIP_TRY(dssm::launch_gemm(dssm::GEMM_DA, Lt.bf16, Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l],
+                                P->weight(l), P->weight_ld(l), P->at<float>(Lt.dA[l - 1]),
+                                Lt.ldp[l - 1], nullptr, false, s));
+    } else {
+      P->probe_begin(DSSM_PROBE_DW1, s);
+      HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
+                               P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), Lt.D, Lt.R,
+                               Lt.max_nnz, P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0], n,
+                               P->g + Lt.fc_off[0], s));
+      P->probe_end(DSSM_PROBE_DW1, s);
+    }
+  }
+  return DSSM_OK;
+}
+
+int dssm_plan_adam(dssm_plan* P, float beta1_power, float beta2_power, float grad_scale,
+                   void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  const dssm_config& c = P->cfg;
+  const float one = 1.0f;
+  const float alpha = c.lr * std::sqrt(one - beta2_power) / (one - beta1_power);
+  P->probe_begin(DSSM_PROBE_ADAM, (hipStream_t)stream);
+  HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, P->Lt.total, alpha, c.beta1, c.beta2,
+                            c.adam_eps, grad_scale, P->shadows(), (hipStream_t)stream));
+  P->probe_end(DSSM_PROBE_ADAM, (hipStream_t)stream);
+  return DSSM_OK;
+}
+
+int dssm_plan_train_step(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
+  if (int rc = dssm_plan_forward(P, 1, stream)) return rc;
+  if (int rc = dssm_plan_backward(P, stream)) return rc;
+  return dssm_plan_adam(P, beta1_power, beta2_power, 1.0f, stream);
+}
+
+// ---- functional entry points ------------------------------------------------------------
+int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                      const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
+                      int ldz, void* stream) {
+  if (!indptr || !W || !bias || !Z || rows < 0 || n < 4 || (n % 4) || ldz < n || (ldz % 8) ||
+      ldw < n || (ldw % 4))
+    return fail(DSSM_E_INVALID, "dssm_spmm_csr_fwd: bad arguments (n%4==0, ldz%8==0, ldw>=n)");
+  if (w_dtype == DSSM_BF16 && ldw < ldp8(n))
+    return fail(DSSM_E_INVALID, "bf16 W needs ldw >= round_up(n, 8) with zero pads");
+  HIP_TRY(dssm::launch_spmm_fwd(indptr, indices, values, rows, W, w_dtype == DSSM_BF16, ldw, n,
+                                bias, Z, ldz, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                   const float* bias, float* Z, int ldz, void* stream) {
+  if (!A || !W || !bias || !Z || M < 0 || K < 1 || N < 1 || lda < K || ldw < N || ldz < N ||
+      (lda % 8) || (ldw % 4) || (ldz % 4) || (dtype == DSSM_BF16 && (ldw % 8)))
+    return fail(DSSM_E_INVALID, "dssm_dense_fwd: bad arguments");
+  HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, dtype == DSSM_BF16, M, N, K, A, lda, W, ldw, Z, ldz,
+                            bias, false, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+size_t dssm_bn_ws_bytes(int rows, int ldz) {
+  return align256(dssm::bn_partial_floats(rows, ldz, rows) * 4) + 4 * 2 * (size_t)ldz * 4;
+}
+
+int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
+                     float* ema_mean, float* ema_var, float eps, float decay, int train, int relu,
+                     void* out, int out_dtype, float* batch_mean, float* batch_var, void* ws,
+                     void* stream) {
+  if (!Z || !gamma || !beta || !ema_mean || !ema_var || !out || !ws || rows < 1 || n < 4 ||
+      (n % 4) || ldz != ldp8(n))
+    return fail(DSSM_E_INVALID, "dssm_bn_relu_fwd: bad arguments (ldz must be round_up(n,8))");
+  hipStream_t s = (hipStream_t)stream;
+  const dssm::BnTowers tw{rows, rows};
+  float* part = static_cast<float*>(ws);
+  float* coef = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                         align256(dssm::bn_partial_floats(rows, ldz, rows) * 4));
+  HIP_TRY(dssm::launch_bn_fwd_stats(Z, ldz, n, tw, gamma, beta, gamma, beta, ema_mean, ema_var,
+                                    ema_mean, ema_var, eps, decay, train != 0, batch_mean,
+                                    batch_var, part, coef, s));
+  HIP_TRY(dssm::launch_bn_apply(Z, ldz, n, tw, coef, relu != 0, out, out_dtype == DSSM_BF16, s));
+  return DSSM_OK;
+}
+
+int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
+                             float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
+                             float* loss, float* dy, float* ws, void* stream) {
+  if (!y || !cos_sim_raw || !cos_sim || !prob || !query_norm || !loss || !dy || !ws ||
+      query_bs < 1 || neg < 1 || neg > 15 || n < 1 || n > 512 || ld < n)
+    return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss: bad arguments");
+  HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, cos_sim_raw, cos_sim, prob,
+                                   query_norm, ws, ws + query_bs, loss, dy, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+// ---- RCCL ---------------------------------------------------------------------------------
+static ncclComm_t g_comm = nullptr;
+
+int dssm_comm_unique_id(void* out128) {
+  if (!out128) return fail(DSSM_E_INVALID, "null id buffer");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(DSSM_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out128, &id, 128);
+  return DSSM_OK;
+}
+
+int dssm_comm_init(int rank, int world, const void* unique_id128) {
+  if (!unique_id128 || world < 1 || rank < 0 || rank >= world)
+    return fail(DSSM_E_INVALID, "dssm_comm_init: bad arguments");
+  if (g_comm) return fail(DSSM_E_INVALID, "communicator already initialised");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id128, 128);
+  ncclResult_t r = ncclCommInitRank(&g_comm, world, id, rank);
+  if (r != ncclSuccess) {
+    g_comm = nullptr;
+    return fail(DSSM_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  return DSSM_OK;
+}
+
+int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, g_comm,
+                                 (hipStream_t)stream);
+  if (r != ncclSuccess) return fail(DSSM_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return DSSM_OK;
+}
+
+int dssm_comm_destroy(void) {
+  if (g_comm) {
+    ncclCommDestroy(g_comm);
+    g_comm = nullptr;
+  }
+  return DSSM_OK;
+}
+
+}  // extern "C"

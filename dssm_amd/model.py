@@ -1,0 +1,271 @@
+"""The DSSM training step on one MI355X: device arenas + the libdssm.so plan.
+
+This is the engine behind the reference's graph (new_dssm.py:104-217).  All state lives in
+torch-allocated HBM used purely as storage:
+
+* one flat fp32 parameter arena ([W_l; b_l] blocks, then BN gamma/beta per tower), plus gradient,
+  Adam m and Adam v arenas of the same layout (one RCCL all-reduce covers every gradient);
+* an EMA arena for the BN moving averages (non-trainable, as in TF);
+* one workspace carved by the library (activations, BN coefficients, CSC transpose, outputs).
+
+No torch op runs on the hot path: forward/backward/Adam are three C-ABI calls that enqueue
+HIP kernels on the caller's stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+from .data import CSRBatch
+
+
+class DSSM:
+    def __init__(self, trigram_d: int, widths, query_bs: int, neg: int = 4, lr: float = 0.01,
+                 dtype: str = "bf16", max_nnz: Optional[int] = None, device=None, seed: int = 0,
+                 gamma: float = 20.0, bn_eps: float = 1e-3, ema_decay: float = 0.5,
+                 beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-8,
+                 init: bool = True):
+        lib = _lib.load()
+        self.lib = lib
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        widths = list(widths)
+        self.trigram_d, self.widths, self.query_bs, self.neg = trigram_d, widths, query_bs, neg
+        self.rows = query_bs * (2 + neg)
+        self.dtype = dtype
+        if max_nnz is None:
+            max_nnz = self.rows * 96
+        self.max_nnz = int(max_nnz)
+        cfg = _lib.dssm_config()
+        cfg.abi_version = _lib.DSSM_ABI_VERSION
+        cfg.trigram_d = trigram_d
+        cfg.n_layers = len(widths)
+        for i, w in enumerate(widths):
+            cfg.widths[i] = w
+        cfg.query_bs, cfg.neg, cfg.max_nnz = query_bs, neg, self.max_nnz
+        cfg.compute_dtype = {"bf16": _lib.DSSM_BF16, "fp32": _lib.DSSM_F32}[dtype]
+        cfg.gamma, cfg.bn_eps, cfg.ema_decay = gamma, bn_eps, ema_decay
+        cfg.lr, cfg.beta1, cfg.beta2, cfg.adam_eps = lr, beta1, beta2, adam_eps
+        self.cfg = cfg
+        self.lr, self.beta1, self.beta2 = lr, beta1, beta2
+        check(lib.dssm_config_check(C.byref(cfg)), "config")
+        n = lib.dssm_param_count(C.byref(cfg))
+        nseg = lib.dssm_param_layout(C.byref(cfg), None, 0)
+        segs = (_lib.dssm_segment * nseg)()
+        lib.dssm_param_layout(C.byref(cfg), segs, nseg)
+        self.segments = {s.name.decode(): (int(s.offset), int(s.rows), int(s.cols)) for s in segs}
+        dev = self.device
+        f32 = torch.float32
+        self.params = torch.zeros(n, dtype=f32, device=dev)
+        self.grads = torch.zeros(n, dtype=f32, device=dev)
+        self.adam_m = torch.zeros(n, dtype=f32, device=dev)
+        self.adam_v = torch.zeros(n, dtype=f32, device=dev)
+        self.ema = torch.zeros(lib.dssm_ema_count(C.byref(cfg)), dtype=f32, device=dev)
+        wsb = lib.dssm_workspace_bytes(C.byref(cfg))
+        self.workspace = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+        self._indptr = torch.zeros(self.rows + 1, dtype=torch.int32, device=dev)
+        self._indices = torch.zeros(max(1, self.max_nnz), dtype=torch.int32, device=dev)
+        self._values = torch.zeros(max(1, self.max_nnz), dtype=f32, device=dev)
+        h = C.c_void_p()
+        check(lib.dssm_plan_create(C.byref(cfg), ptr(self.workspace), wsb, ptr(self.params),
+                                   ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
+                                   ptr(self.ema), C.byref(h)), "plan_create")
+        self._plan = h
+        self.beta1_power = np.float32(beta1)
+        self.beta2_power = np.float32(beta2)
+        self.global_step = 0
+        if init:
+            self.init_params(seed)
+
+    # ---- parameters ------------------------------------------------------------------------
+    def segment(self, name: str) -> torch.Tensor:
+        off, rows, cols = self.segments[name]
+        return self.params[off:off + rows * cols].view(rows, cols)
+
+    def _named_views(self, arena: torch.Tensor) -> Dict[str, torch.Tensor]:
+        out = {}
+        for l in range(1, len(self.widths) + 1):
+            off, rows, cols = self.segments[f"fc{l}"]
+            blk = arena[off:off + rows * cols].view(rows, cols)
+            out[f"W{l}"] = blk[:-1]
+            out[f"b{l}"] = blk[-1]
+            for t in ("q", "d"):
+                for k in ("gamma", "beta"):
+                    o, _, c = self.segments[f"bn{l}_{t}_{k}"]
+                    out[f"bn{l}_{t}_{k}"] = arena[o:o + c]
+        return out
+
+    def named_params(self) -> Dict[str, torch.Tensor]:
+        """Views keyed like the reference variables: W{l}, b{l}, bn{l}_{q|d}_{gamma|beta}."""
+        return self._named_views(self.params)
+
+    def named_grads(self) -> Dict[str, torch.Tensor]:
+        return self._named_views(self.grads)
+
+    def named_ema(self) -> Dict[str, torch.Tensor]:
+        out, o = {}, 0
+        for l, n in enumerate(self.widths, start=1):
+            for t in ("q", "d"):
+                out[f"bn{l}_{t}_mean"] = self.ema[o:o + n]
+                out[f"bn{l}_{t}_var"] = self.ema[o + n:o + 2 * n]
+                o += 2 * n
+        return out
+
+    def init_params(self, seed: int = 0):
+        """Reference init (new_dssm.py:118-120, :139-142, :75-76) from numpy PCG64(seed):
+        W, b ~ U(-r, r), r = sqrt(6/(fan_in+fan_out)); gamma = 1; beta = 0."""
+        rng = np.random.Generator(np.random.PCG64(seed))
+        dims = [self.trigram_d] + self.widths
+        host = {}
+        for l in range(1, len(self.widths) + 1):
+            fi, fo = dims[l - 1], dims[l]
+            r = np.sqrt(6.0 / (fi + fo))
+            host[f"W{l}"] = rng.uniform(-r, r, size=(fi, fo)).astype(np.float32)
+            host[f"b{l}"] = rng.uniform(-r, r, size=(fo,)).astype(np.float32)
+            for t in ("q", "d"):
+                host[f"bn{l}_{t}_gamma"] = np.ones(fo, np.float32)
+                host[f"bn{l}_{t}_beta"] = np.zeros(fo, np.float32)
+        self.load_params(host)
+
+    def load_params(self, host: Dict[str, np.ndarray], ema: Optional[Dict[str, np.ndarray]] = None):
+        views = self.named_params()
+        for k, v in host.items():
+            views[k].copy_(torch.as_tensor(np.asarray(v, np.float32)).reshape(views[k].shape))
+        if ema is not None:
+            ev = self.named_ema()
+            for k, v in ema.items():
+                ev[k].copy_(torch.as_tensor(np.asarray(v, np.float32)))
+        check(self.lib.dssm_plan_sync_shadows(self._plan, stream_ptr()), "sync_shadows")
+
+    # ---- feed --------------------------------------------------------------------------------
+    def set_batch(self, batch: CSRBatch = None, indptr=None, indices=None, values=None,
+                  non_blocking: bool = False):
+        """Point the plan at one step's combined CSR.  Host batches are copied into the model's
+        device staging buffers; device tensors are used in place (no copy)."""
+        if batch is not None:
+            if batch.rows != self.rows:
+                raise ValueError(f"batch has {batch.rows} rows, model expects {self.rows}")
+            if batch.nnz > self.max_nnz:
+                raise ValueError(f"batch nnz {batch.nnz} exceeds max_nnz {self.max_nnz}")
+            nz = batch.nnz
+            self._indptr.copy_(torch.from_numpy(batch.indptr), non_blocking=non_blocking)
+            if nz:
+                self._indices[:nz].copy_(torch.from_numpy(batch.indices), non_blocking=non_blocking)
+                self._values[:nz].copy_(torch.from_numpy(batch.values), non_blocking=non_blocking)
+            indptr, indices, values = self._indptr, self._indices, self._values
+        for t, dt in ((indptr, torch.int32), (indices, torch.int32), (values, torch.float32)):
+            if t.device != self.device or t.dtype != dt or not t.is_contiguous():
+                raise ValueError("device batch tensors must be contiguous int32/int32/float32 on the model device")
+        self._batch_refs = (indptr, indices, values)
+        check(self.lib.dssm_plan_set_batch(self._plan, ptr(indptr), ptr(indices), ptr(values)),
+              "set_batch")
+
+    # ---- step ---------------------------------------------------------------------------------
+    def forward(self, train: bool = True, stream=None):
+        check(self.lib.dssm_plan_forward(self._plan, 1 if train else 0, stream_ptr(stream)), "forward")
+
+    def backward(self, stream=None):
+        check(self.lib.dssm_plan_backward(self._plan, stream_ptr(stream)), "backward")
+
+    def apply_adam(self, grad_scale: float = 1.0, stream=None):
+        check(self.lib.dssm_plan_adam(self._plan, float(self.beta1_power), float(self.beta2_power),
+                                      float(grad_scale), stream_ptr(stream)), "adam")
+        self.beta1_power = np.float32(self.beta1_power * np.float32(self.beta1))
+        self.beta2_power = np.float32(self.beta2_power * np.float32(self.beta2))
+        self.global_step += 1
+
+    def train_step(self, stream=None):
+        """One sess.run(train_step) (new_dssm.py:267): forward(train) + backward + Adam."""
+        self.forward(True, stream)
+        self.backward(stream)
+        self.apply_adam(1.0, stream)
+
+    # ---- kernel timing probes (HIP events on the launch stream) -------------------------------
+    def probe_enable(self, probe_id: int, max_samples: int):
+        check(self.lib.dssm_plan_probe_enable(self._plan, probe_id, max_samples), "probe_enable")
+
+    def probe_read(self, probe_id: int):
+        tot, cnt = C.c_float(), C.c_int()
+        check(self.lib.dssm_plan_probe_read(self._plan, probe_id, C.byref(tot), C.byref(cnt)), "probe_read")
+        return float(tot.value), int(cnt.value)
+
+    # ---- fetches ------------------------------------------------------------------------------
+    def _buf(self, bid: int, layer: int = -1):
+        p, nb = C.c_void_p(), C.c_size_t()
+        check(self.lib.dssm_plan_buffer(self._plan, bid, layer, C.byref(p), C.byref(nb)), "buffer")
+        return p.value - self.workspace.data_ptr(), nb.value
+
+    def buffer(self, bid: int, layer: int = -1, dtype=torch.float32) -> torch.Tensor:
+        off, nb = self._buf(bid, layer)
+        return self.workspace[off:off + nb].view(dtype)
+
+    def loss_accuracy(self):
+        la = self.buffer(_lib.BUF_LOSS).cpu().numpy()
+        return float(la[0]), float(la[1])
+
+    def fetch(self, name: str) -> np.ndarray:
+        K = self.neg + 1
+        BS = self.query_bs
+        if name == "loss":
+            return np.float32(self.loss_accuracy()[0])
+        if name == "accuracy":
+            return np.float32(self.loss_accuracy()[1])
+        if name == "cos_sim_raw":
+            return self.buffer(_lib.BUF_COS_SIM_RAW).cpu().numpy().reshape(K * BS, 1)
+        if name == "cos_sim":
+            return self.buffer(_lib.BUF_COS_SIM).cpu().numpy().reshape(BS, K)
+        if name == "prob":
+            return self.buffer(_lib.BUF_PROB).cpu().numpy().reshape(BS, K)
+        if name == "query_norm_single":
+            return self.buffer(_lib.BUF_QUERY_NORM).cpu().numpy().reshape(BS, 1)
+        if name.startswith("embedding"):
+            n = self.widths[-1]
+            ld = (n + 7) // 8 * 8
+            y = self.buffer(_lib.BUF_EMBED).cpu().numpy().reshape(self.rows, ld)[:, :n]
+            return {"embedding_query_y": y[:BS], "embedding_doc_positive_y": y[BS:2 * BS],
+                    "embedding_doc_negative_y": y[2 * BS:], "embedding_all": y}[name]
+        raise KeyError(name)
+
+    def batch_moments(self, layer: int):
+        n = self.widths[layer - 1]
+        m = self.buffer(_lib.BUF_BATCH_MEAN, layer - 1).cpu().numpy().reshape(2, n)
+        v = self.buffer(_lib.BUF_BATCH_VAR, layer - 1).cpu().numpy().reshape(2, n)
+        return {"q": (m[0], v[0]), "d": (m[1], v[1])}
+
+    # ---- checkpoint (new_dssm.py:248,331 tf.train.Saver) ---------------------------------------
+    def state_dict(self) -> Dict[str, np.ndarray]:
+        return {"params": self.params.cpu().numpy(), "adam_m": self.adam_m.cpu().numpy(),
+                "adam_v": self.adam_v.cpu().numpy(), "ema": self.ema.cpu().numpy(),
+                "beta_powers": np.array([self.beta1_power, self.beta2_power], np.float32),
+                "global_step": np.array([self.global_step], np.int64)}
+
+    def load_state_dict(self, sd: Dict[str, np.ndarray]):
+        for name, t in (("params", self.params), ("adam_m", self.adam_m), ("adam_v", self.adam_v),
+                        ("ema", self.ema)):
+            a = np.asarray(sd[name], np.float32)
+            if a.shape != tuple(t.shape):
+                raise ValueError(f"checkpoint {name} shape {a.shape} != {tuple(t.shape)}")
+            t.copy_(torch.from_numpy(a))
+        self.beta1_power, self.beta2_power = (np.float32(x) for x in sd["beta_powers"])
+        self.global_step = int(sd["global_step"][0])
+        check(self.lib.dssm_plan_sync_shadows(self._plan, stream_ptr()), "sync_shadows")
+
+    def save(self, path: str):
+        np.savez(path, **self.state_dict())
+
+    def restore(self, path: str):
+        with np.load(path, allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})
+
+    def __del__(self):
+        try:
+            if getattr(self, "_plan", None) is not None and self.lib is not None:
+                torch.cuda.synchronize(self.device)
+                self.lib.dssm_plan_destroy(self._plan)
+                self._plan = None
+        except Exception:
+            pass

@@ -1,0 +1,159 @@
+/*
+ * dssm.h — C-ABI of libdssm.so, the MI355X (gfx950) DSSM two-tower training path.
+ *
+ * The reference (MC-Zealot/dssm) has no FFI: its boundary is the TF1.x graph-building
+ * Python functions plus the Session feed/fetch contract.  Each entry point below names the
+ * reference interface it replaces (file:line under the reference repo).  The Python host
+ * mirror of that interface (dssm_amd/api.py) is the only caller; INTEGRATION.md shows the
+ * ctypes binding.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer owned by the caller unless stated otherwise; the
+ *     library allocates nothing on the hot path (size the workspace with
+ *     dssm_workspace_bytes()).
+ *   - Every call is asynchronous on the given hipStream_t (passed as void*; NULL = default).
+ *   - Return 0 on success, a negative DSSM_E* code on failure; dssm_last_error() returns a
+ *     thread-local message for the last failure.  No C++ exception crosses the ABI.
+ *   - A plan must not be used from two host threads at once.  Data parallelism is one process
+ *     per GPU (one plan per process).
+ *   - Dense activation buffers are row-major with a padded leading dimension
+ *     ldp(n) = round_up(n, 8); pad columns are kept at zero.
+ */
+#ifndef DSSM_H
+#define DSSM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSSM_ABI_VERSION 1
+#define DSSM_MAX_LAYERS 8
+
+enum { DSSM_OK = 0, DSSM_E_INVALID = -1, DSSM_E_HIP = -2, DSSM_E_RCCL = -3, DSSM_E_UNSUPPORTED = -4 };
+enum { DSSM_F32 = 0, DSSM_BF16 = 1 };
+
+/* Model/step configuration (semantic_matching/dssm/config.py:19-28 + new_dssm.py constants). */
+typedef struct dssm_config {
+  int abi_version;              /* must be DSSM_ABI_VERSION */
+  int trigram_d;                /* TRIGRAM_D: sparse input width (new_dssm.py:44) */
+  int n_layers;                 /* number of FC(+BN+ReLU) layers: 2 in new_dssm.py, 3 in the paper shape */
+  int widths[DSSM_MAX_LAYERS];  /* L1_N, L2_N, ... (config.py:20-21); each a multiple of 4, <= 4096 */
+  int query_bs;                 /* query_BS (config.py:19) */
+  int neg;                      /* NEG (config.py:28); 1..15 */
+  int max_nnz;                  /* capacity: non-zeros of one step over all BS*(2+NEG) rows */
+  int compute_dtype;            /* DSSM_F32 (parity mode) or DSSM_BF16 (perf mode, fp32 master/optimizer) */
+  float gamma;                  /* cosine scale, 20 (new_dssm.py:199) */
+  float bn_eps;                 /* 1e-3 (new_dssm.py:87) */
+  float ema_decay;              /* 0.5 (new_dssm.py:78) */
+  float lr, beta1, beta2, adam_eps; /* AdamOptimizer(conf.learning_rate) TF1.x defaults (new_dssm.py:217) */
+} dssm_config;
+
+/* One trainable-variable segment of the flat parameter arena (fp32 elements). */
+typedef struct dssm_segment {
+  char name[32];   /* "fc1" = [W1; b1] as ((in+1) x out), "bn1_q_gamma", ... */
+  int64_t offset;  /* element offset in the arena (multiple of 64) */
+  int64_t rows, cols;
+} dssm_segment;
+
+typedef struct dssm_plan dssm_plan;
+
+/* Plan-owned buffers the caller may read (fetches) — ids for dssm_plan_buffer(). */
+enum {
+  DSSM_BUF_LOSS = 0,        /* float[2]: loss (new_dssm.py:209), accuracy (:221) */
+  DSSM_BUF_COS_SIM_RAW,     /* float[(NEG+1)*BS], index k*BS+j (new_dssm.py:197) */
+  DSSM_BUF_COS_SIM,         /* float[BS*(NEG+1)], 20*cos (new_dssm.py:199) */
+  DSSM_BUF_PROB,            /* float[BS*(NEG+1)] softmax (new_dssm.py:206) */
+  DSSM_BUF_QUERY_NORM,      /* float[BS] query_norm_single (new_dssm.py:187) */
+  DSSM_BUF_EMBED,           /* float[R*ldp(n_L)] embeddings: rows [q; pos; neg] (new_dssm.py:156-158) */
+  DSSM_BUF_Z,               /* float[R*ldp(n_l)] pre-BN activations of layer `layer` */
+  DSSM_BUF_BATCH_MEAN,      /* float[2*n_l]: batch mean, tower q then d (new_dssm.py:77) */
+  DSSM_BUF_BATCH_VAR,       /* float[2*n_l] */
+  DSSM_BUF_DZ,              /* dZ of layer `layer` (compute dtype, R*ldp) */
+  DSSM_BUF_COUNT
+};
+
+int dssm_abi_version(void);
+const char* dssm_last_error(void);
+
+/* ---- layout / sizing --------------------------------------------------------------------- */
+int dssm_config_check(const dssm_config* cfg);
+/* Elements of the flat parameter arena (== gradient, Adam m, Adam v arenas). */
+int64_t dssm_param_count(const dssm_config* cfg);
+/* Fills up to max_segs segments; returns the total number of segments. */
+int dssm_param_layout(const dssm_config* cfg, dssm_segment* segs, int max_segs);
+/* Elements of the EMA shadow arena: per layer, tower q mean|var then tower d mean|var. */
+int64_t dssm_ema_count(const dssm_config* cfg);
+size_t dssm_workspace_bytes(const dssm_config* cfg);
+
+/* ---- plan: the whole training step (new_dssm.py:104-217) ------------------------------- */
+int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_bytes,
+                     float* params, float* grads, float* adam_m, float* adam_v, float* ema,
+                     dssm_plan** out);
+int dssm_plan_destroy(dssm_plan* plan);
+int dssm_plan_buffer(const dssm_plan* plan, int buffer_id, int layer, void** ptr, size_t* bytes);
+
+/* Feed (utils/utils.py:45-61 + the three sparse placeholders new_dssm.py:111-114): one CSR
+ * over rows [q(BS); pos(BS); neg(BS*NEG)], negative i of query j at row 2*BS + j*NEG + i.
+ * nnz is read on device from indptr[rows]; it must not exceed cfg->max_nnz. */
+int dssm_plan_set_batch(dssm_plan* plan, const int32_t* indptr, const int32_t* indices,
+                        const float* values);
+/* Refresh the bf16 weight shadows from the fp32 arena (after loading params; BF16 mode). */
+int dssm_plan_sync_shadows(dssm_plan* plan, void* stream);
+/* Forward through the loss (sess.run(loss)); train!=0 uses batch moments and updates the
+ * EMA shadows (new_dssm.py:85 tf.cond true branch), train==0 uses the shadows. */
+int dssm_plan_forward(dssm_plan* plan, int train, void* stream);
+/* Backward of the last train-mode forward into the gradient arena (TF autodiff of :124-209). */
+int dssm_plan_backward(dssm_plan* plan, void* stream);
+/* ApplyAdam over the whole arena with TF1.x semantics; beta*_power are the values BEFORE this
+ * step's update (beta^t for step t, first step t=1).  grad_scale multiplies every gradient
+ * (1/world for data parallel mean).  Also refreshes the bf16 shadows. */
+int dssm_plan_adam(dssm_plan* plan, float beta1_power, float beta2_power, float grad_scale,
+                   void* stream);
+/* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
+int dssm_plan_train_step(dssm_plan* plan, float beta1_power, float beta2_power, void* stream);
+
+/* Kernel timing probes (bench/roofline): HIP events recorded on the launch stream around one
+ * kernel family for up to max_samples launches (0 disables); read back the summed duration. */
+enum { DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC, DSSM_PROBE_COUNT };
+int dssm_plan_probe_enable(dssm_plan* plan, int probe_id, int max_samples);
+int dssm_plan_probe_read(dssm_plan* plan, int probe_id, float* total_ms, int* count);
+
+/* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
+/* FC1 (new_dssm.py:124-126): Z[r, :] = sum_k values[k] * W[indices[k], :] + bias.
+ * W: [d x ldw] of w_dtype (ldw >= n, multiple of 4); Z: [rows x ldz] fp32, ldz = ldp(n). */
+int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                      const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
+                      int ldz, void* stream);
+/* add_layer (archive/dssm_v3.py:44-53) on device: Z[M x ldz] = A[M x lda] . W[K x ldw] + bias,
+ * inputs of dtype `dtype`, fp32 accumulate and output. */
+int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                   const float* bias, float* Z, int ldz, void* stream);
+/* batch_normalization (new_dssm.py:62-88) + ReLU over rows [row0, row0+rows) of Z (one tower).
+ * train!=0: batch moments, EMA update of ema_mean/ema_var; train==0: uses the EMA.
+ * out: [rows x ldz] of out_dtype; batch_mean/var may be NULL.  ws: >= dssm_bn_ws_bytes(). */
+size_t dssm_bn_ws_bytes(int rows, int ldz);
+int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
+                     float* ema_mean, float* ema_var, float eps, float decay, int train, int relu,
+                     void* out, int out_dtype, float* batch_mean, float* batch_var, void* ws,
+                     void* stream);
+/* Cosine_Similarity + Loss (new_dssm.py:182-213) fused with their backward: y rows
+ * [q; pos; neg] [R x ld] fp32 -> cos_sim_raw, cos_sim, prob, query_norm, loss[2] (loss, acc),
+ * dy [R x ld] (d loss / d y).  ws: >= 2*BS floats. */
+int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
+                             float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
+                             float* loss, float* dy, float* ws, void* stream);
+
+/* ---- data parallel (one RCCL all-reduce of the gradient arena per step) ----------------- */
+/* unique_id: 128 bytes from dssm_comm_unique_id() on rank 0, shared by the caller. */
+int dssm_comm_unique_id(void* out128);
+int dssm_comm_init(int rank, int world, const void* unique_id128);
+int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
+int dssm_comm_destroy(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSSM_H */

@@ -1,0 +1,54 @@
+"""CPU baseline timing of the DSSM step — TEST/BENCH INFRASTRUCTURE ONLY (bench.py's
+cpu_baseline leg).  The reference's own CPU path (TensorFlow 1.x) cannot run here (TF absent,
+no network), so the baseline is the port of the same graph: the C/OpenMP restatement in
+oracle/dssm_cpu.c when it is built (kind "port", all host threads), else the NumPy oracle in
+float32 (kind "port", NumPy/BLAS threads).  The merge of negatives is a permutation in both, so
+the reference's O((BS*NEG)^2) concat chain (new_dssm.py:169-179) is NOT charged to the baseline
+— it is conservative in the reference's favour."""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+
+from . import dssm_oracle as O
+
+
+def _threads():
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        if os.environ.get(k):
+            try:
+                return int(os.environ[k])
+            except ValueError:
+                pass
+    return os.cpu_count() or 1
+
+
+def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 50):
+    from dssm_amd.data import ZipfColumns, synth_batch  # synthetic batches only (host numpy)
+    try:
+        from . import cpu_c
+        if cpu_c.available():
+            return cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
+    except ImportError:
+        pass
+    cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
+    p = O.init_params(cfg, seed=0)
+    ema = O.make_ema(cfg)
+    adam = O.AdamState(cfg, p)
+    cols = ZipfColumns(D)
+    batches = [synth_batch(D, BS, NEG, seed=1000 + b, cols=cols).as_dict() for b in range(2)]
+    # one untimed warm-up step
+    _, ema = O.train_step(cfg, p, ema, adam, batches[0], dtype=np.float32)[0::2]
+    steps, t0 = 0, time.perf_counter()
+    while steps < max_steps:
+        _, _, ema = O.train_step(cfg, p, ema, adam, batches[steps % 2], dtype=np.float32)
+        steps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(steps * BS * (NEG + 1) / el, 1), "unit": "pairs/s",
+            "cores": _threads(), "kind": "port",
+            "sample": f"{steps} full C2 steps (fwd+bwd+dense Adam, BS={BS}) of the NumPy float32 "
+                      f"oracle in {el:.1f}s"}

@@ -1,0 +1,195 @@
+"""GPU parity: the HIP training step (through the C-ABI) against the CPU oracle on identical
+seeded batches.  Tolerances (north star: <= 1e-4 relative on loss and cosine scores):
+
+* fp32 mode: loss rel <= 1e-5, cos_sim_raw / prob abs <= 1e-5 (cosines are O(1)), gradients
+  max-abs error <= 1e-4 x max|g| per tensor, parameters after Adam <= 1e-5 abs except where the
+  oracle's gradient is below 1e-6 x max|g| (Adam normalises such rounding-level gradients to
+  O(lr) steps whose sign is noise).  Biases are excluded from parameter/gradient comparisons:
+  every FC is followed by batch-stat BN, so d loss / d b is exactly 0 in exact arithmetic and
+  both sides hold only rounding noise (tests/test_oracle.py pins this).
+* bf16 mode (perf): bf16 weights/activations with fp32 accumulation — loss rel <= 2e-2,
+  cosine abs <= 2e-2, gradient direction cosine >= 0.99 per tensor.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dssm_oracle as O
+from dssm_amd.data import synth_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def make(D, widths, BS, NEG, dtype, seed=11, **kw):
+    from dssm_amd.model import DSSM
+    cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
+    p = O.init_params(cfg, seed=seed)
+    m = DSSM(D, widths, BS, NEG, dtype=dtype, init=False, **kw)
+    m.load_params(p)
+    return cfg, p, m
+
+
+def rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-12)
+
+
+def grad_check(name, got, ref, tol):
+    scale = np.abs(ref).max()
+    err = np.abs(got - ref).max()
+    assert err <= tol * max(scale, 1e-30), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+CASES = [
+    # (D, widths, BS, NEG)
+    (64, (16, 16), 8, 4),
+    (1000, (100, 100), 128, 4),          # C1 (reference config.py widths)
+    (1000, (100, 100, 64), 64, 3),
+    (5000, (300, 300, 128), 96, 4),      # C2 shape, small batch
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fp32_step_matches_oracle(case):
+    D, widths, BS, NEG = case
+    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    batch = synth_batch(D, BS, NEG, seed=1000, mean_nnz=min(32, D // 4))
+    ema = O.make_ema(cfg)
+    cache, ema1 = O.forward(cfg, p, ema, batch.as_dict(), True, np.float64)
+    grads = O.backward(cfg, p, cache, np.float64)
+
+    m.set_batch(batch)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    loss, acc = m.loss_accuracy()
+    assert rel(loss, cache["loss"]) <= 1e-5, (loss, cache["loss"])
+    assert acc == pytest.approx(cache["accuracy"])
+    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), cache["cos_sim_raw"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(m.fetch("prob"), cache["prob"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(m.fetch("query_norm_single").ravel(), cache["qn"], rtol=1e-5)
+    y = m.fetch("embedding_all")
+    np.testing.assert_allclose(y, cache["layers"][-1]["A"], rtol=1e-4, atol=1e-5)
+    for l in range(1, len(widths) + 1):
+        mo = m.batch_moments(l)
+        for t in ("q", "d"):
+            np.testing.assert_allclose(mo[t][0], cache["layers"][l - 1]["batch_mean"][t], rtol=1e-4, atol=1e-6)
+            np.testing.assert_allclose(mo[t][1], cache["layers"][l - 1]["batch_var"][t], rtol=1e-4, atol=1e-8)
+    ge = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
+    for k in ema1:
+        np.testing.assert_allclose(ge[k], ema1[k], rtol=1e-4, atol=1e-7, err_msg=k)
+    gg = {k: v.cpu().numpy() for k, v in m.named_grads().items()}
+    for k, g in grads.items():
+        if k.startswith("b"):
+            assert np.abs(gg[k]).max() <= 1e-4 * max(np.abs(grads["W1"]).max(), 1e-12) + 1e-6, k
+            continue
+        grad_check(k, gg[k], g, 1e-4)
+
+
+@pytest.mark.parametrize("case", CASES[:3])
+def test_fp32_three_steps_params_and_eval(case):
+    D, widths, BS, NEG = case
+    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    ema = O.make_ema(cfg)
+    adam = O.AdamState(cfg, p)
+    last_grads = None
+    for step in range(3):
+        batch = synth_batch(D, BS, NEG, seed=2000 + step, mean_nnz=min(32, D // 4))
+        cache, ema = O.forward(cfg, p, ema, batch.as_dict(), True, np.float64)
+        last_grads = O.backward(cfg, p, cache, np.float64)
+        adam.step(p, last_grads)
+        m.set_batch(batch)
+        m.train_step()
+        torch.cuda.synchronize()
+        assert rel(m.loss_accuracy()[0], cache["loss"]) <= 1e-5
+    gp = {k: v.cpu().numpy() for k, v in m.named_params().items()}
+    for k in p:
+        if k.startswith("b"):
+            continue
+        d = np.abs(gp[k] - p[k])
+        small = np.abs(last_grads[k]) <= 1e-6 * np.abs(last_grads[k]).max()
+        assert d[~small].max(initial=0.0) <= 1e-5, (k, d[~small].max(initial=0.0))
+        assert d.max() <= 6 * cfg.lr, k
+    ge = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
+    for k in ema:
+        np.testing.assert_allclose(ge[k], ema[k], rtol=2e-4, atol=1e-6, err_msg=k)
+    # eval mode (on_train=False): EMA moments, no EMA update (new_dssm.py:85-86)
+    batch = synth_batch(D, BS, NEG, seed=3000, mean_nnz=min(32, D // 4))
+    gp_t = {k: v for k, v in gp.items()}
+    ev = O.forward(cfg, gp_t, ema, batch.as_dict(), False, np.float64)[0]
+    m.set_batch(batch)
+    m.forward(False)
+    torch.cuda.synchronize()
+    assert rel(m.loss_accuracy()[0], ev["loss"]) <= 1e-4
+    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), ev["cos_sim_raw"], rtol=1e-4, atol=1e-4)
+    ge2 = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
+    for k in ge:
+        np.testing.assert_array_equal(ge[k], ge2[k])
+
+
+def test_fp32_edge_rows():
+    """Empty input rows (Z = bias only), a row at the 96-nnz cap, and a 1-query batch."""
+    D, widths, BS, NEG = 300, (32, 32), 4, 4
+    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    b = synth_batch(D, BS, NEG, seed=5, mean_nnz=20)
+    # make row 1 (a query) and row 9 (a negative) empty, row 2 dense (96 nnz)
+    rows = []
+    for r in range(b.rows):
+        s, e = b.indptr[r], b.indptr[r + 1]
+        rows.append((b.indices[s:e], b.values[s:e]))
+    rows[1] = (np.zeros(0, np.int32), np.zeros(0, np.float32))
+    rows[9] = (np.zeros(0, np.int32), np.zeros(0, np.float32))
+    rows[2] = (np.arange(0, 96 * 3, 3, dtype=np.int32), np.ones(96, np.float32))
+    indptr = np.zeros(b.rows + 1, np.int32)
+    indptr[1:] = np.cumsum([len(r[0]) for r in rows])
+    b.indptr = indptr
+    b.indices = np.concatenate([r[0] for r in rows]).astype(np.int32)
+    b.values = np.concatenate([r[1] for r in rows]).astype(np.float32)
+    cache, _ = O.forward(cfg, p, O.make_ema(cfg), b.as_dict(), True, np.float64)
+    grads = O.backward(cfg, p, cache, np.float64)
+    m.set_batch(b)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    assert rel(m.loss_accuracy()[0], cache["loss"]) <= 1e-5
+    gg = {k: v.cpu().numpy() for k, v in m.named_grads().items()}
+    grad_check("W1", gg["W1"], grads["W1"], 1e-4)
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[3]])
+def test_bf16_step_tracks_oracle(case):
+    D, widths, BS, NEG = case
+    cfg, p, m = make(D, widths, BS, NEG, "bf16")
+    batch = synth_batch(D, BS, NEG, seed=1000, mean_nnz=min(32, D // 4))
+    cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
+    grads = O.backward(cfg, p, cache, np.float64)
+    m.set_batch(batch)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    assert rel(m.loss_accuracy()[0], cache["loss"]) <= 2e-2
+    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), cache["cos_sim_raw"], atol=2e-2)
+    gg = {k: v.cpu().numpy() for k, v in m.named_grads().items()}
+    for k, g in grads.items():
+        if k.startswith("b"):
+            continue
+        a, b = gg[k].ravel().astype(np.float64), g.ravel()
+        cosv = a @ b / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30)
+        assert cosv >= 0.99, (k, cosv)
+
+
+def test_c2_full_size_fp32_one_step():
+    """BASELINE config 2 shape at full size (D=30k, 300/300/128, BS=1024, NEG=4) in fp32 mode."""
+    D, widths, BS, NEG = 30000, (300, 300, 128), 1024, 4
+    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    batch = synth_batch(D, BS, NEG, seed=1000)
+    cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
+    grads = O.backward(cfg, p, cache, np.float64)
+    m.set_batch(batch)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    assert rel(m.loss_accuracy()[0], cache["loss"]) <= 1e-5
+    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), cache["cos_sim_raw"], rtol=1e-4, atol=1e-5)
+    gg = {k: v.cpu().numpy() for k, v in m.named_grads().items()}
+    for k in ("W1", "W2", "W3", "bn1_q_gamma", "bn3_d_beta"):
+        grad_check(k, gg[k], grads[k], 1e-4)
