@@ -152,6 +152,10 @@ class DSSM:
             if batch.nnz > self.max_nnz:
                 raise ValueError(f"batch nnz {batch.nnz} exceeds max_nnz {self.max_nnz}")
             nz = batch.nnz
+            if nz and (int(batch.indices.max()) >= self.trigram_d or int(batch.indices.min()) < 0):
+                raise ValueError("batch column index out of [0, TRIGRAM_D)")
+            if batch.indptr[0] != 0 or np.any(np.diff(batch.indptr) < 0):
+                raise ValueError("batch indptr must start at 0 and be non-decreasing")
             self._indptr.copy_(torch.from_numpy(batch.indptr), non_blocking=non_blocking)
             if nz:
                 self._indices[:nz].copy_(torch.from_numpy(batch.indices), non_blocking=non_blocking)
