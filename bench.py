@@ -82,6 +82,8 @@ def main():
     from dssm_amd.data import ZipfColumns, synth_batch
 
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
+    if world > 1:
+        model.set_fused_w1_adam(False)  # all-reduce needs the materialized dW1
     comm = None
     if world > 1 and args.allreduce == "rccl":
         from dssm_amd.dist import RcclComm

@@ -59,6 +59,7 @@ _SIGS = {
     "dssm_plan_backward": (C.c_int, [_P, _P]),
     "dssm_plan_adam": (C.c_int, [_P, C.c_float, C.c_float, C.c_float, _P]),
     "dssm_plan_train_step": (C.c_int, [_P, C.c_float, C.c_float, _P]),
+    "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),
     "dssm_plan_probe_read": (C.c_int, [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
     "dssm_spmm_csr_fwd": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,

@@ -1,0 +1,85 @@
+// Sparse row-gather accumulation shared by the SpMM, the dW1 kernels and the fused W1 Adam.
+#pragma once
+#include "common.h"
+
+namespace dssm {
+
+// Columns with at most this many CSC entries are "light": one wave sums the whole dW1 row.
+constexpr int kLightEntries = 64;
+
+// One gathered 8-column slice kept in its storage format until it is consumed, so a batch of
+// in-flight bf16 rows costs 4 VGPRs each (not 8).
+template <typename T> struct RawRow8;
+template <> struct RawRow8<u16> {
+  uint4 a;
+  __device__ __forceinline__ void load(const u16* p, int) { a = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void fma(float v, float (&acc)[8]) const {
+    acc[0] = __fmaf_rn(v, __uint_as_float(a.x << 16), acc[0]);
+    acc[1] = __fmaf_rn(v, __uint_as_float(a.x & 0xffff0000u), acc[1]);
+    acc[2] = __fmaf_rn(v, __uint_as_float(a.y << 16), acc[2]);
+    acc[3] = __fmaf_rn(v, __uint_as_float(a.y & 0xffff0000u), acc[3]);
+    acc[4] = __fmaf_rn(v, __uint_as_float(a.z << 16), acc[4]);
+    acc[5] = __fmaf_rn(v, __uint_as_float(a.z & 0xffff0000u), acc[5]);
+    acc[6] = __fmaf_rn(v, __uint_as_float(a.w << 16), acc[6]);
+    acc[7] = __fmaf_rn(v, __uint_as_float(a.w & 0xffff0000u), acc[7]);
+  }
+};
+template <> struct RawRow8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p, int nvalid) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = nvalid > 4 ? *reinterpret_cast<const float4*>(p + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __device__ __forceinline__ void fma(float v, float (&acc)[8]) const {
+    acc[0] = __fmaf_rn(v, a.x, acc[0]); acc[1] = __fmaf_rn(v, a.y, acc[1]);
+    acc[2] = __fmaf_rn(v, a.z, acc[2]); acc[3] = __fmaf_rn(v, a.w, acc[3]);
+    acc[4] = __fmaf_rn(v, b.x, acc[4]); acc[5] = __fmaf_rn(v, b.y, acc[5]);
+    acc[6] = __fmaf_rn(v, b.z, acc[6]); acc[7] = __fmaf_rn(v, b.w, acc[7]);
+  }
+};
+
+// Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc.  All 64 lanes must be
+// active (the index broadcast reads every lane's register; v_readlane ignores EXEC); lanes with
+// nvalid <= 0 only skip their loads.
+template <typename T>
+__device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
+                                                  const float* __restrict__ val, int s, int e,
+                                                  const T* __restrict__ M, int ldm, int c,
+                                                  int nvalid, float (&acc)[8]) {
+  constexpr int U = sizeof(T) == 2 ? 8 : 4;  // rows in flight per lane
+  const int lane = lane_id();
+  for (int base = s; base < e; base += 64) {
+    const int cnt = min(64, e - base);
+    int my_i = 0;
+    float my_v = 0.f;
+    if (lane < cnt) {
+      my_i = idx[base + lane];
+      my_v = val[base + lane];
+    }
+    int j = 0;
+    for (; j + U <= cnt; j += U) {
+      RawRow8<T> x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = bcast_i(my_i, j + u);
+        if (nvalid > 0) x[u].load(M + (size_t)r * ldm + c, nvalid);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float v = bcast_f(my_v, j + u);
+        if (nvalid > 0) x[u].fma(v, acc);
+      }
+    }
+    for (; j < cnt; ++j) {
+      const int r = bcast_i(my_i, j);
+      const float v = bcast_f(my_v, j);
+      if (nvalid > 0) {
+        RawRow8<T> x;
+        x.load(M + (size_t)r * ldm + c, nvalid);
+        x.fma(v, acc);
+      }
+    }
+  }
+}
+
+}  // namespace dssm

@@ -2,12 +2,16 @@
 // autodiff: dA = dZ*W^T, dW = A^T*dZ, db = colsum(dZ)).
 //
 // One 256-thread workgroup computes a 64x64 output tile; its 4 waves each own 32x32 = 2x2
-// MFMA 16x16 tiles.  K is staged through LDS in 32-deep steps, both operands stored
-// k-contiguous ([row][k] for A, [col][k] for B) so every MFMA fragment is one contiguous LDS
-// read: bf16 -> v_mfma_f32_16x16x32_bf16 (8 elements per lane, one ds_read_b128 each),
-// fp32 (parity mode) -> v_mfma_f32_16x16x4_f32 (exact f32 FMA chain).  fp32 accumulate.
+// MFMA 16x16 tiles.  K is staged through a double-buffered LDS ring (64-deep for bf16, 32 for
+// fp32) with the next step's global loads issued into registers before the current step's
+// MFMAs (one barrier per K-step).  Both operands are stored k-contiguous ([row][k] for A,
+// [col][k] for B) so every MFMA fragment is one contiguous LDS read: bf16 ->
+// v_mfma_f32_16x16x32_bf16 (8 elements per lane, one ds_read_b128), fp32 (parity mode) ->
+// v_mfma_f32_16x16x4_f32 (exact f32 FMA chain).  fp32 accumulate.
 //
-// The bias gradient rides along with dW: the A^T operand gets a virtual all-ones row at
+// dW is a split-K GEMM over the batch rows (K = R = 6144 at C2); each split writes a plain fp32
+// partial slab and k_splitk_reduce sums the slabs in fixed order (deterministic, no atomics, no
+// zero-init).  The bias gradient rides along: the A^T operand gets a virtual all-ones row at
 // m = K_in, so row K_in of the [K_in+1 x N] output (the arena's [W; b] block) is colsum(dZ).
 #include "common.h"
 #include "launch.h"
@@ -15,13 +19,12 @@
 namespace dssm {
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32;
+constexpr int BM = 64, BN = 64;
 
-template <typename T> struct LdsPad;
-template <> struct LdsPad<u16> { static constexpr int v = 8; };    // 80-B rows
-template <> struct LdsPad<float> { static constexpr int v = 4; };  // 144-B rows
+template <typename T> struct Cfg;
+template <> struct Cfg<u16> { static constexpr int BK = 64, PAD = 8; };    // 144-B LDS rows
+template <> struct Cfg<float> { static constexpr int BK = 32, PAD = 4; };  // 144-B LDS rows
 
-template <typename T> __device__ __forceinline__ T zero_v() { return T(0); }
 template <typename T> __device__ __forceinline__ T one_v();
 template <> __device__ __forceinline__ float one_v<float>() { return 1.0f; }
 template <> __device__ __forceinline__ u16 one_v<u16>() { return (u16)0x3f80; }
@@ -42,7 +45,23 @@ __device__ __forceinline__ void ld8(const T* p, int nv, T (&x)[8]) {
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = (i < nv) ? p[i] : zero_v<T>();
+    for (int i = 0; i < 8; ++i) x[i] = (i < nv) ? p[i] : T(0);
+  }
+}
+
+// 8 contiguous elements into LDS (16-B aligned destination)
+template <typename T>
+__device__ __forceinline__ void st8(T* d, const T (&x)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 a;
+    a.x = (unsigned)x[0] | ((unsigned)x[1] << 16);
+    a.y = (unsigned)x[2] | ((unsigned)x[3] << 16);
+    a.z = (unsigned)x[4] | ((unsigned)x[5] << 16);
+    a.w = (unsigned)x[6] | ((unsigned)x[7] << 16);
+    *reinterpret_cast<uint4*>(d) = a;
+  } else {
+    *reinterpret_cast<float4*>(d) = make_float4(x[0], x[1], x[2], x[3]);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(x[4], x[5], x[6], x[7]);
   }
 }
 
@@ -54,9 +73,11 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
                                               int k_per_split) {
   constexpr bool TA = (MODE == GEMM_DW);
   constexpr bool TB = (MODE == GEMM_DA);
-  constexpr int LDK = BK + LdsPad<T>::v;
-  __shared__ __attribute__((aligned(16))) T sA[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T sB[BN * LDK];
+  constexpr int BK = Cfg<T>::BK;
+  constexpr int LDK = BK + Cfg<T>::PAD;
+  constexpr int G = (BM * BK / 256) / 8;  // 8-element groups per thread per operand
+  __shared__ __attribute__((aligned(16))) T sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) T sB[2][BN * LDK];
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -65,77 +86,100 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
   const int kend = min(K, kbeg + k_per_split);
   const int Mload = ones_row ? M - 1 : M;
 
+  T ra[G][8], rb[G][8];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int e = t + 256 * g;
+      if constexpr (!TA) {  // A[m][k]
+        const int m = e / (BK / 8), kk = (e % (BK / 8)) * 8;
+        const int gm = bm + m, gk = k0 + kk;
+        ld8(A + (size_t)gm * lda + gk, (gm < Mload) ? min(8, kend - gk) : 0, ra[g]);
+      } else {  // A^T: A[k][m]
+        const int k = e / (BM / 8), mm = (e % (BM / 8)) * 8;
+        const int gk = k0 + k, gm = bm + mm;
+        ld8(A + (size_t)gk * lda + gm, (gk < kend) ? min(8, Mload - gm) : 0, ra[g]);
+        if (ones_row && gk < kend) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (gm + i == Mload) ra[g][i] = one_v<T>();
+        }
+      }
+      if constexpr (!TB) {  // B[k][n]
+        const int k = e / (BN / 8), nn = (e % (BN / 8)) * 8;
+        const int gk = k0 + k, gn = bn + nn;
+        ld8(B + (size_t)gk * ldb + gn, (gk < kend) ? min(8, N - gn) : 0, rb[g]);
+      } else {  // B^T: B[n][k]
+        const int n = e / (BK / 8), kk = (e % (BK / 8)) * 8;
+        const int gn = bn + n, gk = k0 + kk;
+        ld8(B + (size_t)gn * ldb + gk, (gn < N) ? min(8, kend - gk) : 0, rb[g]);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int e = t + 256 * g;
+      if constexpr (!TA) {
+        const int m = e / (BK / 8), kk = (e % (BK / 8)) * 8;
+        st8(&sA[buf][m * LDK + kk], ra[g]);
+      } else {
+        const int k = e / (BM / 8), mm = (e % (BM / 8)) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sA[buf][(mm + i) * LDK + k] = ra[g][i];
+      }
+      if constexpr (!TB) {
+        const int k = e / (BN / 8), nn = (e % (BN / 8)) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sB[buf][(nn + i) * LDK + k] = rb[g][i];
+      } else {
+        const int n = e / (BK / 8), kk = (e % (BK / 8)) * 8;
+        st8(&sB[buf][n * LDK + kk], rb[g]);
+      }
+    }
+  };
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    // ---- stage A tile (BM x BK) as sA[m][k]
-    if constexpr (!TA) {
-      const int m = t >> 2, kk = (t & 3) * 8;
-      T x[8];
-      const int gm = bm + m, gk = k0 + kk;
-      const int nv = (gm < Mload) ? min(8, kend - gk) : 0;
-      ld8(A + (size_t)gm * lda + gk, nv, x);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sA[m * LDK + kk + i] = x[i];
-    } else {
-      const int k = t >> 3, mm = (t & 7) * 8;
-      T x[8];
-      const int gk = k0 + k, gm = bm + mm;
-      const int nv = (gk < kend) ? min(8, Mload - gm) : 0;
-      ld8(A + (size_t)gk * lda + gm, nv, x);
-      if (ones_row && gk < kend) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (gm + i == Mload) x[i] = one_v<T>();
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sA[(mm + i) * LDK + k] = x[i];
-    }
-    // ---- stage B tile (BK x BN) as sB[n][k]
-    if constexpr (!TB) {
-      const int k = t >> 3, nn = (t & 7) * 8;
-      T x[8];
-      const int gk = k0 + k, gn = bn + nn;
-      const int nv = (gk < kend) ? min(8, N - gn) : 0;
-      ld8(B + (size_t)gk * ldb + gn, nv, x);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sB[(nn + i) * LDK + k] = x[i];
-    } else {
-      const int n = t >> 2, kk = (t & 3) * 8;
-      T x[8];
-      const int gn = bn + n, gk = k0 + kk;
-      const int nv = (gn < N) ? min(8, kend - gk) : 0;
-      ld8(B + (size_t)gn * ldb + gk, nv, x);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sB[n * LDK + kk + i] = x[i];
-    }
-    __syncthreads();
-
+  if (kbeg < kend) {
+    load(kbeg);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BK, buf ^= 1) {
+    const bool more = k0 + BK < kend;
+    if (more) load(k0 + BK);  // next step's global loads in flight during this step's MFMAs
+    const T* a = sA[buf];
+    const T* b = sB[buf];
     if constexpr (sizeof(T) == 2) {
-      bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(&sA[(wm * 32 + i * 16 + (lane & 15)) * LDK + 8 * (lane >> 4)]);
+      for (int ks = 0; ks < BK; ks += 32) {
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(&sB[(wn * 32 + j * 16 + (lane & 15)) * LDK + 8 * (lane >> 4)]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(&a[(wm * 32 + i * 16 + (lane & 15)) * LDK + ks + 8 * (lane >> 4)]);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&b[(wn * 32 + j * 16 + (lane & 15)) * LDK + ks + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         float af[2], bfr[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = sA[(wm * 32 + i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+        for (int i = 0; i < 2; ++i) af[i] = a[(wm * 32 + i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = sB[(wn * 32 + j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+        for (int j = 0; j < 2; ++j) bfr[j] = b[(wn * 32 + j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -143,10 +187,13 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (more) store(buf ^ 1);
     __syncthreads();
   }
 
   // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+  float* out = C;
+  if constexpr (MODE == GEMM_DW) out = C + (size_t)blockIdx.z * M * ldc;  // this split's slab
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -158,29 +205,65 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
         const float v = acc[i][j][r];
         if (m >= M) continue;
         if constexpr (MODE == GEMM_FWD) {
-          if (n < ldc) C[(size_t)m * ldc + n] = (n < N) ? v + bias[n] : 0.f;
+          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? v + bias[n] : 0.f;
         } else if constexpr (MODE == GEMM_DA) {
-          if (n < ldc) C[(size_t)m * ldc + n] = (n < N) ? v : 0.f;
+          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? v : 0.f;
         } else {
-          if (n < N) atomicAdd(&C[(size_t)m * ldc + n], v);
+          if (n < N) out[(size_t)m * ldc + n] = v;
         }
       }
     }
   }
 }
 
+// dst[i] = sum_s slab[s][i] in fixed split order.
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ slab, int splits,
+                                                       int64_t n, float* __restrict__ dst) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(slab)[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(slab + (size_t)s * n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = acc;
+  }
+  // tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    float acc = slab[i];
+    for (int s = 1; s < splits; ++s) acc += slab[(size_t)s * n + i];
+    dst[i] = acc;
+  }
+}
+
+int dw_splits(int M, int N, int K, int BK) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  int splits = max(1, min(cdiv(384, tiles), cdiv(K, 4 * BK)));
+  splits = min(splits, kMaxDwSplits);
+  const int kps = cdiv(cdiv(K, splits), BK) * BK;
+  return cdiv(K, kps);
+}
+
 template <typename T>
 hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, const T* B, int ldb,
-                    float* C, int ldc, const float* bias, bool ones_row, hipStream_t s) {
+                    float* C, int ldc, const float* bias, bool ones_row, float* slab,
+                    hipStream_t s) {
   dim3 block(256);
+  constexpr int BK = Cfg<T>::BK;
   if (mode == GEMM_DW) {
-    const int tiles = cdiv(M, BM) * cdiv(N, BN);
-    int splits = max(1, min(cdiv(1024, tiles), cdiv(K, 128)));
-    int kps = cdiv(cdiv(K, splits), BK) * BK;
-    splits = cdiv(K, kps);
+    const int splits = dw_splits(M, N, K, BK);
+    const int kps = cdiv(cdiv(K, splits), BK) * BK;
     dim3 grid(cdiv(N, BN), cdiv(M, BM), splits);
-    hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       bias, ones_row ? 1 : 0, kps);
+    float* target = splits > 1 ? slab : C;
+    hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
+                       ldc, bias, ones_row ? 1 : 0, kps);
+    if (splits > 1) {
+      const int64_t n = (int64_t)M * ldc;
+      const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), block, 0, s, slab, splits, n, C);
+    }
   } else {
     dim3 grid(cdiv(ldc, BN), cdiv(M, BM), 1);
     const int kps = cdiv(K, BK) * BK;
@@ -196,14 +279,19 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
 
 }  // namespace
 
+size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
+  const int splits = dw_splits(M, N, K, bf16 ? Cfg<u16>::BK : Cfg<float>::BK);
+  return splits > 1 ? (size_t)splits * M * N : 0;
+}
+
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
-                       hipStream_t s) {
+                       float* slab, hipStream_t s) {
   if (bf16)
     return launch_t<u16>(mode, M, N, K, (const u16*)A, lda, (const u16*)B, ldb, C, ldc, bias,
-                         ones_row, s);
+                         ones_row, slab, s);
   return launch_t<float>(mode, M, N, K, (const float*)A, lda, (const float*)B, ldb, C, ldc, bias,
-                         ones_row, s);
+                         ones_row, slab, s);
 }
 
 }  // namespace dssm

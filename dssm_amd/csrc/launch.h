@@ -11,24 +11,32 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
                            int ldz, hipStream_t s);
 // CSR -> CSC transpose of X with a virtual all-ones column D appended (its dW row = db1).
-// cnt: int[D+1] scratch, col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
+// scratch: csc_scratch_ints() ints, zero on first use (kept zero between calls);
+// col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
+size_t csc_scratch_ints(int D, int rows, int max_nnz);
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
-                            int D, int max_nnz, int* cnt, int* col_ptr, int* csc_row,
+                            int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s);
-// dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).
+// dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row
+// is written (light rows summed, heavy rows zeroed) then heavy rows accumulated with atomics;
+// light=false: only the heavy rows are accumulated (into rows that must already be zero).
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
-                      bool dz_bf16, int lddz, int n, float* G, hipStream_t s);
+                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s);
 
 // ---- dense GEMM (gemm.hip) ----
 enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
+constexpr int kMaxDwSplits = 32;
+// Workspace floats the DW split-K partial slabs need for an (M x N) output over K rows.
+size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16);
 // FWD: C[M x ldc] = A[M x K] * B[K x N] + bias (cols >= N written 0)
 // DA : C[M x ldc] = A[M x K] * B^T where B is [N x K] (ld ldb)
-// DW : C[M x N] += A^T * B, A is [K x M] (ld lda) with a virtual ones row at m == M-1 when
-//      ones_row != 0; B is [K x N]; split-K over the K (rows) dimension with fp32 atomics.
+// DW : C[M x N] = A^T * B, A is [K x M] (ld lda) with a virtual ones row at m == M-1 when
+//      ones_row != 0; B is [K x N]; split-K over the K (rows) dimension into `slab`
+//      (gemm_dw_slab_floats) then a fixed-order reduce into C (ldc must equal N).
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
-                       hipStream_t s);
+                       float* slab, hipStream_t s);
 
 // ---- batch norm (bn.hip) ----
 struct BnTowers {
@@ -71,9 +79,18 @@ struct ShadowList {
   int count;
   ShadowSeg seg[8];
 };
-hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float alpha,
-                       float beta1, float beta2, float eps, float grad_scale, ShadowList sh,
-                       hipStream_t s);
+// Adam over arena elements [begin, end) (multiples of 4); gradients at index >= clear_from are
+// zeroed after use.
+hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t begin, int64_t end,
+                       int64_t clear_from, float alpha, float beta1, float beta2, float eps,
+                       float grad_scale, ShadowList sh, hipStream_t s);
+// Fused dW1 (light rows, inline from the CSC transpose) + Adam over the [W1; b1] block whose
+// arena pointers p/g/m/v are passed already offset; heavy rows read from g and cleared.
+hipError_t launch_adam_w1_fused(float* p, float* g, float* m, float* v, int D, int n,
+                                const int* col_ptr, const int* csc_row, const float* csc_val,
+                                const void* dZ, bool dz_bf16, int lddz, float alpha, float beta1,
+                                float beta2, float eps, float grad_scale, uint16_t* shadow,
+                                int ldsh, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 
 }  // namespace dssm

@@ -46,8 +46,8 @@ struct Layout {
   size_t Z[DSSM_MAX_LAYERS], A[DSSM_MAX_LAYERS], dA[DSSM_MAX_LAYERS], dZ[DSSM_MAX_LAYERS];
   size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS];
-  size_t partial, cos_raw, cos_sim, prob, qnorm, loss_j, correct_j, loss;
-  size_t cnt, col_ptr, csc_row, csc_val, csc_col;
+  size_t dw_slab, partial, cos_raw, cos_sim, prob, qnorm, loss_j, correct_j, loss;
+  size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col;
   size_t ws = 0;
   int max_nnz = 0;
 };
@@ -126,6 +126,10 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
   Lt.partial = take(max_part * 4);
+  size_t slab = 0;
+  for (int l = 1; l < Lt.L; ++l)
+    slab = std::max(slab, dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16));
+  Lt.dw_slab = take(std::max<size_t>(slab, 1) * 4);
   const size_t K = Lt.NEG + 1;
   Lt.cos_raw = take(K * Lt.BS * 4);
   Lt.cos_sim = take(K * Lt.BS * 4);
@@ -134,7 +138,7 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.loss_j = take(Lt.BS * 4);
   Lt.correct_j = take(Lt.BS * 4);
   Lt.loss = take(2 * 4);
-  Lt.cnt = take((size_t)(Lt.D + 1) * 4);
+  Lt.csc_scratch = take(dssm::csc_scratch_ints(Lt.D, Lt.R, Lt.max_nnz) * 4);
   Lt.col_ptr = take((size_t)(Lt.D + 2) * 4);
   const size_t ent = (size_t)Lt.max_nnz + R;
   Lt.csc_row = take(ent * 4);
@@ -154,6 +158,11 @@ struct dssm_plan {
   const int32_t* indices = nullptr;
   const float* values = nullptr;
   bool fwd_train_done = false;
+  bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
+  bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
+  bool csc_pending = false;
+  hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
+  hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
   // Kernel timing probes: HIP events recorded on the launch stream around one kernel family.
   struct Probe {
     bool on = false;
@@ -273,14 +282,27 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->m = adam_m;
   P->v = adam_v;
   P->ema = ema;
+  if (hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&P->ev_batch, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&P->ev_csc, hipEventDisableTiming) != hipSuccess) {
+    delete P;
+    return fail(DSSM_E_HIP, "failed to create the plan's side stream/events");
+  }
   *out = P;
   return DSSM_OK;
 }
 
 int dssm_plan_destroy(dssm_plan* plan) {
-  if (plan)
+  if (plan) {
     for (auto& p : plan->probe)
       for (hipEvent_t e : p.ev) hipEventDestroy(e);
+    if (plan->side) {
+      hipStreamSynchronize(plan->side);
+      hipStreamDestroy(plan->side);
+    }
+    if (plan->ev_batch) hipEventDestroy(plan->ev_batch);
+    if (plan->ev_csc) hipEventDestroy(plan->ev_csc);
+  }
   delete plan;
   return DSSM_OK;
 }
@@ -367,6 +389,21 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   const Layout& Lt = P->Lt;
   const dssm_config& c = P->cfg;
   const dssm::BnTowers tw{Lt.BS, Lt.R};
+  if (train) {
+    // The CSC transpose depends only on the batch: run it on the side stream, overlapped with
+    // the forward pass.  ev_batch orders it after everything already queued on `s` (including
+    // the previous step's consumers of the CSC arrays).
+    HIP_TRY(hipEventRecord(P->ev_batch, s));
+    HIP_TRY(hipStreamWaitEvent(P->side, P->ev_batch, 0));
+    P->probe_begin(DSSM_PROBE_CSC, P->side);
+    HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
+                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
+                                   P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
+                                   P->at<int>(Lt.csc_col), P->side));
+    P->probe_end(DSSM_PROBE_CSC, P->side);
+    HIP_TRY(hipEventRecord(P->ev_csc, P->side));
+    P->csc_pending = true;
+  }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
                                 P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
@@ -387,7 +424,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     if (!last)
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, Lt.bf16, Lt.R, Lt.n[l + 1], n, P->ws + Lt.A[l],
                                 Lt.ldp[l], P->weight(l + 1), P->weight_ld(l + 1),
-                                P->at<float>(Lt.Z[l + 1]), Lt.ldp[l + 1], P->bias(l + 1), false, s));
+                                P->at<float>(Lt.Z[l + 1]), Lt.ldp[l + 1], P->bias(l + 1), false,
+                                nullptr, s));
   }
   const int lL = Lt.L - 1;
   HIP_TRY(dssm::launch_cosine_loss(
@@ -405,11 +443,11 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const Layout& Lt = P->Lt;
   const dssm::BnTowers tw{Lt.BS, Lt.R};
-  P->probe_begin(DSSM_PROBE_CSC, s);
-  HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
-                                 P->at<int>(Lt.cnt), P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
-                                 P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s));
-  P->probe_end(DSSM_PROBE_CSC, s);
+  if (!P->grads_clean) {
+    // backward() twice without an Adam step in between: re-zero the atomic-target blocks.
+    HIP_TRY(hipMemsetAsync(P->g, 0, sizeof(float) * (size_t)Lt.total, s));
+  }
+  P->grads_clean = false;
   for (int l = Lt.L - 1; l >= 0; --l) {
     const int n = Lt.n[l];
     HIP_TRY(dssm::launch_bn_bwd(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), Lt.ldp[l], n, tw,
@@ -420,18 +458,22 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
     if (l > 0) {
       const int kin = Lt.in_dim[l];
       float* gw = P->g + Lt.fc_off[l];
-      HIP_TRY(hipMemsetAsync(gw, 0, sizeof(float) * (size_t)(kin + 1) * n, s));
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_DW, Lt.bf16, kin + 1, n, Lt.R, P->ws + Lt.A[l - 1],
-                                Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true, s));
+                                Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true,
+                                P->at<float>(Lt.dw_slab), s));
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_DA, Lt.bf16, Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l],
                                 P->weight(l), P->weight_ld(l), P->at<float>(Lt.dA[l - 1]),
-                                Lt.ldp[l - 1], nullptr, false, s));
+                                Lt.ldp[l - 1], nullptr, false, nullptr, s));
     } else {
+      if (P->csc_pending) {
+        HIP_TRY(hipStreamWaitEvent(s, P->ev_csc, 0));
+        P->csc_pending = false;
+      }
       P->probe_begin(DSSM_PROBE_DW1, s);
       HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
                                P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), Lt.D, Lt.R,
                                Lt.max_nnz, P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0], n,
-                               P->g + Lt.fc_off[0], s));
+                               P->g + Lt.fc_off[0], !P->fused_w1_adam, s));
       P->probe_end(DSSM_PROBE_DW1, s);
     }
   }
@@ -444,10 +486,37 @@ int dssm_plan_adam(dssm_plan* P, float beta1_power, float beta2_power, float gra
   const dssm_config& c = P->cfg;
   const float one = 1.0f;
   const float alpha = c.lr * std::sqrt(one - beta2_power) / (one - beta1_power);
-  P->probe_begin(DSSM_PROBE_ADAM, (hipStream_t)stream);
-  HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, P->Lt.total, alpha, c.beta1, c.beta2,
-                            c.adam_eps, grad_scale, P->shadows(), (hipStream_t)stream));
-  P->probe_end(DSSM_PROBE_ADAM, (hipStream_t)stream);
+  const Layout& Lt = P->Lt;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rest = Lt.L > 1 ? Lt.fc_off[1] : Lt.bn_off[0][0];
+  dssm::ShadowList sh = P->shadows();
+  P->probe_begin(DSSM_PROBE_ADAM, s);
+  if (P->fused_w1_adam) {
+    if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
+    const int64_t o = Lt.fc_off[0];
+    HIP_TRY(dssm::launch_adam_w1_fused(
+        P->p + o, P->g + o, P->m + o, P->v + o, Lt.D, Lt.n[0], P->at<int>(Lt.col_ptr),
+        P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val), P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0],
+        alpha, c.beta1, c.beta2, c.adam_eps, grad_scale,
+        Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr, Lt.ldp[0], s));
+    if (sh.count) {  // W1's shadow is written by the fused kernel
+      for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
+      sh.count -= 1;
+    }
+    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, rest, Lt.total, Lt.total, alpha, c.beta1,
+                              c.beta2, c.adam_eps, grad_scale, sh, s));
+  } else {
+    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, 0, Lt.total, Lt.total, alpha, c.beta1,
+                              c.beta2, c.adam_eps, grad_scale, sh, s));
+  }
+  P->probe_end(DSSM_PROBE_ADAM, s);
+  P->grads_clean = true;
+  return DSSM_OK;
+}
+
+int dssm_plan_set_fused_w1_adam(dssm_plan* P, int on) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  P->fused_w1_adam = on != 0;
   return DSSM_OK;
 }
 
@@ -477,7 +546,7 @@ int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, in
       (lda % 8) || (ldw % 4) || (ldz % 4) || (dtype == DSSM_BF16 && (ldw % 8)))
     return fail(DSSM_E_INVALID, "dssm_dense_fwd: bad arguments");
   HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, dtype == DSSM_BF16, M, N, K, A, lda, W, ldw, Z, ldz,
-                            bias, false, (hipStream_t)stream));
+                            bias, false, nullptr, (hipStream_t)stream));
   return DSSM_OK;
 }
 

@@ -7,64 +7,31 @@
 // columns [8l, 8l+8): each gathered W1 / dZ1 row is read with one 16-B load per lane (bf16)
 // or two (fp32), so a 300-wide bf16 row is one 608-B wave-instruction.  Column indices and
 // values are loaded coalesced by lane and broadcast with v_readlane (scalar address math).
+//
+// The transpose never puts a Zipf-hot column on one global atomic: each 1024-thread block
+// histograms its rows' columns in LDS (D+1 bins fit the 160 KiB LDS for D <= 38k), then adds
+// or reserves whole per-block counts with one global atomic per (block, column).
+//
+// dW1 splits columns by count: "heavy" columns (> kLight entries, incl. the virtual bias column
+// with every row) are summed by fixed 64-entry slices and added with coalesced fp32 atomics
+// (each atomic wave-instruction covers 256 contiguous bytes); "light" columns are summed by
+// one wave each, either here (materialized dW1 for the all-reduce) or inside the fused
+// W1 Adam kernel (adam.hip), which then never writes or re-reads a dense dW1.
 #include "common.h"
+#include "gather.h"
 #include "launch.h"
 
 namespace dssm {
 namespace {
-
-constexpr int kUnroll = 8;
-constexpr int kChunk = 64;  // CSC entries per wave in the dW1 kernels
 
 __device__ __forceinline__ void store8n(float* p, const float (&x)[8], int nvalid) {
   *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
   if (nvalid > 4) *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
 }
 
-// Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc.
-template <typename T>
-__device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
-                                                  const float* __restrict__ val, int s, int e,
-                                                  const T* __restrict__ M, int ldm, int c,
-                                                  int nvalid, float (&acc)[8]) {
-  const int lane = lane_id();
-  for (int base = s; base < e; base += 64) {
-    const int cnt = min(64, e - base);
-    int my_i = 0;
-    float my_v = 0.f;
-    if (lane < cnt) {
-      my_i = idx[base + lane];
-      my_v = val[base + lane];
-    }
-    int j = 0;
-    for (; j + kUnroll <= cnt; j += kUnroll) {
-      float x[kUnroll][8];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int r = bcast_i(my_i, j + u);
-        if (nvalid > 0) load8(M + (size_t)r * ldm + c, nvalid, x[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const float v = bcast_f(my_v, j + u);
-        if (nvalid > 0) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) acc[i] = __fmaf_rn(v, x[u][i], acc[i]);
-        }
-      }
-    }
-    for (; j < cnt; ++j) {
-      const int r = bcast_i(my_i, j);
-      const float v = bcast_f(my_v, j);
-      if (nvalid > 0) {
-        float x[8];
-        load8(M + (size_t)r * ldm + c, nvalid, x);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = __fmaf_rn(v, x[i], acc[i]);
-      }
-    }
-  }
-}
+}  // namespace
+
+namespace {
 
 template <typename TW>
 __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr,
@@ -78,8 +45,6 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
   for (int c0 = 0; c0 < ldz; c0 += 512) {
-    // All 64 lanes stay active through gather_accumulate: its index broadcasts read every
-    // lane's register (v_readlane ignores EXEC), so out-of-range lanes only skip the loads.
     const int c = c0 + lane * 8;
     const int nvalid = (c < ldz) ? n - c : 0;  // >= 8 full, 4 half, <= 0 pad-only/idle
     float acc[8];
@@ -90,61 +55,158 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
   }
 }
 
-__global__ void k_csc_count(const int* __restrict__ indptr, const int* __restrict__ indices,
-                            int rows, int* __restrict__ cnt) {
+// ---- CSR -> CSC ------------------------------------------------------------------------------
+// Blocks own contiguous row ranges; wave w of a block walks rows r0+w, r0+w+16, ... and its
+// lanes the row's entries (a row's columns are distinct, so a wave-instruction never collides).
+constexpr int kTB = 1024;  // threads per transpose block
+
+__global__ __launch_bounds__(kTB) void k_csc_hist(const int* __restrict__ indptr,
+                                                  const int* __restrict__ indices, int rows, int D,
+                                                  int rows_per_block, int* __restrict__ gcnt) {
+  extern __shared__ int hist[];
+  for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
+  __syncthreads();
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = r0 + w; r < r1; r += kTB / 64) {
+    const int s = indptr[r], e = indptr[r + 1];
+    for (int k = s + lane; k < e; k += 64) atomicAdd(&hist[indices[k]], 1);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += kTB) {
+    const int v = hist[c];
+    if (v) atomicAdd(&gcnt[c], v);
+  }
+}
+
+// Fallback when D+1 bins do not fit LDS: direct global atomics.
+__global__ void k_csc_count_global(const int* __restrict__ indptr, const int* __restrict__ indices,
+                                   int rows, int* __restrict__ cnt) {
   const int nnz = indptr[rows];
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += gridDim.x * blockDim.x)
     atomicAdd(&cnt[indices[e]], 1);
 }
 
-// Single-workgroup exclusive scan of the D+1 column counts (column D = virtual ones column
-// holding every row).  Also turns cnt[] into per-column fill cursors.
+// Single-workgroup exclusive scan of the D+1 column counts (column D = the virtual ones column
+// holding every row).  Counts are staged through LDS with coalesced loads/stores (thread t owns
+// 16 consecutive bins of each 16K-bin tile).  Writes col_ptr and the fill cursors, and
+// re-zeroes the counts for the next step (so no memset is needed on the stream).
+constexpr int kScanPer = 16, kScanTile = 1024 * kScanPer;
 __global__ __launch_bounds__(1024) void k_csc_scan(int* __restrict__ cnt, int D, int rows,
-                                                   int* __restrict__ col_ptr) {
+                                                   int* __restrict__ col_ptr,
+                                                   int* __restrict__ cursor) {
+  __shared__ int tile[kScanTile + kScanTile / 32];  // +1 int per 32: breaks the stride-16 conflicts
   __shared__ int wave_tot[16];
+  __shared__ int carry_s;
   const int ncols = D + 1;
-  const int t = threadIdx.x;
-  const int per = cdiv(ncols, 1024);
-  const int c0 = min(t * per, ncols), c1 = min(c0 + per, ncols);
-  int sum = 0;
-  for (int c = c0; c < c1; ++c) sum += (c == D) ? rows : cnt[c];
-  // inclusive wave scan
-  const int lane = t & 63, w = t >> 6;
-  int x = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wave_tot[w] = x;
-  __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int i = 0; i < 16; ++i) {
-      int v = wave_tot[i];
-      wave_tot[i] = run;
-      run += v;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  auto pad = [](int i) { return i + (i >> 5); };
+  if (t == 0) carry_s = 0;
+  for (int base = 0; base < ncols; base += kScanTile) {
+    for (int i = t; i < kScanTile; i += 1024) {
+      const int c = base + i;
+      tile[pad(i)] = (c < D) ? cnt[c] : (c == D ? rows : 0);
     }
+    __syncthreads();
+    int v[kScanPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      v[k] = tile[pad(t * kScanPer + k)];
+      sum += v[k];
+    }
+    int x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wave_tot[w] = x;
+    __syncthreads();
+    if (t == 0) {
+      int run = carry_s;
+      for (int i = 0; i < 16; ++i) {
+        const int a = wave_tot[i];
+        wave_tot[i] = run;
+        run += a;
+      }
+      carry_s = run;
+    }
+    __syncthreads();
+    int run = wave_tot[w] + x - sum;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      tile[pad(t * kScanPer + k)] = run;
+      run += v[k];
+    }
+    __syncthreads();
+    for (int i = t; i < kScanTile; i += 1024) {
+      const int c = base + i;
+      if (c < ncols) {
+        const int o = tile[pad(i)];
+        col_ptr[c] = o;
+        cursor[c] = o;
+        if (c < D) cnt[c] = 0;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  int run = wave_tot[w] + x - sum;  // exclusive prefix of this thread's chunk
-  for (int c = c0; c < c1; ++c) {
-    const int v = (c == D) ? rows : cnt[c];
-    col_ptr[c] = run;
-    cnt[c] = run;  // fill cursor
-    run += v;
-  }
-  if (t == 1023) col_ptr[ncols] = run;
+  if (t == 0) col_ptr[ncols] = carry_s;
 }
 
-__global__ __launch_bounds__(256) void k_csc_fill(const int* __restrict__ indptr,
+// Fill: local rank per entry from an LDS histogram, one returning global atomic per
+// (block, column) to reserve the block's slot range, then scatter (row, value, column).
+__global__ __launch_bounds__(kTB) void k_csc_fill(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices,
-                                                  const float* __restrict__ values, int rows, int D,
+                                                  const float* __restrict__ values, int rows,
+                                                  int D, int rows_per_block,
                                                   int* __restrict__ cursor,
                                                   const int* __restrict__ col_ptr,
+                                                  int* __restrict__ rank_tmp,
                                                   int* __restrict__ csc_row,
                                                   float* __restrict__ csc_val,
                                                   int* __restrict__ csc_col) {
+  extern __shared__ int hist[];
+  for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
+  __syncthreads();
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r = r0 + w; r < r1; r += kTB / 64) {
+    const int s = indptr[r], e = indptr[r + 1];
+    for (int k = s + lane; k < e; k += 64) rank_tmp[k] = atomicAdd(&hist[indices[k]], 1);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += kTB) {
+    const int v = hist[c];
+    if (v) hist[c] = atomicAdd(&cursor[c], v);
+  }
+  __syncthreads();
+  for (int r = r0 + w; r < r1; r += kTB / 64) {
+    const int s = indptr[r], e = indptr[r + 1];
+    for (int k = s + lane; k < e; k += 64) {
+      const int c = indices[k];
+      const int pos = hist[c] + rank_tmp[k];
+      csc_row[pos] = r;
+      csc_val[pos] = values[k];
+      csc_col[pos] = c;
+    }
+  }
+  const int vbase = col_ptr[D];
+  for (int r = r0 + threadIdx.x; r < r1; r += kTB) {
+    csc_row[vbase + r] = r;
+    csc_val[vbase + r] = 1.0f;
+    csc_col[vbase + r] = D;
+  }
+}
+
+// Fallback fill with per-entry global atomics (one wave per row).
+__global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__ indptr,
+                                                         const int* __restrict__ indices,
+                                                         const float* __restrict__ values,
+                                                         int rows, int D, int* __restrict__ cursor,
+                                                         const int* __restrict__ col_ptr,
+                                                         int* __restrict__ csc_row,
+                                                         float* __restrict__ csc_val,
+                                                         int* __restrict__ csc_col) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = lane_id();
@@ -164,7 +226,9 @@ __global__ __launch_bounds__(256) void k_csc_fill(const int* __restrict__ indptr
   }
 }
 
-// Columns' first kChunk entries: plain store of the row of G (zero for untouched columns).
+// ---- dW1 ---------------------------------------------------------------------------------------
+// Light columns (<= kLight entries): one wave sums and stores the whole row; heavy rows get 0
+// here (the heavy kernel adds into them afterwards).
 template <typename TZ>
 __global__ __launch_bounds__(256) void k_dw1_light(const int* __restrict__ col_ptr,
                                                    const int* __restrict__ csc_row,
@@ -174,19 +238,19 @@ __global__ __launch_bounds__(256) void k_dw1_light(const int* __restrict__ col_p
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c > D) return;
   const int lane = lane_id();
-  const int s = col_ptr[c];
-  const int e = min(col_ptr[c + 1], s + kChunk);
+  const int s = col_ptr[c], e = col_ptr[c + 1];
+  const bool heavy = e - s > kLightEntries;
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
-    const int nvalid = n - cc;  // lanes with nvalid <= 0 stay active for the broadcasts
+    const int nvalid = n - cc;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    gather_accumulate(csc_row, csc_val, s, e, dZ, lddz, cc, nvalid, acc);
+    if (!heavy) gather_accumulate(csc_row, csc_val, s, e, dZ, lddz, cc, nvalid, acc);
     if (nvalid > 0) store8n(G + (size_t)c * n + cc, acc, nvalid);
   }
 }
 
-// Remaining entries of heavy columns: fixed kChunk-entry slices of the CSC arrays, summed per
-// column run and added with fp32 atomics (after k_dw1_light has stored the first slice).
+// Heavy columns: fixed 64-entry slices of the CSC arrays, summed per column run, transposed
+// through LDS so each fp32 atomic wave-instruction covers 64 consecutive floats.
 template <typename TZ>
 __global__ __launch_bounds__(256) void k_dw1_heavy(const int* __restrict__ col_ptr,
                                                    const int* __restrict__ csc_row,
@@ -194,29 +258,34 @@ __global__ __launch_bounds__(256) void k_dw1_heavy(const int* __restrict__ col_p
                                                    const int* __restrict__ csc_col, int D,
                                                    const TZ* __restrict__ dZ, int lddz, int n,
                                                    float* __restrict__ G) {
-  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float sbuf[4][512];
+  const int wv = threadIdx.x >> 6;
+  const int chunk = blockIdx.x * 4 + wv;
   const int total = col_ptr[D + 1];
-  const int j0 = chunk * kChunk;
+  const int j0 = chunk * 64;
   if (j0 >= total) return;
-  const int j1 = min(j0 + kChunk, total);
+  const int j1 = min(j0 + 64, total);
   const int lane = lane_id();
   int j = j0;
   while (j < j1) {
     const int c = csc_col[j];
-    const int cs = col_ptr[c];
-    const int ce = min(col_ptr[c + 1], j1);
-    const int first = max(j, cs + kChunk);
-    if (first < ce) {
+    const int cs = col_ptr[c], cend = col_ptr[c + 1];
+    const int ce = min(cend, j1);
+    if (cend - cs > kLightEntries) {
       for (int c0 = 0; c0 < n; c0 += 512) {
         const int cc = c0 + lane * 8;
         const int nvalid = n - cc;
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        gather_accumulate(csc_row, csc_val, first, ce, dZ, lddz, cc, nvalid, acc);
+        gather_accumulate(csc_row, csc_val, j, ce, dZ, lddz, cc, nvalid, acc);
         if (nvalid > 0) {
-          float* g = G + (size_t)c * n + cc;
-          const int m = nvalid >= 8 ? 8 : 4;
-          for (int i = 0; i < m; ++i) atomicAdd(g + i, acc[i]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sbuf[wv][lane * 8 + i] = acc[i];
         }
+        __builtin_amdgcn_wave_barrier();
+        const int m = min(512, n - c0);
+        float* g = G + (size_t)c * n + c0;
+        for (int i = lane; i < m; i += 64) atomicAdd(g + i, sbuf[wv][i]);
+        __builtin_amdgcn_wave_barrier();
       }
     }
     j = ce;
@@ -238,33 +307,56 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
   return hipGetLastError();
 }
 
+size_t csc_scratch_ints(int D, int rows, int max_nnz) {
+  // cnt (D+1, padded) + cursor (D+1) + rank_tmp (max_nnz)
+  return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64;
+}
+
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
-                            int D, int max_nnz, int* cnt, int* col_ptr, int* csc_row,
+                            int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s) {
-  hipError_t err = hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)(D + 1), s);
-  if (err != hipSuccess) return err;
-  const int cblocks = max(1, min(cdiv(max_nnz, 256), 2048));
-  hipLaunchKernelGGL(k_csc_count, dim3(cblocks), dim3(256), 0, s, indptr, indices, rows, cnt);
-  hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr);
-  hipLaunchKernelGGL(k_csc_fill, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices, values,
-                     rows, D, cnt, col_ptr, csc_row, csc_val, csc_col);
+  int* cnt = scratch;                 // zero between steps (re-zeroed by k_csc_scan)
+  int* cursor = scratch + (D + 1 + 64);
+  int* rank_tmp = cursor + (D + 1 + 64);
+  const size_t lds = (size_t)D * sizeof(int);
+  if (lds <= 152 * 1024) {
+    // Few fat blocks (one CU each: the LDS histogram takes 120 KB): enough to keep the transpose
+    // short while leaving most CUs to the forward pass it overlaps on the main stream.
+    const int nblk = max(1, min(32, cdiv(rows, 64)));
+    const int rpb = cdiv(rows, nblk);
+    const int grid = cdiv(rows, rpb);
+    hipLaunchKernelGGL(k_csc_hist, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb,
+                       cnt);
+    hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
+    hipLaunchKernelGGL(k_csc_fill, dim3(grid), dim3(kTB), lds, s, indptr, indices, values, rows,
+                       D, rpb, cursor, col_ptr, rank_tmp, csc_row, csc_val, csc_col);
+  } else {
+    const int cblocks = max(1, min(cdiv(max_nnz, 256), 2048));
+    hipLaunchKernelGGL(k_csc_count_global, dim3(cblocks), dim3(256), 0, s, indptr, indices, rows,
+                       cnt);
+    hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
+    hipLaunchKernelGGL(k_csc_fill_global, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
+                       values, rows, D, cursor, col_ptr, csc_row, csc_val, csc_col);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
-                      bool dz_bf16, int lddz, int n, float* G, hipStream_t s) {
+                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s) {
   dim3 block(256);
   dim3 g1(cdiv(D + 1, 4));
-  dim3 g2(max(1, cdiv(cdiv(max_nnz + rows, kChunk), 4)));
+  dim3 g2(max(1, cdiv(cdiv(max_nnz + rows, 64), 4)));
   if (dz_bf16) {
-    hipLaunchKernelGGL(k_dw1_light<u16>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
-                       (const u16*)dZ, lddz, n, G);
+    if (light)
+      hipLaunchKernelGGL(k_dw1_light<u16>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
+                         (const u16*)dZ, lddz, n, G);
     hipLaunchKernelGGL(k_dw1_heavy<u16>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col, D,
                        (const u16*)dZ, lddz, n, G);
   } else {
-    hipLaunchKernelGGL(k_dw1_light<float>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
-                       (const float*)dZ, lddz, n, G);
+    if (light)
+      hipLaunchKernelGGL(k_dw1_light<float>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
+                         (const float*)dZ, lddz, n, G);
     hipLaunchKernelGGL(k_dw1_heavy<float>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col,
                        D, (const float*)dZ, lddz, n, G);
   }

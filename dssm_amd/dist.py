@@ -49,6 +49,8 @@ class DataParallel:
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.comm = RcclComm(self.rank, self.world) if (comm == "rccl" and self.world > 1) else None
+        if self.world > 1:
+            model.set_fused_w1_adam(False)  # the all-reduce needs the materialized dW1
 
     def allreduce_grads(self):
         if self.world == 1:

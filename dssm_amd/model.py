@@ -78,6 +78,7 @@ class DSSM:
         self.beta1_power = np.float32(beta1)
         self.beta2_power = np.float32(beta2)
         self.global_step = 0
+        self.fused_w1_adam = True
         if init:
             self.init_params(seed)
 
@@ -141,6 +142,19 @@ class DSSM:
                 ev[k].copy_(torch.as_tensor(np.asarray(v, np.float32)))
         check(self.lib.dssm_plan_sync_shadows(self._plan, stream_ptr()), "sync_shadows")
 
+    def load_adam_state(self, m: Dict[str, np.ndarray], v: Dict[str, np.ndarray],
+                        beta1_power: float, beta2_power: float, step: int = 0):
+        """Load named Adam slots (keys like named_params()) and the TF beta-power accumulators."""
+        for arena, src in ((self.adam_m, m), (self.adam_v, v)):
+            views = self._named_views(arena)
+            for k, a in src.items():
+                views[k].copy_(torch.as_tensor(np.asarray(a, np.float32)).reshape(views[k].shape))
+        self.beta1_power, self.beta2_power = np.float32(beta1_power), np.float32(beta2_power)
+        self.global_step = int(step)
+
+    def named_adam(self):
+        return self._named_views(self.adam_m), self._named_views(self.adam_v)
+
     # ---- feed --------------------------------------------------------------------------------
     def set_batch(self, batch: CSRBatch = None, indptr=None, indices=None, values=None,
                   non_blocking: bool = False):
@@ -167,6 +181,12 @@ class DSSM:
         self._batch_refs = (indptr, indices, values)
         check(self.lib.dssm_plan_set_batch(self._plan, ptr(indptr), ptr(indices), ptr(values)),
               "set_batch")
+
+    def set_fused_w1_adam(self, on: bool):
+        """Single-GPU fast path (default): dW1's light rows are computed inside Adam and never
+        materialized.  Must be off for the data-parallel all-reduce or to read dW1."""
+        check(self.lib.dssm_plan_set_fused_w1_adam(self._plan, 1 if on else 0), "set_fused")
+        self.fused_w1_adam = bool(on)
 
     # ---- step ---------------------------------------------------------------------------------
     def forward(self, train: bool = True, stream=None):

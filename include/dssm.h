@@ -112,6 +112,11 @@ int dssm_plan_backward(dssm_plan* plan, void* stream);
  * (1/world for data parallel mean).  Also refreshes the bf16 shadows. */
 int dssm_plan_adam(dssm_plan* plan, float beta1_power, float beta2_power, float grad_scale,
                    void* stream);
+/* Single-GPU fast path (default on): backward leaves the light rows of dW1 un-materialized and
+ * dssm_plan_adam computes them inline from the CSC transpose while updating W1, so a dense dW1 is
+ * never written or re-read.  Turn it off when the gradient arena must hold the full gradient
+ * (data-parallel all-reduce, or inspecting dW1). */
+int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, float beta1_power, float beta2_power, void* stream);
 

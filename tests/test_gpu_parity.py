@@ -2,9 +2,10 @@
 seeded batches.  Tolerances (north star: <= 1e-4 relative on loss and cosine scores):
 
 * fp32 mode: loss rel <= 1e-5, cos_sim_raw / prob abs <= 1e-5 (cosines are O(1)), gradients
-  max-abs error <= 1e-4 x max|g| per tensor, parameters after Adam <= 1e-5 abs except where the
-  oracle's gradient is below 1e-6 x max|g| (Adam normalises such rounding-level gradients to
-  O(lr) steps whose sign is noise).  Biases are excluded from parameter/gradient comparisons:
+  max-abs error <= 1e-4 x max|g| per tensor; one teacher-forced Adam step <= 1e-5 abs on every
+  element whose gradient is above 1e-3 x max|g| and <= 2 lr everywhere (Adam normalises
+  rounding-level gradients to O(lr) steps whose sign is noise; free-running steps amplify that
+  chaotically, so free runs only check the loss trajectory and a 3 lr envelope).  Biases are excluded from parameter/gradient comparisons:
   every FC is followed by batch-stat BN, so d loss / d b is exactly 0 in exact arithmetic and
   both sides hold only rounding noise (tests/test_oracle.py pins this).
 * bf16 mode (perf): bf16 weights/activations with fp32 accumulation — loss rel <= 2e-2,
@@ -26,8 +27,10 @@ def make(D, widths, BS, NEG, dtype, seed=11, **kw):
     from dssm_amd.model import DSSM
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
     p = O.init_params(cfg, seed=seed)
+    fused = kw.pop("fused", True)
     m = DSSM(D, widths, BS, NEG, dtype=dtype, init=False, **kw)
     m.load_params(p)
+    m.set_fused_w1_adam(fused)
     return cfg, p, m
 
 
@@ -57,7 +60,7 @@ CASES = [
 @pytest.mark.parametrize("case", CASES)
 def test_fp32_step_matches_oracle(case):
     D, widths, BS, NEG = case
-    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    cfg, p, m = make(D, widths, BS, NEG, "fp32", fused=False)  # materialize dW1 to compare it
     batch = synth_batch(D, BS, NEG, seed=1000, mean_nnz=min(32, D // 4))
     ema = O.make_ema(cfg)
     cache, ema1 = O.forward(cfg, p, ema, batch.as_dict(), True, np.float64)
@@ -91,56 +94,83 @@ def test_fp32_step_matches_oracle(case):
         grad_check(k, gg[k], g, 1e-4)
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("case", CASES[:3])
-def test_fp32_three_steps_params_and_eval(case):
+def test_fp32_adam_steps_teacher_forced(case, fused):
+    """Each step starts the GPU from the oracle's exact state (params, Adam slots, beta powers,
+    EMA), so one step's update is compared without the chaotic amplification of earlier
+    rounding-level differences (see test_gpu_golden.py for the tolerance rationale)."""
     D, widths, BS, NEG = case
-    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    cfg, p, m = make(D, widths, BS, NEG, "fp32", fused=fused)
     ema = O.make_ema(cfg)
     adam = O.AdamState(cfg, p)
-    last_grads = None
     for step in range(3):
         batch = synth_batch(D, BS, NEG, seed=2000 + step, mean_nnz=min(32, D // 4))
+        m.load_params(p, ema=ema)
+        m.load_adam_state(adam.m, adam.v, adam.beta1_power, adam.beta2_power, step)
         cache, ema = O.forward(cfg, p, ema, batch.as_dict(), True, np.float64)
-        last_grads = O.backward(cfg, p, cache, np.float64)
-        adam.step(p, last_grads)
+        grads = O.backward(cfg, p, cache, np.float64)
+        adam.step(p, grads)
         m.set_batch(batch)
         m.train_step()
         torch.cuda.synchronize()
         assert rel(m.loss_accuracy()[0], cache["loss"]) <= 1e-5
-        # Biases only carry Adam-amplified rounding noise (d loss/d b == 0 under batch-stat BN);
-        # re-sync them so that noise does not leak into the EMA means compared below.
-        views = m.named_params()
-        for l in range(1, len(widths) + 1):
-            views[f"b{l}"].copy_(torch.from_numpy(p[f"b{l}"]))
+        gp = {k: v.cpu().numpy() for k, v in m.named_params().items()}
+        gm, gv = m.named_adam()
+        for k in p:
+            if is_bias(k):
+                continue
+            d = np.abs(gp[k] - p[k])
+            well = np.abs(grads[k]) > 1e-3 * np.abs(grads[k]).max()
+            assert d[well].max(initial=0.0) <= 1e-5, (step, k, d[well].max(initial=0.0))
+            assert d.max() <= 2 * cfg.lr, (step, k)
+            assert np.abs(gm[k].cpu().numpy() - adam.m[k]).max() <= 1e-4 * np.abs(adam.m[k]).max() + 1e-12
+            assert np.abs(gv[k].cpu().numpy() - adam.v[k]).max() <= 1e-3 * np.abs(adam.v[k]).max() + 1e-20
+        ge = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
+        for k in ema:
+            np.testing.assert_allclose(ge[k], ema[k], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("case", CASES[:3])
+def test_fp32_free_running_and_eval(case):
+    """Three free-running steps: loss trajectory, EMA variances and a 3 lr parameter envelope,
+    then an eval-mode forward (EMA moments, no EMA update, new_dssm.py:85-86)."""
+    D, widths, BS, NEG = case
+    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    ema = O.make_ema(cfg)
+    adam = O.AdamState(cfg, p)
+    for step in range(3):
+        batch = synth_batch(D, BS, NEG, seed=2000 + step, mean_nnz=min(32, D // 4))
+        cache, grads, ema = O.train_step(cfg, p, ema, adam, batch.as_dict(), np.float64)
+        m.set_batch(batch)
+        m.train_step()
+        torch.cuda.synchronize()
+        assert rel(m.loss_accuracy()[0], cache["loss"]) <= 1e-4
     gp = {k: v.cpu().numpy() for k, v in m.named_params().items()}
     for k in p:
-        if is_bias(k):
-            continue
-        d = np.abs(gp[k] - p[k])
-        small = np.abs(last_grads[k]) <= 1e-6 * np.abs(last_grads[k]).max()
-        assert d[~small].max(initial=0.0) <= 1e-5, (k, d[~small].max(initial=0.0))
-        assert d.max() <= 6 * cfg.lr, k
+        if not is_bias(k):
+            assert np.abs(gp[k] - p[k]).max() <= 3 * cfg.lr, k
     ge = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
     for k in ema:
-        np.testing.assert_allclose(ge[k], ema[k], rtol=2e-4, atol=1e-6, err_msg=k)
-    # eval mode (on_train=False): EMA moments, no EMA update (new_dssm.py:85-86)
+        if k.endswith("_var"):
+            np.testing.assert_allclose(ge[k], ema[k], rtol=1e-3, atol=1e-6, err_msg=k)
     batch = synth_batch(D, BS, NEG, seed=3000, mean_nnz=min(32, D // 4))
-    gp_t = {k: v for k, v in gp.items()}
-    ev = O.forward(cfg, gp_t, ema, batch.as_dict(), False, np.float64)[0]
+    m.load_params(p, ema=ema)
+    ev = O.forward(cfg, p, ema, batch.as_dict(), False, np.float64)[0]
     m.set_batch(batch)
     m.forward(False)
     torch.cuda.synchronize()
-    assert rel(m.loss_accuracy()[0], ev["loss"]) <= 1e-4
-    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), ev["cos_sim_raw"], rtol=1e-4, atol=1e-4)
+    assert rel(m.loss_accuracy()[0], ev["loss"]) <= 1e-5
+    np.testing.assert_allclose(m.fetch("cos_sim_raw").ravel(), ev["cos_sim_raw"], rtol=1e-4, atol=1e-5)
     ge2 = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
-    for k in ge:
-        np.testing.assert_array_equal(ge[k], ge2[k])
+    for k in ge2:
+        np.testing.assert_array_equal(ema[k], ge2[k])
 
 
 def test_fp32_edge_rows():
     """Empty input rows (Z = bias only), a row at the 96-nnz cap, and a 1-query batch."""
     D, widths, BS, NEG = 300, (32, 32), 4, 4
-    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    cfg, p, m = make(D, widths, BS, NEG, "fp32", fused=False)
     b = synth_batch(D, BS, NEG, seed=5, mean_nnz=20)
     # make row 1 (a query) and row 9 (a negative) empty, row 2 dense (96 nnz)
     rows = []
@@ -169,7 +199,7 @@ def test_fp32_edge_rows():
 @pytest.mark.parametrize("case", [CASES[1], CASES[3]])
 def test_bf16_step_tracks_oracle(case):
     D, widths, BS, NEG = case
-    cfg, p, m = make(D, widths, BS, NEG, "bf16")
+    cfg, p, m = make(D, widths, BS, NEG, "bf16", fused=False)
     batch = synth_batch(D, BS, NEG, seed=1000, mean_nnz=min(32, D // 4))
     cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
     grads = O.backward(cfg, p, cache, np.float64)
@@ -191,7 +221,7 @@ def test_bf16_step_tracks_oracle(case):
 def test_c2_full_size_fp32_one_step():
     """BASELINE config 2 shape at full size (D=30k, 300/300/128, BS=1024, NEG=4) in fp32 mode."""
     D, widths, BS, NEG = 30000, (300, 300, 128), 1024, 4
-    cfg, p, m = make(D, widths, BS, NEG, "fp32")
+    cfg, p, m = make(D, widths, BS, NEG, "fp32", fused=False)
     batch = synth_batch(D, BS, NEG, seed=1000)
     cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
     grads = O.backward(cfg, p, cache, np.float64)
