@@ -35,6 +35,12 @@ __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, f
       p.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
       p.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
       *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) = p;
+      if (g.tptr) {
+        g.tptr[(int64_t)(c + 0) * g.tld + r] = f2bf(v.x);
+        g.tptr[(int64_t)(c + 1) * g.tld + r] = f2bf(v.y);
+        g.tptr[(int64_t)(c + 2) * g.tld + r] = f2bf(v.z);
+        g.tptr[(int64_t)(c + 3) * g.tld + r] = f2bf(v.w);
+      }
       return;
     }
   }
@@ -142,6 +148,12 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
     q.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
     q.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
     *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) = q;
+    if (g.tptr) {
+      g.tptr[(int64_t)(c + 0) * g.tld + r] = f2bf(v.x);
+      g.tptr[(int64_t)(c + 1) * g.tld + r] = f2bf(v.y);
+      g.tptr[(int64_t)(c + 2) * g.tld + r] = f2bf(v.z);
+      g.tptr[(int64_t)(c + 3) * g.tld + r] = f2bf(v.w);
+    }
   }
 }
 

@@ -2,17 +2,28 @@
 //
 // Towers: rows [0, row_split) are the query tower, [row_split, rows) the doc tower
 // (concat[pos; neg], new_dssm.py:130) — each gets its own moments / gamma / beta / EMA.
-// Statistics are deterministic two-level reductions: 64-row blocks (never straddling a tower)
-// produce per-column Welford partials (mean, M2), a finalize kernel merges them in a fixed
-// order (Chan et al.), so results do not depend on scheduling.  Thread <-> column keeps every
-// Z access a coalesced 256-B row segment per wave.
+//
+// Statistics are ONE launch per layer and direction: blocks of 256 rows (never straddling a
+// tower) x 64 columns (1024 threads: 16 row groups) compute per-column partials with all their loads in flight at once
+// (thread <-> column, so every access is a coalesced 256-B row segment per wave), publish them,
+// and the last block to finish a column chunk (agent-scope release/acquire ticket, per
+// cdna_hip_programming.md §6 G16) merges the partials of that chunk in a fixed order and writes
+// the per-column coefficients.  Results are deterministic: no float atomics, fixed merge order.
+//   forward : partial (mean, M2) by two-pass over the block's rows; merge by the parallel-axis
+//             formula (no E[x^2]-E[x]^2 cancellation); EMA update + affine coefficients.
+//   backward: partial sum(dy), sum(dy*xhat) with dy = dA*[y>0]; finals are dbeta, dgamma and the
+//             two means the input gradient needs.
+// The affine+ReLU itself is applied by the consumers (GEMM A-operand staging, cosine kernel) or
+// by k_bn_apply / k_bn_bwd_apply where a materialized tensor is needed.
 #include "common.h"
 #include "launch.h"
 
 namespace dssm {
 namespace {
 
-constexpr int RB = 64;  // rows per statistics block
+constexpr int NG = 16;        // row groups per block: 1024 threads = 16 groups x 64 columns
+constexpr int RB = 256;       // rows per statistics block
+constexpr int RPT = RB / NG;  // rows per thread
 
 struct RowBlocks {
   int nq, nd;
@@ -28,43 +39,28 @@ struct RowBlocks {
   }
 };
 
-__device__ __forceinline__ void chan_merge(float& na, float& ma, float& m2a, float nb, float mb,
-                                           float m2b) {
-  const float n = na + nb;
-  if (nb == 0.f) return;
-  const float delta = mb - ma;
-  const float f = nb / n;
-  ma = ma + delta * f;
-  m2a = m2a + m2b + delta * delta * na * f;
-  na = n;
-}
-
-__global__ __launch_bounds__(256) void k_bn_stats_partial(const float* __restrict__ Z, int ldz,
-                                                          BnTowers tw, float* __restrict__ part) {
-  __shared__ float sn[4][64], smu[4][64], sm2[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  const int rb = blockIdx.y;
-  RowBlocks blk(tw);
-  int r0, r1, tower;
-  blk.range(tw, rb, r0, r1, tower);
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < ldz) {
-    for (int r = r0 + g; r < r1; r += 4) {
-      const float x = Z[(size_t)r * ldz + c];
-      n += 1.f;
-      const float d = x - mean;
-      mean += d / n;
-      m2 = __fmaf_rn(d, x - mean, m2);
-    }
-  }
-  sn[g][lane] = n; smu[g][lane] = mean; sm2[g][lane] = m2;
+// Publish this block's partials and return true in every thread of the LAST block to arrive
+// for ticket `cnt` (expected arrivals: `arrivals`).  Producer: every wave drains its stores,
+// workgroup barrier, one agent-scope release, relaxed agent ticket.  Last block: one agent
+// acquire before any thread reads other blocks' partials.  The last block re-arms the ticket.
+__device__ __forceinline__ bool last_block_arrival(unsigned* cnt, unsigned arrivals,
+                                                   int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (g == 0 && c < ldz) {
-    for (int k = 1; k < 4; ++k) chan_merge(n, mean, m2, sn[k][lane], smu[k][lane], sm2[k][lane]);
-    part[((size_t)rb * 2 + 0) * ldz + c] = mean;
-    part[((size_t)rb * 2 + 1) * ldz + c] = m2;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == arrivals - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    *s_flag = last;
   }
+  __syncthreads();
+  return *s_flag != 0;
 }
 
 struct BnParams {
@@ -74,64 +70,159 @@ struct BnParams {
   float* ema_var[2];
 };
 
-__global__ __launch_bounds__(256) void k_bn_stats_finalize(const float* __restrict__ part, int ldz,
-                                                           int ncol, BnTowers tw, BnParams P,
-                                                           float eps, float decay, int train,
-                                                           float* __restrict__ batch_mean,
-                                                           float* __restrict__ batch_var,
-                                                           float* __restrict__ coef) {
-  __shared__ float sn[4][64], smu[4][64], sm2[4][64];
+// ---- forward statistics ----------------------------------------------------------------
+// part layout: [rb][2][ldz] = (mean, M2) of the block's rows.  coef: [4][2][ldz] = mean_used,
+// rstd, inv = gamma*rstd, shift = beta - mean*inv per tower.
+__global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, int ldz, int ncol,
+                                                  BnTowers tw, BnParams P, float eps, float decay,
+                                                  int train, float* __restrict__ part,
+                                                  unsigned* __restrict__ tickets,
+                                                  float* __restrict__ batch_mean,
+                                                  float* __restrict__ batch_var,
+                                                  float* __restrict__ coef) {
+  __shared__ float s_a[NG][64], s_b[NG][64];
+  __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int tower = blockIdx.y;
-  RowBlocks blk(tw);
-  const int first = tower == 0 ? 0 : blk.nq;
-  const int count = tower == 0 ? blk.nq : blk.nd;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (train && c < ncol) {
-    for (int k = g; k < count; k += 4) {
-      const int rb = first + k;
-      int r0, r1, tw_;
-      blk.range(tw, rb, r0, r1, tw_);
-      chan_merge(n, mean, m2, (float)(r1 - r0), part[((size_t)rb * 2) * ldz + c],
-                 part[((size_t)rb * 2 + 1) * ldz + c]);
-    }
-  }
-  sn[g][lane] = n; smu[g][lane] = mean; sm2[g][lane] = m2;
-  __syncthreads();
-  if (g != 0 || c >= ldz) return;
-  float* co = coef;  // [4][2][ldz]
-  const size_t o = (size_t)tower * ldz + c;
+  const int rb = blockIdx.y;
+  const RowBlocks blk(tw);
   const size_t plane = (size_t)2 * ldz;
-  if (c >= ncol) {
-    co[o] = 0.f; co[plane + o] = 0.f; co[2 * plane + o] = 0.f; co[3 * plane + o] = 0.f;
-    return;
-  }
-  float mu, var;
   if (train) {
-    for (int k = 1; k < 4; ++k) chan_merge(n, mean, m2, sn[k][lane], smu[k][lane], sm2[k][lane]);
-    mu = mean;
-    var = m2 / n;  // biased (tf.nn.moments)
-    if (batch_mean) {
-      batch_mean[tower * ncol + c] = mu;
-      batch_var[tower * ncol + c] = var;
+    int r0, r1, tower;
+    blk.range(tw, rb, r0, r1, tower);
+    float x[RPT];
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {  // all loads issued before any arithmetic
+      const int r = r0 + g + NG * i;
+      x[i] = (r < r1 && c < ldz) ? Z[(size_t)r * ldz + c] : 0.f;
+      n += (r < r1) ? 1 : 0;
     }
-    // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
-    float* em = P.ema_mean[tower];
-    float* ev = P.ema_var[tower];
-    const float one_m = 1.0f - decay;
-    em[c] = em[c] - (em[c] - mu) * one_m;
-    ev[c] = ev[c] - (ev[c] - var) * one_m;
-  } else {
-    mu = P.ema_mean[tower][c];
-    var = P.ema_var[tower][c];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) s += x[i];
+    const float mean = n ? s / (float)n : 0.f;
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + g + NG * i;
+      const float d = (r < r1) ? x[i] - mean : 0.f;
+      m2 = __fmaf_rn(d, d, m2);
+    }
+    // merge the 4 row groups (counts n_g) with the parallel-axis formula
+    s_a[g][lane] = s;
+    s_b[g][lane] = m2;
+    __syncthreads();
+    if (g == 0 && c < ldz) {
+      const int nb = r1 - r0;
+      float tot = 0.f;
+      for (int k = 0; k < NG; ++k) tot += s_a[k][lane];
+      const float mu = tot / (float)nb;
+      float M2 = 0.f;
+      for (int k = 0; k < NG; ++k) {
+        const int nk = max(0, min(RPT, (nb - k + NG - 1) / NG));
+        const float mk = nk ? s_a[k][lane] / (float)nk : 0.f;
+        const float dk = mk - mu;
+        M2 += s_b[k][lane] + (float)nk * dk * dk;
+      }
+      part[((size_t)rb * 2) * ldz + c] = mu;
+      part[((size_t)rb * 2 + 1) * ldz + c] = M2;
+    }
+    if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
+  } else if (rb != 0) {
+    return;  // eval: one block per column chunk just builds the coefficients from the EMA
   }
-  const float rstd = 1.0f / sqrtf(var + eps);
-  const float inv = rstd * P.gamma[tower][c];
-  co[o] = mu;
-  co[plane + o] = rstd;
-  co[2 * plane + o] = inv;
-  co[3 * plane + o] = P.beta[tower][c] - mu * inv;
+  // ---- finalize this column chunk (both towers) -------------------------------------------
+  for (int tower = 0; tower < 2; ++tower) {
+    const int first = tower == 0 ? 0 : blk.nq;
+    const int count = tower == 0 ? blk.nq : blk.nd;
+    const int nrows = tower == 0 ? tw.row_split : tw.rows - tw.row_split;
+    if (count == 0) continue;
+    float mu = 0.f, var = 0.f;
+    if (train) {
+      // pass 1: global mean = sum_i n_i mean_i / N
+      // every partial this thread merges is loaded up front (one round of loads)
+      constexpr int KMAX = 4;
+      float pm[KMAX], pv[KMAX], pn[KMAX];
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const int k = g + NG * j;
+        pm[j] = pv[j] = pn[j] = 0.f;
+        if (k < count && c < ldz) {
+          const int rbk = first + k;
+          int r0, r1, tt;
+          blk.range(tw, rbk, r0, r1, tt);
+          pn[j] = (float)(r1 - r0);
+          pm[j] = part[((size_t)rbk * 2) * ldz + c];
+          pv[j] = part[((size_t)rbk * 2 + 1) * ldz + c];
+        }
+      }
+      float a = 0.f;
+      for (int k = g + NG * KMAX; k < count; k += NG) {  // only for > KMAX*NG partials
+        const int rbk = first + k;
+        int r0, r1, tt;
+        blk.range(tw, rbk, r0, r1, tt);
+        if (c < ldz) a = __fmaf_rn((float)(r1 - r0), part[((size_t)rbk * 2) * ldz + c], a);
+      }
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) a = __fmaf_rn(pn[j], pm[j], a);
+      __syncthreads();
+      s_a[g][lane] = a;
+      __syncthreads();
+      float tot = 0.f;
+      for (int k = 0; k < NG; ++k) tot += s_a[k][lane];
+      mu = tot / (float)nrows;
+      // pass 2: M2 = sum_i M2_i + n_i (mean_i - mu)^2
+      float b = 0.f;
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const float d = pm[j] - mu;
+        b += pv[j] + pn[j] * d * d;
+      }
+      for (int k = g + NG * KMAX; k < count; k += NG) {
+        const int rbk = first + k;
+        int r0, r1, tt;
+        blk.range(tw, rbk, r0, r1, tt);
+        if (c < ldz) {
+          const float d = part[((size_t)rbk * 2) * ldz + c] - mu;
+          b += part[((size_t)rbk * 2 + 1) * ldz + c] + (float)(r1 - r0) * d * d;
+        }
+      }
+      s_b[g][lane] = b;
+      __syncthreads();
+      float tv = 0.f;
+      for (int k = 0; k < NG; ++k) tv += s_b[k][lane];
+      var = tv / (float)nrows;
+    }
+    if (g == 0 && c < ldz) {
+      const size_t o = (size_t)tower * ldz + c;
+      if (c >= ncol) {
+        coef[o] = 0.f; coef[plane + o] = 0.f; coef[2 * plane + o] = 0.f; coef[3 * plane + o] = 0.f;
+      } else {
+        if (train) {
+          if (batch_mean) {
+            batch_mean[tower * ncol + c] = mu;
+            batch_var[tower * ncol + c] = var;
+          }
+          // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
+          float* em = P.ema_mean[tower];
+          float* ev = P.ema_var[tower];
+          const float one_m = 1.0f - decay;
+          em[c] = em[c] - (em[c] - mu) * one_m;
+          ev[c] = ev[c] - (ev[c] - var) * one_m;
+        } else {
+          mu = P.ema_mean[tower][c];
+          var = P.ema_var[tower][c];
+        }
+        const float rstd = 1.0f / sqrtf(var + eps);
+        const float inv = rstd * P.gamma[tower][c];
+        coef[o] = mu;
+        coef[plane + o] = rstd;
+        coef[2 * plane + o] = inv;
+        coef[3 * plane + o] = P.beta[tower][c] - mu * inv;
+      }
+    }
+  }
 }
 
 template <typename TO>
@@ -160,8 +251,8 @@ __global__ __launch_bounds__(256) void k_bn_apply(const float* __restrict__ Z, i
       *reinterpret_cast<float4*>((float*)out + (size_t)r * ldz + c) = make_float4(y[0], y[1], y[2], y[3]);
     } else {
       uint2 p;
-      p.x = (unsigned)f2bf(y[0]) | ((unsigned)f2bf(y[1]) << 16);
-      p.y = (unsigned)f2bf(y[2]) | ((unsigned)f2bf(y[3]) << 16);
+      p.x = pack2bf(y[0], y[1]);
+      p.y = pack2bf(y[2], y[3]);
       *reinterpret_cast<uint2*>((u16*)out + (size_t)r * ldz + c) = p;
     }
   }
@@ -174,74 +265,92 @@ __device__ __forceinline__ void bwd_terms(float z, float da, float mu, float rst
   xhat = (z - mu) * rstd;
 }
 
-__global__ __launch_bounds__(256) void k_bn_bwd_partial(const float* __restrict__ Z,
-                                                        const float* __restrict__ dA, int ldz,
-                                                        BnTowers tw, const float* __restrict__ coef,
-                                                        float* __restrict__ part) {
-  __shared__ float s1s[4][64], s2s[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  const int rb = blockIdx.y;
-  RowBlocks blk(tw);
-  int r0, r1, tower;
-  blk.range(tw, rb, r0, r1, tower);
-  float s1 = 0.f, s2 = 0.f;
-  if (c < ldz) {
-    const size_t plane = (size_t)2 * ldz, o = (size_t)tower * ldz + c;
-    const float mu = coef[o], rstd = coef[plane + o], inv = coef[2 * plane + o],
-                sh = coef[3 * plane + o];
-    for (int r = r0 + g; r < r1; r += 4) {
-      float dy, xh;
-      bwd_terms(Z[(size_t)r * ldz + c], dA[(size_t)r * ldz + c], mu, rstd, inv, sh, dy, xh);
-      s1 += dy;
-      s2 = __fmaf_rn(dy, xh, s2);
-    }
-  }
-  s1s[g][lane] = s1; s2s[g][lane] = s2;
-  __syncthreads();
-  if (g == 0 && c < ldz) {
-    for (int k = 1; k < 4; ++k) { s1 += s1s[k][lane]; s2 += s2s[k][lane]; }
-    part[((size_t)rb * 2 + 0) * ldz + c] = s1;
-    part[((size_t)rb * 2 + 1) * ldz + c] = s2;
-  }
-}
-
 struct BnGrads {
   float* dgamma[2];
   float* dbeta[2];
 };
 
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float* __restrict__ part, int ldz,
-                                                         int ncol, BnTowers tw, BnGrads G,
-                                                         float* __restrict__ bcoef) {
-  __shared__ float s1s[4][64], s2s[4][64];
+// part: [rb][2][ldz] = (sum dy, sum dy*xhat); bcoef: [2][2][ldz] = (mean dy, mean dy*xhat).
+__global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__ Z,
+                                                      const float* __restrict__ dA, int ldz,
+                                                      int ncol, BnTowers tw,
+                                                      const float* __restrict__ coef, BnGrads G,
+                                                      float* __restrict__ part,
+                                                      unsigned* __restrict__ tickets,
+                                                      float* __restrict__ bcoef) {
+  __shared__ float s_a[NG][64], s_b[NG][64];
+  __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int tower = blockIdx.y;
-  RowBlocks blk(tw);
-  const int first = tower == 0 ? 0 : blk.nq;
-  const int count = tower == 0 ? blk.nq : blk.nd;
-  float s1 = 0.f, s2 = 0.f;
-  if (c < ldz) {
-    for (int k = g; k < count; k += 4) {
-      s1 += part[((size_t)(first + k) * 2) * ldz + c];
-      s2 += part[((size_t)(first + k) * 2 + 1) * ldz + c];
+  const int rb = blockIdx.y;
+  const RowBlocks blk(tw);
+  const size_t plane = (size_t)2 * ldz;
+  {
+    int r0, r1, tower;
+    blk.range(tw, rb, r0, r1, tower);
+    float zz[RPT], dd[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = r0 + g + NG * i;
+      const bool ok = r < r1 && c < ldz;
+      zz[i] = ok ? Z[(size_t)r * ldz + c] : 0.f;
+      dd[i] = ok ? dA[(size_t)r * ldz + c] : 0.f;
+    }
+    float s1 = 0.f, s2 = 0.f;
+    if (c < ldz) {
+      const size_t o = (size_t)tower * ldz + c;
+      const float mu = coef[o], rstd = coef[plane + o], inv = coef[2 * plane + o],
+                  sh = coef[3 * plane + o];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        float dy, xh;
+        bwd_terms(zz[i], dd[i], mu, rstd, inv, sh, dy, xh);  // dd = 0 on padded rows
+        s1 += dy;
+        s2 = __fmaf_rn(dy, xh, s2);
+      }
+    }
+    s_a[g][lane] = s1;
+    s_b[g][lane] = s2;
+    __syncthreads();
+    if (g == 0 && c < ldz) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = 0; k < NG; ++k) { t1 += s_a[k][lane]; t2 += s_b[k][lane]; }
+      part[((size_t)rb * 2) * ldz + c] = t1;
+      part[((size_t)rb * 2 + 1) * ldz + c] = t2;
     }
   }
-  s1s[g][lane] = s1; s2s[g][lane] = s2;
-  __syncthreads();
-  if (g != 0 || c >= ldz) return;
-  for (int k = 1; k < 4; ++k) { s1 += s1s[k][lane]; s2 += s2s[k][lane]; }
-  const float nrows = (float)(tower == 0 ? tw.row_split : tw.rows - tw.row_split);
-  const size_t o = (size_t)tower * ldz + c;
-  if (c < ncol) {
-    G.dbeta[tower][c] = s1;
-    G.dgamma[tower][c] = s2;
-    bcoef[o] = s1 / nrows;
-    bcoef[(size_t)2 * ldz + o] = s2 / nrows;
-  } else {
-    bcoef[o] = 0.f;
-    bcoef[(size_t)2 * ldz + o] = 0.f;
+  if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
+  for (int tower = 0; tower < 2; ++tower) {
+    const int first = tower == 0 ? 0 : blk.nq;
+    const int count = tower == 0 ? blk.nq : blk.nd;
+    if (count == 0) continue;
+    float a = 0.f, b = 0.f;
+    if (c < ldz) {
+#pragma unroll 4
+      for (int k = g; k < count; k += NG) {
+        a += part[((size_t)(first + k) * 2) * ldz + c];
+        b += part[((size_t)(first + k) * 2 + 1) * ldz + c];
+      }
+    }
+    __syncthreads();
+    s_a[g][lane] = a;
+    s_b[g][lane] = b;
+    __syncthreads();
+    if (g == 0 && c < ldz) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int k = 0; k < NG; ++k) { s1 += s_a[k][lane]; s2 += s_b[k][lane]; }
+      const float nrows = (float)(tower == 0 ? tw.row_split : tw.rows - tw.row_split);
+      const size_t o = (size_t)tower * ldz + c;
+      if (c < ncol) {
+        G.dbeta[tower][c] = s1;
+        G.dgamma[tower][c] = s2;
+        bcoef[o] = s1 / nrows;
+        bcoef[plane + o] = s2 / nrows;
+      } else {
+        bcoef[o] = 0.f;
+        bcoef[plane + o] = 0.f;
+      }
+    }
   }
 }
 
@@ -283,8 +392,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
       *reinterpret_cast<float4*>((float*)dZ + (size_t)r * ldz + c) = make_float4(out[0], out[1], out[2], out[3]);
     } else {
       uint2 p;
-      p.x = (unsigned)f2bf(out[0]) | ((unsigned)f2bf(out[1]) << 16);
-      p.y = (unsigned)f2bf(out[2]) | ((unsigned)f2bf(out[3]) << 16);
+      p.x = pack2bf(out[0], out[1]);
+      p.y = pack2bf(out[2], out[3]);
       *reinterpret_cast<uint2*>((u16*)dZ + (size_t)r * ldz + c) = p;
     }
   }
@@ -292,7 +401,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
 
 int ew_grid(size_t total) {
   size_t g = (total + 255) / 256;
-  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
 }  // namespace
@@ -303,24 +412,23 @@ size_t bn_partial_floats(int rows, int ldz, int row_split) {
   return (size_t)b.total() * 2 * ldz;
 }
 
+size_t bn_ticket_count(int ldz) { return (size_t)cdiv(ldz, 64); }
+
 hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const float* gamma_q,
                                const float* beta_q, const float* gamma_d, const float* beta_d,
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
-                               float* batch_mean, float* batch_var, float* partial, float* coef,
-                               hipStream_t s) {
+                               float* batch_mean, float* batch_var, float* partial,
+                               unsigned* tickets, float* coef, hipStream_t s) {
   RowBlocks b(t);
-  if (train)
-    hipLaunchKernelGGL(k_bn_stats_partial, dim3(cdiv(ldz, 64), b.total()), dim3(256), 0, s, Z,
-                       ldz, t, partial);
   BnParams P;
   P.gamma[0] = gamma_q; P.gamma[1] = gamma_d;
   P.beta[0] = beta_q; P.beta[1] = beta_d;
   P.ema_mean[0] = ema_q_mean; P.ema_mean[1] = ema_d_mean;
   P.ema_var[0] = ema_q_var; P.ema_var[1] = ema_d_var;
-  const int ntowers = t.row_split < t.rows ? 2 : 1;
-  hipLaunchKernelGGL(k_bn_stats_finalize, dim3(cdiv(ldz, 64), ntowers), dim3(256), 0, s, partial, ldz,
-                     n, t, P, eps, decay, train ? 1 : 0, batch_mean, batch_var, coef);
+  hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s, Z,
+                     ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean,
+                     batch_var, coef);
   return hipGetLastError();
 }
 
@@ -339,17 +447,14 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
-                         float* dbeta_d, float* partial, float* bcoef, void* dZ, bool dz_bf16,
-                         hipStream_t s) {
+                         float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
+                         void* dZ, bool dz_bf16, hipStream_t s) {
   RowBlocks b(t);
-  hipLaunchKernelGGL(k_bn_bwd_partial, dim3(cdiv(ldz, 64), b.total()), dim3(256), 0, s, Z, dA,
-                     ldz, t, coef, partial);
   BnGrads G;
   G.dgamma[0] = dgamma_q; G.dgamma[1] = dgamma_d;
   G.dbeta[0] = dbeta_q; G.dbeta[1] = dbeta_d;
-  const int ntowers = t.row_split < t.rows ? 2 : 1;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(ldz, 64), ntowers), dim3(256), 0, s, partial, ldz, n,
-                     t, G, bcoef);
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA, ldz,
+                     n, t, coef, G, partial, tickets, bcoef);
   const int grid = ew_grid((size_t)t.rows * (ldz / 4));
   if (dz_bf16)
     hipLaunchKernelGGL(k_bn_bwd_apply<u16>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,

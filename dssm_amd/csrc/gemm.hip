@@ -216,6 +216,245 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
   }
 }
 
+// ---- bf16 specialised GEMMs (perf mode) ------------------------------------------------------
+// Shared geometry: 64x64 output tile, 4 waves (2x2 of 32x32), BK = 64, double-buffered LDS with
+// the next K-step's global loads issued into registers before the current step's MFMAs.
+constexpr int NBK = 64, NLD = NBK + 8;  // k-contiguous tiles: [row][k], 144-B rows
+
+// "NT": C[M x ldc] = A[M x K] . B where B is given k-contiguous as BT[N x ldb] (BT[n][k]).
+// Forward (BT = transposed weight shadow, + bias) and dA (BT = the weight shadow itself).
+// BN_A: A = relu(Z*inv + shift) from the fp32 pre-BN activations Z [M x lda] and the layer's
+// BN coefficients (per row tower), converted to bf16 while staging; the blockIdx.x == 0 blocks
+// also write that activation (bf16, ld lda) to a_out for the dW GEMM.
+template <bool BN_A>
+__global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void* __restrict__ Aptr,
+                                                 int lda, const float* __restrict__ coef,
+                                                 int row_split, const u16* __restrict__ BT, int ldb,
+                                                 float* __restrict__ C, int ldc,
+                                                 const float* __restrict__ bias,
+                                                 u16* __restrict__ a_out) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2][64 * NLD];
+  __shared__ __attribute__((aligned(16))) u16 sB[2][64 * NLD];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
+  const bool write_a = BN_A && a_out != nullptr && blockIdx.x == 0;
+  const size_t plane = (size_t)2 * lda;
+  // thread -> (row, 8-wide k group) for the two staging groups of each operand
+  int am[2], ak[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int e = t + 256 * g;
+    am[g] = e >> 3;
+    ak[g] = (e & 7) * 8;
+  }
+  uint4 ra[2], rb[2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int gm = bm + am[g], gk = k0 + ak[g];
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (gm < M && gk < lda) {
+        if constexpr (BN_A) {
+          const float* z = (const float*)Aptr + (size_t)gm * lda + gk;
+          const float4 z0 = *reinterpret_cast<const float4*>(z);
+          const float4 z1 = *reinterpret_cast<const float4*>(z + 4);
+          const size_t o = (size_t)(gm < row_split ? 0 : 1) * lda + gk;
+          const float4 i0 = *reinterpret_cast<const float4*>(coef + 2 * plane + o);
+          const float4 i1 = *reinterpret_cast<const float4*>(coef + 2 * plane + o + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(coef + 3 * plane + o);
+          const float4 h1 = *reinterpret_cast<const float4*>(coef + 3 * plane + o + 4);
+          v.x = pack2bf(fmaxf(bn_affine(z0.x, i0.x, h0.x), 0.f), fmaxf(bn_affine(z0.y, i0.y, h0.y), 0.f));
+          v.y = pack2bf(fmaxf(bn_affine(z0.z, i0.z, h0.z), 0.f), fmaxf(bn_affine(z0.w, i0.w, h0.w), 0.f));
+          v.z = pack2bf(fmaxf(bn_affine(z1.x, i1.x, h1.x), 0.f), fmaxf(bn_affine(z1.y, i1.y, h1.y), 0.f));
+          v.w = pack2bf(fmaxf(bn_affine(z1.z, i1.z, h1.z), 0.f), fmaxf(bn_affine(z1.w, i1.w, h1.w), 0.f));
+          if (write_a) *reinterpret_cast<uint4*>(a_out + (size_t)gm * lda + gk) = v;
+        } else {
+          v = *reinterpret_cast<const uint4*>((const u16*)Aptr + (size_t)gm * lda + gk);
+        }
+      }
+      ra[g] = v;
+      const int gn = bn + am[g];
+      rb[g] = (gn < N && gk < ldb) ? *reinterpret_cast<const uint4*>(BT + (size_t)gn * ldb + gk)
+                                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      *reinterpret_cast<uint4*>(&sA[buf][am[g] * NLD + ak[g]]) = ra[g];
+      *reinterpret_cast<uint4*>(&sB[buf][am[g] * NLD + ak[g]]) = rb[g];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += NBK, buf ^= 1) {
+    const bool more = k0 + NBK < K;
+    if (more) load(k0 + NBK);
+#pragma unroll
+    for (int ks = 0; ks < NBK; ks += 32) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 32 + i * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 32 + j * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M && n < ldc) {
+          const float v = acc[i][j][r];
+          C[(size_t)m * ldc + n] = (n < N) ? (bias ? v + bias[n] : v) : 0.f;
+        }
+      }
+    }
+  }
+}
+
+// "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
+// B [K x ldb] (n contiguous), both bf16.  Both tiles are staged exactly as they lie in memory
+// ([k][m], [k][n]: 16-B loads and 16-B LDS writes) and the MFMA fragments, which need 8
+// consecutive k per lane, come from ds_read_b64_tr_b16 (4 k x 16 columns per 16-lane group,
+// delivered column-major).  ones_row: virtual all-ones A column at m == M-1 (-> bias grad).
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+__device__ __forceinline__ bf16x8 tr_frag(const u16* tile, int row0, int col0, int lane) {
+  // lanes 16g+4q+p read rows (row0 + 8g + q [+4]) at columns col0 + 4p..4p+3
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const u16* a0 = tile + (row0 + 8 * g + q) * NLD + col0 + 4 * p;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0 + 4 * NLD));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16* __restrict__ A,
+                                                 int lda, const u16* __restrict__ B, int ldb,
+                                                 float* __restrict__ C, int ldc, int ones_row,
+                                                 int k_per_split) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2][NBK * NLD];  // [k][m]
+  __shared__ __attribute__((aligned(16))) u16 sB[2][NBK * NLD];  // [k][n]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  const int Mload = ones_row ? M - 1 : M;
+  int sk[2], sc[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int e = t + 256 * g;
+    sk[g] = e >> 3;
+    sc[g] = (e & 7) * 8;
+  }
+  uint4 ra[2], rb[2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int gk = k0 + sk[g], gm = bm + sc[g], gn = bn + sc[g];
+      uint4 a = make_uint4(0u, 0u, 0u, 0u), b = make_uint4(0u, 0u, 0u, 0u);
+      if (gk < kend) {
+        if (gm + 8 <= Mload) {
+          a = *reinterpret_cast<const uint4*>(A + (size_t)gk * lda + gm);
+        } else {
+          u16 x[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            x[i] = (gm + i < Mload) ? A[(size_t)gk * lda + gm + i]
+                                    : ((ones_row && gm + i == Mload) ? (u16)0x3f80 : (u16)0);
+          a.x = x[0] | ((unsigned)x[1] << 16); a.y = x[2] | ((unsigned)x[3] << 16);
+          a.z = x[4] | ((unsigned)x[5] << 16); a.w = x[6] | ((unsigned)x[7] << 16);
+        }
+        if (gn + 8 <= N) {
+          b = *reinterpret_cast<const uint4*>(B + (size_t)gk * ldb + gn);
+        } else {
+          u16 x[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) x[i] = (gn + i < N) ? B[(size_t)gk * ldb + gn + i] : (u16)0;
+          b.x = x[0] | ((unsigned)x[1] << 16); b.y = x[2] | ((unsigned)x[3] << 16);
+          b.z = x[4] | ((unsigned)x[5] << 16); b.w = x[6] | ((unsigned)x[7] << 16);
+        }
+      }
+      ra[g] = a;
+      rb[g] = b;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      *reinterpret_cast<uint4*>(&sA[buf][sk[g] * NLD + sc[g]]) = ra[g];
+      *reinterpret_cast<uint4*>(&sB[buf][sk[g] * NLD + sc[g]]) = rb[g];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (kbeg < kend) {
+    load(kbeg);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += NBK, buf ^= 1) {
+    const bool more = k0 + NBK < kend;
+    if (more) load(k0 + NBK);
+#pragma unroll
+    for (int ks = 0; ks < NBK; ks += 32) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = tr_frag(sA[buf], ks, wm * 32 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(sB[buf], ks, wn * 32 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = C + (size_t)blockIdx.z * M * ldc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M && n < N) out[(size_t)m * ldc + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // dst[i] = sum_s slab[s][i] in fixed split order.
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ slab, int splits,
                                                        int64_t n, float* __restrict__ dst) {
@@ -257,8 +496,17 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
     const int kps = cdiv(cdiv(K, splits), BK) * BK;
     dim3 grid(cdiv(N, BN), cdiv(M, BM), splits);
     float* target = splits > 1 ? slab : C;
-    hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
-                       ldc, bias, ones_row ? 1 : 0, kps);
+    if constexpr (sizeof(T) == 2) {
+      if ((lda % 8) == 0 && (ldb % 8) == 0)
+        hipLaunchKernelGGL(k_gemm_tn, grid, block, 0, s, M, N, K, (const u16*)A, lda,
+                           (const u16*)B, ldb, target, ldc, ones_row ? 1 : 0, kps);
+      else
+        hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb,
+                           target, ldc, bias, ones_row ? 1 : 0, kps);
+    } else {
+      hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
+                         ldc, bias, ones_row ? 1 : 0, kps);
+    }
     if (splits > 1) {
       const int64_t n = (int64_t)M * ldc;
       const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
@@ -278,6 +526,20 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
 }
 
 }  // namespace
+
+hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a,
+                          const float* coef, int row_split, const uint16_t* BT, int ldb, float* C,
+                          int ldc, const float* bias, uint16_t* a_out, hipStream_t s) {
+  if ((lda % 8) || (ldb % 8) || K > lda || K > ldb) return hipErrorInvalidValue;
+  dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
+  if (bn_a)
+    hipLaunchKernelGGL(k_gemm_nt<true>, grid, block, 0, s, M, N, K, A, lda, coef, row_split,
+                       (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out);
+  else
+    hipLaunchKernelGGL(k_gemm_nt<false>, grid, block, 0, s, M, N, K, A, lda, coef, row_split,
+                       (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out);
+  return hipGetLastError();
+}
 
 size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
   const int splits = dw_splits(M, N, K, bf16 ? Cfg<u16>::BK : Cfg<float>::BK);

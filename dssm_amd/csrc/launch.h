@@ -38,28 +38,39 @@ hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
                        float* slab, hipStream_t s);
 
+// bf16 "NT" GEMM: C[M x ldc] = A . B + bias, B given k-contiguous as BT [N x ldb]
+// (BT[n][k] = B[k][n]).  bn_a: A = relu(Z*inv + shift) from fp32 Z [M x lda] with BN coefficients
+// coef ([4][2][lda], tower by row < row_split), also written once to a_out (bf16, ld lda) when
+// a_out != null; otherwise A is bf16 [M x lda].  bias may be null (dA).
+hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a,
+                          const float* coef, int row_split, const uint16_t* BT, int ldb, float* C,
+                          int ldc, const float* bias, uint16_t* a_out, hipStream_t s);
+
 // ---- batch norm (bn.hip) ----
 struct BnTowers {
   int row_split;   // rows [0,row_split) tower 0 (query), [row_split, rows) tower 1 (doc)
   int rows;
 };
 size_t bn_partial_floats(int rows, int ldz, int row_split);
-// Forward statistics + EMA + affine coefficients for both towers.
+// Ticket words one statistics launch needs (zero-initialised once; re-armed by the kernel).
+size_t bn_ticket_count(int ldz);
+// Forward statistics + EMA + affine coefficients for both towers, one launch.
 // coef layout (floats): [4][2][ldz] = mean_used, rstd, inv, shift per tower.
 hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const float* gamma_q,
                                const float* beta_q, const float* gamma_d, const float* beta_d,
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean /*[2*n] or null*/, float* batch_var,
-                               float* partial, float* coef, hipStream_t s);
+                               float* partial, unsigned* tickets, float* coef, hipStream_t s);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
 // Backward: dY = dA*(y>0); dgamma/dbeta per tower into grad slots; dZ (out dtype).
+// bcoef layout: [2][2][ldz] = (mean dy, mean dy*xhat) per tower.
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
-                         float* dbeta_d, float* partial, float* bcoef, void* dZ, bool dz_bf16,
-                         hipStream_t s);
+                         float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
+                         void* dZ, bool dz_bf16, hipStream_t s);
 
 // ---- cosine / loss (cosine.hip) ----
 hipError_t launch_cosine_loss(const float* y, int ld, int n, int bs, int neg, float gamma,
@@ -73,7 +84,9 @@ struct ShadowSeg {
   int64_t rows;    // weight rows (bias row excluded)
   int cols;        // == arena row length
   int ld;          // shadow leading dimension
-  uint16_t* ptr;   // bf16 shadow
+  uint16_t* ptr;   // bf16 shadow [rows x ld]
+  uint16_t* tptr;  // optional transposed bf16 shadow [cols x tld] (null: none)
+  int tld;
 };
 struct ShadowList {
   int count;

@@ -44,8 +44,9 @@ struct Layout {
   int64_t ema_total = 0;
   // workspace (bytes)
   size_t Z[DSSM_MAX_LAYERS], A[DSSM_MAX_LAYERS], dA[DSSM_MAX_LAYERS], dZ[DSSM_MAX_LAYERS];
+  size_t tickets[DSSM_MAX_LAYERS][2];
   size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
-      bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS];
+      bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
   size_t dw_slab, partial, cos_raw, cos_sim, prob, qnorm, loss_j, correct_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col;
   size_t ws = 0;
@@ -119,10 +120,14 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     Lt.dA[l] = take(R * ld * 4);
     Lt.dZ[l] = take(R * ld * act);
     Lt.coef[l] = take(4 * 2 * ld * 4);
+    Lt.tickets[l][0] = take(dssm::bn_ticket_count(Lt.ldp[l]) * 4);
+    Lt.tickets[l][1] = take(dssm::bn_ticket_count(Lt.ldp[l]) * 4);
     Lt.bcoef[l] = take(2 * 2 * ld * 4);
     Lt.bmean[l] = take(2 * Lt.n[l] * 4);
     Lt.bvar[l] = take(2 * Lt.n[l] * 4);
     Lt.shadow[l] = Lt.bf16 ? take((size_t)Lt.in_dim[l] * ld * 2) : 0;
+    // transposed bf16 weights [n_l x ldp(in)] for the whole-K forward GEMM (layers >= 2)
+    Lt.shadowT[l] = (Lt.bf16 && l > 0) ? take((size_t)Lt.n[l] * Lt.ldp[l - 1] * 2) : 0;
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
   Lt.partial = take(max_part * 4);
@@ -187,6 +192,8 @@ struct dssm_plan {
     return Lt.bf16 ? (const void*)at<u16>(Lt.shadow[l]) : (const void*)(p + Lt.fc_off[l]);
   }
   int weight_ld(int l) const { return Lt.bf16 ? Lt.ldp[l] : Lt.n[l]; }
+  // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
+  bool wholek(int l) const { return Lt.bf16 && l > 0; }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
   dssm::ShadowList shadows() {
     dssm::ShadowList s;
@@ -199,6 +206,8 @@ struct dssm_plan {
       g.cols = Lt.n[l];
       g.ld = Lt.ldp[l];
       g.ptr = at<uint16_t>(Lt.shadow[l]);
+      g.tptr = l > 0 ? at<uint16_t>(Lt.shadowT[l]) : nullptr;
+      g.tld = Lt.ldp[l - (l > 0 ? 1 : 0)];
     }
     return s;
   }
@@ -416,8 +425,18 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
         P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
         c.bn_eps, c.ema_decay, train != 0, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
-        P->at<float>(Lt.partial), P->at<float>(Lt.coef[l]), s));
+        P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]), s));
     const bool last = l == Lt.L - 1;
+    if (!last && P->wholek(l + 1)) {
+      // BN+ReLU of layer l applied while staging the next GEMM's A operand; the bf16 activation
+      // is written once (for the dW GEMM) by the first column tile.
+      HIP_TRY(dssm::launch_gemm_nt(Lt.R, Lt.n[l + 1], n, P->ws + Lt.Z[l], Lt.ldp[l], true,
+                                   P->at<float>(Lt.coef[l]), Lt.BS,
+                                   P->at<uint16_t>(Lt.shadowT[l + 1]), Lt.ldp[l],
+                                   P->at<float>(Lt.Z[l + 1]), Lt.ldp[l + 1], P->bias(l + 1),
+                                   P->at<uint16_t>(Lt.A[l]), s));
+      continue;
+    }
     HIP_TRY(dssm::launch_bn_apply(P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw,
                                   P->at<float>(Lt.coef[l]), true, P->ws + Lt.A[l],
                                   Lt.bf16 && !last, s));
@@ -454,16 +473,23 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
                                 P->at<float>(Lt.coef[l]), P->g + Lt.bn_off[l][0],
                                 P->g + Lt.bn_off[l][1], P->g + Lt.bn_off[l][2],
                                 P->g + Lt.bn_off[l][3], P->at<float>(Lt.partial),
-                                P->at<float>(Lt.bcoef[l]), P->ws + Lt.dZ[l], Lt.bf16, s));
+                                P->at<unsigned>(Lt.tickets[l][1]), P->at<float>(Lt.bcoef[l]),
+                                P->ws + Lt.dZ[l], Lt.bf16, s));
     if (l > 0) {
       const int kin = Lt.in_dim[l];
       float* gw = P->g + Lt.fc_off[l];
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_DW, Lt.bf16, kin + 1, n, Lt.R, P->ws + Lt.A[l - 1],
                                 Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true,
                                 P->at<float>(Lt.dw_slab), s));
-      HIP_TRY(dssm::launch_gemm(dssm::GEMM_DA, Lt.bf16, Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l],
-                                P->weight(l), P->weight_ld(l), P->at<float>(Lt.dA[l - 1]),
-                                Lt.ldp[l - 1], nullptr, false, nullptr, s));
+      if (P->wholek(l))  // dA = dZ . W^T: the weight shadow rows are already k-contiguous
+        HIP_TRY(dssm::launch_gemm_nt(Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l], false, nullptr,
+                                     Lt.BS, P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l],
+                                     P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], nullptr, nullptr, s));
+      else
+        HIP_TRY(dssm::launch_gemm(dssm::GEMM_DA, Lt.bf16, Lt.R, kin, n, P->ws + Lt.dZ[l],
+                                  Lt.ldp[l], P->weight(l), P->weight_ld(l),
+                                  P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], nullptr, false,
+                                  nullptr, s));
     } else {
       if (P->csc_pending) {
         HIP_TRY(hipStreamWaitEvent(s, P->ev_csc, 0));
@@ -551,7 +577,8 @@ int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, in
 }
 
 size_t dssm_bn_ws_bytes(int rows, int ldz) {
-  return align256(dssm::bn_partial_floats(rows, ldz, rows) * 4) + 4 * 2 * (size_t)ldz * 4;
+  return align256(dssm::bn_partial_floats(rows, ldz, rows) * 4) + align256(4 * 2 * (size_t)ldz * 4) +
+         align256(dssm::bn_ticket_count(ldz) * 4);
 }
 
 int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
@@ -563,12 +590,16 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
     return fail(DSSM_E_INVALID, "dssm_bn_relu_fwd: bad arguments (ldz must be round_up(n,8))");
   hipStream_t s = (hipStream_t)stream;
   const dssm::BnTowers tw{rows, rows};
-  float* part = static_cast<float*>(ws);
-  float* coef = reinterpret_cast<float*>(static_cast<char*>(ws) +
-                                         align256(dssm::bn_partial_floats(rows, ldz, rows) * 4));
+  // ws: [partials | coef | tickets]; the tickets must be zero on first use (caller zeroes ws
+  // once) and are re-armed by the kernel.
+  char* w = static_cast<char*>(ws);
+  float* part = reinterpret_cast<float*>(w);
+  const size_t o1 = align256(dssm::bn_partial_floats(rows, ldz, rows) * 4);
+  float* coef = reinterpret_cast<float*>(w + o1);
+  unsigned* tickets = reinterpret_cast<unsigned*>(w + o1 + align256(4 * 2 * (size_t)ldz * 4));
   HIP_TRY(dssm::launch_bn_fwd_stats(Z, ldz, n, tw, gamma, beta, gamma, beta, ema_mean, ema_var,
                                     ema_mean, ema_var, eps, decay, train != 0, batch_mean,
-                                    batch_var, part, coef, s));
+                                    batch_var, part, tickets, coef, s));
   HIP_TRY(dssm::launch_bn_apply(Z, ldz, n, tw, coef, relu != 0, out, out_dtype == DSSM_BF16, s));
   return DSSM_OK;
 }

@@ -60,17 +60,26 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
 // lanes the row's entries (a row's columns are distinct, so a wave-instruction never collides).
 constexpr int kTB = 1024;  // threads per transpose block
 
+constexpr int kTU = 8;  // entries per thread in flight
+
 __global__ __launch_bounds__(kTB) void k_csc_hist(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices, int rows, int D,
                                                   int rows_per_block, int* __restrict__ gcnt) {
   extern __shared__ int hist[];
   for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
-  __syncthreads();
   const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int r = r0 + w; r < r1; r += kTB / 64) {
-    const int s = indptr[r], e = indptr[r + 1];
-    for (int k = s + lane; k < e; k += 64) atomicAdd(&hist[indices[k]], 1);
+  const int e0 = indptr[r0], e1 = indptr[r1];  // the block's rows own a contiguous entry range
+  __syncthreads();
+  for (int base = e0; base < e1; base += kTB * kTU) {
+    int c[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + (int)threadIdx.x;
+      c[u] = e < e1 ? indices[e] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u)
+      if (c[u] >= 0) atomicAdd(&hist[c[u]], 1);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += kTB) {
@@ -103,9 +112,15 @@ __global__ __launch_bounds__(1024) void k_csc_scan(int* __restrict__ cnt, int D,
   auto pad = [](int i) { return i + (i >> 5); };
   if (t == 0) carry_s = 0;
   for (int base = 0; base < ncols; base += kScanTile) {
-    for (int i = t; i < kScanTile; i += 1024) {
-      const int c = base + i;
-      tile[pad(i)] = (c < D) ? cnt[c] : (c == D ? rows : 0);
+    {
+      int ld[kScanPer];  // all 16 loads in flight before the LDS writes
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k) {
+        const int c = base + k * 1024 + t;
+        ld[k] = (c < D) ? cnt[c] : (c == D ? rows : 0);
+      }
+#pragma unroll
+      for (int k = 0; k < kScanPer; ++k) tile[pad(k * 1024 + t)] = ld[k];
     }
     __syncthreads();
     int v[kScanPer], sum = 0;
@@ -154,7 +169,8 @@ __global__ __launch_bounds__(1024) void k_csc_scan(int* __restrict__ cnt, int D,
 }
 
 // Fill: local rank per entry from an LDS histogram, one returning global atomic per
-// (block, column) to reserve the block's slot range, then scatter (row, value, column).
+// (block, column) to reserve the block's slot range, then scatter (row, value, column).  Rows of
+// entries come from a binary search of the block's indptr slice staged in LDS.
 __global__ __launch_bounds__(kTB) void k_csc_fill(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices,
                                                   const float* __restrict__ values, int rows,
@@ -165,29 +181,71 @@ __global__ __launch_bounds__(kTB) void k_csc_fill(const int* __restrict__ indptr
                                                   int* __restrict__ csc_row,
                                                   float* __restrict__ csc_val,
                                                   int* __restrict__ csc_col) {
-  extern __shared__ int hist[];
-  for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
-  __syncthreads();
+  extern __shared__ int hist[];  // D bins, then the block's indptr slice
+  int* sptr = hist + D;
   const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int r = r0 + w; r < r1; r += kTB / 64) {
-    const int s = indptr[r], e = indptr[r + 1];
-    for (int k = s + lane; k < e; k += 64) rank_tmp[k] = atomicAdd(&hist[indices[k]], 1);
+  const int nr = r1 - r0;
+  for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
+  for (int i = threadIdx.x; i <= nr; i += kTB) sptr[i] = indptr[r0 + i];
+  __syncthreads();
+  const int e0 = sptr[0], e1 = sptr[nr];
+  for (int base = e0; base < e1; base += kTB * kTU) {
+    int c[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + (int)threadIdx.x;
+      c[u] = e < e1 ? indices[e] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + (int)threadIdx.x;
+      if (c[u] >= 0) rank_tmp[e] = atomicAdd(&hist[c[u]], 1);
+    }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < D; c += kTB) {
-    const int v = hist[c];
-    if (v) hist[c] = atomicAdd(&cursor[c], v);
+  for (int base = 0; base < D; base += kTB * kTU) {  // reserve: independent returning atomics
+    int v[kTU], got[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int c = base + u * kTB + (int)threadIdx.x;
+      v[u] = c < D ? hist[c] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int c = base + u * kTB + (int)threadIdx.x;
+      got[u] = v[u] ? atomicAdd(&cursor[c], v[u]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int c = base + u * kTB + (int)threadIdx.x;
+      if (v[u]) hist[c] = got[u];
+    }
   }
   __syncthreads();
-  for (int r = r0 + w; r < r1; r += kTB / 64) {
-    const int s = indptr[r], e = indptr[r + 1];
-    for (int k = s + lane; k < e; k += 64) {
-      const int c = indices[k];
-      const int pos = hist[c] + rank_tmp[k];
-      csc_row[pos] = r;
-      csc_val[pos] = values[k];
-      csc_col[pos] = c;
+  for (int base = e0; base < e1; base += kTB * kTU) {
+    int c[kTU], rk[kTU];
+    float val[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + (int)threadIdx.x;
+      const bool ok = e < e1;
+      c[u] = ok ? indices[e] : -1;
+      rk[u] = ok ? rank_tmp[e] : 0;
+      val[u] = ok ? values[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      if (c[u] < 0) continue;
+      const int e = base + u * kTB + (int)threadIdx.x;
+      int lo = 0, hi = nr;  // largest i with sptr[i] <= e
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (sptr[mid] <= e) lo = mid; else hi = mid;
+      }
+      const int pos = hist[c[u]] + rk[u];
+      csc_row[pos] = r0 + lo;
+      csc_val[pos] = val[u];
+      csc_col[pos] = c[u];
     }
   }
   const int vbase = col_ptr[D];
@@ -319,7 +377,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
   const size_t lds = (size_t)D * sizeof(int);
-  if (lds <= 152 * 1024) {
+  if (lds + (size_t)(cdiv(rows, max(1, min(32, cdiv(rows, 64)))) + 1) * sizeof(int) <= 156 * 1024) {
     // Few fat blocks (one CU each: the LDS histogram takes 120 KB): enough to keep the transpose
     // short while leaving most CUs to the forward pass it overlaps on the main stream.
     const int nblk = max(1, min(32, cdiv(rows, 64)));
@@ -328,8 +386,9 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     hipLaunchKernelGGL(k_csc_hist, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb,
                        cnt);
     hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
-    hipLaunchKernelGGL(k_csc_fill, dim3(grid), dim3(kTB), lds, s, indptr, indices, values, rows,
-                       D, rpb, cursor, col_ptr, rank_tmp, csc_row, csc_val, csc_col);
+    hipLaunchKernelGGL(k_csc_fill, dim3(grid), dim3(kTB), lds + (size_t)(rpb + 1) * sizeof(int), s,
+                       indptr, indices, values, rows, D, rpb, cursor, col_ptr, rank_tmp, csc_row,
+                       csc_val, csc_col);
   } else {
     const int cblocks = max(1, min(cdiv(max_nnz, 256), 2048));
     hipLaunchKernelGGL(k_csc_count_global, dim3(cblocks), dim3(256), 0, s, indptr, indices, rows,

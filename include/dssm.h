@@ -138,7 +138,8 @@ int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, in
                    const float* bias, float* Z, int ldz, void* stream);
 /* batch_normalization (new_dssm.py:62-88) + ReLU over rows [row0, row0+rows) of Z (one tower).
  * train!=0: batch moments, EMA update of ema_mean/ema_var; train==0: uses the EMA.
- * out: [rows x ldz] of out_dtype; batch_mean/var may be NULL.  ws: >= dssm_bn_ws_bytes(). */
+ * out: [rows x ldz] of out_dtype; batch_mean/var may be NULL.  ws: >= dssm_bn_ws_bytes(),
+ * zero-filled before its first use (it holds re-armed completion tickets). */
 size_t dssm_bn_ws_bytes(int rows, int ldz);
 int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
                      float* ema_mean, float* ema_var, float eps, float decay, int train, int relu,
