@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--allreduce", default="torch", choices=["torch", "rccl"])
+    ap.add_argument("--graph", type=int, default=1, help="replay hipGraph-captured steps (0: eager launches)")
+    ap.add_argument("--probes", type=int, default=1, help="HIP-event kernel probes in the timed region")
     return ap.parse_args()
 
 
@@ -99,25 +101,54 @@ def main():
                        torch.from_numpy(hb.indices).to(dev),
                        torch.from_numpy(hb.values).to(dev)))
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream(dev)  # graph capture needs a non-default stream
+    torch.cuda.set_stream(stream)
+    probe_ids = (("spmm_fwd", _lib.PROBE_SPMM_FWD), ("adam", _lib.PROBE_ADAM),
+                 ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC))
 
-    def step(i):
-        ip, ix, vv = staged[i % len(staged)]
-        model.set_batch(indptr=ip, indices=ix, values=vv)
-        model.forward(True)
-        model.backward()
-        if world > 1:
-            if comm is not None:
-                comm.allreduce_(model.grads)
+    def allreduce():
+        if comm is not None:
+            comm.allreduce_(model.grads)
+        else:
+            dist.all_reduce(model.grads)
+
+    if args.graph:
+        # One captured step per staged batch (the batch pointers are baked into the graph); with
+        # N>1 the all-reduce runs between the fwd+bwd graph and the Adam graph.  Timing probes
+        # are event nodes inside the graphs (their last replay is read after the timed region).
+        graphs = []
+        # Probes (graph event-record nodes cost a few us each) ride in batch 0's graph only, so
+        # they are sampled once per len(staged) steps inside the timed region.
+        for b, (ip, ix, vv) in enumerate(staged):
+            model.set_batch(indptr=ip, indices=ix, values=vv)
+            pr = bool(args.probes) and b == 0
+            if world > 1:
+                graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
             else:
-                dist.all_reduce(model.grads)
-        model.apply_adam(1.0 / world)
+                graphs.append(model.graph_build(probes=pr))
+        adam_graph = model.graph_build(_lib.GRAPH_ADAM, 1.0 / world, probes=bool(args.probes)) if world > 1 else None
+
+        def step(i):
+            model.graph_launch(graphs[i % len(graphs)])
+            if world > 1:
+                allreduce()
+                model.graph_launch(adam_graph)
+    else:
+        def step(i):
+            ip, ix, vv = staged[i % len(staged)]
+            model.set_batch(indptr=ip, indices=ix, values=vv)
+            model.forward(True)
+            model.backward()
+            if world > 1:
+                allreduce()
+            model.apply_adam(1.0 / world)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    for pid in (_lib.PROBE_SPMM_FWD, _lib.PROBE_ADAM, _lib.PROBE_DW1, _lib.PROBE_CSC):
-        model.probe_enable(pid, args.steps)
+    if not args.graph and args.probes:
+        for _, pid in probe_ids:
+            model.probe_enable(pid, args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -135,23 +166,26 @@ def main():
     loss, acc = model.loss_accuracy()
 
     probes = {}
-    for name, pid in (("spmm_fwd", _lib.PROBE_SPMM_FWD), ("adam", _lib.PROBE_ADAM),
-                      ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC)):
-        tot, cnt = model.probe_read(pid)
-        probes[name] = tot / max(cnt, 1)  # ms per launch
+    for name, pid in (probe_ids if args.probes else ()):
+        if args.graph:  # last replay of every staged-batch graph, all inside the timed region
+            g = adam_graph if (name == "adam" and adam_graph is not None) else graphs[0]
+            probes[name] = model.graph_probe_read(g, pid)
+        else:
+            tot, cnt = model.probe_read(pid)
+            probes[name] = tot / max(cnt, 1)  # ms per launch
     ms_per_step = 1e3 * elapsed / args.steps
     pairs = world * BS * (NEG + 1) * args.steps
     value = pairs / elapsed
 
     # roofline of the dominant HBM-bound kernels (algorithmic bytes / measured avg duration)
     rows = BS * (2 + NEG)
-    nnz_avg = int(np.mean([nnzs[(args.warmup + i) % len(nnzs)] for i in range(args.steps)]))
+    nnz_avg = int(nnzs[0] if args.graph else np.mean( [nnzs[(args.warmup + i) % len(nnzs)] for i in range(args.steps)]))
     s_w = 2 if args.dtype == "bf16" else 4
     n_params = int(model.params.numel())
     shadow = sum((D if l == 0 else WIDTHS[l - 1]) * WIDTHS[l] for l in range(len(WIDTHS))) if args.dtype == "bf16" else 0
     kern = {
-        "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes["spmm_fwd"]),
-        "adam": (adam_alg_bytes(n_params, shadow), probes["adam"]),
+        "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
+        "adam": (adam_alg_bytes(n_params, shadow), probes.get("adam", 0.0)),
     }
     rl = {}
     for k, (byt, ms) in kern.items():
@@ -170,7 +204,7 @@ def main():
                                "Zipf(1.1) trigram batches ~32 nnz/row, fwd+bwd+dense Adam",
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
-                   "avg_nnz_per_step": nnz_avg},
+                   "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager"},
         "roofline": dict(rl[dominant], kernel=dominant),
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,

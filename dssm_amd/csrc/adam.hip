@@ -2,7 +2,9 @@
 // parameter arena, dense (every element decays m/v every step, as TF does), fused with the
 // refresh of the bf16 weight shadows that the perf-mode SpMM/GEMMs read.
 //
-//   alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)          (host, fp32, like the TF kernel)
+//   alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)   (fp32, like the TF kernel; the beta powers
+//   live on the device and k_adam_advance multiplies them after each step, so a captured step
+//   graph needs no per-step host scalars)
 //   m += (g - m) * (1 - beta1);  v += (g*g - v) * (1 - beta2)
 //   p -= (m * alpha) / (sqrt(v) + eps)
 //
@@ -56,8 +58,9 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               int64_t i4_begin, int64_t i4_end, int64_t clear_from,
-                                              float alpha, float b1c, float b2c, float eps,
-                                              float gs, ShadowList sh) {
+                                              const float* __restrict__ st, float lr, float b1c,
+                                              float b2c, float eps, float gs, ShadowList sh) {
+  const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
   for (int64_t i = i4_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i4_end;
        i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -80,8 +83,10 @@ template <typename TZ>
 __global__ __launch_bounds__(256) void k_adam_w1_fused(
     float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     int D, int n, const int* __restrict__ col_ptr, const int* __restrict__ csc_row,
-    const float* __restrict__ csc_val, const TZ* __restrict__ dZ, int lddz, float alpha,
-    float b1c, float b2c, float eps, float gs, u16* __restrict__ shadow, int ldsh) {
+    const float* __restrict__ csc_val, const TZ* __restrict__ dZ, int lddz,
+    const float* __restrict__ st, float lr, float b1c, float b2c, float eps, float gs,
+    u16* __restrict__ shadow, int ldsh) {
+  const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);  // row of [W1; b1] == CSC column
   if (c > D) return;
   const int lane = lane_id();
@@ -136,6 +141,14 @@ __global__ __launch_bounds__(256) void k_adam_w1_fused(
   }
 }
 
+// beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32)
+__global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2) {
+  if (threadIdx.x == 0) {
+    st[0] = st[0] * beta1;
+    st[1] = st[1] * beta2;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p, ShadowSeg g) {
   const int64_t n4 = g.rows * g.cols / 4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
@@ -165,30 +178,35 @@ int grid_for(int64_t n4) {
 }  // namespace
 
 hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t begin, int64_t end,
-                       int64_t clear_from, float alpha, float beta1, float beta2, float eps,
-                       float grad_scale, ShadowList sh, hipStream_t s) {
+                       int64_t clear_from, const float* st, float lr, float beta1, float beta2,
+                       float eps, float grad_scale, ShadowList sh, hipStream_t s) {
   if ((begin % 4) || (end % 4)) return hipErrorInvalidValue;
   if (end <= begin) return hipSuccess;
   const int64_t b4 = begin / 4, e4 = end / 4;
   hipLaunchKernelGGL(k_adam, dim3(grid_for(e4 - b4)), dim3(256), 0, s, p, g, m, v, b4, e4,
-                     clear_from, alpha, 1.0f - beta1, 1.0f - beta2, eps, grad_scale, sh);
+                     clear_from, st, lr, 1.0f - beta1, 1.0f - beta2, eps, grad_scale, sh);
   return hipGetLastError();
 }
 
 hipError_t launch_adam_w1_fused(float* p, float* g, float* m, float* v, int D, int n,
                                 const int* col_ptr, const int* csc_row, const float* csc_val,
-                                const void* dZ, bool dz_bf16, int lddz, float alpha, float beta1,
-                                float beta2, float eps, float grad_scale, uint16_t* shadow,
-                                int ldsh, hipStream_t s) {
+                                const void* dZ, bool dz_bf16, int lddz, const float* st, float lr,
+                                float beta1, float beta2, float eps, float grad_scale,
+                                uint16_t* shadow, int ldsh, hipStream_t s) {
   dim3 grid(cdiv(D + 1, 4)), block(256);
   if (dz_bf16)
     hipLaunchKernelGGL(k_adam_w1_fused<u16>, grid, block, 0, s, p, g, m, v, D, n, col_ptr, csc_row,
-                       csc_val, (const u16*)dZ, lddz, alpha, 1.0f - beta1, 1.0f - beta2, eps,
+                       csc_val, (const u16*)dZ, lddz, st, lr, 1.0f - beta1, 1.0f - beta2, eps,
                        grad_scale, shadow, ldsh);
   else
     hipLaunchKernelGGL(k_adam_w1_fused<float>, grid, block, 0, s, p, g, m, v, D, n, col_ptr,
-                       csc_row, csc_val, (const float*)dZ, lddz, alpha, 1.0f - beta1,
+                       csc_row, csc_val, (const float*)dZ, lddz, st, lr, 1.0f - beta1,
                        1.0f - beta2, eps, grad_scale, shadow, ldsh);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam_advance(float* st, float beta1, float beta2, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, st, beta1, beta2);
   return hipGetLastError();
 }
 

@@ -39,30 +39,6 @@ struct RowBlocks {
   }
 };
 
-// Publish this block's partials and return true in every thread of the LAST block to arrive
-// for ticket `cnt` (expected arrivals: `arrivals`).  Producer: every wave drains its stores,
-// workgroup barrier, one agent-scope release, relaxed agent ticket.  Last block: one agent
-// acquire before any thread reads other blocks' partials.  The last block re-arms the ticket.
-__device__ __forceinline__ bool last_block_arrival(unsigned* cnt, unsigned arrivals,
-                                                   int* s_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == arrivals - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
-    *s_flag = last;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
-
 struct BnParams {
   const float* gamma[2];
   const float* beta[2];
@@ -79,7 +55,8 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
                                                   unsigned* __restrict__ tickets,
                                                   float* __restrict__ batch_mean,
                                                   float* __restrict__ batch_var,
-                                                  float* __restrict__ coef) {
+                                                  float* __restrict__ coef, int phase) {
+  // phase 0: partials + last-block finalize; 1: partials only; 2: finalize only (own launch)
   __shared__ float s_a[NG][64], s_b[NG][64];
   __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -87,7 +64,7 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
   const int rb = blockIdx.y;
   const RowBlocks blk(tw);
   const size_t plane = (size_t)2 * ldz;
-  if (train) {
+  if (train && phase != 2) {
     int r0, r1, tower;
     blk.range(tw, rb, r0, r1, tower);
     float x[RPT];
@@ -128,6 +105,7 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
       part[((size_t)rb * 2) * ldz + c] = mu;
       part[((size_t)rb * 2 + 1) * ldz + c] = M2;
     }
+    if (phase == 1) return;
     if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
   } else if (rb != 0) {
     return;  // eval: one block per column chunk just builds the coefficients from the EMA
@@ -277,7 +255,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
                                                       const float* __restrict__ coef, BnGrads G,
                                                       float* __restrict__ part,
                                                       unsigned* __restrict__ tickets,
-                                                      float* __restrict__ bcoef) {
+                                                      float* __restrict__ bcoef, int phase) {
   __shared__ float s_a[NG][64], s_b[NG][64];
   __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -285,7 +263,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
   const int rb = blockIdx.y;
   const RowBlocks blk(tw);
   const size_t plane = (size_t)2 * ldz;
-  {
+  if (phase != 2) {
     int r0, r1, tower;
     blk.range(tw, rb, r0, r1, tower);
     float zz[RPT], dd[RPT];
@@ -319,7 +297,8 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
       part[((size_t)rb * 2 + 1) * ldz + c] = t2;
     }
   }
-  if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
+  if (phase == 1) return;
+  if (phase == 0 && !last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
   for (int tower = 0; tower < 2; ++tower) {
     const int first = tower == 0 ? 0 : blk.nq;
     const int count = tower == 0 ? blk.nq : blk.nd;
@@ -419,16 +398,23 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean, float* batch_var, float* partial,
-                               unsigned* tickets, float* coef, hipStream_t s) {
+                               unsigned* tickets, float* coef, bool split, hipStream_t s) {
   RowBlocks b(t);
   BnParams P;
   P.gamma[0] = gamma_q; P.gamma[1] = gamma_d;
   P.beta[0] = beta_q; P.beta[1] = beta_d;
   P.ema_mean[0] = ema_q_mean; P.ema_mean[1] = ema_d_mean;
   P.ema_var[0] = ema_q_var; P.ema_var[1] = ema_d_var;
-  hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s, Z,
-                     ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean,
-                     batch_var, coef);
+  if (split && train) {
+    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t,
+                       P, eps, decay, 1, partial, tickets, batch_mean, batch_var, coef, 1);
+    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), 1), dim3(1024), 0, s, Z, ldz, n, t, P, eps,
+                       decay, 1, partial, tickets, batch_mean, batch_var, coef, 2);
+  } else {
+    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s,
+                       Z, ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean,
+                       batch_var, coef, 0);
+  }
   return hipGetLastError();
 }
 
@@ -448,13 +434,20 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, hipStream_t s) {
+                         void* dZ, bool dz_bf16, bool split, hipStream_t s) {
   RowBlocks b(t);
   BnGrads G;
   G.dgamma[0] = dgamma_q; G.dgamma[1] = dgamma_d;
   G.dbeta[0] = dbeta_q; G.dbeta[1] = dbeta_d;
-  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA, ldz,
-                     n, t, coef, G, partial, tickets, bcoef);
+  if (split) {
+    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA,
+                       ldz, n, t, coef, G, partial, tickets, bcoef, 1);
+    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), 1), dim3(1024), 0, s, Z, dA, ldz, n, t,
+                       coef, G, partial, tickets, bcoef, 2);
+  } else {
+    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA,
+                       ldz, n, t, coef, G, partial, tickets, bcoef, 0);
+  }
   const int grid = ew_grid((size_t)t.rows * (ldz / 4));
   if (dz_bf16)
     hipLaunchKernelGGL(k_bn_bwd_apply<u16>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,

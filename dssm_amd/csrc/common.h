@@ -74,5 +74,29 @@ __device__ __forceinline__ float bn_affine(float z, float inv, float shift) {
   return __fmaf_rn(z, inv, shift);
 }
 
+// Publish this block's partials and return true in every thread of the LAST block to arrive
+// for ticket `cnt` (expected arrivals: `arrivals`).  Producer: every wave drains its stores,
+// workgroup barrier, one agent-scope release, relaxed agent ticket.  Last block: one agent
+// acquire before any thread reads other blocks' partials.  The last block re-arms the ticket.
+__device__ __forceinline__ bool last_block_arrival(unsigned* cnt, unsigned arrivals,
+                                                   int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == arrivals - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 __host__ __device__ inline int ldp8(int n) { return (n + 7) & ~7; }
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -220,6 +220,7 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 // Shared geometry: 64x64 output tile, 4 waves (2x2 of 32x32), BK = 64, double-buffered LDS with
 // the next K-step's global loads issued into registers before the current step's MFMAs.
 constexpr int NBK = 64, NLD = NBK + 8;  // k-contiguous tiles: [row][k], 144-B rows
+constexpr int kNtMaxK = 512;            // BN-staged A: max K (LDS coefficient cache)
 
 // "NT": C[M x ldc] = A[M x K] . B where B is given k-contiguous as BT[N x ldb] (BT[n][k]).
 // Forward (BT = transposed weight shadow, + bias) and dA (BT = the weight shadow itself).
@@ -239,7 +240,18 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
   const int wm = w >> 1, wn = w & 1;
   const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
   const bool write_a = BN_A && a_out != nullptr && blockIdx.x == 0;
-  const size_t plane = (size_t)2 * lda;
+  // BN_A: the layer's (inv, shift) for both towers staged in LDS once; the raw fp32 Z loads of
+  // the next K-step stay in flight across this step's MFMAs and are transformed in store().
+  __shared__ float sCoef[BN_A ? 4 * kNtMaxK : 1];  // [tower][inv|shift][k]
+  if constexpr (BN_A) {
+    const size_t plane = (size_t)2 * lda;
+    for (int i = t; i < 2 * lda; i += 256) {
+      const int tower = i / lda, k = i - tower * lda;
+      sCoef[(tower * 2 + 0) * kNtMaxK + k] = coef[2 * plane + (size_t)tower * lda + k];
+      sCoef[(tower * 2 + 1) * kNtMaxK + k] = coef[3 * plane + (size_t)tower * lda + k];
+    }
+    __syncthreads();
+  }
   // thread -> (row, 8-wide k group) for the two staging groups of each operand
   int am[2], ak[2];
 #pragma unroll
@@ -249,31 +261,22 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
     ak[g] = (e & 7) * 8;
   }
   uint4 ra[2], rb[2];
+  float4 rz[2][2];
+  int kcur = 0;
   auto load = [&](int k0) {
+    kcur = k0;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       const int gm = bm + am[g], gk = k0 + ak[g];
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (gm < M && gk < lda) {
-        if constexpr (BN_A) {
-          const float* z = (const float*)Aptr + (size_t)gm * lda + gk;
-          const float4 z0 = *reinterpret_cast<const float4*>(z);
-          const float4 z1 = *reinterpret_cast<const float4*>(z + 4);
-          const size_t o = (size_t)(gm < row_split ? 0 : 1) * lda + gk;
-          const float4 i0 = *reinterpret_cast<const float4*>(coef + 2 * plane + o);
-          const float4 i1 = *reinterpret_cast<const float4*>(coef + 2 * plane + o + 4);
-          const float4 h0 = *reinterpret_cast<const float4*>(coef + 3 * plane + o);
-          const float4 h1 = *reinterpret_cast<const float4*>(coef + 3 * plane + o + 4);
-          v.x = pack2bf(fmaxf(bn_affine(z0.x, i0.x, h0.x), 0.f), fmaxf(bn_affine(z0.y, i0.y, h0.y), 0.f));
-          v.y = pack2bf(fmaxf(bn_affine(z0.z, i0.z, h0.z), 0.f), fmaxf(bn_affine(z0.w, i0.w, h0.w), 0.f));
-          v.z = pack2bf(fmaxf(bn_affine(z1.x, i1.x, h1.x), 0.f), fmaxf(bn_affine(z1.y, i1.y, h1.y), 0.f));
-          v.w = pack2bf(fmaxf(bn_affine(z1.z, i1.z, h1.z), 0.f), fmaxf(bn_affine(z1.w, i1.w, h1.w), 0.f));
-          if (write_a) *reinterpret_cast<uint4*>(a_out + (size_t)gm * lda + gk) = v;
-        } else {
-          v = *reinterpret_cast<const uint4*>((const u16*)Aptr + (size_t)gm * lda + gk);
-        }
+      const bool ok = gm < M && gk < lda;
+      if constexpr (BN_A) {
+        const float* z = (const float*)Aptr + (size_t)gm * lda + gk;
+        rz[g][0] = ok ? *reinterpret_cast<const float4*>(z) : make_float4(0.f, 0.f, 0.f, 0.f);
+        rz[g][1] = ok ? *reinterpret_cast<const float4*>(z + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        ra[g] = ok ? *reinterpret_cast<const uint4*>((const u16*)Aptr + (size_t)gm * lda + gk)
+                   : make_uint4(0u, 0u, 0u, 0u);
       }
-      ra[g] = v;
       const int gn = bn + am[g];
       rb[g] = (gn < N && gk < ldb) ? *reinterpret_cast<const uint4*>(BT + (size_t)gn * ldb + gk)
                                    : make_uint4(0u, 0u, 0u, 0u);
@@ -282,6 +285,23 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
   auto store = [&](int buf) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
+      if constexpr (BN_A) {
+        const int gm = bm + am[g], gk = kcur + ak[g];
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (gm < M && gk < lda) {
+          const float* ci = &sCoef[((gm < row_split ? 0 : 1) * 2) * kNtMaxK + gk];
+          const float* ch = ci + kNtMaxK;
+          const float z[8] = {rz[g][0].x, rz[g][0].y, rz[g][0].z, rz[g][0].w,
+                              rz[g][1].x, rz[g][1].y, rz[g][1].z, rz[g][1].w};
+          float y[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) y[i] = fmaxf(bn_affine(z[i], ci[i], ch[i]), 0.f);
+          v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
+          v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
+          if (write_a) *reinterpret_cast<uint4*>(a_out + (size_t)gm * lda + gk) = v;
+        }
+        ra[g] = v;
+      }
       *reinterpret_cast<uint4*>(&sA[buf][am[g] * NLD + ak[g]]) = ra[g];
       *reinterpret_cast<uint4*>(&sB[buf][am[g] * NLD + ak[g]]) = rb[g];
     }
@@ -530,7 +550,8 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
 hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a,
                           const float* coef, int row_split, const uint16_t* BT, int ldb, float* C,
                           int ldc, const float* bias, uint16_t* a_out, hipStream_t s) {
-  if ((lda % 8) || (ldb % 8) || K > lda || K > ldb) return hipErrorInvalidValue;
+  if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || (bn_a && lda > kNtMaxK))
+    return hipErrorInvalidValue;
   dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
   if (bn_a)
     hipLaunchKernelGGL(k_gemm_nt<true>, grid, block, 0, s, M, N, K, A, lda, coef, row_split,

@@ -5,6 +5,9 @@
 
 namespace dssm {
 
+// split=true: cross-block finalize steps run as their own small launch instead of inside the
+// producing kernel behind an agent-scope release/acquire ticket.
+
 // ---- sparse (spmm.hip) ----
 // FC1 forward: Z = X*W + b, one wave per CSR row, lane owns 8 output columns.
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
@@ -61,7 +64,8 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean /*[2*n] or null*/, float* batch_var,
-                               float* partial, unsigned* tickets, float* coef, hipStream_t s);
+                               float* partial, unsigned* tickets, float* coef, bool split,
+                               hipStream_t s);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
@@ -70,13 +74,17 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, hipStream_t s);
+                         void* dZ, bool dz_bf16, bool split, hipStream_t s);
 
 // ---- cosine / loss (cosine.hip) ----
-hipError_t launch_cosine_loss(const float* y, int ld, int n, int bs, int neg, float gamma,
-                              float* cos_raw, float* cos_sim, float* prob, float* qnorm,
-                              float* loss_j, float* correct_j, float* loss_out, float* dy,
-                              hipStream_t s);
+// z: last-layer activations [R x ld] fp32: pre-BN when coef != null (BN+ReLU applied on the
+// fly, embeddings written to y_out if non-null), else the embeddings themselves.
+// ws: cosine_ws_floats(bs) floats, zero-filled before first use (holds a re-armed ticket).
+size_t cosine_ws_floats(int bs);
+hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
+                              const float* coef, float* y_out, float* cos_raw, float* cos_sim,
+                              float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
+                              bool split, hipStream_t s);
 
 // ---- optimizer (adam.hip) ----
 struct ShadowSeg {
@@ -94,16 +102,18 @@ struct ShadowList {
 };
 // Adam over arena elements [begin, end) (multiples of 4); gradients at index >= clear_from are
 // zeroed after use.
+// st: device {beta1_power, beta2_power} of this step (alpha computed in-kernel).
 hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t begin, int64_t end,
-                       int64_t clear_from, float alpha, float beta1, float beta2, float eps,
-                       float grad_scale, ShadowList sh, hipStream_t s);
+                       int64_t clear_from, const float* st, float lr, float beta1, float beta2,
+                       float eps, float grad_scale, ShadowList sh, hipStream_t s);
+hipError_t launch_adam_advance(float* st, float beta1, float beta2, hipStream_t s);
 // Fused dW1 (light rows, inline from the CSC transpose) + Adam over the [W1; b1] block whose
 // arena pointers p/g/m/v are passed already offset; heavy rows read from g and cleared.
 hipError_t launch_adam_w1_fused(float* p, float* g, float* m, float* v, int D, int n,
                                 const int* col_ptr, const int* csc_row, const float* csc_val,
-                                const void* dZ, bool dz_bf16, int lddz, float alpha, float beta1,
-                                float beta2, float eps, float grad_scale, uint16_t* shadow,
-                                int ldsh, hipStream_t s);
+                                const void* dZ, bool dz_bf16, int lddz, const float* st, float lr,
+                                float beta1, float beta2, float eps, float grad_scale,
+                                uint16_t* shadow, int ldsh, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 
 }  // namespace dssm

@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -47,8 +48,8 @@ struct Layout {
   size_t tickets[DSSM_MAX_LAYERS][2];
   size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
-  size_t dw_slab, partial, cos_raw, cos_sim, prob, qnorm, loss_j, correct_j, loss;
-  size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col;
+  size_t dw_slab, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
+  size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
   size_t ws = 0;
   int max_nnz = 0;
 };
@@ -140,8 +141,7 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.cos_sim = take(K * Lt.BS * 4);
   Lt.prob = take(K * Lt.BS * 4);
   Lt.qnorm = take(Lt.BS * 4);
-  Lt.loss_j = take(Lt.BS * 4);
-  Lt.correct_j = take(Lt.BS * 4);
+  Lt.loss_j = take(dssm::cosine_ws_floats(Lt.BS) * 4);
   Lt.loss = take(2 * 4);
   Lt.csc_scratch = take(dssm::csc_scratch_ints(Lt.D, Lt.R, Lt.max_nnz) * 4);
   Lt.col_ptr = take((size_t)(Lt.D + 2) * 4);
@@ -149,6 +149,7 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.csc_row = take(ent * 4);
   Lt.csc_val = take(ent * 4);
   Lt.csc_col = take(ent * 4);
+  Lt.adam_state = take(4 * 4);  // {beta1_power, beta2_power} (device-side Adam step state)
   Lt.ws = w;
 }
 
@@ -166,8 +167,36 @@ struct dssm_plan {
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
+  // CSC build on the launch stream (default: measured faster than overlapping it on the side
+  // stream, whose join costs a cross-queue wait and whose kernels contend with the forward's);
+  // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
+  bool csc_inline = true;
+  bool split_finalize = false;  // DSSM_SPLIT_FINALIZE=1: finalize steps as separate launches
   hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
   hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
+  // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
+  struct GraphSlot {
+    hipGraphExec_t exec = nullptr;
+    hipEvent_t ev[DSSM_PROBE_COUNT][2] = {};
+    bool probes = false;
+  };
+  std::vector<GraphSlot*> graphs;
+  GraphSlot* capturing = nullptr;
+  // hipEventRecord on a capturing stream only marks a fork/join point; a timing record needs an
+  // explicit event-record node appended after the stream's current capture frontier.
+  static void graph_event_node(hipStream_t s, hipEvent_t e) {
+    hipStreamCaptureStatus st;
+    unsigned long long id;
+    hipGraph_t g;
+    const hipGraphNode_t* deps;
+    size_t nd;
+    if (hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &nd) != hipSuccess ||
+        st != hipStreamCaptureStatusActive)
+      return;
+    hipGraphNode_t node;
+    if (hipGraphAddEventRecordNode(&node, g, deps, nd, e) != hipSuccess) return;
+    hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+  }
   // Kernel timing probes: HIP events recorded on the launch stream around one kernel family.
   struct Probe {
     bool on = false;
@@ -176,10 +205,18 @@ struct dssm_plan {
   } probe[DSSM_PROBE_COUNT];
 
   void probe_begin(int id, hipStream_t s) {
+    if (capturing) {
+      if (capturing->probes) graph_event_node(s, capturing->ev[id][0]);
+      return;
+    }
     Probe& p = probe[id];
     if (p.on && p.next + 1 < (int)p.ev.size()) hipEventRecord(p.ev[p.next], s);
   }
   void probe_end(int id, hipStream_t s) {
+    if (capturing) {
+      if (capturing->probes) graph_event_node(s, capturing->ev[id][1]);
+      return;
+    }
     Probe& p = probe[id];
     if (p.on && p.next + 1 < (int)p.ev.size()) {
       hipEventRecord(p.ev[p.next + 1], s);
@@ -193,7 +230,7 @@ struct dssm_plan {
   }
   int weight_ld(int l) const { return Lt.bf16 ? Lt.ldp[l] : Lt.n[l]; }
   // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
-  bool wholek(int l) const { return Lt.bf16 && l > 0; }
+  bool wholek(int l) const { return Lt.bf16 && l > 0 && Lt.ldp[l - 1] <= 512; }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
   dssm::ShadowList shadows() {
     dssm::ShadowList s;
@@ -291,6 +328,15 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->m = adam_m;
   P->v = adam_v;
   P->ema = ema;
+  if (const char* e = std::getenv("DSSM_SPLIT_FINALIZE")) P->split_finalize = e[0] == '1';
+  if (const char* e = std::getenv("DSSM_CSC_SIDE")) P->csc_inline = e[0] != '1';
+  {
+    const float st[4] = {cfg->beta1, cfg->beta2, 0.f, 0.f};  // TF: beta*_power start at beta*
+    if (hipMemcpy(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice) != hipSuccess) {
+      delete P;
+      return fail(DSSM_E_HIP, "failed to initialise the device Adam state");
+    }
+  }
   if (hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&P->ev_batch, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&P->ev_csc, hipEventDisableTiming) != hipSuccess) {
@@ -308,6 +354,13 @@ int dssm_plan_destroy(dssm_plan* plan) {
     if (plan->side) {
       hipStreamSynchronize(plan->side);
       hipStreamDestroy(plan->side);
+    }
+    for (auto* g : plan->graphs) {
+      if (g->exec) hipGraphExecDestroy(g->exec);
+      for (auto& pr : g->ev)
+        for (hipEvent_t e : pr)
+          if (e) hipEventDestroy(e);
+      delete g;
     }
     if (plan->ev_batch) hipEventDestroy(plan->ev_batch);
     if (plan->ev_csc) hipEventDestroy(plan->ev_csc);
@@ -402,16 +455,21 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     // The CSC transpose depends only on the batch: run it on the side stream, overlapped with
     // the forward pass.  ev_batch orders it after everything already queued on `s` (including
     // the previous step's consumers of the CSC arrays).
-    HIP_TRY(hipEventRecord(P->ev_batch, s));
-    HIP_TRY(hipStreamWaitEvent(P->side, P->ev_batch, 0));
-    P->probe_begin(DSSM_PROBE_CSC, P->side);
+    hipStream_t cs = P->csc_inline ? s : P->side;
+    if (!P->csc_inline) {
+      HIP_TRY(hipEventRecord(P->ev_batch, s));
+      HIP_TRY(hipStreamWaitEvent(P->side, P->ev_batch, 0));
+    }
+    P->probe_begin(DSSM_PROBE_CSC, cs);
     HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
-                                   P->at<int>(Lt.csc_col), P->side));
-    P->probe_end(DSSM_PROBE_CSC, P->side);
-    HIP_TRY(hipEventRecord(P->ev_csc, P->side));
-    P->csc_pending = true;
+                                   P->at<int>(Lt.csc_col), cs));
+    P->probe_end(DSSM_PROBE_CSC, cs);
+    if (!P->csc_inline) {
+      HIP_TRY(hipEventRecord(P->ev_csc, P->side));
+      P->csc_pending = true;
+    }
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
@@ -425,8 +483,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
         P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
         c.bn_eps, c.ema_decay, train != 0, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
-        P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]), s));
+        P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]),
+        P->split_finalize, s));
     const bool last = l == Lt.L - 1;
+    if (last && Lt.bf16) break;  // the cosine kernel applies the last BN+ReLU itself
     if (!last && P->wholek(l + 1)) {
       // BN+ReLU of layer l applied while staging the next GEMM's A operand; the bf16 activation
       // is written once (for the dW GEMM) by the first column tile.
@@ -447,11 +507,14 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                 nullptr, s));
   }
   const int lL = Lt.L - 1;
+  const bool fused_last = Lt.bf16;  // fp32 parity mode keeps the separately applied embeddings
   HIP_TRY(dssm::launch_cosine_loss(
-      P->at<float>(Lt.A[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG, c.gamma,
-      P->at<float>(Lt.cos_raw), P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob),
-      P->at<float>(Lt.qnorm), P->at<float>(Lt.loss_j), P->at<float>(Lt.correct_j),
-      P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]), s));
+      P->at<float>(fused_last ? Lt.Z[lL] : Lt.A[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG,
+      c.gamma, fused_last ? P->at<float>(Lt.coef[lL]) : nullptr,
+      fused_last ? P->at<float>(Lt.A[lL]) : nullptr, P->at<float>(Lt.cos_raw),
+      P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
+      P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
+      P->split_finalize, s));
   P->fwd_train_done = train != 0;
   return DSSM_OK;
 }
@@ -462,8 +525,10 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const Layout& Lt = P->Lt;
   const dssm::BnTowers tw{Lt.BS, Lt.R};
-  if (!P->grads_clean) {
-    // backward() twice without an Adam step in between: re-zero the atomic-target blocks.
+  if (!P->grads_clean && P->fused_w1_adam) {
+    // backward() twice without an Adam step in between: re-zero the atomic-target blocks (only
+    // the fused path leaves dW1's heavy rows to be cleared by Adam; otherwise dw1-light
+    // overwrites every row before the heavy atomics).
     HIP_TRY(hipMemsetAsync(P->g, 0, sizeof(float) * (size_t)Lt.total, s));
   }
   P->grads_clean = false;
@@ -474,7 +539,7 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
                                 P->g + Lt.bn_off[l][1], P->g + Lt.bn_off[l][2],
                                 P->g + Lt.bn_off[l][3], P->at<float>(Lt.partial),
                                 P->at<unsigned>(Lt.tickets[l][1]), P->at<float>(Lt.bcoef[l]),
-                                P->ws + Lt.dZ[l], Lt.bf16, s));
+                                P->ws + Lt.dZ[l], Lt.bf16, P->split_finalize, s));
     if (l > 0) {
       const int kin = Lt.in_dim[l];
       float* gw = P->g + Lt.fc_off[l];
@@ -506,13 +571,11 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
   return DSSM_OK;
 }
 
-int dssm_plan_adam(dssm_plan* P, float beta1_power, float beta2_power, float grad_scale,
-                   void* stream) {
+int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   const dssm_config& c = P->cfg;
-  const float one = 1.0f;
-  const float alpha = c.lr * std::sqrt(one - beta2_power) / (one - beta1_power);
   const Layout& Lt = P->Lt;
+  float* st = P->at<float>(Lt.adam_state);
   hipStream_t s = (hipStream_t)stream;
   const int64_t rest = Lt.L > 1 ? Lt.fc_off[1] : Lt.bn_off[0][0];
   dssm::ShadowList sh = P->shadows();
@@ -523,19 +586,20 @@ int dssm_plan_adam(dssm_plan* P, float beta1_power, float beta2_power, float gra
     HIP_TRY(dssm::launch_adam_w1_fused(
         P->p + o, P->g + o, P->m + o, P->v + o, Lt.D, Lt.n[0], P->at<int>(Lt.col_ptr),
         P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val), P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0],
-        alpha, c.beta1, c.beta2, c.adam_eps, grad_scale,
+        st, c.lr, c.beta1, c.beta2, c.adam_eps, grad_scale,
         Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr, Lt.ldp[0], s));
     if (sh.count) {  // W1's shadow is written by the fused kernel
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
     }
-    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, rest, Lt.total, Lt.total, alpha, c.beta1,
-                              c.beta2, c.adam_eps, grad_scale, sh, s));
+    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, rest, Lt.total, Lt.total, st, c.lr,
+                              c.beta1, c.beta2, c.adam_eps, grad_scale, sh, s));
   } else {
-    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, 0, Lt.total, Lt.total, alpha, c.beta1,
+    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, 0, Lt.total, Lt.total, st, c.lr, c.beta1,
                               c.beta2, c.adam_eps, grad_scale, sh, s));
   }
   P->probe_end(DSSM_PROBE_ADAM, s);
+  HIP_TRY(dssm::launch_adam_advance(st, c.beta1, c.beta2, s));
   P->grads_clean = true;
   return DSSM_OK;
 }
@@ -546,10 +610,105 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* P, int on) {
   return DSSM_OK;
 }
 
-int dssm_plan_train_step(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
+int dssm_plan_train_step(dssm_plan* P, void* stream) {
   if (int rc = dssm_plan_forward(P, 1, stream)) return rc;
   if (int rc = dssm_plan_backward(P, stream)) return rc;
-  return dssm_plan_adam(P, beta1_power, beta2_power, 1.0f, stream);
+  return dssm_plan_adam(P, 1.0f, stream);
+}
+
+int dssm_plan_set_adam_state(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  const float st[2] = {beta1_power, beta2_power};
+  HIP_TRY(hipMemcpyAsync(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice,
+                         (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_plan_get_adam_state(dssm_plan* P, float* beta1_power, float* beta2_power, void* stream) {
+  if (!P || !beta1_power || !beta2_power) return fail(DSSM_E_INVALID, "null argument");
+  float st[2];
+  HIP_TRY(hipMemcpyAsync(st, P->ws + P->Lt.adam_state, sizeof st, hipMemcpyDeviceToHost,
+                         (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  *beta1_power = st[0];
+  *beta2_power = st[1];
+  return DSSM_OK;
+}
+
+int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_probes, void* stream,
+                          int* graph_id) {
+  if (!P || !graph_id) return fail(DSSM_E_INVALID, "null argument");
+  if (!stream) return fail(DSSM_E_INVALID, "graph capture needs a non-default stream");
+  if (!(parts & (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM)))
+    return fail(DSSM_E_INVALID, "graph parts must include DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM");
+  if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
+  if (P->fused_w1_adam && parts != (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM))
+    return fail(DSSM_E_INVALID, "with the fused W1 Adam a graph must hold the whole step");
+  hipStream_t s = (hipStream_t)stream;
+  auto* g = new dssm_plan::GraphSlot();
+  g->probes = with_probes != 0;
+  if (g->probes)
+    for (auto& pr : g->ev)
+      for (hipEvent_t& e : pr)
+        if (hipEventCreate(&e) != hipSuccess) {
+          delete g;
+          return fail(DSSM_E_HIP, "hipEventCreate failed");
+        }
+  const bool was_clean = P->grads_clean, was_fwd = P->fwd_train_done;
+  // A replayed step starts from the state a previous step leaves: clean gradients.
+  if (parts & DSSM_GRAPH_FWD_BWD) P->grads_clean = true;
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+  }
+  P->capturing = g;
+  int rc = DSSM_OK;
+  if (parts & DSSM_GRAPH_FWD_BWD) {
+    rc = dssm_plan_forward(P, 1, stream);
+    if (!rc) rc = dssm_plan_backward(P, stream);
+  }
+  if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
+  P->capturing = nullptr;
+  std::string err = rc ? g_err : std::string();
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(s, &graph);
+  // capture only recorded work: restore the host-side step state it advanced
+  P->grads_clean = (parts & DSSM_GRAPH_ADAM) ? true : (parts & DSSM_GRAPH_FWD_BWD ? false : was_clean);
+  P->fwd_train_done = (parts & DSSM_GRAPH_FWD_BWD) ? true : was_fwd;
+  if (rc || e != hipSuccess || !graph) {
+    if (graph) hipGraphDestroy(graph);
+    delete g;
+    return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  }
+  e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+  P->graphs.push_back(g);
+  *graph_id = (int)P->graphs.size() - 1;
+  return DSSM_OK;
+}
+
+int dssm_plan_graph_launch(dssm_plan* P, int graph_id, void* stream) {
+  if (!P || graph_id < 0 || graph_id >= (int)P->graphs.size())
+    return fail(DSSM_E_INVALID, "bad graph id");
+  HIP_TRY(hipGraphLaunch(P->graphs[graph_id]->exec, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_plan_graph_probe_read(dssm_plan* P, int graph_id, int probe_id, float* ms) {
+  if (!P || !ms || graph_id < 0 || graph_id >= (int)P->graphs.size() || probe_id < 0 ||
+      probe_id >= DSSM_PROBE_COUNT)
+    return fail(DSSM_E_INVALID, "bad argument");
+  auto* g = P->graphs[graph_id];
+  if (!g->probes) return fail(DSSM_E_INVALID, "graph built without probes");
+  HIP_TRY(hipEventSynchronize(g->ev[probe_id][1]));
+  HIP_TRY(hipEventElapsedTime(ms, g->ev[probe_id][0], g->ev[probe_id][1]));
+  return DSSM_OK;
 }
 
 // ---- functional entry points ------------------------------------------------------------
@@ -599,7 +758,7 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
   unsigned* tickets = reinterpret_cast<unsigned*>(w + o1 + align256(4 * 2 * (size_t)ldz * 4));
   HIP_TRY(dssm::launch_bn_fwd_stats(Z, ldz, n, tw, gamma, beta, gamma, beta, ema_mean, ema_var,
                                     ema_mean, ema_var, eps, decay, train != 0, batch_mean,
-                                    batch_var, part, tickets, coef, s));
+                                    batch_var, part, tickets, coef, false, s));
   HIP_TRY(dssm::launch_bn_apply(Z, ldz, n, tw, coef, relu != 0, out, out_dtype == DSSM_BF16, s));
   return DSSM_OK;
 }
@@ -610,8 +769,9 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
   if (!y || !cos_sim_raw || !cos_sim || !prob || !query_norm || !loss || !dy || !ws ||
       query_bs < 1 || neg < 1 || neg > 15 || n < 1 || n > 512 || ld < n)
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss: bad arguments");
-  HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, cos_sim_raw, cos_sim, prob,
-                                   query_norm, ws, ws + query_bs, loss, dy, (hipStream_t)stream));
+  HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
+                                   cos_sim, prob, query_norm, ws, loss, dy, false,
+                                   (hipStream_t)stream));
   return DSSM_OK;
 }
 

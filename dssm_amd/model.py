@@ -75,9 +75,8 @@ class DSSM:
                                    ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
                                    ptr(self.ema), C.byref(h)), "plan_create")
         self._plan = h
-        self.beta1_power = np.float32(beta1)
-        self.beta2_power = np.float32(beta2)
         self.global_step = 0
+        self._graphs = {}
         self.fused_w1_adam = True
         if init:
             self.init_params(seed)
@@ -149,8 +148,28 @@ class DSSM:
             views = self._named_views(arena)
             for k, a in src.items():
                 views[k].copy_(torch.as_tensor(np.asarray(a, np.float32)).reshape(views[k].shape))
-        self.beta1_power, self.beta2_power = np.float32(beta1_power), np.float32(beta2_power)
+        self.set_beta_powers(beta1_power, beta2_power)
         self.global_step = int(step)
+
+    # TF's beta1_power/beta2_power variables live on the device (advanced by the Adam launch, so a
+    # captured step needs no host scalars).
+    def beta_powers(self, stream=None):
+        b1, b2 = C.c_float(), C.c_float()
+        check(self.lib.dssm_plan_get_adam_state(self._plan, C.byref(b1), C.byref(b2),
+                                                stream_ptr(stream)), "get_adam_state")
+        return np.float32(b1.value), np.float32(b2.value)
+
+    def set_beta_powers(self, beta1_power: float, beta2_power: float, stream=None):
+        check(self.lib.dssm_plan_set_adam_state(self._plan, float(beta1_power), float(beta2_power),
+                                                stream_ptr(stream)), "set_adam_state")
+
+    @property
+    def beta1_power(self):
+        return self.beta_powers()[0]
+
+    @property
+    def beta2_power(self):
+        return self.beta_powers()[1]
 
     def named_adam(self):
         return self._named_views(self.adam_m), self._named_views(self.adam_v)
@@ -196,17 +215,38 @@ class DSSM:
         check(self.lib.dssm_plan_backward(self._plan, stream_ptr(stream)), "backward")
 
     def apply_adam(self, grad_scale: float = 1.0, stream=None):
-        check(self.lib.dssm_plan_adam(self._plan, float(self.beta1_power), float(self.beta2_power),
-                                      float(grad_scale), stream_ptr(stream)), "adam")
-        self.beta1_power = np.float32(self.beta1_power * np.float32(self.beta1))
-        self.beta2_power = np.float32(self.beta2_power * np.float32(self.beta2))
+        check(self.lib.dssm_plan_adam(self._plan, float(grad_scale), stream_ptr(stream)), "adam")
         self.global_step += 1
 
     def train_step(self, stream=None):
         """One sess.run(train_step) (new_dssm.py:267): forward(train) + backward + Adam."""
-        self.forward(True, stream)
-        self.backward(stream)
-        self.apply_adam(1.0, stream)
+        check(self.lib.dssm_plan_train_step(self._plan, stream_ptr(stream)), "train_step")
+        self.global_step += 1
+
+    # ---- hipGraph capture of a whole step ----------------------------------------------------
+    def graph_build(self, parts: int = _lib.GRAPH_FWD_BWD | _lib.GRAPH_ADAM, grad_scale: float = 1.0,
+                    probes: bool = False, stream=None) -> int:
+        """Capture the step for the CURRENT batch (set_batch) into a hipGraph owned by the plan.
+        Capture records work only; nothing runs until graph_launch.  Needs a non-default stream."""
+        sp = stream_ptr(stream)
+        if not sp:
+            raise ValueError("graph capture needs a non-default stream (torch.cuda.Stream())")
+        gid = C.c_int()
+        check(self.lib.dssm_plan_graph_build(self._plan, int(parts), float(grad_scale),
+                                             1 if probes else 0, sp, C.byref(gid)), "graph_build")
+        self._graphs[gid.value] = (parts, self._batch_refs)  # keep the batch tensors alive
+        return gid.value
+
+    def graph_launch(self, gid: int, stream=None):
+        check(self.lib.dssm_plan_graph_launch(self._plan, int(gid), stream_ptr(stream)), "graph_launch")
+        if self._graphs[gid][0] & _lib.GRAPH_ADAM:
+            self.global_step += 1
+
+    def graph_probe_read(self, gid: int, probe_id: int) -> float:
+        ms = C.c_float()
+        check(self.lib.dssm_plan_graph_probe_read(self._plan, int(gid), int(probe_id), C.byref(ms)),
+              "graph_probe_read")
+        return float(ms.value)
 
     # ---- kernel timing probes (HIP events on the launch stream) -------------------------------
     def probe_enable(self, probe_id: int, max_samples: int):
@@ -264,7 +304,7 @@ class DSSM:
     def state_dict(self) -> Dict[str, np.ndarray]:
         return {"params": self.params.cpu().numpy(), "adam_m": self.adam_m.cpu().numpy(),
                 "adam_v": self.adam_v.cpu().numpy(), "ema": self.ema.cpu().numpy(),
-                "beta_powers": np.array([self.beta1_power, self.beta2_power], np.float32),
+                "beta_powers": np.array(self.beta_powers(), np.float32),
                 "global_step": np.array([self.global_step], np.int64)}
 
     def load_state_dict(self, sd: Dict[str, np.ndarray]):
@@ -274,7 +314,7 @@ class DSSM:
             if a.shape != tuple(t.shape):
                 raise ValueError(f"checkpoint {name} shape {a.shape} != {tuple(t.shape)}")
             t.copy_(torch.from_numpy(a))
-        self.beta1_power, self.beta2_power = (np.float32(x) for x in sd["beta_powers"])
+        self.set_beta_powers(*(float(x) for x in sd["beta_powers"]))
         self.global_step = int(sd["global_step"][0])
         check(self.lib.dssm_plan_sync_shadows(self._plan, stream_ptr()), "sync_shadows")
 

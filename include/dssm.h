@@ -107,24 +107,37 @@ int dssm_plan_sync_shadows(dssm_plan* plan, void* stream);
 int dssm_plan_forward(dssm_plan* plan, int train, void* stream);
 /* Backward of the last train-mode forward into the gradient arena (TF autodiff of :124-209). */
 int dssm_plan_backward(dssm_plan* plan, void* stream);
-/* ApplyAdam over the whole arena with TF1.x semantics; beta*_power are the values BEFORE this
- * step's update (beta^t for step t, first step t=1).  grad_scale multiplies every gradient
- * (1/world for data parallel mean).  Also refreshes the bf16 shadows. */
-int dssm_plan_adam(dssm_plan* plan, float beta1_power, float beta2_power, float grad_scale,
-                   void* stream);
+/* ApplyAdam over the whole arena with TF1.x semantics, then beta*_power *= beta* (the powers
+ * live on the device: dssm_plan_set/get_adam_state; they start at beta1, beta2 like TF's
+ * beta1_power/beta2_power variables).  grad_scale multiplies every gradient (1/world for the
+ * data-parallel mean).  Also refreshes the bf16 shadows. */
+int dssm_plan_adam(dssm_plan* plan, float grad_scale, void* stream);
+int dssm_plan_set_adam_state(dssm_plan* plan, float beta1_power, float beta2_power, void* stream);
+int dssm_plan_get_adam_state(dssm_plan* plan, float* beta1_power, float* beta2_power, void* stream);
 /* Single-GPU fast path (default on): backward leaves the light rows of dW1 un-materialized and
  * dssm_plan_adam computes them inline from the CSC transpose while updating W1, so a dense dW1 is
  * never written or re-read.  Turn it off when the gradient arena must hold the full gradient
  * (data-parallel all-reduce, or inspecting dW1). */
 int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
-int dssm_plan_train_step(dssm_plan* plan, float beta1_power, float beta2_power, void* stream);
+int dssm_plan_train_step(dssm_plan* plan, void* stream);
+
+/* hipGraph capture of a step for the CURRENT batch pointers (dssm_plan_set_batch): parts =
+ * DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM (data-parallel runs launch the all-reduce between
+ * the two).  Replays then cost one launch per step.  with_probes: the graph records the timing
+ * probes' events (read back for its last replay with dssm_plan_graph_probe_read).  stream must
+ * not be the default stream.  Graphs are owned by the plan. */
+enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2 };
+int dssm_plan_graph_build(dssm_plan* plan, int parts, float grad_scale, int with_probes,
+                          void* stream, int* graph_id);
+int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);
 
 /* Kernel timing probes (bench/roofline): HIP events recorded on the launch stream around one
  * kernel family for up to max_samples launches (0 disables); read back the summed duration. */
 enum { DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC, DSSM_PROBE_COUNT };
 int dssm_plan_probe_enable(dssm_plan* plan, int probe_id, int max_samples);
 int dssm_plan_probe_read(dssm_plan* plan, int probe_id, float* total_ms, int* count);
+int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, float* ms);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
 /* FC1 (new_dssm.py:124-126): Z[r, :] = sum_k values[k] * W[indices[k], :] + bias.
@@ -147,7 +160,8 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
                      void* stream);
 /* Cosine_Similarity + Loss (new_dssm.py:182-213) fused with their backward: y rows
  * [q; pos; neg] [R x ld] fp32 -> cos_sim_raw, cos_sim, prob, query_norm, loss[2] (loss, acc),
- * dy [R x ld] (d loss / d y).  ws: >= 2*BS floats. */
+ * dy [R x ld] (d loss / d y).  ws: >= 2*ceil(BS/4) + 64 floats, zero-filled before its first
+ * use (it holds a completion ticket the kernel re-arms). */
 int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
                              float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
                              float* loss, float* dy, float* ws, void* stream);
