@@ -57,6 +57,26 @@ def adam_alg_bytes(n_params: int, shadow_elems: int) -> int:
     return 28 * n_params + 2 * shadow_elems
 
 
+# probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py)
+PMC_KERNELS = {"adam": "k_adam_step<{t}>", "spmm_fwd": "k_spmm_fwd<{t}>"}
+
+
+def pmc_traffic(dtype: str):
+    """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) from the newest
+    committed profiles/*_traffic.json; PMC counters cannot be read from inside the timed run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files or dtype != "bf16":
+        return {}, None
+    d = json.load(open(files[-1]))
+    out = {}
+    for probe, kname in PMC_KERNELS.items():
+        k = kname.format(t="unsigned short")
+        if k in d:
+            out[probe] = d[k]["hbm_bytes"]
+    return out, os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(seconds: float):
     """Time the CPU port of the step (oracle/, test infrastructure) on a bounded sample."""
     from oracle import cpu_port
@@ -187,12 +207,14 @@ def main():
         "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
         "adam": (adam_alg_bytes(n_params, shadow), probes.get("adam", 0.0)),
     }
+    traffic, traffic_src = pmc_traffic(args.dtype)
     rl = {}
     for k, (byt, ms) in kern.items():
         gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         rl[k] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": byt,
-                 "avg_ms": round(ms, 5), "traffic": None}
+                 "avg_ms": round(ms, 5), "traffic": traffic.get(k),
+                 "traffic_source": traffic_src if k in traffic else None}
     dominant = max(kern, key=lambda k: kern[k][1])
 
     out = {

@@ -3,24 +3,27 @@
 // refresh of the bf16 weight shadows that the perf-mode SpMM/GEMMs read.
 //
 //   alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t)   (fp32, like the TF kernel; the beta powers
-//   live on the device and k_adam_advance multiplies them after each step, so a captured step
-//   graph needs no per-step host scalars)
+//   live on the device and the step's last block multiplies them, so a captured step graph
+//   needs no per-step host scalars)
 //   m += (g - m) * (1 - beta1);  v += (g*g - v) * (1 - beta2)
 //   p -= (m * alpha) / (sqrt(v) + eps)
 //
 // HBM-bound: 28 B/param (p, m, v read+write, g read) + 2 B/param of shadow.
 //
-// Two kernels:
-//  * k_adam — float4 per thread over an arena range; gradients at index >= clear_from are
-//    zeroed after use ("consume and clear"), so the atomically accumulated gradient blocks
-//    start the next step at zero without a memset.
-//  * k_adam_w1_fused — single-GPU path: one wave per row of the [W1; b1] block computes the
-//    light rows' gradient inline from the CSC transpose and dZ1 (gather.h) and applies Adam in
-//    the same pass, so a dense dW1 is never written or re-read; heavy rows (summed by
-//    k_dw1_heavy into the gradient arena) are read and cleared.
+// One launch (k_adam_step) per step, two block roles:
+//  * fused W1 rows (single-GPU path): one wave per row of the [W1; b1] block computes the light
+//    rows' gradient inline from the CSC transpose and dZ1 (gather.h) and applies Adam in the
+//    same pass, so a dense dW1 is never written or re-read; heavy rows (summed by k_dw1_heavy
+//    into the gradient arena) are read and cleared ("consume and clear": the atomic targets
+//    start the next step at zero without a memset);
+//  * dense float4 streaming over the rest of the arena (or all of it when unfused).
+// The last block to finish advances the device beta powers.
 #include "common.h"
 #include "gather.h"
 #include "launch.h"
+
+#include <algorithm>
+#include <cstdlib>
 
 namespace dssm {
 namespace {
@@ -48,6 +51,26 @@ __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, f
   }
 }
 
+// Gradient of element i..i+3: from a deferred split-K slab (fixed split order, as
+// k_splitk_reduce would have summed it) or from the arena.
+__device__ __forceinline__ float4 slab_grad4(const SlabList& sl, int64_t i, const float* g) {
+#pragma unroll 1
+  for (int s = 0; s < sl.count; ++s) {
+    const SlabSeg& q = sl.seg[s];
+    const int64_t rel = i - q.offset;
+    if (rel >= 0 && rel < q.count) {
+      const float* b = q.slab + rel;
+      float4 acc = *reinterpret_cast<const float4*>(b);
+      for (int z = 1; z < q.splits; ++z) {
+        const float4 x = *reinterpret_cast<const float4*>(b + (size_t)z * q.count);
+        acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+      }
+      return acc;
+    }
+  }
+  return *reinterpret_cast<const float4*>(g + i);
+}
+
 __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, float alpha,
                                       float b1c, float b2c, float eps) {
   m += (g - m) * b1c;
@@ -55,77 +78,49 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
   p -= (m * alpha) / (sqrtf(v) + eps);
 }
 
-__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g,
-                                              float* __restrict__ m, float* __restrict__ v,
-                                              int64_t i4_begin, int64_t i4_end, int64_t clear_from,
-                                              const float* __restrict__ st, float lr, float b1c,
-                                              float b2c, float eps, float gs, ShadowList sh) {
-  const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
-  for (int64_t i = i4_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i4_end;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam1(pp.x, mm.x, vv.x, gg.x * gs, alpha, b1c, b2c, eps);
-    adam1(pp.y, mm.y, vv.y, gg.y * gs, alpha, b1c, b2c, eps);
-    adam1(pp.z, mm.z, vv.z, gg.z * gs, alpha, b1c, b2c, eps);
-    adam1(pp.w, mm.w, vv.w, gg.w * gs, alpha, b1c, b2c, eps);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (i * 4 >= clear_from) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (sh.count) write_shadow4(sh, i * 4, pp);
-  }
-}
-
+// One wave updates row c of [W1; b1] (CSC column c): light rows' gradient is gathered inline
+// from the CSC transpose and dZ1, heavy rows' gradient (k_dw1_heavy) is read and cleared.
 template <typename TZ>
-__global__ __launch_bounds__(256) void k_adam_w1_fused(
-    float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-    int D, int n, const int* __restrict__ col_ptr, const int* __restrict__ csc_row,
-    const float* __restrict__ csc_val, const TZ* __restrict__ dZ, int lddz,
-    const float* __restrict__ st, float lr, float b1c, float b2c, float eps, float gs,
-    u16* __restrict__ shadow, int ldsh) {
-  const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);  // row of [W1; b1] == CSC column
-  if (c > D) return;
+__device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
   const int lane = lane_id();
-  const int s = col_ptr[c], e = col_ptr[c + 1];
+  const int n = a.n;
+  const int s = a.col_ptr[c], e = a.col_ptr[c + 1];
   const bool heavy = e - s > kLightEntries;
+  const TZ* dZ = static_cast<const TZ*>(a.dZ);
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
     const int nvalid = n - cc;
     const size_t o = (size_t)c * n + cc;
     float P[8], M[8], V[8], G[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (nvalid > 0) {  // stream loads first: independent of the gather chain below
-      load8(p + o, nvalid, P);
-      load8(m + o, nvalid, M);
-      load8(v + o, nvalid, V);
+      load8(a.p + o, nvalid, P);
+      load8(a.m + o, nvalid, M);
+      load8(a.v + o, nvalid, V);
     }
     if (heavy) {
       if (nvalid > 0) {
-        load8(g + o, nvalid, G);
-        *reinterpret_cast<float4*>(g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (nvalid > 4) *reinterpret_cast<float4*>(g + o + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        load8(a.g + o, nvalid, G);
+        *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (nvalid > 4) *reinterpret_cast<float4*>(a.g + o + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     } else {
-      gather_accumulate(csc_row, csc_val, s, e, dZ, lddz, cc, nvalid, G);
+      gather_accumulate(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
     }
     if (nvalid > 0) {
       const int k = nvalid >= 8 ? 8 : 4;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        if (i < k) adam1(P[i], M[i], V[i], G[i] * gs, alpha, b1c, b2c, eps);
-      *reinterpret_cast<float4*>(p + o) = make_float4(P[0], P[1], P[2], P[3]);
-      *reinterpret_cast<float4*>(m + o) = make_float4(M[0], M[1], M[2], M[3]);
-      *reinterpret_cast<float4*>(v + o) = make_float4(V[0], V[1], V[2], V[3]);
+        if (i < k) adam1(P[i], M[i], V[i], G[i] * a.gs, alpha, a.b1c, a.b2c, a.eps);
+      *reinterpret_cast<float4*>(a.p + o) = make_float4(P[0], P[1], P[2], P[3]);
+      *reinterpret_cast<float4*>(a.m + o) = make_float4(M[0], M[1], M[2], M[3]);
+      *reinterpret_cast<float4*>(a.v + o) = make_float4(V[0], V[1], V[2], V[3]);
       if (k == 8) {
-        *reinterpret_cast<float4*>(p + o + 4) = make_float4(P[4], P[5], P[6], P[7]);
-        *reinterpret_cast<float4*>(m + o + 4) = make_float4(M[4], M[5], M[6], M[7]);
-        *reinterpret_cast<float4*>(v + o + 4) = make_float4(V[4], V[5], V[6], V[7]);
+        *reinterpret_cast<float4*>(a.p + o + 4) = make_float4(P[4], P[5], P[6], P[7]);
+        *reinterpret_cast<float4*>(a.m + o + 4) = make_float4(M[4], M[5], M[6], M[7]);
+        *reinterpret_cast<float4*>(a.v + o + 4) = make_float4(V[4], V[5], V[6], V[7]);
       }
-      if (shadow && c < D) {
-        u16* q = shadow + (size_t)c * ldsh + cc;
+      if (a.shadow && c < a.D) {
+        u16* q = a.shadow + (size_t)c * a.ldsh + cc;
         uint2 lo;
         lo.x = pack2bf(P[0], P[1]);
         lo.y = pack2bf(P[2], P[3]);
@@ -141,7 +136,64 @@ __global__ __launch_bounds__(256) void k_adam_w1_fused(
   }
 }
 
-// beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32)
+// The whole optimizer step in one launch: blocks [0, w1_blocks) run the fused W1 rows (grid-
+// stride over rows, one wave per row), the others stream the dense float4 range.  Every block
+// reads the beta powers at its start; the last block to finish (relaxed agent-scope tickets: it
+// only needs every other block to have READ them, which precedes their arrival) advances them
+// (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
+// the ticket.
+template <typename TZ>
+__global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
+  const float b1p = a.st[0], b2p = a.st[1];
+  const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+  if ((int)blockIdx.x < a.w1_blocks) {
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c <= a.D; c += a.w1_blocks * 4)
+      w1_row<TZ>(a, c, alpha);
+  } else {
+    const int bi = blockIdx.x - a.w1_blocks;
+    for (int64_t i = a.d4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < a.d4_end;
+         i += (int64_t)a.dense_blocks * blockDim.x) {
+      float4 pp = reinterpret_cast<float4*>(a.p)[i];
+      float4 gg = slab_grad4(a.slabs, i * 4, a.g);
+      float4 mm = reinterpret_cast<float4*>(a.m)[i];
+      float4 vv = reinterpret_cast<float4*>(a.v)[i];
+      adam1(pp.x, mm.x, vv.x, gg.x * a.gs, alpha, a.b1c, a.b2c, a.eps);
+      adam1(pp.y, mm.y, vv.y, gg.y * a.gs, alpha, a.b1c, a.b2c, a.eps);
+      adam1(pp.z, mm.z, vv.z, gg.z * a.gs, alpha, a.b1c, a.b2c, a.eps);
+      adam1(pp.w, mm.w, vv.w, gg.w * a.gs, alpha, a.b1c, a.b2c, a.eps);
+      reinterpret_cast<float4*>(a.p)[i] = pp;
+      reinterpret_cast<float4*>(a.m)[i] = mm;
+      reinterpret_cast<float4*>(a.v)[i] = vv;
+      if (i * 4 >= a.clear_from)
+        reinterpret_cast<float4*>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.sh.count) write_shadow4(a.sh, i * 4, pp);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && a.ticket) {
+    // Two-level ticket: same-address atomics serialise (~6 ns each; one counter for ~8k blocks
+    // measured +45 us), so blocks arrive on kAdamSubTickets counters 256 B apart and only the
+    // last arrival of each moves the top counter.
+    const unsigned k = blockIdx.x % kAdamSubTickets;
+    const unsigned nk = gridDim.x / kAdamSubTickets + (k < gridDim.x % kAdamSubTickets ? 1u : 0u);
+    unsigned* sub = a.ticket + 64 * (k + 1);
+    const unsigned t = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == nk - 1) {
+      __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned ntop = min(gridDim.x, (unsigned)kAdamSubTickets);
+      const unsigned u =
+          __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (u == ntop - 1) {
+        a.st[0] = b1p * a.beta1;
+        a.st[1] = b2p * a.beta2;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32): the separate-
+// launch variant (A/B knob DSSM_ADAM_SEP_ADVANCE=1)
 __global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2) {
   if (threadIdx.x == 0) {
     st[0] = st[0] * beta1;
@@ -170,6 +222,8 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
   }
 }
 
+int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
 int grid_for(int64_t n4) {
   const int64_t g = (n4 + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -177,36 +231,28 @@ int grid_for(int64_t n4) {
 
 }  // namespace
 
-hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t begin, int64_t end,
-                       int64_t clear_from, const float* st, float lr, float beta1, float beta2,
-                       float eps, float grad_scale, ShadowList sh, hipStream_t s) {
-  if ((begin % 4) || (end % 4)) return hipErrorInvalidValue;
-  if (end <= begin) return hipSuccess;
-  const int64_t b4 = begin / 4, e4 = end / 4;
-  hipLaunchKernelGGL(k_adam, dim3(grid_for(e4 - b4)), dim3(256), 0, s, p, g, m, v, b4, e4,
-                     clear_from, st, lr, 1.0f - beta1, 1.0f - beta2, eps, grad_scale, sh);
-  return hipGetLastError();
-}
-
-hipError_t launch_adam_w1_fused(float* p, float* g, float* m, float* v, int D, int n,
-                                const int* col_ptr, const int* csc_row, const float* csc_val,
-                                const void* dZ, bool dz_bf16, int lddz, const float* st, float lr,
-                                float beta1, float beta2, float eps, float grad_scale,
-                                uint16_t* shadow, int ldsh, hipStream_t s) {
-  dim3 grid(cdiv(D + 1, 4)), block(256);
+hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
+  if ((a.d4_begin < 0) || (a.d4_end < a.d4_begin)) return hipErrorInvalidValue;
+  a.b1c = 1.0f - a.beta1;
+  a.b2c = 1.0f - a.beta2;
+  static const int w1_cap = [] {
+    const char* e = std::getenv("DSSM_ADAM_W1_BLOCKS");
+    return e ? std::atoi(e) : kAdamW1Blocks;
+  }();
+  static const bool sep_advance = [] {
+    const char* e = std::getenv("DSSM_ADAM_SEP_ADVANCE");
+    return e && e[0] == '1';
+  }();
+  if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), w1_cap);
+  if (sep_advance) a.ticket = nullptr;
+  const int64_t n4 = a.d4_end - a.d4_begin;
+  a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
+  dim3 grid(a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
-    hipLaunchKernelGGL(k_adam_w1_fused<u16>, grid, block, 0, s, p, g, m, v, D, n, col_ptr, csc_row,
-                       csc_val, (const u16*)dZ, lddz, st, lr, 1.0f - beta1, 1.0f - beta2, eps,
-                       grad_scale, shadow, ldsh);
+    hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL(k_adam_w1_fused<float>, grid, block, 0, s, p, g, m, v, D, n, col_ptr,
-                       csc_row, csc_val, (const float*)dZ, lddz, st, lr, 1.0f - beta1,
-                       1.0f - beta2, eps, grad_scale, shadow, ldsh);
-  return hipGetLastError();
-}
-
-hipError_t launch_adam_advance(float* st, float beta1, float beta2, hipStream_t s) {
-  hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, st, beta1, beta2);
+    hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
+  if (!a.ticket) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2);
   return hipGetLastError();
 }
 

@@ -508,7 +508,7 @@ int dw_splits(int M, int N, int K, int BK) {
 template <typename T>
 hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, const T* B, int ldb,
                     float* C, int ldc, const float* bias, bool ones_row, float* slab,
-                    hipStream_t s) {
+                    hipStream_t s, int* deferred_splits) {
   dim3 block(256);
   constexpr int BK = Cfg<T>::BK;
   if (mode == GEMM_DW) {
@@ -527,7 +527,8 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
       hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
                          ldc, bias, ones_row ? 1 : 0, kps);
     }
-    if (splits > 1) {
+    if (deferred_splits) *deferred_splits = splits > 1 ? splits : 0;
+    if (splits > 1 && !deferred_splits) {
       const int64_t n = (int64_t)M * ldc;
       const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
       hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), block, 0, s, slab, splits, n, C);
@@ -569,12 +570,12 @@ size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
 
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
-                       float* slab, hipStream_t s) {
+                       float* slab, hipStream_t s, int* deferred_splits) {
   if (bf16)
     return launch_t<u16>(mode, M, N, K, (const u16*)A, lda, (const u16*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s);
+                         ones_row, slab, s, deferred_splits);
   return launch_t<float>(mode, M, N, K, (const float*)A, lda, (const float*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s);
+                         ones_row, slab, s, deferred_splits);
 }
 
 }  // namespace dssm

@@ -39,7 +39,8 @@ size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16);
 //      (gemm_dw_slab_floats) then a fixed-order reduce into C (ldc must equal N).
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
-                       float* slab, hipStream_t s);
+                       float* slab, hipStream_t s,
+                       int* deferred_splits = nullptr);
 
 // bf16 "NT" GEMM: C[M x ldc] = A . B + bias, B given k-contiguous as BT [N x ldb]
 // (BT[n][k] = B[k][n]).  bn_a: A = relu(Z*inv + shift) from fp32 Z [M x lda] with BN coefficients
@@ -102,18 +103,50 @@ struct ShadowList {
 };
 // Adam over arena elements [begin, end) (multiples of 4); gradients at index >= clear_from are
 // zeroed after use.
-// st: device {beta1_power, beta2_power} of this step (alpha computed in-kernel).
-hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t begin, int64_t end,
-                       int64_t clear_from, const float* st, float lr, float beta1, float beta2,
-                       float eps, float grad_scale, ShadowList sh, hipStream_t s);
-hipError_t launch_adam_advance(float* st, float beta1, float beta2, hipStream_t s);
-// Fused dW1 (light rows, inline from the CSC transpose) + Adam over the [W1; b1] block whose
-// arena pointers p/g/m/v are passed already offset; heavy rows read from g and cleared.
-hipError_t launch_adam_w1_fused(float* p, float* g, float* m, float* v, int D, int n,
-                                const int* col_ptr, const int* csc_row, const float* csc_val,
-                                const void* dZ, bool dz_bf16, int lddz, const float* st, float lr,
-                                float beta1, float beta2, float eps, float grad_scale,
-                                uint16_t* shadow, int ldsh, hipStream_t s);
+// One optimizer step over the arena (adam.hip).  st: device {beta1_power, beta2_power} of this
+// step, advanced by the kernel; ticket: kAdamTicketUints zero-initialised counters, re-armed by
+// the kernel.
+constexpr int kAdamW1Blocks = 2048;
+constexpr int kAdamDenseBlocks = 2048;
+constexpr int kAdamSubTickets = 64;
+// ticket area: top counter + kAdamSubTickets counters, each on its own 256-B line
+constexpr int kAdamTicketUints = 64 * (kAdamSubTickets + 1);
+// A gradient block left as split-K partial slabs [splits][count] (plan fused mode): the Adam step
+// sums them in fixed split order instead of a separate reduce launch.
+struct SlabSeg {
+  int64_t offset, count;
+  int splits;
+  const float* slab;
+};
+struct SlabList {
+  int count;
+  SlabSeg seg[8];
+};
+struct AdamStep {
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  // fused W1 rows (w1_blocks > 0): rows [0, D] of the [W1; b1] block at arena offset 0
+  int w1_blocks;
+  int D, n;
+  const int* col_ptr;
+  const int* csc_row;
+  const float* csc_val;
+  const void* dZ;
+  int lddz;
+  uint16_t* shadow;
+  int ldsh;
+  // dense float4 range [d4_begin, d4_end); gradients at element index >= clear_from are zeroed
+  int64_t d4_begin, d4_end, clear_from;
+  int dense_blocks;
+  float* st;
+  unsigned* ticket;
+  float lr, beta1, beta2, b1c, b2c, eps, gs;
+  ShadowList sh;
+  SlabList slabs;
+};
+hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 
 }  // namespace dssm

@@ -48,7 +48,7 @@ struct Layout {
   size_t tickets[DSSM_MAX_LAYERS][2];
   size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
-  size_t dw_slab, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
+  size_t dw_slab[DSSM_MAX_LAYERS] = {}, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
   size_t ws = 0;
   int max_nnz = 0;
@@ -132,10 +132,10 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
   Lt.partial = take(max_part * 4);
-  size_t slab = 0;
+  // split-K slabs of dW_l (l >= 2), one per layer: in fused mode the Adam step sums them
   for (int l = 1; l < Lt.L; ++l)
-    slab = std::max(slab, dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16));
-  Lt.dw_slab = take(std::max<size_t>(slab, 1) * 4);
+    Lt.dw_slab[l] = take(
+        std::max<size_t>(dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16), 1) * 4);
   const size_t K = Lt.NEG + 1;
   Lt.cos_raw = take(K * Lt.BS * 4);
   Lt.cos_sim = take(K * Lt.BS * 4);
@@ -149,7 +149,8 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.csc_row = take(ent * 4);
   Lt.csc_val = take(ent * 4);
   Lt.csc_col = take(ent * 4);
-  Lt.adam_state = take(4 * 4);  // {beta1_power, beta2_power} (device-side Adam step state)
+  // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
+  Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
   Lt.ws = w;
 }
 
@@ -167,6 +168,7 @@ struct dssm_plan {
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
+  int dw_deferred[DSSM_MAX_LAYERS] = {};  // split count of dW_l left in its slab (fused mode)
   // CSC build on the launch stream (default: measured faster than overlapping it on the side
   // stream, whose join costs a cross-queue wait and whose kernels contend with the forward's);
   // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
@@ -545,7 +547,9 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
       float* gw = P->g + Lt.fc_off[l];
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_DW, Lt.bf16, kin + 1, n, Lt.R, P->ws + Lt.A[l - 1],
                                 Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true,
-                                P->at<float>(Lt.dw_slab), s));
+                                P->at<float>(Lt.dw_slab[l]), s,
+                                P->fused_w1_adam ? &P->dw_deferred[l] : nullptr));
+      if (!P->fused_w1_adam) P->dw_deferred[l] = 0;
       if (P->wholek(l))  // dA = dZ . W^T: the weight shadow rows are already k-contiguous
         HIP_TRY(dssm::launch_gemm_nt(Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l], false, nullptr,
                                      Lt.BS, P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l],
@@ -579,27 +583,50 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int64_t rest = Lt.L > 1 ? Lt.fc_off[1] : Lt.bn_off[0][0];
   dssm::ShadowList sh = P->shadows();
-  P->probe_begin(DSSM_PROBE_ADAM, s);
+  dssm::AdamStep a{};
+  a.p = P->p;
+  a.g = P->g;
+  a.m = P->m;
+  a.v = P->v;
+  a.st = st;
+  a.ticket = reinterpret_cast<unsigned*>(st + 64);
+  a.lr = c.lr;
+  a.beta1 = c.beta1;
+  a.beta2 = c.beta2;
+  a.eps = c.adam_eps;
+  a.gs = grad_scale;
+  a.clear_from = Lt.total;
+  a.d4_end = Lt.total / 4;
   if (P->fused_w1_adam) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
-    const int64_t o = Lt.fc_off[0];
-    HIP_TRY(dssm::launch_adam_w1_fused(
-        P->p + o, P->g + o, P->m + o, P->v + o, Lt.D, Lt.n[0], P->at<int>(Lt.col_ptr),
-        P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val), P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0],
-        st, c.lr, c.beta1, c.beta2, c.adam_eps, grad_scale,
-        Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr, Lt.ldp[0], s));
-    if (sh.count) {  // W1's shadow is written by the fused kernel
+    a.w1_blocks = 1;  // sized by the launcher
+    a.D = Lt.D;
+    a.n = Lt.n[0];
+    a.col_ptr = P->at<int>(Lt.col_ptr);
+    a.csc_row = P->at<int>(Lt.csc_row);
+    a.csc_val = P->at<float>(Lt.csc_val);
+    a.dZ = P->ws + Lt.dZ[0];
+    a.lddz = Lt.ldp[0];
+    a.shadow = Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr;
+    a.ldsh = Lt.ldp[0];
+    a.d4_begin = rest / 4;
+    if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
     }
-    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, rest, Lt.total, Lt.total, st, c.lr,
-                              c.beta1, c.beta2, c.adam_eps, grad_scale, sh, s));
-  } else {
-    HIP_TRY(dssm::launch_adam(P->p, P->g, P->m, P->v, 0, Lt.total, Lt.total, st, c.lr, c.beta1,
-                              c.beta2, c.adam_eps, grad_scale, sh, s));
   }
+  for (int l = 1; l < Lt.L; ++l)
+    if (P->dw_deferred[l] > 0) {  // dW_l still in its split-K slab: summed inside the step
+      dssm::SlabSeg& sg = a.slabs.seg[a.slabs.count++];
+      sg.offset = Lt.fc_off[l];
+      sg.count = (int64_t)(Lt.in_dim[l] + 1) * Lt.n[l];
+      sg.splits = P->dw_deferred[l];
+      sg.slab = P->at<float>(Lt.dw_slab[l]);
+    }
+  a.sh = sh;
+  P->probe_begin(DSSM_PROBE_ADAM, s);
+  HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
   P->probe_end(DSSM_PROBE_ADAM, s);
-  HIP_TRY(dssm::launch_adam_advance(st, c.beta1, c.beta2, s));
   P->grads_clean = true;
   return DSSM_OK;
 }

@@ -202,8 +202,9 @@ class DSSM:
               "set_batch")
 
     def set_fused_w1_adam(self, on: bool):
-        """Single-GPU fast path (default): dW1's light rows are computed inside Adam and never
-        materialized.  Must be off for the data-parallel all-reduce or to read dW1."""
+        """Single-GPU fast path (default): dW1's light rows are computed inside Adam and the
+        split-K slabs of dW_l (l >= 2) are summed there, so neither is materialized in the gradient
+        arena.  Must be off for the data-parallel all-reduce or to read the gradients."""
         check(self.lib.dssm_plan_set_fused_w1_adam(self._plan, 1 if on else 0), "set_fused")
         self.fused_w1_adam = bool(on)
 

@@ -116,8 +116,9 @@ int dssm_plan_set_adam_state(dssm_plan* plan, float beta1_power, float beta2_pow
 int dssm_plan_get_adam_state(dssm_plan* plan, float* beta1_power, float* beta2_power, void* stream);
 /* Single-GPU fast path (default on): backward leaves the light rows of dW1 un-materialized and
  * dssm_plan_adam computes them inline from the CSC transpose while updating W1, so a dense dW1 is
- * never written or re-read.  Turn it off when the gradient arena must hold the full gradient
- * (data-parallel all-reduce, or inspecting dW1). */
+ * never written or re-read; the split-K partial slabs of dW_l (l >= 2) are likewise summed inside
+ * the Adam step instead of by a reduce launch.  Turn it off when the gradient arena must hold
+ * the full gradient (data-parallel all-reduce, or inspecting the gradients). */
 int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, void* stream);

@@ -1,14 +1,15 @@
 """hipGraph replay of the training step (what bench.py times) against eager launches.
 
 The captured graph holds the same kernels with the same arguments as the eager step, and the
-Adam beta powers live on the device, so replaying a graph must reproduce the eager step.  The
-only run-to-run nondeterminism in the step is the order of dW1's heavy-row float atomics, which
-free-running Adam amplifies (bias gradients are pure rounding noise, see test_gpu_parity; bf16
-shadows flip roundings).  So the bar is relative to the step's own noise floor: the first step's
-loss is bit-identical, the second (one Adam step in) within 1e-5 relative, and afterwards the
-graph-vs-eager divergence (loss per step, parameters, EMA) stays within 20x the divergence of
-two eager runs of the same steps (+1e-3 relative on the loss), inside the 3 lr free-running
-envelope; beta powers and step counts are identical.
+Adam beta powers live on the device, so a replay must compute what the eager step computes.
+The step has one source of run-to-run nondeterminism (the order of float atomics: dW1's heavy
+rows and the CSC fill's per-column entry order), which free-running Adam amplifies chaotically,
+so the replay is checked teacher-forced: before every step the graph model is given the eager
+model's full state (parameters, Adam slots, EMA, beta powers), then both run step i on batch i.
+Bar per step: bit-identical loss (the forward is deterministic), parameters <= 2 lr everywhere
+and within 1e-5 on >= 99.9% of elements, EMA within 1e-5 (1e-3 relative), identical beta
+powers after the step; after all steps, identical step counts.  Then a free-running stretch of
+graph replays must keep training (loss finite and falling).
 """
 import numpy as np
 import pytest
@@ -32,16 +33,21 @@ def _batches(D, BS, NEG, k):
     return [synth_batch(D, BS, NEG, seed=2000 + i, mean_nnz=32) for i in range(k)]
 
 
+def _copy_state(dst, src):
+    for name in ("params", "grads", "adam_m", "adam_v", "ema"):
+        getattr(dst, name).copy_(getattr(src, name))
+    dst.set_beta_powers(*src.beta_powers())
+    _lib.check(dst.lib.dssm_plan_sync_shadows(dst._plan, _lib.stream_ptr()), "sync_shadows")
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_graph_replay_matches_eager(case):
     D, widths, BS, NEG, dtype, fused = case
     lr, steps = 0.01, 6
     _, _, ea = make(D, widths, BS, NEG, dtype, fused=fused)
-    _, _, eb = make(D, widths, BS, NEG, dtype, fused=fused)
     _, _, gr = make(D, widths, BS, NEG, dtype, fused=fused)
     batches = _batches(D, BS, NEG, 3)
     s = torch.cuda.Stream()
-    la, lb, lg = [], [], []
     with torch.cuda.stream(s):
         staged = []
         for hb in batches:
@@ -49,39 +55,37 @@ def test_graph_replay_matches_eager(case):
         gids = []
         for ip, ix, vv in staged:
             gr.set_batch(indptr=ip, indices=ix, values=vv)
-            if fused:
-                gids.append(gr.graph_build())
-            else:
-                gids.append(gr.graph_build(_lib.GRAPH_FWD_BWD))
+            gids.append(gr.graph_build() if fused else gr.graph_build(_lib.GRAPH_FWD_BWD))
         adam = None if fused else gr.graph_build(_lib.GRAPH_ADAM)
         # capture must not have run anything or advanced the step state
         assert gr.global_step == 0
         assert gr.beta_powers() == (np.float32(0.9), np.float32(0.999))
         for i in range(steps):
+            _copy_state(gr, ea)
             ip, ix, vv = staged[i % 3]
-            for m in (ea, eb):
-                m.set_batch(indptr=ip, indices=ix, values=vv)
-                m.train_step()
+            ea.set_batch(indptr=ip, indices=ix, values=vv)
+            ea.train_step()
             gr.graph_launch(gids[i % 3])
             if adam is not None:
                 gr.graph_launch(adam)
             torch.cuda.synchronize()
-            la.append(ea.loss_accuracy()[0])
-            lb.append(eb.loss_accuracy()[0])
-            lg.append(gr.loss_accuracy()[0])
-    la, lb, lg = map(np.array, (la, lb, lg))
-    assert lg[0] == la[0]  # identical parameters and batch: the forward is deterministic
-    # one Adam step in: a wrong beta power / batch / missed update shows here at >= 1e-3
-    assert abs(lg[1] - la[1]) <= 1e-5 * abs(la[1]), (la, lg)
-    noise = np.abs(la - lb).max()
-    assert np.all(np.abs(lg - la) <= 20 * noise + 1e-3 * np.abs(la)), (la, lb, lg)
-    for name in ("params", "ema"):
-        a, b, g = (getattr(m, name).cpu().numpy() for m in (ea, eb, gr))
-        d_ref, d_g = np.abs(a - b), np.abs(a - g)
-        assert d_g.max() <= 3 * lr * steps, (name, d_g.max())
-        assert d_g.mean() <= 20 * d_ref.mean() + 1e-6, (name, d_g.mean(), d_ref.mean())
-    assert ea.beta_powers() == gr.beta_powers()
-    assert ea.global_step == gr.global_step == steps
+            la, lg = ea.loss_accuracy()[0], gr.loss_accuracy()[0]
+            assert la == lg, (i, la, lg)
+            d = (ea.params - gr.params).abs()
+            assert float(d.max()) <= 2 * lr, (i, float(d.max()))
+            assert float((d <= 1e-5).float().mean()) >= 0.999, (i, float((d <= 1e-5).float().mean()))
+            torch.testing.assert_close(gr.ema, ea.ema, rtol=1e-3, atol=1e-5)
+            assert ea.beta_powers() == gr.beta_powers()
+        assert ea.global_step == gr.global_step == steps
+        # free-running replays keep training
+        losses = []
+        for i in range(9):
+            gr.graph_launch(gids[i % 3])
+            if adam is not None:
+                gr.graph_launch(adam)
+            torch.cuda.synchronize()
+            losses.append(gr.loss_accuracy()[0])
+        assert np.all(np.isfinite(losses)) and losses[-1] < losses[0], losses
 
 
 def test_graph_probes_and_eager_interleave():
