@@ -17,7 +17,7 @@ DSSM_ABI_VERSION = 1
 DSSM_MAX_LAYERS = 8
 DSSM_F32, DSSM_BF16 = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
- BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
+ BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING) = range(11)
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
 GRAPH_FWD_BWD, GRAPH_ADAM = 1, 2
 
@@ -64,6 +64,8 @@ _SIGS = {
     "dssm_plan_train_step": (C.c_int, [_P, _P]),
     "dssm_plan_graph_build": (C.c_int, [_P, C.c_int, C.c_float, C.c_int, _P, C.POINTER(C.c_int)]),
     "dssm_plan_graph_launch": (C.c_int, [_P, C.c_int, _P]),
+    "dssm_plan_check": (C.c_int, [_P, _P]),
+    "dssm_plan_dense_enabled": (C.c_int, [_P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),

@@ -12,6 +12,7 @@
 
 #include "../../include/dssm.h"
 #include "common.h"
+#include "dense.h"
 #include "launch.h"
 
 namespace {
@@ -31,6 +32,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+constexpr int kDenseMaxGrid = 1024;  // workgroups of the persistent dense kernels (one per CU)
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Layout {
@@ -50,6 +52,12 @@ struct Layout {
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
   size_t dw_slab[DSSM_MAX_LAYERS] = {}, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
+  // persistent dense-stack path (dense.hip), bf16 only
+  bool dense_ok = false;
+  int dense_kmax = 0, dense_splits = 0;
+  size_t dense_sums = 0, dense_sums_bytes = 0, dense_args = 0, dense_bar = 0, loss_part = 0,
+         dense_tickets = 0, dense_timing = 0;
+  size_t fsum[DSSM_MAX_LAYERS] = {}, bsum[DSSM_MAX_LAYERS] = {};
   size_t ws = 0;
   int max_nnz = 0;
 };
@@ -131,11 +139,24 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     Lt.shadowT[l] = (Lt.bf16 && l > 0) ? take((size_t)Lt.n[l] * Lt.ldp[l - 1] * 2) : 0;
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
+  {
+    int ld[DSSM_MAX_LAYERS], n[DSSM_MAX_LAYERS];
+    for (int l = 0; l < Lt.L; ++l) ld[l] = Lt.ldp[l], n[l] = Lt.n[l];
+    Lt.dense_ok = Lt.bf16 && dssm::dense_supported(Lt.L, n, ld, Lt.BS, Lt.NEG);
+    if (Lt.dense_ok) {
+      for (int l = 0; l < Lt.L; ++l) {
+        Lt.dense_kmax = std::max(Lt.dense_kmax, Lt.ldp[l]);
+        max_part = std::max(max_part, (size_t)(Lt.R / 64) * 2 * Lt.ldp[l]);
+      }
+      Lt.dense_splits = dssm::dense_dw_splits(Lt.R);
+    }
+  }
   Lt.partial = take(max_part * 4);
   // split-K slabs of dW_l (l >= 2), one per layer: in fused mode the Adam step sums them
   for (int l = 1; l < Lt.L; ++l)
     Lt.dw_slab[l] = take(
-        std::max<size_t>(dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16), 1) * 4);
+        std::max<size_t>({dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16),
+                          (size_t)Lt.dense_splits * (Lt.in_dim[l] + 1) * Lt.n[l], (size_t)1}) * 4);
   const size_t K = Lt.NEG + 1;
   Lt.cos_raw = take(K * Lt.BS * 4);
   Lt.cos_sim = take(K * Lt.BS * 4);
@@ -151,6 +172,25 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.csc_col = take(ent * 4);
   // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
   Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
+  if (Lt.dense_ok) {
+    // fp64 statistics accumulators (one contiguous region: re-zeroed after a failed launch)
+    size_t sums = 0;
+    for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
+    Lt.dense_sums = take(sums);
+    Lt.dense_sums_bytes = sums;
+    size_t o = Lt.dense_sums;
+    for (int l = 0; l < Lt.L; ++l) {
+      Lt.fsum[l] = o;
+      o += (size_t)4 * Lt.ldp[l] * 8;
+      Lt.bsum[l] = o;
+      o += (size_t)4 * Lt.ldp[l] * 8;
+    }
+    Lt.dense_args = take(sizeof(dssm::DenseArgs));
+    Lt.dense_bar = take(3 * 256);
+    Lt.loss_part = take((size_t)kDenseMaxGrid * 2 * 4);
+    Lt.dense_tickets = take(2 * 256);
+    Lt.dense_timing = take(4 * 64 * 8);
+  }
   Lt.ws = w;
 }
 
@@ -169,6 +209,10 @@ struct dssm_plan {
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
   int dw_deferred[DSSM_MAX_LAYERS] = {};  // split count of dW_l left in its slab (fused mode)
+  // persistent dense-stack kernels (bf16; DSSM_DENSE=0 selects the per-op launches)
+  bool dense_on = false;
+  int dense_grid = 0;
+  size_t dense_smem = 0;
   // CSC build on the launch stream (default: measured faster than overlapping it on the side
   // stream, whose join costs a cross-queue wait and whose kernels contend with the forward's);
   // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
@@ -227,6 +271,59 @@ struct dssm_plan {
   }
 
   template <typename T> T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+  dssm::DenseArgs dense_args() const {
+    dssm::DenseArgs a{};
+    a.L = Lt.L;
+    a.R = Lt.R;
+    a.BS = Lt.BS;
+    a.NEG = Lt.NEG;
+    a.gamma_cos = cfg.gamma;
+    a.eps = cfg.bn_eps;
+    a.decay = cfg.ema_decay;
+    for (int l = 0; l < Lt.L; ++l) {
+      dssm::DenseLayer& d = a.ly[l];
+      const int n = Lt.n[l];
+      d.n = n;
+      d.ld = Lt.ldp[l];
+      d.Z = at<float>(Lt.Z[l]);
+      d.A = l < Lt.L - 1 ? at<uint16_t>(Lt.A[l]) : nullptr;
+      d.Y = l == Lt.L - 1 ? at<float>(Lt.A[l]) : nullptr;
+      d.dy = at<float>(Lt.dA[l]);
+      d.dZ = at<uint16_t>(Lt.dZ[l]);
+      d.W = at<uint16_t>(Lt.shadow[l]);
+      d.WT = l > 0 ? at<uint16_t>(Lt.shadowT[l]) : nullptr;
+      d.bias = bias(l);
+      for (int t = 0; t < 2; ++t) {
+        d.gamma[t] = p + Lt.bn_off[l][2 * t];
+        d.beta[t] = p + Lt.bn_off[l][2 * t + 1];
+        d.dgamma[t] = g + Lt.bn_off[l][2 * t];
+        d.dbeta[t] = g + Lt.bn_off[l][2 * t + 1];
+        d.ema_mean[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t) * n;
+        d.ema_var[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t + 1) * n;
+      }
+      d.coef = at<float>(Lt.coef[l]);
+      d.fsum = at<double>(Lt.fsum[l]);
+      d.bsum = at<double>(Lt.bsum[l]);
+      d.bmean = at<float>(Lt.bmean[l]);
+      d.bvar = at<float>(Lt.bvar[l]);
+      d.gW = g + Lt.fc_off[l];
+      d.slab = l > 0 ? at<float>(Lt.dw_slab[l]) : nullptr;
+      d.splits = Lt.dense_splits;
+    }
+    a.cos_raw = at<float>(Lt.cos_raw);
+    a.cos_sim = at<float>(Lt.cos_sim);
+    a.prob = at<float>(Lt.prob);
+    a.qnorm = at<float>(Lt.qnorm);
+    a.loss = at<float>(Lt.loss);
+    a.loss_part = at<float>(Lt.loss_part);
+    a.tickets = at<unsigned>(Lt.dense_tickets);
+    a.bar = at<unsigned>(Lt.dense_bar);
+    const char* tv = std::getenv("DSSM_DENSE_TIMING");
+    a.timing = (tv && tv[0] == '1') ? at<unsigned long long>(Lt.dense_timing) : nullptr;
+    const char* ex = std::getenv("DSSM_DENSE_EXP");
+    a.exp = ex ? std::atoi(ex) : 0;
+    return a;
+  }
   const void* weight(int l) const {  // what the kernels read for W_l
     return Lt.bf16 ? (const void*)at<u16>(Lt.shadow[l]) : (const void*)(p + Lt.fc_off[l]);
   }
@@ -339,6 +436,25 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
       return fail(DSSM_E_HIP, "failed to initialise the device Adam state");
     }
   }
+  if (P->Lt.dense_ok) {
+    // opt-in until it outruns the per-op launches (DSSM_DENSE=1)
+    const char* e = std::getenv("DSSM_DENSE");
+    if (e && e[0] == '1') {
+      const Layout& Lt = P->Lt;
+      int ld[DSSM_MAX_LAYERS];
+      for (int l = 0; l < Lt.L; ++l) ld[l] = Lt.ldp[l];
+      P->dense_smem = dssm::dense_smem_bytes(ld, Lt.L);
+      P->dense_grid = std::min(dssm::dense_max_grid(P->dense_smem), kDenseMaxGrid);
+      if (P->dense_grid > 0) {
+        const dssm::DenseArgs a = P->dense_args();
+        if (hipMemcpy(P->ws + Lt.dense_args, &a, sizeof a, hipMemcpyHostToDevice) != hipSuccess) {
+          delete P;
+          return fail(DSSM_E_HIP, "failed to write the dense-kernel arguments");
+        }
+        P->dense_on = true;
+      }
+    }
+  }
   if (hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&P->ev_batch, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&P->ev_csc, hipEventDisableTiming) != hipSuccess) {
@@ -422,6 +538,9 @@ int dssm_plan_buffer(const dssm_plan* P, int id, int layer, void** ptr, size_t* 
     case DSSM_BUF_BATCH_MEAN: off = Lt.bmean[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
     case DSSM_BUF_BATCH_VAR: off = Lt.bvar[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
     case DSSM_BUF_DZ: off = Lt.dZ[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * (Lt.bf16 ? 2 : 4); break;
+    case DSSM_BUF_DENSE_TIMING:
+      if (!Lt.dense_ok) return fail(DSSM_E_UNSUPPORTED, "no dense-kernel workspace in this plan");
+      off = Lt.dense_timing; n = 4 * 64 * 8; break;
     default: return fail(DSSM_E_INVALID, "unknown buffer id");
   }
   *ptr = P->ws + off;
@@ -478,6 +597,13 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                 P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
                                 Lt.ldp[0], s));
   P->probe_end(DSSM_PROBE_SPMM_FWD, s);
+  if (P->dense_on) {  // BN1 .. cosine + loss (+ dy_L and its BN partials) in one launch
+    HIP_TRY(dssm::launch_dense_fwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.ldp[Lt.L - 1],
+                                   Lt.dense_kmax, Lt.NEG, train != 0, P->dense_grid,
+                                   P->dense_smem, s));
+    P->fwd_train_done = train != 0;
+    return DSSM_OK;
+  }
   for (int l = 0; l < Lt.L; ++l) {
     float* ema = P->ema + Lt.ema_off[l];
     const int n = Lt.n[l];
@@ -521,6 +647,22 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   return DSSM_OK;
 }
 
+// dW1 = X^T dZ1 from the batch's CSC transpose: heavy columns here, light columns either here
+// (unfused) or inside the Adam step (fused).
+static int dw1_backward(dssm_plan* P, hipStream_t s) {
+  const Layout& Lt = P->Lt;
+  if (P->csc_pending) {
+    HIP_TRY(hipStreamWaitEvent(s, P->ev_csc, 0));
+    P->csc_pending = false;
+  }
+  P->probe_begin(DSSM_PROBE_DW1, s);
+  HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
+                           P->at<int>(Lt.csc_col), Lt.D, Lt.R, Lt.max_nnz, P->ws + Lt.dZ[0],
+                           Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam, s));
+  P->probe_end(DSSM_PROBE_DW1, s);
+  return DSSM_OK;
+}
+
 int dssm_plan_backward(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (!P->fwd_train_done) return fail(DSSM_E_INVALID, "backward needs a train-mode forward first");
@@ -534,6 +676,14 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
     HIP_TRY(hipMemsetAsync(P->g, 0, sizeof(float) * (size_t)Lt.total, s));
   }
   P->grads_clean = false;
+  if (P->dense_on) {
+    // BN_L .. BN1 backward, dA GEMMs, dW_l (l >= 2) split-K, dZ1 in one launch; then dW1
+    const bool defer = P->fused_w1_adam;
+    HIP_TRY(dssm::launch_dense_bwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.dense_kmax,
+                                   defer ? 1 : 0, P->dense_grid, P->dense_smem, s));
+    for (int l = 1; l < Lt.L; ++l) P->dw_deferred[l] = defer ? Lt.dense_splits : 0;
+    return dw1_backward(P, s);
+  }
   for (int l = Lt.L - 1; l >= 0; --l) {
     const int n = Lt.n[l];
     HIP_TRY(dssm::launch_bn_bwd(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), Lt.ldp[l], n, tw,
@@ -560,16 +710,7 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
                                   P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], nullptr, false,
                                   nullptr, s));
     } else {
-      if (P->csc_pending) {
-        HIP_TRY(hipStreamWaitEvent(s, P->ev_csc, 0));
-        P->csc_pending = false;
-      }
-      P->probe_begin(DSSM_PROBE_DW1, s);
-      HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
-                               P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), Lt.D, Lt.R,
-                               Lt.max_nnz, P->ws + Lt.dZ[0], Lt.bf16, Lt.ldp[0], n,
-                               P->g + Lt.fc_off[0], !P->fused_w1_adam, s));
-      P->probe_end(DSSM_PROBE_DW1, s);
+      return dw1_backward(P, s);
     }
   }
   return DSSM_OK;
@@ -642,6 +783,24 @@ int dssm_plan_train_step(dssm_plan* P, void* stream) {
   if (int rc = dssm_plan_backward(P, stream)) return rc;
   return dssm_plan_adam(P, 1.0f, stream);
 }
+
+int dssm_plan_check(dssm_plan* P, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (!P->dense_on) return DSSM_OK;
+  unsigned err = 0;
+  HIP_TRY(hipMemcpy(&err, P->ws + P->Lt.dense_bar + 128 * 4, 4, hipMemcpyDeviceToHost));
+  if (err) {
+    // re-arm the barrier and tickets, clear the statistics accumulators
+    HIP_TRY(hipMemset(P->ws + P->Lt.dense_bar, 0, 3 * 256));
+    HIP_TRY(hipMemset(P->ws + P->Lt.dense_tickets, 0, 2 * 256));
+    HIP_TRY(hipMemset(P->ws + P->Lt.dense_sums, 0, P->Lt.dense_sums_bytes));
+    return fail(DSSM_E_HIP, "dense kernel grid barrier timed out (results of that step are invalid)");
+  }
+  return DSSM_OK;
+}
+
+int dssm_plan_dense_enabled(dssm_plan* P) { return P && P->dense_on ? P->dense_grid : 0; }
 
 int dssm_plan_set_adam_state(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");

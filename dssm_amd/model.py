@@ -249,6 +249,14 @@ class DSSM:
               "graph_probe_read")
         return float(ms.value)
 
+    def check(self, stream=None):
+        """Synchronize and raise if a persistent dense kernel reported a device-side failure."""
+        check(self.lib.dssm_plan_check(self._plan, stream_ptr(stream)), "plan_check")
+
+    @property
+    def dense_persistent(self) -> bool:
+        return bool(self.lib.dssm_plan_dense_enabled(self._plan))
+
     # ---- kernel timing probes (HIP events on the launch stream) -------------------------------
     def probe_enable(self, probe_id: int, max_samples: int):
         check(self.lib.dssm_plan_probe_enable(self._plan, probe_id, max_samples), "probe_enable")

@@ -72,6 +72,8 @@ enum {
   DSSM_BUF_BATCH_MEAN,      /* float[2*n_l]: batch mean, tower q then d (new_dssm.py:77) */
   DSSM_BUF_BATCH_VAR,       /* float[2*n_l] */
   DSSM_BUF_DZ,              /* dZ of layer `layer` (compute dtype, R*ldp) */
+  DSSM_BUF_DENSE_TIMING,    /* uint64[2][64] phase stamps of the persistent dense kernels
+                               (100 MHz clock; written only when DSSM_DENSE_TIMING=1) */
   DSSM_BUF_COUNT
 };
 
@@ -138,6 +140,13 @@ int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);
 enum { DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC, DSSM_PROBE_COUNT };
 int dssm_plan_probe_enable(dssm_plan* plan, int probe_id, int max_samples);
 int dssm_plan_probe_read(dssm_plan* plan, int probe_id, float* total_ms, int* count);
+/* Synchronize the stream and report a device-side failure of the persistent dense kernels
+ * (a grid barrier that timed out: the step's results are invalid; the barrier is re-armed). */
+int dssm_plan_check(dssm_plan* plan, void* stream);
+/* The persistent kernels' grid size (> 0) when the bf16 plan runs the dense stack as the two
+ * persistent kernels (dense.hip), 0 when
+ * it uses per-op launches (fp32 mode, unsupported shapes, or DSSM_DENSE=0). */
+int dssm_plan_dense_enabled(dssm_plan* plan);
 int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, float* ms);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
