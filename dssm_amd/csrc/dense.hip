@@ -263,253 +263,299 @@ __device__ __forceinline__ void tile_colsum_add(double s, double q, int wm, int 
   }
 }
 
-// XCD-aware item decode: id -> (row tile, column tile) such that every column tile of a row
-// tile goes to blocks with the same blockIdx % 8 — the same XCD under the round-robin dispatch
-// — so the A rows (re-read by each column tile) are L2 hits after the first read.  Placement
-// is a speed hint only; any mapping is correct.  Needs nrt % 8 == 0 and a grid that is a
-// multiple of 8 (else the plain row-major decode).
-__device__ __forceinline__ void item_rc(int id, int nrt, int ncol, int& rt, int& ct) {
-  if ((nrt & 7) == 0 && (gridDim.x & 7) == 0) {
-    const int x = id & 7, j = id >> 3;
-    rt = x + 8 * (j / ncol);
-    ct = j - (j / ncol) * ncol;
-  } else {
-    rt = id / ncol;
-    ct = id - rt * ncol;
-  }
-}
+// ---- weight-stationary GEMM phases -----------------------------------------------------------
+// A block owns a column part of the layer's weights (<= ~105 KB bf16, whole K) in LDS for the
+// whole phase and streams 32-row A panels through it: every weight byte is read once per block,
+// every A row once per part, and a row tile's whole part is one MFMA pass (no per-column-tile
+// round trips).  Parts: nparts = ceil(ld_out / pc_max), pc = columns per part (multiple of 16);
+// blocks b = part (mod nparts) share a part and split the row tiles.
+constexpr int kDenseSmem = 144 * 1024;  // dynamic LDS per workgroup
 
-// ---- forward GEMM phase: Z_l = relu(bn_{l-1}(Z_{l-1})) . W_l + b_l (+ BN_l sums) ------------
-// Item = 32 batch rows x 64 output columns with the whole K panel; a block walks its items with
-// the next item's panels loaded into registers while the current one computes.
-struct FwdRegs {
-  float4 z[MAXG_A][2];
-  BRegs b;
-  float bias;
+struct WsGeom {
+  int K, Kp, ldk, nparts, pc, part, c0, cols, nsub, bi, nb;
 };
 
-__device__ __forceinline__ void fwd_load(const DenseArgs& a, const DenseLayer& P, const DenseLayer& C,
-                                         int item, int ncol, int K, int Kp, FwdRegs& r) {
-  const int t = threadIdx.x, lane = t & 63, wn = (t >> 6) & 3;
-  int rt, ct;
-  item_rc(item, a.R / RT, ncol, rt, ct);
-  const int bm = rt * RT;
-  const int gpr = Kp >> 3, totA = RT * gpr;
-#pragma unroll
-  for (int g = 0; g < MAXG_A; ++g) {
-    const int e = t + NTH * g;
-    const int ee = e < totA ? e : 0;
-    const int row = ee / gpr, kg = (ee - row * gpr) * 8;
-    const bool ok = e < totA && kg < K;  // zeroed when staged (kg >= K)
-    const float DSSM_GAS* z = P.Z + (size_t)(bm + row) * K + kg;
-    r.z[g][0] = gload_f4(ok ? z : P.Z);
-    r.z[g][1] = gload_f4(ok ? z + 4 : P.Z);
-  }
-  load_b(r.b, C.WT, K, C.n, K, ct * TM, Kp);
-  const int n = ct * TM + wn * 16 + (lane & 15);
-  r.bias = *(n < C.n ? C.bias + n : C.bias);
+__device__ __forceinline__ WsGeom ws_geom(int K, int ld_out, int coef_floats) {
+  WsGeom g;
+  g.K = K;
+  g.Kp = round32(K);
+  g.ldk = g.Kp + 8;
+  const int fixed = RT * g.ldk * 2 + coef_floats * g.Kp * 4 + 1024;
+  const int percol = g.ldk * 2 + 8 * 4 + 4 * 8 + 4;  // W row, coefficients, fp64 sums, bias
+  int pcmax = ((kDenseSmem - fixed) / percol) & ~15;
+  if (pcmax < 16) pcmax = 16;
+  g.nparts = cdiv(ld_out, pcmax);
+  g.pc = (cdiv(cdiv(ld_out, g.nparts), 16)) * 16;
+  g.part = blockIdx.x % g.nparts;
+  g.c0 = g.part * g.pc;
+  g.cols = min(g.pc, ld_out - g.c0);
+  g.nsub = cdiv(g.cols, 16);
+  g.bi = blockIdx.x / g.nparts;
+  g.nb = ((int)gridDim.x - g.part + g.nparts - 1) / g.nparts;
+  return g;
 }
 
-__device__ __forceinline__ void fwd_phase(const DenseArgs& a, int l, int train, u16* smem, double* dred) {
+// stage rows [c0, c0 + pc) x K of a k-contiguous bf16 matrix [nrows x ldb] into sW [pc][ldk]
+__device__ __forceinline__ void ws_load_w(u16* sW, const WsGeom& g, const u16 DSSM_GAS* Bm, int ldb,
+                                          int nrows) {
+  const int gpr = g.Kp >> 3, tot = g.pc * gpr;
+  for (int base = 0; base < tot; base += NTH * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = base + threadIdx.x + NTH * i;
+      const int ee = e < tot ? e : 0;
+      const int row = ee / gpr, kg = (ee - row * gpr) * 8;
+      const int gr = g.c0 + row;
+      const bool ok = e < tot && gr < nrows && kg < g.K;
+      v[i] = gload_u4(ok ? (const void DSSM_GAS*)(Bm + (size_t)gr * ldb + kg) : (const void DSSM_GAS*)Bm);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // zero out-of-range groups only now (no select between loads)
+      const int e = base + threadIdx.x + NTH * i;
+      if (e < tot) {
+        const int row = e / gpr, kg = (e - row * gpr) * 8;
+        const bool ok = g.c0 + row < nrows && kg < g.K;
+        *reinterpret_cast<uint4*>(&sW[row * g.ldk + kg]) = ok ? v[i] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
+}
+
+// A-panel registers: 32 rows x Kp fp32 (x2 in the backward: Z and dy), 8-element groups
+struct APanel {
+  float4 z[MAXG_A][2], d[MAXG_A][2];
+};
+template <bool BWD>
+__device__ __forceinline__ void ws_load_a(APanel& r, const float DSSM_GAS* Z, const float DSSM_GAS* D,
+                                          int bm, const WsGeom& g) {
+  const int gpr = g.Kp >> 3, totA = RT * gpr;
+#pragma unroll
+  for (int i = 0; i < MAXG_A; ++i) {
+    const int e = threadIdx.x + NTH * i;
+    const int ee = e < totA ? e : 0;
+    const int row = ee / gpr, kg = (ee - row * gpr) * 8;
+    const bool ok = e < totA && kg < g.K;  // zeroed when staged
+    const size_t off = ok ? (size_t)(bm + row) * g.K + kg : 0;
+    r.z[i][0] = gload_f4(Z + off);
+    r.z[i][1] = gload_f4(Z + off + 4);
+    if (BWD) {
+      r.d[i][0] = gload_f4(D + off);
+      r.d[i][1] = gload_f4(D + off + 4);
+    }
+  }
+}
+
+// Column sums of the pass: every wave's 16-row partials (lanes 0..15 per 16-column subtile) go
+// to ps[wm][col] / pq[wm][col]; after a barrier the block adds the two halves to the fp64
+// accumulators (column c0 + c of tower `tower`).
+__device__ __forceinline__ void ws_sums_flush(double* ps, double* pq, const WsGeom& g, int ncols_valid,
+                                              double DSSM_GAS* dst, int ld, int tower) {
+  for (int c = threadIdx.x; c < g.cols; c += NTH) {
+    const int n = g.c0 + c;
+    if (n < ncols_valid) {
+      atomic_addd(dst + (size_t)(tower * 2) * ld + n, ps[c] + ps[g.pc + c]);
+      atomic_addd(dst + (size_t)(tower * 2 + 1) * ld + n, pq[c] + pq[g.pc + c]);
+    }
+  }
+}
+
+__device__ __forceinline__ void fwd_phase(const DenseArgs& a, int l, int train, u16* smem, double*) {
   const DenseLayer& P = a.ly[l - 1];
   const DenseLayer& C = a.ly[l];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
-  const int K = P.ld, Kp = round32(K), ldk = Kp + 8;
-  const int ncol = cdiv(C.ld, TM);
-  const int items = (a.R / RT) * ncol;
-  if ((int)blockIdx.x >= items) return;
-  u16* sA = smem;
-  u16* sB = sA + RT * ldk;
-  float* sc = reinterpret_cast<float*>(sB + TM * ldk);  // [tower][inv | shift][Kp]
-  for (int i = t; i < 2 * Kp; i += NTH) {
-    const int tw = i / Kp, k = i - tw * Kp;
-    float mu, var, rs, inv, sh;
-    bn_coef(a, P, tw, k, train, mu, var, rs, inv, sh);
-    sc[(tw * 2) * Kp + k] = inv;
-    sc[(tw * 2 + 1) * Kp + k] = sh;
-  }
-  const int gpr = Kp >> 3, totA = RT * gpr;
-  unsigned long long DSSM_GAS* ftm = (a.timing && l == 1) ? a.timing + 128 : nullptr;
+  const WsGeom g = ws_geom(P.ld, C.ld, 4);
+  const int nrt = a.R / RT;
+  if (g.bi >= nrt) return;
+  unsigned long long DSSM_GAS* ftm = (a.timing && l == 1 && blockIdx.x == 0) ? a.timing + 128 : nullptr;
   int fti = 0;
   stamp(ftm, fti);
-  FwdRegs r;
-  int it = blockIdx.x;
-  fwd_load(a, P, C, it, ncol, K, Kp, r);
-  lds_barrier();  // sc
+  u16* sW = smem;                                   // [pc][ldk]
+  u16* sA = sW + g.pc * g.ldk;                      // [RT][ldk]
+  float* sc = reinterpret_cast<float*>(sA + RT * g.ldk);  // [tower][inv | shift][Kp]
+  float* sb = sc + 4 * g.Kp;                        // [pc] bias
+  double* ps = reinterpret_cast<double*>(sb + g.pc + (g.pc & 1));  // [2][pc] sums, [2][pc] squares
+  double* pq = ps + 2 * g.pc;
+  for (int i = t; i < 2 * g.Kp; i += NTH) {
+    const int tw = i / g.Kp, k = i - tw * g.Kp;
+    float mu, var, rs, inv, sh;
+    bn_coef(a, P, tw, k, train, mu, var, rs, inv, sh);
+    sc[(tw * 2) * g.Kp + k] = inv;
+    sc[(tw * 2 + 1) * g.Kp + k] = sh;
+  }
+  for (int c = t; c < g.pc; c += NTH) sb[c] = *(g.c0 + c < C.n ? C.bias + g.c0 + c : C.bias) * (g.c0 + c < C.n ? 1.f : 0.f);
   stamp(ftm, fti);
-  for (; it < items; it += gridDim.x) {
-    int rt, ct;
-    item_rc(it, a.R / RT, ncol, rt, ct);
+  APanel r;
+  ws_load_a<false>(r, P.Z, nullptr, g.bi * RT, g);
+  stamp(ftm, fti);
+  ws_load_w(sW, g, C.WT, g.K, C.n);
+  stamp(ftm, fti);
+  const int gpr = g.Kp >> 3, totA = RT * gpr;
+  lds_barrier();  // sc, sb, sW
+  stamp(ftm, fti);
+  for (int rt = g.bi; rt < nrt; rt += g.nb) {
     const int bm = rt * RT;
     const int tower = tower_of(bm, a.BS);
-    const float* si = sc + (tower * 2) * Kp;
-    const float* ss = si + Kp;
-    // stage: A = relu(z*inv + shift) -> bf16 (the ct == 0 item also writes A_{l-1}); B as is
+    const float* si = sc + (tower * 2) * g.Kp;
+    const float* ss = si + g.Kp;
 #pragma unroll
-    for (int g = 0; g < MAXG_A; ++g) {
-      const int e = t + NTH * g;
+    for (int i = 0; i < MAXG_A; ++i) {
+      const int e = t + NTH * i;
       if (e < totA) {
         const int row = e / gpr, kg = (e - row * gpr) * 8;
-        const bool okk = kg < K;
-        const float zz[8] = {r.z[g][0].x, r.z[g][0].y, r.z[g][0].z, r.z[g][0].w,
-                             r.z[g][1].x, r.z[g][1].y, r.z[g][1].z, r.z[g][1].w};
+        const bool okk = kg < g.K;
+        const float zz[8] = {r.z[i][0].x, r.z[i][0].y, r.z[i][0].z, r.z[i][0].w,
+                             r.z[i][1].x, r.z[i][1].y, r.z[i][1].z, r.z[i][1].w};
         float y[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) y[i] = okk ? fmaxf(bn_affine(zz[i], si[kg + i], ss[kg + i]), 0.f) : 0.f;
+        for (int k = 0; k < 8; ++k) y[k] = okk ? fmaxf(bn_affine(zz[k], si[kg + k], ss[kg + k]), 0.f) : 0.f;
         uint4 v;
         v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
         v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
-        *reinterpret_cast<uint4*>(&sA[row * ldk + kg]) = v;
-        if (ct == 0 && P.A && okk) gstore_u4(P.A + (size_t)(bm + row) * K + kg, v);
+        *reinterpret_cast<uint4*>(&sA[row * g.ldk + kg]) = v;
+        if (g.part == 0 && P.A && okk) gstore_u4(P.A + (size_t)(bm + row) * g.K + kg, v);
       }
     }
-    store_b(r.b, sB, ldk, Kp);
-    const float b = r.bias;
     lds_barrier();
     stamp(ftm, fti);
-    const int nxt = it + gridDim.x;
-    if (nxt < items) fwd_load(a, P, C, nxt, ncol, K, Kp, r);  // in flight during this item
+    if (rt + g.nb < nrt) ws_load_a<false>(r, P.Z, nullptr, (rt + g.nb) * RT, g);  // next tile in flight
     stamp(ftm, fti);
-    const f32x4 acc = mfma16(sA, wm * 16, sB, wn * 16, ldk, Kp, lane);
-    stamp(ftm, fti);
-    const int n = ct * TM + wn * 16 + (lane & 15);
-    double s = 0.0, q = 0.0;
+    // MFMA: wave (wm, wn) -> rows wm*16, subtiles j = wn, wn + 4, wn + 8
+    const u16* pa = sA + (wm * 16 + (lane & 15)) * g.ldk + 8 * (lane >> 4);
+    for (int j = wn; j < g.nsub; j += 4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const u16* pb = sW + (j * 16 + (lane & 15)) * g.ldk + 8 * (lane >> 4);
+      for (int ks = 0; ks < g.Kp; ks += 32)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pa + ks),
+                                                      *reinterpret_cast<const bf16x8*>(pb + ks), acc, 0, 0, 0);
+      const int cl = j * 16 + (lane & 15), n = g.c0 + cl;
+      const float b = sb[cl];
+      double s = 0.0, q = 0.0;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = bm + wm * 16 + (lane >> 4) * 4 + rr;
-      const float x = n < C.n ? acc[rr] + b : 0.f;
-      if (n < C.ld) C.Z[(size_t)m * C.ld + n] = x;
-      s += x;
-      q += (double)x * x;
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = bm + wm * 16 + (lane >> 4) * 4 + rr;
+        const float x = n < C.n ? acc[rr] + b : 0.f;
+        if (cl < g.cols) C.Z[(size_t)m * C.ld + n] = x;
+        s += x;
+        q += (double)x * x;
+      }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lane < 16) {
+        ps[wm * g.pc + cl] = s;
+        pq[wm * g.pc + cl] = q;
+      }
     }
     stamp(ftm, fti);
-    if (train && !(a.exp & 1))
-      tile_colsum_add(s, q, wm, wn, lane, dred, C.fsum + (size_t)(tower * 2) * C.ld + n,
-                      C.fsum + (size_t)(tower * 2 + 1) * C.ld + n, n < C.n && !(a.exp & 2));
     lds_barrier();
+    stamp(ftm, fti);
+    if (train) ws_sums_flush(ps, pq, g, C.n, C.fsum, C.ld, tower);
     stamp(ftm, fti);
   }
 }
 
-// ---- backward GEMM phase: dA_{l-1} = dZ_l . W_l^T with dZ_l staged from (dy_l, Z_l); the
-//      epilogue masks with layer l-1, writes its dy and adds its BN backward sums -------------
-struct BwdRegs {
-  float4 z[MAXG_A][2], d[MAXG_A][2];
-  BRegs b;
-  float ez[4], emu, ers, einv, esh;  // epilogue operands of layer l-1
-};
-
-__device__ __forceinline__ void bwd_load(const DenseArgs& a, const DenseLayer& C, const DenseLayer& P,
-                                         int item, int ncol, int K, int Kp, BwdRegs& r) {
+__device__ __forceinline__ void bwd_phase(const DenseArgs& a, int l, u16* smem, double*) {
+  const DenseLayer& C = a.ly[l];      // dZ_l staged from (dy_l, Z_l)
+  const DenseLayer& P = a.ly[l - 1];  // produces dy_{l-1}
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
-  int rt, ct;
-  item_rc(item, a.R / RT, ncol, rt, ct);
-  const int bm = rt * RT;
-  const int tower = tower_of(bm, a.BS);
-  const int gpr = Kp >> 3, totA = RT * gpr;
-#pragma unroll
-  for (int g = 0; g < MAXG_A; ++g) {
-    const int e = t + NTH * g;
-    const int ee = e < totA ? e : 0;
-    const int row = ee / gpr, kg = (ee - row * gpr) * 8;
-    const bool ok = e < totA && kg < K;  // zeroed when staged (kg >= K)
-    const size_t off = ok ? (size_t)(bm + row) * K + kg : 0;
-    r.z[g][0] = gload_f4(C.Z + off);
-    r.z[g][1] = gload_f4(C.Z + off + 4);
-    r.d[g][0] = gload_f4(C.dy + off);
-    r.d[g][1] = gload_f4(C.dy + off + 4);
-  }
-  load_b(r.b, C.W, K, P.n, K, ct * TM, Kp);
-  const int n = ct * TM + wn * 16 + (lane & 15);
-  const bool okn = n < P.ld;
-  const size_t pplane = (size_t)2 * P.ld;
-  const size_t o = okn ? (size_t)tower * P.ld + n : 0;
-  r.emu = P.coef[o];
-  r.ers = P.coef[pplane + o];
-  r.einv = P.coef[2 * pplane + o];
-  r.esh = P.coef[3 * pplane + o];
-  const int m0 = bm + wm * 16 + (lane >> 4) * 4;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) r.ez[rr] = *(okn ? P.Z + (size_t)(m0 + rr) * P.ld + n : P.Z);
-}
-
-__device__ __forceinline__ void bwd_phase(const DenseArgs& a, int l, u16* smem, double* dred) {
-  const DenseLayer& C = a.ly[l];
-  const DenseLayer& P = a.ly[l - 1];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 2, wn = w & 3;
-  const int K = C.ld, Kp = round32(K), ldk = Kp + 8;
-  const int ncol = cdiv(P.ld, TM);
-  const int items = (a.R / RT) * ncol;
-  if ((int)blockIdx.x >= items) return;
-  u16* sA = smem;
-  u16* sB = sA + RT * ldk;
-  float* sc = reinterpret_cast<float*>(sB + TM * ldk);  // [tower][inv | c1 | c0][Kp]
-  for (int i = t; i < 2 * Kp; i += NTH) {
-    const int tw = i / Kp, k = i - tw * Kp;
+  const WsGeom g = ws_geom(C.ld, P.ld, 6);
+  const int nrt = a.R / RT;
+  if (g.bi >= nrt) return;
+  u16* sW = smem;
+  u16* sA = sW + g.pc * g.ldk;
+  float* sc = reinterpret_cast<float*>(sA + RT * g.ldk);  // [tower][inv | c1 | c0][Kp]
+  float* se = sc + 6 * g.Kp;                          // [tower][mu | rstd | inv | shift][pc]
+  double* ps = reinterpret_cast<double*>(se + 8 * g.pc);
+  double* pq = ps + 2 * g.pc;
+  for (int i = t; i < 2 * g.Kp; i += NTH) {
+    const int tw = i / g.Kp, k = i - tw * g.Kp;
     float inv, c1, c0;
     bn_dcoef(a, C, tw, k, inv, c1, c0);
-    sc[(tw * 3) * Kp + k] = inv;
-    sc[(tw * 3 + 1) * Kp + k] = c1;
-    sc[(tw * 3 + 2) * Kp + k] = c0;
+    sc[(tw * 3) * g.Kp + k] = inv;
+    sc[(tw * 3 + 1) * g.Kp + k] = c1;
+    sc[(tw * 3 + 2) * g.Kp + k] = c0;
   }
-  const int gpr = Kp >> 3, totA = RT * gpr;
-  BwdRegs r;
-  int it = blockIdx.x;
-  bwd_load(a, C, P, it, ncol, K, Kp, r);
-  lds_barrier();  // sc
-  for (; it < items; it += gridDim.x) {
-    int rt, ct;
-    item_rc(it, a.R / RT, ncol, rt, ct);
+  const size_t pplane = (size_t)2 * P.ld;
+  for (int i = t; i < 2 * g.pc; i += NTH) {
+    const int tw = i / g.pc, c = i - tw * g.pc, n = g.c0 + c;
+    const bool ok = n < P.ld;
+    const size_t o = ok ? (size_t)tw * P.ld + n : 0;
+    se[(tw * 4 + 0) * g.pc + c] = ok ? P.coef[o] : 0.f;
+    se[(tw * 4 + 1) * g.pc + c] = ok ? P.coef[pplane + o] : 0.f;
+    se[(tw * 4 + 2) * g.pc + c] = ok ? P.coef[2 * pplane + o] : 0.f;
+    se[(tw * 4 + 3) * g.pc + c] = ok ? P.coef[3 * pplane + o] : 0.f;
+  }
+  APanel r;
+  ws_load_a<true>(r, C.Z, C.dy, g.bi * RT, g);
+  ws_load_w(sW, g, C.W, g.K, P.n);
+  const int gpr = g.Kp >> 3, totA = RT * gpr;
+  lds_barrier();
+  for (int rt = g.bi; rt < nrt; rt += g.nb) {
     const int bm = rt * RT;
     const int tower = tower_of(bm, a.BS);
-    const float* k0 = sc + (tower * 3) * Kp;
-    const float* k1 = k0 + Kp;
-    const float* k2 = k1 + Kp;
+    const float* k0 = sc + (tower * 3) * g.Kp;
+    const float* k1 = k0 + g.Kp;
+    const float* k2 = k1 + g.Kp;
 #pragma unroll
-    for (int g = 0; g < MAXG_A; ++g) {
-      const int e = t + NTH * g;
+    for (int i = 0; i < MAXG_A; ++i) {
+      const int e = t + NTH * i;
       if (e < totA) {
         const int row = e / gpr, kg = (e - row * gpr) * 8;
-        const bool okk = kg < K;
-        const float zz[8] = {r.z[g][0].x, r.z[g][0].y, r.z[g][0].z, r.z[g][0].w,
-                             r.z[g][1].x, r.z[g][1].y, r.z[g][1].z, r.z[g][1].w};
-        const float dd[8] = {r.d[g][0].x, r.d[g][0].y, r.d[g][0].z, r.d[g][0].w,
-                             r.d[g][1].x, r.d[g][1].y, r.d[g][1].z, r.d[g][1].w};
+        const bool okk = kg < g.K;
+        const float zz[8] = {r.z[i][0].x, r.z[i][0].y, r.z[i][0].z, r.z[i][0].w,
+                             r.z[i][1].x, r.z[i][1].y, r.z[i][1].z, r.z[i][1].w};
+        const float dd[8] = {r.d[i][0].x, r.d[i][0].y, r.d[i][0].z, r.d[i][0].w,
+                             r.d[i][1].x, r.d[i][1].y, r.d[i][1].z, r.d[i][1].w};
         float y[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          y[i] = okk ? __fmaf_rn(k0[kg + i], dd[i], __fmaf_rn(k1[kg + i], zz[i], k2[kg + i])) : 0.f;
+        for (int k = 0; k < 8; ++k)
+          y[k] = okk ? __fmaf_rn(k0[kg + k], dd[k], __fmaf_rn(k1[kg + k], zz[k], k2[kg + k])) : 0.f;
         uint4 v;
         v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
         v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
-        *reinterpret_cast<uint4*>(&sA[row * ldk + kg]) = v;
-        if (ct == 0 && okk) gstore_u4(C.dZ + (size_t)(bm + row) * K + kg, v);
+        *reinterpret_cast<uint4*>(&sA[row * g.ldk + kg]) = v;
+        if (g.part == 0 && okk) gstore_u4(C.dZ + (size_t)(bm + row) * g.K + kg, v);
       }
     }
-    store_b(r.b, sB, ldk, Kp);
-    const float z[4] = {r.ez[0], r.ez[1], r.ez[2], r.ez[3]};
-    const float mu = r.emu, rs = r.ers, inv = r.einv, sh = r.esh;
     lds_barrier();
-    const int nxt = it + gridDim.x;
-    if (nxt < items) bwd_load(a, C, P, nxt, ncol, K, Kp, r);  // in flight during this item
-    const f32x4 acc = mfma16(sA, wm * 16, sB, wn * 16, ldk, Kp, lane);
-    const int n = ct * TM + wn * 16 + (lane & 15);
-    const bool okn = n < P.ld;
+    if (rt + g.nb < nrt) ws_load_a<true>(r, C.Z, C.dy, (rt + g.nb) * RT, g);
+    const u16* pa = sA + (wm * 16 + (lane & 15)) * g.ldk + 8 * (lane >> 4);
     const int m0 = bm + wm * 16 + (lane >> 4) * 4;
-    double s = 0.0, q = 0.0;
+    for (int j = wn; j < g.nsub; j += 4) {
+      const int cl = j * 16 + (lane & 15), n = g.c0 + cl;
+      const bool okn = cl < g.cols;
+      float z[4];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      if (okn) {
-        const float dy = (bn_affine(z[rr], inv, sh) > 0.f) ? acc[rr] : 0.f;
+      for (int rr = 0; rr < 4; ++rr) z[rr] = *(okn ? P.Z + (size_t)(m0 + rr) * P.ld + n : P.Z);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const u16* pb = sW + (j * 16 + (lane & 15)) * g.ldk + 8 * (lane >> 4);
+      for (int ks = 0; ks < g.Kp; ks += 32)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pa + ks),
+                                                      *reinterpret_cast<const bf16x8*>(pb + ks), acc, 0, 0, 0);
+      const float mu = se[(tower * 4 + 0) * g.pc + cl], rs = se[(tower * 4 + 1) * g.pc + cl];
+      const float inv = se[(tower * 4 + 2) * g.pc + cl], sh = se[(tower * 4 + 3) * g.pc + cl];
+      double s = 0.0, q = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float dy = (okn && bn_affine(z[rr], inv, sh) > 0.f) ? acc[rr] : 0.f;
         const float xh = (z[rr] - mu) * rs;
-        P.dy[(size_t)(m0 + rr) * P.ld + n] = dy;
+        if (okn) P.dy[(size_t)(m0 + rr) * P.ld + n] = dy;
         s += dy;
         q += (double)dy * xh;
       }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lane < 16) {
+        ps[wm * g.pc + cl] = s;
+        pq[wm * g.pc + cl] = q;
+      }
     }
-    tile_colsum_add(s, q, wm, wn, lane, dred, P.bsum + (size_t)(tower * 2) * P.ld + n,
-                    P.bsum + (size_t)(tower * 2 + 1) * P.ld + n, n < P.n);
     lds_barrier();
+    ws_sums_flush(ps, pq, g, P.n, P.bsum, P.ld, tower);
   }
 }
 
@@ -1011,16 +1057,11 @@ const void* const kDenseKernels[] = {DSSM_DENSE_KERNELS(DSSM_KPTR)};
 int dense_dw_splits(int R) { return cdiv(R, DW_K); }
 
 size_t dense_smem_bytes(const int* ld, int L) {
-  size_t best = 2 * (size_t)DW_K * TLD * 2;  // dW chunk
-  for (int l = 0; l < L; ++l) {
-    const size_t kp = (size_t)((ld[l] + 31) & ~31), ldk = kp + 8;
-    best = std::max(best, (RT + TM) * ldk * 2 + 6 * kp * 4);
-  }
-  const int ldl = ld[L - 1];
-  const int epl = ldl <= 64 ? 1 : ldl <= 128 ? 2 : ldl <= 256 ? 4 : 8;
-  best = std::max(best, (size_t)(8 * ldl + NW * 2 * 2 * 64 * epl) * 4);  // cosine
-  best = std::max(best, (size_t)6 * ld[0] * 4);                           // dZ1 coefficients
-  return best;
+  // the weight-stationary GEMM phases size their parts to kDenseSmem; the dW chunk (74 KB),
+  // cosine (<= 64 KB) and dZ1 coefficients fit inside it
+  (void)ld;
+  (void)L;
+  return (size_t)kDenseSmem;
 }
 
 bool dense_supported(int L, const int* n, const int* ld, int BS, int NEG) {

@@ -4,6 +4,7 @@ import os
 import sys
 
 os.environ.setdefault("DSSM_DENSE_TIMING", "1")
+os.environ.setdefault("DSSM_DENSE", "1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
