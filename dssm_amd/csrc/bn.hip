@@ -15,6 +15,9 @@
 //             two means the input gradient needs.
 // The affine+ReLU itself is applied by the consumers (GEMM A-operand staging, cosine kernel) or
 // by k_bn_apply / k_bn_bwd_apply where a materialized tensor is needed.
+#include <algorithm>
+
+#include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
 
@@ -55,8 +58,15 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
                                                   unsigned* __restrict__ tickets,
                                                   float* __restrict__ batch_mean,
                                                   float* __restrict__ batch_var,
-                                                  float* __restrict__ coef, int phase) {
+                                                  float* __restrict__ coef, int phase,
+                                                  double* __restrict__ zero, int nzero) {
   // phase 0: partials + last-block finalize; 1: partials only; 2: finalize only (own launch)
+  // zero: fused-statistics accumulators of this step's later layers (bnfuse.h), cleared here
+  if (phase != 2 && zero) {
+    const int nb = gridDim.x * gridDim.y;
+    for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * 1024 + threadIdx.x; i < nzero; i += nb * 1024)
+      zero[i] = 0.0;
+  }
   __shared__ float s_a[NG][64], s_b[NG][64];
   __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -378,6 +388,54 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   }
 }
 
+// Fused-statistics backward apply (bnfuse.h): the workgroup derives mean(dy), mean(dy*xhat)
+// from the layer's fp64 sums into LDS along with the forward coefficients; workgroup 0 also
+// writes dbeta / dgamma.  Same arithmetic per element as k_bn_bwd_apply.
+constexpr int kApplyMaxLd = 512;
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
+                                                         const float* __restrict__ dA, BnSide b,
+                                                         u16* __restrict__ dZ) {
+  __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
+  const int ld = b.ld;
+  const size_t plane = (size_t)2 * ld;
+  for (int i = threadIdx.x; i < 2 * ld; i += 256) {
+    const int t = i / ld, c = i - t * ld;
+    const size_t o = (size_t)t * ld + c;
+    float m1 = 0.f, m2 = 0.f;
+    if (c < b.n) fs_dcoef(b, t, c, m1, m2);
+    sc[t][0][c] = b.coef[o];
+    sc[t][1][c] = b.coef[plane + o];
+    sc[t][2][c] = b.coef[2 * plane + o];
+    sc[t][3][c] = b.coef[3 * plane + o];
+    sc[t][4][c] = m1;
+    sc[t][5][c] = m2;
+  }
+  if (blockIdx.x == 0) fs_materialize_bwd(b);
+  __syncthreads();
+  const int q = ld >> 2;
+  const int rows = b.rows_q + b.rows_d;
+  const size_t total = (size_t)rows * q;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int r = (int)(i / q);
+    const int c = (int)(i - (size_t)r * q) * 4;
+    const int t = r < b.rows_q ? 0 : 1;
+    const float4 z = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
+    const float4 da = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+    const float zz[4] = {z.x, z.y, z.z, z.w}, dd[4] = {da.x, da.y, da.z, da.w};
+    float out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float dy, xh;
+      bwd_terms(zz[k], dd[k], sc[t][0][c + k], sc[t][1][c + k], sc[t][2][c + k], sc[t][3][c + k], dy, xh);
+      out[k] = sc[t][2][c + k] * (dy - sc[t][4][c + k] - xh * sc[t][5][c + k]);
+    }
+    uint2 p;
+    p.x = pack2bf(out[0], out[1]);
+    p.y = pack2bf(out[2], out[3]);
+    *reinterpret_cast<uint2*>(dZ + (size_t)r * ld + c) = p;
+  }
+}
+
 int ew_grid(size_t total) {
   size_t g = (total + 255) / 256;
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
@@ -398,7 +456,8 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean, float* batch_var, float* partial,
-                               unsigned* tickets, float* coef, bool split, hipStream_t s) {
+                               unsigned* tickets, float* coef, bool split, hipStream_t s,
+                               double* zero, int nzero) {
   RowBlocks b(t);
   BnParams P;
   P.gamma[0] = gamma_q; P.gamma[1] = gamma_d;
@@ -407,13 +466,13 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
   P.ema_var[0] = ema_q_var; P.ema_var[1] = ema_d_var;
   if (split && train) {
     hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t,
-                       P, eps, decay, 1, partial, tickets, batch_mean, batch_var, coef, 1);
+                       P, eps, decay, 1, partial, tickets, batch_mean, batch_var, coef, 1, zero, nzero);
     hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), 1), dim3(1024), 0, s, Z, ldz, n, t, P, eps,
-                       decay, 1, partial, tickets, batch_mean, batch_var, coef, 2);
+                       decay, 1, partial, tickets, batch_mean, batch_var, coef, 2, nullptr, 0);
   } else {
     hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s,
                        Z, ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean,
-                       batch_var, coef, 0);
+                       batch_var, coef, 0, zero, nzero);
   }
   return hipGetLastError();
 }
@@ -455,6 +514,14 @@ hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowe
   else
     hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,
                        bcoef, (float*)dZ);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
+                                     hipStream_t s) {
+  if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
+  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), 1024);
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid), dim3(256), 0, s, Z, dA, b, (u16*)dZ);
   return hipGetLastError();
 }
 

@@ -1,0 +1,100 @@
+// Fused batch-norm statistics for the per-op bf16 path (gemm.hip, cosine.hip, bn.hip).
+//
+// The reference's tf.nn.moments (new_dssm.py:62-88) is a full reduction over the batch rows
+// between a layer's MatMul and its normalisation.  Instead of a separate statistics launch per
+// layer and direction, the kernel that PRODUCES a layer's pre-BN activations (the NT GEMM
+// epilogue) or its backward input (the dA GEMM epilogue, the cosine kernel) adds per-column
+// fp64 sums of its tile to a small accumulator with hardware fp64 atomics:
+//   forward : sum z, sum z^2                   -> mean, biased variance (E[z^2] - mean^2 in fp64)
+//   backward: sum dy, sum dy*xhat (dy = ReLU-masked dA, xhat = (z - mean) * rstd)
+// and the kernel that CONSUMES the layer derives the coefficients it needs from the sums in its
+// prologue (every workgroup redundantly: <= 2 x 512 columns).  One designated workgroup of the
+// consumer also materialises them (coef / batch moments / EMA update, or dgamma / dbeta), so
+// the rest of the step and the host read exactly what the unfused path writes.
+//
+// The sums are fp64 accumulations of fp32 values: the result does not depend on the atomic
+// order beyond fp64 rounding, far below the fp32 outputs' resolution.  They are zeroed by the
+// first statistics launch of the next train step (bn.hip, layer 1).
+#pragma once
+#include "common.h"
+
+namespace dssm {
+
+struct BnSide {
+  int n, ld;        // width, padded row stride
+  int rows_q, rows_d;  // rows of the query / doc tower (row_split, rows - row_split)
+  float eps, decay;
+  const float* gamma[2];
+  const float* beta[2];
+  float* ema_mean[2];
+  float* ema_var[2];
+  float* coef;      // [4][2][ld]: mean, rstd, inv = gamma*rstd, shift = beta - mean*inv
+  float* bmean;     // [2][n] batch moments (train)
+  float* bvar;
+  double* fsum;     // [2 towers][2][ld]: sum z, sum z^2
+  double* bsum;     // [2 towers][2][ld]: sum dy, sum dy*xhat
+  float* dgamma[2];
+  float* dbeta[2];
+};
+
+__device__ __forceinline__ void atomic_add_f64(double* p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Forward coefficients of column c (< n), tower t, from the step's sums (biased variance).
+__device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu, float& var,
+                                        float& rstd, float& inv, float& shift) {
+  const double N = t == 0 ? b.rows_q : b.rows_d;
+  const double m = b.fsum[(t * 2) * b.ld + c] / N;
+  const double v = b.fsum[(t * 2 + 1) * b.ld + c] / N - m * m;
+  mu = (float)m;
+  var = (float)(v > 0.0 ? v : 0.0);
+  rstd = 1.0f / sqrtf(var + b.eps);
+  inv = rstd * b.gamma[t][c];
+  shift = b.beta[t][c] - mu * inv;
+}
+
+// Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup).
+__device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
+  const size_t plane = (size_t)2 * b.ld;
+  for (int i = threadIdx.x; i < 2 * b.ld; i += blockDim.x) {
+    const int t = i / b.ld, c = i - t * b.ld;
+    const size_t o = (size_t)t * b.ld + c;
+    if (c >= b.n) {
+      b.coef[o] = 0.f; b.coef[plane + o] = 0.f; b.coef[2 * plane + o] = 0.f; b.coef[3 * plane + o] = 0.f;
+      continue;
+    }
+    float mu, var, rstd, inv, shift;
+    fs_coef(b, t, c, mu, var, rstd, inv, shift);
+    b.coef[o] = mu;
+    b.coef[plane + o] = rstd;
+    b.coef[2 * plane + o] = inv;
+    b.coef[3 * plane + o] = shift;
+    b.bmean[t * b.n + c] = mu;
+    b.bvar[t * b.n + c] = var;
+    // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
+    const float one_m = 1.0f - b.decay;
+    float* em = b.ema_mean[t];
+    float* ev = b.ema_var[t];
+    em[c] = em[c] - (em[c] - mu) * one_m;
+    ev[c] = ev[c] - (ev[c] - var) * one_m;
+  }
+}
+
+// Backward means of column c, tower t: m1 = mean(dy), m2 = mean(dy*xhat).
+__device__ __forceinline__ void fs_dcoef(const BnSide& b, int t, int c, float& m1, float& m2) {
+  const double N = t == 0 ? b.rows_q : b.rows_d;
+  m1 = (float)(b.bsum[(t * 2) * b.ld + c] / N);
+  m2 = (float)(b.bsum[(t * 2 + 1) * b.ld + c] / N);
+}
+
+// dbeta = sum dy, dgamma = sum dy*xhat per tower (one workgroup).
+__device__ __forceinline__ void fs_materialize_bwd(const BnSide& b) {
+  for (int i = threadIdx.x; i < 2 * b.n; i += blockDim.x) {
+    const int t = i / b.n, c = i - t * b.n;
+    b.dbeta[t][c] = (float)b.bsum[(t * 2) * b.ld + c];
+    b.dgamma[t][c] = (float)b.bsum[(t * 2 + 1) * b.ld + c];
+  }
+}
+
+}  // namespace dssm

@@ -10,6 +10,7 @@
 // gradient of every embedding row it owns (each doc row belongs to exactly one query: no
 // atomics).  The per-block loss/accuracy partials are summed by the last block to finish
 // (agent-scope ticket), in fixed order.
+#include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
 
@@ -28,45 +29,79 @@ __device__ __forceinline__ void loss_finalize(const float* part, int nblk, int b
   loss_finalize_impl(part, nblk, bs, out);
 }
 
-template <int EPL>
+// KM: register rows per query (NEG + 1 <= KM).  FSC (fused statistics, bnfuse.h): the last
+// layer's coefficients come from its forward sums (workgroup 0 materialises them, the batch
+// moments and the EMA update) and the workgroup adds its rows' backward sums (sum dy,
+// sum dy*xhat per tower, ReLU mask applied) to fs.bsum.
+constexpr int kCosMaxN = 512;
+template <int EPL, int KM, bool FSC>
 __global__ __launch_bounds__(256) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int split) {
+    float* __restrict__ dy, int split, BnSide fs) {
   __shared__ float s_part[2][4];
   __shared__ int s_flag;
+  __shared__ float s_co[FSC ? 2 * 4 * kCosMaxN : 1];     // [tower][mu|rstd|inv|shift][c]
+  __shared__ float s_bs[FSC ? 4 * 4 * EPL * 64 : 1];     // [wave][sq1|sq2|sd1|sd2][c]
   (void)s_flag;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int j = blockIdx.x * 4 + wv;
   const int K = neg + 1;
   const size_t plane = (size_t)2 * ld;
+  if constexpr (FSC) {
+    for (int i = threadIdx.x; i < 2 * n; i += 256) {
+      const int t = i / n, c = i - t * n;
+      float mu, var, rs, inv, sh;
+      fs_coef(fs, t, c, mu, var, rs, inv, sh);
+      s_co[(t * 4 + 0) * kCosMaxN + c] = mu;
+      s_co[(t * 4 + 1) * kCosMaxN + c] = rs;
+      s_co[(t * 4 + 2) * kCosMaxN + c] = inv;
+      s_co[(t * 4 + 3) * kCosMaxN + c] = sh;
+    }
+    if (blockIdx.x == 0) fs_materialize_fwd(fs);
+    __syncthreads();
+  }
   float lj = 0.f, cj = 0.f;
+  float bq1[EPL], bq2[EPL], bd1[EPL], bd2[EPL];  // FSC: this wave's backward sums per column
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) bq1[e] = bq2[e] = bd1[e] = bd2[e] = 0.f;
   if (j < bs) {
     // ---- all loads first: query row + K doc rows
-    float q[EPL], d[MAXK][EPL];
+    float q[EPL], d[KM][EPL], zq[EPL], zd[FSC ? KM : 1][EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const int c = lane + 64 * e;
       q[e] = (c < n) ? z[(size_t)j * ld + c] : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
+    for (int k = 0; k < KM; ++k)
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
         const int c = lane + 64 * e;
         d[k][e] = (k < K && c < n) ? z[(size_t)doc_row(j, k, bs, neg) * ld + c] : 0.f;
       }
-    if (coef) {  // last layer's BN + ReLU (query tower for q, doc tower for the docs)
+    if constexpr (FSC) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        zq[e] = q[e];
+#pragma unroll
+        for (int k = 0; k < KM; ++k) zd[k][e] = d[k][e];
+      }
+    }
+    if (coef || FSC) {  // last layer's BN + ReLU (query tower for q, doc tower for the docs)
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
         const int c = lane + 64 * e;
         if (c < n) {
-          q[e] = fmaxf(bn_affine(q[e], coef[2 * plane + c], coef[3 * plane + c]), 0.f);
-          const float inv = coef[2 * plane + ld + c], sh = coef[3 * plane + ld + c];
+          const float iq = FSC ? s_co[2 * kCosMaxN + c] : coef[2 * plane + c];
+          const float sq = FSC ? s_co[3 * kCosMaxN + c] : coef[3 * plane + c];
+          q[e] = fmaxf(bn_affine(q[e], iq, sq), 0.f);
+          const float inv = FSC ? s_co[6 * kCosMaxN + c] : coef[2 * plane + ld + c];
+          const float sh = FSC ? s_co[7 * kCosMaxN + c] : coef[3 * plane + ld + c];
 #pragma unroll
-          for (int k = 0; k < MAXK; ++k)
+          for (int k = 0; k < KM; ++k)
             if (k < K) d[k][e] = fmaxf(bn_affine(d[k][e], inv, sh), 0.f);
         }
       }
@@ -78,7 +113,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
         if (c < ld) {
           y_out[(size_t)j * ld + c] = q[e];
 #pragma unroll
-          for (int k = 0; k < MAXK; ++k)
+          for (int k = 0; k < KM; ++k)
             if (k < K) y_out[(size_t)doc_row(j, k, bs, neg) * ld + c] = d[k][e];
         }
       }
@@ -88,9 +123,9 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     for (int e = 0; e < EPL; ++e) qq = __fmaf_rn(q[e], q[e], qq);
     qq = wave_sum(qq);
     const float qn = sqrtf(qq);
-    float cs[MAXK], dn[MAXK];
+    float cs[KM], dn[KM];
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
+    for (int k = 0; k < KM; ++k) {
       cs[k] = 0.f;
       dn[k] = 1.f;
       if (k < K) {
@@ -109,24 +144,24 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     // softmax over the K scaled scores (tf.nn.softmax: exp(x - max) / sum)
     float mx = gamma * cs[0];
 #pragma unroll
-    for (int k = 1; k < MAXK; ++k)
+    for (int k = 1; k < KM; ++k)
       if (k < K) mx = fmaxf(mx, gamma * cs[k]);
-    float ex[MAXK], sum = 0.f;
+    float ex[KM], sum = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
+    for (int k = 0; k < KM; ++k) {
       ex[k] = (k < K) ? expf(gamma * cs[k] - mx) : 0.f;
       sum += ex[k];
     }
-    float p[MAXK];
+    float p[KM];
     int amax = 0;
     float pbest = -1.f;
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
+    for (int k = 0; k < KM; ++k) {
       p[k] = ex[k] / sum;
       if (k < K && p[k] > pbest) { pbest = p[k]; amax = k; }
     }
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
+    for (int k = 0; k < KM; ++k)
       if (k < K && k == lane) {
         cos_raw[(size_t)k * bs + j] = cs[k];
         cos_sim[(size_t)j * K + k] = gamma * cs[k];
@@ -140,7 +175,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
 #pragma unroll
     for (int e = 0; e < EPL; ++e) dq[e] = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
+    for (int k = 0; k < KM; ++k) {
       if (k < K) {
         const float g = gamma * (p[k] - (k == 0 ? 1.f : 0.f)) / (float)bs;
         const float a = g / (qn * dn[k]);
@@ -151,7 +186,15 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
         for (int e = 0; e < EPL; ++e) {
           const int c = lane + 64 * e;
           dq[e] += a * d[k][e] - bq * q[e];
-          if (c < ld) dy[row + c] = (c < n) ? a * q[e] - bd * d[k][e] : 0.f;
+          const float gd = (c < n) ? a * q[e] - bd * d[k][e] : 0.f;
+          if (c < ld) dy[row + c] = gd;
+          if constexpr (FSC) {
+            if (c < n) {
+              const float m = d[k][e] > 0.f ? gd : 0.f;  // ReluGrad on the doc row
+              bd1[e] += m;
+              bd2[e] = __fmaf_rn(m, (zd[k][e] - s_co[4 * kCosMaxN + c]) * s_co[5 * kCosMaxN + c], bd2[e]);
+            }
+          }
         }
       }
     }
@@ -159,6 +202,32 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     for (int e = 0; e < EPL; ++e) {
       const int c = lane + 64 * e;
       if (c < ld) dy[(size_t)j * ld + c] = (c < n) ? dq[e] : 0.f;
+      if constexpr (FSC) {
+        if (c < n) {
+          const float m = q[e] > 0.f ? dq[e] : 0.f;
+          bq1[e] = m;
+          bq2[e] = m * ((zq[e] - s_co[c]) * s_co[kCosMaxN + c]);
+        }
+      }
+    }
+  }
+  if constexpr (FSC) {
+    // workgroup sums of the 4 waves (fp64) -> the layer's backward accumulators
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int c = lane + 64 * e;
+      s_bs[(wv * 4 + 0) * EPL * 64 + c] = bq1[e];
+      s_bs[(wv * 4 + 1) * EPL * 64 + c] = bq2[e];
+      s_bs[(wv * 4 + 2) * EPL * 64 + c] = bd1[e];
+      s_bs[(wv * 4 + 3) * EPL * 64 + c] = bd2[e];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * n; i += 256) {
+      const int st = i / n, c = i - st * n;  // st: q-sum, q-sum*xhat, d-sum, d-sum*xhat
+      double acc = 0.0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
+      atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
     }
   }
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block
@@ -210,21 +279,28 @@ size_t cosine_ws_floats(int bs) { return (size_t)2 * cdiv(bs, 4) + 64; }
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s) {
-  if (neg + 1 > MAXK || n > 512) return hipErrorInvalidValue;
+                              bool split, hipStream_t s, const BnSide* fused) {
+  if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
   unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * blocks + 32);
   dim3 grid(blocks), block(256);
   const int epl = cdiv(n, 64);
-#define DSSM_COS(E)                                                                           \
-  hipLaunchKernelGGL(k_cosine_loss<E>, grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, y_out, \
-                     cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy, split ? 1 : 0)
-  if (epl <= 1) DSSM_COS(1);
-  else if (epl <= 2) DSSM_COS(2);
-  else if (epl <= 4) DSSM_COS(4);
-  else DSSM_COS(8);
+  const BnSide fs = fused ? *fused : BnSide{};
+#define DSSM_COS3(E, KM, F)                                                                     \
+  hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
+                     y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy, split ? 1 : 0, fs)
+#define DSSM_COS2(E, KM) \
+  if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
+#define DSSM_COS(E) \
+  if (neg + 1 <= 8) { DSSM_COS2(E, 8); } else { DSSM_COS2(E, 16); }
+  if (epl <= 1) { DSSM_COS(1) }
+  else if (epl <= 2) { DSSM_COS(2) }
+  else if (epl <= 4) { DSSM_COS(4) }
+  else { DSSM_COS(8) }
 #undef DSSM_COS
+#undef DSSM_COS2
+#undef DSSM_COS3
   if (split)
     hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
   return hipGetLastError();

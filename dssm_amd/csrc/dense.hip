@@ -428,6 +428,7 @@ __device__ __forceinline__ void fwd_phase(const DenseArgs& a, int l, int train, 
       for (int ks = 0; ks < g.Kp; ks += 32)
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pa + ks),
                                                       *reinterpret_cast<const bf16x8*>(pb + ks), acc, 0, 0, 0);
+      if (ftm && j == wn) { asm volatile("s_nop 0" :: "v"(acc[0]), "v"(acc[3])); stamp(ftm, fti); }
       const int cl = j * 16 + (lane & 15), n = g.c0 + cl;
       const float b = sb[cl];
       double s = 0.0, q = 0.0;
@@ -447,6 +448,7 @@ __device__ __forceinline__ void fwd_phase(const DenseArgs& a, int l, int train, 
         ps[wm * g.pc + cl] = s;
         pq[wm * g.pc + cl] = q;
       }
+      if (ftm && j == wn) { asm volatile("s_nop 0" :: "v"(s), "v"(q)); stamp(ftm, fti); }
     }
     stamp(ftm, fti);
     lds_barrier();

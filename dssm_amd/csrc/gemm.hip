@@ -13,6 +13,7 @@
 // partial slab and k_splitk_reduce sums the slabs in fixed order (deterministic, no atomics, no
 // zero-init).  The bias gradient rides along: the A^T operand gets a virtual all-ones row at
 // m = K_in, so row K_in of the [K_in+1 x N] output (the arena's [W; b] block) is colsum(dZ).
+#include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
 
@@ -219,38 +220,91 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 // ---- bf16 specialised GEMMs (perf mode) ------------------------------------------------------
 // Shared geometry: 64x64 output tile, 4 waves (2x2 of 32x32), BK = 64, double-buffered LDS with
 // the next K-step's global loads issued into registers before the current step's MFMAs.
+// The tile bodies take their tile coordinates and LDS buffers explicitly so one launch can run
+// tiles of two GEMMs (k_bwd_pair).
 constexpr int NBK = 64, NLD = NBK + 8;  // k-contiguous tiles: [row][k], 144-B rows
 constexpr int kNtMaxK = 512;            // BN-staged A: max K (LDS coefficient cache)
+constexpr int kTileElems = 64 * NLD;    // one LDS operand buffer (u16)
 
 // "NT": C[M x ldc] = A[M x K] . B where B is given k-contiguous as BT[N x ldb] (BT[n][k]).
 // Forward (BT = transposed weight shadow, + bias) and dA (BT = the weight shadow itself).
 // BN_A: A = relu(Z*inv + shift) from the fp32 pre-BN activations Z [M x lda] and the layer's
-// BN coefficients (per row tower), converted to bf16 while staging; the blockIdx.x == 0 blocks
+// BN coefficients (per row tower), converted to bf16 while staging; the column-tile-0 blocks
 // also write that activation (bf16, ld lda) to a_out for the dW GEMM.
-template <bool BN_A>
-__global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void* __restrict__ Aptr,
-                                                 int lda, const float* __restrict__ coef,
-                                                 int row_split, const u16* __restrict__ BT, int ldb,
-                                                 float* __restrict__ C, int ldc,
-                                                 const float* __restrict__ bias,
-                                                 u16* __restrict__ a_out) {
-  __shared__ __attribute__((aligned(16))) u16 sA[2][64 * NLD];
-  __shared__ __attribute__((aligned(16))) u16 sB[2][64 * NLD];
+// FS (bnfuse.h): 1 = forward, add the output tile's per-column sum / sum of squares (+ bias) to
+// f.out_sum; 2 = dA, add sum dy / sum dy*xhat of the output layer (mask and xhat from f.zb /
+// f.coefb) to f.out_sum.  Tiles never straddle the tower boundary (row_split % 64 == 0).
+struct NtParams {
+  int M, N, K;
+  const void* A;
+  int lda;
+  const float* coef;
+  int row_split;
+  const u16* BT;
+  int ldb;
+  float* C;
+  int ldc;
+  const float* bias;
+  u16* a_out;
+};
+struct NtFuse {
+  int in_from_sums;  // BN_A: derive the A operand's coefficients from `in`'s sums
+  BnSide in;
+  double* out_sum;   // [2 towers][2][ldc]
+  const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
+  const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
+};
+
+template <bool BN_A, int FS>
+__device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int tx, int ty,
+                                        u16* sA, u16* sB, float* sCoef, double* sRed) {
+  const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
-  const bool write_a = BN_A && a_out != nullptr && blockIdx.x == 0;
+  const int bm = ty * 64, bn = tx * 64;
+  const int tower = bm < a.row_split ? 0 : 1;
+  const bool write_a = BN_A && a.a_out != nullptr && tx == 0;
   // BN_A: the layer's (inv, shift) for both towers staged in LDS once; the raw fp32 Z loads of
   // the next K-step stay in flight across this step's MFMAs and are transformed in store().
-  __shared__ float sCoef[BN_A ? 4 * kNtMaxK : 1];  // [tower][inv|shift][k]
   if constexpr (BN_A) {
-    const size_t plane = (size_t)2 * lda;
-    for (int i = t; i < 2 * lda; i += 256) {
-      const int tower = i / lda, k = i - tower * lda;
-      sCoef[(tower * 2 + 0) * kNtMaxK + k] = coef[2 * plane + (size_t)tower * lda + k];
-      sCoef[(tower * 2 + 1) * kNtMaxK + k] = coef[3 * plane + (size_t)tower * lda + k];
+    if (FS == 1 && f.in_from_sums) {
+      for (int i = t; i < 2 * lda; i += 256) {
+        const int tw = i / lda, k = i - tw * lda;
+        float mu = 0.f, var = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
+        if (k < f.in.n) fs_coef(f.in, tw, k, mu, var, rs, inv, sh);
+        sCoef[(tw * 2 + 0) * kNtMaxK + k] = inv;
+        sCoef[(tw * 2 + 1) * kNtMaxK + k] = sh;
+      }
+      if (tx == 0 && ty == 0) fs_materialize_fwd(f.in);
+    } else {
+      const size_t plane = (size_t)2 * lda;
+      for (int i = t; i < 2 * lda; i += 256) {
+        const int tw = i / lda, k = i - tw * lda;
+        sCoef[(tw * 2 + 0) * kNtMaxK + k] = a.coef[2 * plane + (size_t)tw * lda + k];
+        sCoef[(tw * 2 + 1) * kNtMaxK + k] = a.coef[3 * plane + (size_t)tw * lda + k];
+      }
     }
     __syncthreads();
+  }
+  // FS == 2: the epilogue's pre-BN values and coefficients, loaded before the K loop
+  float zb[2][2][4], cb[2][4];
+  if constexpr (FS == 2) {
+    const size_t plane = (size_t)2 * ldc;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+      const bool okn = n < N;
+      const size_t o = (size_t)tower * ldc + (okn ? n : 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cb[j][q] = f.coefb[q * plane + o];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+          zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * ldc + (okn ? n : 0)];
+        }
+    }
   }
   // thread -> (row, 8-wide k group) for the two staging groups of each operand
   int am[2], ak[2];
@@ -270,15 +324,15 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
       const int gm = bm + am[g], gk = k0 + ak[g];
       const bool ok = gm < M && gk < lda;
       if constexpr (BN_A) {
-        const float* z = (const float*)Aptr + (size_t)gm * lda + gk;
+        const float* z = (const float*)a.A + (size_t)gm * lda + gk;
         rz[g][0] = ok ? *reinterpret_cast<const float4*>(z) : make_float4(0.f, 0.f, 0.f, 0.f);
         rz[g][1] = ok ? *reinterpret_cast<const float4*>(z + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
-        ra[g] = ok ? *reinterpret_cast<const uint4*>((const u16*)Aptr + (size_t)gm * lda + gk)
+        ra[g] = ok ? *reinterpret_cast<const uint4*>((const u16*)a.A + (size_t)gm * lda + gk)
                    : make_uint4(0u, 0u, 0u, 0u);
       }
       const int gn = bn + am[g];
-      rb[g] = (gn < N && gk < ldb) ? *reinterpret_cast<const uint4*>(BT + (size_t)gn * ldb + gk)
+      rb[g] = (gn < N && gk < ldb) ? *reinterpret_cast<const uint4*>(a.BT + (size_t)gn * ldb + gk)
                                    : make_uint4(0u, 0u, 0u, 0u);
     }
   };
@@ -289,7 +343,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
         const int gm = bm + am[g], gk = kcur + ak[g];
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (gm < M && gk < lda) {
-          const float* ci = &sCoef[((gm < row_split ? 0 : 1) * 2) * kNtMaxK + gk];
+          const float* ci = &sCoef[((gm < a.row_split ? 0 : 1) * 2) * kNtMaxK + gk];
           const float* ch = ci + kNtMaxK;
           const float z[8] = {rz[g][0].x, rz[g][0].y, rz[g][0].z, rz[g][0].w,
                               rz[g][1].x, rz[g][1].y, rz[g][1].z, rz[g][1].w};
@@ -298,12 +352,12 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
           for (int i = 0; i < 8; ++i) y[i] = fmaxf(bn_affine(z[i], ci[i], ch[i]), 0.f);
           v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
           v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
-          if (write_a) *reinterpret_cast<uint4*>(a_out + (size_t)gm * lda + gk) = v;
+          if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)gm * lda + gk) = v;
         }
         ra[g] = v;
       }
-      *reinterpret_cast<uint4*>(&sA[buf][am[g] * NLD + ak[g]]) = ra[g];
-      *reinterpret_cast<uint4*>(&sB[buf][am[g] * NLD + ak[g]]) = rb[g];
+      *reinterpret_cast<uint4*>(&sA[buf * kTileElems + am[g] * NLD + ak[g]]) = ra[g];
+      *reinterpret_cast<uint4*>(&sB[buf * kTileElems + am[g] * NLD + ak[g]]) = rb[g];
     }
   };
   f32x4 acc[2][2];
@@ -318,15 +372,17 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
   for (int k0 = 0; k0 < K; k0 += NBK, buf ^= 1) {
     const bool more = k0 + NBK < K;
     if (more) load(k0 + NBK);
+    const u16* ta = sA + buf * kTileElems;
+    const u16* tb = sB + buf * kTileElems;
 #pragma unroll
     for (int ks = 0; ks < NBK; ks += 32) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 32 + i * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
+        af[i] = *reinterpret_cast<const bf16x8*>(&ta[(wm * 32 + i * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 32 + j * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&tb[(wn * 32 + j * 16 + (lane & 15)) * NLD + ks + 8 * (lane >> 4)]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -336,6 +392,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
     if (more) store(buf ^ 1);
     __syncthreads();
   }
+  double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};  // FS: this lane's column partials per j
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -346,11 +403,60 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const void
         const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m < M && n < ldc) {
           const float v = acc[i][j][r];
-          C[(size_t)m * ldc + n] = (n < N) ? (bias ? v + bias[n] : v) : 0.f;
+          const float x = (n < N) ? (a.bias ? v + a.bias[n] : v) : 0.f;
+          a.C[(size_t)m * ldc + n] = x;
+          if constexpr (FS == 1) {
+            cs[j] += x;
+            cq[j] += (double)x * x;
+          } else if constexpr (FS == 2) {
+            const float z = zb[i][j][r];
+            // same mask / xhat as bn.hip's bwd_terms: dy = dA where BN(z) > 0
+            const float dy = (n < N && bn_affine(z, cb[j][2], cb[j][3]) > 0.f) ? x : 0.f;
+            const float xh = (z - cb[j][0]) * cb[j][1];
+            cs[j] += dy;
+            cq[j] += (double)dy * xh;
+          }
         }
       }
     }
   }
+  if constexpr (FS != 0) {
+    // reduce the 4 row groups of the wave, then the two wm halves through LDS
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16);
+      cs[j] += __shfl_xor(cs[j], 32);
+      cq[j] += __shfl_xor(cq[j], 16);
+      cq[j] += __shfl_xor(cq[j], 32);
+    }
+    if (wm == 1 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        sRed[(wn * 32 + j * 16 + lane) * 2] = cs[j];
+        sRed[(wn * 32 + j * 16 + lane) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn * 32 + j * 16 + lane, n = bn + c;
+        if (n < N) {
+          atomic_add_f64(f.out_sum + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
+          atomic_add_f64(f.out_sum + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
+        }
+      }
+    }
+  }
+}
+
+template <bool BN_A, int FS>
+__global__ __launch_bounds__(256) void k_gemm_nt(NtParams a, NtFuse f) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];
+  __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];
+  __shared__ float sCoef[BN_A ? 4 * kNtMaxK : 1];  // [tower][inv|shift][k]
+  __shared__ double sRed[FS ? 128 : 1];
+  nt_body<BN_A, FS>(a, f, blockIdx.x, blockIdx.y, sA, sB, sCoef, sRed);
 }
 
 // "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
@@ -372,18 +478,24 @@ __device__ __forceinline__ bf16x8 tr_frag(const u16* tile, int row0, int col0, i
   return __builtin_bit_cast(bf16x8, r);
 }
 
-__global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16* __restrict__ A,
-                                                 int lda, const u16* __restrict__ B, int ldb,
-                                                 float* __restrict__ C, int ldc, int ones_row,
-                                                 int k_per_split) {
-  __shared__ __attribute__((aligned(16))) u16 sA[2][NBK * NLD];  // [k][m]
-  __shared__ __attribute__((aligned(16))) u16 sB[2][NBK * NLD];  // [k][n]
+struct TnParams {
+  int M, N, K;
+  const u16* A;
+  int lda;
+  const u16* B;
+  int ldb;
+  float* C;
+  int ldc, ones_row, k_per_split;
+};
+
+__device__ __forceinline__ void tn_body(const TnParams& p, int tx, int ty, int tz, u16* sA, u16* sB) {
+  const int M = p.M, N = p.N, lda = p.lda, ldb = p.ldb;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
-  const int kbeg = blockIdx.z * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
-  const int Mload = ones_row ? M - 1 : M;
+  const int bm = ty * 64, bn = tx * 64;
+  const int kbeg = tz * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int Mload = p.ones_row ? M - 1 : M;
   int sk[2], sc[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -396,38 +508,38 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16*
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       const int gk = k0 + sk[g], gm = bm + sc[g], gn = bn + sc[g];
-      uint4 a = make_uint4(0u, 0u, 0u, 0u), b = make_uint4(0u, 0u, 0u, 0u);
+      uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = make_uint4(0u, 0u, 0u, 0u);
       if (gk < kend) {
         if (gm + 8 <= Mload) {
-          a = *reinterpret_cast<const uint4*>(A + (size_t)gk * lda + gm);
+          va = *reinterpret_cast<const uint4*>(p.A + (size_t)gk * lda + gm);
         } else {
           u16 x[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            x[i] = (gm + i < Mload) ? A[(size_t)gk * lda + gm + i]
-                                    : ((ones_row && gm + i == Mload) ? (u16)0x3f80 : (u16)0);
-          a.x = x[0] | ((unsigned)x[1] << 16); a.y = x[2] | ((unsigned)x[3] << 16);
-          a.z = x[4] | ((unsigned)x[5] << 16); a.w = x[6] | ((unsigned)x[7] << 16);
+            x[i] = (gm + i < Mload) ? p.A[(size_t)gk * lda + gm + i]
+                                    : ((p.ones_row && gm + i == Mload) ? (u16)0x3f80 : (u16)0);
+          va.x = x[0] | ((unsigned)x[1] << 16); va.y = x[2] | ((unsigned)x[3] << 16);
+          va.z = x[4] | ((unsigned)x[5] << 16); va.w = x[6] | ((unsigned)x[7] << 16);
         }
         if (gn + 8 <= N) {
-          b = *reinterpret_cast<const uint4*>(B + (size_t)gk * ldb + gn);
+          vb = *reinterpret_cast<const uint4*>(p.B + (size_t)gk * ldb + gn);
         } else {
           u16 x[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) x[i] = (gn + i < N) ? B[(size_t)gk * ldb + gn + i] : (u16)0;
-          b.x = x[0] | ((unsigned)x[1] << 16); b.y = x[2] | ((unsigned)x[3] << 16);
-          b.z = x[4] | ((unsigned)x[5] << 16); b.w = x[6] | ((unsigned)x[7] << 16);
+          for (int i = 0; i < 8; ++i) x[i] = (gn + i < N) ? p.B[(size_t)gk * ldb + gn + i] : (u16)0;
+          vb.x = x[0] | ((unsigned)x[1] << 16); vb.y = x[2] | ((unsigned)x[3] << 16);
+          vb.z = x[4] | ((unsigned)x[5] << 16); vb.w = x[6] | ((unsigned)x[7] << 16);
         }
       }
-      ra[g] = a;
-      rb[g] = b;
+      ra[g] = va;
+      rb[g] = vb;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      *reinterpret_cast<uint4*>(&sA[buf][sk[g] * NLD + sc[g]]) = ra[g];
-      *reinterpret_cast<uint4*>(&sB[buf][sk[g] * NLD + sc[g]]) = rb[g];
+      *reinterpret_cast<uint4*>(&sA[buf * kTileElems + sk[g] * NLD + sc[g]]) = ra[g];
+      *reinterpret_cast<uint4*>(&sB[buf * kTileElems + sk[g] * NLD + sc[g]]) = rb[g];
     }
   };
   f32x4 acc[2][2];
@@ -448,9 +560,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16*
     for (int ks = 0; ks < NBK; ks += 32) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = tr_frag(sA[buf], ks, wm * 32 + i * 16, lane);
+      for (int i = 0; i < 2; ++i) af[i] = tr_frag(sA + buf * kTileElems, ks, wm * 32 + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(sB[buf], ks, wn * 32 + j * 16, lane);
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(sB + buf * kTileElems, ks, wn * 32 + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -460,7 +572,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16*
     if (more) store(buf ^ 1);
     __syncthreads();
   }
-  float* out = C + (size_t)blockIdx.z * M * ldc;
+  float* out = p.C + (size_t)tz * M * p.ldc;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -469,9 +581,32 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, const u16*
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) out[(size_t)m * ldc + n] = acc[i][j][r];
+        if (m < M && n < N) out[(size_t)m * p.ldc + n] = acc[i][j][r];
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gemm_tn(TnParams p) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];  // [k][m]
+  __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];  // [k][n]
+  tn_body(p, blockIdx.x, blockIdx.y, blockIdx.z, sA, sB);
+}
+
+// One launch for the two backward GEMMs of layer l that both consume dZ_l: the dA tiles
+// (critical path: they feed BN_{l-1}'s backward, with its sums fused) come first, then the
+// split-K dW tiles.  Same 256-thread geometry and LDS buffers.
+__global__ __launch_bounds__(256) void k_bwd_pair(NtParams a, NtFuse f, int nt_x, int nt_blocks,
+                                                  TnParams p, int tn_x, int tn_y) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];
+  __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];
+  __shared__ double sRed[128];
+  const int b = blockIdx.x;
+  if (b < nt_blocks) {
+    nt_body<false, 2>(a, f, b % nt_x, b / nt_x, sA, sB, nullptr, sRed);
+  } else {
+    const int r = b - nt_blocks;
+    tn_body(p, r % tn_x, (r / tn_x) % tn_y, r / (tn_x * tn_y), sA, sB);
   }
 }
 
@@ -518,8 +653,9 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
     float* target = splits > 1 ? slab : C;
     if constexpr (sizeof(T) == 2) {
       if ((lda % 8) == 0 && (ldb % 8) == 0)
-        hipLaunchKernelGGL(k_gemm_tn, grid, block, 0, s, M, N, K, (const u16*)A, lda,
-                           (const u16*)B, ldb, target, ldc, ones_row ? 1 : 0, kps);
+        hipLaunchKernelGGL(k_gemm_tn, grid, block, 0, s,
+                           TnParams{M, N, K, (const u16*)A, lda, (const u16*)B, ldb, target, ldc,
+                                    ones_row ? 1 : 0, kps});
       else
         hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb,
                            target, ldc, bias, ones_row ? 1 : 0, kps);
@@ -554,12 +690,66 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || (bn_a && lda > kNtMaxK))
     return hipErrorInvalidValue;
   dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
+  const NtParams a{M, N, K, A, lda, coef, row_split, (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out};
+  const NtFuse f{};
   if (bn_a)
-    hipLaunchKernelGGL(k_gemm_nt<true>, grid, block, 0, s, M, N, K, A, lda, coef, row_split,
-                       (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out);
+    hipLaunchKernelGGL((k_gemm_nt<true, 0>), grid, block, 0, s, a, f);
   else
-    hipLaunchKernelGGL(k_gemm_nt<false>, grid, block, 0, s, M, N, K, A, lda, coef, row_split,
-                       (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out);
+    hipLaunchKernelGGL((k_gemm_nt<false, 0>), grid, block, 0, s, a, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
+                                    const BnSide* in_from_sums, int row_split, const uint16_t* BT,
+                                    int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
+                                    double* out_sum, hipStream_t s) {
+  if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
+    return hipErrorInvalidValue;
+  dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
+  const NtParams a{M, N, K, Z, lda, coef, row_split, (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out};
+  NtFuse f{};
+  if (in_from_sums) {
+    f.in_from_sums = 1;
+    f.in = *in_from_sums;
+  }
+  f.out_sum = out_sum;
+  hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
+                           int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
+                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
+                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits) {
+  if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
+    return hipErrorInvalidValue;
+  // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
+  const NtParams a{M, kin, n, dZ, lddz, nullptr, row_split, W, ldw, dA, ldda, nullptr, nullptr};
+  NtFuse f{};
+  f.out_sum = bsum_prev;
+  f.zb = z_prev;
+  f.coefb = coef_prev;
+  const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 64);
+  // dW_l = [A_{l-1}; 1]^T . dZ_l, split-K slabs left for the Adam step to sum
+  const int Mw = kin + 1;
+  const int splits = dw_splits(Mw, n, M, NBK);
+  const int kps = cdiv(cdiv(M, splits), NBK) * NBK;
+  const int nsplit = cdiv(M, kps);
+  const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kps};
+  const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
+  const int tn_blocks = tn_x * tn_y * nsplit;
+  hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
+                     nt_blocks, p, tn_x, tn_y);
+  *deferred_splits = 0;
+  if (nsplit > 1) {
+    if (defer) {
+      *deferred_splits = nsplit;  // summed inside the Adam step
+    } else {
+      const int64_t cnt = (int64_t)Mw * n;
+      const int rg = (int)std::min<int64_t>((cnt / 4 + 255) / 256 + 1, 2048);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), dim3(256), 0, s, slab, nsplit, cnt, gw);
+    }
+  }
   return hipGetLastError();
 }
 

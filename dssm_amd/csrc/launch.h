@@ -5,6 +5,8 @@
 
 namespace dssm {
 
+struct BnSide;  // bnfuse.h
+
 // split=true: cross-block finalize steps run as their own small launch instead of inside the
 // producing kernel behind an agent-scope release/acquire ticket.
 
@@ -50,6 +52,22 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
                           const float* coef, int row_split, const uint16_t* BT, int ldb, float* C,
                           int ldc, const float* bias, uint16_t* a_out, hipStream_t s);
 
+// Fused-statistics variants (bnfuse.h; bf16, row_split % 64 == 0):
+// forward NT GEMM of layer l with BN_{l-1}+ReLU staged on the A operand, whose coefficients come
+// from `coef` or, when in_from_sums != null, from that layer's sums (and are materialised by
+// one workgroup); the output's per-tower column sums (with bias) are added to out_sum.
+hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
+                                    const BnSide* in_from_sums, int row_split, const uint16_t* BT,
+                                    int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
+                                    double* out_sum, hipStream_t s);
+// Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
+// z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
+// defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
+hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
+                           int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
+                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
+                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits);
+
 // ---- batch norm (bn.hip) ----
 struct BnTowers {
   int row_split;   // rows [0,row_split) tower 0 (query), [row_split, rows) tower 1 (doc)
@@ -66,7 +84,11 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean /*[2*n] or null*/, float* batch_var,
                                float* partial, unsigned* tickets, float* coef, bool split,
-                               hipStream_t s);
+                               hipStream_t s, double* zero = nullptr, int nzero = 0);
+// Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
+// also writes b.dgamma / b.dbeta.
+hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
+                                     hipStream_t s);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
@@ -85,7 +107,7 @@ size_t cosine_ws_floats(int bs);
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s);
+                              bool split, hipStream_t s, const BnSide* fused = nullptr);
 
 // ---- optimizer (adam.hip) ----
 struct ShadowSeg {

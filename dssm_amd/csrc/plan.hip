@@ -12,6 +12,7 @@
 
 #include "../../include/dssm.h"
 #include "common.h"
+#include "bnfuse.h"
 #include "dense.h"
 #include "launch.h"
 
@@ -172,8 +173,9 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.csc_col = take(ent * 4);
   // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
   Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
-  if (Lt.dense_ok) {
-    // fp64 statistics accumulators (one contiguous region: re-zeroed after a failed launch)
+  if (Lt.bf16) {
+    // fp64 statistics accumulators of the fused-statistics per-op path and the dense kernels
+    // (one contiguous region: zeroed as a whole)
     size_t sums = 0;
     for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
     Lt.dense_sums = take(sums);
@@ -185,6 +187,8 @@ void make_layout(const dssm_config* c, Layout& Lt) {
       Lt.bsum[l] = o;
       o += (size_t)4 * Lt.ldp[l] * 8;
     }
+  }
+  if (Lt.dense_ok) {
     Lt.dense_args = take(sizeof(dssm::DenseArgs));
     Lt.dense_bar = take(3 * 256);
     Lt.loss_part = take((size_t)kDenseMaxGrid * 2 * 4);
@@ -205,6 +209,7 @@ struct dssm_plan {
   const int32_t* indices = nullptr;
   const float* values = nullptr;
   bool fwd_train_done = false;
+  bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
@@ -218,6 +223,9 @@ struct dssm_plan {
   // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
   bool csc_inline = true;
   bool split_finalize = false;  // DSSM_SPLIT_FINALIZE=1: finalize steps as separate launches
+  // bf16 train steps with the BN statistics fused into the producing / consuming kernels
+  // (bnfuse.h); DSSM_FUSED_STATS=0 selects the separate statistics launches
+  bool fused_stats = false;
   hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
   hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -331,6 +339,38 @@ struct dssm_plan {
   // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
   bool wholek(int l) const { return Lt.bf16 && l > 0 && Lt.ldp[l - 1] <= 512; }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
+  dssm::BnSide bn_side(int l) const {
+    dssm::BnSide b{};
+    const int n = Lt.n[l];
+    b.n = n;
+    b.ld = Lt.ldp[l];
+    b.rows_q = Lt.BS;
+    b.rows_d = Lt.R - Lt.BS;
+    b.eps = cfg.bn_eps;
+    b.decay = cfg.ema_decay;
+    for (int t = 0; t < 2; ++t) {
+      b.gamma[t] = p + Lt.bn_off[l][2 * t];
+      b.beta[t] = p + Lt.bn_off[l][2 * t + 1];
+      b.dgamma[t] = g + Lt.bn_off[l][2 * t];
+      b.dbeta[t] = g + Lt.bn_off[l][2 * t + 1];
+      b.ema_mean[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t) * n;
+      b.ema_var[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t + 1) * n;
+    }
+    b.coef = at<float>(Lt.coef[l]);
+    b.bmean = at<float>(Lt.bmean[l]);
+    b.bvar = at<float>(Lt.bvar[l]);
+    b.fsum = at<double>(Lt.fsum[l]);
+    b.bsum = at<double>(Lt.bsum[l]);
+    return b;
+  }
+  bool fused_stats_ok() const {
+    if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.dense_sums_bytes) return false;
+    for (int l = 0; l < Lt.L; ++l)
+      if (Lt.ldp[l] > 512) return false;
+    for (int l = 1; l < Lt.L; ++l)
+      if (!wholek(l)) return false;
+    return true;
+  }
   dssm::ShadowList shadows() {
     dssm::ShadowList s;
     s.count = 0;
@@ -429,6 +469,8 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->ema = ema;
   if (const char* e = std::getenv("DSSM_SPLIT_FINALIZE")) P->split_finalize = e[0] == '1';
   if (const char* e = std::getenv("DSSM_CSC_SIDE")) P->csc_inline = e[0] != '1';
+  P->fused_stats = P->fused_stats_ok();
+  if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   {
     const float st[4] = {cfg->beta1, cfg->beta2, 0.f, 0.f};  // TF: beta*_power start at beta*
     if (hipMemcpy(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice) != hipSuccess) {
@@ -604,6 +646,41 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     P->fwd_train_done = train != 0;
     return DSSM_OK;
   }
+  if (train && P->fused_stats) {
+    // BN1 statistics (+ clearing this step's fused accumulators), then each NT GEMM stages the
+    // previous layer's BN+ReLU and accumulates its own output's sums, the cosine kernel the last
+    // layer's backward sums (bnfuse.h)
+    {
+      float* ema = P->ema + Lt.ema_off[0];
+      const int n = Lt.n[0];
+      HIP_TRY(dssm::launch_bn_fwd_stats(
+          P->at<float>(Lt.Z[0]), Lt.ldp[0], n, tw, P->p + Lt.bn_off[0][0], P->p + Lt.bn_off[0][1],
+          P->p + Lt.bn_off[0][2], P->p + Lt.bn_off[0][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
+          c.bn_eps, c.ema_decay, true, P->at<float>(Lt.bmean[0]), P->at<float>(Lt.bvar[0]),
+          P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[0][0]), P->at<float>(Lt.coef[0]),
+          P->split_finalize, s, P->at<double>(Lt.dense_sums), (int)(Lt.dense_sums_bytes / 8)));
+    }
+    for (int l = 1; l < Lt.L; ++l) {
+      const dssm::BnSide in = P->bn_side(l - 1);
+      HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
+          Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
+          P->at<float>(Lt.coef[l - 1]), l - 1 >= 1 ? &in : nullptr, Lt.BS,
+          P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
+          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s));
+    }
+    const int lL = Lt.L - 1;
+    const dssm::BnSide last = P->bn_side(lL);
+    HIP_TRY(dssm::launch_cosine_loss(
+        P->at<float>(Lt.Z[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG, c.gamma,
+        P->at<float>(Lt.coef[lL]), P->at<float>(Lt.A[lL]), P->at<float>(Lt.cos_raw),
+        P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
+        P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
+        P->split_finalize, s, &last));
+    P->fwd_train_done = true;
+    P->fwd_fused = true;
+    return DSSM_OK;
+  }
+  P->fwd_fused = false;
   for (int l = 0; l < Lt.L; ++l) {
     float* ema = P->ema + Lt.ema_off[l];
     const int n = Lt.n[l];
@@ -682,6 +759,23 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
     HIP_TRY(dssm::launch_dense_bwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.dense_kmax,
                                    defer ? 1 : 0, P->dense_grid, P->dense_smem, s));
     for (int l = 1; l < Lt.L; ++l) P->dw_deferred[l] = defer ? Lt.dense_splits : 0;
+    return dw1_backward(P, s);
+  }
+  if (P->fwd_fused) {
+    // BN_L apply from the cosine kernel's sums, then per layer one launch for dA_{l-1} (with
+    // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply
+    for (int l = Lt.L - 1; l >= 0; --l) {
+      const dssm::BnSide b = P->bn_side(l);
+      HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
+                                              P->at<uint16_t>(Lt.dZ[l]), s));
+      if (l == 0) break;
+      HIP_TRY(dssm::launch_bwd_pair(
+          Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
+          P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
+          P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
+          Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
+          P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l]));
+    }
     return dw1_backward(P, s);
   }
   for (int l = Lt.L - 1; l >= 0; --l) {
@@ -801,6 +895,8 @@ int dssm_plan_check(dssm_plan* P, void* stream) {
 }
 
 int dssm_plan_dense_enabled(dssm_plan* P) { return P && P->dense_on ? P->dense_grid : 0; }
+
+int dssm_plan_fused_stats(dssm_plan* P) { return P && P->fused_stats && !P->dense_on ? 1 : 0; }
 
 int dssm_plan_set_adam_state(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");

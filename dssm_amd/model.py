@@ -257,6 +257,11 @@ class DSSM:
     def dense_persistent(self) -> bool:
         return bool(self.lib.dssm_plan_dense_enabled(self._plan))
 
+    @property
+    def fused_stats(self) -> bool:
+        """True when bf16 train steps run with the BN statistics fused (csrc/bnfuse.h)."""
+        return bool(self.lib.dssm_plan_fused_stats(self._plan))
+
     # ---- kernel timing probes (HIP events on the launch stream) -------------------------------
     def probe_enable(self, probe_id: int, max_samples: int):
         check(self.lib.dssm_plan_probe_enable(self._plan, probe_id, max_samples), "probe_enable")

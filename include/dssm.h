@@ -147,6 +147,10 @@ int dssm_plan_check(dssm_plan* plan, void* stream);
  * persistent kernels (dense.hip), 0 when
  * it uses per-op launches (fp32 mode, unsupported shapes, or DSSM_DENSE=0). */
 int dssm_plan_dense_enabled(dssm_plan* plan);
+/* 1 when the plan's bf16 train steps run the per-op schedule with the batch-norm statistics
+ * fused into the producing / consuming kernels (DSSM_FUSED_STATS, default on where supported:
+ * bf16, query_bs % 64 == 0, widths <= 512), else 0. */
+int dssm_plan_fused_stats(dssm_plan* plan);
 int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, float* ms);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
