@@ -14,7 +14,9 @@
 //
 // The sums are fp64 accumulations of fp32 values: the result does not depend on the atomic
 // order beyond fp64 rounding, far below the fp32 outputs' resolution.  They are zeroed by the
-// first statistics launch of the next train step (bn.hip, layer 1).
+// first launch of the next train step (the CSC histogram, spmm.hip).  Same-address fp64 atomics
+// serialise (measured on MI355X: ~23 ns each; tools/micro/atomics.hip), so the SpMM's 384
+// workgroups spread layer 1's sums over fcopies replicas that the consumers add up.
 #pragma once
 #include "common.h"
 
@@ -31,7 +33,8 @@ struct BnSide {
   float* coef;      // [4][2][ld]: mean, rstd, inv = gamma*rstd, shift = beta - mean*inv
   float* bmean;     // [2][n] batch moments (train)
   float* bvar;
-  double* fsum;     // [2 towers][2][ld]: sum z, sum z^2
+  double* fsum;     // fcopies x [2 towers][2][ld]: sum z, sum z^2 (replicas summed by consumers)
+  int fcopies;
   double* bsum;     // [2 towers][2][ld]: sum dy, sum dy*xhat
   float* dgamma[2];
   float* dbeta[2];
@@ -41,17 +44,67 @@ __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Forward coefficients of column c (< n), tower t, from the step's sums (biased variance).
-__device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu, float& var,
-                                        float& rstd, float& inv, float& shift) {
+// Forward coefficients of column c (< n), tower t, from the step's sums s = sum z, q = sum z^2
+// (biased variance).
+__device__ __forceinline__ void fs_coef_from(const BnSide& b, int t, int c, double s, double q,
+                                             float& mu, float& var, float& rstd, float& inv,
+                                             float& shift) {
   const double N = t == 0 ? b.rows_q : b.rows_d;
-  const double m = b.fsum[(t * 2) * b.ld + c] / N;
-  const double v = b.fsum[(t * 2 + 1) * b.ld + c] / N - m * m;
+  const double m = s / N;
+  const double v = q / N - m * m;
   mu = (float)m;
   var = (float)(v > 0.0 ? v : 0.0);
   rstd = 1.0f / sqrtf(var + b.eps);
   inv = rstd * b.gamma[t][c];
   shift = b.beta[t][c] - mu * inv;
+}
+__device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu, float& var,
+                                        float& rstd, float& inv, float& shift) {
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < b.fcopies; ++k) {
+    s += b.fsum[(size_t)k * 4 * b.ld + (t * 2) * b.ld + c];
+    q += b.fsum[(size_t)k * 4 * b.ld + (t * 2 + 1) * b.ld + c];
+  }
+  fs_coef_from(b, t, c, s, q, mu, var, rstd, inv, shift);
+}
+
+// Every thread of the workgroup derives the coefficients of items i = tid + nthreads*u
+// (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all replica loads in flight at once,
+// then calls out(tower, column, mu, rstd, inv, shift) (zeros for pad columns >= n).
+constexpr int kMaxFsumCopies = 8;
+template <int NPER, typename F>
+__device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthreads, F&& out) {
+  double s[NPER], q[NPER];
+  int off[NPER];
+#pragma unroll
+  for (int u = 0; u < NPER; ++u) {
+    const int i = tid + nthreads * u;
+    const int ic = i < 2 * b.ld ? i : 0;  // clamped: every load issued, unconditionally
+    const int t = ic / b.ld, c = ic - t * b.ld;
+    off[u] = (t * 2) * b.ld + c;
+    s[u] = q[u] = 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxFsumCopies; ++k) {
+    if (k < b.fcopies) {  // uniform
+      const double* base = b.fsum + (size_t)k * 4 * b.ld;
+#pragma unroll
+      for (int u = 0; u < NPER; ++u) {
+        s[u] += base[off[u]];
+        q[u] += base[off[u] + b.ld];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NPER; ++u) {
+    const int i = tid + nthreads * u;
+    if (i < 2 * b.ld) {
+      const int t = i / b.ld, c = i - t * b.ld;
+      float mu = 0.f, var = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
+      if (c < b.n) fs_coef_from(b, t, c, s[u], q[u], mu, var, rs, inv, sh);
+      out(t, c, mu, rs, inv, sh);
+    }
+  }
 }
 
 // Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup).

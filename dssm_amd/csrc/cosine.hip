@@ -51,15 +51,13 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   const int K = neg + 1;
   const size_t plane = (size_t)2 * ld;
   if constexpr (FSC) {
-    for (int i = threadIdx.x; i < 2 * n; i += 256) {
-      const int t = i / n, c = i - t * n;
-      float mu, var, rs, inv, sh;
-      fs_coef(fs, t, c, mu, var, rs, inv, sh);
+    fs_coef_stage<(2 * kCosMaxN) / 256>(fs, threadIdx.x, 256,
+                                          [&](int t, int c, float mu, float rs, float inv, float sh) {
       s_co[(t * 4 + 0) * kCosMaxN + c] = mu;
       s_co[(t * 4 + 1) * kCosMaxN + c] = rs;
       s_co[(t * 4 + 2) * kCosMaxN + c] = inv;
       s_co[(t * 4 + 3) * kCosMaxN + c] = sh;
-    }
+    });
     if (blockIdx.x == 0) fs_materialize_fwd(fs);
     __syncthreads();
   }

@@ -268,13 +268,10 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
   // the next K-step stay in flight across this step's MFMAs and are transformed in store().
   if constexpr (BN_A) {
     if (FS == 1 && f.in_from_sums) {
-      for (int i = t; i < 2 * lda; i += 256) {
-        const int tw = i / lda, k = i - tw * lda;
-        float mu = 0.f, var = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
-        if (k < f.in.n) fs_coef(f.in, tw, k, mu, var, rs, inv, sh);
+      fs_coef_stage<(2 * kNtMaxK) / 256>(f.in, t, 256, [&](int tw, int k, float, float, float inv, float sh) {
         sCoef[(tw * 2 + 0) * kNtMaxK + k] = inv;
         sCoef[(tw * 2 + 1) * kNtMaxK + k] = sh;
-      }
+      });
       if (tx == 0 && ty == 0) fs_materialize_fwd(f.in);
     } else {
       const size_t plane = (size_t)2 * lda;

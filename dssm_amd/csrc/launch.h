@@ -21,7 +21,13 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
 size_t csc_scratch_ints(int D, int rows, int max_nnz);
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
-                            float* csc_val, int* csc_col, hipStream_t s);
+                            float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
+                            int nzero = 0);
+// FC1 forward (bf16 W1 shadow, ldz <= 512) + BN1 per-tower column sums into fsum (bnfuse.h).
+hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
+                                 int rows, const uint16_t* W, int ldw, int n, const float* bias,
+                                 float* Z, int ldz, double* fsum, int row_split, int copies,
+                                 hipStream_t s);
 // dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row
 // is written (light rows summed, heavy rows zeroed) then heavy rows accumulated with atomics;
 // light=false: only the heavy rows are accumulated (into rows that must already be zero).

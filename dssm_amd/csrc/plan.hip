@@ -33,6 +33,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+constexpr int kFsum0Copies = 8;     // max replicas of layer 1's fused forward sums (bnfuse.h)
 constexpr int kDenseMaxGrid = 1024;  // workgroups of the persistent dense kernels (one per CU)
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -177,13 +178,14 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     // fp64 statistics accumulators of the fused-statistics per-op path and the dense kernels
     // (one contiguous region: zeroed as a whole)
     size_t sums = 0;
-    for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
+    // layer 1's forward sums come from the SpMM's many workgroups: kFsum0Copies replicas
+    for (int l = 0; l < Lt.L; ++l) sums += ((l == 0 ? kFsum0Copies : 1) + 1) * (size_t)4 * Lt.ldp[l] * 8;
     Lt.dense_sums = take(sums);
     Lt.dense_sums_bytes = sums;
     size_t o = Lt.dense_sums;
     for (int l = 0; l < Lt.L; ++l) {
       Lt.fsum[l] = o;
-      o += (size_t)4 * Lt.ldp[l] * 8;
+      o += (size_t)(l == 0 ? kFsum0Copies : 1) * 4 * Lt.ldp[l] * 8;
       Lt.bsum[l] = o;
       o += (size_t)4 * Lt.ldp[l] * 8;
     }
@@ -226,6 +228,11 @@ struct dssm_plan {
   // bf16 train steps with the BN statistics fused into the producing / consuming kernels
   // (bnfuse.h); DSSM_FUSED_STATS=0 selects the separate statistics launches
   bool fused_stats = false;
+  // fused-statistics steps: BN1 sums accumulated by the SpMM itself (16-row workgroups, 8
+  // accumulator replicas) instead of the separate statistics launch; DSSM_SPMM_STATS=1.
+  // Measured slower on MI355X at C2 (the 16-row workgroups cost more than the launch saves).
+  bool spmm_stats = false;
+  int fsum0_copies = 1;  // DSSM_FSUM_COPIES (<= kFsum0Copies)
   hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
   hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -360,6 +367,7 @@ struct dssm_plan {
     b.bmean = at<float>(Lt.bmean[l]);
     b.bvar = at<float>(Lt.bvar[l]);
     b.fsum = at<double>(Lt.fsum[l]);
+    b.fcopies = (l == 0 && spmm_stats) ? fsum0_copies : 1;
     b.bsum = at<double>(Lt.bsum[l]);
     return b;
   }
@@ -471,6 +479,9 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   if (const char* e = std::getenv("DSSM_CSC_SIDE")) P->csc_inline = e[0] != '1';
   P->fused_stats = P->fused_stats_ok();
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
+  if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
+  if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
+    P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
   {
     const float st[4] = {cfg->beta1, cfg->beta2, 0.f, 0.f};  // TF: beta*_power start at beta*
     if (hipMemcpy(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice) != hipSuccess) {
@@ -624,10 +635,17 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
       HIP_TRY(hipStreamWaitEvent(P->side, P->ev_batch, 0));
     }
     P->probe_begin(DSSM_PROBE_CSC, cs);
+    // fused-statistics steps: the transpose's first launch also clears the step's BN sums (on
+    // the launch stream; the side-stream schedule clears them with a memset there instead)
+    const bool clear = P->fused_stats && !P->dense_on;
+    if (clear && !P->csc_inline)
+      HIP_TRY(hipMemsetAsync(P->ws + Lt.dense_sums, 0, Lt.dense_sums_bytes, s));
     HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
-                                   P->at<int>(Lt.csc_col), cs));
+                                   P->at<int>(Lt.csc_col), cs,
+                                   clear && P->csc_inline ? P->at<double>(Lt.dense_sums) : nullptr,
+                                   clear && P->csc_inline ? (int)(Lt.dense_sums_bytes / 8) : 0));
     P->probe_end(DSSM_PROBE_CSC, cs);
     if (!P->csc_inline) {
       HIP_TRY(hipEventRecord(P->ev_csc, P->side));
@@ -635,9 +653,16 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     }
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
-  HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
+  if (train && P->fused_stats && P->spmm_stats && !P->dense_on) {
+    HIP_TRY(dssm::launch_spmm_fwd_stats(P->indptr, P->indices, P->values, Lt.R,
+                                        P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
+                                        P->at<float>(Lt.Z[0]), Lt.ldp[0], P->at<double>(Lt.fsum[0]),
+                                        Lt.BS, P->fsum0_copies, s));
+  } else {
+    HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
                                 P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
                                 Lt.ldp[0], s));
+  }
   P->probe_end(DSSM_PROBE_SPMM_FWD, s);
   if (P->dense_on) {  // BN1 .. cosine + loss (+ dy_L and its BN partials) in one launch
     HIP_TRY(dssm::launch_dense_fwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.ldp[Lt.L - 1],
@@ -647,10 +672,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     return DSSM_OK;
   }
   if (train && P->fused_stats) {
-    // BN1 statistics (+ clearing this step's fused accumulators), then each NT GEMM stages the
-    // previous layer's BN+ReLU and accumulates its own output's sums, the cosine kernel the last
-    // layer's backward sums (bnfuse.h)
-    {
+    // BN1 statistics by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
+    // stages the previous layer's BN+ReLU and accumulates its own output's sums, the cosine
+    // kernel the last layer's backward sums (bnfuse.h)
+    if (!P->spmm_stats) {
       float* ema = P->ema + Lt.ema_off[0];
       const int n = Lt.n[0];
       HIP_TRY(dssm::launch_bn_fwd_stats(
@@ -658,13 +683,13 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           P->p + Lt.bn_off[0][2], P->p + Lt.bn_off[0][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
           c.bn_eps, c.ema_decay, true, P->at<float>(Lt.bmean[0]), P->at<float>(Lt.bvar[0]),
           P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[0][0]), P->at<float>(Lt.coef[0]),
-          P->split_finalize, s, P->at<double>(Lt.dense_sums), (int)(Lt.dense_sums_bytes / 8)));
+          P->split_finalize, s));
     }
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
-          P->at<float>(Lt.coef[l - 1]), l - 1 >= 1 ? &in : nullptr, Lt.BS,
+          P->at<float>(Lt.coef[l - 1]), (l > 1 || P->spmm_stats) ? &in : nullptr, Lt.BS,
           P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
           P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s));
     }

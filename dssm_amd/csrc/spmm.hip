@@ -17,6 +17,8 @@
 // (each atomic wave-instruction covers 256 contiguous bytes); "light" columns are summed by
 // one wave each, either here (materialized dW1 for the all-reduce) or inside the fused
 // W1 Adam kernel (adam.hip), which then never writes or re-reads a dense dW1.
+#include <cstdlib>
+
 #include "common.h"
 #include "gather.h"
 #include "launch.h"
@@ -55,6 +57,65 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
   }
 }
 
+// FC1 forward + BN1 statistics (fused-statistics schedule, bnfuse.h): 16 rows per 1024-thread
+// workgroup (one tower: row_split % 16 == 0); every wave stages its row's z and z^2 in LDS,
+// the workgroup sums its 16 rows per column in fp64 and adds them to fsum[tower] with one atomic
+// per (column, statistic).
+constexpr int kSpmmStatRows = 16;
+template <typename TW, int RPW>
+__global__ __launch_bounds__(64 * kSpmmStatRows / RPW) void k_spmm_fwd_stats(
+    const int* __restrict__ indptr, const int* __restrict__ indices,
+    const float* __restrict__ values, int rows, const TW* __restrict__ W, int ldw, int n,
+    const float* __restrict__ bias, float* __restrict__ Z, int ldz, double* __restrict__ fsum,
+    int row_split, int copies) {
+  constexpr int NT = 64 * kSpmmStatRows / RPW;
+  extern __shared__ float red[];  // [waves][2][ldz]
+  const int wv = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * kSpmmStatRows;
+  const int lane = lane_id();
+  const int c = lane * 8;  // ldz <= 512: one 512-column pass
+  const int nvalid = (c < ldz) ? n - c : 0;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + wv * RPW + rr;
+    if (row >= rows) break;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = (c + i < n) ? bias[c + i] : 0.f;
+    const int s = indptr[row], e = indptr[row + 1];
+    gather_accumulate(indices, values, s, e, W, ldw, c, nvalid, acc);
+    if (c < ldz) store8(Z + (size_t)row * ldz + c, acc);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s1[i] += acc[i];
+      s2[i] = __fmaf_rn(acc[i], acc[i], s2[i]);
+    }
+  }
+  if (c < ldz) {
+    float* r0 = red + (size_t)(wv * 2) * ldz + c;
+    float* r1 = r0 + ldz;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      r0[i] = s1[i];
+      r1[i] = s2[i];
+    }
+  }
+  __syncthreads();
+  const int tower = row0 < row_split ? 0 : 1;
+  // replica blockIdx % copies: spreads the same-address atomics (bnfuse.h)
+  fsum += (size_t)(blockIdx.x % copies) * 4 * ldz;
+  for (int i = threadIdx.x; i < 2 * n; i += NT) {
+    const int st = i / n, cc = i - st * n;
+    double a = 0.0;
+#pragma unroll
+    for (int w = 0; w < kSpmmStatRows / RPW; ++w) a += red[(size_t)(w * 2 + st) * ldz + cc];
+    __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + st) * ldz + cc, a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- CSR -> CSC ------------------------------------------------------------------------------
 // Blocks own contiguous row ranges; wave w of a block walks rows r0+w, r0+w+16, ... and its
 // lanes the row's entries (a row's columns are distinct, so a wave-instruction never collides).
@@ -64,8 +125,11 @@ constexpr int kTU = 8;  // entries per thread in flight
 
 __global__ __launch_bounds__(kTB) void k_csc_hist(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices, int rows, int D,
-                                                  int rows_per_block, int* __restrict__ gcnt) {
+                                                  int rows_per_block, int* __restrict__ gcnt,
+                                                  double* __restrict__ zero, int nzero) {
   extern __shared__ int hist[];
+  // the first launch of a train step also clears the step's fused BN accumulators (bnfuse.h)
+  for (int i = blockIdx.x * kTB + threadIdx.x; i < nzero; i += gridDim.x * kTB) zero[i] = 0.0;
   for (int c = threadIdx.x; c < D; c += kTB) hist[c] = 0;
   const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
   const int e0 = indptr[r0], e1 = indptr[r1];  // the block's rows own a contiguous entry range
@@ -365,6 +429,27 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
   return hipGetLastError();
 }
 
+hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
+                                 int rows, const uint16_t* W, int ldw, int n, const float* bias,
+                                 float* Z, int ldz, double* fsum, int row_split, int copies,
+                                 hipStream_t s) {
+  if (ldz > 512 || (row_split % kSpmmStatRows)) return hipErrorInvalidValue;
+  static const int rpw = [] {
+    const char* e = std::getenv("DSSM_SPMM_STATS_RPW");
+    return e ? std::atoi(e) : 2;
+  }();
+  const dim3 grid(cdiv(rows, kSpmmStatRows));
+#define DSSM_SPS(R)                                                                              \
+  hipLaunchKernelGGL((k_spmm_fwd_stats<u16, R>), grid, dim3(64 * kSpmmStatRows / R),              \
+                     (size_t)(kSpmmStatRows / R) * 2 * ldz * sizeof(float), s, indptr, indices,    \
+                     values, rows, (const u16*)W, ldw, n, bias, Z, ldz, fsum, row_split, copies)
+  if (rpw == 1) DSSM_SPS(1);
+  else if (rpw == 4) DSSM_SPS(4);
+  else DSSM_SPS(2);
+#undef DSSM_SPS
+  return hipGetLastError();
+}
+
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
   // cnt (D+1, padded) + cursor (D+1) + rank_tmp (max_nnz)
   return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64;
@@ -372,7 +457,8 @@ size_t csc_scratch_ints(int D, int rows, int max_nnz) {
 
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
-                            float* csc_val, int* csc_col, hipStream_t s) {
+                            float* csc_val, int* csc_col, hipStream_t s, double* zero,
+                            int nzero) {
   int* cnt = scratch;                 // zero between steps (re-zeroed by k_csc_scan)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
@@ -384,12 +470,16 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     const int rpb = cdiv(rows, nblk);
     const int grid = cdiv(rows, rpb);
     hipLaunchKernelGGL(k_csc_hist, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb,
-                       cnt);
+                       cnt, zero, nzero);
     hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
     hipLaunchKernelGGL(k_csc_fill, dim3(grid), dim3(kTB), lds + (size_t)(rpb + 1) * sizeof(int), s,
                        indptr, indices, values, rows, D, rpb, cursor, col_ptr, rank_tmp, csc_row,
                        csc_val, csc_col);
   } else {
+    if (nzero) {
+      const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(double), s);
+      if (e != hipSuccess) return e;
+    }
     const int cblocks = max(1, min(cdiv(max_nnz, 256), 2048));
     hipLaunchKernelGGL(k_csc_count_global, dim3(cblocks), dim3(256), 0, s, indptr, indices, rows,
                        cnt);

@@ -37,12 +37,13 @@ CASES = [
 ]
 
 
-def _model(case, fused: bool, p):
+def _model(case, fused: bool, p, spmm_stats: bool = False):
     from dssm_amd.model import DSSM
     D, widths, BS, NEG = case
-    saved = {k: os.environ.get(k) for k in ("DSSM_DENSE", "DSSM_FUSED_STATS")}
+    saved = {k: os.environ.get(k) for k in ("DSSM_DENSE", "DSSM_FUSED_STATS", "DSSM_SPMM_STATS")}
     os.environ["DSSM_DENSE"] = "0"
     os.environ["DSSM_FUSED_STATS"] = "1" if fused else "0"
+    os.environ["DSSM_SPMM_STATS"] = "1" if spmm_stats else "0"
     try:
         m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
     finally:
@@ -62,13 +63,14 @@ def _is_bias(k):
     return re.fullmatch(r"b\d+", k) is not None
 
 
+@pytest.mark.parametrize("spmm_stats", [False, True], ids=["bn1-launch", "bn1-in-spmm"])
 @pytest.mark.parametrize("case", CASES)
-def test_fused_stats_match_separate_launches_and_oracle(case):
+def test_fused_stats_match_separate_launches_and_oracle(case, spmm_stats):
     D, widths, BS, NEG = case
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
     p = O.init_params(cfg, seed=21)
     batch = synth_batch(D, BS, NEG, seed=99, mean_nnz=24)
-    a, b = _model(case, True, p), _model(case, False, p)
+    a, b = _model(case, True, p, spmm_stats), _model(case, False, p)
     for m in (a, b):
         m.set_batch(batch)
         m.forward(True)
