@@ -22,7 +22,7 @@ size_t csc_scratch_ints(int D, int rows, int max_nnz);
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
-                            int nzero = 0);
+                            int nzero = 0, bool rank_path = true);
 // FC1 forward (bf16 W1 shadow, ldz <= 512) + BN1 per-tower column sums into fsum (bnfuse.h).
 hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
                                  int rows, const uint16_t* W, int ldw, int n, const float* bias,

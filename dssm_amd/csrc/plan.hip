@@ -224,6 +224,9 @@ struct dssm_plan {
   // stream, whose join costs a cross-queue wait and whose kernels contend with the forward's);
   // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
   bool csc_inline = true;
+  // CSC transpose by rank / multi-block scan / row-parallel scatter launches (spmm.hip);
+  // DSSM_CSC_LEGACY=1 selects the histogram / single-block scan / fill launches
+  bool csc_rank_path = true;
   bool split_finalize = false;  // DSSM_SPLIT_FINALIZE=1: finalize steps as separate launches
   // bf16 train steps with the BN statistics fused into the producing / consuming kernels
   // (bnfuse.h); DSSM_FUSED_STATS=0 selects the separate statistics launches
@@ -477,6 +480,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->ema = ema;
   if (const char* e = std::getenv("DSSM_SPLIT_FINALIZE")) P->split_finalize = e[0] == '1';
   if (const char* e = std::getenv("DSSM_CSC_SIDE")) P->csc_inline = e[0] != '1';
+  if (const char* e = std::getenv("DSSM_CSC_LEGACY")) P->csc_rank_path = e[0] != '1';
   P->fused_stats = P->fused_stats_ok();
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
@@ -645,7 +649,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
                                    P->at<int>(Lt.csc_col), cs,
                                    clear && P->csc_inline ? P->at<double>(Lt.dense_sums) : nullptr,
-                                   clear && P->csc_inline ? (int)(Lt.dense_sums_bytes / 8) : 0));
+                                   clear && P->csc_inline ? (int)(Lt.dense_sums_bytes / 8) : 0,
+                                   P->csc_rank_path));
     P->probe_end(DSSM_PROBE_CSC, cs);
     if (!P->csc_inline) {
       HIP_TRY(hipEventRecord(P->ev_csc, P->side));

@@ -17,6 +17,7 @@
 // (each atomic wave-instruction covers 256 contiguous bytes); "light" columns are summed by
 // one wave each, either here (materialized dW1 for the all-reduce) or inside the fused
 // W1 Adam kernel (adam.hip), which then never writes or re-reads a dense dW1.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -320,6 +321,198 @@ __global__ __launch_bounds__(kTB) void k_csc_fill(const int* __restrict__ indptr
   }
 }
 
+// ---- three-launch transpose without re-histogramming -----------------------------------------
+// k_csc_rank (workgroups own row ranges; one per CU: the histogram fills LDS): every entry's rank
+// among the block's entries of its column comes from an LDS histogram; ONE returning global
+// atomic per distinct column of the block reserves the block's range inside the column (hot
+// Zipf columns see one atomic per block, never one per entry); each entry's position inside its
+// column (block base + rank) is stored in place of its rank.
+// k_csc_scan_multi: column pointers; every workgroup sums the counts before its chunk itself
+// (all its loads in flight at once) and scans its chunk.
+// k_csc_scatter: one wave per CSR row scatters (row, value, column) to col_ptr[c] + position, and
+// re-zeroes the counts for the next step.
+// Kernel boundaries (~1.5-2 us) are cheaper than in-kernel grid barriers on MI355X
+// (MI355X_MICROARCH.md: boundary vs barrier-xcd / barrier-counter rows).
+constexpr int kCscRankBlocks = 128;
+constexpr int kCscListMax = 4096;  // LDS list of the block's distinct columns
+__global__ __launch_bounds__(kTB) void k_csc_rank(const int* __restrict__ indptr,
+                                                  const int* __restrict__ indices, int rows, int D,
+                                                  int rows_per_block, int* __restrict__ cnt,
+                                                  int* __restrict__ pos_tmp,
+                                                  double* __restrict__ zero, int nzero) {
+  extern __shared__ int hist[];  // D bins
+  __shared__ int s_list[kCscListMax];
+  __shared__ int s_nlist;
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  // the first launch of a train step also clears the step's fused BN accumulators (bnfuse.h)
+  for (int i = blockIdx.x * kTB + t; i < nzero; i += gridDim.x * kTB) zero[i] = 0.0;
+  for (int c = t; c < D; c += kTB) hist[c] = 0;
+  if (t == 0) s_nlist = 0;
+  __syncthreads();
+  const int e0 = indptr[r0], e1 = indptr[max(r0, r1)];
+  for (int base = e0; base < e1; base += kTB * kTU) {
+    int c[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + t;
+      c[u] = e < e1 ? indices[e] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + t;
+      if (c[u] >= 0) {
+        const int r = atomicAdd(&hist[c[u]], 1);
+        pos_tmp[e] = r;
+        if (r == 0) s_list[min(atomicAdd(&s_nlist, 1), kCscListMax - 1)] = c[u];  // first touch
+      }
+    }
+  }
+  __syncthreads();
+  const int nl = s_nlist;
+  if (nl < kCscListMax) {  // every distinct column listed: all reservations in flight at once
+    for (int i0 = 0; i0 < nl; i0 += kTB * 4) {
+      int cc[4], got[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * kTB + t;
+        cc[u] = i < nl ? s_list[i] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) got[u] = cc[u] >= 0 ? atomicAdd(&cnt[cc[u]], hist[cc[u]]) : 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (cc[u] >= 0) hist[cc[u]] = got[u];
+    }
+  } else {
+    for (int base = 0; base < D; base += kTB * kTU) {
+      int v[kTU], got[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const int c = base + u * kTB + t;
+        v[u] = c < D ? hist[c] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const int c = base + u * kTB + t;
+        got[u] = v[u] ? atomicAdd(&cnt[c], v[u]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kTU; ++u) {
+        const int c = base + u * kTB + t;
+        if (v[u]) hist[c] = got[u];
+      }
+    }
+  }
+  __syncthreads();
+  for (int base = e0; base < e1; base += kTB * kTU) {  // rank -> position inside the column
+    int c[kTU], rk[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + t;
+      const bool ok = e < e1;
+      c[u] = ok ? indices[e] : 0;
+      rk[u] = ok ? pos_tmp[e] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int e = base + u * kTB + t;
+      if (e < e1) pos_tmp[e] = hist[c[u]] + rk[u];
+    }
+  }
+}
+
+// block-wide exclusive scan of one value per thread (kTB threads); returns the block total too
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wave[w] = x;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+#pragma unroll
+  for (int i = 0; i < kTB / 64; ++i) {
+    const int t = s_wave[i];
+    before += i < w ? t : 0;
+    total += t;
+  }
+  __syncthreads();
+  return before + x - v;
+}
+
+constexpr int kScanMultiCols = 4096;  // columns per scan workgroup (4 per thread)
+__global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ cnt, int D, int rows,
+                                                        int* __restrict__ col_ptr) {
+  __shared__ int s_wave[kTB / 64];
+  const int t = threadIdx.x;
+  const int ncols = D + 1;
+  const int c0 = blockIdx.x * kScanMultiCols, c1 = min(ncols, c0 + kScanMultiCols);
+  int pre = 0;  // all counts before the chunk (< D: column D is the last), 32 loads per thread
+  for (int b = 0; b < c0; b += kTB * 32) {
+    int x[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int c = b + u * kTB + t;
+      x[u] = cnt[c < c0 ? c : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) pre += (b + u * kTB + t < c0) ? x[u] : 0;
+  }
+  int tot;
+  (void)block_excl_scan(pre, s_wave, tot);
+  const int base = tot;
+  int v[4], sum = 0;
+  const int cb = c0 + t * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = cb + k;
+    v[k] = c < c1 ? (c < D ? cnt[c] : rows) : 0;
+    sum += v[k];
+  }
+  int run = base + block_excl_scan(sum, s_wave, tot);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (cb + k < c1) col_ptr[cb + k] = run;
+    run += v[k];
+  }
+  if (c1 == ncols && t == 0) col_ptr[ncols] = base + tot;
+}
+
+__global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ indptr,
+                                                     const int* __restrict__ indices,
+                                                     const float* __restrict__ values, int rows,
+                                                     int D, const int* __restrict__ col_ptr,
+                                                     const int* __restrict__ pos_tmp,
+                                                     int* __restrict__ cnt,
+                                                     int* __restrict__ csc_row,
+                                                     float* __restrict__ csc_val,
+                                                     int* __restrict__ csc_col) {
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < D; c += gridDim.x * 256) cnt[c] = 0;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = lane_id();
+  const int s = indptr[row], e = indptr[row + 1];
+  for (int k = s + lane; k < e; k += 64) {
+    const int c = indices[k];
+    const float v = values[k];
+    const int pos = col_ptr[c] + pos_tmp[k];
+    csc_row[pos] = row;
+    csc_val[pos] = v;
+    csc_col[pos] = c;
+  }
+  if (lane == 0) {
+    const int pos = col_ptr[D] + row;
+    csc_row[pos] = row;
+    csc_val[pos] = 1.0f;
+    csc_col[pos] = D;
+  }
+}
+
 // Fallback fill with per-entry global atomics (one wave per row).
 __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__ indptr,
                                                          const int* __restrict__ indices,
@@ -451,18 +644,30 @@ hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const fl
 }
 
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
-  // cnt (D+1, padded) + cursor (D+1) + rank_tmp (max_nnz)
+  // cnt (D+1, padded) + cursor (D+1) + rank / position per entry (max_nnz)
   return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64;
 }
 
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero,
-                            int nzero) {
-  int* cnt = scratch;                 // zero between steps (re-zeroed by k_csc_scan)
+                            int nzero, bool rank_path) {
+  int* cnt = scratch;  // zero between steps (re-zeroed by k_csc_scan / k_csc_scatter)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
   const size_t lds = (size_t)D * sizeof(int);
+  if (rank_path && lds + (kCscListMax + 64) * sizeof(int) <= 160 * 1024 &&
+      D + 1 <= 1024 * kScanMultiCols) {
+    const int rpb = cdiv(rows, kCscRankBlocks);
+    const int grid = cdiv(rows, rpb);
+    hipLaunchKernelGGL(k_csc_rank, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb, cnt,
+                       rank_tmp, zero, nzero);
+    hipLaunchKernelGGL(k_csc_scan_multi, dim3(cdiv(D + 1, kScanMultiCols)), dim3(kTB), 0, s, cnt, D,
+                       rows, col_ptr);
+    hipLaunchKernelGGL(k_csc_scatter, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices, values,
+                       rows, D, col_ptr, rank_tmp, cnt, csc_row, csc_val, csc_col);
+    return hipGetLastError();
+  }
   if (lds + (size_t)(cdiv(rows, max(1, min(32, cdiv(rows, 64)))) + 1) * sizeof(int) <= 156 * 1024) {
     // Few fat blocks (one CU each: the LDS histogram takes 120 KB): enough to keep the transpose
     // short while leaving most CUs to the forward pass it overlaps on the main stream.
