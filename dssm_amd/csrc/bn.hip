@@ -213,6 +213,42 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
   }
 }
 
+// Fused-statistics schedule (bnfuse.h): per-tower column sums of z and z^2 in fp64, one
+// atomic per (column, statistic) per 256-row block; no partials, no finalize (the consumer
+// derives the coefficients).
+__global__ __launch_bounds__(1024) void k_bn_sums(const float* __restrict__ Z, int ldz, int ncol,
+                                                 BnTowers tw, double* __restrict__ fsum) {
+  __shared__ double s_a[NG][64], s_b[NG][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const RowBlocks blk(tw);
+  int r0, r1, tower;
+  blk.range(tw, blockIdx.y, r0, r1, tower);
+  float x[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {  // all loads issued before any arithmetic
+    const int r = r0 + g + NG * i;
+    x[i] = Z[(size_t)(r < r1 ? r : r0) * ldz + (c < ldz ? c : 0)];
+  }
+  double s = 0.0, q = 0.0;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const float v = (r0 + g + NG * i < r1) ? x[i] : 0.f;
+    s += v;
+    q += (double)v * v;
+  }
+  s_a[g][lane] = s;
+  s_b[g][lane] = q;
+  __syncthreads();
+  if (g < 2 && c < ncol) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) a += g == 0 ? s_a[k][lane] : s_b[k][lane];
+    __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + g) * ldz + c, a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <typename TO>
 __global__ __launch_bounds__(256) void k_bn_apply(const float* __restrict__ Z, int ldz,
                                                   BnTowers tw, const float* __restrict__ coef,
@@ -514,6 +550,12 @@ hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowe
   else
     hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,
                        bcoef, (float*)dZ);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s) {
+  RowBlocks b(t);
+  hipLaunchKernelGGL(k_bn_sums, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t, fsum);
   return hipGetLastError();
 }
 

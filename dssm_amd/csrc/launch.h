@@ -19,6 +19,8 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
 // scratch: csc_scratch_ints() ints, zero on first use (kept zero between calls);
 // col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
 size_t csc_scratch_ints(int D, int rows, int max_nnz);
+// the rank transpose (default) fits: D-bin LDS histogram; it also lists the heavy columns
+bool csc_rank_supported(int D);
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
@@ -33,7 +35,8 @@ hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const fl
 // light=false: only the heavy rows are accumulated (into rows that must already be zero).
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
-                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s);
+                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s,
+                      int* csc_scratch = nullptr);  // non-null: heavy items of the rank transpose
 
 // ---- dense GEMM (gemm.hip) ----
 enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
@@ -91,6 +94,8 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* batch_mean /*[2*n] or null*/, float* batch_var,
                                float* partial, unsigned* tickets, float* coef, bool split,
                                hipStream_t s, double* zero = nullptr, int nzero = 0);
+// Fused-statistics forward sums of one layer (bnfuse.h): fsum [2 towers][2][ldz] += sum z, z^2.
+hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s);
 // Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
 // also writes b.dgamma / b.dbeta.
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,

@@ -677,24 +677,17 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     return DSSM_OK;
   }
   if (train && P->fused_stats) {
-    // BN1 statistics by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
+    // BN1 sums by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
     // stages the previous layer's BN+ReLU and accumulates its own output's sums, the cosine
     // kernel the last layer's backward sums (bnfuse.h)
-    if (!P->spmm_stats) {
-      float* ema = P->ema + Lt.ema_off[0];
-      const int n = Lt.n[0];
-      HIP_TRY(dssm::launch_bn_fwd_stats(
-          P->at<float>(Lt.Z[0]), Lt.ldp[0], n, tw, P->p + Lt.bn_off[0][0], P->p + Lt.bn_off[0][1],
-          P->p + Lt.bn_off[0][2], P->p + Lt.bn_off[0][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
-          c.bn_eps, c.ema_decay, true, P->at<float>(Lt.bmean[0]), P->at<float>(Lt.bvar[0]),
-          P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[0][0]), P->at<float>(Lt.coef[0]),
-          P->split_finalize, s));
-    }
+    if (!P->spmm_stats)
+      HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
+                                   P->at<double>(Lt.fsum[0]), s));
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
-          P->at<float>(Lt.coef[l - 1]), (l > 1 || P->spmm_stats) ? &in : nullptr, Lt.BS,
+          P->at<float>(Lt.coef[l - 1]), &in, Lt.BS,
           P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
           P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s));
     }
@@ -765,7 +758,9 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
   P->probe_begin(DSSM_PROBE_DW1, s);
   HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
                            P->at<int>(Lt.csc_col), Lt.D, Lt.R, Lt.max_nnz, P->ws + Lt.dZ[0],
-                           Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam, s));
+                           Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam, s,
+                           P->csc_rank_path && dssm::csc_rank_supported(Lt.D)
+                               ? P->at<int>(Lt.csc_scratch) : nullptr));
   P->probe_end(DSSM_PROBE_DW1, s);
   return DSSM_OK;
 }

@@ -339,7 +339,8 @@ __global__ __launch_bounds__(kTB) void k_csc_rank(const int* __restrict__ indptr
                                                   const int* __restrict__ indices, int rows, int D,
                                                   int rows_per_block, int* __restrict__ cnt,
                                                   int* __restrict__ pos_tmp,
-                                                  double* __restrict__ zero, int nzero) {
+                                                  double* __restrict__ zero, int nzero,
+                                                  int* __restrict__ heavy_n) {
   extern __shared__ int hist[];  // D bins
   __shared__ int s_list[kCscListMax];
   __shared__ int s_nlist;
@@ -349,6 +350,7 @@ __global__ __launch_bounds__(kTB) void k_csc_rank(const int* __restrict__ indptr
   for (int i = blockIdx.x * kTB + t; i < nzero; i += gridDim.x * kTB) zero[i] = 0.0;
   for (int c = t; c < D; c += kTB) hist[c] = 0;
   if (t == 0) s_nlist = 0;
+  if (blockIdx.x == 0 && t == 0) *heavy_n = 0;  // this step's heavy-item list (k_csc_scan_multi)
   __syncthreads();
   const int e0 = indptr[r0], e1 = indptr[max(r0, r1)];
   for (int base = e0; base < e1; base += kTB * kTU) {
@@ -446,9 +448,16 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
 }
 
 constexpr int kScanMultiCols = 4096;  // columns per scan workgroup (4 per thread)
+// Heavy columns (> kLightEntries entries, the ones column included) are also listed as
+// kHeavyItem-entry work items {column, item} for k_dw1_heavy_items (one returning atomic per
+// workgroup reserves its slots).
+constexpr int kHeavyItem = 256;
 __global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ cnt, int D, int rows,
-                                                        int* __restrict__ col_ptr) {
+                                                        int* __restrict__ col_ptr,
+                                                        int* __restrict__ heavy_n,
+                                                        int2* __restrict__ heavy_items) {
   __shared__ int s_wave[kTB / 64];
+  __shared__ int s_hbase;
   const int t = threadIdx.x;
   const int ncols = D + 1;
   const int c0 = blockIdx.x * kScanMultiCols, c1 = min(ncols, c0 + kScanMultiCols);
@@ -481,6 +490,21 @@ __global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ 
     run += v[k];
   }
   if (c1 == ncols && t == 0) col_ptr[ncols] = base + tot;
+  // heavy work items of this chunk
+  int hi[4], hsum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hi[k] = v[k] > kLightEntries ? cdiv(v[k], kHeavyItem) : 0;
+    hsum += hi[k];
+  }
+  int htot;
+  int hrun = block_excl_scan(hsum, s_wave, htot);
+  if (t == 0) s_hbase = htot ? atomicAdd(heavy_n, htot) : 0;
+  __syncthreads();
+  hrun += s_hbase;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (int i = 0; i < hi[k]; ++i) heavy_items[hrun++] = make_int2(cb + k, i);
 }
 
 __global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ indptr,
@@ -607,6 +631,51 @@ __global__ __launch_bounds__(256) void k_dw1_heavy(const int* __restrict__ col_p
   }
 }
 
+// Heavy columns by work items of kHeavyItem entries: 16 waves x 16 entries each (two gather
+// batches), the 16 partial rows summed through LDS; a column that is one item is STORED (no
+// atomics), longer columns add their items' rows with fp32 atomics (ones column, Zipf-hot
+// trigrams: cdiv(count, 256) atomic row-adds instead of one per 64 entries).
+constexpr int kHeavyWaves = 16, kHeavyPerWave = kHeavyItem / kHeavyWaves;
+template <typename TZ>
+__global__ __launch_bounds__(1024) void k_dw1_heavy_items(const int* __restrict__ col_ptr,
+                                                         const int* __restrict__ csc_row,
+                                                         const float* __restrict__ csc_val,
+                                                         const int* __restrict__ heavy_n,
+                                                         const int2* __restrict__ items,
+                                                         const TZ* __restrict__ dZ, int lddz, int n,
+                                                         float* __restrict__ G) {
+  __shared__ float part[kHeavyWaves][512];
+  const int wv = threadIdx.x >> 6, lane = lane_id();
+  const int nitems = *heavy_n;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int2 item = items[it];
+    const int c = item.x;
+    const int cs = col_ptr[c], ce = col_ptr[c + 1];
+    const int i0 = cs + item.y * kHeavyItem;
+    const int s = min(ce, i0 + wv * kHeavyPerWave), e = min(ce, s + kHeavyPerWave);
+    const bool single = ce - cs <= kHeavyItem;
+    for (int c0 = 0; c0 < n; c0 += 512) {
+      const int cc = c0 + lane * 8;
+      const int nvalid = n - cc;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (s < e) gather_accumulate(csc_row, csc_val, s, e, dZ, lddz, cc, nvalid, acc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) part[wv][lane * 8 + i] = acc[i];
+      __syncthreads();
+      const int m = min(512, n - c0);
+      for (int i = threadIdx.x; i < m; i += 1024) {
+        float a = 0.f;
+#pragma unroll
+        for (int w = 0; w < kHeavyWaves; ++w) a += part[w][i];
+        float* g = G + (size_t)c * n + c0 + i;
+        if (single) *g = a;
+        else atomicAdd(g, a);
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
@@ -643,9 +712,21 @@ hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const fl
   return hipGetLastError();
 }
 
+bool csc_rank_supported(int D) {
+  return (size_t)D * sizeof(int) + (kCscListMax + 64) * sizeof(int) <= 160 * 1024 &&
+         D + 1 <= 1024 * kScanMultiCols;
+}
+
+size_t csc_heavy_cap(int rows, int max_nnz) { return (size_t)(max_nnz + rows) / 32 + 64; }
+
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
-  // cnt (D+1, padded) + cursor (D+1) + rank / position per entry (max_nnz)
-  return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64;
+  // cnt (D+1, padded) + cursor (D+1) + rank / position per entry (max_nnz) + heavy-item count
+  // (64, padded) + heavy items (int2 each)
+  return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64 + 64 + 2 * csc_heavy_cap(rows, max_nnz);
+}
+
+int* csc_heavy_count(int* scratch, int D, int max_nnz) {
+  return scratch + 2 * (D + 1 + 64) + max_nnz + 64;
 }
 
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
@@ -655,15 +736,16 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
   int* cnt = scratch;  // zero between steps (re-zeroed by k_csc_scan / k_csc_scatter)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
+  int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
+  int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const size_t lds = (size_t)D * sizeof(int);
-  if (rank_path && lds + (kCscListMax + 64) * sizeof(int) <= 160 * 1024 &&
-      D + 1 <= 1024 * kScanMultiCols) {
+  if (rank_path && csc_rank_supported(D)) {
     const int rpb = cdiv(rows, kCscRankBlocks);
     const int grid = cdiv(rows, rpb);
     hipLaunchKernelGGL(k_csc_rank, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb, cnt,
-                       rank_tmp, zero, nzero);
+                       rank_tmp, zero, nzero, heavy_n);
     hipLaunchKernelGGL(k_csc_scan_multi, dim3(cdiv(D + 1, kScanMultiCols)), dim3(kTB), 0, s, cnt, D,
-                       rows, col_ptr);
+                       rows, col_ptr, heavy_n, heavy_items);
     hipLaunchKernelGGL(k_csc_scatter, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices, values,
                        rows, D, col_ptr, rank_tmp, cnt, csc_row, csc_val, csc_col);
     return hipGetLastError();
@@ -697,22 +779,35 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
 
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
-                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s) {
+                      bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s,
+                      int* scratch) {
   dim3 block(256);
   dim3 g1(cdiv(D + 1, 4));
   dim3 g2(max(1, cdiv(cdiv(max_nnz + rows, 64), 4)));
+  // heavy-item list of the rank transpose (scratch != null), else 64-entry slices
+  const int* heavy_n = scratch ? csc_heavy_count(scratch, D, max_nnz) : nullptr;
+  const int2* items = scratch ? reinterpret_cast<const int2*>(heavy_n + 64) : nullptr;
+  const int gi = 512;
   if (dz_bf16) {
     if (light)
       hipLaunchKernelGGL(k_dw1_light<u16>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
                          (const u16*)dZ, lddz, n, G);
-    hipLaunchKernelGGL(k_dw1_heavy<u16>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col, D,
-                       (const u16*)dZ, lddz, n, G);
+    if (items)
+      hipLaunchKernelGGL(k_dw1_heavy_items<u16>, dim3(gi), dim3(1024), 0, s, col_ptr, csc_row,
+                         csc_val, heavy_n, items, (const u16*)dZ, lddz, n, G);
+    else
+      hipLaunchKernelGGL(k_dw1_heavy<u16>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col, D,
+                         (const u16*)dZ, lddz, n, G);
   } else {
     if (light)
       hipLaunchKernelGGL(k_dw1_light<float>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
                          (const float*)dZ, lddz, n, G);
-    hipLaunchKernelGGL(k_dw1_heavy<float>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col,
-                       D, (const float*)dZ, lddz, n, G);
+    if (items)
+      hipLaunchKernelGGL(k_dw1_heavy_items<float>, dim3(gi), dim3(1024), 0, s, col_ptr, csc_row,
+                         csc_val, heavy_n, items, (const float*)dZ, lddz, n, G);
+    else
+      hipLaunchKernelGGL(k_dw1_heavy<float>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col,
+                         D, (const float*)dZ, lddz, n, G);
   }
   return hipGetLastError();
 }
