@@ -75,14 +75,18 @@ constexpr int kMaxFsumCopies = 8;
 template <int NPER, typename F>
 __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthreads, F&& out) {
   double s[NPER], q[NPER];
+  float gm[NPER], bt[NPER];
   int off[NPER];
 #pragma unroll
   for (int u = 0; u < NPER; ++u) {
     const int i = tid + nthreads * u;
     const int ic = i < 2 * b.ld ? i : 0;  // clamped: every load issued, unconditionally
     const int t = ic / b.ld, c = ic - t * b.ld;
+    const int cn = c < b.n ? c : 0;
     off[u] = (t * 2) * b.ld + c;
     s[u] = q[u] = 0.0;
+    gm[u] = b.gamma[t][cn];
+    bt[u] = b.beta[t][cn];
   }
 #pragma unroll
   for (int k = 0; k < kMaxFsumCopies; ++k) {
@@ -100,8 +104,17 @@ __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthr
     const int i = tid + nthreads * u;
     if (i < 2 * b.ld) {
       const int t = i / b.ld, c = i - t * b.ld;
-      float mu = 0.f, var = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
-      if (c < b.n) fs_coef_from(b, t, c, s[u], q[u], mu, var, rs, inv, sh);
+      float mu = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
+      if (c < b.n) {
+        const double N = t == 0 ? b.rows_q : b.rows_d;
+        const double m = s[u] / N;
+        const double v = q[u] / N - m * m;
+        mu = (float)m;
+        const float var = (float)(v > 0.0 ? v : 0.0);
+        rs = 1.0f / sqrtf(var + b.eps);
+        inv = rs * gm[u];
+        sh = bt[u] - mu * inv;
+      }
       out(t, c, mu, rs, inv, sh);
     }
   }

@@ -13,6 +13,8 @@
 // partial slab and k_splitk_reduce sums the slabs in fixed order (deterministic, no atomics, no
 // zero-init).  The bias gradient rides along: the A^T operand gets a virtual all-ones row at
 // m = K_in, so row K_in of the [K_in+1 x N] output (the arena's [W; b] block) is colsum(dZ).
+#include <cstdlib>
+
 #include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
@@ -253,6 +255,7 @@ struct NtFuse {
   double* out_sum;   // [2 towers][2][ldc]
   const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
+  unsigned long long* tm;  // optional phase stamps (diagnostics: DSSM_NT_TIMING=1)
 };
 
 template <bool BN_A, int FS>
@@ -454,6 +457,248 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NtParams a, NtFuse f) {
   __shared__ float sCoef[BN_A ? 4 * kNtMaxK : 1];  // [tower][inv|shift][k]
   __shared__ double sRed[FS ? 128 : 1];
   nt_body<BN_A, FS>(a, f, blockIdx.x, blockIdx.y, sA, sB, sCoef, sRed);
+}
+
+// ---- whole-K NT GEMM (K <= 352): one load round per tile -----------------------------------
+// 128 x 64 output tile per 512-thread workgroup (8 waves = 4 x 2 of 32 x 32), the tile's WHOLE K
+// panel of A (128 rows) and BT (64 rows) staged once: every global load of the tile is issued
+// before the first LDS write, so a tile costs one memory round trip instead of one per 64-deep
+// K step; the A panel is converted to bf16 (with BN+ReLU when BN_A) on the way into LDS.
+// 240 tiles at C2 (M 6144, N 300): one wave of workgroups over 256 CUs.  FS epilogues as
+// nt_body's (tiles never straddle the tower boundary: row_split % 128 == 0).
+constexpr int kWkMaxK = 352;
+constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: 128 rows x Kp/8 / 512
+__host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
+__host__ __device__ inline size_t wk_smem_bytes(int Kp) {
+  return (size_t)(128 + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4 + 4 * 64 * 2 * 8;
+}
+
+template <bool BN_A, int FS>
+__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
+  extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
+  const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc;
+  const int Kp = (K + 31) & ~31, LDK = wk_ldk(Kp);
+  u16* sA = wk_smem;                                     // [128][LDK]
+  u16* sB = sA + 128 * LDK;                              // [64][LDK]
+  float* sCoef = reinterpret_cast<float*>(sB + 64 * LDK);  // [tower][inv|shift][Kp]
+  double* sRed = reinterpret_cast<double*>(sCoef + 4 * Kp);  // [4 wm][64][2]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int bm = blockIdx.y * 128, bn = blockIdx.x * 64;
+  const int tower = bm < a.row_split ? 0 : 1;
+  unsigned long long* tm = (f.tm && t == 0 && blockIdx.x == 1 && blockIdx.y == 1) ? f.tm : nullptr;
+  int ti = 0;
+  auto stamp = [&]() {
+    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
+    ++ti;
+  };
+  stamp();
+  // ---- every global load of the tile, issued first.  A: 4 threads per row (groups t%4 + 4i),
+  // B: 8 threads per row (groups t%8 + 8i): no divisions, 128-B row segments per 4 / 8 lanes.
+  const int arow = t >> 2, ag0 = t & 3;
+  const int brow = t >> 3, bg0 = t & 7;
+  constexpr int NGA = kWkMaxG, NGB = (kWkMaxG + 1) / 2;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / 8)
+  float4 fa[NGA][2];  // fp32 A groups (BN_A)
+  uint4 ua[NGA];      // bf16 A groups
+  uint4 ub[NGB];
+  {
+    const bool rok = bm + arow < M;
+    const size_t rbase = (size_t)(rok ? bm + arow : 0) * lda;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) {
+      const int kg = (ag0 + 4 * i) * 8;
+      const size_t off = (rok && kg < lda) ? rbase + kg : 0;
+      if constexpr (BN_A) {
+        fa[i][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
+        fa[i][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
+      } else {
+        ua[i] = *reinterpret_cast<const uint4*>((const u16*)a.A + off);
+      }
+    }
+    const bool bok = bn + brow < N;
+    const size_t bbase = (size_t)(bok ? bn + brow : 0) * ldb;
+#pragma unroll
+    for (int i = 0; i < NGB; ++i) {
+      const int kg = (bg0 + 8 * i) * 8;
+      ub[i] = *reinterpret_cast<const uint4*>(a.BT + ((bok && kg < ldb) ? bbase + kg : 0));
+    }
+  }
+  float zb[2][2][4], cb[2][4];  // FS == 2: the epilogue's pre-BN values and coefficients
+  if constexpr (FS == 2) {
+    const size_t plane = (size_t)2 * ldc;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+      const size_t o = (size_t)tower * ldc + (n < N ? n : 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cb[j][q] = f.coefb[q * plane + o];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+          zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * ldc + (n < N ? n : 0)];
+        }
+    }
+  }
+  stamp();
+  // ---- BN coefficients of the A operand (from the sums or the materialised coefficients)
+  if constexpr (BN_A) {
+    if (FS == 1 && f.in_from_sums) {
+      fs_coef_stage<(2 * kWkMaxK + 511) / 512>(f.in, t, 512, [&](int tw, int k, float, float, float inv, float sh) {
+        if (k < Kp) {
+          sCoef[(tw * 2 + 0) * Kp + k] = inv;
+          sCoef[(tw * 2 + 1) * Kp + k] = sh;
+        }
+      });
+      for (int i = t; i < 2 * (Kp - lda); i += 512) {  // K pad beyond the stored width
+        const int tw = i / (Kp - lda), k = lda + i % (Kp - lda);
+        sCoef[(tw * 2 + 0) * Kp + k] = 0.f;
+        sCoef[(tw * 2 + 1) * Kp + k] = 0.f;
+      }
+      if (blockIdx.x == 0 && blockIdx.y == 0) fs_materialize_fwd(f.in);
+    } else {
+      const size_t plane = (size_t)2 * lda;
+      for (int i = t; i < 2 * Kp; i += 512) {
+        const int tw = i / Kp, k = i - tw * Kp;
+        const bool ok = k < lda;
+        sCoef[(tw * 2 + 0) * Kp + k] = ok ? a.coef[2 * plane + (size_t)tw * lda + k] : 0.f;
+        sCoef[(tw * 2 + 1) * Kp + k] = ok ? a.coef[3 * plane + (size_t)tw * lda + k] : 0.f;
+      }
+    }
+    __syncthreads();
+  }
+  stamp();
+  // ---- LDS images (bf16); out-of-range groups zeroed here, after every load was issued
+  const bool write_a = BN_A && a.a_out != nullptr && blockIdx.x == 0;
+  {
+    const bool rok = bm + arow < M;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) {
+      const int kg = (ag0 + 4 * i) * 8;
+      if (kg < Kp) {
+        const bool ok = rok && kg < lda;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (BN_A) {
+          if (ok) {
+            const float* ci = &sCoef[(tower * 2) * Kp + kg];
+            const float* ch = ci + Kp;
+            const float z[8] = {fa[i][0].x, fa[i][0].y, fa[i][0].z, fa[i][0].w,
+                                fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
+            float y[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
+            v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
+            v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
+            if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + arow) * lda + kg) = v;
+          }
+        } else {
+          v = ok ? ua[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        *reinterpret_cast<uint4*>(&sA[arow * LDK + kg]) = v;
+      }
+    }
+    const bool bok = bn + brow < N;
+#pragma unroll
+    for (int i = 0; i < NGB; ++i) {
+      const int kg = (bg0 + 8 * i) * 8;
+      if (kg < Kp)
+        *reinterpret_cast<uint4*>(&sB[brow * LDK + kg]) =
+            (bok && kg < ldb) ? ub[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __syncthreads();
+  stamp();
+  // ---- MFMA over the whole K (fragments of the next k-step read ahead of this step's MFMAs)
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const u16* pa0 = sA + (wm * 32 + (lane & 15)) * LDK + 8 * (lane >> 4);
+  const u16* pb0 = sB + (wn * 32 + (lane & 15)) * LDK + 8 * (lane >> 4);
+  bf16x8 af[2], bfr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(pa0 + i * 16 * LDK);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(pb0 + j * 16 * LDK);
+  for (int ks = 0; ks < Kp; ks += 32) {
+    bf16x8 an[2], bnx[2];
+    const int kn = ks + 32 < Kp ? ks + 32 : ks;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) an[i] = *reinterpret_cast<const bf16x8*>(pa0 + i * 16 * LDK + kn);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bnx[j] = *reinterpret_cast<const bf16x8*>(pb0 + j * 16 * LDK + kn);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = an[i];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = bnx[j];
+  }
+  if (tm) { asm volatile("s_nop 0" :: "v"(acc[0][0][0]), "v"(acc[1][1][3])); }
+  stamp();
+  // ---- epilogue
+  double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M && n < ldc) {
+          const float v = acc[i][j][r];
+          const float x = (n < N) ? (a.bias ? v + a.bias[n] : v) : 0.f;
+          a.C[(size_t)m * ldc + n] = x;
+          if constexpr (FS == 1) {
+            cs[j] += x;
+            cq[j] += (double)x * x;
+          } else if constexpr (FS == 2) {
+            const float z = zb[i][j][r];
+            const float dy = (n < N && bn_affine(z, cb[j][2], cb[j][3]) > 0.f) ? x : 0.f;
+            const float xh = (z - cb[j][0]) * cb[j][1];
+            cs[j] += dy;
+            cq[j] += (double)dy * xh;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (FS != 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16);
+      cs[j] += __shfl_xor(cs[j], 32);
+      cq[j] += __shfl_xor(cq[j], 16);
+      cq[j] += __shfl_xor(cq[j], 32);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn * 32 + j * 16 + lane;
+        sRed[(wm * 64 + c) * 2] = cs[j];
+        sRed[(wm * 64 + c) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (t < 128) {
+      const int c = t >> 1, st = t & 1, n = bn + c;
+      if (n < N) {
+        const double v = sRed[(0 * 64 + c) * 2 + st] + sRed[(1 * 64 + c) * 2 + st] +
+                         sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
+        atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
+      }
+    }
+  }
+  if (tm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+  }
 }
 
 // "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
@@ -699,7 +944,7 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s) {
+                                    double* out_sum, hipStream_t s, unsigned long long* timing) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
   dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
@@ -710,6 +955,17 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     f.in = *in_from_sums;
   }
   f.out_sum = out_sum;
+  f.tm = timing;
+  static const bool wk_on = [] {
+    const char* e = std::getenv("DSSM_NT_WHOLEK");
+    return !(e && e[0] == '0');
+  }();
+  if (wk_on && K <= kWkMaxK && (row_split % 128) == 0) {
+    const int Kp = (K + 31) & ~31;
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 128)), dim3(512),
+                       wk_smem_bytes(Kp), s, a, f);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);
   return hipGetLastError();
 }

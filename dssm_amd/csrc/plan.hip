@@ -235,6 +235,7 @@ struct dssm_plan {
   // accumulator replicas) instead of the separate statistics launch; DSSM_SPMM_STATS=1.
   // Measured slower on MI355X at C2 (the 16-row workgroups cost more than the launch saves).
   bool spmm_stats = false;
+  bool nt_timing = false;  // DSSM_NT_TIMING=1: layer-2 NT GEMM phase stamps (BUF_DENSE_TIMING row 3)
   int fsum0_copies = 1;  // DSSM_FSUM_COPIES (<= kFsum0Copies)
   hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
   hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
@@ -484,6 +485,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->fused_stats = P->fused_stats_ok();
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
+  if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
     P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
   {
@@ -689,7 +691,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS,
           P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
-          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s));
+          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s,
+          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 192 : nullptr));
     }
     const int lL = Lt.L - 1;
     const dssm::BnSide last = P->bn_side(lL);
