@@ -15,8 +15,9 @@
 // The sums are fp64 accumulations of fp32 values: the result does not depend on the atomic
 // order beyond fp64 rounding, far below the fp32 outputs' resolution.  They are zeroed by the
 // first launch of the next train step (the CSC histogram, spmm.hip).  Same-address fp64 atomics
-// serialise (measured on MI355X: ~23 ns each; tools/micro/atomics.hip), so the SpMM's 384
-// workgroups spread layer 1's sums over fcopies replicas that the consumers add up.
+// serialise (measured on MI355X: ~23 ns each; tools/micro/atomics.hip), so producers with many
+// workgroups spread their sums over fcopies / bcopies replicas (workgroup index mod copies)
+// that the consumers add up.
 #pragma once
 #include "common.h"
 
@@ -35,10 +36,13 @@ struct BnSide {
   float* bvar;
   double* fsum;     // fcopies x [2 towers][2][ld]: sum z, sum z^2 (replicas summed by consumers)
   int fcopies;
-  double* bsum;     // [2 towers][2][ld]: sum dy, sum dy*xhat
+  double* bsum;     // bcopies x [2 towers][2][ld]: sum dy, sum dy*xhat
+  int bcopies;
   float* dgamma[2];
   float* dbeta[2];
 };
+
+constexpr int kMaxSumCopies = 8;  // replicas of an accumulator (producers spread their atomics)
 
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -71,7 +75,7 @@ __device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu
 // Every thread of the workgroup derives the coefficients of items i = tid + nthreads*u
 // (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all replica loads in flight at once,
 // then calls out(tower, column, mu, rstd, inv, shift) (zeros for pad columns >= n).
-constexpr int kMaxFsumCopies = 8;
+
 template <int NPER, typename F>
 __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthreads, F&& out) {
   double s[NPER], q[NPER];
@@ -89,7 +93,7 @@ __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthr
     bt[u] = b.beta[t][cn];
   }
 #pragma unroll
-  for (int k = 0; k < kMaxFsumCopies; ++k) {
+  for (int k = 0; k < kMaxSumCopies; ++k) {
     if (k < b.fcopies) {  // uniform
       const double* base = b.fsum + (size_t)k * 4 * b.ld;
 #pragma unroll
@@ -148,18 +152,32 @@ __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
 }
 
 // Backward means of column c, tower t: m1 = mean(dy), m2 = mean(dy*xhat).
+__device__ __forceinline__ void fs_bsums(const BnSide& b, int t, int c, double& s1, double& s2) {
+  s1 = s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < kMaxSumCopies; ++k) {
+    if (k < b.bcopies) {  // uniform
+      s1 += b.bsum[(size_t)k * 4 * b.ld + (t * 2) * b.ld + c];
+      s2 += b.bsum[(size_t)k * 4 * b.ld + (t * 2 + 1) * b.ld + c];
+    }
+  }
+}
 __device__ __forceinline__ void fs_dcoef(const BnSide& b, int t, int c, float& m1, float& m2) {
   const double N = t == 0 ? b.rows_q : b.rows_d;
-  m1 = (float)(b.bsum[(t * 2) * b.ld + c] / N);
-  m2 = (float)(b.bsum[(t * 2 + 1) * b.ld + c] / N);
+  double s1, s2;
+  fs_bsums(b, t, c, s1, s2);
+  m1 = (float)(s1 / N);
+  m2 = (float)(s2 / N);
 }
 
 // dbeta = sum dy, dgamma = sum dy*xhat per tower (one workgroup).
 __device__ __forceinline__ void fs_materialize_bwd(const BnSide& b) {
   for (int i = threadIdx.x; i < 2 * b.n; i += blockDim.x) {
     const int t = i / b.n, c = i - t * b.n;
-    b.dbeta[t][c] = (float)b.bsum[(t * 2) * b.ld + c];
-    b.dgamma[t][c] = (float)b.bsum[(t * 2 + 1) * b.ld + c];
+    double s1, s2;
+    fs_bsums(b, t, c, s1, s2);
+    b.dbeta[t][c] = (float)s1;
+    b.dgamma[t][c] = (float)s2;
   }
 }
 

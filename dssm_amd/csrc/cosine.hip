@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
       double acc = 0.0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
-      atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
+      atomic_add_f64(fs.bsum + (size_t)(blockIdx.x % fs.bcopies) * 4 * ld + (size_t)st * ld + c, acc);
     }
   }
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block

@@ -252,7 +252,8 @@ struct NtParams {
 struct NtFuse {
   int in_from_sums;  // BN_A: derive the A operand's coefficients from `in`'s sums
   BnSide in;
-  double* out_sum;   // [2 towers][2][ldc]
+  double* out_sum;   // out_copies x [2 towers][2][ldc] (tile index mod out_copies)
+  int out_copies;
   const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
   unsigned long long* tm;  // optional phase stamps (diagnostics: DSSM_NT_TIMING=1)
@@ -442,8 +443,9 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
       for (int j = 0; j < 2; ++j) {
         const int c = wn * 32 + j * 16 + lane, n = bn + c;
         if (n < N) {
-          atomic_add_f64(f.out_sum + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
-          atomic_add_f64(f.out_sum + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
+          double* os = f.out_sum + (size_t)(ty % f.out_copies) * 4 * ldc;
+          atomic_add_f64(os + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
+          atomic_add_f64(os + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
         }
       }
     }
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
       if (n < N) {
         const double v = sRed[(0 * 64 + c) * 2 + st] + sRed[(1 * 64 + c) * 2 + st] +
                          sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
-        atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
+        atomic_add_f64(f.out_sum + (size_t)(blockIdx.y % f.out_copies) * 4 * ldc + (size_t)(tower * 2 + st) * ldc + n, v);
       }
     }
   }
@@ -944,7 +946,8 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s, unsigned long long* timing) {
+                                    double* out_sum, int out_copies, hipStream_t s,
+                                    unsigned long long* timing) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
   dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
@@ -955,6 +958,7 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     f.in = *in_from_sums;
   }
   f.out_sum = out_sum;
+  f.out_copies = out_copies;
   f.tm = timing;
   static const bool wk_on = [] {
     const char* e = std::getenv("DSSM_NT_WHOLEK");
@@ -972,14 +976,16 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
 
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
-                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
-                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits) {
+                           double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
+                           int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
+                           int* deferred_splits) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
   const NtParams a{M, kin, n, dZ, lddz, nullptr, row_split, W, ldw, dA, ldda, nullptr, nullptr};
   NtFuse f{};
   f.out_sum = bsum_prev;
+  f.out_copies = bsum_copies;
   f.zb = z_prev;
   f.coefb = coef_prev;
   const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 64);

@@ -68,15 +68,16 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s,
+                                    double* out_sum, int out_copies, hipStream_t s,
                                     unsigned long long* timing = nullptr);
 // Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
 // z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
 // defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
-                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
-                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits);
+                           double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
+                           int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
+                           int* deferred_splits);
 
 // ---- batch norm (bn.hip) ----
 struct BnTowers {

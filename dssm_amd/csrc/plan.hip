@@ -33,7 +33,9 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
-constexpr int kFsum0Copies = 8;     // max replicas of layer 1's fused forward sums (bnfuse.h)
+constexpr int kSumCopies = 8;   // replicas allocated per fused-statistics accumulator (bnfuse.h)
+constexpr int kNtSumCopies = 1, kPairSumCopies = 1, kCosSumCopies = 1;  // used by each producer
+constexpr int kFsum0Copies = 8;  // max replicas of layer 1's sums when the SpMM produces them
 constexpr int kDenseMaxGrid = 1024;  // workgroups of the persistent dense kernels (one per CU)
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -178,16 +180,16 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     // fp64 statistics accumulators of the fused-statistics per-op path and the dense kernels
     // (one contiguous region: zeroed as a whole)
     size_t sums = 0;
-    // layer 1's forward sums come from the SpMM's many workgroups: kFsum0Copies replicas
-    for (int l = 0; l < Lt.L; ++l) sums += ((l == 0 ? kFsum0Copies : 1) + 1) * (size_t)4 * Lt.ldp[l] * 8;
+    // kSumCopies replicas of every accumulator (producers spread same-address atomics)
+    for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
     Lt.dense_sums = take(sums);
     Lt.dense_sums_bytes = sums;
     size_t o = Lt.dense_sums;
     for (int l = 0; l < Lt.L; ++l) {
       Lt.fsum[l] = o;
-      o += (size_t)(l == 0 ? kFsum0Copies : 1) * 4 * Lt.ldp[l] * 8;
+      o += (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
       Lt.bsum[l] = o;
-      o += (size_t)4 * Lt.ldp[l] * 8;
+      o += (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
     }
   }
   if (Lt.dense_ok) {
@@ -371,10 +373,15 @@ struct dssm_plan {
     b.bmean = at<float>(Lt.bmean[l]);
     b.bvar = at<float>(Lt.bvar[l]);
     b.fsum = at<double>(Lt.fsum[l]);
-    b.fcopies = (l == 0 && spmm_stats) ? fsum0_copies : 1;
+    b.fcopies = fcopies(l);
+    b.bcopies = bcopies(l);
     b.bsum = at<double>(Lt.bsum[l]);
     return b;
   }
+  // replicas each fused accumulator is spread over, set by its producer's workgroup count
+  int fcopies(int l) const { return l == 0 ? (spmm_stats ? fsum0_copies : 1) : copies_nt; }
+  int bcopies(int l) const { return l == Lt.L - 1 ? copies_cos : copies_pair; }
+  int copies_nt = kNtSumCopies, copies_pair = kPairSumCopies, copies_cos = kCosSumCopies;
   bool fused_stats_ok() const {
     if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.dense_sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -485,6 +492,14 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->fused_stats = P->fused_stats_ok();
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
+  if (const char* e = std::getenv("DSSM_SUM_COPIES")) {  // "nt,pair,cos" (each 1..kSumCopies)
+    int a = 1, b = 1, c = 1;
+    if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
+      P->copies_nt = std::max(1, std::min(kSumCopies, a));
+      P->copies_pair = std::max(1, std::min(kSumCopies, b));
+      P->copies_cos = std::max(1, std::min(kSumCopies, c));
+    }
+  }
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
     P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
@@ -691,7 +706,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS,
           P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
-          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), s,
+          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), P->fcopies(l), s,
           (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 192 : nullptr));
     }
     const int lL = Lt.L - 1;
@@ -801,7 +816,7 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
-          Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
+          P->bcopies(l - 1), Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
           P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l]));
     }
     return dw1_backward(P, s);
