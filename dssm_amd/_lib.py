@@ -67,6 +67,7 @@ _SIGS = {
     "dssm_plan_check": (C.c_int, [_P, _P]),
     "dssm_plan_dense_enabled": (C.c_int, [_P]),
     "dssm_plan_fused_stats": (C.c_int, [_P]),
+    "dssm_plan_finalize_loss": (C.c_int, [_P, _P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),

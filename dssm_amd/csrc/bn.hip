@@ -430,7 +430,13 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
 constexpr int kApplyMaxLd = 512;
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
-                                                         u16* __restrict__ dZ) {
+                                                         u16* __restrict__ dZ,
+                                                         const float* __restrict__ loss_part,
+                                                         int loss_blocks,
+                                                         float* __restrict__ loss_out) {
+  // the step's loss / accuracy from the cosine kernel's partials (deferred finalize: no
+  // cross-workgroup ticket in the cosine launch)
+  if (loss_part && blockIdx.x == gridDim.x - 1) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
   __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
   const int ld = b.ld;
   const size_t plane = (size_t)2 * ld;
@@ -560,10 +566,12 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 }
 
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
-                                     hipStream_t s) {
+                                     hipStream_t s, const float* loss_part, int loss_blocks,
+                                     float* loss_out) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
   const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), 1024);
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid), dim3(256), 0, s, Z, dA, b, (u16*)dZ);
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid), dim3(256), 0, s, Z, dA, b, (u16*)dZ, loss_part,
+                     loss_blocks, loss_out);
   return hipGetLastError();
 }
 

@@ -100,3 +100,27 @@ __device__ __forceinline__ bool last_block_arrival(unsigned* cnt, unsigned arriv
 
 __host__ __device__ inline int ldp8(int n) { return (n + 7) & ~7; }
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Loss / accuracy of the step from the cosine kernel's per-workgroup partials: wave 0 of the
+// calling workgroup, fixed order (lane-strided partial sums, then a shuffle tree).
+__device__ __forceinline__ void loss_reduce(const float* __restrict__ part, int nblk, int bs,
+                                            float* __restrict__ loss_out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (wv == 0) {
+    float a = 0.f, b = 0.f;
+    for (int i = lane; i < nblk; i += 64) {
+      a += part[2 * i];
+      b += part[2 * i + 1];
+    }
+    // fixed-order tree over the 64 lane partials
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o);
+      b += __shfl_down(b, o);
+    }
+    if (lane == 0) {
+      loss_out[0] = a / (float)bs;
+      loss_out[1] = b / (float)bs;
+    }
+  }
+}

@@ -23,10 +23,8 @@ __device__ __forceinline__ int doc_row(int j, int k, int bs, int neg) {
   return k == 0 ? bs + j : 2 * bs + j * neg + (k - 1);
 }
 
-__device__ void loss_finalize_impl(const float* __restrict__ part, int nblk, int bs,
-                                   float* __restrict__ loss_out);
 __device__ __forceinline__ void loss_finalize(const float* part, int nblk, int bs, float* out) {
-  loss_finalize_impl(part, nblk, bs, out);
+  loss_reduce(part, nblk, bs, out);
 }
 
 // KM: register rows per query (NEG + 1 <= KM).  FSC (fused statistics, bnfuse.h): the last
@@ -248,28 +246,6 @@ __global__ __launch_bounds__(64) void k_loss_finalize(const float* __restrict__ 
   loss_finalize(part, nblk, bs, loss_out);
 }
 
-__device__ void loss_finalize_impl(const float* __restrict__ part, int nblk, int bs,
-                                   float* __restrict__ loss_out) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (wv == 0) {
-    float a = 0.f, b = 0.f;
-    for (int i = lane; i < nblk; i += 64) {
-      a += part[2 * i];
-      b += part[2 * i + 1];
-    }
-    // fixed-order tree over the 64 lane partials
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      a += __shfl_down(a, o);
-      b += __shfl_down(b, o);
-    }
-    if (lane == 0) {
-      loss_out[0] = a / (float)bs;
-      loss_out[1] = b / (float)bs;
-    }
-  }
-}
-
 }  // namespace
 
 size_t cosine_ws_floats(int bs) { return (size_t)2 * cdiv(bs, 4) + 64; }
@@ -277,7 +253,7 @@ size_t cosine_ws_floats(int bs) { return (size_t)2 * cdiv(bs, 4) + 64; }
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s, const BnSide* fused) {
+                              bool split, hipStream_t s, const BnSide* fused, bool defer_finalize) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
@@ -287,7 +263,8 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \
   hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
-                     y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy, split ? 1 : 0, fs)
+                     y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,               \
+                     (split || defer_finalize) ? 1 : 0, fs)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -299,8 +276,13 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #undef DSSM_COS
 #undef DSSM_COS2
 #undef DSSM_COS3
-  if (split)
+  if (split && !defer_finalize)
     hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, cosine_blocks(bs), bs, loss_out);
   return hipGetLastError();
 }
 

@@ -101,7 +101,8 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 // Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
 // also writes b.dgamma / b.dbeta.
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
-                                     hipStream_t s);
+                                     hipStream_t s, const float* loss_part = nullptr,
+                                     int loss_blocks = 0, float* loss_out = nullptr);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
@@ -120,7 +121,11 @@ size_t cosine_ws_floats(int bs);
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s, const BnSide* fused = nullptr);
+                              bool split, hipStream_t s, const BnSide* fused = nullptr,
+                              bool defer_finalize = false);
+// the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
+inline int cosine_blocks(int bs) { return (bs + 3) / 4; }
+hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s);
 
 // ---- optimizer (adam.hip) ----
 struct ShadowSeg {

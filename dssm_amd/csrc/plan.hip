@@ -214,6 +214,7 @@ struct dssm_plan {
   const float* values = nullptr;
   bool fwd_train_done = false;
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
+  bool loss_pending = false;  // its loss partials await the backward's first launch
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
@@ -716,9 +717,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.coef[lL]), P->at<float>(Lt.A[lL]), P->at<float>(Lt.cos_raw),
         P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
         P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
-        P->split_finalize, s, &last));
+        P->split_finalize, s, &last, /*defer_finalize=*/true));
     P->fwd_train_done = true;
     P->fwd_fused = true;
+    P->loss_pending = true;
     return DSSM_OK;
   }
   P->fwd_fused = false;
@@ -809,8 +811,12 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
     // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
+      const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
       HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
-                                              P->at<uint16_t>(Lt.dZ[l]), s));
+                                              P->at<uint16_t>(Lt.dZ[l]), s,
+                                              fin ? P->at<float>(Lt.loss_j) : nullptr,
+                                              dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss)));
+      if (fin) P->loss_pending = false;
       if (l == 0) break;
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
@@ -938,6 +944,16 @@ int dssm_plan_check(dssm_plan* P, void* stream) {
 }
 
 int dssm_plan_dense_enabled(dssm_plan* P) { return P && P->dense_on ? P->dense_grid : 0; }
+
+int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (P->loss_pending) {
+    HIP_TRY(dssm::launch_loss_finalize(P->at<float>(P->Lt.loss_j), P->Lt.BS, P->at<float>(P->Lt.loss),
+                                       (hipStream_t)stream));
+    P->loss_pending = false;
+  }
+  return DSSM_OK;
+}
 
 int dssm_plan_fused_stats(dssm_plan* P) { return P && P->fused_stats && !P->dense_on ? 1 : 0; }
 

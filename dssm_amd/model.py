@@ -282,6 +282,7 @@ class DSSM:
         return self.workspace[off:off + nb].view(dtype)
 
     def loss_accuracy(self):
+        check(self.lib.dssm_plan_finalize_loss(self._plan, stream_ptr(None)), "finalize_loss")
         la = self.buffer(_lib.BUF_LOSS).cpu().numpy()
         return float(la[0]), float(la[1])
 

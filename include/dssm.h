@@ -151,6 +151,10 @@ int dssm_plan_dense_enabled(dssm_plan* plan);
  * fused into the producing / consuming kernels (DSSM_FUSED_STATS, default on where supported:
  * bf16, query_bs % 64 == 0, widths <= 512), else 0. */
 int dssm_plan_fused_stats(dssm_plan* plan);
+/* The fused-statistics train forward leaves the loss / accuracy reduction to the backward's first
+ * launch; call this before reading DSSM_BUF_LOSS after a train forward that was not followed by
+ * dssm_plan_backward (no-op otherwise). */
+int dssm_plan_finalize_loss(dssm_plan* plan, void* stream);
 int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, float* ms);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */

@@ -155,3 +155,24 @@ def test_fused_stats_unsupported_batch_falls_back():
         os.environ.pop("DSSM_DENSE", None)
         if old is not None:
             os.environ["DSSM_DENSE"] = old
+
+
+def test_train_forward_without_backward_reports_its_loss():
+    """The fused schedule defers the loss reduction to the backward's first launch; a train
+    forward read on its own (dssm_plan_finalize_loss) must report the same loss."""
+    case = (2000, (64, 64, 32), 64, 3)
+    D, widths, BS, NEG = case
+    cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
+    p = O.init_params(cfg, seed=8)
+    batch = synth_batch(D, BS, NEG, seed=5, mean_nnz=16)
+    a, b = _model(case, True, p), _model(case, True, p)
+    a.set_batch(batch)
+    a.forward(True)
+    la = a.loss_accuracy()
+    b.set_batch(batch)
+    b.forward(True)
+    b.backward()
+    lb = b.loss_accuracy()
+    assert la == lb, (la, lb)
+    cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
+    assert abs(la[0] - cache["loss"]) <= 2e-2 * abs(cache["loss"])
