@@ -16,6 +16,7 @@
 // The affine+ReLU itself is applied by the consumers (GEMM A-operand staging, cosine kernel) or
 // by k_bn_apply / k_bn_bwd_apply where a materialized tensor is needed.
 #include <algorithm>
+#include <cstdlib>
 
 #include "bnfuse.h"
 #include "common.h"
@@ -569,7 +570,11 @@ hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSi
                                      hipStream_t s, const float* loss_part, int loss_blocks,
                                      float* loss_out) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
-  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), 1024);
+  static const int gmax = [] {
+    const char* e = std::getenv("DSSM_APPLY_GRID");
+    return e ? std::max(1, std::atoi(e)) : 1024;
+  }();
+  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), gmax);
   hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid), dim3(256), 0, s, Z, dA, b, (u16*)dZ, loss_part,
                      loss_blocks, loss_out);
   return hipGetLastError();

@@ -73,55 +73,66 @@ __device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu
 }
 
 // Every thread of the workgroup derives the coefficients of items i = tid + nthreads*u
-// (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all replica loads in flight at once,
-// then calls out(tower, column, mu, rstd, inv, shift) (zeros for pad columns >= n).
-
-template <int NPER, typename F>
-__device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthreads, F&& out) {
+// (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all replica loads in flight at once:
+// load() issues the loads (call it before a kernel's bulk loads so these return first),
+// finish() calls out(tower, column, mu, rstd, inv, shift) (zeros for pad columns >= n).
+template <int NPER>
+struct FsCoefStage {
   double s[NPER], q[NPER];
   float gm[NPER], bt[NPER];
-  int off[NPER];
+  __device__ __forceinline__ void load(const BnSide& b, int tid, int nthreads) {
+    int off[NPER];
 #pragma unroll
-  for (int u = 0; u < NPER; ++u) {
-    const int i = tid + nthreads * u;
-    const int ic = i < 2 * b.ld ? i : 0;  // clamped: every load issued, unconditionally
-    const int t = ic / b.ld, c = ic - t * b.ld;
-    const int cn = c < b.n ? c : 0;
-    off[u] = (t * 2) * b.ld + c;
-    s[u] = q[u] = 0.0;
-    gm[u] = b.gamma[t][cn];
-    bt[u] = b.beta[t][cn];
-  }
+    for (int u = 0; u < NPER; ++u) {
+      const int i = tid + nthreads * u;
+      const int ic = i < 2 * b.ld ? i : 0;  // clamped: every load issued, unconditionally
+      const int t = ic / b.ld, c = ic - t * b.ld;
+      const int cn = c < b.n ? c : 0;
+      off[u] = (t * 2) * b.ld + c;
+      s[u] = q[u] = 0.0;
+      gm[u] = b.gamma[t][cn];
+      bt[u] = b.beta[t][cn];
+    }
 #pragma unroll
-  for (int k = 0; k < kMaxSumCopies; ++k) {
-    if (k < b.fcopies) {  // uniform
-      const double* base = b.fsum + (size_t)k * 4 * b.ld;
+    for (int k = 0; k < kMaxSumCopies; ++k) {
+      if (k < b.fcopies) {  // uniform
+        const double* base = b.fsum + (size_t)k * 4 * b.ld;
 #pragma unroll
-      for (int u = 0; u < NPER; ++u) {
-        s[u] += base[off[u]];
-        q[u] += base[off[u] + b.ld];
+        for (int u = 0; u < NPER; ++u) {
+          s[u] += base[off[u]];
+          q[u] += base[off[u] + b.ld];
+        }
       }
     }
   }
+  template <typename F>
+  __device__ __forceinline__ void finish(const BnSide& b, int tid, int nthreads, F&& out) const {
 #pragma unroll
-  for (int u = 0; u < NPER; ++u) {
-    const int i = tid + nthreads * u;
-    if (i < 2 * b.ld) {
-      const int t = i / b.ld, c = i - t * b.ld;
-      float mu = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
-      if (c < b.n) {
-        const double N = t == 0 ? b.rows_q : b.rows_d;
-        const double m = s[u] / N;
-        const double v = q[u] / N - m * m;
-        mu = (float)m;
-        const float var = (float)(v > 0.0 ? v : 0.0);
-        rs = 1.0f / sqrtf(var + b.eps);
-        inv = rs * gm[u];
-        sh = bt[u] - mu * inv;
+    for (int u = 0; u < NPER; ++u) {
+      const int i = tid + nthreads * u;
+      if (i < 2 * b.ld) {
+        const int t = i / b.ld, c = i - t * b.ld;
+        float mu = 0.f, rs = 0.f, inv = 0.f, sh = 0.f;
+        if (c < b.n) {
+          const double N = t == 0 ? b.rows_q : b.rows_d;
+          const double m = s[u] / N;
+          const double v = q[u] / N - m * m;
+          mu = (float)m;
+          const float var = (float)(v > 0.0 ? v : 0.0);
+          rs = 1.0f / sqrtf(var + b.eps);
+          inv = rs * gm[u];
+          sh = bt[u] - mu * inv;
+        }
+        out(t, c, mu, rs, inv, sh);
       }
-      out(t, c, mu, rs, inv, sh);
     }
   }
+};
+template <int NPER, typename F>
+__device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthreads, F&& out) {
+  FsCoefStage<NPER> st;
+  st.load(b, tid, nthreads);
+  st.finish(b, tid, nthreads, out);
 }
 
 // Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup).

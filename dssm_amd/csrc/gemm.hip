@@ -476,8 +476,8 @@ __host__ __device__ inline size_t wk_smem_bytes(int Kp) {
 }
 
 template <bool BN_A, int FS>
-__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
-  extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
+__device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
+                                           u16* wk_smem) {
   const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc;
   const int Kp = (K + 31) & ~31, LDK = wk_ldk(Kp);
   u16* sA = wk_smem;                                     // [128][LDK]
@@ -486,15 +486,21 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
   double* sRed = reinterpret_cast<double*>(sCoef + 4 * Kp);  // [4 wm][64][2]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int bm = blockIdx.y * 128, bn = blockIdx.x * 64;
+  const int bm = ty * 128, bn = tx * 64;
   const int tower = bm < a.row_split ? 0 : 1;
-  unsigned long long* tm = (f.tm && t == 0 && blockIdx.x == 1 && blockIdx.y == 1) ? f.tm : nullptr;
+  unsigned long long* tm = (f.tm && t == 0 && tx == 1 && ty == 1) ? f.tm : nullptr;
   int ti = 0;
   auto stamp = [&]() {
     if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
     ++ti;
   };
   stamp();
+  // the A operand's BN coefficient inputs (sums, gamma, beta) first: they return ahead of the
+  // tile's bulk loads
+  constexpr int NPC = (2 * kWkMaxK + 511) / 512;
+  FsCoefStage<NPC> cst;
+  const bool from_sums = BN_A && FS == 1 && f.in_from_sums;
+  if (from_sums) cst.load(f.in, t, 512);
   // ---- every global load of the tile, issued first.  A: 4 threads per row (groups t%4 + 4i),
   // B: 8 threads per row (groups t%8 + 8i): no divisions, 128-B row segments per 4 / 8 lanes.
   const int arow = t >> 2, ag0 = t & 3;
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
   // ---- BN coefficients of the A operand (from the sums or the materialised coefficients)
   if constexpr (BN_A) {
     if (FS == 1 && f.in_from_sums) {
-      fs_coef_stage<(2 * kWkMaxK + 511) / 512>(f.in, t, 512, [&](int tw, int k, float, float, float inv, float sh) {
+      cst.finish(f.in, t, 512, [&](int tw, int k, float, float, float inv, float sh) {
         if (k < Kp) {
           sCoef[(tw * 2 + 0) * Kp + k] = inv;
           sCoef[(tw * 2 + 1) * Kp + k] = sh;
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
         sCoef[(tw * 2 + 0) * Kp + k] = 0.f;
         sCoef[(tw * 2 + 1) * Kp + k] = 0.f;
       }
-      if (blockIdx.x == 0 && blockIdx.y == 0) fs_materialize_fwd(f.in);
+      if (tx == 0 && ty == 0) fs_materialize_fwd(f.in);
     } else {
       const size_t plane = (size_t)2 * lda;
       for (int i = t; i < 2 * Kp; i += 512) {
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
   }
   stamp();
   // ---- LDS images (bf16); out-of-range groups zeroed here, after every load was issued
-  const bool write_a = BN_A && a.a_out != nullptr && blockIdx.x == 0;
+  const bool write_a = BN_A && a.a_out != nullptr && tx == 0;
   {
     const bool rok = bm + arow < M;
 #pragma unroll
@@ -693,7 +699,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
       if (n < N) {
         const double v = sRed[(0 * 64 + c) * 2 + st] + sRed[(1 * 64 + c) * 2 + st] +
                          sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
-        atomic_add_f64(f.out_sum + (size_t)(blockIdx.y % f.out_copies) * 4 * ldc + (size_t)(tower * 2 + st) * ldc + n, v);
+        atomic_add_f64(f.out_sum + (size_t)(ty % f.out_copies) * 4 * ldc + (size_t)(tower * 2 + st) * ldc + n, v);
       }
     }
   }
@@ -701,6 +707,12 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp();
   }
+}
+
+template <bool BN_A, int FS>
+__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
+  extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
+  nt_wk_body<BN_A, FS>(a, f, blockIdx.x, blockIdx.y, wk_smem);
 }
 
 // "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
@@ -835,6 +847,140 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TnParams p) {
   __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];  // [k][m]
   __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];  // [k][n]
   tn_body(p, blockIdx.x, blockIdx.y, blockIdx.z, sA, sB);
+}
+
+// ---- whole-K-chunk TN (dW) tile: 128 (m) x 64 (n) per 512-thread workgroup ------------------
+// The tile's whole chunk of kTwKc batch rows of both operands is loaded at once (one round
+// trip) and staged as it lies in memory ([k][m], [k][n]); fragments by ds_read_b64_tr_b16.
+// At C2: 16 splits of 384 rows x 15 tiles = 240 workgroups for dW2 (one per CU).
+constexpr int kTwKc = 384;
+constexpr int kTwLdA = 136, kTwLdB = 72;  // LDS row strides (u16)
+__host__ __device__ inline size_t tw_smem_bytes() { return (size_t)kTwKc * (kTwLdA + kTwLdB) * 2; }
+
+__device__ __forceinline__ bf16x8 tr_frag_s(const u16* tile, int ld, int row0, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const u16* a0 = tile + (row0 + 8 * g + q) * ld + col0 + 4 * p;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0 + 4 * ld));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, int tz, u16* smem,
+                                           unsigned long long* tmp = nullptr) {
+  const int M = p.M, N = p.N, lda = p.lda, ldb = p.ldb;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  unsigned long long* tm = (tmp && t == 0 && tx == 1 && ty == 1 && tz == 1) ? tmp : nullptr;
+  int ti = 0;
+  auto stamp = [&]() {
+    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
+    ++ti;
+  };
+  stamp();
+  const int wm = w >> 1, wn = w & 1;
+  const int bm = ty * 128, bn = tx * 64;
+  const int kbeg = tz * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int Mload = p.ones_row ? M - 1 : M;
+  u16* sA = smem;                    // [kTwKc][kTwLdA]  ([k][m])
+  u16* sB = smem + kTwKc * kTwLdA;   // [kTwKc][kTwLdB]  ([k][n])
+  // A: 16 threads per k-row (8 m each), rows (t>>4) + 32 i; B: 8 per row, rows (t>>3) + 64 i
+  const int ar = t >> 4, am = bm + (t & 15) * 8;
+  const int br = t >> 3, bnn = bn + (t & 7) * 8;
+  constexpr int NA = kTwKc / 32, NB = kTwKc / 64;
+  uint4 ra[NA], rb[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int k = kbeg + ar + 32 * i;
+    const bool ok = k < kend && am < lda;
+    ra[i] = *reinterpret_cast<const uint4*>(p.A + (ok ? (size_t)k * lda + am : 0));
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int k = kbeg + br + 64 * i;
+    const bool ok = k < kend && bnn < ldb;
+    rb[i] = *reinterpret_cast<const uint4*>(p.B + (ok ? (size_t)k * ldb + bnn : 0));
+  }
+  stamp();
+  // stage; the group holding m == Mload gets the virtual ones column, m > Mload zeros
+  const bool aedge = am + 8 > Mload;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int k = kbeg + ar + 32 * i;
+    uint4 v = (k < kend && am < lda) ? ra[i] : make_uint4(0u, 0u, 0u, 0u);
+    if (aedge) {
+      unsigned e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int m = am + q;
+        const unsigned keep = m < Mload ? ((e[q >> 1] >> (16 * (q & 1))) & 0xffffu)
+                                        : ((p.ones_row && m == Mload && k < kend) ? 0x3f80u : 0u);
+        e[q >> 1] = (e[q >> 1] & ~(0xffffu << (16 * (q & 1)))) | (keep << (16 * (q & 1)));
+      }
+      v = make_uint4(e[0], e[1], e[2], e[3]);
+    }
+    *reinterpret_cast<uint4*>(&sA[(ar + 32 * i) * kTwLdA + (t & 15) * 8]) = v;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int k = kbeg + br + 64 * i;
+    *reinterpret_cast<uint4*>(&sB[(br + 64 * i) * kTwLdB + (t & 7) * 8]) =
+        (k < kend && bnn < ldb) ? rb[i] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  stamp();
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kc = min(kTwKc, ((kend - kbeg) + 31) & ~31);
+  if (tm) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int ks = 0; ks < kc; ks += 32) {
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = tr_frag_s(sA, kTwLdA, ks, wm * 32 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = tr_frag_s(sB, kTwLdB, ks, wn * 32 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  if (tm) { asm volatile("s_nop 0" :: "v"(acc[0][0][0]), "v"(acc[1][1][3])); }
+  stamp();
+  float* out = p.C + (size_t)tz * M * p.ldc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M && n < N) out[(size_t)m * p.ldc + n] = acc[i][j][r];
+      }
+    }
+  }
+  if (tm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+  }
+}
+
+// Whole-K backward pair: the dA tiles (nt_wk_body, FS == 2) first, then the dW chunk tiles.
+__global__ __launch_bounds__(512) void k_bwd_pair_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks,
+                                                     TnParams p, int tn_x, int tn_y) {
+  extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
+  const int b = blockIdx.x;
+  if (b < nt_blocks) {
+    nt_wk_body<false, 2>(a, f, b % nt_x, b / nt_x, pw_smem);
+  } else {
+    const int r = b - nt_blocks;
+    tn_wk_body(p, r % tn_x, (r / tn_x) % tn_y, r / (tn_x * tn_y), pw_smem, f.tm ? f.tm - 128 + 64 : nullptr);
+  }
 }
 
 // One launch for the two backward GEMMs of layer l that both consume dZ_l: the dA tiles
@@ -978,7 +1124,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
                            int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits) {
+                           int* deferred_splits, unsigned long long* timing) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
@@ -986,8 +1132,36 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   NtFuse f{};
   f.out_sum = bsum_prev;
   f.out_copies = bsum_copies;
+  f.tm = timing;
   f.zb = z_prev;
   f.coefb = coef_prev;
+  static const bool wk_pair = [] {
+    const char* e = std::getenv("DSSM_PAIR_WHOLEK");
+    return !(e && e[0] == '0');
+  }();
+  if (wk_pair && n <= kWkMaxK && (row_split % 128) == 0 && lda_prev >= kin) {
+    const int Kp = (n + 31) & ~31;
+    const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 128);
+    const int Mw = kin + 1;
+    const int nsplit = cdiv(M, kTwKc);
+    const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
+    const int tn_x = cdiv(n, 64), tn_y = cdiv(Mw, 128);
+    const int tn_blocks = tn_x * tn_y * nsplit;
+    const size_t smem = std::max(wk_smem_bytes(Kp), tw_smem_bytes());
+    hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks + tn_blocks), dim3(512), smem, s, a, f, nt_x,
+                       nt_blocks, p, tn_x, tn_y);
+    *deferred_splits = 0;
+    if (nsplit > 1) {
+      if (defer) {
+        *deferred_splits = nsplit;
+      } else {
+        const int64_t cnt = (int64_t)Mw * n;
+        const int rg = (int)std::min<int64_t>((cnt / 4 + 255) / 256 + 1, 2048);
+        hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), dim3(256), 0, s, slab, nsplit, cnt, gw);
+      }
+    }
+    return hipGetLastError();
+  }
   const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 64);
   // dW_l = [A_{l-1}; 1]^T . dZ_l, split-K slabs left for the Adam step to sum
   const int Mw = kin + 1;
@@ -997,8 +1171,17 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kps};
   const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
   const int tn_blocks = tn_x * tn_y * nsplit;
-  hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
-                     nt_blocks, p, tn_x, tn_y);
+  static const bool split_pair = [] {  // diagnostics: the two GEMMs as separate launches
+    const char* e = std::getenv("DSSM_PAIR_SPLIT");
+    return e && e[0] == '1';
+  }();
+  if (split_pair) {
+    hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks), dim3(256), 0, s, a, f, nt_x, nt_blocks, p, tn_x, tn_y);
+    hipLaunchKernelGGL(k_gemm_tn, dim3(tn_x, tn_y, nsplit), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
+                       nt_blocks, p, tn_x, tn_y);
+  }
   *deferred_splits = 0;
   if (nsplit > 1) {
     if (defer) {
@@ -1013,7 +1196,8 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 }
 
 size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
-  const int splits = dw_splits(M, N, K, bf16 ? Cfg<u16>::BK : Cfg<float>::BK);
+  int splits = dw_splits(M, N, K, bf16 ? Cfg<u16>::BK : Cfg<float>::BK);
+  if (bf16) splits = std::max(splits, cdiv(K, kTwKc));  // the whole-K pair's chunk count
   return splits > 1 ? (size_t)splits * M * N : 0;
 }
 

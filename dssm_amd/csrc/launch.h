@@ -77,7 +77,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
                            int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits);
+                           int* deferred_splits, unsigned long long* timing = nullptr);
 
 // ---- batch norm (bn.hip) ----
 struct BnTowers {

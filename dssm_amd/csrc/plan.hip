@@ -823,7 +823,8 @@ int dssm_plan_backward(dssm_plan* P, void* stream) {
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
           P->bcopies(l - 1), Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
-          P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l]));
+          P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l],
+          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 128 : nullptr));
     }
     return dw1_backward(P, s);
   }

@@ -22,7 +22,7 @@ for _ in range(5):
 m.check()
 print("dense grid:", m.lib.dssm_plan_dense_enabled(m._plan))
 t = m.buffer(_lib.BUF_DENSE_TIMING, dtype=torch.int64).cpu().numpy().reshape(4, 64)
-for k, name in enumerate(("fwd", "bwd", "fwd_item0", "nt_l2_tile")):
+for k, name in enumerate(("fwd | pair_l2 tn tile", "bwd", "fwd_item0 | pair_l2 dA tile", "nt_l2_tile")):
     row = t[k]
     n = int(np.argmax(row == 0)) if np.any(row == 0) else 64
     st = row[:n].astype(np.int64)
