@@ -25,7 +25,7 @@ def _threads():
     return os.cpu_count() or 1
 
 
-def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 50):
+def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000):
     from dssm_amd.data import ZipfColumns, synth_batch  # synthetic batches only (host numpy)
     try:
         from . import cpu_c
