@@ -86,6 +86,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
   const int n = a.n;
   const int s = a.col_ptr[c], e = a.col_ptr[c + 1];
   const bool heavy = e - s > kLightEntries;
+  if (heavy && a.item_blocks) return;  // updated by the heavy-item workgroups
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
@@ -136,6 +137,80 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
   }
 }
 
+// Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
+__device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
+  for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
+    const size_t o = (size_t)c * a.n + j;
+    float P = a.p[o], M = a.m[o], V = a.v[o];
+    adam1(P, M, V, grow[j] * a.gs, alpha, a.b1c, a.b2c, a.eps);
+    a.p[o] = P;
+    a.m[o] = M;
+    a.v[o] = V;
+    if (a.shadow && c < a.D) a.shadow[(size_t)c * a.ldsh + j] = f2bf(P);
+  }
+}
+
+// Heavy W1 columns (> kLightEntries entries, the ones column included) inside the step: each
+// work item {column, k} is kHeavyItem CSC entries, 64 per wave, the 4 partial rows summed in LDS.
+// A one-item column is updated right here; a longer column's items add their rows to the
+// gradient arena with fp32 atomics and arrive on the column's ticket: the last arrival takes
+// the row with atomic exchanges (read and clear at the coherence point), updates it and
+// re-arms the ticket.
+template <typename TZ>
+__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha) {
+  __shared__ float part[4][512];
+  __shared__ float grow[512];
+  __shared__ int s_last;
+  const int wv = threadIdx.x >> 6, lane = lane_id();
+  const TZ* dZ = static_cast<const TZ*>(a.dZ);
+  const int nitems = *a.heavy_n;
+  for (int it = blockIdx.x; it < nitems; it += a.item_blocks) {
+    const int2 item = a.heavy_items[it];
+    const int c = item.x;
+    const int cs = a.col_ptr[c], ce = a.col_ptr[c + 1];
+    const int i0 = cs + item.y * kHeavyItem;
+    const int s = min(ce, i0 + wv * (kHeavyItem / 4)), e = min(ce, s + kHeavyItem / 4);
+    const int nit = (ce - cs + kHeavyItem - 1) / kHeavyItem;
+    for (int c0 = 0; c0 < a.n; c0 += 512) {
+      const int cc = c0 + lane * 8;
+      const int nvalid = a.n - cc;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (s < e) gather_accumulate(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, acc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) part[wv][lane * 8 + i] = acc[i];
+      __syncthreads();
+      const int m = min(512, a.n - c0);
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const float v = part[0][i] + part[1][i] + part[2][i] + part[3][i];
+        if (nit == 1) grow[c0 + i] = v;
+        else atomicAdd(a.g + (size_t)c * a.n + c0 + i, v);
+      }
+      __syncthreads();
+    }
+    if (nit == 1) {
+      w1_row_from(a, c, grow, alpha);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(a.heavy_ticket + c, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        s_last = t == (unsigned)nit - 1;
+        if (s_last) __hip_atomic_store(a.heavy_ticket + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_last) {
+        for (int j = threadIdx.x; j < a.n; j += blockDim.x)
+          grow[j] = __hip_atomic_exchange(a.g + (size_t)c * a.n + j, 0.f, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        w1_row_from(a, c, grow, alpha);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // The whole optimizer step in one launch: blocks [0, w1_blocks) run the fused W1 rows (grid-
 // stride over rows, one wave per row), the others stream the dense float4 range.  Every block
 // reads the beta powers at its start; the last block to finish (relaxed agent-scope tickets: it
@@ -146,11 +221,14 @@ template <typename TZ>
 __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  if ((int)blockIdx.x < a.w1_blocks) {
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c <= a.D; c += a.w1_blocks * 4)
+  if ((int)blockIdx.x < a.item_blocks) {
+    heavy_items<TZ>(a, alpha);
+  } else if ((int)blockIdx.x < a.item_blocks + a.w1_blocks) {
+    const int b = blockIdx.x - a.item_blocks;
+    for (int c = b * 4 + (threadIdx.x >> 6); c <= a.D; c += a.w1_blocks * 4)
       w1_row<TZ>(a, c, alpha);
   } else {
-    const int bi = blockIdx.x - a.w1_blocks;
+    const int bi = blockIdx.x - a.item_blocks - a.w1_blocks;
     for (int64_t i = a.d4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < a.d4_end;
          i += (int64_t)a.dense_blocks * blockDim.x) {
       float4 pp = reinterpret_cast<float4*>(a.p)[i];
@@ -247,7 +325,8 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (sep_advance) a.ticket = nullptr;
   const int64_t n4 = a.d4_end - a.d4_begin;
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
-  dim3 grid(a.w1_blocks + a.dense_blocks), block(256);
+  if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
+  dim3 grid(a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else

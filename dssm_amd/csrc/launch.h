@@ -21,6 +21,11 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
 size_t csc_scratch_ints(int D, int rows, int max_nnz);
 // the rank transpose (default) fits: D-bin LDS histogram; it also lists the heavy columns
 bool csc_rank_supported(int D);
+// heavy-column work list of the rank transpose inside its scratch: item count, items {column,
+// item} (kHeavyItem entries each), per-column tickets (D+1, zero-initialised)
+int* csc_heavy_count(int* scratch, int D, int max_nnz);
+unsigned* csc_heavy_tickets(int* scratch, int D, int rows, int max_nnz);
+constexpr int kHeavyItem = 256;
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
@@ -185,7 +190,14 @@ struct AdamStep {
   float lr, beta1, beta2, b1c, b2c, eps, gs;
   ShadowList sh;
   SlabList slabs;
+  // heavy W1 columns computed inside the step (item_blocks > 0): work items of the CSC scan
+  // (k_csc_scan_multi), per-column arrival tickets (zero-initialised, re-armed)
+  int item_blocks;
+  const int* heavy_n;
+  const int2* heavy_items;
+  unsigned* heavy_ticket;
 };
+constexpr int kAdamItemBlocks = 512;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 

@@ -383,6 +383,9 @@ struct dssm_plan {
   int fcopies(int l) const { return l == 0 ? (spmm_stats ? fsum0_copies : 1) : copies_nt; }
   int bcopies(int l) const { return l == Lt.L - 1 ? copies_cos : copies_pair; }
   int copies_nt = kNtSumCopies, copies_pair = kPairSumCopies, copies_cos = kCosSumCopies;
+  // heavy dW1 columns as work items inside the Adam launch (DSSM_HEAVY_IN_ADAM=0: own launch)
+  bool heavy_adam = true;
+  bool heavy_in_adam() const { return heavy_adam && csc_rank_path && dssm::csc_rank_supported(Lt.D); }
   bool fused_stats_ok() const {
     if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.dense_sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -493,6 +496,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->fused_stats = P->fused_stats_ok();
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
+  if (const char* e = std::getenv("DSSM_HEAVY_IN_ADAM")) P->heavy_adam = e[0] != '0';
   if (const char* e = std::getenv("DSSM_SUM_COPIES")) {  // "nt,pair,cos" (each 1..kSumCopies)
     int a = 1, b = 1, c = 1;
     if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
@@ -776,6 +780,12 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
     P->csc_pending = false;
   }
   P->probe_begin(DSSM_PROBE_DW1, s);
+  // fused single-GPU step with the rank transpose: the heavy columns are computed inside Adam
+  // (the DW1 probe then brackets no kernel)
+  if (P->fused_w1_adam && P->heavy_in_adam()) {
+    P->probe_end(DSSM_PROBE_DW1, s);
+    return DSSM_OK;
+  }
   HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
                            P->at<int>(Lt.csc_col), Lt.D, Lt.R, Lt.max_nnz, P->ws + Lt.dZ[0],
                            Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam, s,
@@ -895,6 +905,13 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     a.shadow = Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr;
     a.ldsh = Lt.ldp[0];
     a.d4_begin = rest / 4;
+    if (P->heavy_in_adam()) {
+      int* scr = P->at<int>(Lt.csc_scratch);
+      a.item_blocks = dssm::kAdamItemBlocks;
+      a.heavy_n = dssm::csc_heavy_count(scr, Lt.D, Lt.max_nnz);
+      a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
+      a.heavy_ticket = dssm::csc_heavy_tickets(scr, Lt.D, Lt.R, Lt.max_nnz);
+    }
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;

@@ -451,7 +451,6 @@ constexpr int kScanMultiCols = 4096;  // columns per scan workgroup (4 per threa
 // Heavy columns (> kLightEntries entries, the ones column included) are also listed as
 // kHeavyItem-entry work items {column, item} for k_dw1_heavy_items (one returning atomic per
 // workgroup reserves its slots).
-constexpr int kHeavyItem = 256;
 __global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ cnt, int D, int rows,
                                                         int* __restrict__ col_ptr,
                                                         int* __restrict__ heavy_n,
@@ -721,8 +720,14 @@ size_t csc_heavy_cap(int rows, int max_nnz) { return (size_t)(max_nnz + rows) / 
 
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
   // cnt (D+1, padded) + cursor (D+1) + rank / position per entry (max_nnz) + heavy-item count
-  // (64, padded) + heavy items (int2 each)
-  return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64 + 64 + 2 * csc_heavy_cap(rows, max_nnz);
+  // (64, padded) + heavy items (int2 each) + per-column heavy tickets (D+1, padded)
+  return (size_t)2 * (D + 1 + 64) + (size_t)max_nnz + 64 + 64 + 2 * csc_heavy_cap(rows, max_nnz) +
+         (D + 1 + 64);
+}
+
+unsigned* csc_heavy_tickets(int* scratch, int D, int rows, int max_nnz) {
+  return reinterpret_cast<unsigned*>(csc_heavy_count(scratch, D, max_nnz) + 64 +
+                                     2 * csc_heavy_cap(rows, max_nnz));
 }
 
 int* csc_heavy_count(int* scratch, int D, int max_nnz) {

@@ -107,7 +107,9 @@ def test_graph_probes_and_eager_interleave():
         assert m.global_step == 3
         for pid in (_lib.PROBE_SPMM_FWD, _lib.PROBE_ADAM, _lib.PROBE_DW1, _lib.PROBE_CSC):
             ms = m.graph_probe_read(g, pid)
-            assert 0.0 < ms < 50.0, (pid, ms)
+            # DW1 brackets no kernel when the heavy dW1 columns run inside the Adam launch
+            lo = 0.0 if pid == _lib.PROBE_DW1 else 1e-6
+            assert lo <= ms < 50.0, (pid, ms)
         assert np.isfinite(m.loss_accuracy()[0])
 
 
