@@ -325,7 +325,12 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (sep_advance) a.ticket = nullptr;
   const int64_t n4 = a.d4_end - a.d4_begin;
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
+  static const int item_cap = [] {
+    const char* e = std::getenv("DSSM_ADAM_ITEM_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : kAdamItemBlocks;
+  }();
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
+  else a.item_blocks = std::min(a.item_blocks, item_cap);
   dim3 grid(a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
