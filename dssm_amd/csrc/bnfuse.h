@@ -135,6 +135,42 @@ __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthr
   st.finish(b, tid, nthreads, out);
 }
 
+// Per-tower column sums of z and z^2 of one kSumsRows x 64 block (NT threads: NT/64 row groups),
+// fp64 atomics into fsum [2 towers][2][ldz]; blocks never straddle the tower boundary.
+constexpr int kSumsRows = 128;
+template <int NT>
+__device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int ldz, int ncol,
+                                              int row_split, int rows, double* __restrict__ fsum,
+                                              int bx, int by, double (*s_red)[NT / 64][64]) {
+  constexpr int NG = NT / 64, RPT = kSumsRows / NG;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = bx * 64 + lane;
+  const int r0 = by * kSumsRows, r1 = min(rows, r0 + kSumsRows);
+  const int tower = r0 < row_split ? 0 : 1;
+  float x[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {  // all loads issued before any arithmetic
+    const int r = r0 + g + NG * i;
+    x[i] = Z[(size_t)(r < r1 ? r : r0) * ldz + (c < ldz ? c : 0)];
+  }
+  double s = 0.0, q = 0.0;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const float v = (r0 + g + NG * i < r1) ? x[i] : 0.f;
+    s += v;
+    q += (double)v * v;
+  }
+  s_red[0][g][lane] = s;
+  s_red[1][g][lane] = q;
+  __syncthreads();
+  if (g < 2 && c < ncol) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) a += s_red[g][k][lane];
+    atomic_add_f64(fsum + (size_t)(tower * 2 + g) * ldz + c, a);
+  }
+}
+
 // Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup).
 __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
   const size_t plane = (size_t)2 * b.ld;

@@ -29,7 +29,16 @@ constexpr int kHeavyItem = 256;
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
-                            int nzero = 0, bool rank_path = true);
+                            int nzero = 0, bool rank_path = true, bool rank_only = false);
+// The rank transpose split across the fused-statistics forward (rank_only above first):
+// FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
+hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
+                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s);
+hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
+                               const int* indptr, const int* indices, const float* values, int rows,
+                               int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
+                               float* csc_val, int* csc_col, hipStream_t s);
 // FC1 forward (bf16 W1 shadow, ldz <= 512) + BN1 per-tower column sums into fsum (bnfuse.h).
 hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
                                  int rows, const uint16_t* W, int ldw, int n, const float* bias,

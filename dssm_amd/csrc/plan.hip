@@ -385,6 +385,13 @@ struct dssm_plan {
   int copies_nt = kNtSumCopies, copies_pair = kPairSumCopies, copies_cos = kCosSumCopies;
   // heavy dW1 columns as work items inside the Adam launch (DSSM_HEAVY_IN_ADAM=0: own launch)
   bool heavy_adam = true;
+  // rank transpose split across the fused-statistics forward (scan beside the SpMM, scatter
+  // beside BN1's sums); DSSM_MERGE_CSC=0 keeps its three launches together
+  bool merge_csc = true;
+  bool merged_csc() const {
+    return merge_csc && fused_stats && !dense_on && !spmm_stats && csc_inline && csc_rank_path &&
+           dssm::csc_rank_supported(Lt.D) && (Lt.BS % 128) == 0;
+  }
   bool heavy_in_adam() const { return heavy_adam && csc_rank_path && dssm::csc_rank_supported(Lt.D); }
   bool fused_stats_ok() const {
     if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.dense_sums_bytes) return false;
@@ -497,6 +504,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
   if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
   if (const char* e = std::getenv("DSSM_HEAVY_IN_ADAM")) P->heavy_adam = e[0] != '0';
+  if (const char* e = std::getenv("DSSM_MERGE_CSC")) P->merge_csc = e[0] != '0';
   if (const char* e = std::getenv("DSSM_SUM_COPIES")) {  // "nt,pair,cos" (each 1..kSumCopies)
     int a = 1, b = 1, c = 1;
     if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
@@ -672,7 +680,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                    P->at<int>(Lt.csc_col), cs,
                                    clear && P->csc_inline ? P->at<double>(Lt.dense_sums) : nullptr,
                                    clear && P->csc_inline ? (int)(Lt.dense_sums_bytes / 8) : 0,
-                                   P->csc_rank_path));
+                                   P->csc_rank_path, P->merged_csc()));
     P->probe_end(DSSM_PROBE_CSC, cs);
     if (!P->csc_inline) {
       HIP_TRY(hipEventRecord(P->ev_csc, P->side));
@@ -680,7 +688,12 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     }
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
-  if (train && P->fused_stats && P->spmm_stats && !P->dense_on) {
+  if (train && P->merged_csc()) {  // the SpMM rows share their launch with the column scan
+    HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
+                                   P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
+                                   P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
+                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
+  } else if (train && P->fused_stats && P->spmm_stats && !P->dense_on) {
     HIP_TRY(dssm::launch_spmm_fwd_stats(P->indptr, P->indices, P->values, Lt.R,
                                         P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
                                         P->at<float>(Lt.Z[0]), Lt.ldp[0], P->at<double>(Lt.fsum[0]),
@@ -702,7 +715,13 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     // BN1 sums by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
     // stages the previous layer's BN+ReLU and accumulates its own output's sums, the cosine
     // kernel the last layer's backward sums (bnfuse.h)
-    if (!P->spmm_stats)
+    if (P->merged_csc())  // BN1 sums beside the transpose's scatter
+      HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
+                                        P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
+                                        Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
+                                        P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
+                                        P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s));
+    else if (!P->spmm_stats)
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s));
     for (int l = 1; l < Lt.L; ++l) {

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "bnfuse.h"
 #include "common.h"
 #include "gather.h"
 #include "launch.h"
@@ -37,13 +38,13 @@ __device__ __forceinline__ void store8n(float* p, const float (&x)[8], int nvali
 namespace {
 
 template <typename TW>
-__global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr,
-                                                  const int* __restrict__ indices,
-                                                  const float* __restrict__ values, int rows,
-                                                  const TW* __restrict__ W, int ldw, int n,
-                                                  const float* __restrict__ bias,
-                                                  float* __restrict__ Z, int ldz) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
+                                          const int* __restrict__ indices,
+                                          const float* __restrict__ values, int rows,
+                                          const TW* __restrict__ W, int ldw, int n,
+                                          const float* __restrict__ bias, float* __restrict__ Z,
+                                          int ldz, int b) {
+  const int row = b * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
@@ -56,6 +57,16 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
     gather_accumulate(indices, values, s, e, W, ldw, c, nvalid, acc);
     if (c < ldz) store8(Z + (size_t)row * ldz + c, acc);
   }
+}
+
+template <typename TW>
+__global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr,
+                                                  const int* __restrict__ indices,
+                                                  const float* __restrict__ values, int rows,
+                                                  const TW* __restrict__ W, int ldw, int n,
+                                                  const float* __restrict__ bias,
+                                                  float* __restrict__ Z, int ldz) {
+  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, blockIdx.x);
 }
 
 // FC1 forward + BN1 statistics (fused-statistics schedule, bnfuse.h): 16 rows per 1024-thread
@@ -424,7 +435,8 @@ __global__ __launch_bounds__(kTB) void k_csc_rank(const int* __restrict__ indptr
   }
 }
 
-// block-wide exclusive scan of one value per thread (kTB threads); returns the block total too
+// block-wide exclusive scan of one value per thread (NT threads); returns the block total too
+template <int NT = kTB>
 __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int x = v;
@@ -438,7 +450,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_wave, int& total) {
   int before = 0;
   total = 0;
 #pragma unroll
-  for (int i = 0; i < kTB / 64; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     const int t = s_wave[i];
     before += i < w ? t : 0;
     total += t;
@@ -451,28 +463,28 @@ constexpr int kScanMultiCols = 4096;  // columns per scan workgroup (4 per threa
 // Heavy columns (> kLightEntries entries, the ones column included) are also listed as
 // kHeavyItem-entry work items {column, item} for k_dw1_heavy_items (one returning atomic per
 // workgroup reserves its slots).
-__global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ cnt, int D, int rows,
-                                                        int* __restrict__ col_ptr,
-                                                        int* __restrict__ heavy_n,
-                                                        int2* __restrict__ heavy_items) {
-  __shared__ int s_wave[kTB / 64];
-  __shared__ int s_hbase;
+template <int NT>
+__device__ __forceinline__ void scan_chunk(const int* __restrict__ cnt, int D, int rows,
+                                           int* __restrict__ col_ptr, int* __restrict__ heavy_n,
+                                           int2* __restrict__ heavy_items, int chunk, int* s_wave,
+                                           int* s_hbase) {
+  constexpr int COLS = NT * 4;
   const int t = threadIdx.x;
   const int ncols = D + 1;
-  const int c0 = blockIdx.x * kScanMultiCols, c1 = min(ncols, c0 + kScanMultiCols);
+  const int c0 = chunk * COLS, c1 = min(ncols, c0 + COLS);
   int pre = 0;  // all counts before the chunk (< D: column D is the last), 32 loads per thread
-  for (int b = 0; b < c0; b += kTB * 32) {
+  for (int b = 0; b < c0; b += NT * 32) {
     int x[32];
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
-      const int c = b + u * kTB + t;
+      const int c = b + u * NT + t;
       x[u] = cnt[c < c0 ? c : 0];
     }
 #pragma unroll
-    for (int u = 0; u < 32; ++u) pre += (b + u * kTB + t < c0) ? x[u] : 0;
+    for (int u = 0; u < 32; ++u) pre += (b + u * NT + t < c0) ? x[u] : 0;
   }
   int tot;
-  (void)block_excl_scan(pre, s_wave, tot);
+  (void)block_excl_scan<NT>(pre, s_wave, tot);
   const int base = tot;
   int v[4], sum = 0;
   const int cb = c0 + t * 4;
@@ -482,7 +494,7 @@ __global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ 
     v[k] = c < c1 ? (c < D ? cnt[c] : rows) : 0;
     sum += v[k];
   }
-  int run = base + block_excl_scan(sum, s_wave, tot);
+  int run = base + block_excl_scan<NT>(sum, s_wave, tot);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (cb + k < c1) col_ptr[cb + k] = run;
@@ -497,26 +509,34 @@ __global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ 
     hsum += hi[k];
   }
   int htot;
-  int hrun = block_excl_scan(hsum, s_wave, htot);
-  if (t == 0) s_hbase = htot ? atomicAdd(heavy_n, htot) : 0;
+  int hrun = block_excl_scan<NT>(hsum, s_wave, htot);
+  if (t == 0) *s_hbase = htot ? atomicAdd(heavy_n, htot) : 0;
   __syncthreads();
-  hrun += s_hbase;
+  hrun += *s_hbase;
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     for (int i = 0; i < hi[k]; ++i) heavy_items[hrun++] = make_int2(cb + k, i);
 }
 
-__global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ indptr,
-                                                     const int* __restrict__ indices,
-                                                     const float* __restrict__ values, int rows,
-                                                     int D, const int* __restrict__ col_ptr,
-                                                     const int* __restrict__ pos_tmp,
-                                                     int* __restrict__ cnt,
-                                                     int* __restrict__ csc_row,
-                                                     float* __restrict__ csc_val,
-                                                     int* __restrict__ csc_col) {
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < D; c += gridDim.x * 256) cnt[c] = 0;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ __launch_bounds__(kTB) void k_csc_scan_multi(const int* __restrict__ cnt, int D, int rows,
+                                                        int* __restrict__ col_ptr,
+                                                        int* __restrict__ heavy_n,
+                                                        int2* __restrict__ heavy_items) {
+  __shared__ int s_wave[kTB / 64];
+  __shared__ int s_hbase;
+  scan_chunk<kTB>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x, s_wave, &s_hbase);
+}
+
+// rows 4b .. 4b+3 of the scatter (one wave each); cnt cleared grid-stride over the nb blocks
+__device__ __forceinline__ void scatter_rows(const int* __restrict__ indptr,
+                                             const int* __restrict__ indices,
+                                             const float* __restrict__ values, int rows, int D,
+                                             const int* __restrict__ col_ptr,
+                                             const int* __restrict__ pos_tmp, int* __restrict__ cnt,
+                                             int* __restrict__ csc_row, float* __restrict__ csc_val,
+                                             int* __restrict__ csc_col, int b, int nb) {
+  for (int c = b * 256 + threadIdx.x; c < D; c += nb * 256) cnt[c] = 0;
+  const int row = b * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
@@ -534,6 +554,65 @@ __global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ ind
     csc_val[pos] = 1.0f;
     csc_col[pos] = D;
   }
+}
+
+__global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ indptr,
+                                                     const int* __restrict__ indices,
+                                                     const float* __restrict__ values, int rows,
+                                                     int D, const int* __restrict__ col_ptr,
+                                                     const int* __restrict__ pos_tmp,
+                                                     int* __restrict__ cnt,
+                                                     int* __restrict__ csc_row,
+                                                     float* __restrict__ csc_val,
+                                                     int* __restrict__ csc_col) {
+  scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val, csc_col,
+               blockIdx.x, gridDim.x);
+}
+
+// ---- independent launches sharing one grid (fused-statistics train step) -----------------------
+// k_spmm_scan: the FC1 SpMM rows beside the transpose's column scan (both depend only on
+// k_csc_rank / the batch); k_sums_scatter: BN1's column sums beside the transpose's scatter.  One
+// launch each instead of two: a kernel boundary saved, and the small scan / scatter work fills the
+// gaps of the latency-bound SpMM / sums.  The scan and sums workgroups come first.
+constexpr int kScanSmallNT = 256;
+template <typename TW>
+__global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indptr,
+                                                   const int* __restrict__ indices,
+                                                   const float* __restrict__ values, int rows,
+                                                   const TW* __restrict__ W, int ldw, int n,
+                                                   const float* __restrict__ bias,
+                                                   float* __restrict__ Z, int ldz,
+                                                   const int* __restrict__ cnt, int D,
+                                                   int* __restrict__ col_ptr,
+                                                   int* __restrict__ heavy_n,
+                                                   int2* __restrict__ heavy_items, int nscan) {
+  __shared__ int s_wave[kScanSmallNT / 64];
+  __shared__ int s_hbase;
+  if ((int)blockIdx.x < nscan)
+    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x, s_wave, &s_hbase);
+  else
+    spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, blockIdx.x - nscan);
+}
+
+__global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ Z, int ldz, int ncol,
+                                                      int row_split, double* __restrict__ fsum,
+                                                      int nsum_x, int nsum,
+                                                      const int* __restrict__ indptr,
+                                                      const int* __restrict__ indices,
+                                                      const float* __restrict__ values, int rows,
+                                                      int D, const int* __restrict__ col_ptr,
+                                                      const int* __restrict__ pos_tmp,
+                                                      int* __restrict__ cnt,
+                                                      int* __restrict__ csc_row,
+                                                      float* __restrict__ csc_val,
+                                                      int* __restrict__ csc_col) {
+  __shared__ double s_red[2][4][64];
+  const int b = blockIdx.x;
+  if (b < nsum)
+    bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red);
+  else
+    scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val,
+                 csc_col, b - nsum, (int)gridDim.x - nsum);
 }
 
 // Fallback fill with per-entry global atomics (one wave per row).
@@ -716,6 +795,34 @@ bool csc_rank_supported(int D) {
          D + 1 <= 1024 * kScanMultiCols;
 }
 
+hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
+                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s) {
+  int* cnt = scratch;
+  int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
+  int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
+  const int nscan = cdiv(D + 1, kScanSmallNT * 4);
+  hipLaunchKernelGGL(k_spmm_scan<u16>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
+                     values, rows, (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
+                     heavy_items, nscan);
+  return hipGetLastError();
+}
+
+hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
+                               const int* indptr, const int* indices, const float* values, int rows,
+                               int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
+                               float* csc_val, int* csc_col, hipStream_t s) {
+  (void)max_nnz;
+  if (row_split % kSumsRows) return hipErrorInvalidValue;
+  int* cnt = scratch;
+  int* pos_tmp = scratch + 2 * (D + 1 + 64);
+  const int nsum_x = cdiv(ldz, 64), nsum = nsum_x * cdiv(rows, kSumsRows);
+  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + cdiv(rows, 4)), dim3(256), 0, s, Z, ldz, n, row_split,
+                     fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
+                     csc_row, csc_val, csc_col);
+  return hipGetLastError();
+}
+
 size_t csc_heavy_cap(int rows, int max_nnz) { return (size_t)(max_nnz + rows) / 32 + 64; }
 
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
@@ -737,7 +844,7 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero,
-                            int nzero, bool rank_path) {
+                            int nzero, bool rank_path, bool rank_only) {
   int* cnt = scratch;  // zero between steps (re-zeroed by k_csc_scan / k_csc_scatter)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
@@ -749,6 +856,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     const int grid = cdiv(rows, rpb);
     hipLaunchKernelGGL(k_csc_rank, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb, cnt,
                        rank_tmp, zero, nzero, heavy_n);
+    if (rank_only) return hipGetLastError();  // scan and scatter ride in later launches
     hipLaunchKernelGGL(k_csc_scan_multi, dim3(cdiv(D + 1, kScanMultiCols)), dim3(kTB), 0, s, cnt, D,
                        rows, col_ptr, heavy_n, heavy_items);
     hipLaunchKernelGGL(k_csc_scatter, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices, values,
