@@ -441,29 +441,57 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
   const int ld = b.ld;
   const size_t plane = (size_t)2 * ld;
-  for (int i = threadIdx.x; i < 2 * ld; i += 256) {
-    const int t = i / ld, c = i - t * ld;
-    const size_t o = (size_t)t * ld + c;
-    float m1 = 0.f, m2 = 0.f;
-    if (c < b.n) fs_dcoef(b, t, c, m1, m2);
-    sc[t][0][c] = b.coef[o];
-    sc[t][1][c] = b.coef[plane + o];
-    sc[t][2][c] = b.coef[2 * plane + o];
-    sc[t][3][c] = b.coef[3 * plane + o];
-    sc[t][4][c] = m1;
-    sc[t][5][c] = m2;
-  }
-  if (blockIdx.x == 0) fs_materialize_bwd(b);
-  __syncthreads();
   const int q = ld >> 2;
   const int rows = b.rows_q + b.rows_d;
   const size_t total = (size_t)rows * q;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+  // the first grid-stride element's loads go out before the coefficient prologue
+  const size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), da0 = z0;
+  if (i0 < total) {
+    const int r = (int)(i0 / q);
+    const int c = (int)(i0 - (size_t)r * q) * 4;
+    z0 = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
+    da0 = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+  }
+  {  // coefficients of all 2*ld (tower, column) items: every load in flight at once
+    constexpr int NPER = 2 * kApplyMaxLd / 256;
+    float cf[NPER][4];
+    double s1[NPER], s2[NPER];
+#pragma unroll
+    for (int u = 0; u < NPER; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int ic = i < 2 * ld ? i : 0;
+      const int t = ic / ld, c = ic - t * ld;
+      const size_t o = (size_t)t * ld + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cf[u][k] = b.coef[k * plane + o];
+      fs_bsums(b, t, c < b.n ? c : 0, s1[u], s2[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NPER; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < 2 * ld) {
+        const int t = i / ld, c = i - t * ld;
+        const double N = t == 0 ? b.rows_q : b.rows_d;
+        const bool ok = c < b.n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sc[t][k][c] = cf[u][k];
+        sc[t][4][c] = ok ? (float)(s1[u] / N) : 0.f;
+        sc[t][5][c] = ok ? (float)(s2[u] / N) : 0.f;
+      }
+    }
+  }
+  if (blockIdx.x == 0) fs_materialize_bwd(b);
+  __syncthreads();
+  for (size_t i = i0; i < total; i += (size_t)gridDim.x * 256) {
     const int r = (int)(i / q);
     const int c = (int)(i - (size_t)r * q) * 4;
     const int t = r < b.rows_q ? 0 : 1;
-    const float4 z = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
-    const float4 da = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+    float4 z = z0, da = da0;
+    if (i != i0) {
+      z = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
+      da = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+    }
     const float zz[4] = {z.x, z.y, z.z, z.w}, dd[4] = {da.x, da.y, da.z, da.w};
     float out[4];
 #pragma unroll

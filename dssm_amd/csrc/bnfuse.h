@@ -171,30 +171,47 @@ __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int l
   }
 }
 
-// Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup).
+// Materialise layer b's forward coefficients, batch moments and EMA update (one workgroup; its
+// sums, gamma/beta and EMA loads all in flight at once).
 __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
+  constexpr int NPER = 4;  // 2 * 512 (max ld) / 256 threads; larger workgroups loop
   const size_t plane = (size_t)2 * b.ld;
-  for (int i = threadIdx.x; i < 2 * b.ld; i += blockDim.x) {
-    const int t = i / b.ld, c = i - t * b.ld;
-    const size_t o = (size_t)t * b.ld + c;
-    if (c >= b.n) {
-      b.coef[o] = 0.f; b.coef[plane + o] = 0.f; b.coef[2 * plane + o] = 0.f; b.coef[3 * plane + o] = 0.f;
-      continue;
+  for (int base = 0; base < 2 * b.ld; base += NPER * (int)blockDim.x) {
+    FsCoefStage<NPER> st;
+    st.load(b, base + threadIdx.x, blockDim.x);
+    float em[NPER], ev[NPER];
+#pragma unroll
+    for (int u = 0; u < NPER; ++u) {
+      const int i = base + threadIdx.x + blockDim.x * u;
+      const int ic = i < 2 * b.ld ? i : 0;
+      const int t = ic / b.ld, c = ic - t * b.ld;
+      const int cn = c < b.n ? c : 0;
+      em[u] = b.ema_mean[t][cn];
+      ev[u] = b.ema_var[t][cn];
     }
-    float mu, var, rstd, inv, shift;
-    fs_coef(b, t, c, mu, var, rstd, inv, shift);
-    b.coef[o] = mu;
-    b.coef[plane + o] = rstd;
-    b.coef[2 * plane + o] = inv;
-    b.coef[3 * plane + o] = shift;
-    b.bmean[t * b.n + c] = mu;
-    b.bvar[t * b.n + c] = var;
-    // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
-    const float one_m = 1.0f - b.decay;
-    float* em = b.ema_mean[t];
-    float* ev = b.ema_var[t];
-    em[c] = em[c] - (em[c] - mu) * one_m;
-    ev[c] = ev[c] - (ev[c] - var) * one_m;
+    int u = 0;
+    st.finish(b, base + threadIdx.x, blockDim.x,
+              [&](int t, int c, float mu, float rstd, float inv, float shift) {
+      const size_t o = (size_t)t * b.ld + c;
+      b.coef[o] = mu;
+      b.coef[plane + o] = rstd;
+      b.coef[2 * plane + o] = inv;
+      b.coef[3 * plane + o] = shift;
+      if (c < b.n) {
+        // biased batch variance back from rstd would lose bits: recompute it from the sums
+        const double N = t == 0 ? b.rows_q : b.rows_d;
+        const double m = st.s[u] / N;
+        const double v = st.q[u] / N - m * m;
+        const float var = (float)(v > 0.0 ? v : 0.0);
+        b.bmean[t * b.n + c] = mu;
+        b.bvar[t * b.n + c] = var;
+        // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
+        const float one_m = 1.0f - b.decay;
+        b.ema_mean[t][c] = em[u] - (em[u] - mu) * one_m;
+        b.ema_var[t][c] = ev[u] - (ev[u] - var) * one_m;
+      }
+      ++u;
+    });
   }
 }
 

@@ -38,7 +38,14 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int split, BnSide fs) {
+    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp) {
+  unsigned long long* tm = (tmp && threadIdx.x == 0 && blockIdx.x == 1) ? tmp : nullptr;
+  int ti = 0;
+  auto stamp = [&]() {
+    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
+    ++ti;
+  };
+  stamp();
   __shared__ float s_part[2][4];
   __shared__ int s_flag;
   __shared__ float s_co[FSC ? 2 * 4 * kCosMaxN : 1];     // [tower][mu|rstd|inv|shift][c]
@@ -59,6 +66,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     if (blockIdx.x == 0) fs_materialize_fwd(fs);
     __syncthreads();
   }
+  stamp();
   float lj = 0.f, cj = 0.f;
   float bq1[EPL], bq2[EPL], bd1[EPL], bd2[EPL];  // FSC: this wave's backward sums per column
 #pragma unroll
@@ -78,6 +86,8 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
         const int c = lane + 64 * e;
         d[k][e] = (k < K && c < n) ? z[(size_t)doc_row(j, k, bs, neg) * ld + c] : 0.f;
       }
+    if (tm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
     if constexpr (FSC) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
@@ -114,27 +124,36 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
         }
       }
     }
-    float qq = 0.f;
+    // all 1 + 2*KM lane partials first, then one interleaved butterfly (same order per value as
+    // wave_sum: the shuffles of the independent sums overlap instead of chaining)
+    float red[1 + 2 * KM];
+    red[0] = 0.f;
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) qq = __fmaf_rn(q[e], q[e], qq);
-    qq = wave_sum(qq);
-    const float qn = sqrtf(qq);
+    for (int e = 0; e < EPL; ++e) red[0] = __fmaf_rn(q[e], q[e], red[0]);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      float dd = 0.f, qd = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        dd = __fmaf_rn(d[k][e], d[k][e], dd);
+        qd = __fmaf_rn(q[e], d[k][e], qd);
+      }
+      red[1 + 2 * k] = dd;
+      red[2 + 2 * k] = qd;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int i = 0; i < 1 + 2 * KM; ++i) red[i] += __shfl_xor(red[i], o);
+    const float qn = sqrtf(red[0]);
     float cs[KM], dn[KM];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       cs[k] = 0.f;
       dn[k] = 1.f;
       if (k < K) {
-        float dd = 0.f, qd = 0.f;
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          dd = __fmaf_rn(d[k][e], d[k][e], dd);
-          qd = __fmaf_rn(q[e], d[k][e], qd);
-        }
-        dd = wave_sum(dd);
-        qd = wave_sum(qd);
-        dn[k] = sqrtf(dd);
-        cs[k] = qd / (qn * dn[k]);  // truediv(prod, query_norm*doc_norm); NaN on a zero row, as TF
+        dn[k] = sqrtf(red[1 + 2 * k]);
+        cs[k] = red[2 + 2 * k] / (qn * dn[k]);  // truediv(prod, query_norm*doc_norm); NaN on a zero row, as TF
       }
     }
     // softmax over the K scaled scores (tf.nn.softmax: exp(x - max) / sum)
@@ -166,6 +185,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     if (lane == 0) qnorm[j] = qn;
     lj = -logf(p[0]);
     cj = (amax == 0) ? 1.f : 0.f;
+    stamp();
     // ---- backward: d loss / d cos_sim[j,k] = (p_k - [k==0]) / BS
     float dq[EPL];
 #pragma unroll
@@ -226,6 +246,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
       atomic_add_f64(fs.bsum + (size_t)(blockIdx.x % fs.bcopies) * 4 * ld + (size_t)st * ld + c, acc);
     }
   }
+  stamp();
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block
   if (lane == 0) {
     s_part[0][wv] = lj;
@@ -235,6 +256,10 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = s_part[0][0] + s_part[0][1] + s_part[0][2] + s_part[0][3];
     part[2 * blockIdx.x + 1] = s_part[1][0] + s_part[1][1] + s_part[1][2] + s_part[1][3];
+  }
+  if (tm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
   }
   if (split) return;  // k_loss_finalize sums the partials in its own launch
   if (!last_block_arrival(ticket, gridDim.x, &s_flag)) return;
@@ -253,7 +278,8 @@ size_t cosine_ws_floats(int bs) { return (size_t)2 * cdiv(bs, 4) + 64; }
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s, const BnSide* fused, bool defer_finalize) {
+                              bool split, hipStream_t s, const BnSide* fused, bool defer_finalize,
+                              unsigned long long* timing) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
@@ -264,7 +290,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #define DSSM_COS3(E, KM, F)                                                                     \
   hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
                      y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,               \
-                     (split || defer_finalize) ? 1 : 0, fs)
+                     (split || defer_finalize) ? 1 : 0, fs, timing)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \

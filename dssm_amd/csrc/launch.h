@@ -136,7 +136,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               bool split, hipStream_t s, const BnSide* fused = nullptr,
-                              bool defer_finalize = false);
+                              bool defer_finalize = false, unsigned long long* timing = nullptr);
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 inline int cosine_blocks(int bs) { return (bs + 3) / 4; }
 hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s);

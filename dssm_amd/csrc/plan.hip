@@ -740,7 +740,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.coef[lL]), P->at<float>(Lt.A[lL]), P->at<float>(Lt.cos_raw),
         P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
         P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
-        P->split_finalize, s, &last, /*defer_finalize=*/true));
+        P->split_finalize, s, &last, /*defer_finalize=*/true,
+        P->nt_timing ? P->at<unsigned long long>(Lt.dense_timing) : nullptr));
     P->fwd_train_done = true;
     P->fwd_fused = true;
     P->loss_pending = true;
