@@ -41,6 +41,11 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--allreduce", default="torch", choices=["torch", "rccl"])
+    ap.add_argument("--dp-mode", default="auto", choices=["auto", "zero", "allreduce"],
+                    help="N>1 exchange: zero = reduce-scatter + sharded Adam + all-gather "
+                         "(default with torch.distributed), allreduce = all-reduce + replicated Adam")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend (gloo: functional rehearsal of N>1 on one GPU)")
     ap.add_argument("--graph", type=int, default=1, help="replay hipGraph-captured steps (0: eager launches)")
     ap.add_argument("--probes", type=int, default=1, help="HIP-event kernel probes in the timed region")
     return ap.parse_args()
@@ -94,22 +99,25 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    local = local % max(1, torch.cuda.device_count()) if args.backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from dssm_amd import _lib
     from dssm_amd.model import DSSM
     from dssm_amd.data import ZipfColumns, synth_batch
 
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
+    dp = None
     if world > 1:
-        model.set_fused_w1_adam(False)  # all-reduce needs the materialized dW1
-    comm = None
-    if world > 1 and args.allreduce == "rccl":
-        from dssm_amd.dist import RcclComm
-        comm = RcclComm(rank, world)
+        from dssm_amd.dist import DataParallel
+        dp = DataParallel(model, comm="rccl" if args.allreduce == "rccl" else "torch",
+                          mode="allreduce" if args.allreduce == "rccl" else args.dp_mode)
 
     cols = ZipfColumns(D)
     staged = []
@@ -126,11 +134,6 @@ def main():
     probe_ids = (("spmm_fwd", _lib.PROBE_SPMM_FWD), ("adam", _lib.PROBE_ADAM),
                  ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC))
 
-    def allreduce():
-        if comm is not None:
-            comm.allreduce_(model.grads)
-        else:
-            dist.all_reduce(model.grads)
 
     if args.graph:
         # One captured step per staged batch (the batch pointers are baked into the graph); with
@@ -147,12 +150,16 @@ def main():
             else:
                 graphs.append(model.graph_build(probes=pr))
         adam_graph = model.graph_build(_lib.GRAPH_ADAM, 1.0 / world, probes=bool(args.probes)) if world > 1 else None
+        shadow_graph = model.graph_build(_lib.GRAPH_SHADOWS) if (dp is not None and dp.mode == "zero") else None
 
         def step(i):
             model.graph_launch(graphs[i % len(graphs)])
             if world > 1:
-                allreduce()
+                dp.exchange_before_adam()
                 model.graph_launch(adam_graph)
+                if shadow_graph is not None:
+                    dp.exchange_after_adam()
+                    model.graph_launch(shadow_graph)
     else:
         def step(i):
             ip, ix, vv = staged[i % len(staged)]
@@ -160,8 +167,11 @@ def main():
             model.forward(True)
             model.backward()
             if world > 1:
-                allreduce()
+                dp.exchange_before_adam()
             model.apply_adam(1.0 / world)
+            if dp is not None and dp.mode == "zero":
+                dp.exchange_after_adam()
+                model.sync_shadows()
 
     for i in range(args.warmup):
         step(i)
@@ -201,7 +211,7 @@ def main():
     rows = BS * (2 + NEG)
     nnz_avg = int(nnzs[0] if args.graph else np.mean( [nnzs[(args.warmup + i) % len(nnzs)] for i in range(args.steps)]))
     s_w = 2 if args.dtype == "bf16" else 4
-    n_params = int(model.params.numel())
+    n_params = int(model.n_params)
     shadow = sum((D if l == 0 else WIDTHS[l - 1]) * WIDTHS[l] for l in range(len(WIDTHS))) if args.dtype == "bf16" else 0
     kern = {
         "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
@@ -226,7 +236,8 @@ def main():
                                "Zipf(1.1) trigram batches ~32 nnz/row, fwd+bwd+dense Adam",
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
-                   "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager"},
+                   "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
+                   "dp_exchange": dp.mode if dp is not None else None},
         "roofline": dict(rl[dominant], kernel=dominant),
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,
@@ -239,8 +250,8 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if comm is not None:
-        comm.destroy()
+    if dp is not None and dp.comm is not None:
+        dp.comm.destroy()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -19,7 +19,7 @@ DSSM_F32, DSSM_BF16 = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
  BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING) = range(11)
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
-GRAPH_FWD_BWD, GRAPH_ADAM = 1, 2
+GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS = 1, 2, 4
 
 
 class DssmError(RuntimeError):
@@ -67,6 +67,7 @@ _SIGS = {
     "dssm_plan_check": (C.c_int, [_P, _P]),
     "dssm_plan_dense_enabled": (C.c_int, [_P]),
     "dssm_plan_fused_stats": (C.c_int, [_P]),
+    "dssm_plan_set_adam_range": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "dssm_plan_finalize_loss": (C.c_int, [_P, _P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),

@@ -213,6 +213,7 @@ struct dssm_plan {
   const int32_t* indices = nullptr;
   const float* values = nullptr;
   bool fwd_train_done = false;
+  int64_t adam_begin = 0, adam_end = -1;  // sharded optimizer range (dssm_plan_set_adam_range)
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
@@ -911,7 +912,10 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   a.eps = c.adam_eps;
   a.gs = grad_scale;
   a.clear_from = Lt.total;
-  a.d4_end = Lt.total / 4;
+  a.d4_begin = P->adam_begin / 4;
+  a.d4_end = (P->adam_end >= 0 ? P->adam_end : Lt.total) / 4;
+  if (P->fused_w1_adam && (P->adam_begin != 0 || (P->adam_end >= 0 && P->adam_end != Lt.total)))
+    return fail(DSSM_E_INVALID, "a sharded Adam range needs the fused W1 Adam off");
   if (P->fused_w1_adam) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
     a.w1_blocks = 1;  // sized by the launcher
@@ -950,6 +954,17 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
   P->probe_end(DSSM_PROBE_ADAM, s);
   P->grads_clean = true;
+  return DSSM_OK;
+}
+
+int dssm_plan_set_adam_range(dssm_plan* P, int64_t begin, int64_t end) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  const int64_t total = P->Lt.total;
+  if (begin < 0 || end < begin || end > total || (begin % 4) || (end % 4 && end != total))
+    return fail(DSSM_E_INVALID, "adam range must be 4-aligned within [0, param_count]");
+  if ((end % 4) && end == total) return fail(DSSM_E_INVALID, "param_count is a multiple of 64");
+  P->adam_begin = begin;
+  P->adam_end = end;
   return DSSM_OK;
 }
 
@@ -1019,8 +1034,9 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
                           int* graph_id) {
   if (!P || !graph_id) return fail(DSSM_E_INVALID, "null argument");
   if (!stream) return fail(DSSM_E_INVALID, "graph capture needs a non-default stream");
-  if (!(parts & (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM)))
-    return fail(DSSM_E_INVALID, "graph parts must include DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM");
+  if (!(parts & (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS)) ||
+      (parts & ~(DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS)))
+    return fail(DSSM_E_INVALID, "graph parts: DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS");
   if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
   if (P->fused_w1_adam && parts != (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM))
     return fail(DSSM_E_INVALID, "with the fused W1 Adam a graph must hold the whole step");
@@ -1049,6 +1065,7 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
     if (!rc) rc = dssm_plan_backward(P, stream);
   }
   if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
+  if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();
   hipGraph_t graph = nullptr;

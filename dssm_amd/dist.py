@@ -1,5 +1,12 @@
-"""Data parallelism: one process per GPU, batch sharded by query, one all-reduce of
-the flat gradient arena per step (RCCL over xGMI), replicated Adam with grad_scale = 1/world.
+"""Data parallelism: one process per GPU, batch sharded by query.
+
+Two exchange schedules over the flat fp32 arenas (RCCL over xGMI):
+* "zero" (default for world sizes 2, 4, 8): reduce-scatter of the gradient arena, Adam on the
+  rank's shard only (p, m, v of the shard; grad_scale = 1/world), all-gather of the updated
+  parameters, then the bf16 weight shadows refreshed from them.  Same bytes on the links as one
+  all-reduce, but the optimizer pass (the largest kernel, HBM-bound) shrinks by the world size.
+  m / v live sharded: gather_state() collects them for a checkpoint.
+* "allreduce": one all-reduce of the gradient arena and replicated Adam.
 
 BN statistics stay per replica (unsynced), which is the reference's BN semantics applied to a
 replica's shard; EMA shadows stay rank-local and rank 0's are the ones checkpointed.
@@ -41,17 +48,34 @@ class RcclComm:
         self.lib.dssm_comm_destroy()
 
 
-class DataParallel:
-    """Wraps a DSSM model: step(batch) = forward + backward + all-reduce + Adam(1/world)."""
+def shard_bounds(n_pad: int, n: int, rank: int, world: int):
+    """Rank's optimizer shard of an arena of n elements padded to n_pad (equal shards)."""
+    s = n_pad // world
+    return rank * s, min((rank + 1) * s, n), s
 
-    def __init__(self, model, comm: str = "torch"):
+
+class DataParallel:
+    """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
+
+    def __init__(self, model, comm: str = "torch", mode: str = "auto"):
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.comm = RcclComm(self.rank, self.world) if (comm == "rccl" and self.world > 1) else None
+        npad = model.params.numel()
+        if mode == "auto":
+            mode = "zero" if (self.world > 1 and self.comm is None and npad % (64 * self.world) == 0) else "allreduce"
+        if mode == "zero" and (self.comm is not None or npad % (64 * self.world)):
+            raise ValueError("the zero schedule needs torch.distributed and 64-float aligned equal shards")
+        self.mode = mode if self.world > 1 else "allreduce"
+        self._nccl = dist.is_initialized() and dist.get_backend() == "nccl"
         if self.world > 1:
-            model.set_fused_w1_adam(False)  # the all-reduce needs the materialized dW1
+            model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
+        if self.mode == "zero":
+            self.begin, self.end, self.shard = shard_bounds(npad, model.n_params, self.rank, self.world)
+            model.set_adam_range(self.begin, max(self.begin, self.end))
 
+    # ---- collectives ----------------------------------------------------------------------
     def allreduce_grads(self):
         if self.world == 1:
             return
@@ -60,8 +84,57 @@ class DataParallel:
         else:
             dist.all_reduce(self.model.grads)
 
+    def reduce_scatter_grads(self):
+        """Sum of the gradient arenas, the rank's shard landing in place in its own arena."""
+        g = self.model.grads
+        mine = g[self.rank * self.shard:(self.rank + 1) * self.shard]
+        if self._nccl:
+            dist.reduce_scatter_tensor(mine, g)  # in place: output == input + rank * count
+        else:
+            dist.all_reduce(g)  # gloo: the shard of the full sum is the same bytes
+
+    def all_gather_params(self):
+        p = self.model.params
+        mine = p[self.rank * self.shard:(self.rank + 1) * self.shard]
+        if self._nccl:
+            dist.all_gather_into_tensor(p, mine)  # in place: input == output + rank * count
+        else:
+            parts = list(p.view(self.world, self.shard).unbind(0))
+            got = [torch.empty_like(x) for x in parts]
+            dist.all_gather(got, mine.clone())
+            for dst, src in zip(parts, got):
+                dst.copy_(src)
+
+    def exchange_before_adam(self):
+        if self.mode == "zero":
+            self.reduce_scatter_grads()
+        else:
+            self.allreduce_grads()
+
+    def exchange_after_adam(self):
+        if self.mode == "zero":
+            self.all_gather_params()
+
+    def gather_state(self):
+        """Full Adam m / v on every rank (the zero schedule keeps them sharded): before a checkpoint."""
+        if self.mode != "zero":
+            return
+        for t in (self.model.adam_m, self.model.adam_v):
+            mine = t[self.rank * self.shard:(self.rank + 1) * self.shard]
+            if self._nccl:
+                dist.all_gather_into_tensor(t, mine)
+            else:
+                parts = list(t.view(self.world, self.shard).unbind(0))
+                got = [torch.empty_like(x) for x in parts]
+                dist.all_gather(got, mine.clone())
+                for dst, src in zip(parts, got):
+                    dst.copy_(src)
+
     def train_step(self):
         self.model.forward(True)
         self.model.backward()
-        self.allreduce_grads()
+        self.exchange_before_adam()
         self.model.apply_adam(1.0 / self.world)
+        if self.mode == "zero":
+            self.all_gather_params()
+            self.model.sync_shadows()

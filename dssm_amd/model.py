@@ -24,6 +24,9 @@ from ._lib import check, ptr, stream_ptr
 from .data import CSRBatch
 
 
+ARENA_ALIGN = 512  # floats: equal 64-aligned shards for world sizes 1, 2, 4, 8
+
+
 class DSSM:
     def __init__(self, trigram_d: int, widths, query_bs: int, neg: int = 4, lr: float = 0.01,
                  dtype: str = "bf16", max_nnz: Optional[int] = None, device=None, seed: int = 0,
@@ -54,16 +57,20 @@ class DSSM:
         self.lr, self.beta1, self.beta2 = lr, beta1, beta2
         check(lib.dssm_config_check(C.byref(cfg)), "config")
         n = lib.dssm_param_count(C.byref(cfg))
+        self.n_params = int(n)
         nseg = lib.dssm_param_layout(C.byref(cfg), None, 0)
         segs = (_lib.dssm_segment * nseg)()
         lib.dssm_param_layout(C.byref(cfg), segs, nseg)
         self.segments = {s.name.decode(): (int(s.offset), int(s.rows), int(s.cols)) for s in segs}
         dev = self.device
         f32 = torch.float32
-        self.params = torch.zeros(n, dtype=f32, device=dev)
-        self.grads = torch.zeros(n, dtype=f32, device=dev)
-        self.adam_m = torch.zeros(n, dtype=f32, device=dev)
-        self.adam_v = torch.zeros(n, dtype=f32, device=dev)
+        # arenas padded to a multiple of ARENA_ALIGN floats (zeros the library never touches) so a
+        # data-parallel reduce-scatter / all-gather splits them into equal 64-float-aligned shards
+        npad = -(-n // ARENA_ALIGN) * ARENA_ALIGN
+        self.params = torch.zeros(npad, dtype=f32, device=dev)
+        self.grads = torch.zeros(npad, dtype=f32, device=dev)
+        self.adam_m = torch.zeros(npad, dtype=f32, device=dev)
+        self.adam_v = torch.zeros(npad, dtype=f32, device=dev)
         self.ema = torch.zeros(lib.dssm_ema_count(C.byref(cfg)), dtype=f32, device=dev)
         wsb = lib.dssm_workspace_bytes(C.byref(cfg))
         self.workspace = torch.zeros(wsb, dtype=torch.uint8, device=dev)
@@ -215,6 +222,15 @@ class DSSM:
     def backward(self, stream=None):
         check(self.lib.dssm_plan_backward(self._plan, stream_ptr(stream)), "backward")
 
+    def sync_shadows(self, stream=None):
+        """Rewrite the bf16 weight shadows from the fp32 parameters (after an external update)."""
+        check(self.lib.dssm_plan_sync_shadows(self._plan, stream_ptr(stream)), "sync_shadows")
+
+    def set_adam_range(self, begin: int = 0, end: Optional[int] = None):
+        """Optimizer shard: Adam updates arena elements [begin, end) only (data parallel)."""
+        end = self.n_params if end is None else int(end)
+        check(self.lib.dssm_plan_set_adam_range(self._plan, int(begin), int(end)), "set_adam_range")
+
     def apply_adam(self, grad_scale: float = 1.0, stream=None):
         check(self.lib.dssm_plan_adam(self._plan, float(grad_scale), stream_ptr(stream)), "adam")
         self.global_step += 1
@@ -317,8 +333,9 @@ class DSSM:
 
     # ---- checkpoint (new_dssm.py:248,331 tf.train.Saver) ---------------------------------------
     def state_dict(self) -> Dict[str, np.ndarray]:
-        return {"params": self.params.cpu().numpy(), "adam_m": self.adam_m.cpu().numpy(),
-                "adam_v": self.adam_v.cpu().numpy(), "ema": self.ema.cpu().numpy(),
+        n = self.n_params
+        return {"params": self.params[:n].cpu().numpy(), "adam_m": self.adam_m[:n].cpu().numpy(),
+                "adam_v": self.adam_v[:n].cpu().numpy(), "ema": self.ema.cpu().numpy(),
                 "beta_powers": np.array(self.beta_powers(), np.float32),
                 "global_step": np.array([self.global_step], np.int64)}
 
@@ -326,6 +343,8 @@ class DSSM:
         for name, t in (("params", self.params), ("adam_m", self.adam_m), ("adam_v", self.adam_v),
                         ("ema", self.ema)):
             a = np.asarray(sd[name], np.float32)
+            if name != "ema" and a.shape == (self.n_params,):
+                t = t[:self.n_params]  # arenas are stored without their shard padding
             if a.shape != tuple(t.shape):
                 raise ValueError(f"checkpoint {name} shape {a.shape} != {tuple(t.shape)}")
             t.copy_(torch.from_numpy(a))

@@ -122,15 +122,21 @@ int dssm_plan_get_adam_state(dssm_plan* plan, float* beta1_power, float* beta2_p
  * the Adam step instead of by a reduce launch.  Turn it off when the gradient arena must hold
  * the full gradient (data-parallel all-reduce, or inspecting the gradients). */
 int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
+/* Sharded optimizer step (data parallel, ZeRO-1 style): dssm_plan_adam updates only arena
+ * elements [begin, end) (multiples of 4; [0, param_count) restores the full step) -- the rank's
+ * shard of a reduce-scattered gradient -- together with the bf16 shadows of those elements.  The
+ * fused W1 Adam must be off.  DSSM_GRAPH_SHADOWS captures dssm_plan_sync_shadows (the shadows of
+ * the all-gathered parameters). */
+int dssm_plan_set_adam_range(dssm_plan* plan, int64_t begin, int64_t end);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, void* stream);
 
 /* hipGraph capture of a step for the CURRENT batch pointers (dssm_plan_set_batch): parts =
- * DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM (data-parallel runs launch the all-reduce between
- * the two).  Replays then cost one launch per step.  with_probes: the graph records the timing
+ * DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM and/or DSSM_GRAPH_SHADOWS (data-parallel runs launch
+ * the gradient collective between the first two).  Replays then cost one launch per step.  with_probes: the graph records the timing
  * probes' events (read back for its last replay with dssm_plan_graph_probe_read).  stream must
  * not be the default stream.  Graphs are owned by the plan. */
-enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2 };
+enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2, DSSM_GRAPH_SHADOWS = 4 };
 int dssm_plan_graph_build(dssm_plan* plan, int parts, float grad_scale, int with_probes,
                           void* stream, int* graph_id);
 int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);

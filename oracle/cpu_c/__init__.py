@@ -88,7 +88,8 @@ class CpuDSSM:
     bn{l}_{q|d}_{gamma|beta}; bn{l}_{q|d}_{mean|var})."""
 
     def __init__(self, D, widths, BS, NEG, params: Dict[str, np.ndarray], lr=0.01, beta1=0.9,
-                 beta2=0.999, adam_eps=1e-8, bn_eps=1e-3, ema_decay=0.5, gamma=20.0, max_nnz=None):
+                 beta2=0.999, adam_eps=1e-8, bn_eps=1e-3, ema_decay=0.5, gamma=20.0, max_nnz=None,
+                 pad_to: int = 1):
         self.lib = _load()
         L = len(widths)
         self.cfg = _Cfg(D, L, BS, NEG, (C.c_int * MAXL)(*widths), lr, beta1, beta2, adam_eps, bn_eps,
@@ -106,9 +107,10 @@ class CpuDSSM:
             shapes += [(f"W{l}", (dims[l - 1], dims[l])), (f"b{l}", (dims[l],)),
                        (f"bn{l}_g", (2, dims[l])), (f"bn{l}_b", (2, dims[l]))]
         total = sum(int(np.prod(s)) for _, s in shapes)
+        self.total = total
         self.flat = {}
         for role in ("p", "g", "m", "v"):
-            buf = np.zeros(total, np.float32)
+            buf = np.zeros(-(-total // pad_to) * pad_to, np.float32)  # zero tail: equal DP shards
             self.flat[role] = buf
             arr, o = {}, 0
             for name, s in shapes:

@@ -32,15 +32,27 @@ D, WIDTHS, BS, NEG, WORLD = 600, [64, 32], 32, 4, 2
 
 
 class CpuEngine:
-    """The DSSM model interface DataParallel drives (forward/backward/grads/apply_adam)."""
+    """The DSSM model interface DataParallel drives (forward/backward/arenas/apply_adam, the
+    optimizer range and the shadow refresh of the zero schedule)."""
 
     def __init__(self, params):
-        self.cpu = cpu_c.CpuDSSM(D, WIDTHS, BS // WORLD, NEG, params)
-        self.grads = torch.from_numpy(self.cpu.flat["g"])  # the flat gradient arena
+        self.cpu = cpu_c.CpuDSSM(D, WIDTHS, BS // WORLD, NEG, params, pad_to=64 * WORLD)
+        self.n_params = self.cpu.total
+        self.params = torch.from_numpy(self.cpu.flat["p"])  # flat arenas (padded), shared memory
+        self.grads = torch.from_numpy(self.cpu.flat["g"])
+        self.adam_m = torch.from_numpy(self.cpu.flat["m"])
+        self.adam_v = torch.from_numpy(self.cpu.flat["v"])
+        self.range = (0, self.n_params)
         self._train = None
 
     def set_fused_w1_adam(self, on):
         pass
+
+    def set_adam_range(self, begin, end):
+        self.range = (begin, end)
+
+    def sync_shadows(self):
+        pass  # fp32 engine: no bf16 shadows
 
     def set_batch(self, batch):
         self.batch = batch.as_dict()
@@ -52,7 +64,13 @@ class CpuEngine:
         self.loss = self.cpu.forward_backward(self.batch, train=self._train, backward=True)
 
     def apply_adam(self, grad_scale=1.0):
+        # a range step is the full step with the elements outside [begin, end) left as they were
+        keep = {r: self.cpu.flat[r].copy() for r in ("p", "m", "v")}
         self.cpu.adam(grad_scale)
+        b, e = self.range
+        for r, old in keep.items():
+            self.cpu.flat[r][:b] = old[:b]
+            self.cpu.flat[r][e:] = old[e:]
 
 
 def _free_port():
@@ -61,7 +79,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, mode):
     os.environ["OMP_NUM_THREADS"] = "2"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
     try:
@@ -69,24 +87,31 @@ def _worker(rank, port, out_dir):
         p0 = O.init_params(cfg, seed=9)
         glob = synth_batch(D, BS, NEG, seed=1234, mean_nnz=16)
         eng = CpuEngine(p0)
-        dp = DataParallel(eng, comm="torch")
-        assert dp.world == WORLD and dp.rank == rank
+        dp = DataParallel(eng, comm="torch", mode=mode)
+        assert dp.world == WORLD and dp.rank == rank and dp.mode == mode
         eng.set_batch(shard_batch(glob, BS, NEG, rank, WORLD))
         dp.train_step()
-        np.save(os.path.join(out_dir, f"p{rank}.npy"), eng.cpu.flat["p"])
+        dp.gather_state()
+        np.save(os.path.join(out_dir, f"p{rank}.npy"), eng.cpu.flat["p"][:eng.n_params])
+        np.save(os.path.join(out_dir, f"m{rank}.npy"), eng.cpu.flat["m"][:eng.n_params])
         np.save(os.path.join(out_dir, f"ema{rank}.npy"), eng.cpu.ema)
         np.save(os.path.join(out_dir, f"loss{rank}.npy"), np.array([eng.loss]))
     finally:
         dist.destroy_process_group()
 
 
-def test_data_parallel_two_ranks_gloo():
+@pytest.mark.parametrize("mode", ["allreduce", "zero"])
+def test_data_parallel_two_ranks_gloo(mode):
+    """allreduce: all-reduce + replicated Adam; zero: reduce-scatter + Adam on the rank's shard +
+    all-gather of the parameters. Both must give the same step."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, mode), nprocs=WORLD, join=True)
         p = [np.load(os.path.join(d, f"p{r}.npy")) for r in range(WORLD)]
+        m_ = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(WORLD)]
         ema = [np.load(os.path.join(d, f"ema{r}.npy")) for r in range(WORLD)]
         loss = [float(np.load(os.path.join(d, f"loss{r}.npy"))[0]) for r in range(WORLD)]
-    np.testing.assert_array_equal(p[0], p[1])  # replicated Adam on the all-reduced gradient
+    np.testing.assert_array_equal(p[0], p[1])  # identical parameters on every rank
+    np.testing.assert_array_equal(m_[0], m_[1])  # and identical (gathered) Adam state
 
     # oracle: mean of the per-shard gradients, then one Adam step
     cfg_l = O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS // WORLD, neg=NEG)

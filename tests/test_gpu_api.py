@@ -187,3 +187,36 @@ def test_functional_ops_match_oracle():
     np.testing.assert_allclose(res["cos_sim_raw"].cpu().numpy().ravel(), c.T.ravel(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(res["prob"].cpu().numpy(), pr, rtol=1e-4, atol=1e-6)
     assert abs(float(res["loss"]) + np.log(pr[:, 0]).mean()) <= 1e-5 * abs(np.log(pr[:, 0]).mean())
+
+
+def test_sharded_adam_range_updates_only_its_shard():
+    """dssm_plan_set_adam_range (the data-parallel zero schedule's optimizer shard): elements
+    inside the range step exactly as in the full step, the rest keep their values."""
+    from dssm_amd.model import DSSM
+    from dssm_amd.data import synth_batch
+    D, widths, BS, NEG = 3000, (128, 64), 64, 4
+    a = DSSM(D, widths, BS, NEG, dtype="bf16", seed=2)
+    b = DSSM(D, widths, BS, NEG, dtype="bf16", seed=2)
+    for m in (a, b):
+        m.set_fused_w1_adam(False)
+        m.set_batch(synth_batch(D, BS, NEG, seed=11, mean_nnz=20))
+        m.forward(True)
+        m.backward()
+    b.grads.copy_(a.grads)  # same gradient (the backward's atomics may differ in the last bits)
+    n = a.n_params
+    s0, s1 = 64 * 37, 64 * ((n // 64) // 2)
+    p0 = b.params.clone()
+    a.apply_adam()
+    b.set_adam_range(s0, s1)
+    b.apply_adam()
+    torch.cuda.synchronize()
+    assert torch.equal(b.params[s0:s1], a.params[s0:s1])
+    assert torch.equal(b.adam_m[s0:s1], a.adam_m[s0:s1])
+    assert torch.equal(b.params[:s0], p0[:s0]) and torch.equal(b.params[s1:], p0[s1:])
+    assert not torch.any(b.adam_v[s1:n] != 0)
+    assert a.beta_powers() == b.beta_powers()
+    with pytest.raises(Exception):
+        b.set_adam_range(3, 64)  # not 4-aligned
+    b.set_fused_w1_adam(True)
+    with pytest.raises(Exception):
+        b.apply_adam()  # a shard range needs the fused W1 Adam off
