@@ -71,9 +71,34 @@ class DataParallel:
         self._nccl = dist.is_initialized() and dist.get_backend() == "nccl"
         if self.world > 1:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
+        if self.mode == "zero" and self._nccl and not self._inplace_ok():
+            self.mode = "allreduce"  # the in-place collectives misbehaved: exchange by all-reduce
         if self.mode == "zero":
             self.begin, self.end, self.shard = shard_bounds(npad, model.n_params, self.rank, self.world)
             model.set_adam_range(self.begin, max(self.begin, self.end))
+
+    def _inplace_ok(self) -> bool:
+        """Self-test of the in-place reduce-scatter / all-gather this schedule relies on (small
+        tensors with known contents; every rank must agree), before any capture."""
+        dev = self.model.params.device
+        k = 64
+        try:
+            x = torch.arange(self.world * k, dtype=torch.float32, device=dev) + 1000.0 * self.rank
+            mine = x[self.rank * k:(self.rank + 1) * k]
+            dist.reduce_scatter_tensor(mine, x)
+            ref = (torch.arange(self.rank * k, (self.rank + 1) * k, dtype=torch.float32, device=dev)
+                   * self.world + 1000.0 * sum(range(self.world)))
+            ok = bool(torch.equal(mine, ref))
+            y = torch.zeros(self.world * k, dtype=torch.float32, device=dev)
+            y[self.rank * k:(self.rank + 1) * k] = self.rank + 1
+            dist.all_gather_into_tensor(y, y[self.rank * k:(self.rank + 1) * k])
+            ok = ok and bool(torch.equal(y, torch.arange(1, self.world + 1, dtype=torch.float32,
+                                                         device=dev).repeat_interleave(k)))
+        except Exception:
+            ok = False
+        flag = torch.tensor([1.0 if ok else 0.0], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item() == 1.0)
 
     # ---- collectives ----------------------------------------------------------------------
     def allreduce_grads(self):
