@@ -87,6 +87,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
   const int s = a.col_ptr[c], e = a.col_ptr[c + 1];
   const bool heavy = e - s > kLightEntries;
   if (heavy && a.item_blocks) return;  // updated by the heavy-item workgroups
+  if (e == s && a.w1_flat) return;     // untouched row: the flat role's decay-only pass
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
@@ -229,6 +230,31 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       w1_row<TZ>(a, c, alpha);
   } else {
     const int bi = blockIdx.x - a.item_blocks - a.w1_blocks;
+    if (a.w1_flat) {
+      // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
+      const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
+      for (int64_t i = (int64_t)bi * blockDim.x + threadIdx.x; i < w4;
+           i += (int64_t)a.dense_blocks * blockDim.x) {
+        const int c = (int)((i * 4) / a.n);
+        if (a.col_ptr[c + 1] != a.col_ptr[c]) continue;
+        float4 pp = reinterpret_cast<float4*>(a.p)[i];
+        float4 mm = reinterpret_cast<float4*>(a.m)[i];
+        float4 vv = reinterpret_cast<float4*>(a.v)[i];
+        adam1(pp.x, mm.x, vv.x, 0.f, alpha, a.b1c, a.b2c, a.eps);
+        adam1(pp.y, mm.y, vv.y, 0.f, alpha, a.b1c, a.b2c, a.eps);
+        adam1(pp.z, mm.z, vv.z, 0.f, alpha, a.b1c, a.b2c, a.eps);
+        adam1(pp.w, mm.w, vv.w, 0.f, alpha, a.b1c, a.b2c, a.eps);
+        reinterpret_cast<float4*>(a.p)[i] = pp;
+        reinterpret_cast<float4*>(a.m)[i] = mm;
+        reinterpret_cast<float4*>(a.v)[i] = vv;
+        if (a.shadow && c < a.D) {
+          uint2 q;
+          q.x = pack2bf(pp.x, pp.y);
+          q.y = pack2bf(pp.z, pp.w);
+          *reinterpret_cast<uint2*>(a.shadow + (size_t)c * a.ldsh + (i * 4 - (int64_t)c * a.n)) = q;
+        }
+      }
+    }
     for (int64_t i = a.d4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < a.d4_end;
          i += (int64_t)a.dense_blocks * blockDim.x) {
       float4 pp = reinterpret_cast<float4*>(a.p)[i];
@@ -323,14 +349,19 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   }();
   if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), w1_cap);
   if (sep_advance) a.ticket = nullptr;
-  const int64_t n4 = a.d4_end - a.d4_begin;
-  a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
+  static const bool w1_flat_on = [] {
+    const char* e = std::getenv("DSSM_ADAM_W1_FLAT");
+    return !(e && e[0] == '0');
+  }();
   static const int item_cap = [] {
     const char* e = std::getenv("DSSM_ADAM_ITEM_BLOCKS");
     return e ? std::max(1, std::atoi(e)) : kAdamItemBlocks;
   }();
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, item_cap);
+  a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0) ? 1 : 0;
+  const int64_t n4 = a.d4_end - a.d4_begin + (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
+  a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   dim3 grid(a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);

@@ -202,6 +202,9 @@ struct AdamStep {
   // heavy W1 columns computed inside the step (item_blocks > 0): work items of the CSC scan
   // (k_csc_scan_multi), per-column arrival tickets (zero-initialised, re-armed)
   int item_blocks;
+  // W1 rows with no entry this step (g = 0: pure decay) by the flat streaming role instead of a
+  // wave per row (full lanes, no gather); set with item_blocks
+  int w1_flat;
   const int* heavy_n;
   const int2* heavy_items;
   unsigned* heavy_ticket;
