@@ -48,6 +48,12 @@ def parse():
                     help="torch.distributed backend (gloo: functional rehearsal of N>1 on one GPU)")
     ap.add_argument("--graph", type=int, default=1, help="replay hipGraph-captured steps (0: eager launches)")
     ap.add_argument("--probes", type=int, default=1, help="HIP-event kernel probes in the timed region")
+    ap.add_argument("--rehearse-world", type=int, default=1,
+                    help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
+                         "(unfused dW1, wire pack, 1/W Adam shard, wire shadows) with the "
+                         "collectives omitted, to time the per-rank compute of the N>1 path")
+    ap.add_argument("--wire", default="auto", choices=["auto", "bf16", "fp32"],
+                    help="zero schedule: W1 rows on a bf16 or fp32 wire (auto: bf16 in bf16 mode)")
     return ap.parse_args()
 
 
@@ -57,9 +63,31 @@ def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int) -> int:
     return 4 * (rows + 1) + nnz * (4 + 4) + nnz * n1 * s_w + rows * n1 * 4
 
 
-def adam_alg_bytes(n_params: int, shadow_elems: int) -> int:
-    """p, m, v read+write, g read (28 B/param) + bf16 shadow writes."""
-    return 28 * n_params + 2 * shadow_elems
+def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: int, rows: int,
+                   n1: int, range_elems: int = None, wire_elems: int = 0) -> int:
+    """Algorithmic bytes of one k_adam_step launch.
+
+    Every updated element streams p, m, v in and out (24 B).  Its gradient is read as fp32 (4 B),
+    except (a) fused single-GPU step: the [W1; b1] rows' gradient is never stored -- the launch
+    gathers it from the CSC transpose instead, (index, value) 8 B + one bf16 dZ1 row (2 n1 B) per
+    entry, over nnz + rows entries (the ones column gives db1) -- the SpMM-backward bytes of
+    SURVEY §8(d) minus its dense dW1 write; (b) data-parallel bf16 wire: the rank's W1 shard
+    reads a bf16 gradient (2 B) and writes a bf16 parameter copy (2 B).  bf16 mode adds 2 B per
+    weight element written to its shadows (W_l for l >= 2 also transposed: 4 B)."""
+    if range_elems is None:
+        range_elems = n_params
+    b = 24 * range_elems
+    if fused:
+        b += 4 * (n_params - w1_elems) + (nnz + rows) * (8 + 2 * n1)
+    else:
+        b += 4 * (range_elems - wire_elems) + 4 * wire_elems
+    if bf16:
+        sh_w1 = (w1_elems - n1) if fused else 0  # W1's shadow (bias row excluded); wired: from the wire
+        sh_rest = sum(2 * WIDTHS[l - 1] * WIDTHS[l] for l in range(1, len(WIDTHS)))
+        if not fused and not wire_elems:
+            sh_w1 = (w1_elems - n1) * range_elems / max(n_params, 1)  # the shard's share
+        b += 2 * (sh_w1 + sh_rest)
+    return int(b)
 
 
 # probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py)
@@ -117,7 +145,19 @@ def main():
     if world > 1:
         from dssm_amd.dist import DataParallel
         dp = DataParallel(model, comm="rccl" if args.allreduce == "rccl" else "torch",
-                          mode="allreduce" if args.allreduce == "rccl" else args.dp_mode)
+                          mode="allreduce" if args.allreduce == "rccl" else args.dp_mode,
+                          wire=args.wire)
+    rehearse = args.rehearse_world if world == 1 else 1
+    if rehearse > 1:
+        # rank 0's kernels of a W-rank bf16-wire step; the reduce-scatter / all-reduce / all-gather
+        # that would sit between the graphs are left out (analysis of the N>1 compute share)
+        model.set_fused_w1_adam(False)
+        ext = model.wire_extent()
+        shard = -(-ext // (64 * rehearse)) * 64
+        wires = [torch.zeros(shard * rehearse, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        wires[1][:ext].copy_(model.params[:ext])
+        model.set_wire(*wires)
+        model.set_adam_range(0, min(shard, ext))
 
     cols = ZipfColumns(D)
     staged = []
@@ -145,20 +185,28 @@ def main():
         for b, (ip, ix, vv) in enumerate(staged):
             model.set_batch(indptr=ip, indices=ix, values=vv)
             pr = bool(args.probes) and b == 0
-            if world > 1:
+            if world > 1 or rehearse > 1:
                 graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
             else:
                 graphs.append(model.graph_build(probes=pr))
-        adam_graph = model.graph_build(_lib.GRAPH_ADAM, 1.0 / world, probes=bool(args.probes)) if world > 1 else None
-        shadow_graph = model.graph_build(_lib.GRAPH_SHADOWS) if (dp is not None and dp.mode == "zero") else None
+        split = world > 1 or rehearse > 1
+        adam_graph = (model.graph_build(_lib.GRAPH_ADAM, 1.0 / max(world, rehearse), probes=bool(args.probes))
+                      if split else None)
+        shadow_graph = None
+        if dp is not None and dp.mode == "zero":
+            shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS if dp.wire == "bf16" else _lib.GRAPH_SHADOWS)
+        elif rehearse > 1:
+            shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS)
 
         def step(i):
             model.graph_launch(graphs[i % len(graphs)])
-            if world > 1:
-                dp.exchange_before_adam()
+            if split:
+                if dp is not None:
+                    dp.exchange_before_adam()
                 model.graph_launch(adam_graph)
                 if shadow_graph is not None:
-                    dp.exchange_after_adam()
+                    if dp is not None:
+                        dp.exchange_after_adam()
                     model.graph_launch(shadow_graph)
     else:
         def step(i):
@@ -168,10 +216,12 @@ def main():
             model.backward()
             if world > 1:
                 dp.exchange_before_adam()
-            model.apply_adam(1.0 / world)
+            model.apply_adam(1.0 / max(world, rehearse))
             if dp is not None and dp.mode == "zero":
                 dp.exchange_after_adam()
-                model.sync_shadows()
+                dp.refresh_shadows()
+            elif rehearse > 1:
+                model.wire_shadows()
 
     for i in range(args.warmup):
         step(i)
@@ -212,12 +262,26 @@ def main():
     nnz_avg = int(nnzs[0] if args.graph else np.mean( [nnzs[(args.warmup + i) % len(nnzs)] for i in range(args.steps)]))
     s_w = 2 if args.dtype == "bf16" else 4
     n_params = int(model.n_params)
-    shadow = sum((D if l == 0 else WIDTHS[l - 1]) * WIDTHS[l] for l in range(len(WIDTHS))) if args.dtype == "bf16" else 0
+    w1_elems = (D + 1) * WIDTHS[0]
+    fused = world == 1 and rehearse == 1
+    wire_elems, range_elems = 0, n_params
+    if dp is not None and dp.mode == "zero":
+        if dp.wire == "bf16":
+            wire_elems = max(0, dp.end - dp.begin)
+            range_elems = wire_elems + (n_params - dp.extent)
+        else:
+            range_elems = max(0, dp.end - dp.begin)
+    elif rehearse > 1:
+        ext = D * WIDTHS[0]
+        wire_elems = min(-(-ext // (64 * rehearse)) * 64, ext)
+        range_elems = wire_elems + (n_params - ext)
     kern = {
         "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
-        "adam": (adam_alg_bytes(n_params, shadow), probes.get("adam", 0.0)),
+        "adam": (adam_alg_bytes(n_params, args.dtype == "bf16", fused, w1_elems, nnz_avg, rows,
+                                WIDTHS[0], range_elems, wire_elems), probes.get("adam", 0.0)),
     }
-    traffic, traffic_src = pmc_traffic(args.dtype)
+    # the committed PMC summary profiles the default single-GPU step (fused Adam) only
+    traffic, traffic_src = pmc_traffic(args.dtype) if fused else ({}, None)
     rl = {}
     for k, (byt, ms) in kern.items():
         gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -237,12 +301,15 @@ def main():
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
-                   "dp_exchange": dp.mode if dp is not None else None},
+                   "dp_exchange": (f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) if dp is not None else None},
         "roofline": dict(rl[dominant], kernel=dominant),
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,
         "final_loss": round(loss, 5), "final_accuracy": round(acc, 4),
     }
+    if rehearse > 1:
+        out["rehearsal"] = {"world": rehearse, "collectives": "omitted",
+                            "note": "rank 0's compute share of an N-rank bf16-wire step; not a headline number"}
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -19,7 +19,7 @@ DSSM_F32, DSSM_BF16 = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
  BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING) = range(11)
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
-GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS = 1, 2, 4
+GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS, GRAPH_WIRE_SHADOWS = 1, 2, 4, 8
 
 
 class DssmError(RuntimeError):
@@ -71,6 +71,9 @@ _SIGS = {
     "dssm_plan_finalize_loss": (C.c_int, [_P, _P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
+    "dssm_plan_wire_extent": (C.c_int64, [_P]),
+    "dssm_plan_set_wire": (C.c_int, [_P, _P, _P, C.c_int64]),
+    "dssm_plan_wire_shadows": (C.c_int, [_P, _P]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),
     "dssm_plan_probe_read": (C.c_int, [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
     "dssm_spmm_csr_fwd": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,

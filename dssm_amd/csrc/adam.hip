@@ -255,10 +255,20 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
         }
       }
     }
-    for (int64_t i = a.d4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < a.d4_end;
-         i += (int64_t)a.dense_blocks * blockDim.x) {
+    const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
+    for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < na + nt;
+         j += (int64_t)a.dense_blocks * blockDim.x) {
+      const int64_t i = j < na ? a.d4_begin + j : a.t4_begin + (j - na);
+      const bool wired = i < a.wire4;
       float4 pp = reinterpret_cast<float4*>(a.p)[i];
-      float4 gg = slab_grad4(a.slabs, i * 4, a.g);
+      float4 gg;
+      if (wired) {
+        const uint2 q = reinterpret_cast<const uint2*>(a.gwire)[i];
+        gg = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                         __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+      } else {
+        gg = slab_grad4(a.slabs, i * 4, a.g);
+      }
       float4 mm = reinterpret_cast<float4*>(a.m)[i];
       float4 vv = reinterpret_cast<float4*>(a.v)[i];
       adam1(pp.x, mm.x, vv.x, gg.x * a.gs, alpha, a.b1c, a.b2c, a.eps);
@@ -270,7 +280,14 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       reinterpret_cast<float4*>(a.v)[i] = vv;
       if (i * 4 >= a.clear_from)
         reinterpret_cast<float4*>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a.sh.count) write_shadow4(a.sh, i * 4, pp);
+      if (wired) {
+        uint2 q;
+        q.x = pack2bf(pp.x, pp.y);
+        q.y = pack2bf(pp.z, pp.w);
+        reinterpret_cast<uint2*>(a.pwire)[i] = q;
+      } else if (a.sh.count) {
+        write_shadow4(a.sh, i * 4, pp);
+      }
     }
   }
   __syncthreads();
@@ -326,6 +343,32 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
   }
 }
 
+__global__ __launch_bounds__(256) void k_wire_pack(const float* __restrict__ g, u16* __restrict__ w,
+                                                   int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    uint2 q;
+    q.x = pack2bf(v.x, v.y);
+    q.y = pack2bf(v.z, v.w);
+    reinterpret_cast<uint2*>(w)[i] = q;
+  }
+}
+
+// W1 shadow rows [rows x ld] from the bf16 parameter wire (rows of g.cols, at g.offset): one
+// 4-element group per thread (cols % 4 == 0, so a group never straddles two rows)
+__global__ __launch_bounds__(256) void k_wire_shadow(const u16* __restrict__ w, ShadowSeg g) {
+  const int64_t n4 = g.rows * g.cols / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rel = i * 4;
+    const int64_t r = rel / g.cols;
+    const int c = (int)(rel - r * g.cols);
+    *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) =
+        *reinterpret_cast<const uint2*>(w + g.offset + rel);
+  }
+}
+
 int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 int grid_for(int64_t n4) {
@@ -360,7 +403,9 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, item_cap);
   a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0) ? 1 : 0;
-  const int64_t n4 = a.d4_end - a.d4_begin + (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
+  if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
+  const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) +
+                     (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   dim3 grid(a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
@@ -368,6 +413,19 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   else
     hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
   if (!a.ticket) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_pack(const float* g, uint16_t* wire, int64_t n, hipStream_t s) {
+  if (n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wire_pack, dim3(grid_for(n / 4)), dim3(256), 0, s, g, wire, n / 4);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s) {
+  if (seg.cols % 4) return hipErrorInvalidValue;
+  const int64_t n4 = seg.rows * seg.cols / 4;
+  hipLaunchKernelGGL(k_wire_shadow, dim3(grid_for(n4)), dim3(256), 0, s, wire, seg);
   return hipGetLastError();
 }
 

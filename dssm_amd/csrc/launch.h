@@ -208,9 +208,21 @@ struct AdamStep {
   const int* heavy_n;
   const int2* heavy_items;
   unsigned* heavy_ticket;
+  // data-parallel bf16 wire (dssm_plan_set_wire): float4 index i < wire4 takes its gradient from
+  // the reduce-scattered bf16 gradient wire and writes bf16(p) to the parameter wire (the
+  // all-gather's input) instead of the shadows; a second dense range [t4_begin, t4_end) (the
+  // replicated fp32 tail) follows [d4_begin, d4_end)
+  const uint16_t* gwire;
+  uint16_t* pwire;
+  int64_t wire4;
+  int64_t t4_begin, t4_end;
 };
 constexpr int kAdamItemBlocks = 512;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
+// bf16 wire helpers (data parallel): wire[i] = bf16(g[i]) for i < n (n % 4 == 0); the W1 shadow
+// rows from the all-gathered bf16 parameter wire (row length cols, shadow stride ld)
+hipError_t launch_wire_pack(const float* g, uint16_t* wire, int64_t n, hipStream_t s);
+hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s);
 
 }  // namespace dssm

@@ -214,6 +214,11 @@ struct dssm_plan {
   const float* values = nullptr;
   bool fwd_train_done = false;
   int64_t adam_begin = 0, adam_end = -1;  // sharded optimizer range (dssm_plan_set_adam_range)
+  // data-parallel bf16 wire (dssm_plan_set_wire): W1 gradient / parameter copies exchanged by
+  // the reduce-scatter / all-gather; arena elements [0, wire_end) are W1's rows
+  uint16_t* gwire = nullptr;
+  uint16_t* pwire = nullptr;
+  int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
@@ -816,7 +821,16 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
   return DSSM_OK;
 }
 
+static int backward_impl(dssm_plan* P, void* stream);
+
 int dssm_plan_backward(dssm_plan* P, void* stream) {
+  if (int rc = backward_impl(P, stream)) return rc;
+  if (P->gwire)  // data parallel: the W1 gradient rows leave as bf16
+    HIP_TRY(dssm::launch_wire_pack(P->g, P->gwire, P->wire_end(), (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+static int backward_impl(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (!P->fwd_train_done) return fail(DSSM_E_INVALID, "backward needs a train-mode forward first");
   hipStream_t s = (hipStream_t)stream;
@@ -916,6 +930,22 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   a.d4_end = (P->adam_end >= 0 ? P->adam_end : Lt.total) / 4;
   if (P->fused_w1_adam && (P->adam_begin != 0 || (P->adam_end >= 0 && P->adam_end != Lt.total)))
     return fail(DSSM_E_INVALID, "a sharded Adam range needs the fused W1 Adam off");
+  if (P->pwire) {
+    // bf16 wire: the rank's W1 shard from the reduce-scattered wire (writing the parameter wire),
+    // then the replicated fp32 tail [wire_end, total) with its shadows
+    if (P->fused_w1_adam) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
+    const int64_t we = P->wire_end();
+    a.d4_begin = std::min(P->adam_begin, we) / 4;
+    a.d4_end = std::min(P->adam_end >= 0 ? P->adam_end : we, we) / 4;
+    if (a.d4_end < a.d4_begin) a.d4_end = a.d4_begin;
+    a.t4_begin = we / 4;
+    a.t4_end = Lt.total / 4;
+    a.gwire = P->gwire;
+    a.pwire = P->pwire;
+    a.wire4 = we / 4;
+    for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
+    if (sh.count) sh.count -= 1;
+  }
   if (P->fused_w1_adam) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
     a.w1_blocks = 1;  // sized by the launcher
@@ -965,6 +995,33 @@ int dssm_plan_set_adam_range(dssm_plan* P, int64_t begin, int64_t end) {
   if ((end % 4) && end == total) return fail(DSSM_E_INVALID, "param_count is a multiple of 64");
   P->adam_begin = begin;
   P->adam_end = end;
+  return DSSM_OK;
+}
+
+int64_t dssm_plan_wire_extent(const dssm_plan* P) { return P ? P->wire_end() : -1; }
+
+int dssm_plan_set_wire(dssm_plan* P, uint16_t* grad_wire, uint16_t* param_wire, int64_t count) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!grad_wire && !param_wire) {
+    P->gwire = P->pwire = nullptr;
+    return DSSM_OK;
+  }
+  if (!grad_wire || !param_wire) return fail(DSSM_E_INVALID, "both wires or neither");
+  if (!P->Lt.bf16) return fail(DSSM_E_UNSUPPORTED, "the bf16 wire is a bf16-mode (perf) option");
+  if (P->fused_w1_adam) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
+  if (P->Lt.fc_off[0] != 0 || count < P->wire_end())
+    return fail(DSSM_E_INVALID, "wire buffers must hold dssm_plan_wire_extent() elements");
+  if ((reinterpret_cast<uintptr_t>(grad_wire) | reinterpret_cast<uintptr_t>(param_wire)) & 7)
+    return fail(DSSM_E_INVALID, "wire buffers must be 8-byte aligned");
+  P->gwire = grad_wire;
+  P->pwire = param_wire;
+  return DSSM_OK;
+}
+
+int dssm_plan_wire_shadows(dssm_plan* P, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!P->pwire) return fail(DSSM_E_INVALID, "no wire set (dssm_plan_set_wire)");
+  HIP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], (hipStream_t)stream));
   return DSSM_OK;
 }
 
@@ -1034,9 +1091,10 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
                           int* graph_id) {
   if (!P || !graph_id) return fail(DSSM_E_INVALID, "null argument");
   if (!stream) return fail(DSSM_E_INVALID, "graph capture needs a non-default stream");
-  if (!(parts & (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS)) ||
-      (parts & ~(DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS)))
-    return fail(DSSM_E_INVALID, "graph parts: DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS");
+  const int all = DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS | DSSM_GRAPH_WIRE_SHADOWS;
+  if (!(parts & all) || (parts & ~all))
+    return fail(DSSM_E_INVALID, "graph parts: DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS"
+                                " | DSSM_GRAPH_WIRE_SHADOWS");
   if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
   if (P->fused_w1_adam && parts != (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM))
     return fail(DSSM_E_INVALID, "with the fused W1 Adam a graph must hold the whole step");
@@ -1066,6 +1124,7 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
   }
   if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
   if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
+  if (!rc && (parts & DSSM_GRAPH_WIRE_SHADOWS)) rc = dssm_plan_wire_shadows(P, stream);
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();
   hipGraph_t graph = nullptr;

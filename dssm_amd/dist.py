@@ -8,6 +8,18 @@ Two exchange schedules over the flat fp32 arenas (RCCL over xGMI):
   m / v live sharded: gather_state() collects them for a checkpoint.
 * "allreduce": one all-reduce of the gradient arena and replicated Adam.
 
+The zero schedule's wire ("wire" argument; "bf16" by default for a bf16-mode model):
+* "fp32": the whole padded fp32 arena is reduce-scattered and all-gathered (36.5 MB each way at
+  C2), the shadows refreshed from the gathered fp32 parameters;
+* "bf16": only W1's rows ([0, model.wire_extent()), 99% of the parameters) are sharded, and they
+  cross the links as bf16: the backward packs bf16(dW1) into a gradient wire that is reduce-
+  scattered, Adam updates the rank's fp32 W1 shard from it and writes bf16(W1) into a parameter
+  wire that is all-gathered, and W1's bf16 shadow (all the bf16 forward reads of W1) is rebuilt
+  from it.  The small tail ([extent, n_params): b1, W2.., BN) is all-reduced in fp32 and updated
+  replicated, so every rank's biases / BN parameters stay bit-identical fp32.  Half the link
+  bytes of the fp32 wire; W1's fp32 master rows outside a rank's shard are stale between
+  gather_state() calls (the forward never reads them in bf16 mode).
+
 BN statistics stay per replica (unsynced), which is the reference's BN semantics applied to a
 replica's shard; EMA shadows stay rank-local and rank 0's are the ones checkpointed.
 
@@ -57,7 +69,7 @@ def shard_bounds(n_pad: int, n: int, rank: int, world: int):
 class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
-    def __init__(self, model, comm: str = "torch", mode: str = "auto"):
+    def __init__(self, model, comm: str = "torch", mode: str = "auto", wire: str = "auto"):
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
@@ -71,29 +83,49 @@ class DataParallel:
         self._nccl = dist.is_initialized() and dist.get_backend() == "nccl"
         if self.world > 1:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
-        if self.mode == "zero" and self._nccl and not self._inplace_ok():
+        if wire == "auto":
+            wire = "bf16" if getattr(model, "dtype", "fp32") == "bf16" else "fp32"
+        if wire not in ("bf16", "fp32"):
+            raise ValueError("wire: 'bf16' or 'fp32'")
+        if self.mode == "zero" and self._nccl and not (
+                self._inplace_ok(torch.float32) and (wire == "fp32" or self._inplace_ok(torch.bfloat16))):
             self.mode = "allreduce"  # the in-place collectives misbehaved: exchange by all-reduce
-        if self.mode == "zero":
+        self.wire = wire if self.mode == "zero" else "fp32"
+        self.grad_wire = self.param_wire = None
+        if self.mode == "zero" and self.wire == "bf16":
+            ext = model.wire_extent()
+            self.extent = ext
+            self.shard = -(-ext // (64 * self.world)) * 64
+            self.begin, self.end = self.rank * self.shard, min((self.rank + 1) * self.shard, ext)
+            n = self.shard * self.world
+            dev = model.params.device
+            self.grad_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+            self.param_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+            self.param_wire[:ext].copy_(model.params[:ext])
+            model.set_wire(self.grad_wire, self.param_wire)
+            model.set_adam_range(self.begin, max(self.begin, self.end))
+        elif self.mode == "zero":
             self.begin, self.end, self.shard = shard_bounds(npad, model.n_params, self.rank, self.world)
             model.set_adam_range(self.begin, max(self.begin, self.end))
 
-    def _inplace_ok(self) -> bool:
+    def _inplace_ok(self, dtype) -> bool:
         """Self-test of the in-place reduce-scatter / all-gather this schedule relies on (small
-        tensors with known contents; every rank must agree), before any capture."""
+        tensors with known contents, exact in bf16 too; every rank must agree), before any
+        capture."""
         dev = self.model.params.device
         k = 64
         try:
-            x = torch.arange(self.world * k, dtype=torch.float32, device=dev) + 1000.0 * self.rank
+            x = (torch.arange(self.world * k, device=dev) % 4 + 4 * self.rank).to(dtype)
             mine = x[self.rank * k:(self.rank + 1) * k]
             dist.reduce_scatter_tensor(mine, x)
-            ref = (torch.arange(self.rank * k, (self.rank + 1) * k, dtype=torch.float32, device=dev)
-                   * self.world + 1000.0 * sum(range(self.world)))
+            ref = ((torch.arange(self.rank * k, (self.rank + 1) * k, device=dev) % 4) * self.world
+                   + 4 * sum(range(self.world))).to(dtype)  # every partial sum <= 256: exact in bf16
             ok = bool(torch.equal(mine, ref))
-            y = torch.zeros(self.world * k, dtype=torch.float32, device=dev)
+            y = torch.zeros(self.world * k, dtype=dtype, device=dev)
             y[self.rank * k:(self.rank + 1) * k] = self.rank + 1
             dist.all_gather_into_tensor(y, y[self.rank * k:(self.rank + 1) * k])
-            ok = ok and bool(torch.equal(y, torch.arange(1, self.world + 1, dtype=torch.float32,
-                                                         device=dev).repeat_interleave(k)))
+            ok = ok and bool(torch.equal(y, torch.arange(1, self.world + 1, device=dev)
+                                         .to(dtype).repeat_interleave(k)))
         except Exception:
             ok = False
         flag = torch.tensor([1.0 if ok else 0.0], device=dev)
@@ -109,17 +141,15 @@ class DataParallel:
         else:
             dist.all_reduce(self.model.grads)
 
-    def reduce_scatter_grads(self):
-        """Sum of the gradient arenas, the rank's shard landing in place in its own arena."""
-        g = self.model.grads
+    def _reduce_scatter(self, g):
+        """Sum over ranks, the rank's shard landing in place in its own copy of g."""
         mine = g[self.rank * self.shard:(self.rank + 1) * self.shard]
         if self._nccl:
             dist.reduce_scatter_tensor(mine, g)  # in place: output == input + rank * count
         else:
             dist.all_reduce(g)  # gloo: the shard of the full sum is the same bytes
 
-    def all_gather_params(self):
-        p = self.model.params
+    def _all_gather(self, p):
         mine = p[self.rank * self.shard:(self.rank + 1) * self.shard]
         if self._nccl:
             dist.all_gather_into_tensor(p, mine)  # in place: input == output + rank * count
@@ -129,6 +159,22 @@ class DataParallel:
             dist.all_gather(got, mine.clone())
             for dst, src in zip(parts, got):
                 dst.copy_(src)
+
+    def reduce_scatter_grads(self):
+        if self.wire == "bf16":
+            self._reduce_scatter(self.grad_wire)
+            dist.all_reduce(self.model.grads[self.extent:self.model.n_params])  # fp32 tail
+        else:
+            self._reduce_scatter(self.model.grads)
+
+    def all_gather_params(self):
+        self._all_gather(self.param_wire if self.wire == "bf16" else self.model.params)
+
+    def refresh_shadows(self):
+        if self.wire == "bf16":
+            self.model.wire_shadows()
+        else:
+            self.model.sync_shadows()
 
     def exchange_before_adam(self):
         if self.mode == "zero":
@@ -144,16 +190,18 @@ class DataParallel:
         """Full Adam m / v on every rank (the zero schedule keeps them sharded): before a checkpoint."""
         if self.mode != "zero":
             return
+        if self.wire == "bf16":
+            # W1's fp32 rows (parameters too: other ranks' shards are stale on this one) through
+            # a padded staging buffer; the tail is replicated already
+            ext = self.extent
+            for t in (self.model.params, self.model.adam_m, self.model.adam_v):
+                buf = torch.zeros(self.shard * self.world, dtype=t.dtype, device=t.device)
+                buf[self.begin:self.end].copy_(t[self.begin:self.end])
+                self._all_gather(buf)
+                t[:ext].copy_(buf[:ext])
+            return
         for t in (self.model.adam_m, self.model.adam_v):
-            mine = t[self.rank * self.shard:(self.rank + 1) * self.shard]
-            if self._nccl:
-                dist.all_gather_into_tensor(t, mine)
-            else:
-                parts = list(t.view(self.world, self.shard).unbind(0))
-                got = [torch.empty_like(x) for x in parts]
-                dist.all_gather(got, mine.clone())
-                for dst, src in zip(parts, got):
-                    dst.copy_(src)
+            self._all_gather(t)
 
     def train_step(self):
         self.model.forward(True)
@@ -162,4 +210,4 @@ class DataParallel:
         self.model.apply_adam(1.0 / self.world)
         if self.mode == "zero":
             self.all_gather_params()
-            self.model.sync_shadows()
+            self.refresh_shadows()

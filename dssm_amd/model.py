@@ -235,6 +235,27 @@ class DSSM:
         check(self.lib.dssm_plan_adam(self._plan, float(grad_scale), stream_ptr(stream)), "adam")
         self.global_step += 1
 
+    # ---- data-parallel bf16 wire (include/dssm.h dssm_plan_set_wire) ---------------------------
+    def wire_extent(self) -> int:
+        """Arena elements [0, extent) that cross the links as bf16 (W1's rows)."""
+        return int(self.lib.dssm_plan_wire_extent(self._plan))
+
+    def set_wire(self, grad_wire: Optional[torch.Tensor], param_wire: Optional[torch.Tensor]):
+        """Attach (or detach, with None) the bf16 gradient / parameter wires: backward() then ends
+        by packing W1's gradient rows into grad_wire, apply_adam() reads the rank's W1 shard from
+        it and writes bf16 parameters into param_wire, wire_shadows() rebuilds W1's shadow from it."""
+        if grad_wire is None and param_wire is None:
+            check(self.lib.dssm_plan_set_wire(self._plan, None, None, 0), "set_wire")
+            return
+        for t in (grad_wire, param_wire):
+            if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.device != self.device:
+                raise ValueError("wires are contiguous bf16 tensors on the model's device")
+        n = min(grad_wire.numel(), param_wire.numel())
+        check(self.lib.dssm_plan_set_wire(self._plan, ptr(grad_wire), ptr(param_wire), n), "set_wire")
+
+    def wire_shadows(self, stream=None):
+        check(self.lib.dssm_plan_wire_shadows(self._plan, stream_ptr(stream)), "wire_shadows")
+
     def train_step(self, stream=None):
         """One sess.run(train_step) (new_dssm.py:267): forward(train) + backward + Adam."""
         check(self.lib.dssm_plan_train_step(self._plan, stream_ptr(stream)), "train_step")

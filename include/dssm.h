@@ -128,6 +128,23 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  * fused W1 Adam must be off.  DSSM_GRAPH_SHADOWS captures dssm_plan_sync_shadows (the shadows of
  * the all-gathered parameters). */
 int dssm_plan_set_adam_range(dssm_plan* plan, int64_t begin, int64_t end);
+/* Data-parallel bf16 wire (perf mode; replaces the fp32 gradient all-reduce of the reference's
+ * single-process optimizer, new_dssm.py:215-217, when the batch is sharded over ranks).  W1's rows
+ * -- arena elements [0, dssm_plan_wire_extent()) -- cross the links as bf16:
+ *   - dssm_plan_backward ends by writing grad_wire[i] = bf16(grad[i]) for those elements (the
+ *     caller reduce-scatters grad_wire in place);
+ *   - dssm_plan_adam then updates the adam-range shard of W1 from grad_wire (x grad_scale) and
+ *     writes bf16(param) of the shard into param_wire (the caller all-gathers it), and updates
+ *     the replicated fp32 tail [extent, param_count) -- b1, W2.., BN -- from the fp32 gradient
+ *     arena (the caller all-reduces that tail first) with its shadows;
+ *   - dssm_plan_wire_shadows (graph part DSSM_GRAPH_WIRE_SHADOWS) rewrites W1's bf16 shadow from
+ *     the all-gathered param_wire.
+ * W1's fp32 master rows outside the rank's shard are then stale (all-gather them for a
+ * checkpoint).  count: elements of each wire (>= extent; the caller pads to equal shards).
+ * Both NULL: off.  Needs bf16 mode and the fused W1 Adam off. */
+int64_t dssm_plan_wire_extent(const dssm_plan* plan);
+int dssm_plan_set_wire(dssm_plan* plan, uint16_t* grad_wire, uint16_t* param_wire, int64_t count);
+int dssm_plan_wire_shadows(dssm_plan* plan, void* stream);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, void* stream);
 
@@ -136,7 +153,7 @@ int dssm_plan_train_step(dssm_plan* plan, void* stream);
  * the gradient collective between the first two).  Replays then cost one launch per step.  with_probes: the graph records the timing
  * probes' events (read back for its last replay with dssm_plan_graph_probe_read).  stream must
  * not be the default stream.  Graphs are owned by the plan. */
-enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2, DSSM_GRAPH_SHADOWS = 4 };
+enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2, DSSM_GRAPH_SHADOWS = 4, DSSM_GRAPH_WIRE_SHADOWS = 8 };
 int dssm_plan_graph_build(dssm_plan* plan, int parts, float grad_scale, int with_probes,
                           void* stream, int* graph_id);
 int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);

@@ -44,6 +44,17 @@ class CpuEngine:
         self.adam_v = torch.from_numpy(self.cpu.flat["v"])
         self.range = (0, self.n_params)
         self._train = None
+        self.gwire = self.pwire = None
+
+    # bf16 wire (include/dssm.h dssm_plan_set_wire): W1's rows, arena [0, D*WIDTHS[0])
+    def wire_extent(self):
+        return D * WIDTHS[0]  # the port's arena starts with W1 [D x L1], like the device layout
+
+    def set_wire(self, gw, pw):
+        self.gwire, self.pwire = gw, pw
+
+    def wire_shadows(self):
+        pass  # fp32 engine: the bf16 W1 shadow is the parameter wire itself
 
     def set_fused_w1_adam(self, on):
         pass
@@ -62,15 +73,28 @@ class CpuEngine:
 
     def backward(self):
         self.loss = self.cpu.forward_backward(self.batch, train=self._train, backward=True)
+        if self.gwire is not None:  # the plan's backward ends by packing W1's gradient rows
+            ext = self.wire_extent()
+            self.gwire[:ext] = self.grads[:ext].to(torch.bfloat16)
 
     def apply_adam(self, grad_scale=1.0):
         # a range step is the full step with the elements outside [begin, end) left as they were
+        # (with the wire: [begin, end) from the bf16 gradient wire plus the replicated tail)
         keep = {r: self.cpu.flat[r].copy() for r in ("p", "m", "v")}
-        self.cpu.adam(grad_scale)
         b, e = self.range
+        if self.gwire is not None:
+            ext = self.wire_extent()
+            self.grads[b:e] = self.gwire[b:e].float()
+        self.cpu.adam(grad_scale)
         for r, old in keep.items():
-            self.cpu.flat[r][:b] = old[:b]
-            self.cpu.flat[r][e:] = old[e:]
+            if self.gwire is not None:
+                self.cpu.flat[r][:b] = old[:b]
+                self.cpu.flat[r][e:ext] = old[e:ext]
+            else:
+                self.cpu.flat[r][:b] = old[:b]
+                self.cpu.flat[r][e:] = old[e:]
+        if self.pwire is not None:
+            self.pwire[b:e] = self.params[b:e].to(torch.bfloat16)
 
 
 def _free_port():
@@ -79,7 +103,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, port, out_dir, mode):
+def _worker(rank, port, out_dir, mode, wire="fp32"):
     os.environ["OMP_NUM_THREADS"] = "2"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
     try:
@@ -87,8 +111,9 @@ def _worker(rank, port, out_dir, mode):
         p0 = O.init_params(cfg, seed=9)
         glob = synth_batch(D, BS, NEG, seed=1234, mean_nnz=16)
         eng = CpuEngine(p0)
-        dp = DataParallel(eng, comm="torch", mode=mode)
+        dp = DataParallel(eng, comm="torch", mode=mode, wire=wire)
         assert dp.world == WORLD and dp.rank == rank and dp.mode == mode
+        assert dp.wire == (wire if mode == "zero" else "fp32")
         eng.set_batch(shard_batch(glob, BS, NEG, rank, WORLD))
         dp.train_step()
         dp.gather_state()
@@ -100,12 +125,14 @@ def _worker(rank, port, out_dir, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["allreduce", "zero"])
-def test_data_parallel_two_ranks_gloo(mode):
+@pytest.mark.parametrize("mode,wire", [("allreduce", "fp32"), ("zero", "fp32"), ("zero", "bf16")])
+def test_data_parallel_two_ranks_gloo(mode, wire):
     """allreduce: all-reduce + replicated Adam; zero: reduce-scatter + Adam on the rank's shard +
-    all-gather of the parameters. Both must give the same step."""
+    all-gather of the parameters, with W1's rows on an fp32 or a bf16 wire. All must give the
+    same step (the bf16 wire within Adam's insensitivity to gradient rounding: a first step
+    moves each element by lr * sign(g) wherever |g| >> eps)."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d, mode), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, mode, wire), nprocs=WORLD, join=True)
         p = [np.load(os.path.join(d, f"p{r}.npy")) for r in range(WORLD)]
         m_ = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(WORLD)]
         ema = [np.load(os.path.join(d, f"ema{r}.npy")) for r in range(WORLD)]

@@ -1,0 +1,87 @@
+"""Data-parallel bf16 wire kernels on one GPU (include/dssm.h dssm_plan_set_wire).
+
+The collectives are the caller's (dssm_amd/dist.py, covered over gloo in test_dist_gloo.py);
+what runs on the device is checked here with world = 1, where the reduce-scatter and
+all-gather are identities:
+* backward() ends by packing bf16(dW1) into the gradient wire (exactly torch's RNE rounding of
+  the materialized fp32 gradient);
+* Adam over a W1 shard reads the wire, updates the shard only, writes bf16(W1) into the
+  parameter wire, and updates the fp32 tail (b1, W2.., BN) as the unwired step does;
+* wire_shadows() rebuilds W1's bf16 shadow: a forward after it equals one after the fp32
+  shadow refresh.
+"""
+import numpy as np
+import pytest
+import torch
+
+from dssm_amd.data import synth_batch
+from tests.test_gpu_parity import make
+
+pytestmark = pytest.mark.gpu
+
+D, WIDTHS, BS, NEG, LR = 5000, (300, 300, 128), 96, 4, 0.01
+
+
+def _wired(m):
+    ext = m.wire_extent()
+    assert ext == D * WIDTHS[0]
+    n = -(-ext // 512) * 512
+    gw = torch.zeros(n, dtype=torch.bfloat16, device=m.device)
+    pw = torch.zeros(n, dtype=torch.bfloat16, device=m.device)
+    pw[:ext].copy_(m.params[:ext])
+    m.set_wire(gw, pw)
+    return ext, gw, pw
+
+
+def _close(a, b):
+    d = (a - b).abs()
+    assert float(d.max()) <= 2 * LR, float(d.max())
+    assert float((d <= 1e-5).float().mean()) >= 0.999, float((d <= 1e-5).float().mean())
+
+
+@pytest.mark.parametrize("shard", ["all", "first_half"])
+def test_wire_step_matches_unwired(shard):
+    _, _, ref = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    ext, gw, pw = _wired(m)
+    end = ext if shard == "all" else (ext // 2) // 64 * 64
+    m.set_adam_range(0, end)
+    p0, m0 = m.params.clone(), m.adam_m.clone()
+    hb = synth_batch(D, BS, NEG, seed=77, mean_nnz=32)
+    for x in (ref, m):
+        x.set_batch(hb)
+        x.forward(True)
+        x.backward()
+    torch.cuda.synchronize()
+    assert torch.equal(gw[:ext], m.grads[:ext].to(torch.bfloat16))
+    ref.apply_adam(1.0)
+    m.apply_adam(1.0)
+    torch.cuda.synchronize()
+    n = m.n_params
+    _close(m.params[:end], ref.params[:end])
+    _close(m.params[ext:n], ref.params[ext:n])
+    torch.testing.assert_close(m.adam_m[ext:n], ref.adam_m[ext:n], rtol=1e-3, atol=1e-6)
+    assert torch.equal(pw[:end], m.params[:end].to(torch.bfloat16))
+    if end < ext:  # outside the shard: untouched
+        assert torch.equal(m.params[end:ext], p0[end:ext])
+        assert torch.equal(m.adam_m[end:ext], m0[end:ext])
+    assert m.beta_powers() == ref.beta_powers()
+
+
+def test_wire_shadows_equal_fp32_refresh():
+    _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    ext, gw, pw = _wired(m)
+    m.set_adam_range(0, ext)
+    hb = synth_batch(D, BS, NEG, seed=78, mean_nnz=32)
+    m.set_batch(hb)
+    m.forward(True)
+    m.backward()
+    m.apply_adam(1.0)
+    m.wire_shadows()
+    m.forward(False)
+    torch.cuda.synchronize()
+    a = m.fetch("cos_sim_raw").copy()
+    m.sync_shadows()
+    m.forward(False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m.fetch("cos_sim_raw"), a)
