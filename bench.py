@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend (gloo: functional rehearsal of N>1 on one GPU)")
     ap.add_argument("--graph", type=int, default=1, help="replay hipGraph-captured steps (0: eager launches)")
+    ap.add_argument("--multi-step", type=int, default=1,
+                    help="N=1 graph mode: one graph holding a step per staged batch (replayed per cycle)")
     ap.add_argument("--probes", type=int, default=1, help="HIP-event kernel probes in the timed region")
     ap.add_argument("--rehearse-world", type=int, default=1,
                     help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
@@ -184,7 +186,7 @@ def main():
         # they are sampled once per len(staged) steps inside the timed region.
         for b, (ip, ix, vv) in enumerate(staged):
             model.set_batch(indptr=ip, indices=ix, values=vv)
-            pr = bool(args.probes) and b == 0
+            pr = bool(args.probes) and b == 0 and (world > 1 or rehearse > 1 or not args.multi_step)
             if world > 1 or rehearse > 1:
                 graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
             else:
@@ -197,6 +199,22 @@ def main():
             shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS if dp.wire == "bf16" else _lib.GRAPH_SHADOWS)
         elif rehearse > 1:
             shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS)
+
+        # single GPU: the staged batches' steps also captured back to back into one graph, replayed
+        # for each full cycle of len(staged) steps (one host launch boundary per cycle; a partial
+        # cycle falls back to the per-step graphs)
+        cycle = (model.graph_build_steps(staged, probes=bool(args.probes))
+                 if (not split and args.multi_step) else None)
+
+        def run_steps(i0, n):
+            i = i0
+            while i < i0 + n:
+                if cycle is not None and i % len(staged) == 0 and i + len(staged) <= i0 + n:
+                    model.graph_launch(cycle)
+                    i += len(staged)
+                else:
+                    step(i)
+                    i += 1
 
         def step(i):
             model.graph_launch(graphs[i % len(graphs)])
@@ -223,8 +241,13 @@ def main():
             elif rehearse > 1:
                 model.wire_shadows()
 
-    for i in range(args.warmup):
-        step(i)
+    if not args.graph:
+        cycle = None
+
+        def run_steps(i0, n):
+            for i in range(i0, i0 + n):
+                step(i)
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if not args.graph and args.probes:
         for _, pid in probe_ids:
@@ -233,8 +256,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -248,7 +270,8 @@ def main():
     probes = {}
     for name, pid in (probe_ids if args.probes else ()):
         if args.graph:  # last replay of every staged-batch graph, all inside the timed region
-            g = adam_graph if (name == "adam" and adam_graph is not None) else graphs[0]
+            g = adam_graph if (name == "adam" and adam_graph is not None) else (
+                cycle if cycle is not None else graphs[0])
             probes[name] = model.graph_probe_read(g, pid)
         else:
             tot, cnt = model.probe_read(pid)

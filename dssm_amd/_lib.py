@@ -64,6 +64,8 @@ _SIGS = {
     "dssm_plan_train_step": (C.c_int, [_P, _P]),
     "dssm_plan_graph_build": (C.c_int, [_P, C.c_int, C.c_float, C.c_int, _P, C.POINTER(C.c_int)]),
     "dssm_plan_graph_launch": (C.c_int, [_P, C.c_int, _P]),
+    "dssm_plan_graph_build_steps": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.c_int,
+                                              C.c_int, _P, C.POINTER(C.c_int)]),
     "dssm_plan_check": (C.c_int, [_P, _P]),
     "dssm_plan_dense_enabled": (C.c_int, [_P]),
     "dssm_plan_fused_stats": (C.c_int, [_P]),

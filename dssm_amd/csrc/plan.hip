@@ -1148,6 +1148,72 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
   return DSSM_OK;
 }
 
+int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
+                                const int32_t* const* indices, const float* const* values,
+                                int nsteps, int with_probes, void* stream, int* graph_id) {
+  if (!P || !graph_id || !indptrs || !indices || !values || nsteps < 1)
+    return fail(DSSM_E_INVALID, "null argument or nsteps < 1");
+  if (!stream) return fail(DSSM_E_INVALID, "graph capture needs a non-default stream");
+  if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
+  for (int i = 0; i < nsteps; ++i)
+    if (!indptrs[i] || (P->Lt.max_nnz && (!indices[i] || !values[i])))
+      return fail(DSSM_E_INVALID, "null batch pointer");
+  hipStream_t s = (hipStream_t)stream;
+  auto* g = new dssm_plan::GraphSlot();
+  g->probes = with_probes != 0;
+  if (g->probes)
+    for (auto& pr : g->ev)
+      for (hipEvent_t& e : pr)
+        if (hipEventCreate(&e) != hipSuccess) {
+          delete g;
+          return fail(DSSM_E_HIP, "hipEventCreate failed");
+        }
+  const int32_t* keep_ip = P->indptr;
+  const int32_t* keep_ix = P->indices;
+  const float* keep_v = P->values;
+  const bool was_fwd = P->fwd_train_done;
+  P->grads_clean = true;  // a replay starts from the state a completed step leaves
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+  }
+  P->capturing = g;
+  int rc = DSSM_OK;
+  for (int i = 0; i < nsteps && !rc; ++i) {
+    // probes (event-record nodes) ride in the first step only
+    g->probes = with_probes != 0 && i == 0;
+    P->indptr = indptrs[i];
+    P->indices = indices[i];
+    P->values = values[i];
+    rc = dssm_plan_train_step(P, stream);
+  }
+  g->probes = with_probes != 0;
+  P->capturing = nullptr;
+  std::string err = rc ? g_err : std::string();
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(s, &graph);
+  P->indptr = keep_ip;
+  P->indices = keep_ix;
+  P->values = keep_v;
+  P->grads_clean = true;
+  P->fwd_train_done = was_fwd;
+  if (rc || e != hipSuccess || !graph) {
+    if (graph) hipGraphDestroy(graph);
+    delete g;
+    return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  }
+  e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+  P->graphs.push_back(g);
+  *graph_id = (int)P->graphs.size() - 1;
+  return DSSM_OK;
+}
+
 int dssm_plan_graph_launch(dssm_plan* P, int graph_id, void* stream) {
   if (!P || graph_id < 0 || graph_id >= (int)P->graphs.size())
     return fail(DSSM_E_INVALID, "bad graph id");

@@ -275,10 +275,27 @@ class DSSM:
         self._graphs[gid.value] = (parts, self._batch_refs)  # keep the batch tensors alive
         return gid.value
 
+    def graph_build_steps(self, batches, probes: bool = False, stream=None) -> int:
+        """Capture len(batches) whole training steps back to back into ONE graph, step i on the
+        device CSR batch (indptr, indices, values) = batches[i]; a replay runs all of them (the
+        host launch boundary is paid once per replay, not once per step)."""
+        sp = stream_ptr(stream)
+        if not sp:
+            raise ValueError("graph capture needs a non-default stream (torch.cuda.Stream())")
+        n = len(batches)
+        arr = [(C.c_void_p * n)(*[ptr(b[k]) for b in batches]) for k in range(3)]
+        gid = C.c_int()
+        check(self.lib.dssm_plan_graph_build_steps(self._plan, arr[0], arr[1], arr[2], n,
+                                                   1 if probes else 0, sp, C.byref(gid)),
+              "graph_build_steps")
+        self._graphs[gid.value] = (_lib.GRAPH_FWD_BWD | _lib.GRAPH_ADAM, tuple(batches), n)
+        return gid.value
+
     def graph_launch(self, gid: int, stream=None):
         check(self.lib.dssm_plan_graph_launch(self._plan, int(gid), stream_ptr(stream)), "graph_launch")
-        if self._graphs[gid][0] & _lib.GRAPH_ADAM:
-            self.global_step += 1
+        g = self._graphs[gid]
+        if g[0] & _lib.GRAPH_ADAM:
+            self.global_step += g[2] if len(g) > 2 else 1
 
     def graph_probe_read(self, gid: int, probe_id: int) -> float:
         ms = C.c_float()

@@ -157,6 +157,13 @@ enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2, DSSM_GRAPH_SHADOWS = 4, DSSM
 int dssm_plan_graph_build(dssm_plan* plan, int parts, float grad_scale, int with_probes,
                           void* stream, int* graph_id);
 int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);
+/* nsteps whole training steps (forward + backward + Adam, as dssm_plan_train_step) captured
+ * back to back into ONE graph, step i on batch (indptrs[i], indices[i], values[i]): a replay
+ * runs them with no host launch boundary between steps.  Probes record the first step only.
+ * The plan's current batch is left as it was. */
+int dssm_plan_graph_build_steps(dssm_plan* plan, const int32_t* const* indptrs,
+                                const int32_t* const* indices, const float* const* values,
+                                int nsteps, int with_probes, void* stream, int* graph_id);
 
 /* Kernel timing probes (bench/roofline): HIP events recorded on the launch stream around one
  * kernel family for up to max_samples launches (0 disables); read back the summed duration. */

@@ -123,3 +123,33 @@ def test_graph_rejects_partial_fused_and_default_stream():
     with torch.cuda.stream(s):
         with pytest.raises(_lib.DssmError):
             m.graph_build(_lib.GRAPH_FWD_BWD)  # fused W1 Adam: the step cannot be split
+
+
+@pytest.mark.parametrize("case", CASES[:2])
+def test_multi_step_graph_matches_eager(case):
+    """graph_build_steps: k whole steps captured back to back in one graph (bench's cycle graph)
+    equal k eager steps on the same batches (free-running over 3 steps: the atomics' rounding
+    noise stays within the per-step bar widened by the step count)."""
+    D, widths, BS, NEG, dtype, fused = case
+    lr, k = 0.01, 3
+    _, _, ea = make(D, widths, BS, NEG, dtype, fused=fused)
+    _, _, gr = make(D, widths, BS, NEG, dtype, fused=fused)
+    batches = _batches(D, BS, NEG, k)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        staged = [tuple(torch.from_numpy(x).cuda() for x in (hb.indptr, hb.indices, hb.values))
+                  for hb in batches]
+        gid = gr.graph_build_steps(staged)
+        assert gr.global_step == 0
+        for ip, ix, vv in staged:
+            ea.set_batch(indptr=ip, indices=ix, values=vv)
+            ea.train_step()
+        gr.graph_launch(gid)
+        torch.cuda.synchronize()
+    assert ea.global_step == gr.global_step == k
+    assert ea.beta_powers() == gr.beta_powers()
+    la, lg = ea.loss_accuracy()[0], gr.loss_accuracy()[0]
+    assert abs(la - lg) <= 1e-3 * abs(la) + 1e-6, (la, lg)
+    d = (ea.params - gr.params).abs()
+    assert float(d.max()) <= 2 * k * lr, float(d.max())
+    assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
