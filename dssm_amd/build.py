@@ -18,6 +18,7 @@ HEADERS = ["common.h", "launch.h"]
 ARCH = os.environ.get("DSSM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+CFLAGS += os.environ.get("DSSM_EXTRA_CFLAGS", "").split()  # diagnostics builds (e.g. -DDSSM_WG_TL)
 
 
 def _mtime(p):

@@ -435,9 +435,15 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
                                                          const float* __restrict__ loss_part,
                                                          int loss_blocks,
                                                          float* __restrict__ loss_out) {
-  // the step's loss / accuracy from the cosine kernel's partials (deferred finalize: no
-  // cross-workgroup ticket in the cosine launch)
-  if (loss_part && blockIdx.x == gridDim.x - 1) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
+  // one extra block past the element blocks: the step's loss / accuracy from the cosine kernel's
+  // partials (deferred finalize: no cross-workgroup ticket in the cosine launch) and dgamma /
+  // dbeta, off the element blocks' critical path
+  const int nwork = (int)gridDim.x - 1;
+  if ((int)blockIdx.x == nwork) {
+    if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
+    fs_materialize_bwd(b);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
   const int ld = b.ld;
   const size_t plane = (size_t)2 * ld;
@@ -481,9 +487,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
       }
     }
   }
-  if (blockIdx.x == 0) fs_materialize_bwd(b);
   __syncthreads();
-  for (size_t i = i0; i < total; i += (size_t)gridDim.x * 256) {
+  for (size_t i = i0; i < total; i += (size_t)nwork * 256) {
     const int r = (int)(i / q);
     const int c = (int)(i - (size_t)r * q) * 4;
     const int t = r < b.rows_q ? 0 : 1;
@@ -603,7 +608,7 @@ hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSi
     return e ? std::max(1, std::atoi(e)) : 1024;
   }();
   const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), gmax);
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid), dim3(256), 0, s, Z, dA, b, (u16*)dZ, loss_part,
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid + 1), dim3(256), 0, s, Z, dA, b, (u16*)dZ, loss_part,
                      loss_blocks, loss_out);
   return hipGetLastError();
 }

@@ -55,7 +55,12 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   const int j = blockIdx.x * 4 + wv;
   const int K = neg + 1;
   const size_t plane = (size_t)2 * ld;
+  const int nrow_blocks = (bs + 3) / 4;
   if constexpr (FSC) {
+    if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
+      fs_materialize_fwd(fs);
+      return;
+    }
     fs_coef_stage<(2 * kCosMaxN) / 256>(fs, threadIdx.x, 256,
                                           [&](int t, int c, float mu, float rs, float inv, float sh) {
       s_co[(t * 4 + 0) * kCosMaxN + c] = mu;
@@ -63,7 +68,6 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
       s_co[(t * 4 + 2) * kCosMaxN + c] = inv;
       s_co[(t * 4 + 3) * kCosMaxN + c] = sh;
     });
-    if (blockIdx.x == 0) fs_materialize_fwd(fs);
     __syncthreads();
   }
   stamp();
@@ -262,8 +266,8 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     stamp();
   }
   if (split) return;  // k_loss_finalize sums the partials in its own launch
-  if (!last_block_arrival(ticket, gridDim.x, &s_flag)) return;
-  loss_finalize(part, (int)gridDim.x, bs, loss_out);
+  if (!last_block_arrival(ticket, nrow_blocks, &s_flag)) return;
+  loss_finalize(part, nrow_blocks, bs, loss_out);
 }
 
 __global__ __launch_bounds__(64) void k_loss_finalize(const float* __restrict__ part, int nblk,
@@ -284,7 +288,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
   unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * blocks + 32);
-  dim3 grid(blocks), block(256);
+  dim3 grid(blocks + (fused ? 1 : 0)), block(256);  // fused: + the materialising block
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \

@@ -24,6 +24,21 @@ namespace {
 
 constexpr int BM = 64, BN = 64;
 
+// Diagnostics build only (-DDSSM_WG_TL): per-workgroup start / end stamps (s_memrealtime,
+// 100 MHz) of the dense GEMM launches, read back by dssm_debug_wg_timeline (tools/wg_timeline.py).
+#ifdef DSSM_WG_TL
+__device__ unsigned long long g_wg_tl[4][2048][2];
+#define WG_TL(slot, idx)                                                                    \
+  do {                                                                                      \
+    if (threadIdx.x == 0)                                                                   \
+      g_wg_tl[slot][(blockIdx.y * gridDim.x + blockIdx.x) & 2047][idx] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define WG_TL(slot, idx) \
+  do {                   \
+  } while (0)
+#endif
+
 template <typename T> struct Cfg;
 template <> struct Cfg<u16> { static constexpr int BK = 64, PAD = 8; };    // 144-B LDS rows
 template <> struct Cfg<float> { static constexpr int BK = 32, PAD = 4; };  // 144-B LDS rows
@@ -564,7 +579,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         sCoef[(tw * 2 + 0) * Kp + k] = 0.f;
         sCoef[(tw * 2 + 1) * Kp + k] = 0.f;
       }
-      if (tx == 0 && ty == 0) fs_materialize_fwd(f.in);
     } else {
       const size_t plane = (size_t)2 * lda;
       for (int i = t; i < 2 * Kp; i += 512) {
@@ -709,10 +723,32 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   }
 }
 
+// Block b -> tile: tiles [x n/8, (x+1) n/8) go to the blocks b = x (mod 8), which the observed
+// round-robin dispatch places on one XCD (speed only, never correctness: any placement computes
+// the same tiles).  Consecutive tiles share their A rows (a row block's column tiles) or their
+// batch-row chunk (dW), so those re-reads hit that XCD's L2 instead of the Infinity Cache.
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+  return (n % 8) ? b : (b % 8) * (n / 8) + b / 8;
+}
+
+// Whole-K forward NT GEMM: blocks [0, ntiles) compute tiles (XCD-grouped row blocks); with the
+// A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
+// EMA update) off the tiles' critical path.
 template <bool BN_A, int FS>
-__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f) {
+__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
-  nt_wk_body<BN_A, FS>(a, f, blockIdx.x, blockIdx.y, wk_smem);
+  WG_TL(a.N == 300 ? 0 : 1, 0);
+  if ((int)blockIdx.x >= ntiles) {
+    if (BN_A && FS == 1 && f.in_from_sums) fs_materialize_fwd(f.in);
+    return;
+  }
+  const int tile = xcd_tile(blockIdx.x, ntiles);
+  nt_wk_body<BN_A, FS>(a, f, tile % nx, tile / nx, wk_smem);
+#ifdef DSSM_WG_TL
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  WG_TL(a.N == 300 ? 0 : 1, 1);
+#endif
 }
 
 // "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
@@ -975,12 +1011,21 @@ __global__ __launch_bounds__(512) void k_bwd_pair_wk(NtParams a, NtFuse f, int n
                                                      TnParams p, int tn_x, int tn_y) {
   extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
   const int b = blockIdx.x;
+  WG_TL(a.K == 300 ? 3 : 2, 0);
   if (b < nt_blocks) {
-    nt_wk_body<false, 2>(a, f, b % nt_x, b / nt_x, pw_smem);
+    const int tile = xcd_tile(b, nt_blocks);
+    nt_wk_body<false, 2>(a, f, tile % nt_x, tile / nt_x, pw_smem);
   } else {
-    const int r = b - nt_blocks;
+    // XCD grouping of the dW tiles needs the dA range to end on a multiple of 8
+    const int nr = (int)gridDim.x - nt_blocks;
+    const int r = (nt_blocks % 8) ? b - nt_blocks : xcd_tile(b - nt_blocks, nr);
     tn_wk_body(p, r % tn_x, (r / tn_x) % tn_y, r / (tn_x * tn_y), pw_smem, f.tm ? f.tm - 128 + 64 : nullptr);
   }
+#ifdef DSSM_WG_TL
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  WG_TL(a.K == 300 ? 3 : 2, 1);
+#endif
 }
 
 // One launch for the two backward GEMMs of layer l that both consume dZ_l: the dA tiles
@@ -1112,8 +1157,9 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   }();
   if (wk_on && K <= kWkMaxK && (row_split % 128) == 0) {
     const int Kp = (K + 31) & ~31;
-    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 128)), dim3(512),
-                       wk_smem_bytes(Kp), s, a, f);
+    const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 128);
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0)), dim3(512),
+                       wk_smem_bytes(Kp), s, a, f, nx, ntiles);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);
@@ -1212,3 +1258,11 @@ hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_WG_TL
+extern "C" int dssm_debug_wg_timeline(int slot, unsigned long long* out, int n) {
+  if (slot < 0 || slot >= 4 || n > 2048) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_wg_tl), sizeof(unsigned long long) * 2 * n,
+                             sizeof(unsigned long long) * 2 * 2048 * slot) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -1,0 +1,44 @@
+"""Per-workgroup start/end timeline of the dense GEMM launches (diagnostics build only).
+
+On the GPU box:  DSSM_EXTRA_CFLAGS=-DDSSM_WG_TL python -m dssm_amd.build --force &&
+                 python tools/wg_timeline.py
+Slots: 0 = forward NT GEMM N=300 (layer 2), 1 = forward NT GEMM N=128 (layer 3),
+2 = backward pair of layer 3 (dA K=128), 3 = backward pair of layer 2 (K=300)."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from dssm_amd import _lib
+from dssm_amd.data import ZipfColumns, synth_batch
+from dssm_amd.model import DSSM
+
+D, W, BS, NEG = 30000, (300, 300, 128), 1024, 4
+m = DSSM(D, W, BS, NEG, dtype="bf16")
+b = synth_batch(D, BS, NEG, seed=1000, cols=ZipfColumns(D))
+m.set_batch(b)
+for _ in range(5):
+    m.train_step()
+torch.cuda.synchronize()
+lib = _lib.load()
+f = lib.dssm_debug_wg_timeline
+f.restype = C.c_int
+f.argtypes = [C.c_int, C.c_void_p, C.c_int]
+grids = {0: 5 * 48, 1: 2 * 48, 2: None, 3: None}
+for slot, name in enumerate(("nt L2 (N=300)", "nt L3 (N=128)", "pair L3", "pair L2")):
+    buf = np.zeros((2048, 2), np.uint64)
+    assert f(slot, buf.ctypes.data, 2048) == 0
+    n = int(np.sum(buf[:, 0] > 0))
+    t = buf[:n].astype(np.int64)
+    t0 = t[:, 0].min()
+    st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
+    dur = en - st
+    print(f"{name}: {n} WGs, span {en.max():.2f} us; start spread {st.max():.2f} us; "
+          f"WG duration min/median/max {dur.min():.2f}/{np.median(dur):.2f}/{dur.max():.2f} us; "
+          f"last end {en.max():.2f}")
+    order = np.argsort(st)
+    print("   starts (us, by start order, every 16th):", " ".join(f"{x:.1f}" for x in st[order][::16]))
+    print("   ends   (us, same WGs):                ", " ".join(f"{x:.1f}" for x in en[order][::16]))
