@@ -28,6 +28,20 @@
 namespace dssm {
 namespace {
 
+// Diagnostics build only (-DDSSM_WG_TL): per-workgroup start / end stamps of k_adam_step
+// (s_memrealtime, 100 MHz), read back by dssm_debug_adam_timeline (tools/wg_timeline.py).
+#ifdef DSSM_WG_TL
+__device__ unsigned long long g_adam_tl[8192][2];
+#define ADAM_TL(idx)                                                                          \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_adam_tl[blockIdx.x][idx] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define ADAM_TL(idx) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, float4 v) {
 #pragma unroll 1
   for (int s = 0; s < sh.count; ++s) {
@@ -158,14 +172,14 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
 // the row with atomic exchanges (read and clear at the coherence point), updates it and
 // re-arms the ticket.
 template <typename TZ>
-__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha) {
+__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb) {
   __shared__ float part[4][512];
   __shared__ float grow[512];
   __shared__ int s_last;
   const int wv = threadIdx.x >> 6, lane = lane_id();
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   const int nitems = *a.heavy_n;
-  for (int it = blockIdx.x; it < nitems; it += a.item_blocks) {
+  for (int it = hb; it < nitems; it += a.item_blocks) {
     const int2 item = a.heavy_items[it];
     const int c = item.x;
     const int cs = a.col_ptr[c], ce = a.col_ptr[c + 1];
@@ -220,16 +234,37 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha) {
 // the ticket.
 template <typename TZ>
 __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
+  ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  if ((int)blockIdx.x < a.item_blocks) {
-    heavy_items<TZ>(a, alpha);
-  } else if ((int)blockIdx.x < a.item_blocks + a.w1_blocks) {
-    const int b = blockIdx.x - a.item_blocks;
+  // Block roles.  Dispatch is in block order: the heavy-item blocks (the longest dependent
+  // chains) come first; the W1-row gather blocks and the flat/dense streaming blocks follow,
+  // either contiguous (interleave == 0) or interleaved in proportion (Bresenham over the block
+  // index) so every CU runs latency-bound gathers beside HBM streaming from the start.
+  const int64_t nb = gridDim.x, b0 = blockIdx.x;
+  const int nh = a.item_blocks, nw = a.w1_blocks;
+  const int nf = (int)nb - nh - nw;
+  const bool is_heavy = b0 < nh;
+  const int hcount = (int)(is_heavy ? b0 : nh);
+  const int64_t j = b0 - hcount;  // index among the other roles
+  const int64_t nwf = nw + nf;
+  int wcount;
+  bool is_w1;
+  if (a.interleave) {
+    wcount = nwf ? (int)(j * nw / nwf) : 0;
+    is_w1 = !is_heavy && nwf && (j + 1) * nw / nwf > wcount;
+  } else {
+    is_w1 = !is_heavy && j < nw;
+    wcount = (int)(j < nw ? j : nw);
+  }
+  if (is_heavy) {
+    heavy_items<TZ>(a, alpha, hcount);
+  } else if (is_w1) {
+    const int b = wcount;
     for (int c = b * 4 + (threadIdx.x >> 6); c <= a.D; c += a.w1_blocks * 4)
       w1_row<TZ>(a, c, alpha);
   } else {
-    const int bi = blockIdx.x - a.item_blocks - a.w1_blocks;
+    const int bi = (int)(j - wcount);
     if (a.w1_flat) {
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
       const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
@@ -290,7 +325,11 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       }
     }
   }
+#ifdef DSSM_WG_TL
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
+  ADAM_TL(1);
   if (threadIdx.x == 0 && a.ticket) {
     // Two-level ticket: same-address atomics serialise (~6 ns each; one counter for ~8k blocks
     // measured +45 us), so blocks arrive on kAdamSubTickets counters 256 B apart and only the
@@ -307,6 +346,9 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       if (u == ntop - 1) {
         a.st[0] = b1p * a.beta1;
         a.st[1] = b2p * a.beta2;
+        // every block has read this step's heavy-item count: re-arm it for the next step's scan
+        // (the next step's rank launch may already be running beside this one)
+        if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -315,10 +357,11 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
 
 // beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32): the separate-
 // launch variant (A/B knob DSSM_ADAM_SEP_ADVANCE=1)
-__global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2) {
+__global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2, int* heavy_reset) {
   if (threadIdx.x == 0) {
     st[0] = st[0] * beta1;
     st[1] = st[1] * beta2;
+    if (heavy_reset) *heavy_reset = 0;
   }
 }
 
@@ -400,6 +443,11 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     const char* e = std::getenv("DSSM_ADAM_ITEM_BLOCKS");
     return e ? std::max(1, std::atoi(e)) : kAdamItemBlocks;
   }();
+  static const int interleave = [] {
+    const char* e = std::getenv("DSSM_ADAM_INTERLEAVE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.interleave = interleave;
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, item_cap);
   a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0) ? 1 : 0;
@@ -412,7 +460,8 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
-  if (!a.ticket) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2);
+  if (!a.ticket)
+    hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2, a.heavy_reset);
   return hipGetLastError();
 }
 
@@ -438,3 +487,11 @@ hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s) {
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_WG_TL
+extern "C" int dssm_debug_adam_timeline(unsigned long long* out, int n) {
+  if (n > 8192) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_adam_tl), sizeof(unsigned long long) * 2 * n, 0) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif

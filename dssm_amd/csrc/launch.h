@@ -29,7 +29,8 @@ constexpr int kHeavyItem = 256;
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
-                            int nzero = 0, bool rank_path = true, bool rank_only = false);
+                            int nzero = 0, bool rank_path = true, bool rank_only = false,
+                            bool reset_heavy = true);
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
@@ -216,6 +217,10 @@ struct AdamStep {
   uint16_t* pwire;
   int64_t wire4;
   int64_t t4_begin, t4_end;
+  // role layout after the heavy-item blocks (0: contiguous, 1: interleaved; DSSM_ADAM_INTERLEAVE)
+  int interleave;
+  // zeroed once every block has read heavy_n (the next step's rank launch does not reset it)
+  int* heavy_reset;
 };
 constexpr int kAdamItemBlocks = 512;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);

@@ -222,6 +222,11 @@ struct dssm_plan {
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
   bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
+  // multi-step graphs: the next step's CSC rank launch runs on the side stream beside this step's
+  // Adam (DSSM_RANK_PREFETCH=1; measured slower: the cross-stream fork / join in the graph costs
+  // more than the rank launch it hides); the forward of that batch then skips its rank launch
+  bool rank_prefetch = false;
+  const int32_t* rank_prefetched = nullptr;
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
   int dw_deferred[DSSM_MAX_LAYERS] = {};  // split count of dW_l left in its slab (fused mode)
@@ -519,6 +524,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
       P->copies_cos = std::max(1, std::min(kSumCopies, c));
     }
   }
+  if (const char* e = std::getenv("DSSM_RANK_PREFETCH")) P->rank_prefetch = e[0] != '0';
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
     P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
@@ -680,6 +686,9 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     const bool clear = P->fused_stats && !P->dense_on;
     if (clear && !P->csc_inline)
       HIP_TRY(hipMemsetAsync(P->ws + Lt.dense_sums, 0, Lt.dense_sums_bytes, s));
+    if (P->rank_prefetched == P->indptr && P->merged_csc()) {
+      P->rank_prefetched = nullptr;  // launched beside the previous step's Adam
+    } else
     HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
@@ -965,6 +974,7 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
       a.heavy_n = dssm::csc_heavy_count(scr, Lt.D, Lt.max_nnz);
       a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
       a.heavy_ticket = dssm::csc_heavy_tickets(scr, Lt.D, Lt.R, Lt.max_nnz);
+      a.heavy_reset = const_cast<int*>(a.heavy_n);
     }
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
@@ -1180,14 +1190,44 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   }
   P->capturing = g;
   int rc = DSSM_OK;
+  const bool prefetch = P->rank_prefetch && P->merged_csc() && P->fused_w1_adam && P->heavy_in_adam();
+  P->rank_prefetched = nullptr;
   for (int i = 0; i < nsteps && !rc; ++i) {
     // probes (event-record nodes) ride in the first step only
     g->probes = with_probes != 0 && i == 0;
     P->indptr = indptrs[i];
     P->indices = indices[i];
     P->values = values[i];
-    rc = dssm_plan_train_step(P, stream);
+    rc = dssm_plan_forward(P, 1, stream);
+    if (!rc) rc = dssm_plan_backward(P, stream);
+    if (rc) break;
+    const bool pf = prefetch && i + 1 < nsteps;
+    if (pf) {
+      // step i+1's rank launch (its batch only; it also clears the BN sums, whose last reader,
+      // this step's backward, is complete) on the side stream beside this step's Adam, which
+      // re-arms the heavy-item count once every block has read it
+      const Layout& Lt = P->Lt;
+      hipError_t he = hipEventRecord(P->ev_batch, s);
+      if (he == hipSuccess) he = hipStreamWaitEvent(P->side, P->ev_batch, 0);
+      if (he == hipSuccess)
+        he = dssm::launch_csc_build(indptrs[i + 1], indices[i + 1], values[i + 1], Lt.R, Lt.D,
+                                    Lt.max_nnz, P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
+                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
+                                    P->at<int>(Lt.csc_col), P->side, P->at<double>(Lt.dense_sums),
+                                    (int)(Lt.dense_sums_bytes / 8), true, true, /*reset_heavy=*/false);
+      if (he == hipSuccess) he = hipEventRecord(P->ev_csc, P->side);
+      if (he != hipSuccess) {
+        rc = fail(DSSM_E_HIP, std::string("rank prefetch: ") + hipGetErrorString(he));
+        break;
+      }
+    }
+    rc = dssm_plan_adam(P, 1.0f, stream);
+    if (!rc && pf) {
+      if (hipStreamWaitEvent(s, P->ev_csc, 0) != hipSuccess) rc = fail(DSSM_E_HIP, "rank prefetch join");
+      P->rank_prefetched = indptrs[i + 1];
+    }
   }
+  P->rank_prefetched = nullptr;
   g->probes = with_probes != 0;
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();

@@ -361,7 +361,8 @@ __global__ __launch_bounds__(kTB) void k_csc_rank(const int* __restrict__ indptr
   for (int i = blockIdx.x * kTB + t; i < nzero; i += gridDim.x * kTB) zero[i] = 0.0;
   for (int c = t; c < D; c += kTB) hist[c] = 0;
   if (t == 0) s_nlist = 0;
-  if (blockIdx.x == 0 && t == 0) *heavy_n = 0;  // this step's heavy-item list (k_csc_scan_multi)
+  // this step's heavy-item list (k_csc_scan_multi); null when the previous step's Adam re-arms it
+  if (heavy_n && blockIdx.x == 0 && t == 0) *heavy_n = 0;
   __syncthreads();
   const int e0 = indptr[r0], e1 = indptr[max(r0, r1)];
   for (int base = e0; base < e1; base += kTB * kTU) {
@@ -844,7 +845,7 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero,
-                            int nzero, bool rank_path, bool rank_only) {
+                            int nzero, bool rank_path, bool rank_only, bool reset_heavy) {
   int* cnt = scratch;  // zero between steps (re-zeroed by k_csc_scan / k_csc_scatter)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
@@ -855,7 +856,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     const int rpb = cdiv(rows, kCscRankBlocks);
     const int grid = cdiv(rows, rpb);
     hipLaunchKernelGGL(k_csc_rank, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb, cnt,
-                       rank_tmp, zero, nzero, heavy_n);
+                       rank_tmp, zero, nzero, reset_heavy ? heavy_n : nullptr);
     if (rank_only) return hipGetLastError();  // scan and scatter ride in later launches
     hipLaunchKernelGGL(k_csc_scan_multi, dim3(cdiv(D + 1, kScanMultiCols)), dim3(kTB), 0, s, cnt, D,
                        rows, col_ptr, heavy_n, heavy_items);

@@ -42,3 +42,31 @@ for slot, name in enumerate(("nt L2 (N=300)", "nt L3 (N=128)", "pair L3", "pair 
     order = np.argsort(st)
     print("   starts (us, by start order, every 16th):", " ".join(f"{x:.1f}" for x in st[order][::16]))
     print("   ends   (us, same WGs):                ", " ".join(f"{x:.1f}" for x in en[order][::16]))
+
+# k_adam_step: roles by block index (heavy items, W1 rows, flat/dense streaming); the launch
+# geometry is recomputed the way launch_adam_step sizes it
+g = lib.dssm_debug_adam_timeline
+g.restype = C.c_int
+g.argtypes = [C.c_void_p, C.c_int]
+buf = np.zeros((8192, 2), np.uint64)
+assert g(buf.ctypes.data, 8192) == 0
+n = int(np.sum(buf[:, 0] > 0))
+t = buf[:n].astype(np.int64)
+t0 = t[:, 0].min()
+st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
+items, w1 = 512, 2048  # kAdamItemBlocks, kAdamW1Blocks: roles interleaved as k_adam_step assigns them
+b = np.arange(n, dtype=np.int64)
+hc = b * items // n
+heavy = (b + 1) * items // n > hc
+j = b - hc
+wc = j * w1 // (n - items)
+w1r = ~heavy & ((j + 1) * w1 // (n - items) > wc)
+for name, sel in (("heavy items", heavy), ("W1 rows", w1r), ("flat/dense", ~heavy & ~w1r)):
+    if not sel.any():
+        continue
+    d = en[sel] - st[sel]
+    print(f"adam {name}: blocks {int(sel.sum())}, start {st[sel].min():.1f}..{st[sel].max():.1f} us, "
+          f"end {en[sel].min():.1f}..{en[sel].max():.1f} us, duration median {np.median(d):.2f} max {d.max():.2f}")
+print(f"adam span {en.max():.1f} us over {n} blocks")
+hist = np.histogram(en, bins=12)[0]
+print("  block ends histogram (12 bins over the span):", hist.tolist())
