@@ -54,6 +54,10 @@ def parse():
                     help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
                          "(unfused dW1, wire pack, 1/W Adam shard, wire shadows) with the "
                          "collectives omitted, to time the per-rank compute of the N>1 path")
+    ap.add_argument("--feed", default="device", choices=["device", "host"],
+                    help="device: batches staged in HBM before the timed region (the headline); host: "
+                         "batches streamed from host CSR matrices by the native pinned async feeder "
+                         "inside the timed region (PCIe-inclusive rate, N=1)")
     ap.add_argument("--wire", default="auto", choices=["auto", "bf16", "fp32"],
                     help="zero schedule: W1 rows on a bf16 or fp32 wire (auto: bf16 in bf16 mode)")
     return ap.parse_args()
@@ -177,7 +181,39 @@ def main():
                  ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC))
 
 
-    if args.graph:
+    feeder = None
+    if args.feed == "host":
+        if world > 1 or rehearse > 1 or not args.graph:
+            raise SystemExit("--feed host is the N=1 graph-mode measurement")
+        # the staged batches re-laid out as the reference's three host CSR matrices; the native
+        # feeder assembles each step's combined CSR in pinned memory and copies it on its own
+        # stream while the previous step runs; one captured step per feeder slot
+        import scipy.sparse as sps
+        from dssm_amd.data import csr_rows_slice
+        from dssm_amd.feed import Feeder
+        hosts = [synth_batch(D, BS, NEG, seed=1000 + b, cols=cols) for b in range(args.batches)]
+        mats = []
+        for r0, r1 in ((0, BS), (BS, 2 * BS), (2 * BS, BS * (2 + NEG))):
+            parts = [csr_rows_slice(h, r0, r1) for h in hosts]
+            mats.append(sps.vstack([sps.csr_matrix((p.values, p.indices, p.indptr), shape=(r1 - r0, D))
+                                    for p in parts]).tocsr())
+        feeder = Feeder(*mats, BS, NEG, max_nnz=model.max_nnz)
+        gslots = []
+        for slot in range(2):
+            feeder.start(slot)
+            feeder.next(model)
+            gslots.append(model.graph_build(probes=bool(args.probes) and slot == 0))
+            feeder.done()
+        torch.cuda.synchronize()
+        feeder.start(0)
+        graphs, adam_graph, cycle = gslots, None, None
+
+        def run_steps(i0, n):
+            for i in range(i0, i0 + n):
+                feeder.next(model, next_batch=(i + 1) % args.batches)
+                model.graph_launch(gslots[feeder._cur])
+                feeder.done()
+    elif args.graph:
         # One captured step per staged batch (the batch pointers are baked into the graph); with
         # N>1 the all-reduce runs between the fwd+bwd graph and the Adam graph.  Timing probes
         # are event nodes inside the graphs (their last replay is read after the timed region).
@@ -241,7 +277,7 @@ def main():
             elif rehearse > 1:
                 model.wire_shadows()
 
-    if not args.graph:
+    if not args.graph and feeder is None:
         cycle = None
 
         def run_steps(i0, n):
@@ -324,7 +360,9 @@ def main():
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
-                   "dp_exchange": (f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) if dp is not None else None},
+                   "dp_exchange": (f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) if dp is not None else None,
+                   "feed": "host CSR -> pinned async H2D (native feeder), PCIe inside the timed region"
+                           if feeder is not None else "device-resident staged batches"},
         "roofline": dict(rl[dominant], kernel=dominant),
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,
@@ -338,6 +376,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": repr(e)}
+    if feeder is not None:
+        feeder.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dp is not None and dp.comm is not None:

@@ -87,6 +87,23 @@ _SIGS = {
                                    C.c_float, C.c_int, C.c_int, _P, C.c_int, _P, _P, _P, _P]),
     "dssm_cosine_softmax_loss": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, _P,
                                            _P, _P, _P, _P, _P, _P, _P]),
+    "dssm_text_clean": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "dssm_vocab_create": (C.c_int, [C.POINTER(_P)]),
+    "dssm_vocab_destroy": (C.c_int, [_P]),
+    "dssm_vocab_fit": (C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int64]),
+    "dssm_vocab_finalize": (C.c_int64, [_P]),
+    "dssm_vocab_size": (C.c_int64, [_P]),
+    "dssm_vocab_name": (C.c_int, [_P, C.c_int64, C.c_char_p, C.c_size_t]),
+    "dssm_vocab_add": (C.c_int, [_P, C.c_char_p]),
+    "dssm_vocab_transform": (C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int64, _P, _P, _P, C.c_int64,
+                                       C.POINTER(C.c_int64)]),
+    "dssm_feeder_create": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int64),
+                                     C.c_int, C.c_int, C.c_int64, C.c_int, C.POINTER(_P)]),
+    "dssm_feeder_submit": (C.c_int, [_P, C.c_int, C.c_int64]),
+    "dssm_feeder_acquire": (C.c_int, [_P, C.c_int, _P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P),
+                                      C.POINTER(C.c_int64)]),
+    "dssm_feeder_release": (C.c_int, [_P, C.c_int, _P]),
+    "dssm_feeder_destroy": (C.c_int, [_P]),
     "dssm_comm_unique_id": (C.c_int, [_P]),
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),

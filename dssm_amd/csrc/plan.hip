@@ -430,6 +430,10 @@ struct dssm_plan {
   }
 };
 
+namespace dssm {
+int report_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
+}  // namespace dssm
+
 extern "C" {
 
 int dssm_abi_version(void) { return DSSM_ABI_VERSION; }

@@ -1,0 +1,237 @@
+"""Host data path: raw comment TSV -> sparse feeds -> device CSR.
+
+Mirrors the reference's pipeline with its names:
+
+* ``pre_process`` (utils/utils.py:424-437) and the tokenisation / vocabulary / counting of
+  ``CountVectorizer(token_pattern=r"(?u)\\b\\w+\\b")`` (new_dssm.py:37-45) run natively in
+  libdssm.so (``dssm_text_clean``, ``dssm_vocab_*``); ``TextVectorizer`` has sklearn's
+  fit / transform / get_feature_names / vocabulary_ surface and returns scipy CSR matrices, so
+  ``pull_batch`` and ``convert_sparse_matrix_to_sparse_tensor`` (dssm_amd.data) work on them
+  unchanged.  The vectorizer is saved as a JSON feature list, not a pickle (save_vectorizer,
+  utils/utils.py:241-261).
+* ``get_data_set_comment`` (utils/utils.py:368-421): TSV lines ``prefix \\t title \\t label \\t mid
+  \\t feed_id`` with label '1', one space-separated character per token, NEG negatives per query
+  drawn from the other docs (doc != positive, query differs, no repeats).  The reference draws
+  them with ``random.random()`` into a ``set`` (order depends on the string hash seed, SURVEY
+  Appendix B.3) and can loop forever; here they come from a seeded PCG64 in draw order, and a
+  query with too few eligible docs raises.
+* ``Feeder``: the step's combined CSR [q; pos; neg] of batch b assembled from the three CSR
+  matrices by a native worker thread into pinned memory and copied on its own HIP stream
+  (``dssm_feeder_*``), double-buffered so batch b+1's H2D overlaps step b; ``DSSM.set_batch``
+  then points the plan at the device slot (no host synchronisation on the step path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+from typing import List, Sequence
+
+import numpy as np
+import scipy.sparse as sps
+
+from . import _lib
+from ._lib import check
+
+
+def _cstrs(texts: Sequence[str]):
+    enc = [t.encode("utf8") for t in texts]
+    arr = (C.c_char_p * max(1, len(enc)))(*enc)
+    return arr, enc
+
+
+def pre_process(line):
+    """utils/utils.py:424-437 (native)."""
+    if line is None:
+        return line
+    lib = _lib.load()
+    b = line.encode("utf8")
+    n = C.c_size_t()
+    check(lib.dssm_text_clean(b, None, 0, C.byref(n)), "text_clean")
+    out = C.create_string_buffer(n.value + 1)
+    check(lib.dssm_text_clean(b, out, n.value + 1, C.byref(n)), "text_clean")
+    return out.raw[:n.value].decode("utf8")
+
+
+class TextVectorizer:
+    """CountVectorizer(token_pattern=r"(?u)\\b\\w+\\b") for pre_processed text (native)."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        check(self.lib.dssm_vocab_create(C.byref(h)), "vocab_create")
+        self._h = h
+        self._names: List[str] = []
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self.lib.dssm_vocab_destroy(self._h)
+            self._h = None
+
+    def fit(self, raw_documents: Sequence[str]):
+        arr, _keep = _cstrs(raw_documents)
+        check(self.lib.dssm_vocab_fit(self._h, arr, len(raw_documents)), "vocab_fit")
+        n = self.lib.dssm_vocab_finalize(self._h)
+        if n < 0:
+            check(int(n), "vocab_finalize")
+        self._names = [self._name(i) for i in range(int(n))]
+        return self
+
+    def _name(self, i: int) -> str:
+        buf = C.create_string_buffer(256)
+        k = self.lib.dssm_vocab_name(self._h, i, buf, 256)
+        if k < 0:
+            check(k, "vocab_name")
+        if k >= 256:
+            buf = C.create_string_buffer(k + 1)
+            self.lib.dssm_vocab_name(self._h, i, buf, k + 1)
+        return buf.raw[:k].decode("utf8")
+
+    def get_feature_names(self) -> List[str]:
+        return list(self._names)
+
+    get_feature_names_out = get_feature_names
+
+    @property
+    def vocabulary_(self):
+        return {t: i for i, t in enumerate(self._names)}
+
+    def transform(self, raw_documents: Sequence[str]) -> sps.csr_matrix:
+        n = len(raw_documents)
+        arr, _keep = _cstrs(raw_documents)
+        indptr = np.zeros(n + 1, np.int64)
+        nnz = C.c_int64()
+        ip = indptr.ctypes.data_as(C.c_void_p)
+        check(self.lib.dssm_vocab_transform(self._h, arr, n, ip, None, None, 0, C.byref(nnz)), "transform")
+        indices = np.zeros(max(1, nnz.value), np.int32)
+        values = np.zeros(max(1, nnz.value), np.float32)
+        check(self.lib.dssm_vocab_transform(self._h, arr, n, ip, indices.ctypes.data_as(C.c_void_p),
+                                            values.ctypes.data_as(C.c_void_p), nnz.value,
+                                            C.byref(nnz)), "transform")
+        k = nnz.value
+        return sps.csr_matrix((values[:k], indices[:k], indptr), shape=(n, len(self._names)))
+
+    def fit_transform(self, raw_documents):
+        return self.fit(raw_documents).transform(raw_documents)
+
+    # save_vectorizer / load_vectorizer (utils/utils.py:241-261), as JSON
+    def save(self, path: str):
+        with open(path, "w", encoding="utf8") as f:
+            json.dump({"format": "dssm_amd.TextVectorizer/1", "features": self._names}, f, ensure_ascii=False)
+
+    @classmethod
+    def load(cls, path: str) -> "TextVectorizer":
+        with open(path, encoding="utf8") as f:
+            d = json.load(f)
+        v = cls()
+        for name in d["features"]:
+            check(v.lib.dssm_vocab_add(v._h, name.encode("utf8")), "vocab_add")
+        v._names = list(d["features"])
+        return v
+
+
+def save_vectorizer(vectorizer: TextVectorizer, path: str = "output/vectorizer_data.json"):
+    vectorizer.save(path)
+
+
+def load_vectorizer(path: str = "output/vectorizer_data.json") -> TextVectorizer:
+    return TextVectorizer.load(path)
+
+
+def get_data_set_comment(FileName: str, conf, seed: int = 0, max_draws: int = 100000):
+    """utils/utils.py:368-421 with seeded, ordered negatives (module doc)."""
+    query, doc = [], []
+    with open(FileName, encoding="utf8") as f:
+        for line in f.readlines():
+            spline = line.split("\t")
+            if len(spline) < 3:
+                continue
+            prefix, title, label, mid, feed_id = spline  # the reference's unpacking (5 fields)
+            if label != "1":
+                continue
+            query.append(" ".join(pre_process(prefix)))
+            doc.append(" ".join(pre_process(title)))
+    return query, doc, sample_negatives(query, doc, conf.NEG, seed, max_draws)
+
+
+def sample_negatives(query: Sequence[str], doc: Sequence[str], neg: int, seed: int = 0,
+                     max_draws: int = 100000) -> List[str]:
+    """NEG negatives per query j, at rows j*NEG .. j*NEG+NEG-1 (utils/utils.py:403-419)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    size = len(doc)
+    out: List[str] = []
+    for i in range(size):
+        picked: List[str] = []
+        draws = 0
+        while len(picked) < neg:
+            r = int(rng.random() * size)
+            cand = doc[r]
+            if cand != doc[i] and query[i] != query[r] and cand not in picked:
+                picked.append(cand)
+            draws += 1
+            if draws > max_draws:
+                raise ValueError(f"query {i}: fewer than NEG={neg} eligible negative docs")
+        out.extend(picked)
+    return out
+
+
+class Feeder:
+    """Pinned, double-buffered, asynchronous H2D feed of the step's combined CSR (module doc).
+
+    query, doc, doc_neg: scipy CSR matrices ([N x D], [N x D], [N*NEG x D]).  ``start(b)`` queues
+    batch b; ``next(model, b_next)`` points the model at the queued batch's device slot (its
+    stream waits for the copy on the device), queues b_next into the other slot and returns the
+    batch index now set; call ``done(model)`` after the step is enqueued."""
+
+    def __init__(self, query, doc, doc_neg, query_bs: int, neg: int, max_nnz: int, nslots: int = 2):
+        self.lib = _lib.load()
+        mats = [sps.csr_matrix(m) for m in (query, doc, doc_neg)]
+        self._ip = [np.ascontiguousarray(m.indptr, np.int64) for m in mats]
+        self._ix = [np.ascontiguousarray(m.indices, np.int32) for m in mats]
+        self._vv = [np.ascontiguousarray(m.data, np.float32) for m in mats]
+        rows = (C.c_int64 * 3)(*[m.shape[0] for m in mats])
+        P3 = C.c_void_p * 3
+        h = C.c_void_p()
+        check(self.lib.dssm_feeder_create(P3(*[a.ctypes.data for a in self._ip]),
+                                          P3(*[a.ctypes.data for a in self._ix]),
+                                          P3(*[a.ctypes.data for a in self._vv]), rows, int(query_bs),
+                                          int(neg), int(max_nnz), int(nslots), C.byref(h)), "feeder_create")
+        self._h = h
+        self.nslots = nslots
+        self.n_batches = min(mats[0].shape[0] // query_bs, mats[1].shape[0] // query_bs,
+                             mats[2].shape[0] // (query_bs * neg))
+        self._slot = 0
+        self._cur = None
+        self._queued = {}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.dssm_feeder_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def start(self, batch: int):
+        check(self.lib.dssm_feeder_submit(self._h, self._slot, int(batch)), "feeder_submit")
+        self._queued[self._slot] = int(batch)
+
+    def next(self, model, next_batch=None, stream=None) -> int:
+        slot = self._slot
+        if slot not in self._queued:
+            raise RuntimeError("no batch queued: call start(b) first")
+        ip, ix, vv = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        nnz = C.c_int64()
+        check(self.lib.dssm_feeder_acquire(self._h, slot, _lib.stream_ptr(stream), C.byref(ip), C.byref(ix),
+                                           C.byref(vv), C.byref(nnz)), "feeder_acquire")
+        check(self.lib.dssm_plan_set_batch(model._plan, ip, ix, vv), "set_batch")
+        model._batch_refs = (self,)
+        b = self._queued.pop(slot)
+        self._cur = slot
+        self._slot = (slot + 1) % self.nslots
+        if next_batch is not None:
+            self.start(next_batch)
+        return b
+
+    def done(self, stream=None):
+        """After the step reading the current slot is enqueued on `stream`."""
+        if self._cur is not None:
+            check(self.lib.dssm_feeder_release(self._h, self._cur, _lib.stream_ptr(stream)), "feeder_release")

@@ -221,6 +221,44 @@ int dssm_comm_init(int rank, int world, const void* unique_id128);
 int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
 int dssm_comm_destroy(void);
 
+/* ---- host data path (utils/utils.py:20-24, 45-61, 368-437; new_dssm.py:26-49) ---------------
+ * Host memory only (no device pointers) except the feeder's outputs. */
+/* pre_process (utils/utils.py:424-437) of one UTF-8 line: short links removed, only U+4E00..U+9FA5,
+ * 0-9, A-Z, a-z kept.  Writes up to cap-1 bytes + NUL to out (may be NULL); *len = full length. */
+int dssm_text_clean(const char* text, char* out, size_t cap, size_t* len);
+/* CountVectorizer(token_pattern=r"(?u)\b\w+\b") (new_dssm.py:37-45) for pre_processed text:
+ * lowercase, tokens = maximal runs of [0-9A-Za-z_] / U+4E00..U+9FA5, feature ids in code-point
+ * order of the token strings (sklearn's sorted vocabulary_), counts per document as CSR. */
+typedef struct dssm_vocab dssm_vocab;
+int dssm_vocab_create(dssm_vocab** out);
+int dssm_vocab_destroy(dssm_vocab* v);
+int dssm_vocab_fit(dssm_vocab* v, const char* const* texts, int64_t n);   /* accumulate tokens */
+int64_t dssm_vocab_finalize(dssm_vocab* v);                               /* -> TRIGRAM_D */
+int64_t dssm_vocab_size(const dssm_vocab* v);
+/* feature name i (get_feature_names()[i]) into out; returns its byte length */
+int dssm_vocab_name(const dssm_vocab* v, int64_t i, char* out, size_t cap);
+/* append a feature (restoring a saved vocabulary in id order) */
+int dssm_vocab_add(dssm_vocab* v, const char* name);
+/* vectorizer.transform: indptr [n+1]; indices / values [cap] (NULL: count only) */
+int dssm_vocab_transform(const dssm_vocab* v, const char* const* texts, int64_t n, int64_t* indptr,
+                         int32_t* indices, float* values, int64_t cap, int64_t* nnz_out);
+/* Asynchronous feeder of the step's combined device CSR (pull_batch, utils/utils.py:45-61): from the
+ * three host CSR matrices m = query [N x D], doc [N x D], doc_neg [N*NEG x D] (caller-owned,
+ * alive until destroy), a worker thread assembles batch b's rows [q; pos; neg] into a pinned slot
+ * and copies it to the slot's device buffers on the feeder's stream.  submit(slot, b) queues it;
+ * acquire(slot, stream) waits for the copy to be queued, makes `stream` wait for it on the device
+ * and returns the device pointers (for dssm_plan_set_batch); release(slot, stream) after the step
+ * reading them is enqueued makes the slot's next copy wait for that step. */
+typedef struct dssm_feeder dssm_feeder;
+int dssm_feeder_create(const int64_t* const* indptr, const int32_t* const* indices,
+                       const float* const* values, const int64_t* rows, int query_bs, int neg,
+                       int64_t max_nnz, int nslots, dssm_feeder** out);
+int dssm_feeder_submit(dssm_feeder* f, int slot, int64_t batch);
+int dssm_feeder_acquire(dssm_feeder* f, int slot, void* stream, const int32_t** indptr,
+                        const int32_t** indices, const float** values, int64_t* nnz);
+int dssm_feeder_release(dssm_feeder* f, int slot, void* stream);
+int dssm_feeder_destroy(dssm_feeder* f);
+
 #ifdef __cplusplus
 }
 #endif

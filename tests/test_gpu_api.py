@@ -220,3 +220,34 @@ def test_sharded_adam_range_updates_only_its_shard():
     b.set_fused_w1_adam(True)
     with pytest.raises(Exception):
         b.apply_adam()  # a shard range needs the fused W1 Adam off
+
+
+def test_export_mid_vectors_eval(tmp_path):
+    """load_model_and_save_vector.py end to end: EMA-BN eval forward on the device, the three
+    mid-vector files in the reference's text format, values = the oracle's eval embeddings."""
+    from dssm_amd.export import export_mid_vectors, mid_vector_line
+    conf, g, cfg = _graph()
+    conf.query_mid_vector_file = str(tmp_path / "y.txt")
+    conf.doc_pos_y_mid_vector_file = str(tmp_path / "dp.txt")
+    conf.doc_neg_y_mid_vector_file = str(tmp_path / "dn.txt")
+    q, d, n = _matrices(1)
+    sess = api.Session(g)
+    feed = pull_batch(True, q, d, n, 0, BS, g.query_batch, g.doc_positive_batch, g.doc_negative_batch,
+                      g.on_train, conf)
+    sess.run(g.train_step, feed_dict=feed)
+    texts = [[f"q {i}" for i in range(BS)], [f"d {i}" for i in range(BS)],
+             [f"n {i}" for i in range(BS * NEG)]]
+    out = export_mid_vectors(sess, g, {k: v for k, v in feed.items() if k is not g.on_train},
+                             *texts, conf)
+    p, ema = _oracle_state(g, cfg)
+    feed_eval = dict(feed)
+    feed_eval[g.on_train] = False
+    A = O.forward_eval_loss(cfg, p, ema, _feed_batch(feed_eval, g))["layers"][-1]["A"]
+    y_dev = g.model.fetch("embedding_all")
+    np.testing.assert_allclose(y_dev, A, rtol=1e-4, atol=1e-5)
+    for path, tx, rows in ((conf.query_mid_vector_file, texts[0], y_dev[:BS]),
+                           (conf.doc_pos_y_mid_vector_file, texts[1], y_dev[BS:2 * BS]),
+                           (conf.doc_neg_y_mid_vector_file, texts[2], y_dev[2 * BS:])):
+        lines = open(path, encoding="utf8").read().splitlines()
+        assert lines == [mid_vector_line(t, r) for t, r in zip(tx, rows)]
+        assert out[path] == len(tx)
