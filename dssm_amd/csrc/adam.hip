@@ -108,7 +108,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
     const int nvalid = n - cc;
     const size_t o = (size_t)c * n + cc;
     float P[8], M[8], V[8], G[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (nvalid > 0) {  // stream loads first: independent of the gather chain below
+    if (nvalid > 0 && !a.gout) {  // stream loads first: independent of the gather chain below
       load8(a.p + o, nvalid, P);
       load8(a.m + o, nvalid, M);
       load8(a.v + o, nvalid, V);
@@ -122,7 +122,24 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
     } else {
       gather_accumulate(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
     }
-    if (nvalid > 0) {
+    if (nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
+      const int k = nvalid >= 8 ? 8 : 4;
+      if (c < a.D) {
+        uint2 lo;
+        lo.x = pack2bf(G[0], G[1]);
+        lo.y = pack2bf(G[2], G[3]);
+        *reinterpret_cast<uint2*>(a.gout + o) = lo;
+        if (k == 8) {
+          uint2 hi;
+          hi.x = pack2bf(G[4], G[5]);
+          hi.y = pack2bf(G[6], G[7]);
+          *reinterpret_cast<uint2*>(a.gout + o + 4) = hi;
+        }
+      } else {
+        *reinterpret_cast<float4*>(a.g + o) = make_float4(G[0], G[1], G[2], G[3]);
+        if (k == 8) *reinterpret_cast<float4*>(a.g + o + 4) = make_float4(G[4], G[5], G[6], G[7]);
+      }
+    } else if (nvalid > 0) {
       const int k = nvalid >= 8 ? 8 : 4;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -154,6 +171,14 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
 
 // Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
 __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
+  if (a.gout) {  // gradient pass
+    for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
+      const size_t o = (size_t)c * a.n + j;
+      if (c < a.D) a.gout[o] = f2bf(grow[j]);
+      else a.g[o] = grow[j];
+    }
+    return;
+  }
   for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
     const size_t o = (size_t)c * a.n + j;
     float P = a.p[o], M = a.m[o], V = a.v[o];
@@ -272,6 +297,10 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
            i += (int64_t)a.dense_blocks * blockDim.x) {
         const int c = (int)((i * 4) / a.n);
         if (a.col_ptr[c + 1] != a.col_ptr[c]) continue;
+        if (a.gout) {  // gradient pass: an untouched row's gradient is zero
+          if (c < a.D) reinterpret_cast<uint2*>(a.gout)[i] = make_uint2(0u, 0u);
+          continue;
+        }
         float4 pp = reinterpret_cast<float4*>(a.p)[i];
         float4 mm = reinterpret_cast<float4*>(a.m)[i];
         float4 vv = reinterpret_cast<float4*>(a.v)[i];
@@ -434,7 +463,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     return e && e[0] == '1';
   }();
   if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), w1_cap);
-  if (sep_advance) a.ticket = nullptr;
+  if (sep_advance || a.gout) a.ticket = nullptr;  // the gradient pass advances nothing
   static const bool w1_flat_on = [] {
     const char* e = std::getenv("DSSM_ADAM_W1_FLAT");
     return !(e && e[0] == '0');
@@ -460,7 +489,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
-  if (!a.ticket)
+  if (!a.ticket && !a.gout)
     hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2, a.heavy_reset);
   return hipGetLastError();
 }

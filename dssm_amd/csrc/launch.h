@@ -221,6 +221,10 @@ struct AdamStep {
   int interleave;
   // zeroed once every block has read heavy_n (the next step's rank launch does not reset it)
   int* heavy_reset;
+  // gradient pass (data parallel, bf16 wire): the W1 roles compute dW1 rows (inline gather, heavy
+  // items, zero for untouched rows) and write them as bf16 to gout (arena layout; the bias row as
+  // fp32 into g) instead of updating parameters; no dense range, no beta-power advance
+  uint16_t* gout;
 };
 constexpr int kAdamItemBlocks = 512;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);

@@ -218,6 +218,8 @@ struct dssm_plan {
   // the reduce-scatter / all-gather; arena elements [0, wire_end) are W1's rows
   uint16_t* gwire = nullptr;
   uint16_t* pwire = nullptr;
+  // dW1 into the wire by the gradient pass (DSSM_WIRE_GRAD_PASS=0: materialise + pack)
+  bool wire_grad_pass = true;
   int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
@@ -529,6 +531,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
     }
   }
   if (const char* e = std::getenv("DSSM_RANK_PREFETCH")) P->rank_prefetch = e[0] != '0';
+  if (const char* e = std::getenv("DSSM_WIRE_GRAD_PASS")) P->wire_grad_pass = e[0] != '0';
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
     P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
@@ -810,6 +813,9 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   return DSSM_OK;
 }
 
+static bool wire_gradient_pass(const dssm_plan* P);
+static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s);
+
 // dW1 = X^T dZ1 from the batch's CSC transpose: heavy columns here, light columns either here
 // (unfused) or inside the Adam step (fused).
 static int dw1_backward(dssm_plan* P, hipStream_t s) {
@@ -822,6 +828,11 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
   // fused single-GPU step with the rank transpose: the heavy columns are computed inside Adam
   // (the DW1 probe then brackets no kernel)
   if (P->fused_w1_adam && P->heavy_in_adam()) {
+    P->probe_end(DSSM_PROBE_DW1, s);
+    return DSSM_OK;
+  }
+  if (wire_gradient_pass(P)) {
+    if (int rc = launch_wire_gradient_pass(P, s)) return rc;
     P->probe_end(DSSM_PROBE_DW1, s);
     return DSSM_OK;
   }
@@ -838,7 +849,7 @@ static int backward_impl(dssm_plan* P, void* stream);
 
 int dssm_plan_backward(dssm_plan* P, void* stream) {
   if (int rc = backward_impl(P, stream)) return rc;
-  if (P->gwire)  // data parallel: the W1 gradient rows leave as bf16
+  if (P->gwire && !wire_gradient_pass(P))  // data parallel: the W1 gradient rows leave as bf16
     HIP_TRY(dssm::launch_wire_pack(P->g, P->gwire, P->wire_end(), (hipStream_t)stream));
   return DSSM_OK;
 }
@@ -918,6 +929,56 @@ static int backward_impl(dssm_plan* P, void* stream) {
   return DSSM_OK;
 }
 
+// The W1 roles of k_adam_step (inline gather of the light rows from the CSC transpose, heavy
+// columns as work items): shared by the fused single-GPU Adam and the data-parallel gradient pass.
+static void fill_w1_roles(dssm_plan* P, dssm::AdamStep& a) {
+  const Layout& Lt = P->Lt;
+  a.w1_blocks = 1;  // sized by the launcher
+  a.D = Lt.D;
+  a.n = Lt.n[0];
+  a.col_ptr = P->at<int>(Lt.col_ptr);
+  a.csc_row = P->at<int>(Lt.csc_row);
+  a.csc_val = P->at<float>(Lt.csc_val);
+  a.dZ = P->ws + Lt.dZ[0];
+  a.lddz = Lt.ldp[0];
+  a.shadow = Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr;
+  a.ldsh = Lt.ldp[0];
+  if (P->heavy_in_adam()) {
+    int* scr = P->at<int>(Lt.csc_scratch);
+    a.item_blocks = dssm::kAdamItemBlocks;
+    a.heavy_n = dssm::csc_heavy_count(scr, Lt.D, Lt.max_nnz);
+    a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
+    a.heavy_ticket = dssm::csc_heavy_tickets(scr, Lt.D, Lt.R, Lt.max_nnz);
+  }
+}
+
+// Data parallel with the bf16 wire: dW1 straight into the gradient wire (bf16 rows, b1's row fp32
+// into the gradient arena) by k_adam_step's W1 roles in gradient-pass mode, instead of the
+// materialising dW1 launches + the wire pack.
+static bool wire_gradient_pass(const dssm_plan* P) {
+  return P->gwire && !P->fused_w1_adam && P->heavy_in_adam() && P->wire_grad_pass;
+}
+
+static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s) {
+  dssm::AdamStep a{};
+  a.p = P->p;
+  a.g = P->g;
+  a.m = P->m;
+  a.v = P->v;
+  a.st = P->at<float>(P->Lt.adam_state);
+  a.lr = P->cfg.lr;
+  a.beta1 = P->cfg.beta1;
+  a.beta2 = P->cfg.beta2;
+  a.eps = P->cfg.adam_eps;
+  a.gs = 1.0f;
+  a.clear_from = P->Lt.total;
+  fill_w1_roles(P, a);
+  a.shadow = nullptr;
+  a.gout = P->gwire;
+  HIP_TRY(dssm::launch_adam_step(a, P->Lt.bf16, s));
+  return DSSM_OK;
+}
+
 int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   const dssm_config& c = P->cfg;
@@ -956,30 +1017,16 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     a.gwire = P->gwire;
     a.pwire = P->pwire;
     a.wire4 = we / 4;
+    // the tail's gradient is consumed here; clear it (b1's row is the gradient pass's atomic target)
+    if (wire_gradient_pass(P)) a.clear_from = we;
     for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
     if (sh.count) sh.count -= 1;
   }
   if (P->fused_w1_adam) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
-    a.w1_blocks = 1;  // sized by the launcher
-    a.D = Lt.D;
-    a.n = Lt.n[0];
-    a.col_ptr = P->at<int>(Lt.col_ptr);
-    a.csc_row = P->at<int>(Lt.csc_row);
-    a.csc_val = P->at<float>(Lt.csc_val);
-    a.dZ = P->ws + Lt.dZ[0];
-    a.lddz = Lt.ldp[0];
-    a.shadow = Lt.bf16 ? P->at<uint16_t>(Lt.shadow[0]) : nullptr;
-    a.ldsh = Lt.ldp[0];
+    fill_w1_roles(P, a);
     a.d4_begin = rest / 4;
-    if (P->heavy_in_adam()) {
-      int* scr = P->at<int>(Lt.csc_scratch);
-      a.item_blocks = dssm::kAdamItemBlocks;
-      a.heavy_n = dssm::csc_heavy_count(scr, Lt.D, Lt.max_nnz);
-      a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
-      a.heavy_ticket = dssm::csc_heavy_tickets(scr, Lt.D, Lt.R, Lt.max_nnz);
-      a.heavy_reset = const_cast<int*>(a.heavy_n);
-    }
+    if (a.heavy_n) a.heavy_reset = const_cast<int*>(a.heavy_n);
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
