@@ -104,6 +104,15 @@ _SIGS = {
                                       C.POINTER(C.c_int64)]),
     "dssm_feeder_release": (C.c_int, [_P, C.c_int, _P]),
     "dssm_feeder_destroy": (C.c_int, [_P]),
+    "dssm_rnn_ws_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "dssm_rnn_forward": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.POINTER(_P), _P, _P,
+                                   C.c_int, _P]),
+    "dssm_rnn_dropout": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_float, C.c_uint32, C.c_uint32,
+                                   C.c_float, _P]),
+    "dssm_rnn_backward": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P), _P, C.c_int,
+                                    _P, _P, C.c_int64, C.POINTER(_P), _P]),
+    "dssm_rnn_adam": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_float, C.c_float, C.c_float,
+                                C.c_float, _P]),
     "dssm_comm_unique_id": (C.c_int, [_P]),
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),

@@ -259,6 +259,32 @@ int dssm_feeder_acquire(dssm_feeder* f, int slot, void* stream, const int32_t** 
 int dssm_feeder_release(dssm_feeder* f, int slot, void* stream);
 int dssm_feeder_destroy(dssm_feeder* f);
 
+/* ---- RNN tower (semantic_matching/dssm_rnn/dssm_rnn.py:100-217) ------------
+ * Word-embedding lookup + one bidirectional GRU (tf.contrib.rnn.GRUCell(H) shared by the three
+ * inputs, bidirectional_dynamic_rnn with per-row lengths) over rows [q(BS); pos(BS); neg(BS*NEG)],
+ * fp32.  ids: [R x T] int32 (row r's tokens, valid up to lens[r], 1 <= lens[r] <= T); emb [V x E];
+ * w[4] = {fw [Wg; bg] ((E+H+1) x 2H), fw [Wc; bc] ((E+H+1) x H), bw [Wg; bg], bw [Wc; bc]} (the last
+ * row is the bias, the reference's _gate_bias / _candidate_bias).  E, H multiples of 4, E+H <= 512,
+ * H <= 256.  ws: dssm_rnn_ws_floats() floats (step caches of the forward, read by the backward). */
+size_t dssm_rnn_ws_floats(int R, int T, int E, int H);
+/* y [R x ldy] = concat(final fw state, final bw state) (dssm_rnn.py:138-152) */
+int dssm_rnn_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int E,
+                     int H, const float* const* w, float* ws, float* y, int ldy, void* stream);
+/* tf.nn.dropout(x, keep) (dssm_rnn.py:141,147,153) with a counter-based mask (seed, step): y = x *
+ * mask * scale / keep; the backward is the same call on dy (scale folds the loss scale). */
+int dssm_rnn_dropout(const float* x, float* y, int rows, int cols, int ld, float keep, uint32_t seed,
+                     uint32_t step, float scale, void* stream);
+/* Backward of dssm_rnn_forward for dy [R x lddy]: the dense embedding gradient into demb
+ * (demb_elems = V*E floats, cleared first), [W; b] gradients written to gw[4] (shapes of w). */
+int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int E, int H,
+                      const float* const* w, const float* dy, int lddy, float* ws, float* demb,
+                      int64_t demb_elems, float* const* gw, void* stream);
+/* AdamOptimizer (dssm_rnn.py:218) over a flat arena: [0, n_sparse) the embedding table (TF1's
+ * deduplicated IndexedSlices update, m*b1 + (1-b1) g form), the rest dense ApplyAdam; state =
+ * device {beta1_power, beta2_power}, advanced after the update. */
+int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
+                  float* state, float lr, float beta1, float beta2, float eps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
