@@ -54,6 +54,8 @@ def parse():
                     help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
                          "(unfused dW1, wire pack, 1/W Adam shard, wire shadows) with the "
                          "collectives omitted, to time the per-rank compute of the N>1 path")
+    ap.add_argument("--model", default="bow", choices=["bow", "rnn"],
+                    help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4)")
     ap.add_argument("--feed", default="device", choices=["device", "host"],
                     help="device: batches staged in HBM before the timed region (the headline); host: "
                          "batches streamed from host CSR matrices by the native pinned async feeder "
@@ -122,8 +124,75 @@ def cpu_baseline(seconds: float):
     return cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds)
 
 
+def bench_rnn(args):
+    """BASELINE.json config 4 (the reference's dssm_rnn tower, dssm_rnn.py:100-218): word embeddings
+    (21,128-token vocabulary, data/vocab.txt's size) -> bidirectional GRU(128) over 32 ids per row ->
+    dropout 0.5 -> x20 cosine / softmax, BS=1024, NEG=4; fp32; synthetic ids (uniform, full
+    lengths as the reference feeds); one step = forward + BPTT + Adam.  Not the headline."""
+    import torch
+    from dssm_amd.rnn import RnnDSSM
+    V, E, H, T = 21128, 128, 128, 32
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = RnnDSSM(V, E, H, BS, NEG, T, lr=1e-5, keep_prob=0.5, device=dev)
+    m.init_params(0)
+    rng = np.random.Generator(np.random.PCG64(4))
+    batches = [rng.integers(1, V, size=(m.R, T)).astype(np.int32) for _ in range(4)]
+    staged = []
+    for b in batches:  # device-resident ids, swapped in by pointer copy-free assignment
+        staged.append(torch.from_numpy(b).to(dev))
+    def step(i):
+        m.ids = staged[i % len(staged)]
+        m.train_step()
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ev[1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "query-doc pairs/sec (fwd+bwd), dssm_rnn tower (BASELINE config 4)",
+           "value": round(BS * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic",
+           "config": {"workload": "dssm_rnn: vocab 21128, emb 128, BiGRU(128), seq_len 32, dropout 0.5, "
+                                  "BS=1024, NEG=4, fwd+BPTT+Adam", "global_batch": BS, "neg": NEG,
+                      "parallelism": "dp1"},
+           "final_loss": round(m.loss(), 3)}
+    if args.cpu_baseline:
+        try:  # the NumPy restatement (oracle/, test infrastructure) timed on the host: bounded sample
+            from oracle import rnn_oracle as RO
+            cfg = RO.RnnConfig(nwords=V, emb=E, hidden=H, query_bs=BS, neg=NEG, seq_len=T, lr=1e-5)
+            p = {k: v.astype(np.float64) for k, v in m.named().items()}
+            opt = RO.Adam(cfg, m.named())
+            lens = np.full(m.R, T, np.int32)
+            n, t0 = 0, time.perf_counter()
+            while n < 1 or time.perf_counter() - t0 < min(args.cpu_seconds, 20.0):
+                mask = RO.dropout_mask(m.R, 2 * H, 0.5, 0, n + 1)
+                fw = RO.forward(cfg, p, batches[n % len(batches)], lens, mask, 0.5)
+                g = RO.backward(cfg, p, batches[n % len(batches)], lens, fw)
+                opt.step(p, g)
+                n += 1
+            el = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": round(BS * (NEG + 1) * n / el, 1), "unit": "pairs/s",
+                                   "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                                   "kind": "port",
+                                   "sample": f"{n} full steps of the NumPy float64 restatement "
+                                             f"(oracle/rnn_oracle.py) in {el:.1f}s"}
+        except Exception as e:
+            out["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.model == "rnn":
+        return bench_rnn(args)
     import torch
     import torch.distributed as dist
 

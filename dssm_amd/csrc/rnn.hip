@@ -52,20 +52,21 @@ __global__ __launch_bounds__(256) void k_gru_fwd(GruDims d, const int* __restric
                                                  const float* __restrict__ wg_bw,
                                                  const float* __restrict__ wc_bw, float* __restrict__ Z, float* __restrict__ Z2,
                                                  float* __restrict__ G, float* __restrict__ out, int ldo) {
-  __shared__ float z[kRB][kMaxK];
-  __shared__ float z2[kRB][kMaxK];
-  __shared__ float h[kRB][kMaxH];
-  __shared__ float gate[kRB][2 * kMaxH];
-  __shared__ float part[2][kRB][kMaxH];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int dir = blockIdx.y;
   const float* Wg = dir ? wg_bw : wg_fw;
   const float* Wc = dir ? wc_bw : wc_fw;
   const int E = d.E, H = d.H, K = E + H, T = d.T, R = d.R;
   const int r0 = blockIdx.x * kRB, tid = threadIdx.x;
+  float* z = lds;                  // [kRB][K]
+  float* z2 = z + kRB * K;         // [kRB][K]
+  float* h = z2 + kRB * K;         // [kRB][H]
+  float* gate = h + kRB * H;       // [kRB][2H]
+  float* part = gate + kRB * 2 * H;  // [2][kRB][H]
   int len[kRB];
 #pragma unroll
   for (int i = 0; i < kRB; ++i) len[i] = r0 + i < R ? lens[r0 + i] : 0;
-  for (int i = tid; i < kRB * H; i += 256) h[i / H][i % H] = 0.f;
+  for (int i = tid; i < kRB * H; i += 256) h[i] = 0.f;
   __syncthreads();
   const size_t plane = (size_t)T * R;
   for (int t = 0; t < T; ++t) {
@@ -79,11 +80,11 @@ __global__ __launch_bounds__(256) void k_gru_fwd(GruDims d, const int* __restric
           const int idx = act ? (dir ? len[rr] - 1 - t : t) : 0;
           v = emb[(size_t)ids[(size_t)r * T + idx] * E + k];
         } else {
-          v = h[rr][k - E];
+          v = h[(rr) * H + k - E];
         }
         Z[((size_t)dir * plane + (size_t)t * R + r) * K + k] = v;
       }
-      z[rr][k] = v;
+      z[(rr) * K + k] = v;
     }
     __syncthreads();
     // gates: sigmoid(z Wg + bg)
@@ -92,56 +93,65 @@ __global__ __launch_bounds__(256) void k_gru_fwd(GruDims d, const int* __restric
       const float b = Wg[(size_t)K * 2 * H + o];
 #pragma unroll
       for (int i = 0; i < kRB; ++i) acc[i] = b;
-      for (int k = 0; k < K; ++k) {
-        const float w = Wg[(size_t)k * 2 * H + o];
+      for (int k = 0; k < K; k += 4) {  // 4 k per LDS broadcast (ds_read_b128), W coalesced
+        const float w0 = Wg[(size_t)k * 2 * H + o], w1 = Wg[(size_t)(k + 1) * 2 * H + o];
+        const float w2 = Wg[(size_t)(k + 2) * 2 * H + o], w3 = Wg[(size_t)(k + 3) * 2 * H + o];
 #pragma unroll
-        for (int i = 0; i < kRB; ++i) acc[i] = fmaf(z[i][k], w, acc[i]);
+        for (int i = 0; i < kRB; ++i) {
+          const float4 zz = *reinterpret_cast<const float4*>(&z[(i) * K + k]);
+          acc[i] = fmaf(zz.x, w0, fmaf(zz.y, w1, fmaf(zz.z, w2, fmaf(zz.w, w3, acc[i]))));
+        }
       }
 #pragma unroll
-      for (int i = 0; i < kRB; ++i) gate[i][o] = sigm(acc[i]);
+      for (int i = 0; i < kRB; ++i) gate[(i) * 2 * H + o] = sigm(acc[i]);
     }
     __syncthreads();
     // z2 = [x_t, r * h]
     for (int i = tid; i < kRB * K; i += 256) {
       const int rr = i / K, k = i - rr * K, r = r0 + rr;
-      const float v = k < E ? z[rr][k] : gate[rr][k - E] * h[rr][k - E];
-      z2[rr][k] = v;
+      const float v = k < E ? z[(rr) * K + k] : gate[(rr) * 2 * H + k - E] * h[(rr) * H + k - E];
+      z2[(rr) * K + k] = v;
       if (r < R) Z2[((size_t)dir * plane + (size_t)t * R + r) * K + k] = v;
     }
     __syncthreads();
     // candidate: two halves of K per output column, summed through LDS
     for (int q = tid; q < 2 * H; q += 256) {
       const int o = q % H, half = q / H;
-      const int k0 = half ? K / 2 : 0, k1 = half ? K : K / 2;
+      const int kh = (K / 2) & ~3;
+      const int k0 = half ? kh : 0, k1 = half ? K : kh;
       float acc[kRB];
 #pragma unroll
       for (int i = 0; i < kRB; ++i) acc[i] = 0.f;
-      for (int k = k0; k < k1; ++k) {
-        const float w = Wc[(size_t)k * H + o];
+      for (int k = k0; k < k1; k += 4) {
+        const float w0 = Wc[(size_t)k * H + o], w1 = Wc[(size_t)(k + 1) * H + o];
+        const float w2 = Wc[(size_t)(k + 2) * H + o], w3 = Wc[(size_t)(k + 3) * H + o];
 #pragma unroll
-        for (int i = 0; i < kRB; ++i) acc[i] = fmaf(z2[i][k], w, acc[i]);
+        for (int i = 0; i < kRB; ++i) {
+          const float4 zz = *reinterpret_cast<const float4*>(&z2[(i) * K + k]);
+          acc[i] = fmaf(zz.x, w0, fmaf(zz.y, w1, fmaf(zz.z, w2, fmaf(zz.w, w3, acc[i]))));
+        }
       }
 #pragma unroll
-      for (int i = 0; i < kRB; ++i) part[half][i][o] = acc[i];
+      for (int i = 0; i < kRB; ++i) part[(half * kRB + i) * H + o] = acc[i];
     }
     __syncthreads();
     for (int i = tid; i < kRB * H; i += 256) {
       const int rr = i / H, o = i - rr * H, r = r0 + rr;
-      const float c = tanhf(part[0][rr][o] + part[1][rr][o] + Wc[(size_t)K * H + o]);
-      const float u = gate[rr][H + o], hv = h[rr][o];
+      const float c = tanhf(part[rr * H + o] + part[(kRB + rr) * H + o] + Wc[(size_t)K * H + o]);
+      const float u = gate[(rr) * 2 * H + H + o], hv = h[(rr) * H + o];
       if (r < R) {
         float* g = G + ((size_t)dir * plane + (size_t)t * R + r) * 3 * H;
-        g[o] = gate[rr][o];
+        g[o] = gate[(rr) * 2 * H + o];
         g[H + o] = u;
         g[2 * H + o] = c;
-        if (t < len[rr]) h[rr][o] = u * hv + (1.f - u) * c;
+        if (t < len[rr]) h[(rr) * H + o] = u * hv + (1.f - u) * c;
       }
     }
     __syncthreads();
   }
   for (int i = tid; i < kRB * H; i += 256) {
     const int rr = i / H, o = i - rr * H, r = r0 + rr;
-    if (r < R) out[(size_t)r * ldo + dir * H + o] = h[rr][o];
+    if (r < R) out[(size_t)r * ldo + dir * H + o] = h[(rr) * H + o];
   }
 }
 
@@ -160,25 +170,26 @@ __global__ __launch_bounds__(256) void k_gru_bwd(GruDims d, const int* __restric
                                                  const float* __restrict__ G, float* __restrict__ dG,
                                                  float* __restrict__ dC,
                                                  float* __restrict__ demb) {
-  __shared__ float dh[kRB][kMaxH];     // gradient reaching the state after step t
-  __shared__ float dhp[kRB][kMaxH];    // dh_prev without the gate path
-  __shared__ float hold[kRB][kMaxH];   // state before step t
-  __shared__ float rs[kRB][kMaxH];     // reset gate
-  __shared__ float dcand[kRB][kMaxH];  // candidate pre-activation gradient
-  __shared__ float dgate[kRB][2 * kMaxH];
-  __shared__ float dz2[kRB][kMaxK];    // dcand Wc^T
-  __shared__ float dzs[kRB][kMaxH];    // state part of dgate Wg^T
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int dir = blockIdx.y;
   const float* WgT = dir ? wgT_bw : wgT_fw;
   const float* WcT = dir ? wcT_bw : wcT_fw;
   const int E = d.E, H = d.H, K = E + H, T = d.T, R = d.R;
   const int r0 = blockIdx.x * kRB, tid = threadIdx.x;
+  float* dcand = lds;                // [kRB][H]  candidate pre-activation gradient
+  float* dgate = dcand + kRB * H;    // [kRB][2H]
+  float* dz2 = dgate + kRB * 2 * H;  // [kRB][K]  dcand Wc^T
+  float* dh = dz2 + kRB * K;         // [kRB][H]  gradient reaching the state after step t
+  float* dhp = dh + kRB * H;         // [kRB][H]  dh_prev without the gate path
+  float* hold = dhp + kRB * H;       // [kRB][H]  state before step t
+  float* rs = hold + kRB * H;        // [kRB][H]  reset gate
+  float* dzs = rs + kRB * H;         // [kRB][H]  state part of dgate Wg^T
   int len[kRB];
 #pragma unroll
   for (int i = 0; i < kRB; ++i) len[i] = r0 + i < R ? lens[r0 + i] : 0;
   for (int i = tid; i < kRB * H; i += 256) {
     const int rr = i / H, o = i - rr * H, r = r0 + rr;
-    dh[rr][o] = r < R ? dout[(size_t)r * ldo + dir * H + o] : 0.f;
+    dh[(rr) * H + o] = r < R ? dout[(size_t)r * ldo + dir * H + o] : 0.f;
   }
   __syncthreads();
   const size_t plane = (size_t)T * R;
@@ -193,18 +204,18 @@ __global__ __launch_bounds__(256) void k_gru_bwd(GruDims d, const int* __restric
         rg = g[o];
         const float u = g[H + o], c = g[2 * H + o];
         h0 = Z[row * K + E + o];
-        const float dhn = t < len[rr] ? dh[rr][o] : 0.f;
+        const float dhn = t < len[rr] ? dh[(rr) * H + o] : 0.f;
         dc_ = dhn * (1.f - u) * (1.f - c * c);
         du = dhn * (h0 - c) * u * (1.f - u);
         dC[row * H + o] = dc_;
-        dhp[rr][o] = t < len[rr] ? dhn * u : dh[rr][o];  // carried past the row's length
+        dhp[(rr) * H + o] = t < len[rr] ? dhn * u : dh[(rr) * H + o];  // carried past the row's length
       } else {
-        dhp[rr][o] = 0.f;
+        dhp[(rr) * H + o] = 0.f;
       }
-      hold[rr][o] = h0;
-      rs[rr][o] = rg;
-      dcand[rr][o] = dc_;
-      dgate[rr][H + o] = du;
+      hold[(rr) * H + o] = h0;
+      rs[(rr) * H + o] = rg;
+      dcand[(rr) * H + o] = dc_;
+      dgate[(rr) * 2 * H + H + o] = du;
     }
     __syncthreads();
     // 2. dz2 = dcand Wc^T
@@ -212,26 +223,30 @@ __global__ __launch_bounds__(256) void k_gru_bwd(GruDims d, const int* __restric
       float acc[kRB];
 #pragma unroll
       for (int i = 0; i < kRB; ++i) acc[i] = 0.f;
-      for (int o = 0; o < H; ++o) {
-        const float w = WcT[(size_t)o * K + k];
+      for (int o = 0; o < H; o += 4) {
+        const float w0 = WcT[(size_t)o * K + k], w1 = WcT[(size_t)(o + 1) * K + k];
+        const float w2 = WcT[(size_t)(o + 2) * K + k], w3 = WcT[(size_t)(o + 3) * K + k];
 #pragma unroll
-        for (int i = 0; i < kRB; ++i) acc[i] = fmaf(dcand[i][o], w, acc[i]);
+        for (int i = 0; i < kRB; ++i) {
+          const float4 q = *reinterpret_cast<const float4*>(&dcand[(i) * H + o]);
+          acc[i] = fmaf(q.x, w0, fmaf(q.y, w1, fmaf(q.z, w2, fmaf(q.w, w3, acc[i]))));
+        }
       }
 #pragma unroll
-      for (int i = 0; i < kRB; ++i) dz2[i][k] = acc[i];
+      for (int i = 0; i < kRB; ++i) dz2[(i) * K + k] = acc[i];
     }
     __syncthreads();
     // 3. reset gate through r*h; the state gradient through r*h
     for (int i = tid; i < kRB * H; i += 256) {
       const int rr = i / H, o = i - rr * H, r = r0 + rr;
-      const float rg = rs[rr][o], drh = dz2[rr][E + o];
-      const float dr = drh * hold[rr][o] * rg * (1.f - rg);
-      dgate[rr][o] = dr;
+      const float rg = rs[(rr) * H + o], drh = dz2[(rr) * K + E + o];
+      const float dr = drh * hold[(rr) * H + o] * rg * (1.f - rg);
+      dgate[(rr) * 2 * H + o] = dr;
       if (r < R) {
         const size_t row = (size_t)dir * plane + (size_t)t * R + r;
         dG[row * 2 * H + o] = dr;
-        dG[row * 2 * H + H + o] = dgate[rr][H + o];
-        if (t < len[rr]) dhp[rr][o] += drh * rg;
+        dG[row * 2 * H + H + o] = dgate[(rr) * 2 * H + H + o];
+        if (t < len[rr]) dhp[(rr) * H + o] += drh * rg;
       }
     }
     __syncthreads();
@@ -240,21 +255,25 @@ __global__ __launch_bounds__(256) void k_gru_bwd(GruDims d, const int* __restric
       float acc[kRB];
 #pragma unroll
       for (int i = 0; i < kRB; ++i) acc[i] = 0.f;
-      for (int o = 0; o < 2 * H; ++o) {
-        const float w = WgT[(size_t)o * K + k];
+      for (int o = 0; o < 2 * H; o += 4) {
+        const float w0 = WgT[(size_t)o * K + k], w1 = WgT[(size_t)(o + 1) * K + k];
+        const float w2 = WgT[(size_t)(o + 2) * K + k], w3 = WgT[(size_t)(o + 3) * K + k];
 #pragma unroll
-        for (int i = 0; i < kRB; ++i) acc[i] = fmaf(dgate[i][o], w, acc[i]);
+        for (int i = 0; i < kRB; ++i) {
+          const float4 q = *reinterpret_cast<const float4*>(&dgate[(i) * 2 * H + o]);
+          acc[i] = fmaf(q.x, w0, fmaf(q.y, w1, fmaf(q.z, w2, fmaf(q.w, w3, acc[i]))));
+        }
       }
 #pragma unroll
       for (int i = 0; i < kRB; ++i) {
         const int r = r0 + i;
         if (k >= E) {
-          dzs[i][k - E] = acc[i];
+          dzs[(i) * H + k - E] = acc[i];
         } else if (r < R && t < len[i]) {
           const int idx = dir ? len[i] - 1 - t : t;
           using gfloat = __attribute__((address_space(1))) float;
           __hip_atomic_fetch_add((gfloat*)(demb + (size_t)ids[(size_t)r * T + idx] * E + k),
-                                 acc[i] + dz2[i][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                 acc[i] + dz2[(i) * K + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -262,7 +281,7 @@ __global__ __launch_bounds__(256) void k_gru_bwd(GruDims d, const int* __restric
     // 5. gradient reaching the state before step t
     for (int i = tid; i < kRB * H; i += 256) {
       const int rr = i / H, o = i - rr * H;
-      dh[rr][o] = t < len[rr] ? dhp[rr][o] + dzs[rr][o] : dhp[rr][o];
+      dh[(rr) * H + o] = t < len[rr] ? dhp[(rr) * H + o] + dzs[(rr) * H + o] : dhp[(rr) * H + o];
     }
     __syncthreads();
   }
@@ -373,7 +392,8 @@ int dssm_rnn_forward(const int32_t* ids, const int32_t* lens, int R, int T, cons
   float* Z2 = Z + plane * K;
   float* G = Z2 + plane * K;
   const dssm::GruDims d{R, T, E, H};
-  hipLaunchKernelGGL(dssm::k_gru_fwd, dim3((R + dssm::kRB - 1) / dssm::kRB, 2), dim3(256), 0,
+  const size_t lds = sizeof(float) * dssm::kRB * (2 * K + 5 * (size_t)H);
+  hipLaunchKernelGGL(dssm::k_gru_fwd, dim3((R + dssm::kRB - 1) / dssm::kRB, 2), dim3(256), lds,
                      (hipStream_t)stream, d, ids, lens, emb, w[0], w[1], w[2], w[3], Z, Z2, G, y, ldy);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
@@ -418,7 +438,8 @@ int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int
                        w[2 * dir + 1], K, H, gT + (size_t)2 * H * K, K);
   }
   const dssm::GruDims d{R, T, E, H};
-  hipLaunchKernelGGL(dssm::k_gru_bwd, dim3((R + dssm::kRB - 1) / dssm::kRB, 2), dim3(256), 0, s, d,
+  const size_t lds = sizeof(float) * dssm::kRB * ((size_t)K + 8 * H);
+  hipLaunchKernelGGL(dssm::k_gru_bwd, dim3((R + dssm::kRB - 1) / dssm::kRB, 2), dim3(256), lds, s, d,
                      ids, lens, wT, wT + (size_t)2 * H * K, wT + (size_t)3 * H * K,
                      wT + (size_t)5 * H * K, dy, lddy, Z, G, dG, dC, demb);
   // [W; b] gradients: one split-K TN GEMM per matrix over all (step, row) pairs, ones row = bias
