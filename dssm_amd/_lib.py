@@ -113,6 +113,16 @@ _SIGS = {
                                     _P, _P, C.c_int64, C.POINTER(_P), _P]),
     "dssm_rnn_adam": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_float, C.c_float, C.c_float,
                                 C.c_float, _P]),
+    "dssm_spmm_bwd_ws_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "dssm_spmm_csr_bwd_w": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
+                                      _P, _P, _P]),
+    "dssm_dense_bwd_slab_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "dssm_dense_bwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
+                                 _P, C.c_int, _P, _P, _P]),
+    "dssm_bn_relu_bwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float, C.c_int, _P,
+                                   C.c_int, _P, C.c_int, _P, _P, _P]),
+    "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,
+                                 C.c_float, _P]),
     "dssm_comm_unique_id": (C.c_int, [_P]),
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),

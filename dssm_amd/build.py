@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libdssm.so")
-SOURCES = ["spmm.hip", "gemm.hip", "bn.hip", "cosine.hip", "adam.hip", "dense.hip", "plan.hip", "feed.hip", "rnn.hip"]
+SOURCES = ["spmm.hip", "gemm.hip", "bn.hip", "cosine.hip", "adam.hip", "dense.hip", "plan.hip", "feed.hip", "rnn.hip", "ops.hip"]
 HEADERS = ["common.h", "launch.h", "gather.h", "bnfuse.h", "dense.h"]
 ARCH = os.environ.get("DSSM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -1,0 +1,181 @@
+// Functional backward entry points of the C-ABI: the per-op gradients a caller
+// composes when it drives the layers itself (dssm_amd/api.py's functional ops, the multi-view
+// towers) instead of the fused training-step plan.
+//   dssm_spmm_csr_bwd_w : [dW1; db1] = [X | 1]^T dZ1 (TF's SparseTensorDenseMatMul gradient,
+//                         dense), via the plan's CSC transpose + dW1 kernels
+//   dssm_dense_bwd      : dA = dZ W^T and [dW; db] = [A | 1]^T dZ (tf.matmul + bias autodiff)
+//   dssm_bn_relu_bwd    : batch-statistics batch_normalization + ReLU backward (new_dssm.py:62-88)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "../../include/dssm.h"
+#include "common.h"
+#include "launch.h"
+
+namespace dssm {
+int report_error(int code, const char* msg);
+}
+
+namespace {
+
+int oerr(int code, const char* m) { return dssm::report_error(code, m); }
+
+int hip_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+struct SpmmWs {
+  size_t scratch, col_ptr, row, val, col, total;
+};
+
+SpmmWs spmm_ws(int rows, int D, int max_nnz) {
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  SpmmWs w{};
+  size_t o = 0;
+  w.scratch = o;
+  o += al(dssm::csc_scratch_ints(D, rows, max_nnz) * 4);
+  w.col_ptr = o;
+  o += al((size_t)(D + 2) * 4);
+  const size_t ent = (size_t)max_nnz + rows;
+  w.row = o;
+  o += al(ent * 4);
+  w.val = o;
+  o += al(ent * 4);
+  w.col = o;
+  o += al(ent * 4);
+  w.total = o;
+  return w;
+}
+
+// Column sums of the batch-norm backward: dbeta = sum dy, dgamma = sum dy * xhat (dy through the
+// ReLU mask).  One block per 64 columns, 4 row groups reduced through LDS (fixed order).
+__global__ __launch_bounds__(256) void k_bnr_bwd_sums(const float* __restrict__ Z, int ldz, int rows,
+                                                      int n, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ var, float eps, int relu,
+                                                      const float* __restrict__ dout, int ldd,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float s1[4][64], s2[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  float a = 0.f, b = 0.f;
+  if (c < n) {
+    const float mu = mean[c], rstd = 1.0f / sqrtf(var[c] + eps), gm = gamma[c], bt = beta[c];
+    for (int r = grp; r < rows; r += 4) {
+      const float xh = (Z[(size_t)r * ldz + c] - mu) * rstd;
+      float dy = dout[(size_t)r * ldd + c];
+      if (relu && !(gm * xh + bt > 0.f)) dy = 0.f;
+      a += dy;
+      b += dy * xh;
+    }
+  }
+  s1[grp][threadIdx.x & 63] = a;
+  s2[grp][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (grp == 0 && c < n) {
+    const int l = threadIdx.x;
+    dbeta[c] = s1[0][l] + s1[1][l] + s1[2][l] + s1[3][l];
+    dgamma[c] = s2[0][l] + s2[1][l] + s2[2][l] + s2[3][l];
+  }
+}
+
+// dz = gamma * rstd * (dy - mean(dy) - xhat * mean(dy * xhat))
+__global__ __launch_bounds__(256) void k_bnr_bwd_apply(const float* __restrict__ Z, int ldz, int rows,
+                                                       int n, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ var, float eps, int relu,
+                                                       const float* __restrict__ dout, int ldd,
+                                                       const float* __restrict__ dgamma,
+                                                       const float* __restrict__ dbeta,
+                                                       float* __restrict__ dz, int lddz) {
+  const int64_t total = (int64_t)rows * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / n), c = (int)(i - (int64_t)r * n);
+    const float rstd = 1.0f / sqrtf(var[c] + eps), gm = gamma[c];
+    const float xh = (Z[(size_t)r * ldz + c] - mean[c]) * rstd;
+    float dy = dout[(size_t)r * ldd + c];
+    if (relu && !(gm * xh + beta[c] > 0.f)) dy = 0.f;
+    const float m1 = dbeta[c] / rows, m2 = dgamma[c] / rows;
+    dz[(size_t)r * lddz + c] = gm * rstd * (dy - m1 - xh * m2);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dssm_spmm_bwd_ws_bytes(int rows, int D, int max_nnz) {
+  if (rows <= 0 || D <= 0 || max_nnz < 0) return 0;
+  return spmm_ws(rows, D, max_nnz).total;
+}
+
+int dssm_spmm_csr_bwd_w(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                        int D, int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* dWb,
+                        void* ws, void* stream) {
+  if (!indptr || !dZ || !dWb || !ws || rows <= 0 || D <= 0 || n <= 0 || lddz < n || (lddz % 8) ||
+      (max_nnz && (!indices || !values)))
+    return oerr(DSSM_E_INVALID, "spmm_csr_bwd_w: bad argument (lddz must be a multiple of 8)");
+  hipStream_t s = (hipStream_t)stream;
+  const SpmmWs w = spmm_ws(rows, D, max_nnz);
+  char* b = static_cast<char*>(ws);
+  int* scratch = reinterpret_cast<int*>(b + w.scratch);
+  int* col_ptr = reinterpret_cast<int*>(b + w.col_ptr);
+  int* crow = reinterpret_cast<int*>(b + w.row);
+  float* cval = reinterpret_cast<float*>(b + w.val);
+  int* ccol = reinterpret_cast<int*>(b + w.col);
+  const bool rank = dssm::csc_rank_supported(D);
+  hipError_t e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, crow,
+                                        cval, ccol, s, nullptr, 0, rank, false);
+  if (e == hipSuccess)
+    e = dssm::launch_dw1(col_ptr, crow, cval, ccol, D, rows, max_nnz, dZ, dz_dtype == DSSM_BF16, lddz, n,
+                         dWb, true, s, rank ? scratch : nullptr);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype) {
+  return dssm::gemm_dw_slab_floats(K + 1, N, M, dtype == DSSM_BF16);
+}
+
+int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                   const void* dZ, int lddz, float* dA, int ldda, float* dWb, float* slab, void* stream) {
+  if (!A || !W || !dZ || !dWb || M <= 0 || K <= 0 || N <= 0 || lda < K || ldw < N || lddz < N ||
+      (dA && ldda < K) || (dtype != DSSM_F32 && dtype != DSSM_BF16) || (lda % 4) || (ldw % 4) ||
+      (lddz % 4))
+    return oerr(DSSM_E_INVALID, "dense_bwd: bad argument");
+  if (dssm_dense_bwd_slab_floats(M, K, N, dtype) && !slab)
+    return oerr(DSSM_E_INVALID, "dense_bwd: this shape needs a split-K slab");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = dtype == DSSM_BF16;
+  hipError_t e = hipSuccess;
+  if (dA)
+    e = dssm::launch_gemm(dssm::GEMM_DA, bf, M, K, N, dZ, lddz, W, ldw, dA, ldda, nullptr, false, nullptr,
+                          s, nullptr);
+  if (e == hipSuccess)
+    e = dssm::launch_gemm(dssm::GEMM_DW, bf, K + 1, N, M, A, lda, dZ, lddz, dWb, N, nullptr, true, slab, s,
+                          nullptr);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
+                     const float* batch_mean, const float* batch_var, float eps, int relu,
+                     const float* dout, int ldd, float* dz, int lddz, float* dgamma, float* dbeta,
+                     void* stream) {
+  if (!Z || !gamma || !beta || !batch_mean || !batch_var || !dout || !dz || !dgamma || !dbeta || rows <= 0 ||
+      n <= 0 || ldz < n || ldd < n || lddz < n)
+    return oerr(DSSM_E_INVALID, "bn_relu_bwd: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bnr_bwd_sums, dim3((n + 63) / 64), dim3(256), 0, s, Z, ldz, rows, n, gamma, beta,
+                     batch_mean, batch_var, eps, relu, dout, ldd, dgamma, dbeta);
+  const int64_t total = (int64_t)rows * n;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_bnr_bwd_apply, dim3(grid), dim3(256), 0, s, Z, ldz, rows, n, gamma, beta, batch_mean,
+                     batch_var, eps, relu, dout, ldd, dgamma, dbeta, dz, lddz);
+  return hip_status();
+}
+
+}  // extern "C"

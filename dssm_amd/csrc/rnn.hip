@@ -330,11 +330,11 @@ __global__ void k_dropout(const float* __restrict__ x, float* __restrict__ y, in
 __global__ __launch_bounds__(256) void k_rnn_adam(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ m, float* __restrict__ v,
                                                   int64_t n_sparse, int64_t n, const float* st,
-                                                  float lr, float b1, float b2, float eps) {
+                                                  float lr, float b1, float b2, float eps, float gs) {
   const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i];
+    const float gi = g[i] * gs;
     float mi = m[i], vi = v[i];
     if (i < n_sparse) {
       mi = mi * b1 + gi * (1.0f - b1);
@@ -464,10 +464,23 @@ int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, n_sparse, n, state, lr,
-                     beta1, beta2, eps);
+                     beta1, beta2, eps, 1.0f);
   hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
 }  // extern "C"
+
+extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                              float beta1, float beta2, float eps, float* state, float grad_scale,
+                              void* stream) {
+  if (!p || !g || !m || !v || !state || n < 0) return rerr(DSSM_E_INVALID, "adam_step: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+  hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, (int64_t)0, n, state, lr,
+                     beta1, beta2, eps, grad_scale);
+  hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
+}

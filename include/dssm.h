@@ -214,6 +214,33 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
                              float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
                              float* loss, float* dy, float* ws, void* stream);
 
+/* ---- functional backward (the per-op gradients; the plan fuses them) ---------------------- */
+/* tf.sparse_tensor_dense_matmul's weight gradient (new_dssm.py:124-126 autodiff, dense like
+ * TF1.x): dWb [(D+1) x n] = [X | 1]^T dZ (row D = db).  dZ [rows x lddz] of dz_dtype (lddz % 8 ==
+ * 0).  ws: dssm_spmm_bwd_ws_bytes() bytes, zero-filled before first use (CSC transpose scratch,
+ * kept zero between calls). */
+size_t dssm_spmm_bwd_ws_bytes(int rows, int D, int max_nnz);
+int dssm_spmm_csr_bwd_w(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                        int D, int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* dWb,
+                        void* ws, void* stream);
+/* add_layer / tf.matmul(x, W) + b autodiff (new_dssm.py:146-148): dA [M x ldda] = dZ W^T (dA may be
+ * NULL), dWb [(K+1) x N] = [A | 1]^T dZ (row K = db).  A [M x lda], W [K x ldw], dZ [M x lddz] of
+ * dtype; fp32 accumulation; slab: dssm_dense_bwd_slab_floats() floats (split-K partials). */
+size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype);
+int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                   const void* dZ, int lddz, float* dA, int ldda, float* dWb, float* slab, void* stream);
+/* batch_normalization + ReLU backward with batch statistics (new_dssm.py:62-88, :134-136; ReLU'(0) =
+ * 0): from the forward's Z, gamma, beta and batch mean / biased variance (dssm_bn_relu_fwd's
+ * batch_mean / batch_var), dout -> dz, dgamma, dbeta.  relu = 0: plain batch norm. */
+int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,
+                     const float* batch_mean, const float* batch_var, float eps, int relu,
+                     const float* dout, int ldd, float* dz, int lddz, float* dgamma, float* dbeta,
+                     void* stream);
+/* TF1.x ApplyAdam (new_dssm.py:215-217) over n flat elements with gradient x grad_scale;
+ * state = device {beta1_power, beta2_power} (start at beta1, beta2), advanced after the update. */
+int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                   float beta2, float eps, float* state, float grad_scale, void* stream);
+
 /* ---- data parallel (one RCCL all-reduce of the gradient arena per step) ----------------- */
 /* unique_id: 128 bytes from dssm_comm_unique_id() on rank 0, shared by the caller. */
 int dssm_comm_unique_id(void* out128);

@@ -1,0 +1,141 @@
+"""Functional backward entry points of include/dssm.h against float64 NumPy of the
+same inputs: dssm_spmm_csr_bwd_w ([X|1]^T dZ, dense, fp32 and bf16 dZ), dssm_dense_bwd (dZ W^T,
+[A|1]^T dZ), dssm_bn_relu_bwd (the oracle's batch-stat BN + ReLU backward formula), dssm_adam_step
+(TF1.x ApplyAdam).  Tolerances: fp32 1e-5 relative to the output scale; bf16 inputs 1e-2."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from dssm_amd import _lib
+from dssm_amd._lib import check, ptr
+from dssm_amd.data import ZipfColumns, synth_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, tol):
+    scale = max(np.abs(ref).max(), 1e-30)
+    assert np.abs(got - ref).max() <= tol * scale, (np.abs(got - ref).max(), scale)
+
+
+@pytest.mark.parametrize("D,rows,n,dt", [(5000, 768, 300, "fp32"), (30000, 1536, 304, "bf16"), (700, 64, 64, "fp32")])
+def test_spmm_csr_bwd_w(D, rows, n, dt):
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(1))
+    ip, ix, vv = synth_rows(rng, ZipfColumns(D), rows, 24.0)
+    dZ = rng.standard_normal((rows, n)).astype(np.float32)
+    ldz = -(-n // 8) * 8
+    dZp = np.zeros((rows, ldz), np.float32)
+    dZp[:, :n] = dZ
+    tdz = torch.from_numpy(dZp).cuda()
+    if dt == "bf16":
+        tdz = tdz.to(torch.bfloat16)
+        dZ = tdz.float().cpu().numpy()[:, :n]
+    max_nnz = int(ip[-1])
+    ws = torch.zeros(lib.dssm_spmm_bwd_ws_bytes(rows, D, max_nnz), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((D + 1, n), dtype=torch.float32, device="cuda")
+    t = [torch.from_numpy(x).cuda() for x in (ip, ix, vv)]
+    for _ in range(2):  # the scratch must be re-armed by the call itself
+        check(lib.dssm_spmm_csr_bwd_w(ptr(t[0]), ptr(t[1]), ptr(t[2]), rows, D, max_nnz, ptr(tdz),
+                                      _lib.DSSM_BF16 if dt == "bf16" else _lib.DSSM_F32, ldz, n, ptr(out),
+                                      ptr(ws), _lib.stream_ptr()), "spmm_bwd")
+        torch.cuda.synchronize()
+        X = np.zeros((rows, D + 1))
+        for r in range(rows):
+            X[r, ix[ip[r]:ip[r + 1]]] += vv[ip[r]:ip[r + 1]]
+        X[:, D] = 1.0
+        _close(out.cpu().numpy(), X.T @ dZ.astype(np.float64), 1e-5)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_dense_bwd(dt):
+    lib = _lib.load()
+    M, K, N = 1536, 300, 128
+    rng = np.random.Generator(np.random.PCG64(2))
+    A, W, dZ = (rng.standard_normal(s).astype(np.float32) for s in ((M, K), (K, N), (M, N)))
+    lda, ldw = -(-K // 8) * 8, -(-N // 8) * 8
+    tt = torch.bfloat16 if dt == "bf16" else torch.float32
+
+    def dev(x, ld):
+        y = np.zeros((x.shape[0], ld), np.float32)
+        y[:, :x.shape[1]] = x
+        return torch.from_numpy(y).cuda().to(tt)
+    tA, tW, tZ = dev(A, lda), dev(W, ldw), dev(dZ, ldw)
+    if dt == "bf16":
+        A, W, dZ = (t.float().cpu().numpy()[:, :s] for t, s in ((tA, K), (tW, N), (tZ, N)))
+    dtype = _lib.DSSM_BF16 if dt == "bf16" else _lib.DSSM_F32
+    slab = torch.zeros(max(1, lib.dssm_dense_bwd_slab_floats(M, K, N, dtype)), device="cuda")
+    dA = torch.zeros((M, lda), device="cuda")
+    dWb = torch.zeros((K + 1, N), device="cuda")
+    check(lib.dssm_dense_bwd(ptr(tA), lda, ptr(tW), ldw, dtype, M, K, N, ptr(tZ), ldw, ptr(dA), lda,
+                             ptr(dWb), ptr(slab), _lib.stream_ptr()), "dense_bwd")
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == "fp32" else 1e-2
+    _close(dA.cpu().numpy()[:, :K], dZ.astype(np.float64) @ W.T.astype(np.float64), tol)
+    A1 = np.concatenate([A, np.ones((M, 1), np.float32)], 1).astype(np.float64)
+    _close(dWb.cpu().numpy(), A1.T @ dZ.astype(np.float64), tol)
+
+
+@pytest.mark.parametrize("relu", [1, 0])
+def test_bn_relu_bwd(relu):
+    lib = _lib.load()
+    rows, n, eps = 1000, 100, 1e-3
+    rng = np.random.Generator(np.random.PCG64(3))
+    Z = (rng.standard_normal((rows, n)) * 2 + 0.5).astype(np.float32)
+    g = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    b = rng.uniform(-0.3, 0.3, n).astype(np.float32)
+    dout = rng.standard_normal((rows, n)).astype(np.float32)
+    mu, var = Z.astype(np.float64).mean(0), Z.astype(np.float64).var(0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v, np.float32)).cuda()
+         for k, v in dict(Z=Z, g=g, b=b, mu=mu, var=var, d=dout).items()}
+    dz = torch.zeros((rows, n), device="cuda")
+    dg, db = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    check(lib.dssm_bn_relu_bwd(ptr(t["Z"]), n, rows, n, ptr(t["g"]), ptr(t["b"]), ptr(t["mu"]), ptr(t["var"]),
+                               eps, relu, ptr(t["d"]), n, ptr(dz), n, ptr(dg), ptr(db), _lib.stream_ptr()), "bn_bwd")
+    torch.cuda.synchronize()
+    # float64 reference: y = g xhat + b, out = relu(y)
+    Zd = Z.astype(np.float64)
+    xh = (Zd - mu) / np.sqrt(var + eps)
+    dy = dout.astype(np.float64) * ((g * xh + b > 0) if relu else 1.0)
+    ref_db, ref_dg = dy.sum(0), (dy * xh).sum(0)
+    ref_dz = g / np.sqrt(var + eps) * (dy - dy.mean(0) - xh * (dy * xh).mean(0))
+    _close(db.cpu().numpy(), ref_db, 1e-5)
+    _close(dg.cpu().numpy(), ref_dg, 1e-5)
+    _close(dz.cpu().numpy(), ref_dz, 1e-4)
+    # finite-difference spot check of dz through the full batch-stat BN + ReLU in float64
+    def f(Zx):
+        m, v = Zx.mean(0), Zx.var(0)
+        y = g * (Zx - m) / np.sqrt(v + eps) + b
+        return float(((np.maximum(y, 0) if relu else y) * dout).sum())
+    for (r, c) in ((3, 7), (500, 42)):
+        e = np.zeros_like(Zd)
+        e[r, c] = 1e-6
+        num = (f(Zd + e) - f(Zd - e)) / 2e-6
+        assert abs(num - ref_dz[r, c]) <= 1e-4 * max(1.0, abs(num))
+
+
+def test_adam_step():
+    lib = _lib.load()
+    n = 10000
+    rng = np.random.Generator(np.random.PCG64(4))
+    p0 = rng.standard_normal(n).astype(np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    tp, tg = torch.from_numpy(p0.copy()).cuda(), torch.from_numpy(g).cuda()
+    tm, tv = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    st = torch.tensor([0.9, 0.999], device="cuda")
+    f = np.float32
+    p, m, v, b1p, b2p = p0.copy(), np.zeros(n, f), np.zeros(n, f), f(0.9), f(0.999)
+    for _ in range(3):
+        check(lib.dssm_adam_step(ptr(tp), ptr(tg), ptr(tm), ptr(tv), n, 0.01, 0.9, 0.999, 1e-8, ptr(st), 0.5,
+                                 _lib.stream_ptr()), "adam")
+        lr_t = f(0.01) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+        gs = g * f(0.5)
+        m = m + (gs - m) * f(1 - 0.9)
+        v = v + (gs * gs - v) * f(1 - 0.999)
+        p = p - (m * lr_t) / (np.sqrt(v) + f(1e-8))
+        b1p, b2p = f(b1p * f(0.9)), f(b2p * f(0.999))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(tp.cpu().numpy(), p, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(st.cpu().numpy(), [b1p, b2p], rtol=1e-7)
