@@ -54,8 +54,9 @@ def parse():
                     help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
                          "(unfused dW1, wire pack, 1/W Adam shard, wire shadows) with the "
                          "collectives omitted, to time the per-rank compute of the N>1 path")
-    ap.add_argument("--model", default="bow", choices=["bow", "rnn"],
-                    help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4)")
+    ap.add_argument("--model", default="bow", choices=["bow", "rnn", "multiview"],
+                    help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4); "
+                         "multiview: multi_view_dssm_v3 (config 5)")
     ap.add_argument("--feed", default="device", choices=["device", "host"],
                     help="device: batches staged in HBM before the timed region (the headline); host: "
                          "batches streamed from host CSR matrices by the native pinned async feeder "
@@ -189,10 +190,57 @@ def bench_rnn(args):
     print(json.dumps(out), flush=True)
 
 
+def bench_multiview(args):
+    """BASELINE.json config 5 (archive/multi_view_dssm_v3.py): user tower + 3 item views (30k-wide
+    sparse inputs, FC 300 -> 128, ReLU), in-batch rotated negatives, NEG=4, BS=4096 on one GPU,
+    fp32, synthetic Zipf trigram rows; the active view cycles 1, 2, 3 over the staged batches.
+    One step = forward + backward + Adam (user tower + active view).  Not the headline."""
+    import torch
+    from dssm_amd.data import ZipfColumns, synth_rows
+    from dssm_amd.multiview import MultiViewDSSM
+    B, Dv, L1, L2 = 4096, 30000, 300, 128
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev)
+    m.init_params(0)
+    cols = ZipfColumns(Dv)
+    rng = np.random.Generator(np.random.PCG64(7))
+    feeds = []
+    for b in range(3):
+        u = synth_rows(rng, cols, B, 32.0)
+        it = synth_rows(rng, cols, B, 32.0)
+        m.set_batch(u, it, b + 1)
+        feeds.append((dict(m.batch), b + 1))
+
+    def step(i):
+        m.batch, m.view = dict(feeds[i % 3][0]), feeds[i % 3][1]
+        m.train_step()
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
+           "value": round(B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic",
+           "config": {"workload": "multi_view_dssm_v3: user + 3 views (30k sparse -> 300 -> 128), in-batch "
+                                  "rotated negatives, BS=4096, NEG=4, fwd+bwd+Adam", "global_batch": B,
+                      "neg": NEG, "parallelism": "dp1"},
+           "final_loss": round(m.loss(), 3)}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     if args.model == "rnn":
         return bench_rnn(args)
+    if args.model == "multiview":
+        return bench_multiview(args)
     import torch
     import torch.distributed as dist
 

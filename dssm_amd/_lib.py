@@ -122,7 +122,11 @@ _SIGS = {
     "dssm_bn_relu_bwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float, C.c_int, _P,
                                    C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,
-                                 C.c_float, _P]),
+                                 C.c_float, C.c_int, _P]),
+    "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
+    "dssm_rows_scatter_add": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P]),
+    "dssm_relu": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P]),
+    "dssm_relu_bwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P]),
     "dssm_comm_unique_id": (C.c_int, [_P]),
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),

@@ -105,9 +105,92 @@ __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const float* __restrict__
   }
 }
 
+__global__ void k_rows_gather(const float* __restrict__ src, int lds, const int* __restrict__ map, int n,
+                              int cols, float* __restrict__ dst, int ldd) {
+  const int64_t total = (int64_t)n * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    dst[(size_t)r * ldd + c] = src[(size_t)map[r] * lds + c];
+  }
+}
+
+__global__ void k_rows_scatter_add(const float* __restrict__ src, int lds, const int* __restrict__ map,
+                                   int n, int cols, float* __restrict__ dst, int ldd) {
+  using gfloat = __attribute__((address_space(1))) float;
+  const int64_t total = (int64_t)n * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    __hip_atomic_fetch_add((gfloat*)(dst + (size_t)map[r] * ldd + c), src[(size_t)r * lds + c],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void k_relu(const float* __restrict__ x, int ldx, int rows, int cols, float* __restrict__ y,
+                       int ldy) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    y[(size_t)r * ldy + c] = fmaxf(x[(size_t)r * ldx + c], 0.f);
+  }
+}
+
+// ReLU'(0) = 0 (TF1.x ReluGrad): dx = y > 0 ? dy : 0
+__global__ void k_relu_bwd(const float* __restrict__ y, int ldy, const float* __restrict__ dy, int lddy,
+                           int rows, int cols, float* __restrict__ dx, int lddx) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    dx[(size_t)r * lddx + c] = y[(size_t)r * ldy + c] > 0.f ? dy[(size_t)r * lddy + c] : 0.f;
+  }
+}
+
+int ew_grid(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 2048)); }
+
 }  // namespace
 
 extern "C" {
+
+int dssm_rows_gather(const float* src, int lds, const int32_t* map, int n, int cols, float* dst, int ldd,
+                     void* stream) {
+  if (!src || !map || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols)
+    return oerr(DSSM_E_INVALID, "rows_gather: bad argument");
+  hipLaunchKernelGGL(k_rows_gather, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, (hipStream_t)stream, src,
+                     lds, map, n, cols, dst, ldd);
+  return hip_status();
+}
+
+int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, int cols, float* dst,
+                          int ldd, int dst_rows, void* stream) {
+  if (!src || !map || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols || dst_rows < 0)
+    return oerr(DSSM_E_INVALID, "rows_scatter_add: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(dst, 0, sizeof(float) * (size_t)dst_rows * ldd, s) != hipSuccess)
+    return oerr(DSSM_E_HIP, "rows_scatter_add: hipMemsetAsync");
+  hipLaunchKernelGGL(k_rows_scatter_add, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, s, src, lds, map, n,
+                     cols, dst, ldd);
+  return hip_status();
+}
+
+int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, void* stream) {
+  if (!x || !y || rows < 0 || cols < 0 || ldx < cols || ldy < cols) return oerr(DSSM_E_INVALID, "relu: bad argument");
+  hipLaunchKernelGGL(k_relu, dim3(ew_grid((int64_t)rows * cols)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     rows, cols, y, ldy);
+  return hip_status();
+}
+
+int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, int cols, float* dx, int lddx,
+                  void* stream) {
+  if (!y || !dy || !dx || rows < 0 || cols < 0 || ldy < cols || lddy < cols || lddx < cols)
+    return oerr(DSSM_E_INVALID, "relu_bwd: bad argument");
+  hipLaunchKernelGGL(k_relu_bwd, dim3(ew_grid((int64_t)rows * cols)), dim3(256), 0, (hipStream_t)stream, y,
+                     ldy, dy, lddy, rows, cols, dx, lddx);
+  return hip_status();
+}
+
 
 size_t dssm_spmm_bwd_ws_bytes(int rows, int D, int max_nnz) {
   if (rows <= 0 || D <= 0 || max_nnz < 0) return 0;

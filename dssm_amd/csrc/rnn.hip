@@ -474,13 +474,13 @@ int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse
 
 extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
                               float beta1, float beta2, float eps, float* state, float grad_scale,
-                              void* stream) {
+                              int advance, void* stream) {
   if (!p || !g || !m || !v || !state || n < 0) return rerr(DSSM_E_INVALID, "adam_step: bad argument");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, (int64_t)0, n, state, lr,
                      beta1, beta2, eps, grad_scale);
-  hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
+  if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }

@@ -1,0 +1,229 @@
+"""Multi-view DSSM on one MI355X (BASELINE.json config 5).
+
+The reference's archive/multi_view_dssm_v3.py:107-241: a user tower and three item-view towers
+(sparse FC1 + ReLU + FC2 + ReLU each, no batch norm), the active view's item embeddings as
+positives and in-batch rotations of them as the NEG negatives (Make_Negative_Item), x20 cosine,
+softmax, summed loss, Adam on the user tower and the active view.
+
+Composed from libdssm.so's functional C-ABI (include/dssm.h): dssm_spmm_csr_fwd /
+dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2), dssm_relu / dssm_relu_bwd,
+dssm_rows_gather / dssm_rows_scatter_add (the rotation as an index map and its backward),
+dssm_cosine_softmax_loss (shared with the BoW path), dssm_adam_step.  fp32; torch tensors are
+device storage only.
+
+The reference chooses the view with a Python comparison against a placeholder at graph build, so
+it always trains view 3; here the fed active view selects the tower.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+
+TOWERS = ("user", "view1", "view2", "view3")
+
+
+def _a64(n):
+    return -(-n // 64) * 64
+
+
+def _ld(n):
+    return -(-n // 8) * 8
+
+
+class MultiViewDSSM:
+    def __init__(self, user_d: int, view_d: Sequence[int], l1: int, l2: int, bs: int, neg: int = 4,
+                 lr: float = 0.05, gamma: float = 20.0, max_nnz_per_row: int = 96, device=None,
+                 rotations: Optional[Sequence[int]] = None, seed: int = 0):
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if len(view_d) != 3 or l1 % 4 or l2 % 4:
+            raise ValueError("three item views; l1, l2 multiples of 4")
+        self.dims = [int(user_d)] + [int(d) for d in view_d]
+        self.l1, self.l2, self.bs, self.neg = int(l1), int(l2), int(bs), int(neg)
+        self.ld1, self.ld2 = _ld(self.l1), _ld(self.l2)
+        self.lr, self.gamma = float(lr), float(gamma)
+        self.max_nnz = self.bs * int(max_nnz_per_row)
+        dev, f32 = self.device, torch.float32
+        # arena: per tower [W1; b1] ((D+1) x l1), [W2; b2] ((l1+1) x l2)
+        self.layout: Dict[str, tuple] = {}
+        off = 0
+        for t, d in zip(TOWERS, self.dims):
+            start = off
+            for name, rows, cols in ((f"{t}_1", d + 1, self.l1), (f"{t}_2", self.l1 + 1, self.l2)):
+                self.layout[name] = (off, rows, cols)
+                off = _a64(off + rows * cols)
+            self.layout[t] = (start, off)
+        self.n_params = off
+        self.params = torch.zeros(off, dtype=f32, device=dev)
+        self.grads = torch.zeros(off, dtype=f32, device=dev)
+        self.adam_m = torch.zeros(off, dtype=f32, device=dev)
+        self.adam_v = torch.zeros(off, dtype=f32, device=dev)
+        self.adam_state = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
+        BS, R = self.bs, self.bs * (2 + self.neg)
+        self.z1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
+        self.a1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
+        self.ysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)   # [user_y; item_y]
+        self.dysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)
+        self.merged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
+        self.dmerged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
+        self.dz2 = torch.zeros((BS, self.ld2), dtype=f32, device=dev)
+        self.da1 = torch.zeros((BS, self.ld1), dtype=f32, device=dev)
+        self.dz1 = torch.zeros((BS, self.ld1), dtype=f32, device=dev)
+        K = self.neg + 1
+        self.cos_raw = torch.zeros(K * BS, dtype=f32, device=dev)
+        self.cos_sim = torch.zeros(BS * K, dtype=f32, device=dev)
+        self.prob = torch.zeros(BS * K, dtype=f32, device=dev)
+        self.qnorm = torch.zeros(BS, dtype=f32, device=dev)
+        self.loss_buf = torch.zeros(2, dtype=f32, device=dev)
+        self.cos_ws = torch.zeros(2 * (-(-BS // 4)) + 64, dtype=f32, device=dev)
+        slab = max(self.lib.dssm_dense_bwd_slab_floats(BS, self.l1, self.l2, _lib.DSSM_F32), 1)
+        self.slab = torch.zeros(int(slab), dtype=f32, device=dev)
+        # one CSC-transpose workspace per tower (zero on first use, kept zero by the calls)
+        self.spmm_ws = {t: torch.zeros(int(self.lib.dssm_spmm_bwd_ws_bytes(BS, d, self.max_nnz)),
+                                       dtype=torch.uint8, device=dev) for t, d in zip(TOWERS, self.dims)}
+        self.batch = {}
+        self.view = 3
+        self.set_rotations(rotations if rotations is not None else self.default_rotations(seed))
+        self.global_step = 0
+
+    # ---- parameters ---------------------------------------------------------------------------
+    def _block(self, arena, name):
+        off, rows, cols = self.layout[name]
+        return arena[off:off + rows * cols].view(rows, cols)
+
+    def load_params(self, p: Dict[str, np.ndarray]):
+        for t in TOWERS:
+            for l in (1, 2):
+                blk = np.concatenate([p[f"{t}_W{l}"], p[f"{t}_b{l}"][None, :]], 0).astype(np.float32)
+                self._block(self.params, f"{t}_{l}").copy_(torch.from_numpy(blk))
+
+    def named(self, arena: Optional[torch.Tensor] = None) -> Dict[str, np.ndarray]:
+        a = self.params if arena is None else arena
+        out = {}
+        for t in TOWERS:
+            for l in (1, 2):
+                blk = self._block(a, f"{t}_{l}").cpu().numpy()
+                out[f"{t}_W{l}"], out[f"{t}_b{l}"] = blk[:-1], blk[-1]
+        return out
+
+    def init_params(self, seed: int = 0):
+        """W, b ~ U(-r, r), r = sqrt(6 / (fan_in + fan_out)) (multi_view_dssm_v3.py:115-185)."""
+        rng = np.random.Generator(np.random.PCG64(seed))
+        p = {}
+        for t, d in zip(TOWERS, self.dims):
+            for l, (a, b) in enumerate(((d, self.l1), (self.l1, self.l2)), 1):
+                r = np.sqrt(6.0 / (a + b))
+                p[f"{t}_W{l}"] = rng.uniform(-r, r, size=(a, b)).astype(np.float32)
+                p[f"{t}_b{l}"] = rng.uniform(-r, r, size=b).astype(np.float32)
+        self.load_params(p)
+        return p
+
+    def default_rotations(self, seed: int):
+        u = np.random.Generator(np.random.PCG64(seed)).random(self.neg)
+        return [int((u[i] + i) * self.bs / self.neg) for i in range(self.neg)]
+
+    def set_rotations(self, rot: Sequence[int]):
+        """Make_Negative_Item's offsets (fixed at graph build in the reference): negative i of user j
+        is item row (j + rot[i]) mod BS.  Sets the gather map of the merged [user; pos; neg] rows."""
+        BS = self.bs
+        rot = [int(r) % BS for r in rot]
+        if len(rot) != self.neg:
+            raise ValueError("one rotation per negative")
+        m = [np.arange(BS), BS + np.arange(BS)]
+        # merged neg row 2BS + j*NEG + i (the cosine kernel's layout) = item row (j + rot_i) % BS
+        j = np.repeat(np.arange(BS), self.neg)
+        i = np.tile(np.arange(self.neg), BS)
+        m.append(BS + (j + np.array(rot)[i]) % BS)
+        self.rot = rot
+        self.map = torch.from_numpy(np.concatenate(m).astype(np.int32)).to(self.device)
+
+    # ---- feed ---------------------------------------------------------------------------------
+    def set_batch(self, user_csr, item_csr, view: int):
+        """user_csr, item_csr: (indptr, indices, values) host arrays of BS rows each; view in 1..3."""
+        if view not in (1, 2, 3):
+            raise ValueError("active view is 1, 2 or 3")
+        for name, csr, d in (("u", user_csr, self.dims[0]), ("i", item_csr, self.dims[view])):
+            ip, ix, vv = (np.asarray(x) for x in csr)
+            if ip.size != self.bs + 1 or int(ip[-1]) > self.max_nnz:
+                raise ValueError(f"{name}: {self.bs} rows, at most {self.max_nnz} non-zeros")
+            if ix.size and (ix.min() < 0 or ix.max() >= d):
+                raise ValueError(f"{name}: column index out of range")
+            self.batch[name] = tuple(torch.from_numpy(np.ascontiguousarray(x, dt)).to(self.device)
+                                     for x, dt in ((ip, np.int32), (ix, np.int32), (vv, np.float32)))
+        self.view = view
+
+    # ---- step ---------------------------------------------------------------------------------
+    def _tower_fwd(self, key, tower, y_rows, s):
+        ip, ix, vv = self.batch[key]
+        d = self.dims[TOWERS.index(tower)]
+        w1, w2 = self._block(self.params, f"{tower}_1"), self._block(self.params, f"{tower}_2")
+        check(self.lib.dssm_spmm_csr_fwd(ptr(ip), ptr(ix), ptr(vv), self.bs, ptr(w1), _lib.DSSM_F32, self.l1,
+                                         self.l1, ptr(w1[d]), ptr(self.z1[key]), self.ld1, s), "spmm_fwd")
+        check(self.lib.dssm_relu(ptr(self.z1[key]), self.ld1, self.bs, self.l1, ptr(self.a1[key]), self.ld1, s),
+              "relu")
+        check(self.lib.dssm_dense_fwd(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
+                                      self.l1, self.l2, ptr(w2[self.l1]), ptr(y_rows), self.ld2, s), "dense_fwd")
+        check(self.lib.dssm_relu(ptr(y_rows), self.ld2, self.bs, self.l2, ptr(y_rows), self.ld2, s), "relu")
+
+    def forward(self, stream=None):
+        s = stream_ptr(stream)
+        BS = self.bs
+        self._tower_fwd("u", "user", self.ysrc[:BS], s)
+        self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], s)
+        R = BS * (2 + self.neg)
+        check(self.lib.dssm_rows_gather(ptr(self.ysrc), self.ld2, ptr(self.map), R, self.l2, ptr(self.merged),
+                                        self.ld2, s), "gather")
+        check(self.lib.dssm_cosine_softmax_loss(ptr(self.merged), self.ld2, self.l2, BS, self.neg, self.gamma,
+                                                ptr(self.cos_raw), ptr(self.cos_sim), ptr(self.prob),
+                                                ptr(self.qnorm), ptr(self.loss_buf), ptr(self.dmerged),
+                                                ptr(self.cos_ws), s), "cosine")
+
+    def _tower_bwd(self, key, tower, y_rows, dy_rows, s):
+        ip, ix, vv = self.batch[key]
+        d = self.dims[TOWERS.index(tower)]
+        w2 = self._block(self.params, f"{tower}_2")
+        check(self.lib.dssm_relu_bwd(ptr(y_rows), self.ld2, ptr(dy_rows), self.ld2, self.bs, self.l2,
+                                     ptr(self.dz2), self.ld2, s), "relu_bwd")
+        check(self.lib.dssm_dense_bwd(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
+                                      self.l1, self.l2, ptr(self.dz2), self.ld2, ptr(self.da1), self.ld1,
+                                      ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab), s), "dense_bwd")
+        check(self.lib.dssm_relu_bwd(ptr(self.a1[key]), self.ld1, ptr(self.da1), self.ld1, self.bs, self.l1,
+                                     ptr(self.dz1), self.ld1, s), "relu_bwd")
+        check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(self.dz1),
+                                           _lib.DSSM_F32, self.ld1, self.l1,
+                                           ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),
+                                           s), "spmm_bwd")
+
+    def backward(self, stream=None):
+        s = stream_ptr(stream)
+        BS, R = self.bs, self.bs * (2 + self.neg)
+        # the cosine kernel's d(mean loss)/dy x BS = d(summed loss)/dy (multi_view_dssm_v3.py:234)
+        check(self.lib.dssm_rnn_dropout(ptr(self.dmerged), ptr(self.dmerged), R, self.l2, self.ld2, 1.0, 0, 0,
+                                        float(BS), s), "scale")
+        check(self.lib.dssm_rows_scatter_add(ptr(self.dmerged), self.ld2, ptr(self.map), R, self.l2,
+                                             ptr(self.dysrc), self.ld2, 2 * BS, s), "scatter")
+        self._tower_bwd("u", "user", self.ysrc[:BS], self.dysrc[:BS], s)
+        self._tower_bwd("i", f"view{self.view}", self.ysrc[BS:], self.dysrc[BS:], s)
+
+    def apply_adam(self, stream=None):
+        s = stream_ptr(stream)
+        for k, t in enumerate(("user", f"view{self.view}")):
+            b, e = self.layout[t]
+            check(self.lib.dssm_adam_step(ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]),
+                                          ptr(self.adam_v[b:e]), e - b, self.lr, 0.9, 0.999, 1e-8,
+                                          ptr(self.adam_state), 1.0, k == 1, s), "adam")
+        self.global_step += 1
+
+    def train_step(self, stream=None):
+        self.forward(stream)
+        self.backward(stream)
+        self.apply_adam(stream)
+
+    def loss(self) -> float:
+        return float(self.loss_buf[0].item()) * self.bs

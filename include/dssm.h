@@ -237,9 +237,20 @@ int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamm
                      const float* dout, int ldd, float* dz, int lddz, float* dgamma, float* dbeta,
                      void* stream);
 /* TF1.x ApplyAdam (new_dssm.py:215-217) over n flat elements with gradient x grad_scale;
- * state = device {beta1_power, beta2_power} (start at beta1, beta2), advanced after the update. */
+ * state = device {beta1_power, beta2_power} (start at beta1, beta2), advanced after the update
+ * when advance != 0 (an optimizer step spanning several calls advances on its last one). */
 int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                   float beta2, float eps, float* state, float grad_scale, void* stream);
+                   float beta2, float eps, float* state, float grad_scale, int advance, void* stream);
+/* Row gather / scatter-add (Merge_Negative_Doc by index, its backward): dst[r] = src[map[r]];
+ * dst[map[r]] += src[r] over r < n after dst (dst_rows x ldd) is cleared.  fp32. */
+int dssm_rows_gather(const float* src, int lds, const int32_t* map, int n, int cols, float* dst, int ldd,
+                     void* stream);
+int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, int cols, float* dst,
+                          int ldd, int dst_rows, void* stream);
+/* tf.nn.relu and its gradient (ReluGrad: dx = y > 0 ? dy : 0); y may alias x. */
+int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, void* stream);
+int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, int cols, float* dx,
+                  int lddx, void* stream);
 
 /* ---- data parallel (one RCCL all-reduce of the gradient arena per step) ----------------- */
 /* unique_id: 128 bytes from dssm_comm_unique_id() on rank 0, shared by the caller. */

@@ -128,7 +128,7 @@ def test_adam_step():
     f = np.float32
     p, m, v, b1p, b2p = p0.copy(), np.zeros(n, f), np.zeros(n, f), f(0.9), f(0.999)
     for _ in range(3):
-        check(lib.dssm_adam_step(ptr(tp), ptr(tg), ptr(tm), ptr(tv), n, 0.01, 0.9, 0.999, 1e-8, ptr(st), 0.5,
+        check(lib.dssm_adam_step(ptr(tp), ptr(tg), ptr(tm), ptr(tv), n, 0.01, 0.9, 0.999, 1e-8, ptr(st), 0.5, 1,
                                  _lib.stream_ptr()), "adam")
         lr_t = f(0.01) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
         gs = g * f(0.5)
