@@ -120,7 +120,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
         if (nvalid > 4) *reinterpret_cast<float4*>(a.g + o + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     } else {
-      gather_accumulate(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
+      gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
     }
     if (nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
       const int k = nvalid >= 8 ? 8 : 4;
@@ -215,7 +215,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       const int cc = c0 + lane * 8;
       const int nvalid = a.n - cc;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (s < e) gather_accumulate(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, acc);
+      if (s < e) gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, acc);
 #pragma unroll
       for (int i = 0; i < 8; ++i) part[wv][lane * 8 + i] = acc[i];
       __syncthreads();

@@ -56,6 +56,23 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   const int K = neg + 1;
   const size_t plane = (size_t)2 * ld;
   const int nrow_blocks = (bs + 3) / 4;
+  // ---- the rows' raw loads go out first, ahead of the coefficient prologue (they need no
+  // coefficient): query row + K doc rows
+  float q[EPL], d[KM][EPL], zq[EPL], zd[FSC ? KM : 1][EPL];
+  if (j < bs && (int)blockIdx.x < nrow_blocks) {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int c = lane + 64 * e;
+      q[e] = (c < n) ? z[(size_t)j * ld + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const int c = lane + 64 * e;
+        d[k][e] = (k < K && c < n) ? z[(size_t)doc_row(j, k, bs, neg) * ld + c] : 0.f;
+      }
+  }
   if constexpr (FSC) {
     if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
       fs_materialize_fwd(fs);
@@ -76,20 +93,6 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
 #pragma unroll
   for (int e = 0; e < EPL; ++e) bq1[e] = bq2[e] = bd1[e] = bd2[e] = 0.f;
   if (j < bs) {
-    // ---- all loads first: query row + K doc rows
-    float q[EPL], d[KM][EPL], zq[EPL], zd[FSC ? KM : 1][EPL];
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) {
-      const int c = lane + 64 * e;
-      q[e] = (c < n) ? z[(size_t)j * ld + c] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < KM; ++k)
-#pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const int c = lane + 64 * e;
-        d[k][e] = (k < K && c < n) ? z[(size_t)doc_row(j, k, bs, neg) * ld + c] : 0.f;
-      }
     if (tm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp();
     if constexpr (FSC) {

@@ -41,7 +41,10 @@ template <> struct RawRow8<float> {
 // Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc.  All 64 lanes must be
 // active (the index broadcast reads every lane's register; v_readlane ignores EXEC); lanes with
 // nvalid <= 0 only skip their loads.
-template <typename T>
+// REM: rows in flight in the remainder (< U) loop: 2 for the short CSC columns of dW1 (most light
+// columns have a handful of entries: their chain is the remainder), 1 for the SpMM's ~32-entry rows
+// (measured: the wider remainder costs it occupancy).
+template <typename T, int REM = 1>
 __device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
                                                   const float* __restrict__ val, int s, int e,
                                                   const T* __restrict__ M, int ldm, int c,
@@ -68,6 +71,16 @@ __device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
       for (int u = 0; u < U; ++u) {
         const float v = bcast_f(my_v, j + u);
         if (nvalid > 0) x[u].fma(v, acc);
+      }
+    }
+    for (; REM == 2 && j + 2 <= cnt; j += 2) {  // remainder: two rows in flight, FMAs in entry order
+      RawRow8<T> x0, x1;
+      const int r0 = bcast_i(my_i, j), r1 = bcast_i(my_i, j + 1);
+      if (nvalid > 0) {
+        x0.load(M + (size_t)r0 * ldm + c, nvalid);
+        x1.load(M + (size_t)r1 * ldm + c, nvalid);
+        x0.fma(bcast_f(my_v, j), acc);
+        x1.fma(bcast_f(my_v, j + 1), acc);
       }
     }
     for (; j < cnt; ++j) {
