@@ -19,6 +19,7 @@
 //  * dense float4 streaming over the rest of the arena (or all of it when unfused).
 // The last block to finish advances the device beta powers.
 #include "common.h"
+#include "flat.h"
 #include "gather.h"
 #include "launch.h"
 
@@ -85,23 +86,16 @@ __device__ __forceinline__ float4 slab_grad4(const SlabList& sl, int64_t i, cons
   return *reinterpret_cast<const float4*>(g + i);
 }
 
-__device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, float alpha,
-                                      float b1c, float b2c, float eps) {
-  m += (g - m) * b1c;
-  v += (g * g - v) * b2c;
-  p -= (m * alpha) / (sqrtf(v) + eps);
-}
 
 // One wave updates row c of [W1; b1] (CSC column c): light rows' gradient is gathered inline
 // from the CSC transpose and dZ1, heavy rows' gradient (k_dw1_heavy) is read and cleared.
 template <typename TZ>
-__device__ __forceinline__ void w1_row(const AdamStep& a, int c, float alpha) {
+__device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha) {
   const int lane = lane_id();
   const int n = a.n;
-  const int s = a.col_ptr[c], e = a.col_ptr[c + 1];
   const bool heavy = e - s > kLightEntries;
   if (heavy && a.item_blocks) return;  // updated by the heavy-item workgroups
-  if (e == s && a.w1_flat) return;     // untouched row: the flat role's decay-only pass
+  if (e == s && (a.w1_flat || a.flat_elsewhere)) return;  // untouched: the flat roles' pass
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
@@ -269,13 +263,23 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
   const int64_t nb = gridDim.x, b0 = blockIdx.x;
   const int nh = a.item_blocks, nw = a.w1_blocks;
   const int nf = (int)nb - nh - nw;
-  const bool is_heavy = b0 < nh;
-  const int hcount = (int)(is_heavy ? b0 : nh);
-  const int64_t j = b0 - hcount;  // index among the other roles
+  bool is_heavy = b0 < nh;
+  int hcount = (int)(is_heavy ? b0 : nh);
+  int64_t j = b0 - hcount;  // index among the other roles
   const int64_t nwf = nw + nf;
   int wcount;
   bool is_w1;
-  if (a.interleave) {
+  if (a.interleave >= 2) {
+    // 2: heavy items, flat/dense streaming, W1 rows; 3: flat/dense, heavy items, W1 rows
+    const int64_t f0 = a.interleave == 2 ? nh : 0, h0 = a.interleave == 2 ? 0 : nf;
+    const int64_t w0 = (int64_t)nh + nf;
+    is_heavy = b0 >= h0 && b0 < h0 + nh;
+    hcount = (int)(b0 - h0);
+    is_w1 = b0 >= w0;
+    wcount = (int)(b0 - w0);
+    j = (b0 - f0) + nw;  // flat/dense index = j - wcount below
+    if (!is_heavy && !is_w1) wcount = nw;
+  } else if (a.interleave) {
     wcount = nwf ? (int)(j * nw / nwf) : 0;
     is_w1 = !is_heavy && nwf && (j + 1) * nw / nwf > wcount;
   } else {
@@ -286,38 +290,41 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
     heavy_items<TZ>(a, alpha, hcount);
   } else if (is_w1) {
     const int b = wcount;
-    for (int c = b * 4 + (threadIdx.x >> 6); c <= a.D; c += a.w1_blocks * 4)
-      w1_row<TZ>(a, c, alpha);
+    // the next row's column range is loaded while this row is processed (one dependent load
+    // fewer on each row's chain)
+    const int stride = a.w1_blocks * 4;
+    int c = b * 4 + (threadIdx.x >> 6);
+    int s = 0, e = 0;
+    if (c <= a.D) {
+      s = a.col_ptr[c];
+      e = a.col_ptr[c + 1];
+    }
+    for (; c <= a.D; c += stride) {
+      const int cn = c + stride;
+      int sn = 0, en = 0;
+      if (cn <= a.D) {
+        sn = a.col_ptr[cn];
+        en = a.col_ptr[cn + 1];
+      }
+      w1_row<TZ>(a, c, s, e, alpha);
+      s = sn;
+      e = en;
+    }
   } else {
     const int bi = (int)(j - wcount);
-    if (a.w1_flat) {
-      // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
+    if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
       const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
       for (int64_t i = (int64_t)bi * blockDim.x + threadIdx.x; i < w4;
            i += (int64_t)a.dense_blocks * blockDim.x) {
         const int c = (int)((i * 4) / a.n);
         if (a.col_ptr[c + 1] != a.col_ptr[c]) continue;
-        if (a.gout) {  // gradient pass: an untouched row's gradient is zero
-          if (c < a.D) reinterpret_cast<uint2*>(a.gout)[i] = make_uint2(0u, 0u);
-          continue;
-        }
-        float4 pp = reinterpret_cast<float4*>(a.p)[i];
-        float4 mm = reinterpret_cast<float4*>(a.m)[i];
-        float4 vv = reinterpret_cast<float4*>(a.v)[i];
-        adam1(pp.x, mm.x, vv.x, 0.f, alpha, a.b1c, a.b2c, a.eps);
-        adam1(pp.y, mm.y, vv.y, 0.f, alpha, a.b1c, a.b2c, a.eps);
-        adam1(pp.z, mm.z, vv.z, 0.f, alpha, a.b1c, a.b2c, a.eps);
-        adam1(pp.w, mm.w, vv.w, 0.f, alpha, a.b1c, a.b2c, a.eps);
-        reinterpret_cast<float4*>(a.p)[i] = pp;
-        reinterpret_cast<float4*>(a.m)[i] = mm;
-        reinterpret_cast<float4*>(a.v)[i] = vv;
-        if (a.shadow && c < a.D) {
-          uint2 q;
-          q.x = pack2bf(pp.x, pp.y);
-          q.y = pack2bf(pp.z, pp.w);
-          *reinterpret_cast<uint2*>(a.shadow + (size_t)c * a.ldsh + (i * 4 - (int64_t)c * a.n)) = q;
-        }
+        if (c < a.D) reinterpret_cast<uint2*>(a.gout)[i] = make_uint2(0u, 0u);
       }
+    } else if (a.w1_flat) {
+      // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
+      FlatSlice f{a.p, a.m, a.v, a.shadow, a.ldsh, a.n, a.D, a.col_ptr, a.st, a.lr, a.b1c, a.b2c, a.eps,
+                  0, (int64_t)(a.D + 1) * a.n / 4, a.dense_blocks};
+      flat_untouched(f, bi);
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
     for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < na + nt;
@@ -479,7 +486,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   a.interleave = interleave;
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, item_cap);
-  a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0) ? 1 : 0;
+  a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0 && !a.flat_elsewhere) ? 1 : 0;
   if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) +
                      (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);

@@ -434,14 +434,18 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
                                                          u16* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
                                                          int loss_blocks,
-                                                         float* __restrict__ loss_out) {
+                                                         float* __restrict__ loss_out,
+                                                         FlatSlice flat, int nwork) {
   // one extra block past the element blocks: the step's loss / accuracy from the cosine kernel's
   // partials (deferred finalize: no cross-workgroup ticket in the cosine launch) and dgamma /
   // dbeta, off the element blocks' critical path
-  const int nwork = (int)gridDim.x - 1;
-  if ((int)blockIdx.x == nwork) {
-    if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
-    fs_materialize_bwd(b);
+  if ((int)blockIdx.x >= nwork) {
+    if ((int)blockIdx.x == nwork) {
+      if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
+      fs_materialize_bwd(b);
+    } else {
+      flat_untouched(flat, (int)blockIdx.x - nwork - 1);  // untouched W1 rows (flat.h)
+    }
     return;
   }
   __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
@@ -601,15 +605,17 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part, int loss_blocks,
-                                     float* loss_out) {
+                                     float* loss_out,
+                                     const FlatSlice* flat) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
   static const int gmax = [] {
     const char* e = std::getenv("DSSM_APPLY_GRID");
     return e ? std::max(1, std::atoi(e)) : 1024;
   }();
   const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), gmax);
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid + 1), dim3(256), 0, s, Z, dA, b, (u16*)dZ, loss_part,
-                     loss_blocks, loss_out);
+  const FlatSlice fl = flat ? *flat : FlatSlice{};
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid + 1 + fl.nblocks), dim3(256), 0, s, Z, dA, b, (u16*)dZ,
+                     loss_part, loss_blocks, loss_out, fl, grid);
   return hipGetLastError();
 }
 

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp) {
+    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp, FlatSlice flat) {
   unsigned long long* tm = (tmp && threadIdx.x == 0 && blockIdx.x == 1) ? tmp : nullptr;
   int ti = 0;
   auto stamp = [&]() {
@@ -75,7 +75,8 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   }
   if constexpr (FSC) {
     if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
-      fs_materialize_fwd(fs);
+      if ((int)blockIdx.x == nrow_blocks) fs_materialize_fwd(fs);
+      else flat_untouched(flat, (int)blockIdx.x - nrow_blocks - 1);  // untouched W1 rows (flat.h)
       return;
     }
     fs_coef_stage<(2 * kCosMaxN) / 256>(fs, threadIdx.x, 256,
@@ -286,18 +287,20 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               bool split, hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              unsigned long long* timing) {
+                              unsigned long long* timing,
+                              const FlatSlice* flat) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
   unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * blocks + 32);
-  dim3 grid(blocks + (fused ? 1 : 0)), block(256);  // fused: + the materialising block
+  const FlatSlice fl = (flat && fused) ? *flat : FlatSlice{};
+  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks), block(256);  // fused: + materialising, flat blocks
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \
   hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
                      y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,               \
-                     (split || defer_finalize) ? 1 : 0, fs, timing)
+                     (split || defer_finalize) ? 1 : 0, fs, timing, fl)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \

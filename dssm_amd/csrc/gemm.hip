@@ -735,11 +735,14 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
 // A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
 // EMA update) off the tiles' critical path.
 template <bool BN_A, int FS>
-__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
+__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles,
+                                                    FlatSlice flat) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
   WG_TL(a.N == 300 ? 0 : 1, 0);
   if ((int)blockIdx.x >= ntiles) {
-    if (BN_A && FS == 1 && f.in_from_sums) fs_materialize_fwd(f.in);
+    const bool mat = BN_A && FS == 1 && f.in_from_sums;
+    if (mat && (int)blockIdx.x == ntiles) fs_materialize_fwd(f.in);
+    else flat_untouched(flat, (int)blockIdx.x - ntiles - (mat ? 1 : 0));
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);
@@ -1138,7 +1141,8 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
                                     double* out_sum, int out_copies, hipStream_t s,
-                                    unsigned long long* timing) {
+                                    unsigned long long* timing,
+                                    const FlatSlice* flat) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
   dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
@@ -1158,8 +1162,9 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   if (wk_on && K <= kWkMaxK && (row_split % 128) == 0) {
     const int Kp = (K + 31) & ~31;
     const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 128);
-    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0)), dim3(512),
-                       wk_smem_bytes(Kp), s, a, f, nx, ntiles);
+    const FlatSlice fl = flat ? *flat : FlatSlice{};
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0) + fl.nblocks),
+                       dim3(512), wk_smem_bytes(Kp), s, a, f, nx, ntiles, fl);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);

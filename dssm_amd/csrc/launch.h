@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "flat.h"
+
 namespace dssm {
 
 struct BnSide;  // bnfuse.h
@@ -84,7 +86,8 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
                                     double* out_sum, int out_copies, hipStream_t s,
-                                    unsigned long long* timing = nullptr);
+                                    unsigned long long* timing = nullptr,
+    const FlatSlice* flat = nullptr);
 // Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
 // z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
 // defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
@@ -117,7 +120,8 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 // also writes b.dgamma / b.dbeta.
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part = nullptr,
-                                     int loss_blocks = 0, float* loss_out = nullptr);
+                                     int loss_blocks = 0, float* loss_out = nullptr,
+    const FlatSlice* flat = nullptr);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
@@ -137,7 +141,8 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               bool split, hipStream_t s, const BnSide* fused = nullptr,
-                              bool defer_finalize = false, unsigned long long* timing = nullptr);
+                              bool defer_finalize = false, unsigned long long* timing = nullptr,
+    const FlatSlice* flat = nullptr);
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 inline int cosine_blocks(int bs) { return (bs + 3) / 4; }
 hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s);
@@ -221,6 +226,8 @@ struct AdamStep {
   int interleave;
   // zeroed once every block has read heavy_n (the next step's rank launch does not reset it)
   int* heavy_reset;
+  // the untouched W1 rows were updated by FlatSlice roles earlier in the step (flat.h): skip them
+  int flat_elsewhere;
   // gradient pass (data parallel, bf16 wire): the W1 roles compute dW1 rows (inline gather, heavy
   // items, zero for untouched rows) and write them as bf16 to gout (arena layout; the bias row as
   // fp32 into g) instead of updating parameters; no dense range, no beta-power advance

@@ -228,6 +228,16 @@ struct dssm_plan {
   // Adam (DSSM_RANK_PREFETCH=1; measured slower: the cross-stream fork / join in the graph costs
   // more than the rank launch it hides); the forward of that batch then skips its rank launch
   bool rank_prefetch = false;
+  // untouched W1 rows' decay-only Adam update spread over the step's latency-bound launches
+  // (flat.h) instead of the Adam launch: only inside whole steps (train_step / step graphs), where
+  // Adam is sure to follow.  DSSM_FLAT_SPREAD=0 keeps it in Adam; "a,b,c" = workgroups given to
+  // the last NT GEMM, the cosine and the first BN-backward apply launches (0 skips a launch).
+  // Opt-in (DSSM_FLAT_SPREAD=a,b,c): measured slower -- Adam loses only ~6 us (its critical path
+  // is the W1-row gathers, not the streaming) while the host launches grow by more (205 -> 211).
+  bool flat_spread = false;
+  int flat_blocks[3] = {128, 256, 512};
+  bool in_full_step = false;  // set by train_step / step-graph capture
+  bool flat_this_step = false;  // the slices were enqueued: this step's Adam skips untouched rows
   const int32_t* rank_prefetched = nullptr;
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   bool csc_pending = false;
@@ -432,6 +442,41 @@ struct dssm_plan {
   }
 };
 
+// Whether this step spreads the untouched W1 rows' Adam update (flat.h), and slice k (0: last NT
+// GEMM, 1: cosine, 2: first BN-backward apply) of the [W1; b1] block's float4 range, split in
+// proportion to the workgroups each launch gives it.
+static bool flat_spread_on(const dssm_plan* P) {
+  return P->flat_spread && P->in_full_step && P->fused_w1_adam && P->heavy_in_adam() && P->merged_csc() &&
+         P->Lt.bf16 && (P->Lt.n[0] % 4) == 0 && (P->flat_blocks[0] + P->flat_blocks[1] + P->flat_blocks[2]) > 0;
+}
+
+static dssm::FlatSlice flat_slice(const dssm_plan* P, int k) {
+  const Layout& Lt = P->Lt;
+  const dssm_config& c = P->cfg;
+  dssm::FlatSlice f{};
+  f.p = P->p;
+  f.m = P->m;
+  f.v = P->v;
+  f.shadow = P->at<uint16_t>(Lt.shadow[0]);
+  f.ldsh = Lt.ldp[0];
+  f.n = Lt.n[0];
+  f.D = Lt.D;
+  f.col_ptr = P->at<int>(Lt.col_ptr);
+  f.st = P->at<float>(Lt.adam_state);
+  f.lr = c.lr;
+  f.b1c = 1.0f - c.beta1;
+  f.b2c = 1.0f - c.beta2;
+  f.eps = c.adam_eps;
+  const int64_t w4 = (int64_t)(Lt.D + 1) * Lt.n[0] / 4;
+  const int tot = P->flat_blocks[0] + P->flat_blocks[1] + P->flat_blocks[2];
+  int before = 0;
+  for (int i = 0; i < k; ++i) before += P->flat_blocks[i];
+  f.i4_begin = w4 * before / tot;
+  f.i4_end = w4 * (before + P->flat_blocks[k]) / tot;
+  f.nblocks = P->flat_blocks[k];
+  return f;
+}
+
 namespace dssm {
 int report_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 }  // namespace dssm
@@ -531,6 +576,16 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
     }
   }
   if (const char* e = std::getenv("DSSM_RANK_PREFETCH")) P->rank_prefetch = e[0] != '0';
+  if (const char* e = std::getenv("DSSM_FLAT_SPREAD")) {
+    int a = 0, b = 0, c = 0;
+    if (e[0] == '0' && e[1] == 0) P->flat_spread = false;
+    else if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
+      P->flat_spread = true;
+      P->flat_blocks[0] = std::max(0, a);
+      P->flat_blocks[1] = std::max(0, b);
+      P->flat_blocks[2] = std::max(0, c);
+    }
+  }
   if (const char* e = std::getenv("DSSM_WIRE_GRAD_PASS")) P->wire_grad_pass = e[0] != '0';
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
@@ -746,6 +801,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     else if (!P->spmm_stats)
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s));
+    const bool flat_on = flat_spread_on(P);
+    const dssm::FlatSlice fs0 = flat_slice(P, 0), fs1 = flat_slice(P, 1);
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
@@ -753,7 +810,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS,
           P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
           P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), P->fcopies(l), s,
-          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 192 : nullptr));
+          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 192 : nullptr,
+          (flat_on && l == Lt.L - 1 && fs0.nblocks) ? &fs0 : nullptr));
     }
     const int lL = Lt.L - 1;
     const dssm::BnSide last = P->bn_side(lL);
@@ -763,7 +821,9 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
         P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
         P->split_finalize, s, &last, /*defer_finalize=*/true,
-        P->nt_timing ? P->at<unsigned long long>(Lt.dense_timing) : nullptr));
+        P->nt_timing ? P->at<unsigned long long>(Lt.dense_timing) : nullptr,
+        (flat_on && fs1.nblocks) ? &fs1 : nullptr));
+    P->flat_this_step = flat_on;
     P->fwd_train_done = true;
     P->fwd_fused = true;
     P->loss_pending = true;
@@ -847,6 +907,7 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
 
 static int backward_impl(dssm_plan* P, void* stream);
 
+
 int dssm_plan_backward(dssm_plan* P, void* stream) {
   if (int rc = backward_impl(P, stream)) return rc;
   if (P->gwire && !wire_gradient_pass(P))  // data parallel: the W1 gradient rows leave as bf16
@@ -881,10 +942,12 @@ static int backward_impl(dssm_plan* P, void* stream) {
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
+      const dssm::FlatSlice fs2 = flat_slice(P, 2);
       HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                               P->at<uint16_t>(Lt.dZ[l]), s,
                                               fin ? P->at<float>(Lt.loss_j) : nullptr,
-                                              dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss)));
+                                              dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss),
+                                              (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr));
       if (fin) P->loss_pending = false;
       if (l == 0) break;
       HIP_TRY(dssm::launch_bwd_pair(
@@ -1027,6 +1090,7 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     fill_w1_roles(P, a);
     a.d4_begin = rest / 4;
     if (a.heavy_n) a.heavy_reset = const_cast<int*>(a.heavy_n);
+    a.flat_elsewhere = P->flat_this_step ? 1 : 0;  // the step's slices updated the untouched rows
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
@@ -1045,6 +1109,7 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
   P->probe_end(DSSM_PROBE_ADAM, s);
   P->grads_clean = true;
+  P->flat_this_step = false;
   return DSSM_OK;
 }
 
@@ -1093,9 +1158,14 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* P, int on) {
 }
 
 int dssm_plan_train_step(dssm_plan* P, void* stream) {
-  if (int rc = dssm_plan_forward(P, 1, stream)) return rc;
-  if (int rc = dssm_plan_backward(P, stream)) return rc;
-  return dssm_plan_adam(P, 1.0f, stream);
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  P->in_full_step = true;  // Adam follows: the untouched rows' update may ride in the step's launches
+  int rc = dssm_plan_forward(P, 1, stream);
+  if (!rc) rc = dssm_plan_backward(P, stream);
+  if (!rc) rc = dssm_plan_adam(P, 1.0f, stream);
+  P->in_full_step = false;
+  P->flat_this_step = false;
+  return rc;
 }
 
 int dssm_plan_check(dssm_plan* P, void* stream) {
@@ -1179,11 +1249,14 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
   }
   P->capturing = g;
   int rc = DSSM_OK;
+  P->in_full_step = (parts & DSSM_GRAPH_FWD_BWD) && (parts & DSSM_GRAPH_ADAM);
   if (parts & DSSM_GRAPH_FWD_BWD) {
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
   }
   if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
+  P->in_full_step = false;
+  P->flat_this_step = false;
   if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
   if (!rc && (parts & DSSM_GRAPH_WIRE_SHADOWS)) rc = dssm_plan_wire_shadows(P, stream);
   P->capturing = nullptr;
@@ -1243,6 +1316,7 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   int rc = DSSM_OK;
   const bool prefetch = P->rank_prefetch && P->merged_csc() && P->fused_w1_adam && P->heavy_in_adam();
   P->rank_prefetched = nullptr;
+  P->in_full_step = true;
   for (int i = 0; i < nsteps && !rc; ++i) {
     // probes (event-record nodes) ride in the first step only
     g->probes = with_probes != 0 && i == 0;
@@ -1278,6 +1352,8 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
       P->rank_prefetched = indptrs[i + 1];
     }
   }
+  P->in_full_step = false;
+  P->flat_this_step = false;
   P->rank_prefetched = nullptr;
   g->probes = with_probes != 0;
   P->capturing = nullptr;
