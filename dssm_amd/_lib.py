@@ -12,6 +12,8 @@ import os
 import torch  # noqa: F401  (must precede the library load, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdssm.so")
+# diagnostics only: an alternative in-tree build of the same library (A/B of compile-time variants)
+LIB_PATH = os.environ.get("DSSM_LIB_PATH", LIB_PATH)
 
 DSSM_ABI_VERSION = 1
 DSSM_MAX_LAYERS = 8

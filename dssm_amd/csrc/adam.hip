@@ -251,8 +251,13 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
 // only needs every other block to have READ them, which precedes their arrival) advances them
 // (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
 // the ticket.
+#ifdef DSSM_ADAM_WPE  // diagnostics builds: a minimum occupancy (waves per SIMD) for the step kernel
+#define DSSM_ADAM_ATTR __attribute__((amdgpu_waves_per_eu(DSSM_ADAM_WPE)))
+#else
+#define DSSM_ADAM_ATTR
+#endif
 template <typename TZ>
-__global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
+__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
