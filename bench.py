@@ -100,7 +100,7 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
 
 
 # probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py)
-PMC_KERNELS = {"adam": "k_adam_step<{t}>", "spmm_fwd": "k_spmm_fwd<{t}>"}
+PMC_KERNELS = {"adam": "k_adam_step<{t}>", "spmm_fwd": "k_spmm_scan<{t}>"}  # the SpMM rides in k_spmm_scan
 
 
 def pmc_traffic(dtype: str):
