@@ -272,6 +272,7 @@ struct NtFuse {
   const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
   unsigned long long* tm;  // optional phase stamps (diagnostics: DSSM_NT_TIMING=1)
+  int lds_epi;             // whole-K tiles: C staged through LDS, stored as 16-B row segments
 };
 
 template <bool BN_A, int FS>
@@ -486,8 +487,14 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NtParams a, NtFuse f) {
 constexpr int kWkMaxK = 352;
 constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: 128 rows x Kp/8 / 512
 __host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
-__host__ __device__ inline size_t wk_smem_bytes(int Kp) {
-  return (size_t)(128 + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4 + 4 * 64 * 2 * 8;
+// LDS: A / B panels, BN coefficients, then the column-sum reduction.  The LDS epilogue stages a
+// [128][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
+__host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi) {
+  const size_t panels = (size_t)(128 + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4;
+  return (lds_epi && panels < (size_t)128 * 68 * 4) ? (size_t)128 * 68 * 4 : panels;
+}
+__host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0) {
+  return wk_red_offset(Kp, lds_epi) + 4 * 64 * 2 * 8;
 }
 
 template <bool BN_A, int FS>
@@ -498,7 +505,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   u16* sA = wk_smem;                                     // [128][LDK]
   u16* sB = sA + 128 * LDK;                              // [64][LDK]
   float* sCoef = reinterpret_cast<float*>(sB + 64 * LDK);  // [tower][inv|shift][Kp]
-  double* sRed = reinterpret_cast<double*>(sCoef + 4 * Kp);  // [4 wm][64][2]
+  double* sRed = reinterpret_cast<double*>(reinterpret_cast<char*>(wk_smem) +
+                                           wk_red_offset(Kp, f.lds_epi));  // [4 wm][64][2]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int bm = ty * 128, bn = tx * 64;
@@ -664,6 +672,13 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   if (tm) { asm volatile("s_nop 0" :: "v"(acc[0][0][0]), "v"(acc[1][1][3])); }
   stamp();
   // ---- epilogue
+  // lds_epi: the tile's values go to LDS (the A panel's space, free once every wave is past its
+  // last MFMA) and leave as 16-B row segments (full 256-B rows) instead of the accumulator
+  // layout's 4-B scattered stores
+  const bool lds_epi = f.lds_epi != 0;
+  float* sC = reinterpret_cast<float*>(sA);  // [128][68]
+  constexpr int kCld = 68;
+  if (lds_epi) __syncthreads();
   double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -676,7 +691,10 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         if (m < M && n < ldc) {
           const float v = acc[i][j][r];
           const float x = (n < N) ? (a.bias ? v + a.bias[n] : v) : 0.f;
-          a.C[(size_t)m * ldc + n] = x;
+          if (lds_epi)
+            sC[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * kCld + wn * 32 + j * 16 + (lane & 15)] = x;
+          else
+            a.C[(size_t)m * ldc + n] = x;
           if constexpr (FS == 1) {
             cs[j] += x;
             cq[j] += (double)x * x;
@@ -715,6 +733,17 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
                          sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
         atomic_add_f64(f.out_sum + (size_t)(ty % f.out_copies) * 4 * ldc + (size_t)(tower * 2 + st) * ldc + n, v);
       }
+    }
+  }
+  if (lds_epi) {
+    __syncthreads();
+    const int ncols = min(64, ldc - bn);  // multiple of 8: ldc = ldp8(N)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = t + 512 * k, r = idx >> 4, q = (idx & 15) * 4;
+      if (bm + r < M && q < ncols)
+        *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) =
+            *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
     }
   }
   if (tm) {
@@ -1155,6 +1184,11 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   f.out_sum = out_sum;
   f.out_copies = out_copies;
   f.tm = timing;
+  static const int lds_epi = [] {
+    const char* e = std::getenv("DSSM_NT_LDS_EPI");
+    return e ? std::atoi(e) : 1;  // measured: 14.4 (on) vs 16.2 us (off) per NT launch
+  }();
+  f.lds_epi = lds_epi;
   static const bool wk_on = [] {
     const char* e = std::getenv("DSSM_NT_WHOLEK");
     return !(e && e[0] == '0');
@@ -1164,7 +1198,7 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 128);
     const FlatSlice fl = flat ? *flat : FlatSlice{};
     hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0) + fl.nblocks),
-                       dim3(512), wk_smem_bytes(Kp), s, a, f, nx, ntiles, fl);
+                       dim3(512), wk_smem_bytes(Kp, f.lds_epi), s, a, f, nx, ntiles, fl);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);
@@ -1186,6 +1220,11 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   f.tm = timing;
   f.zb = z_prev;
   f.coefb = coef_prev;
+  static const int pair_lds_epi = [] {
+    const char* e = std::getenv("DSSM_PAIR_LDS_EPI");
+    return e ? std::atoi(e) : 0;  // measured: 18.1 (off) vs 18.3 us (on) per pair launch
+  }();
+  f.lds_epi = pair_lds_epi;
   static const bool wk_pair = [] {
     const char* e = std::getenv("DSSM_PAIR_WHOLEK");
     return !(e && e[0] == '0');
@@ -1198,7 +1237,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
     const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
     const int tn_x = cdiv(n, 64), tn_y = cdiv(Mw, 128);
     const int tn_blocks = tn_x * tn_y * nsplit;
-    const size_t smem = std::max(wk_smem_bytes(Kp), tw_smem_bytes());
+    const size_t smem = std::max(wk_smem_bytes(Kp, f.lds_epi), tw_smem_bytes());
     hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks + tn_blocks), dim3(512), smem, s, a, f, nt_x,
                        nt_blocks, p, tn_x, tn_y);
     *deferred_splits = 0;

@@ -54,6 +54,7 @@ CASES = [
     (1000, (100, 100), 128, 4),          # C1 (reference config.py widths)
     (1000, (100, 100, 64), 64, 3),
     (5000, (300, 300, 128), 96, 4),      # C2 shape, small batch
+    (2000, (40, 64, 32), 128, 4),        # whole-K tiles with K < 64: LDS epilogue larger than the panels
 ]
 
 
