@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libdssm.so")
 SOURCES = ["spmm.hip", "gemm.hip", "bn.hip", "cosine.hip", "adam.hip", "dense.hip", "plan.hip", "feed.hip", "rnn.hip", "ops.hip"]
-HEADERS = ["common.h", "launch.h", "gather.h", "bnfuse.h", "dense.h"]
+HEADERS = ["common.h", "launch.h", "gather.h", "bnfuse.h", "dense.h", "flat.h"]
 ARCH = os.environ.get("DSSM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]

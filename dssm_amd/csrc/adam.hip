@@ -396,6 +396,8 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   }
 }
 
+__global__ void k_noop() {}
+
 // beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32): the separate-
 // launch variant (A/B knob DSSM_ADAM_SEP_ADVANCE=1)
 __global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2, int* heavy_reset) {
@@ -501,6 +503,11 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
+  static const bool gap_probe = [] {  // diagnostics: an empty launch after the step kernel
+    const char* e = std::getenv("DSSM_GAP_PROBE");
+    return e && e[0] == '1';
+  }();
+  if (gap_probe) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
   if (!a.ticket && !a.gout)
     hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2, a.heavy_reset);
   return hipGetLastError();
