@@ -63,6 +63,12 @@ def parse():
                          "inside the timed region (PCIe-inclusive rate, N=1)")
     ap.add_argument("--wire", default="auto", choices=["auto", "bf16", "fp32"],
                     help="zero schedule: W1 rows on a bf16 or fp32 wire (auto: bf16 in bf16 mode)")
+    ap.add_argument("--columns", default="zipf", choices=["zipf", "uniform"],
+                    help="column-id distribution of the synthetic batches (SURVEY 8d: Zipf(1.1) headline, "
+                         "uniform variant)")
+    ap.add_argument("--fwd-only", type=int, default=1,
+                    help="also time the forward alone (eval mode: EMA-BN forward + cosine + loss, "
+                         "new_dssm.py:274-285) over the staged batches, N=1")
     return ap.parse_args()
 
 
@@ -235,6 +241,43 @@ def bench_multiview(args):
     print(json.dumps(out), flush=True)
 
 
+def fwd_only(model, staged, args, stream):
+    """Forward alone, eval mode (on_train=False: EMA-BN, cosine, softmax, loss; new_dssm.py:85-86,
+    274-285) over the staged batches, after the training measurement (the step's own forward is
+    not separable in time: the training forward also builds the CSC transpose for the backward).
+    One graph per staged batch where capture works, else eager launches."""
+    import torch
+    graphs = []
+    try:
+        for ip, ix, vv in staged:
+            model.set_batch(indptr=ip, indices=ix, values=vv)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                model.forward(False)
+            graphs.append(g)
+        launch = "hipgraph"
+    except Exception:  # capture unsupported: eager launches
+        graphs, launch = [], "eager"
+
+    def run(i0, n):
+        for i in range(i0, i0 + n):
+            if graphs:
+                graphs[i % len(graphs)].replay()
+            else:
+                ip, ix, vv = staged[i % len(staged)]
+                model.set_batch(indptr=ip, indices=ix, values=vv)
+                model.forward(False)
+    run(0, args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.warmup, args.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"mode": "eval (EMA-BN) forward + cosine + loss", "launch": launch,
+            "ms_per_step": round(1e3 * el / args.steps, 4),
+            "value": round(BS * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s"}
+
+
 def main():
     args = parse()
     if args.model == "rnn":
@@ -282,7 +325,7 @@ def main():
         model.set_wire(*wires)
         model.set_adam_range(0, min(shard, ext))
 
-    cols = ZipfColumns(D)
+    cols = ZipfColumns(D, uniform=args.columns == "uniform")
     staged = []
     nnzs = []
     for b in range(args.batches):
@@ -419,6 +462,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = model.loss_accuracy()
+    fwd = fwd_only(model, staged, args, stream) if (args.fwd_only and world == 1 and rehearse == 1
+                                                   and feeder is None) else None
 
     probes = {}
     for name, pid in (probe_ids if args.probes else ()):
@@ -485,6 +530,10 @@ def main():
         "rooflines": rl,
         "final_loss": round(loss, 5), "final_accuracy": round(acc, 4),
     }
+    if args.columns != "zipf":
+        out["config"]["columns"] = args.columns
+    if fwd is not None:
+        out["fwd_only"] = fwd
     if rehearse > 1:
         out["rehearsal"] = {"world": rehearse, "collectives": "omitted",
                             "note": "rank 0's compute share of an N-rank bf16-wire step; not a headline number"}

@@ -11,8 +11,10 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OBJ = os.path.join(PKG, "_build")
-LIB = os.path.join(PKG, "libdssm.so")
+# DSSM_BUILD_TAG: a side build (A/B variants of DSSM_EXTRA_CFLAGS) in _build<tag>/, libdssm<tag>.so
+TAG = os.environ.get("DSSM_BUILD_TAG", "")
+OBJ = os.path.join(PKG, "_build" + TAG)
+LIB = os.path.join(PKG, f"libdssm{TAG}.so")
 SOURCES = ["spmm.hip", "gemm.hip", "bn.hip", "cosine.hip", "adam.hip", "dense.hip", "plan.hip", "feed.hip", "rnn.hip", "ops.hip"]
 HEADERS = ["common.h", "launch.h", "gather.h", "bnfuse.h", "dense.h", "flat.h"]
 ARCH = os.environ.get("DSSM_OFFLOAD_ARCH", "gfx950")

@@ -103,9 +103,9 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     const size_t o = (size_t)c * n + cc;
     float P[8], M[8], V[8], G[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (nvalid > 0 && !a.gout) {  // stream loads first: independent of the gather chain below
-      load8(a.p + o, nvalid, P);
-      load8(a.m + o, nvalid, M);
-      load8(a.v + o, nvalid, V);
+      ld_stream8(a.p + o, nvalid, P);
+      ld_stream8(a.m + o, nvalid, M);
+      ld_stream8(a.v + o, nvalid, V);
     }
     if (heavy) {
       if (nvalid > 0) {
@@ -138,13 +138,13 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (i < k) adam1(P[i], M[i], V[i], G[i] * a.gs, alpha, a.b1c, a.b2c, a.eps);
-      *reinterpret_cast<float4*>(a.p + o) = make_float4(P[0], P[1], P[2], P[3]);
-      *reinterpret_cast<float4*>(a.m + o) = make_float4(M[0], M[1], M[2], M[3]);
-      *reinterpret_cast<float4*>(a.v + o) = make_float4(V[0], V[1], V[2], V[3]);
+      st_stream4(a.p + o, make_float4(P[0], P[1], P[2], P[3]));
+      st_stream4(a.m + o, make_float4(M[0], M[1], M[2], M[3]));
+      st_stream4(a.v + o, make_float4(V[0], V[1], V[2], V[3]));
       if (k == 8) {
-        *reinterpret_cast<float4*>(a.p + o + 4) = make_float4(P[4], P[5], P[6], P[7]);
-        *reinterpret_cast<float4*>(a.m + o + 4) = make_float4(M[4], M[5], M[6], M[7]);
-        *reinterpret_cast<float4*>(a.v + o + 4) = make_float4(V[4], V[5], V[6], V[7]);
+        st_stream4(a.p + o + 4, make_float4(P[4], P[5], P[6], P[7]));
+        st_stream4(a.m + o + 4, make_float4(M[4], M[5], M[6], M[7]));
+        st_stream4(a.v + o + 4, make_float4(V[4], V[5], V[6], V[7]));
       }
       if (a.shadow && c < a.D) {
         u16* q = a.shadow + (size_t)c * a.ldsh + cc;
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
          j += (int64_t)a.dense_blocks * blockDim.x) {
       const int64_t i = j < na ? a.d4_begin + j : a.t4_begin + (j - na);
       const bool wired = i < a.wire4;
-      float4 pp = reinterpret_cast<float4*>(a.p)[i];
+      float4 pp = ld_stream4(a.p + i * 4);
       float4 gg;
       if (wired) {
         const uint2 q = reinterpret_cast<const uint2*>(a.gwire)[i];
@@ -345,15 +345,15 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       } else {
         gg = slab_grad4(a.slabs, i * 4, a.g);
       }
-      float4 mm = reinterpret_cast<float4*>(a.m)[i];
-      float4 vv = reinterpret_cast<float4*>(a.v)[i];
+      float4 mm = ld_stream4(a.m + i * 4);
+      float4 vv = ld_stream4(a.v + i * 4);
       adam1(pp.x, mm.x, vv.x, gg.x * a.gs, alpha, a.b1c, a.b2c, a.eps);
       adam1(pp.y, mm.y, vv.y, gg.y * a.gs, alpha, a.b1c, a.b2c, a.eps);
       adam1(pp.z, mm.z, vv.z, gg.z * a.gs, alpha, a.b1c, a.b2c, a.eps);
       adam1(pp.w, mm.w, vv.w, gg.w * a.gs, alpha, a.b1c, a.b2c, a.eps);
-      reinterpret_cast<float4*>(a.p)[i] = pp;
-      reinterpret_cast<float4*>(a.m)[i] = mm;
-      reinterpret_cast<float4*>(a.v)[i] = vv;
+      st_stream4(a.p + i * 4, pp);
+      st_stream4(a.m + i * 4, mm);
+      st_stream4(a.v + i * 4, vv);
       if (i * 4 >= a.clear_from)
         reinterpret_cast<float4*>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (wired) {

@@ -26,6 +26,46 @@ __device__ __forceinline__ float bcast_f(float v, int j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
+// ---- cache policy of the optimizer's once-per-step state streams (p, m, v) ------------------
+// Those 219 MB per step (C2) pass through the XCD L2s between the gathers of dZ1 rows (3.7 MB,
+// re-read by every XCD) that share the launch.  DSSM_STREAM_POLICY (build-time A/B):
+//   bit 0: nt loads;  bit 1: nt stores;  bit 2: sc1 (write-through) stores, which drop the line
+//   from the XCD's L2 (MI355X_MICROARCH.md, store flavours).
+#ifndef DSSM_STREAM_POLICY
+#define DSSM_STREAM_POLICY 0
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_stream4(const float* p) {
+#if DSSM_STREAM_POLICY & 1
+  const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ void st_stream4(float* p, float4 x) {
+#if DSSM_STREAM_POLICY & 4
+  const f32x4v v = {x.x, x.y, x.z, x.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#elif DSSM_STREAM_POLICY & 2
+  const f32x4v v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = x;
+#endif
+}
+// the lane's 8-column group of a stream (nvalid in {4, 8})
+__device__ __forceinline__ void ld_stream8(const float* p, int nvalid, float (&x)[8]) {
+  const float4 a = ld_stream4(p);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  if (nvalid > 4) {
+    const float4 b = ld_stream4(p + 4);
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+    x[4] = x[5] = x[6] = x[7] = 0.f;
+  }
+}
+
 // ---- 8-column vector loads/stores (lane owns 8 consecutive columns) ------------------------
 // nvalid in {4, 8}: widths are multiples of 4, so a lane's group is either full or half.
 __device__ __forceinline__ void load8(const float* p, int nvalid, float (&x)[8]) {

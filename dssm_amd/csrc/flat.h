@@ -38,16 +38,16 @@ __device__ __forceinline__ void flat_untouched(const FlatSlice& f, int bi) {
        i += (int64_t)f.nblocks * blockDim.x) {
     const int c = (int)((i * 4) / f.n);
     if (f.col_ptr[c + 1] != f.col_ptr[c]) continue;
-    float4 pp = reinterpret_cast<float4*>(f.p)[i];
-    float4 mm = reinterpret_cast<float4*>(f.m)[i];
-    float4 vv = reinterpret_cast<float4*>(f.v)[i];
+    float4 pp = ld_stream4(f.p + i * 4);
+    float4 mm = ld_stream4(f.m + i * 4);
+    float4 vv = ld_stream4(f.v + i * 4);
     adam1(pp.x, mm.x, vv.x, 0.f, alpha, f.b1c, f.b2c, f.eps);
     adam1(pp.y, mm.y, vv.y, 0.f, alpha, f.b1c, f.b2c, f.eps);
     adam1(pp.z, mm.z, vv.z, 0.f, alpha, f.b1c, f.b2c, f.eps);
     adam1(pp.w, mm.w, vv.w, 0.f, alpha, f.b1c, f.b2c, f.eps);
-    reinterpret_cast<float4*>(f.p)[i] = pp;
-    reinterpret_cast<float4*>(f.m)[i] = mm;
-    reinterpret_cast<float4*>(f.v)[i] = vv;
+    st_stream4(f.p + i * 4, pp);
+    st_stream4(f.m + i * 4, mm);
+    st_stream4(f.v + i * 4, vv);
     if (f.shadow && c < f.D) {
       uint2 q;
       q.x = pack2bf(pp.x, pp.y);
