@@ -245,28 +245,30 @@ def fwd_only(model, staged, args, stream):
     """Forward alone, eval mode (on_train=False: EMA-BN, cosine, softmax, loss; new_dssm.py:85-86,
     274-285) over the staged batches, after the training measurement (the step's own forward is
     not separable in time: the training forward also builds the CSC transpose for the backward).
-    One graph per staged batch where capture works, else eager launches."""
+    As the training measurement: the staged batches' forwards captured back to back into ONE graph
+    replayed per full cycle (eager launches for a partial cycle, or where capture fails)."""
     import torch
-    graphs = []
+    cycle = torch.cuda.CUDAGraph()
     try:
-        for ip, ix, vv in staged:
-            model.set_batch(indptr=ip, indices=ix, values=vv)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=stream):
-                model.forward(False)
-            graphs.append(g)
-        launch = "hipgraph"
-    except Exception:  # capture unsupported: eager launches
-        graphs, launch = [], "eager"
-
-    def run(i0, n):
-        for i in range(i0, i0 + n):
-            if graphs:
-                graphs[i % len(graphs)].replay()
-            else:
-                ip, ix, vv = staged[i % len(staged)]
+        with torch.cuda.graph(cycle, stream=stream):
+            for ip, ix, vv in staged:
                 model.set_batch(indptr=ip, indices=ix, values=vv)
                 model.forward(False)
+        launch = "hipgraph"
+    except Exception:  # capture unsupported: eager launches
+        cycle, launch = None, "eager"
+
+    def run(i0, n):
+        i = i0
+        while i < i0 + n:
+            if cycle is not None and i % len(staged) == 0 and i + len(staged) <= i0 + n:
+                cycle.replay()
+                i += len(staged)
+                continue
+            ip, ix, vv = staged[i % len(staged)]
+            model.set_batch(indptr=ip, indices=ix, values=vv)
+            model.forward(False)
+            i += 1
     run(0, args.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -12,11 +12,27 @@ struct BnSide;  // bnfuse.h
 // split=true: cross-block finalize steps run as their own small launch instead of inside the
 // producing kernel behind an agent-scope release/acquire ticket.
 
+// Eval-mode (on_train=False) BN coefficients of every layer from the EMA shadows
+// (new_dssm.py:85-86): they depend on the parameters only, not on the batch, so the forward
+// computes all of them up front, in extra workgroups of the SpMM launch.
+struct EvalCoef {
+  int L;
+  int n[8], ld[8];
+  const float* gamma[8][2];
+  const float* beta[8][2];
+  const float* ema_mean[8][2];
+  const float* ema_var[8][2];
+  float* coef[8];  // [4][2][ld]: mean, rstd, inv, shift (as k_bn_stats writes them)
+  float eps;
+};
+int eval_coef_blocks(const EvalCoef& e);
+
 // ---- sparse (spmm.hip) ----
-// FC1 forward: Z = X*W + b, one wave per CSR row, lane owns 8 output columns.
+// FC1 forward: Z = X*W + b, one wave per CSR row, lane owns 8 output columns; with ec, its
+// eval_coef_blocks(*ec) extra workgroups write the eval BN coefficients.
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s);
+                           int ldz, hipStream_t s, const EvalCoef* ec = nullptr);
 // CSR -> CSC transpose of X with a virtual all-ones column D appended (its dW row = db1).
 // scratch: csc_scratch_ints() ints, zero on first use (kept zero between calls);
 // col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.

@@ -776,9 +776,28 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                         P->at<float>(Lt.Z[0]), Lt.ldp[0], P->at<double>(Lt.fsum[0]),
                                         Lt.BS, P->fsum0_copies, s));
   } else {
+    // eval: every layer's BN coefficients from the EMA, in the SpMM launch's extra workgroups
+    dssm::EvalCoef ec{};
+    if (!train) {
+      static_assert(DSSM_MAX_LAYERS <= 8, "EvalCoef holds 8 layers");
+      ec.L = Lt.L;
+      ec.eps = c.bn_eps;
+      for (int l = 0; l < Lt.L; ++l) {
+        const float* ema = P->ema + Lt.ema_off[l];
+        ec.n[l] = Lt.n[l];
+        ec.ld[l] = Lt.ldp[l];
+        ec.coef[l] = P->at<float>(Lt.coef[l]);
+        for (int t = 0; t < 2; ++t) {
+          ec.gamma[l][t] = P->p + Lt.bn_off[l][2 * t];
+          ec.beta[l][t] = P->p + Lt.bn_off[l][2 * t + 1];
+          ec.ema_mean[l][t] = ema + 2 * t * Lt.n[l];
+          ec.ema_var[l][t] = ema + (2 * t + 1) * Lt.n[l];
+        }
+      }
+    }
     HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
                                 P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
-                                Lt.ldp[0], s));
+                                Lt.ldp[0], s, train ? nullptr : &ec));
   }
   P->probe_end(DSSM_PROBE_SPMM_FWD, s);
   if (P->dense_on) {  // BN1 .. cosine + loss (+ dy_L and its BN partials) in one launch
@@ -833,6 +852,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   for (int l = 0; l < Lt.L; ++l) {
     float* ema = P->ema + Lt.ema_off[l];
     const int n = Lt.n[l];
+    if (train || P->dense_on)  // eval coefficients: written by the SpMM launch above
     HIP_TRY(dssm::launch_bn_fwd_stats(
         P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
         P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,

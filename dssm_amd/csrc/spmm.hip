@@ -59,14 +59,48 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
   }
 }
 
+// Eval BN coefficients, item i of all layers' (column, tower) pairs: the arithmetic of
+// k_bn_stats' eval finalize (rstd = 1 / sqrt(var + eps), inv = rstd * gamma, shift = beta - mu * inv;
+// pad columns zero).
+__device__ __forceinline__ void eval_coef_item(const EvalCoef& e, int i) {
+  for (int l = 0; l < e.L; ++l) {
+    const int items = 2 * e.ld[l];
+    if (i >= items) {
+      i -= items;
+      continue;
+    }
+    const int t = i / e.ld[l], c = i - t * e.ld[l];
+    const size_t plane = (size_t)2 * e.ld[l], o = (size_t)t * e.ld[l] + c;
+    float* coef = e.coef[l];
+    if (c >= e.n[l]) {
+      coef[o] = 0.f; coef[plane + o] = 0.f; coef[2 * plane + o] = 0.f; coef[3 * plane + o] = 0.f;
+    } else {
+      const float mu = e.ema_mean[l][t][c], var = e.ema_var[l][t][c];
+      const float rstd = 1.0f / sqrtf(var + e.eps);
+      const float inv = rstd * e.gamma[l][t][c];
+      coef[o] = mu;
+      coef[plane + o] = rstd;
+      coef[2 * plane + o] = inv;
+      coef[3 * plane + o] = e.beta[l][t][c] - mu * inv;
+    }
+    return;
+  }
+}
+
+// blocks [0, ne): eval coefficients (first in dispatch order); the rest: one wave per CSR row
 template <typename TW>
 __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices,
                                                   const float* __restrict__ values, int rows,
                                                   const TW* __restrict__ W, int ldw, int n,
                                                   const float* __restrict__ bias,
-                                                  float* __restrict__ Z, int ldz) {
-  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, blockIdx.x);
+                                                  float* __restrict__ Z, int ldz, EvalCoef ec,
+                                                  int ne) {
+  if ((int)blockIdx.x < ne) {
+    eval_coef_item(ec, (int)blockIdx.x * 256 + threadIdx.x);
+    return;
+  }
+  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne);
 }
 
 // FC1 forward + BN1 statistics (fused-statistics schedule, bnfuse.h): 16 rows per 1024-thread
@@ -757,16 +791,25 @@ __global__ __launch_bounds__(1024) void k_dw1_heavy_items(const int* __restrict_
 
 }  // namespace
 
+int eval_coef_blocks(const EvalCoef& e) {
+  int items = 0;
+  for (int l = 0; l < e.L; ++l) items += 2 * e.ld[l];
+  return cdiv(items, 256);
+}
+
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s) {
-  dim3 grid(cdiv(rows, 4)), block(256);
+                           int ldz, hipStream_t s, const EvalCoef* ec) {
+  EvalCoef e{};
+  const int ne = ec ? eval_coef_blocks(*ec) : 0;
+  if (ec) e = *ec;
+  dim3 grid(ne + cdiv(rows, 4)), block(256);
   if (w_bf16)
     hipLaunchKernelGGL(k_spmm_fwd<u16>, grid, block, 0, s, indptr, indices, values, rows,
-                       (const u16*)W, ldw, n, bias, Z, ldz);
+                       (const u16*)W, ldw, n, bias, Z, ldz, e, ne);
   else
     hipLaunchKernelGGL(k_spmm_fwd<float>, grid, block, 0, s, indptr, indices, values, rows,
-                       (const float*)W, ldw, n, bias, Z, ldz);
+                       (const float*)W, ldw, n, bias, Z, ldz, e, ne);
   return hipGetLastError();
 }
 
