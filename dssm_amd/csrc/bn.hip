@@ -21,6 +21,7 @@
 #include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
+#include "tn.h"
 
 namespace dssm {
 namespace {
@@ -429,33 +430,52 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
 // from the layer's fp64 sums into LDS along with the forward coefficients; workgroup 0 also
 // writes dbeta / dgamma.  Same arithmetic per element as k_bn_bwd_apply.
 constexpr int kApplyMaxLd = 512;
+// LDS of the launch: the coefficient cache of the element blocks, or the double-buffered operand
+// tiles of the dW blocks (tn.h)
+static_assert(kTnTile * 2 >= 128 * kTnLd, "a 128-row sub-chunk per operand");
+constexpr int kApplySmemFloats = 2 * 6 * kApplyMaxLd > kTnTile * 2 ? 2 * 6 * kApplyMaxLd : kTnTile * 2;
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
                                                          u16* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
                                                          int loss_blocks,
                                                          float* __restrict__ loss_out,
-                                                         FlatSlice flat, int nwork) {
+                                                         FlatSlice flat, int nwork, TnParams dw,
+                                                         int dw_x, int dw_y, int dw_blocks) {
+  __shared__ __attribute__((aligned(16))) float smem[kApplySmemFloats];
+  // blocks [0, dw_blocks): the previous backward pair's dW split-K tiles (the longest chains,
+  // first in dispatch order); they read dZ of the layer above and the forward's activations, so
+  // they are independent of this launch's own work
+  if ((int)blockIdx.x < dw_blocks) {
+#ifdef DSSM_DW_SKIP  // timing diagnostics only (wrong dW): the launch without the dW tiles' work
+    return;
+#endif
+    const int r = blockIdx.x;
+    u16* sA = reinterpret_cast<u16*>(smem);
+    tn_chunk_body<3>(dw, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y), sA, sA + 2 * kTnTile);
+    return;
+  }
+  const int bid = (int)blockIdx.x - dw_blocks;
   // one extra block past the element blocks: the step's loss / accuracy from the cosine kernel's
   // partials (deferred finalize: no cross-workgroup ticket in the cosine launch) and dgamma /
   // dbeta, off the element blocks' critical path
-  if ((int)blockIdx.x >= nwork) {
-    if ((int)blockIdx.x == nwork) {
+  if (bid >= nwork) {
+    if (bid == nwork) {
       if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
       fs_materialize_bwd(b);
     } else {
-      flat_untouched(flat, (int)blockIdx.x - nwork - 1);  // untouched W1 rows (flat.h)
+      flat_untouched(flat, bid - nwork - 1);  // untouched W1 rows (flat.h)
     }
     return;
   }
-  __shared__ __attribute__((aligned(16))) float sc[2][6][kApplyMaxLd];  // mu rstd inv shift m1 m2
+  float (*sc)[6][kApplyMaxLd] = reinterpret_cast<float (*)[6][kApplyMaxLd]>(smem);  // mu rstd inv shift m1 m2
   const int ld = b.ld;
   const size_t plane = (size_t)2 * ld;
   const int q = ld >> 2;
   const int rows = b.rows_q + b.rows_d;
   const size_t total = (size_t)rows * q;
   // the first grid-stride element's loads go out before the coefficient prologue
-  const size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t i0 = (size_t)bid * 256 + threadIdx.x;
   float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), da0 = z0;
   if (i0 < total) {
     const int r = (int)(i0 / q);
@@ -606,16 +626,24 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part, int loss_blocks,
                                      float* loss_out,
-                                     const FlatSlice* flat) {
+                                     const FlatSlice* flat, const TnParams* dw) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
   static const int gmax = [] {
     const char* e = std::getenv("DSSM_APPLY_GRID");
     return e ? std::max(1, std::atoi(e)) : 1024;
   }();
-  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), gmax);
+  static const int gmax_dw = [] {  // element blocks beside hosted dW tiles
+    const char* e = std::getenv("DSSM_APPLY_GRID_DW");
+    return e ? std::max(1, std::atoi(e)) : 512;
+  }();
+  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? gmax_dw : gmax);
   const FlatSlice fl = flat ? *flat : FlatSlice{};
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(grid + 1 + fl.nblocks), dim3(256), 0, s, Z, dA, b, (u16*)dZ,
-                     loss_part, loss_blocks, loss_out, fl, grid);
+  if (dw && dw->k_per_split > 3 * 128) return hipErrorInvalidValue;  // tn_chunk_body<3>
+  const TnParams p = dw ? *dw : TnParams{};
+  const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
+  const int dw_blocks = dw ? dw_x * dw_y * cdiv(p.K, p.k_per_split) : 0;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1 + fl.nblocks), dim3(256), 0, s, Z, dA,
+                     b, (u16*)dZ, loss_part, loss_blocks, loss_out, fl, grid, p, dw_x, dw_y, dw_blocks);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 #include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
+#include "tn.h"
 
 namespace dssm {
 namespace {
@@ -783,134 +784,6 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx
 #endif
 }
 
-// "TN" (dW): C[M x N] (+ split slab) = A^T . B over K batch rows, A [K x lda] (m contiguous),
-// B [K x ldb] (n contiguous), both bf16.  Both tiles are staged exactly as they lie in memory
-// ([k][m], [k][n]: 16-B loads and 16-B LDS writes) and the MFMA fragments, which need 8
-// consecutive k per lane, come from ds_read_b64_tr_b16 (4 k x 16 columns per 16-lane group,
-// delivered column-major).  ones_row: virtual all-ones A column at m == M-1 (-> bias grad).
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4s lds_v4s;
-
-__device__ __forceinline__ bf16x8 tr_frag(const u16* tile, int row0, int col0, int lane) {
-  // lanes 16g+4q+p read rows (row0 + 8g + q [+4]) at columns col0 + 4p..4p+3
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const u16* a0 = tile + (row0 + 8 * g + q) * NLD + col0 + 4 * p;
-  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
-  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0 + 4 * NLD));
-  typedef short v8s __attribute__((ext_vector_type(8)));
-  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-struct TnParams {
-  int M, N, K;
-  const u16* A;
-  int lda;
-  const u16* B;
-  int ldb;
-  float* C;
-  int ldc, ones_row, k_per_split;
-};
-
-__device__ __forceinline__ void tn_body(const TnParams& p, int tx, int ty, int tz, u16* sA, u16* sB) {
-  const int M = p.M, N = p.N, lda = p.lda, ldb = p.ldb;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int bm = ty * 64, bn = tx * 64;
-  const int kbeg = tz * p.k_per_split;
-  const int kend = min(p.K, kbeg + p.k_per_split);
-  const int Mload = p.ones_row ? M - 1 : M;
-  int sk[2], sc[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int e = t + 256 * g;
-    sk[g] = e >> 3;
-    sc[g] = (e & 7) * 8;
-  }
-  uint4 ra[2], rb[2];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int gk = k0 + sk[g], gm = bm + sc[g], gn = bn + sc[g];
-      uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = make_uint4(0u, 0u, 0u, 0u);
-      if (gk < kend) {
-        if (gm + 8 <= Mload) {
-          va = *reinterpret_cast<const uint4*>(p.A + (size_t)gk * lda + gm);
-        } else {
-          u16 x[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            x[i] = (gm + i < Mload) ? p.A[(size_t)gk * lda + gm + i]
-                                    : ((p.ones_row && gm + i == Mload) ? (u16)0x3f80 : (u16)0);
-          va.x = x[0] | ((unsigned)x[1] << 16); va.y = x[2] | ((unsigned)x[3] << 16);
-          va.z = x[4] | ((unsigned)x[5] << 16); va.w = x[6] | ((unsigned)x[7] << 16);
-        }
-        if (gn + 8 <= N) {
-          vb = *reinterpret_cast<const uint4*>(p.B + (size_t)gk * ldb + gn);
-        } else {
-          u16 x[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) x[i] = (gn + i < N) ? p.B[(size_t)gk * ldb + gn + i] : (u16)0;
-          vb.x = x[0] | ((unsigned)x[1] << 16); vb.y = x[2] | ((unsigned)x[3] << 16);
-          vb.z = x[4] | ((unsigned)x[5] << 16); vb.w = x[6] | ((unsigned)x[7] << 16);
-        }
-      }
-      ra[g] = va;
-      rb[g] = vb;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      *reinterpret_cast<uint4*>(&sA[buf * kTileElems + sk[g] * NLD + sc[g]]) = ra[g];
-      *reinterpret_cast<uint4*>(&sB[buf * kTileElems + sk[g] * NLD + sc[g]]) = rb[g];
-    }
-  };
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (kbeg < kend) {
-    load(kbeg);
-    store(0);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += NBK, buf ^= 1) {
-    const bool more = k0 + NBK < kend;
-    if (more) load(k0 + NBK);
-#pragma unroll
-    for (int ks = 0; ks < NBK; ks += 32) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = tr_frag(sA + buf * kTileElems, ks, wm * 32 + i * 16, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(sB + buf * kTileElems, ks, wn * 32 + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) store(buf ^ 1);
-    __syncthreads();
-  }
-  float* out = p.C + (size_t)tz * M * p.ldc;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = bn + wn * 32 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) out[(size_t)m * p.ldc + n] = acc[i][j][r];
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void k_gemm_tn(TnParams p) {
   __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];  // [k][m]
   __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];  // [k][n]
@@ -1209,7 +1082,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
                            int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits, unsigned long long* timing) {
+                           int* deferred_splits, unsigned long long* timing, TnParams* dw_out) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
@@ -1235,6 +1108,15 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
     const int Mw = kin + 1;
     const int nsplit = cdiv(M, kTwKc);
     const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
+    if (dw_out && defer) {
+      // dA tiles alone (one round at one workgroup per CU); dW_l's tiles ride in the next
+      // BN-backward apply launch (bn.hip), same splits and slabs
+      *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
+      hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi), s,
+                         a, f, nt_x, nt_blocks, *dw_out, 1, 1);
+      *deferred_splits = nsplit > 1 ? nsplit : 0;
+      return hipGetLastError();
+    }
     const int tn_x = cdiv(n, 64), tn_y = cdiv(Mw, 128);
     const int tn_blocks = tn_x * tn_y * nsplit;
     const size_t smem = std::max(wk_smem_bytes(Kp, f.lds_epi), tw_smem_bytes());

@@ -7,7 +7,8 @@
 
 namespace dssm {
 
-struct BnSide;  // bnfuse.h
+struct BnSide;    // bnfuse.h
+struct TnParams;  // tn.h
 
 // split=true: cross-block finalize steps run as their own small launch instead of inside the
 // producing kernel behind an agent-scope release/acquire ticket.
@@ -111,7 +112,10 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
                            int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits, unsigned long long* timing = nullptr);
+                           int* deferred_splits, unsigned long long* timing = nullptr,
+                           TnParams* dw_out = nullptr);
+// dw_out (whole-K path with defer): the launch runs the dA tiles only and hands dW_l's split-K
+// tiles (64 x 64, 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch.
 
 // ---- batch norm (bn.hip) ----
 struct BnTowers {
@@ -137,7 +141,7 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part = nullptr,
                                      int loss_blocks = 0, float* loss_out = nullptr,
-    const FlatSlice* flat = nullptr);
+    const FlatSlice* flat = nullptr, const TnParams* dw = nullptr);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);

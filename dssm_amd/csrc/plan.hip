@@ -15,6 +15,7 @@
 #include "bnfuse.h"
 #include "dense.h"
 #include "launch.h"
+#include "tn.h"
 
 namespace {
 
@@ -261,6 +262,7 @@ struct dssm_plan {
   // accumulator replicas) instead of the separate statistics launch; DSSM_SPMM_STATS=1.
   // Measured slower on MI355X at C2 (the 16-row workgroups cost more than the launch saves).
   bool spmm_stats = false;
+  bool dw_in_apply = true;  // DSSM_DW_IN_APPLY=0: dW_l tiles in the backward pair launch
   bool nt_timing = false;  // DSSM_NT_TIMING=1: layer-2 NT GEMM phase stamps (BUF_DENSE_TIMING row 3)
   int fsum0_copies = 1;  // DSSM_FSUM_COPIES (<= kFsum0Copies)
   hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
@@ -587,6 +589,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
     }
   }
   if (const char* e = std::getenv("DSSM_WIRE_GRAD_PASS")) P->wire_grad_pass = e[0] != '0';
+  if (const char* e = std::getenv("DSSM_DW_IN_APPLY")) P->dw_in_apply = e[0] != '0';
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
     P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
@@ -959,6 +962,10 @@ static int backward_impl(dssm_plan* P, void* stream) {
   if (P->fwd_fused) {
     // BN_L apply from the cosine kernel's sums, then per layer one launch for dA_{l-1} (with
     // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply
+    // dw_in_apply: the pair launches run their dA tiles only (one round) and each dW_l's tiles
+    // ride in the following apply launch (BN_{l-1}'s), whose element blocks leave CUs idle
+    dssm::TnParams dw{};
+    bool dw_pending = false;
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
@@ -967,16 +974,21 @@ static int backward_impl(dssm_plan* P, void* stream) {
                                               P->at<uint16_t>(Lt.dZ[l]), s,
                                               fin ? P->at<float>(Lt.loss_j) : nullptr,
                                               dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss),
-                                              (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr));
+                                              (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr,
+                                              dw_pending ? &dw : nullptr));
+      dw_pending = false;
       if (fin) P->loss_pending = false;
       if (l == 0) break;
+      const bool host_dw = P->dw_in_apply && P->fused_w1_adam;
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
           P->bcopies(l - 1), Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
           P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l],
-          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 128 : nullptr));
+          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 128 : nullptr,
+          host_dw ? &dw : nullptr));
+      dw_pending = host_dw && dw.C != nullptr;
     }
     return dw1_backward(P, s);
   }
