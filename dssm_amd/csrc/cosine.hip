@@ -13,6 +13,7 @@
 #include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
+#include "csc.h"
 
 namespace dssm {
 namespace {
@@ -38,7 +39,8 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp, FlatSlice flat) {
+    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp, FlatSlice flat,
+    CscScatter scat) {
   unsigned long long* tm = (tmp && threadIdx.x == 0 && blockIdx.x == 1) ? tmp : nullptr;
   int ti = 0;
   auto stamp = [&]() {
@@ -75,8 +77,10 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   }
   if constexpr (FSC) {
     if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
-      if ((int)blockIdx.x == nrow_blocks) fs_materialize_fwd(fs);
-      else flat_untouched(flat, (int)blockIdx.x - nrow_blocks - 1);  // untouched W1 rows (flat.h)
+      const int xb = (int)blockIdx.x - nrow_blocks - 1;
+      if (xb < 0) fs_materialize_fwd(fs);
+      else if (xb < flat.nblocks) flat_untouched(flat, xb);  // untouched W1 rows (flat.h)
+      else csc_scatter_role(scat, xb - flat.nblocks);     // the CSC transpose's scatter (csc.h)
       return;
     }
     fs_coef_stage<(2 * kCosMaxN) / 256>(fs, threadIdx.x, 256,
@@ -288,19 +292,22 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               bool split, hipStream_t s, const BnSide* fused, bool defer_finalize,
                               unsigned long long* timing,
-                              const FlatSlice* flat) {
+                              const FlatSlice* flat, const CscScatter* scatter) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int blocks = cdiv(bs, 4);
   unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * blocks + 32);
   const FlatSlice fl = (flat && fused) ? *flat : FlatSlice{};
-  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks), block(256);  // fused: + materialising, flat blocks
+  const CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
+  if (scatter && !fused) return hipErrorInvalidValue;  // the role rides on the fused kernel only
+  // fused: + materialising, flat and scatter blocks
+  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks + sc.nblocks), block(256);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \
   hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
                      y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,               \
-                     (split || defer_finalize) ? 1 : 0, fs, timing, fl)
+                     (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \

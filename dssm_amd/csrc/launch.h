@@ -9,6 +9,7 @@ namespace dssm {
 
 struct BnSide;    // bnfuse.h
 struct TnParams;  // tn.h
+struct CscScatter;  // csc.h
 
 // split=true: cross-block finalize steps run as their own small launch instead of inside the
 // producing kernel behind an agent-scope release/acquire ticket.
@@ -58,7 +59,10 @@ hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* 
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
-                               float* csc_val, int* csc_col, hipStream_t s);
+                               float* csc_val, int* csc_col, hipStream_t s,
+                               CscScatter* scatter_out = nullptr);
+// scatter_out: the launch runs the BN1 sums alone and hands the scatter to *scatter_out (a role of
+// a later launch: launch_cosine_loss).
 // FC1 forward (bf16 W1 shadow, ldz <= 512) + BN1 per-tower column sums into fsum (bnfuse.h).
 hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
                                  int rows, const uint16_t* W, int ldw, int n, const float* bias,
@@ -162,7 +166,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               bool split, hipStream_t s, const BnSide* fused = nullptr,
                               bool defer_finalize = false, unsigned long long* timing = nullptr,
-    const FlatSlice* flat = nullptr);
+    const FlatSlice* flat = nullptr, const CscScatter* scatter = nullptr);
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 inline int cosine_blocks(int bs) { return (bs + 3) / 4; }
 hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s);

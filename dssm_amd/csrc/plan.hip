@@ -16,6 +16,7 @@
 #include "dense.h"
 #include "launch.h"
 #include "tn.h"
+#include "csc.h"
 
 namespace {
 
@@ -262,6 +263,7 @@ struct dssm_plan {
   // accumulator replicas) instead of the separate statistics launch; DSSM_SPMM_STATS=1.
   // Measured slower on MI355X at C2 (the 16-row workgroups cost more than the launch saves).
   bool spmm_stats = false;
+  bool scatter_in_cos = true;  // DSSM_SCATTER_IN_COS=0: the CSC scatter beside the BN1 sums
   bool dw_in_apply = true;  // DSSM_DW_IN_APPLY=0: dW_l tiles in the backward pair launch
   bool nt_timing = false;  // DSSM_NT_TIMING=1: layer-2 NT GEMM phase stamps (BUF_DENSE_TIMING row 3)
   int fsum0_copies = 1;  // DSSM_FSUM_COPIES (<= kFsum0Copies)
@@ -589,6 +591,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
     }
   }
   if (const char* e = std::getenv("DSSM_WIRE_GRAD_PASS")) P->wire_grad_pass = e[0] != '0';
+  if (const char* e = std::getenv("DSSM_SCATTER_IN_COS")) P->scatter_in_cos = e[0] != '0';
   if (const char* e = std::getenv("DSSM_DW_IN_APPLY")) P->dw_in_apply = e[0] != '0';
   if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
   if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
@@ -814,12 +817,16 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     // BN1 sums by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
     // stages the previous layer's BN+ReLU and accumulates its own output's sums, the cosine
     // kernel the last layer's backward sums (bnfuse.h)
+    // scatter_in_cos: the transpose's scatter rides in the cosine launch instead (csc.h)
+    dssm::CscScatter scat{};
+    const bool scat_cos = P->merged_csc() && P->scatter_in_cos;
     if (P->merged_csc())  // BN1 sums beside the transpose's scatter
       HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
                                         P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
-                                        P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s));
+                                        P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s,
+                                        scat_cos ? &scat : nullptr));
     else if (!P->spmm_stats)
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s));
@@ -844,7 +851,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
         P->split_finalize, s, &last, /*defer_finalize=*/true,
         P->nt_timing ? P->at<unsigned long long>(Lt.dense_timing) : nullptr,
-        (flat_on && fs1.nblocks) ? &fs1 : nullptr));
+        (flat_on && fs1.nblocks) ? &fs1 : nullptr, scat_cos ? &scat : nullptr));
     P->flat_this_step = flat_on;
     P->fwd_train_done = true;
     P->fwd_fused = true;

@@ -24,6 +24,7 @@
 #include "common.h"
 #include "gather.h"
 #include "launch.h"
+#include "csc.h"
 
 namespace dssm {
 namespace {
@@ -855,13 +856,21 @@ hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* 
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
-                               float* csc_val, int* csc_col, hipStream_t s) {
+                               float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out) {
   (void)max_nnz;
   if (row_split % kSumsRows) return hipErrorInvalidValue;
   int* cnt = scratch;
   int* pos_tmp = scratch + 2 * (D + 1 + 64);
   const int nsum_x = cdiv(ldz, 64), nsum = nsum_x * cdiv(rows, kSumsRows);
-  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + cdiv(rows, 4)), dim3(256), 0, s, Z, ldz, n, row_split,
+  if (scatter_out) {
+    static const int nb = [] {
+      const char* e = std::getenv("DSSM_SCATTER_BLOCKS");
+      return e ? std::max(1, std::atoi(e)) : 384;
+    }();
+    *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
+                              csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
+  }
+  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n, row_split,
                      fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                      csc_row, csc_val, csc_col);
   return hipGetLastError();
