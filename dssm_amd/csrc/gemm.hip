@@ -1078,6 +1078,12 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   return hipGetLastError();
 }
 
+hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float* dst, hipStream_t s) {
+  const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
+  hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), dim3(256), 0, s, slab, splits, n, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
@@ -1108,13 +1114,14 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
     const int Mw = kin + 1;
     const int nsplit = cdiv(M, kTwKc);
     const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
-    if (dw_out && defer) {
+    if (dw_out) {
       // dA tiles alone (one round at one workgroup per CU); dW_l's tiles ride in the next
-      // BN-backward apply launch (bn.hip), same splits and slabs
+      // BN-backward apply launch (bn.hip), same splits and slabs.  Without defer the caller sums
+      // the slabs (launch_splitk_reduce) after that launch.
       *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
       hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi), s,
                          a, f, nt_x, nt_blocks, *dw_out, 1, 1);
-      *deferred_splits = nsplit > 1 ? nsplit : 0;
+      *deferred_splits = (defer && nsplit > 1) ? nsplit : 0;
       return hipGetLastError();
     }
     const int tn_x = cdiv(n, 64), tn_y = cdiv(Mw, 128);

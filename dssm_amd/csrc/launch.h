@@ -118,8 +118,10 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
                            int* deferred_splits, unsigned long long* timing = nullptr,
                            TnParams* dw_out = nullptr);
-// dw_out (whole-K path with defer): the launch runs the dA tiles only and hands dW_l's split-K
-// tiles (64 x 64, 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch.
+// dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
+// 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
+// caller then sums the slabs into gw with launch_splitk_reduce.
+hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float* dst, hipStream_t s);
 
 // ---- batch norm (bn.hip) ----
 struct BnTowers {

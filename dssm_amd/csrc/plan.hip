@@ -973,6 +973,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
     // ride in the following apply launch (BN_{l-1}'s), whose element blocks leave CUs idle
     dssm::TnParams dw{};
     bool dw_pending = false;
+    float* dw_reduce_to = nullptr;
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
@@ -983,10 +984,16 @@ static int backward_impl(dssm_plan* P, void* stream) {
                                               dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss),
                                               (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr,
                                               dw_pending ? &dw : nullptr));
+      if (dw_pending && dw_reduce_to) {  // not deferred to Adam: the slabs summed right after
+        const int nsplit = (dw.K + dw.k_per_split - 1) / dw.k_per_split;
+        HIP_TRY(dssm::launch_splitk_reduce(dw.C, nsplit, (int64_t)dw.M * dw.N, dw_reduce_to, s));
+      }
       dw_pending = false;
+      dw_reduce_to = nullptr;
       if (fin) P->loss_pending = false;
       if (l == 0) break;
-      const bool host_dw = P->dw_in_apply && P->fused_w1_adam;
+      const bool host_dw = P->dw_in_apply;
+      dw = dssm::TnParams{};  // filled by the pair launch when it hands its dW tiles over
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
@@ -996,6 +1003,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
           (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 128 : nullptr,
           host_dw ? &dw : nullptr));
       dw_pending = host_dw && dw.C != nullptr;
+      if (dw_pending && !P->fused_w1_adam && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
     }
     return dw1_backward(P, s);
   }
