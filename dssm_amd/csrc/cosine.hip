@@ -10,6 +10,8 @@
 // gradient of every embedding row it owns (each doc row belongs to exactly one query: no
 // atomics).  The per-block loss/accuracy partials are summed by the last block to finish
 // (agent-scope ticket), in fixed order.
+#include <algorithm>
+
 #include "bnfuse.h"
 #include "common.h"
 #include "launch.h"
@@ -33,8 +35,11 @@ __device__ __forceinline__ void loss_finalize(const float* part, int nblk, int b
 // moments and the EMA update) and the workgroup adds its rows' backward sums (sum dy,
 // sum dy*xhat per tower, ReLU mask applied) to fs.bsum.
 constexpr int kCosMaxN = 512;
-template <int EPL, int KM, bool FSC>
-__global__ __launch_bounds__(256) void k_cosine_loss(
+// NW: waves (queries) per workgroup.  The fused kernel uses 16: each workgroup adds its backward
+// sums with one fp64 atomic per (statistic, column), and the 64-deep same-address chains (instead
+// of 256-deep at 4 waves) no longer trail the launch.
+template <int EPL, int KM, bool FSC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
@@ -48,16 +53,17 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     ++ti;
   };
   stamp();
-  __shared__ float s_part[2][4];
+  constexpr int NT = 64 * NW;
+  __shared__ float s_part[2][NW];
   __shared__ int s_flag;
   __shared__ float s_co[FSC ? 2 * 4 * kCosMaxN : 1];     // [tower][mu|rstd|inv|shift][c]
-  __shared__ float s_bs[FSC ? 4 * 4 * EPL * 64 : 1];     // [wave][sq1|sq2|sd1|sd2][c]
+  __shared__ float s_bs[FSC ? NW * 4 * EPL * 64 : 1];    // [wave][sq1|sq2|sd1|sd2][c]
   (void)s_flag;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int j = blockIdx.x * 4 + wv;
+  const int j = blockIdx.x * NW + wv;
   const int K = neg + 1;
   const size_t plane = (size_t)2 * ld;
-  const int nrow_blocks = (bs + 3) / 4;
+  const int nrow_blocks = (bs + NW - 1) / NW;
   // ---- the rows' raw loads go out first, ahead of the coefficient prologue (they need no
   // coefficient): query row + K doc rows
   float q[EPL], d[KM][EPL], zq[EPL], zd[FSC ? KM : 1][EPL];
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
       else csc_scatter_role(scat, xb - flat.nblocks);     // the CSC transpose's scatter (csc.h)
       return;
     }
-    fs_coef_stage<(2 * kCosMaxN) / 256>(fs, threadIdx.x, 256,
+    fs_coef_stage<(2 * kCosMaxN + NT - 1) / NT>(fs, threadIdx.x, NT,
                                           [&](int t, int c, float mu, float rs, float inv, float sh) {
       s_co[(t * 4 + 0) * kCosMaxN + c] = mu;
       s_co[(t * 4 + 1) * kCosMaxN + c] = rs;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
     }
   }
   if constexpr (FSC) {
-    // workgroup sums of the 4 waves (fp64) -> the layer's backward accumulators
+    // workgroup sums of the NW waves (fp64) -> the layer's backward accumulators
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const int c = lane + 64 * e;
@@ -250,11 +256,11 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
       s_bs[(wv * 4 + 3) * EPL * 64 + c] = bd2[e];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 4 * n; i += 256) {
+    for (int i = threadIdx.x; i < 4 * n; i += NT) {
       const int st = i / n, c = i - st * n;  // st: q-sum, q-sum*xhat, d-sum, d-sum*xhat
       double acc = 0.0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
+      for (int w = 0; w < NW; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
       atomic_add_f64(fs.bsum + (size_t)(blockIdx.x % fs.bcopies) * 4 * ld + (size_t)st * ld + c, acc);
     }
   }
@@ -266,8 +272,14 @@ __global__ __launch_bounds__(256) void k_cosine_loss(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = s_part[0][0] + s_part[0][1] + s_part[0][2] + s_part[0][3];
-    part[2 * blockIdx.x + 1] = s_part[1][0] + s_part[1][1] + s_part[1][2] + s_part[1][3];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      a += s_part[0][w];
+      b += s_part[1][w];
+    }
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
   }
   if (tm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -295,19 +307,26 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const FlatSlice* flat, const CscScatter* scatter) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
-  const int blocks = cdiv(bs, 4);
-  unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * blocks + 32);
+  const int nw = cosine_waves(n, fused != nullptr);
+  const int blocks = cosine_blocks(bs, n, fused != nullptr);
+  unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * cdiv(bs, 4) + 32);  // past either layout
   const FlatSlice fl = (flat && fused) ? *flat : FlatSlice{};
-  const CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
+  CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
+  if (sc.nblocks) sc.nblocks = std::max(1, sc.nblocks * 4 / nw);  // sized in 4-wave workgroups
   if (scatter && !fused) return hipErrorInvalidValue;  // the role rides on the fused kernel only
   // fused: + materialising, flat and scatter blocks
-  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks + sc.nblocks), block(256);
+  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \
-  hipLaunchKernelGGL((k_cosine_loss<E, KM, F>), grid, block, 0, s, z, ld, n, bs, neg, gamma, coef, \
-                     y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,               \
-                     (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc)
+  if (nw == kCosFusedWaves)                                                                     \
+    hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,   \
+                       (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc);                      \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,        \
+                       (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -324,8 +343,9 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   return hipGetLastError();
 }
 
-hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, cosine_blocks(bs), bs, loss_out);
+hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s) {
+  // only after a fused-statistics forward (the deferred loss)
+  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, cosine_blocks(bs, n, true), bs, loss_out);
   return hipGetLastError();
 }
 

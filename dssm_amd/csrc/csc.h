@@ -22,11 +22,12 @@ struct CscScatter {
   int nblocks;      // workgroups given to the role (0: none)
 };
 
-// Workgroup b of the role's nblocks (256 threads): one wave per CSR row, grid-stride over rows.
+// Workgroup b of the role's nblocks: one wave per CSR row, grid-stride over rows.
 __device__ __forceinline__ void csc_scatter_role(const CscScatter& s, int b) {
-  for (int c = b * 256 + (int)threadIdx.x; c < s.D; c += s.nblocks * 256) s.cnt[c] = 0;
+  const int nt = blockDim.x, nw = nt >> 6;
+  for (int c = b * nt + (int)threadIdx.x; c < s.D; c += s.nblocks * nt) s.cnt[c] = 0;
   const int lane = threadIdx.x & 63;
-  for (int row = b * 4 + (int)(threadIdx.x >> 6); row < s.rows; row += s.nblocks * 4) {
+  for (int row = b * nw + (int)(threadIdx.x >> 6); row < s.rows; row += s.nblocks * nw) {
     const int st = s.indptr[row], e = s.indptr[row + 1];
     for (int k = st + lane; k < e; k += 64) {
       const int c = s.indices[k];

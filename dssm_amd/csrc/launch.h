@@ -170,8 +170,15 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               bool defer_finalize = false, unsigned long long* timing = nullptr,
     const FlatSlice* flat = nullptr, const CscScatter* scatter = nullptr);
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
-inline int cosine_blocks(int bs) { return (bs + 3) / 4; }
-hipError_t launch_loss_finalize(const float* ws, int bs, float* loss_out, hipStream_t s);
+// (queries per workgroup: kCosFusedWaves for the fused-statistics kernel at widths <= 128,
+// whose per-wave LDS slots then stay small; otherwise 4)
+constexpr int kCosFusedWaves = 16;
+inline int cosine_waves(int n, bool fused) { return (fused && n <= 128) ? kCosFusedWaves : 4; }
+inline int cosine_blocks(int bs, int n = 0, bool fused = false) {
+  const int w = cosine_waves(n, fused);
+  return (bs + w - 1) / w;
+}
+hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s);
 
 // ---- optimizer (adam.hip) ----
 struct ShadowSeg {

@@ -981,7 +981,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
       HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                               P->at<uint16_t>(Lt.dZ[l]), s,
                                               fin ? P->at<float>(Lt.loss_j) : nullptr,
-                                              dssm::cosine_blocks(Lt.BS), P->at<float>(Lt.loss),
+                                              dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true), P->at<float>(Lt.loss),
                                               (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr,
                                               dw_pending ? &dw : nullptr));
       if (dw_pending && dw_reduce_to) {  // not deferred to Adam: the slabs summed right after
@@ -1236,8 +1236,8 @@ int dssm_plan_dense_enabled(dssm_plan* P) { return P && P->dense_on ? P->dense_g
 int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (P->loss_pending) {
-    HIP_TRY(dssm::launch_loss_finalize(P->at<float>(P->Lt.loss_j), P->Lt.BS, P->at<float>(P->Lt.loss),
-                                       (hipStream_t)stream));
+    HIP_TRY(dssm::launch_loss_finalize(P->at<float>(P->Lt.loss_j), P->Lt.BS, P->Lt.n[P->Lt.L - 1],
+                                       P->at<float>(P->Lt.loss), (hipStream_t)stream));
     P->loss_pending = false;
   }
   return DSSM_OK;
