@@ -204,7 +204,8 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     lj = -logf(p[0]);
     cj = (amax == 0) ? 1.f : 0.f;
     stamp();
-    // ---- backward: d loss / d cos_sim[j,k] = (p_k - [k==0]) / BS
+    // ---- backward: d loss / d cos_sim[j,k] = (p_k - [k==0]) / BS (skipped without dy: eval)
+    if (FSC || dy != nullptr) {
     float dq[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) dq[e] = 0.f;
@@ -244,6 +245,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
         }
       }
     }
+    }  // backward
   }
   if constexpr (FSC) {
     // workgroup sums of the NW waves (fp64) -> the layer's backward accumulators

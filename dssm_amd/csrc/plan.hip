@@ -897,7 +897,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
       c.gamma, fused_last ? P->at<float>(Lt.coef[lL]) : nullptr,
       fused_last ? P->at<float>(Lt.A[lL]) : nullptr, P->at<float>(Lt.cos_raw),
       P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
-      P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
+      P->at<float>(Lt.loss_j), P->at<float>(Lt.loss),
+      train ? P->at<float>(Lt.dA[lL]) : nullptr,  // eval: no gradient
       P->split_finalize, s));
   P->fwd_train_done = train != 0;
   return DSSM_OK;
