@@ -332,7 +332,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
-  if (neg + 1 <= 8) { DSSM_COS2(E, 8); } else { DSSM_COS2(E, 16); }
+  if (neg + 1 == 5) { DSSM_COS2(E, 5); } else if (neg + 1 <= 8) { DSSM_COS2(E, 8); } else { DSSM_COS2(E, 16); }
   if (epl <= 1) { DSSM_COS(1) }
   else if (epl <= 2) { DSSM_COS(2) }
   else if (epl <= 4) { DSSM_COS(4) }
