@@ -447,9 +447,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   // first in dispatch order); they read dZ of the layer above and the forward's activations, so
   // they are independent of this launch's own work
   if ((int)blockIdx.x < dw_blocks) {
-#ifdef DSSM_DW_SKIP  // timing diagnostics only (wrong dW): the launch without the dW tiles' work
-    return;
-#endif
     const int r = blockIdx.x;
     u16* sA = reinterpret_cast<u16*>(smem);
     tn_chunk_body<3>(dw, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y), sA, sA + 2 * kTnTile);

@@ -143,35 +143,6 @@ __device__ __forceinline__ void tn_body(const TnParams& p, int tx, int ty, int t
   }
 }
 
-// One 16-B group (8 m of A, 8 n of B) of batch row gk, edges zero-filled, the virtual ones column
-// of A (m == Mload) set to 1.
-__device__ __forceinline__ void tn_load16(const TnParams& p, int gk, int gm, int gn, int kend,
-                                          int Mload, uint4& va, uint4& vb) {
-  va = make_uint4(0u, 0u, 0u, 0u);
-  vb = va;
-  if (gk >= kend) return;
-  if (gm + 8 <= Mload) {
-    va = *reinterpret_cast<const uint4*>(p.A + (size_t)gk * p.lda + gm);
-  } else {
-    u16 x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      x[i] = (gm + i < Mload) ? p.A[(size_t)gk * p.lda + gm + i]
-                              : ((p.ones_row && gm + i == Mload) ? (u16)0x3f80 : (u16)0);
-    va.x = x[0] | ((unsigned)x[1] << 16); va.y = x[2] | ((unsigned)x[3] << 16);
-    va.z = x[4] | ((unsigned)x[5] << 16); va.w = x[6] | ((unsigned)x[7] << 16);
-  }
-  if (gn + 8 <= p.N) {
-    vb = *reinterpret_cast<const uint4*>(p.B + (size_t)gk * p.ldb + gn);
-  } else {
-    u16 x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = (gn + i < p.N) ? p.B[(size_t)gk * p.ldb + gn + i] : (u16)0;
-    vb.x = x[0] | ((unsigned)x[1] << 16); vb.y = x[2] | ((unsigned)x[3] << 16);
-    vb.z = x[4] | ((unsigned)x[5] << 16); vb.w = x[6] | ((unsigned)x[7] << 16);
-  }
-}
-
 // Whole-split variant of tn_body (same tile, same k order, so the same sums): every load of the
 // split's k_per_split <= 128 * NSUB rows is issued at once (one round trip instead of one per
 // 64-row k-step), then staged through the same 2 x 2 x kTnTile LDS 128 rows at a time.
