@@ -19,9 +19,12 @@ DSSM_ABI_VERSION = 1
 DSSM_MAX_LAYERS = 8
 DSSM_F32, DSSM_BF16 = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
- BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING) = range(11)
+ BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING, BUF_A, BUF_DA) = range(13)
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
 GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS, GRAPH_WIRE_SHADOWS = 1, 2, 4, 8
+# dssm_plan_schedule bits (include/dssm.h DSSM_SCHED_*)
+SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_ADAM": 8,
+              "WHOLEK": 16, "DW_IN_APPLY": 32, "SCATTER_IN_COS": 64, "DETERMINISTIC": 128}
 
 
 class DssmError(RuntimeError):
@@ -71,6 +74,7 @@ _SIGS = {
     "dssm_plan_check": (C.c_int, [_P, _P]),
     "dssm_plan_dense_enabled": (C.c_int, [_P]),
     "dssm_plan_fused_stats": (C.c_int, [_P]),
+    "dssm_plan_schedule": (C.c_int, [_P]),
     "dssm_plan_set_adam_range": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "dssm_plan_finalize_loss": (C.c_int, [_P, _P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),

@@ -705,6 +705,11 @@ int dssm_plan_buffer(const dssm_plan* P, int id, int layer, void** ptr, size_t* 
     case DSSM_BUF_BATCH_MEAN: off = Lt.bmean[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
     case DSSM_BUF_BATCH_VAR: off = Lt.bvar[layer]; n = (size_t)2 * Lt.n[layer] * 4; break;
     case DSSM_BUF_DZ: off = Lt.dZ[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * (Lt.bf16 ? 2 : 4); break;
+    case DSSM_BUF_A:
+      off = Lt.A[layer];
+      n = (size_t)Lt.R * Lt.ldp[layer] * (Lt.bf16 && layer < Lt.L - 1 ? 2 : 4);
+      break;
+    case DSSM_BUF_DA: off = Lt.dA[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * 4; break;
     case DSSM_BUF_DENSE_TIMING:
       if (!Lt.dense_ok) return fail(DSSM_E_UNSUPPORTED, "no dense-kernel workspace in this plan");
       off = Lt.dense_timing; n = 4 * 64 * 8; break;
@@ -1242,6 +1247,22 @@ int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
     P->loss_pending = false;
   }
   return DSSM_OK;
+}
+
+int dssm_plan_schedule(const dssm_plan* P) {
+  if (!P) return 0;
+  int f = 0;
+  const bool fs = P->fused_stats && !P->dense_on;
+  if (fs) f |= DSSM_SCHED_FUSED_STATS;
+  if (P->merged_csc()) f |= DSSM_SCHED_MERGED_CSC;
+  if (P->heavy_in_adam()) f |= DSSM_SCHED_HEAVY_IN_ADAM;
+  if (P->fused_w1_adam) f |= DSSM_SCHED_FUSED_W1_ADAM;
+  bool wk = P->Lt.L > 1;
+  for (int l = 1; l < P->Lt.L; ++l) wk = wk && P->wholek(l);
+  if (wk) f |= DSSM_SCHED_WHOLEK;
+  if (fs && P->dw_in_apply) f |= DSSM_SCHED_DW_IN_APPLY;
+  if (P->merged_csc() && P->scatter_in_cos) f |= DSSM_SCHED_SCATTER_IN_COS;
+  return f;
 }
 
 int dssm_plan_fused_stats(dssm_plan* P) { return P && P->fused_stats && !P->dense_on ? 1 : 0; }

@@ -316,6 +316,11 @@ class DSSM:
         """True when bf16 train steps run with the BN statistics fused (csrc/bnfuse.h)."""
         return bool(self.lib.dssm_plan_fused_stats(self._plan))
 
+    def schedule(self) -> Dict[str, bool]:
+        """Which kernels a train step of this plan runs (dssm_plan_schedule, DSSM_SCHED_*)."""
+        f = int(self.lib.dssm_plan_schedule(self._plan))
+        return {k: bool(f & b) for k, b in _lib.SCHED_BITS.items()}
+
     # ---- kernel timing probes (HIP events on the launch stream) -------------------------------
     def probe_enable(self, probe_id: int, max_samples: int):
         check(self.lib.dssm_plan_probe_enable(self._plan, probe_id, max_samples), "probe_enable")

@@ -74,6 +74,9 @@ enum {
   DSSM_BUF_DZ,              /* dZ of layer `layer` (compute dtype, R*ldp) */
   DSSM_BUF_DENSE_TIMING,    /* uint64[2][64] phase stamps of the persistent dense kernels
                                (100 MHz clock; written only when DSSM_DENSE_TIMING=1) */
+  DSSM_BUF_A,               /* post-BN/ReLU activation of layer `layer` (R*ldp): the next product's
+                               operand, bf16 in bf16 mode; fp32 embeddings for the last layer */
+  DSSM_BUF_DA,              /* float[R*ldp(n_l)] d loss / d A of layer `layer` (the last: dy) */
   DSSM_BUF_COUNT
 };
 
@@ -181,6 +184,19 @@ int dssm_plan_dense_enabled(dssm_plan* plan);
  * fused into the producing / consuming kernels (DSSM_FUSED_STATS, default on where supported:
  * bf16, query_bs % 64 == 0, widths <= 512), else 0. */
 int dssm_plan_fused_stats(dssm_plan* plan);
+/* What a train step of this plan runs (bit set of DSSM_SCHED_*), for tests and reports that
+ * must know which kernels produced a result. */
+enum {
+  DSSM_SCHED_FUSED_STATS = 1,      /* BN statistics fused into producers / consumers (bnfuse.h) */
+  DSSM_SCHED_MERGED_CSC = 2,       /* CSC transpose split across the forward's launches */
+  DSSM_SCHED_HEAVY_IN_ADAM = 4,    /* dW1 heavy columns as work items of the Adam launch */
+  DSSM_SCHED_FUSED_W1_ADAM = 8,    /* dW1 light rows + dW_l slabs consumed inside Adam */
+  DSSM_SCHED_WHOLEK = 16,          /* layers >= 2 on the whole-K bf16 NT / backward-pair GEMMs */
+  DSSM_SCHED_DW_IN_APPLY = 32,     /* dW_l split-K tiles inside the next BN-backward apply launch */
+  DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
+  DSSM_SCHED_DETERMINISTIC = 128   /* fixed-order reductions: bit-identical repeated runs */
+};
+int dssm_plan_schedule(const dssm_plan* plan);
 /* The fused-statistics train forward leaves the loss / accuracy reduction to the backward's first
  * launch; call this before reading DSSM_BUF_LOSS after a train forward that was not followed by
  * dssm_plan_backward (no-op otherwise). */

@@ -43,6 +43,19 @@ import numpy as np
 import scipy.sparse as sp
 
 
+def bf16_round(x) -> np.ndarray:
+    """Round to bfloat16 the way the kernels do: the value is first an fp32 (the kernels hold
+    fp32), then ``(__bf16)f`` = round-to-nearest-even on the top 16 bits.  Returned as float64."""
+    u = np.ascontiguousarray(np.asarray(x, np.float32)).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def _rw(a, emulate):
+    """Operand as the matrix cores see it: bf16 under ``emulate == "bf16"``, unchanged otherwise."""
+    return bf16_round(a) if emulate == "bf16" else a
+
+
 @dataclasses.dataclass
 class OracleConfig:
     trigram_d: int
@@ -110,74 +123,75 @@ def csr_matrix(indptr, indices, values, rows, d, dtype):
                          shape=(rows, d))
 
 
-def forward(cfg: OracleConfig, params, ema, batch, train: bool = True, dtype=np.float64):
-    """Forward pass; returns (cache, new_ema).  ``batch`` = dict(indptr, indices, values) of the
-    combined CSR over rows [q(BS); pos(BS); neg(BS*NEG)] (utils/utils.py:45-61 slicing)."""
+def towers_of(cfg: OracleConfig):
+    """Row ranges of the two BN towers: query rows, then doc rows = concat[pos; neg]
+    (new_dssm.py:128-132)."""
+    return {"q": slice(0, cfg.query_bs), "d": slice(cfg.query_bs, cfg.rows)}
+
+
+def bn_relu_forward(cfg: OracleConfig, Z, params, l: int, ema, new_ema=None, dtype=np.float64):
+    """``batch_normalization`` + ReLU of layer l (new_dssm.py:62-88, :134-136) on Z [R x n] per
+    tower.  ``new_ema`` given (train): batch moments, EMA update into ``new_ema``; otherwise the
+    shadows in ``ema`` (new_dssm.py:85-86).  Returns the layer cache {Z, Y, A, mu, var, r, inv,
+    batch_mean, batch_var}."""
     dt = dtype
-    BS, NEG, R = cfg.query_bs, cfg.neg, cfg.rows
-    X = csr_matrix(batch["indptr"], batch["indices"], batch["values"], R, cfg.trigram_d, dt)
-    towers = {"q": slice(0, BS), "d": slice(BS, R)}
-    cache = {"X": X, "layers": []}
-    new_ema = {k: v.copy() for k, v in ema.items()}
-    A = None
-    for l in range(1, cfg.n_layers + 1):
-        W = params[f"W{l}"].astype(dt)
-        b = params[f"b{l}"].astype(dt)
-        Z = (X @ W if l == 1 else A @ W) + b
-        Y = np.empty_like(Z)
-        lc = {"Z": Z, "A_in": A, "mu": {}, "var": {}, "inv": {}, "r": {}}
-        for t, sl in towers.items():
-            z = Z[sl]
-            bmean = z.mean(axis=0)
-            bvar = ((z - bmean) ** 2).mean(axis=0)
-            if train:
-                for nm, val in (("mean", bmean), ("var", bvar)):
-                    key = f"bn{l}_{t}_{nm}"
-                    s = new_ema[key].astype(dt)
-                    new_ema[key] = (s - (s - val) * (1.0 - cfg.ema_decay)).astype(np.float32)
-                mu, var = bmean, bvar
-            else:
-                mu = ema[f"bn{l}_{t}_mean"].astype(dt)
-                var = ema[f"bn{l}_{t}_var"].astype(dt)
-            r = 1.0 / np.sqrt(var + cfg.bn_eps)
-            inv = r * params[f"bn{l}_{t}_gamma"].astype(dt)
-            Y[sl] = z * inv + (params[f"bn{l}_{t}_beta"].astype(dt) - mu * inv)
-            lc["mu"][t], lc["var"][t], lc["inv"][t], lc["r"][t] = mu, var, inv, r
-            lc.setdefault("batch_mean", {})[t] = bmean
-            lc.setdefault("batch_var", {})[t] = bvar
-        A = np.maximum(Y, 0)
-        lc["Y"], lc["A"] = Y, A
-        cache["layers"].append(lc)
+    Z = np.asarray(Z, dt)
+    Y = np.empty_like(Z)
+    lc = {"Z": Z, "mu": {}, "var": {}, "inv": {}, "r": {}, "batch_mean": {}, "batch_var": {}}
+    for t, sl in towers_of(cfg).items():
+        z = Z[sl]
+        bmean = z.mean(axis=0)
+        bvar = ((z - bmean) ** 2).mean(axis=0)
+        if new_ema is not None:
+            for nm, val in (("mean", bmean), ("var", bvar)):
+                key = f"bn{l}_{t}_{nm}"
+                s = new_ema[key].astype(dt)
+                new_ema[key] = (s - (s - val) * (1.0 - cfg.ema_decay)).astype(np.float32)
+            mu, var = bmean, bvar
+        else:
+            mu = ema[f"bn{l}_{t}_mean"].astype(dt)
+            var = ema[f"bn{l}_{t}_var"].astype(dt)
+        r = 1.0 / np.sqrt(var + cfg.bn_eps)
+        inv = r * params[f"bn{l}_{t}_gamma"].astype(dt)
+        Y[sl] = z * inv + (params[f"bn{l}_{t}_beta"].astype(dt) - mu * inv)
+        lc["mu"][t], lc["var"][t], lc["inv"][t], lc["r"][t] = mu, var, inv, r
+        lc["batch_mean"][t], lc["batch_var"][t] = bmean, bvar
+    lc["Y"], lc["A"] = Y, np.maximum(Y, 0)
+    return lc
+
+
+def cosine_loss_forward(cfg: OracleConfig, A, dtype=np.float64):
+    """Merge_Negative_Doc + Cosine_Similarity + softmax loss + accuracy (new_dssm.py:160-222) on
+    the embeddings A [R x n] = rows [q; pos; neg]."""
+    dt = dtype
+    BS, NEG = cfg.query_bs, cfg.neg
+    A = np.asarray(A, dt)
     yq, yp, yn = A[:BS], A[BS:2 * BS], A[2 * BS:]
     # Merge_Negative_Doc as a permutation: doc[k][j]
     docs = [yp] + [yn[k - 1::NEG] for k in range(1, NEG + 1)]
     qn = np.sqrt((yq * yq).sum(1))
     c = np.empty((BS, NEG + 1), dt)
     dn = np.empty((BS, NEG + 1), dt)
-    dots = np.empty((BS, NEG + 1), dt)
     for k, dk in enumerate(docs):
         dn[:, k] = np.sqrt((dk * dk).sum(1))
-        dots[:, k] = (yq * dk).sum(1)
-        c[:, k] = dots[:, k] / (qn * dn[:, k])
+        c[:, k] = (yq * dk).sum(1) / (qn * dn[:, k])
     cos_sim = cfg.gamma * c
     smax = cos_sim - cos_sim.max(1, keepdims=True)
     e = np.exp(smax)
     prob = e / e.sum(1, keepdims=True)
     loss = -np.log(prob[:, 0]).sum() / BS
     acc = float((np.argmax(prob, 1) == 0).mean())
-    cache.update(yq=yq, docs=docs, qn=qn, dn=dn, c=c, cos_sim=cos_sim, prob=prob,
-                 cos_sim_raw=c.T.reshape(-1).copy(), loss=float(loss), accuracy=acc,
-                 query_norm_single=qn)
-    return cache, new_ema
+    return dict(yq=yq, docs=docs, qn=qn, dn=dn, c=c, cos_sim=cos_sim, prob=prob,
+                cos_sim_raw=c.T.reshape(-1).copy(), loss=float(loss), accuracy=acc,
+                query_norm_single=qn)
 
 
-def backward(cfg: OracleConfig, params, cache, dtype=np.float64):
-    """Gradients of the loss w.r.t. every trainable variable (dict keyed like params)."""
-    dt = dtype
+def cosine_loss_backward(cfg: OracleConfig, cc, dtype=np.float64):
+    """d loss / d embeddings [R x n] from a cosine_loss_forward result (TF autodiff of
+    new_dssm.py:182-209; the merge's gradient scatters back to the pos / neg rows)."""
     BS, NEG, R = cfg.query_bs, cfg.neg, cfg.rows
-    towers = {"q": slice(0, BS), "d": slice(BS, R)}
-    prob, c, qn, dn = cache["prob"], cache["c"], cache["qn"], cache["dn"]
-    yq, docs = cache["yq"], cache["docs"]
+    prob, c, qn, dn = cc["prob"], cc["c"], cc["qn"], cc["dn"]
+    yq, docs = cc["yq"], cc["docs"]
     ds = prob.copy()
     ds[:, 0] -= 1.0
     ds /= BS
@@ -189,32 +203,83 @@ def backward(cfg: OracleConfig, params, cache, dtype=np.float64):
         ck = c[:, k]
         dyq += dc[:, k:k + 1] * (dk * inv_nn[:, None] - (ck / (qn * qn))[:, None] * yq)
         ddocs.append(dc[:, k:k + 1] * (yq * inv_nn[:, None] - (ck / (dn[:, k] ** 2))[:, None] * dk))
-    dA = np.empty((R, yq.shape[1]), dt)
+    dA = np.empty((R, yq.shape[1]), dtype)
     dA[:BS] = dyq
     dA[BS:2 * BS] = ddocs[0]
     for k in range(1, NEG + 1):
         dA[2 * BS + (k - 1)::NEG] = ddocs[k]
+    return dA
+
+
+def bn_relu_backward(cfg: OracleConfig, lc, dA, l: int):
+    """Backward of bn_relu_forward (train mode) for d loss / d A: ReluGrad on the output (> 0),
+    then the batch-statistic BN gradient.  Returns (dZ, {bn{l}_{t}_gamma / _beta: grads})."""
+    Z, Y = lc["Z"], lc["Y"]
+    dY = dA * (Y > 0)
+    dZ = np.empty_like(Z)
+    g = {}
+    for t, sl in towers_of(cfg).items():
+        n = sl.stop - sl.start
+        xhat = (Z[sl] - lc["mu"][t]) * lc["r"][t]
+        dy = dY[sl]
+        dbeta = dy.sum(0)
+        dgamma = (dy * xhat).sum(0)
+        g[f"bn{l}_{t}_beta"] = dbeta
+        g[f"bn{l}_{t}_gamma"] = dgamma
+        dZ[sl] = lc["inv"][t] * (dy - dbeta / n - xhat * (dgamma / n))
+    return dZ, g
+
+
+def forward(cfg: OracleConfig, params, ema, batch, train: bool = True, dtype=np.float64,
+            emulate: Optional[str] = None):
+    """Forward pass; returns (cache, new_ema).  ``batch`` = dict(indptr, indices, values) of the
+    combined CSR over rows [q(BS); pos(BS); neg(BS*NEG)] (utils/utils.py:45-61 slicing).
+
+    ``emulate="bf16"`` restates the GPU perf mode's roundings (not a reference behaviour: the
+    reference is fp32 throughout, new_dssm.py:111-114): every weight W_l is read as its bf16
+    shadow, and each hidden layer's post-BN/ReLU activation is rounded to bf16 before it feeds
+    the next layer's product (the last layer's embeddings stay fp32).  Everything else --
+    BN statistics, cosine, softmax, loss -- is computed as in fp32 mode."""
+    dt = dtype
+    X = csr_matrix(batch["indptr"], batch["indices"], batch["values"], cfg.rows, cfg.trigram_d, dt)
+    cache = {"X": X, "layers": [], "emulate": emulate}
+    new_ema = {k: v.copy() for k, v in ema.items()}
+    A = None
+    for l in range(1, cfg.n_layers + 1):
+        W = _rw(params[f"W{l}"], emulate).astype(dt)
+        b = params[f"b{l}"].astype(dt)
+        Z = (X @ W if l == 1 else A @ W) + b
+        lc = bn_relu_forward(cfg, Z, params, l, ema, new_ema if train else None, dt)
+        lc["A_in"] = A
+        A = lc["A"]
+        if l < cfg.n_layers:
+            A = _rw(A, emulate).astype(dt)  # the next product's operand (bf16 in perf mode)
+        cache["layers"].append(lc)
+    cache.update(cosine_loss_forward(cfg, A, dt))
+    return cache, new_ema
+
+
+def backward(cfg: OracleConfig, params, cache, dtype=np.float64):
+    """Gradients of the loss w.r.t. every trainable variable (dict keyed like params).
+
+    Under the forward's ``emulate="bf16"`` every dZ_l is rounded to bf16 before it enters a
+    product (dW_l = A_{l-1}^T dZ_l, dA_{l-1} = dZ_l W_l^T with W_l's bf16 shadow, dW1 = X^T dZ_1),
+    as the GPU perf mode stores it; BN's dgamma / dbeta use the unrounded fp32 dy."""
+    dt = dtype
+    emulate = cache.get("emulate")
+    dA = cosine_loss_backward(cfg, cache, dt)
     grads = {}
     for l in range(cfg.n_layers, 0, -1):
         lc = cache["layers"][l - 1]
-        Z, Y = lc["Z"], lc["Y"]
-        dY = dA * (Y > 0)
-        dZ = np.empty_like(Z)
-        for t, sl in towers.items():
-            n = sl.stop - sl.start
-            xhat = (Z[sl] - lc["mu"][t]) * lc["r"][t]
-            dy = dY[sl]
-            dbeta = dy.sum(0)
-            dgamma = (dy * xhat).sum(0)
-            grads[f"bn{l}_{t}_beta"] = dbeta
-            grads[f"bn{l}_{t}_gamma"] = dgamma
-            dZ[sl] = lc["inv"][t] * (dy - dbeta / n - xhat * (dgamma / n))
+        dZ, bg = bn_relu_backward(cfg, lc, dA, l)
+        grads.update(bg)
+        dZ = _rw(dZ, emulate).astype(dt)
         grads[f"b{l}"] = dZ.sum(0)
         if l == 1:
             grads["W1"] = np.asarray(cache["X"].T @ dZ)
         else:
             grads[f"W{l}"] = lc["A_in"].T @ dZ
-            dA = dZ @ params[f"W{l}"].astype(dt).T
+            dA = dZ @ _rw(params[f"W{l}"], emulate).astype(dt).T
     return grads
 
 
@@ -267,10 +332,11 @@ def make_ema(cfg: OracleConfig) -> Dict[str, np.ndarray]:
     return ema
 
 
-def train_step(cfg: OracleConfig, params, ema, adam: AdamState, batch, dtype=np.float64):
+def train_step(cfg: OracleConfig, params, ema, adam: AdamState, batch, dtype=np.float64,
+               emulate: Optional[str] = None):
     """One ``sess.run(train_step)`` (new_dssm.py:267): forward (EMA update), backward, Adam.
     Mutates params/adam in place; returns (cache, grads, new_ema)."""
-    cache, new_ema = forward(cfg, params, ema, batch, train=True, dtype=dtype)
+    cache, new_ema = forward(cfg, params, ema, batch, train=True, dtype=dtype, emulate=emulate)
     grads = backward(cfg, params, cache, dtype=dtype)
     adam.step(params, grads)
     return cache, grads, new_ema

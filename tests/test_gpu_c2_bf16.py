@@ -1,0 +1,312 @@
+"""The timed path itself, at the headline shape, against the oracle.
+
+BASELINE config 2 (D=30000, widths 300/300/128, BS=1024, NEG=4, bf16) is what bench.py times:
+fused BN statistics, the CSC transpose merged into the forward, the whole-K NT / backward-pair
+GEMMs, the exact-K (K = NEG+1 = 5) cosine kernel, dW1's light rows and heavy columns inside the
+Adam launch, and the multi-step hipGraph.  The reference's own default (config.py:19-28:
+query_BS=400, L1_N=L2_N=100, NEG=4) runs the same kernels on the separate-statistics schedule
+(BS % 64 != 0) and is checked the same way.  The reference computes in fp32 (new_dssm.py:111-114);
+bf16 is the perf mode BASELINE.json names for C2.
+
+Two kinds of check:
+
+1. **Kernel chain, teacher-forced** (``test_bf16_kernel_chain``).  Every product of one step is
+   recomputed by the oracle's per-op functions in float64 FROM THE GPU'S OWN INPUTS to that op
+   (Z_l, A_l, dA_l, dZ_l read back through DSSM_BUF_*), so no rounding cascades between layers:
+   * fp32 outputs (Z_l, embeddings, cosines, prob, loss, dy, dA_l, every gradient):
+     max error <= 2e-5 x the row's / tensor's max magnitude (fp32 accumulation only);
+   * bf16 outputs (A_l of hidden layers, dZ_l): identical to the float64 value rounded to bf16
+     except where the fp32 value sits on a rounding boundary: <= 5e-4 of the elements differ,
+     each by at most one bf16 ulp (2^-7 relative) or 1e-6 absolute (a ReLU mask at Y ~ 0).
+     (2e-4 is the measured worst, for dZ, whose fp32 value carries BN's cancellation: bar 5e-4.)
+2. **End to end** against the bf16-emulating oracle (``emulate="bf16"``: W shadows, hidden
+   activations and dZ rounded where the kernels round).  A bf16 rounding that an fp32-ulp
+   difference tips the other way (see 1) moves its row's next-layer values by ~2^-8/sqrt(K) and
+   cascades inside that row, so per-row bars are quantiles, not maxima (measured: <= 1% of rows
+   affected at C2, tools/diag_bf16.py):
+   * loss rel <= 1e-4 (north star); cos_sim_raw / prob: 99% of entries <= 1e-4 abs, all <= 2e-3;
+   * every non-bias gradient: ||err|| <= 3e-3 ||g|| (tens of cascaded rows contribute to every
+     element of dW_l);
+   * teacher-forced fused Adam step: against the oracle's ApplyAdam on the GPU's own unfused
+     gradients (same state, same batch) to 1e-6 + 1e-4 lr on well-conditioned elements;
+   * bench's cycle graph over two batches from a mid-training state: against two eager steps,
+     loss rel <= 1e-5 and ||p_graph - p_eager|| <= 1e-2 ||update|| per tensor (measured 1.2e-3:
+     the runs differ by the order of float atomics only); against the emulating oracle run
+     free over the same two steps, loss rel <= 1e-3 and ||p - p_oracle|| <= 0.1 ||update||
+     (measured 1.2e-4 and 3.8e-2: the first step's rounding flips change the second step's
+     inputs, so this is a drift bound, not a same-input parity bar).
+Biases are excluded element-wise: under batch-stat BN d loss / d b is exactly 0 (test_oracle.py).
+"""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from dssm_amd import _lib
+from dssm_amd.data import synth_batch
+from oracle import dssm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+C2 = (30000, (300, 300, 128), 1024, 4)
+DEFAULT = (30000, (100, 100), 400, 4)  # the reference's own config.py:19-28 (query_BS=400)
+CASES = [C2, DEFAULT]
+IDS = ["C2", "ref-default-BS400"]
+EMU = "bf16"
+
+
+def _is_bias(k):
+    return re.fullmatch(r"b\d+", k) is not None
+
+
+def _rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-30)
+
+
+def _cfg(case):
+    D, widths, BS, NEG = case
+    return O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
+
+
+def _model(case, p, fused):
+    from dssm_amd.model import DSSM
+    D, widths, BS, NEG = case
+    m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
+    m.load_params(p)
+    m.set_fused_w1_adam(fused)
+    return m
+
+
+def _expect_timed_schedule(m, case):
+    """C2 runs the schedule bench.py times (include/dssm.h DSSM_SCHED_*)."""
+    if case != C2:
+        return
+    f = m.schedule()
+    want = ["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "WHOLEK", "DW_IN_APPLY", "SCATTER_IN_COS"]
+    missing = [w for w in want if not f.get(w)]
+    assert not missing, (case, missing, f)
+
+
+def _layer(m, bid, l, n, bf16=False):
+    ld = (n + 7) // 8 * 8
+    t = m.buffer(bid, l, dtype=torch.bfloat16 if bf16 else torch.float32)
+    return t.float().cpu().numpy().astype(np.float64).reshape(m.rows, ld)[:, :n]
+
+
+def _rowmax_err(got, ref):
+    """max over rows of max|got - ref| / max|ref| in that row."""
+    scale = np.abs(ref).max(axis=-1, keepdims=True) if np.ndim(ref) > 1 else np.abs(ref).max()
+    return float((np.abs(got - ref) / np.maximum(scale, 1e-30)).max())
+
+
+def _tensor_err(got, ref):
+    return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def _bf16_check(errs, name, got, exact):
+    """got: the kernel's bf16 output; exact: the float64 value from the same inputs."""
+    want = O.bf16_round(exact)
+    diff = got != want
+    errs[f"{name}_flip_frac"] = (float(diff.mean()), 5e-4)
+    if diff.any():
+        bound = 2.0 ** -7 * np.abs(exact[diff]) + 1e-6
+        errs[f"{name}_flip_size"] = (float((np.abs(got[diff] - exact[diff]) / bound).max()), 1.0)
+
+
+def _report(tag, errs):
+    bad = {k: v for k, v in errs.items() if not v[0] <= v[1]}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1][0] / kv[1][1])[:8]
+    print(f"\n[{tag}] worst error/bar: " + ", ".join(f"{k}={e:.2e}/{b:.0e}" for k, (e, b) in worst))
+    assert not bad, f"{tag}: over the bar: {bad}"
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_bf16_kernel_chain(case):
+    """Each kernel of the bf16 step against the oracle fed that kernel's GPU inputs."""
+    D, widths, BS, NEG = case
+    cfg = _cfg(case)
+    L = len(widths)
+    p = O.init_params(cfg, seed=11)
+    batch = synth_batch(D, BS, NEG, seed=1000)
+    m = _model(case, p, fused=False)
+    _expect_timed_schedule(m, case)
+    m.set_batch(batch)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    X = O.csr_matrix(batch.indptr, batch.indices, batch.values, cfg.rows, D, np.float64)
+    W = {l: O.bf16_round(p[f"W{l}"]) for l in range(1, L + 1)}
+    errs = {}
+    Z = [_layer(m, _lib.BUF_Z, l, widths[l]) for l in range(L)]
+    A = [_layer(m, _lib.BUF_A, l, widths[l], bf16=l < L - 1) for l in range(L)]
+    ema = O.make_ema(cfg)
+    lcs = []
+    for l in range(L):
+        a_in = X if l == 0 else A[l - 1]
+        z_ref = np.asarray(a_in @ W[l + 1]) + p[f"b{l + 1}"]
+        errs[f"Z{l + 1}"] = (_rowmax_err(Z[l], z_ref), 2e-5)
+        lc = O.bn_relu_forward(cfg, Z[l], p, l + 1, ema, ema)
+        lcs.append(lc)
+        mo = m.batch_moments(l + 1)
+        for t in ("q", "d"):
+            errs[f"bn{l + 1}_{t}_mean"] = (_tensor_err(mo[t][0], lc["batch_mean"][t]), 2e-5)
+            errs[f"bn{l + 1}_{t}_var"] = (_tensor_err(mo[t][1], lc["batch_var"][t]), 2e-5)
+        if l < L - 1:
+            _bf16_check(errs, f"A{l + 1}", A[l], lc["A"])
+        else:
+            errs["embedding"] = (_rowmax_err(A[l], lc["A"]), 2e-5)
+    ge = {k: v.cpu().numpy() for k, v in m.named_ema().items()}
+    for k in ema:
+        errs[f"ema_{k}"] = (_tensor_err(ge[k], ema[k]), 2e-5)
+    cc = O.cosine_loss_forward(cfg, A[L - 1])
+    errs["loss"] = (_rel(m.loss_accuracy()[0], cc["loss"]), 1e-5)
+    errs["cos_sim_raw"] = (float(np.abs(m.fetch("cos_sim_raw").ravel() - cc["cos_sim_raw"]).max()), 2e-5)
+    errs["prob"] = (float(np.abs(m.fetch("prob") - cc["prob"]).max()), 2e-5)
+    errs["query_norm"] = (_tensor_err(m.fetch("query_norm_single").ravel(), cc["qn"]), 2e-5)
+    dA = _layer(m, _lib.BUF_DA, L - 1, widths[-1])
+    errs["dy"] = (_rowmax_err(dA, O.cosine_loss_backward(cfg, cc)), 2e-5)
+    gg = {k: v.cpu().numpy().astype(np.float64) for k, v in m.named_grads().items()}
+    for l in range(L - 1, -1, -1):
+        dA = _layer(m, _lib.BUF_DA, l, widths[l])
+        dz_exact, bg = O.bn_relu_backward(cfg, lcs[l], dA, l + 1)
+        for k, g in bg.items():
+            errs[f"grad_{k}"] = (_tensor_err(gg[k], g), 2e-5)
+        dZ = _layer(m, _lib.BUF_DZ, l, widths[l], bf16=True)
+        _bf16_check(errs, f"dZ{l + 1}", dZ, dz_exact)
+        a_in = X if l == 0 else A[l - 1]
+        errs[f"grad_W{l + 1}"] = (_tensor_err(gg[f"W{l + 1}"], np.asarray(a_in.T @ dZ)), 2e-5)
+        db = dZ.sum(0)
+        errs[f"grad_b{l + 1}"] = (float(np.abs(gg[f"b{l + 1}"] - db).max() / np.abs(dZ).sum(0).max()), 2e-5)
+        if l > 0:
+            da_ref = dZ @ W[l + 1].T
+            errs[f"dA{l}"] = (_rowmax_err(_layer(m, _lib.BUF_DA, l - 1, widths[l - 1]), da_ref), 2e-5)
+    _report(f"chain {case}", errs)
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_bf16_step_matches_emulating_oracle(case):
+    """One unfused step end to end against the bf16-emulating oracle (quantile bars, see doc)."""
+    D, widths, BS, NEG = case
+    cfg = _cfg(case)
+    p = O.init_params(cfg, seed=11)
+    batch = synth_batch(D, BS, NEG, seed=1000)
+    cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64, emulate=EMU)
+    grads = O.backward(cfg, p, cache, np.float64)
+    m = _model(case, p, fused=False)
+    m.set_batch(batch)
+    m.forward(True)
+    m.backward()
+    torch.cuda.synchronize()
+    errs = {"loss": (_rel(m.loss_accuracy()[0], cache["loss"]), 1e-4)}
+    for name, got, ref in (("cos_sim_raw", m.fetch("cos_sim_raw").ravel(), cache["cos_sim_raw"]),
+                           ("prob", m.fetch("prob").ravel(), cache["prob"].ravel())):
+        e = np.abs(got - ref)
+        errs[f"{name}_q99"] = (float(np.quantile(e, 0.99)), 1e-4)
+        errs[f"{name}_max"] = (float(e.max()), 2e-3)
+    gg = {k: v.cpu().numpy() for k, v in m.named_grads().items()}
+    for k, g in grads.items():
+        if not _is_bias(k):
+            errs[f"grad_{k}_l2"] = (float(np.linalg.norm(gg[k] - g) / np.linalg.norm(g)), 3e-3)
+    _report(f"end-to-end {case}", errs)
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_bf16_fused_adam_step_teacher_forced(case):
+    """The fused single-GPU step (dW1's light rows and heavy columns inside Adam, dW_l slabs
+    summed by Adam) from a mid-training state (one oracle step: non-zero m, v, EMA) against the
+    oracle's ApplyAdam on the gradients the unfused schedule computes from the same state."""
+    D, widths, BS, NEG = case
+    cfg = _cfg(case)
+    p = O.init_params(cfg, seed=11)
+    adam = O.AdamState(cfg, p)
+    _, _, ema = O.train_step(cfg, p, O.make_ema(cfg), adam, synth_batch(D, BS, NEG, seed=999).as_dict(),
+                             np.float64, emulate=EMU)
+    batch = synth_batch(D, BS, NEG, seed=1001)
+    models = {}
+    for fused in (False, True):
+        mm = _model(case, p, fused)
+        mm.load_params(p, ema=ema)
+        mm.load_adam_state(adam.m, adam.v, adam.beta1_power, adam.beta2_power, adam.t)
+        mm.set_batch(batch)
+        models[fused] = mm
+    mu = models[False]
+    mu.forward(True)
+    mu.backward()
+    torch.cuda.synchronize()
+    g_gpu = {k: v.cpu().numpy().astype(np.float64) for k, v in mu.named_grads().items()}
+    mf = models[True]
+    mf.train_step()
+    torch.cuda.synchronize()
+    errs = {"loss_fused_vs_unfused": (_rel(mf.loss_accuracy()[0], mu.loss_accuracy()[0]), 1e-6)}
+    adam.step(p, g_gpu)
+    gp = {k: v.cpu().numpy() for k, v in mf.named_params().items()}
+    gm, gv = mf.named_adam()
+    lr = cfg.lr
+    for k in p:
+        if _is_bias(k):
+            continue
+        d = np.abs(gp[k] - p[k])
+        well = np.abs(g_gpu[k]) > 1e-3 * np.abs(g_gpu[k]).max()
+        errs[f"param_{k}_well"] = (float(d[well].max(initial=0.0)), 1e-6 + 1e-4 * lr)
+        errs[f"param_{k}_all"] = (float(d.max()), 2 * lr)
+        errs[f"m_{k}"] = (_tensor_err(gm[k].cpu().numpy(), adam.m[k]), 1e-5)
+        errs[f"v_{k}"] = (_tensor_err(gv[k].cpu().numpy(), adam.v[k]), 1e-5)
+    assert mf.beta_powers() == (adam.beta1_power, adam.beta2_power)
+    _report(f"fused adam {case}", errs)
+
+
+def _mid_state(case):
+    """State after one emulated oracle step: non-zero m, v and EMA, so an Adam update is a
+    continuous function of the gradient (from zero slots it is lr * sign(g), and sign noise of
+    near-zero gradients would dominate every comparison)."""
+    D, widths, BS, NEG = case
+    cfg = _cfg(case)
+    p = O.init_params(cfg, seed=11)
+    adam = O.AdamState(cfg, p)
+    _, _, ema = O.train_step(cfg, p, O.make_ema(cfg), adam, synth_batch(D, BS, NEG, seed=999).as_dict(),
+                             np.float64, emulate=EMU)
+    return cfg, p, adam, ema
+
+
+def test_bf16_cycle_graph_two_steps():
+    """bench.py's cycle graph (dssm_plan_graph_build_steps) over two staged C2 batches from a
+    mid-training state: the second step's loss against the emulating oracle over the same two
+    steps, and the replayed parameters against two eager steps of the same schedule (the two
+    runs differ only by the order of float atomics, whose bf16 rounding flips cascade within a
+    row: a few gradient elements move by ~1e-3 relative, hence the fraction bar)."""
+    case = C2
+    D, widths, BS, NEG = case
+    cfg, p, adam, ema = _mid_state(case)
+    runs = []
+    for _ in range(2):
+        mm = _model(case, p, fused=True)
+        mm.load_params(p, ema=ema)
+        mm.load_adam_state(adam.m, adam.v, adam.beta1_power, adam.beta2_power, adam.t)
+        runs.append(mm)
+    m, ea = runs
+    p0 = {k: v.astype(np.float64) for k, v in p.items()}
+    _expect_timed_schedule(m, case)
+    batches = [synth_batch(D, BS, NEG, seed=1001 + i) for i in range(2)]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        staged = [tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)) for b in batches]
+        gid = m.graph_build_steps(staged)
+        m.graph_launch(gid)
+        for ip, ix, vv in staged:
+            ea.set_batch(indptr=ip, indices=ix, values=vv)
+            ea.train_step()
+    torch.cuda.synchronize()
+    for b in batches:
+        cache, _, ema = O.train_step(cfg, p, ema, adam, b.as_dict(), np.float64, emulate=EMU)
+    errs = {"loss_step2_vs_oracle": (_rel(m.loss_accuracy()[0], cache["loss"]), 1e-3),
+            "loss_step2_vs_eager": (_rel(m.loss_accuracy()[0], ea.loss_accuracy()[0]), 1e-5)}
+    gp = {k: v.cpu().numpy().astype(np.float64) for k, v in m.named_params().items()}
+    ep = {k: v.cpu().numpy().astype(np.float64) for k, v in ea.named_params().items()}
+    for k in ("W1", "W2", "W3", "bn1_q_gamma", "bn3_d_beta"):
+        upd = np.linalg.norm(ep[k] - p0[k])
+        errs[f"update_{k}_graph_vs_eager"] = (float(np.linalg.norm(gp[k] - ep[k]) / upd), 1e-2)
+        errs[f"update_{k}_vs_oracle"] = (float(np.linalg.norm(gp[k] - p[k]) / upd), 1e-1)
+    assert m.beta_powers() == ea.beta_powers() == (adam.beta1_power, adam.beta2_power)
+    assert m.global_step == ea.global_step == adam.t
+    _report("graph", errs)
