@@ -137,8 +137,14 @@ def load_vectorizer(path: str = "output/vectorizer_data.json") -> TextVectorizer
     return TextVectorizer.load(path)
 
 
-def get_data_set_comment(FileName: str, conf, seed: int = 0, max_draws: int = 100000):
-    """utils/utils.py:368-421 with seeded, ordered negatives (module doc)."""
+def get_data_set_comment(FileName: str, conf, seed: int = 0, max_draws: int = 100000,
+                         negatives: str = "seeded"):
+    """utils/utils.py:368-421.  negatives="seeded" (default): seeded, ordered negatives (module
+    doc); negatives="reference": the reference's own draw -- ``random.random()`` from Python's
+    global generator into a set per query -- so the same ``random.seed`` and PYTHONHASHSEED give
+    the reference's exact negatives and order (tests/test_ref_feed.py)."""
+    if negatives not in ("seeded", "reference"):
+        raise ValueError("negatives must be 'seeded' or 'reference'")
     query, doc = [], []
     with open(FileName, encoding="utf8") as f:
         for line in f.readlines():
@@ -150,6 +156,8 @@ def get_data_set_comment(FileName: str, conf, seed: int = 0, max_draws: int = 10
                 continue
             query.append(" ".join(pre_process(prefix)))
             doc.append(" ".join(pre_process(title)))
+    if negatives == "reference":
+        return query, doc, sample_negatives_reference(query, doc, conf.NEG, max_draws=max_draws)
     return query, doc, sample_negatives(query, doc, conf.NEG, seed, max_draws)
 
 
@@ -167,6 +175,33 @@ def sample_negatives(query: Sequence[str], doc: Sequence[str], neg: int, seed: i
             cand = doc[r]
             if cand != doc[i] and query[i] != query[r] and cand not in picked:
                 picked.append(cand)
+            draws += 1
+            if draws > max_draws:
+                raise ValueError(f"query {i}: fewer than NEG={neg} eligible negative docs")
+        out.extend(picked)
+    return out
+
+
+def sample_negatives_reference(query: Sequence[str], doc: Sequence[str], neg: int, rng=None,
+                               max_draws: int = 100000) -> List[str]:
+    """The reference's negative draw (utils/utils.py:403-419) for drop-in reproducibility: per
+    query i, uniform ``int(random() * size)`` picks, rejected when the doc equals the positive,
+    the query equals query i, or the doc was already picked; the NEG picks are collected in a
+    ``set`` and appended in that set's iteration order (hash-seed dependent, SURVEY Appendix
+    B.3).  ``rng`` defaults to Python's global ``random`` module.  Raises instead of spinning
+    forever when a query has fewer than NEG eligible docs."""
+    import random as _random
+    rnd = rng if rng is not None else _random
+    size = len(doc)
+    out: List[str] = []
+    for i in range(size):
+        picked = set()
+        draws = 0
+        while len(picked) < neg:
+            r = int(rnd.random() * size)
+            cand = doc[r]
+            if doc[i] != cand and query[i] != query[r] and cand not in picked:
+                picked.add(cand)
             draws += 1
             if draws > max_draws:
                 raise ValueError(f"query {i}: fewer than NEG={neg} eligible negative docs")
