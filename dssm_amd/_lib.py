@@ -15,16 +15,21 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdssm.so"
 # diagnostics only: an alternative in-tree build of the same library (A/B of compile-time variants)
 LIB_PATH = os.environ.get("DSSM_LIB_PATH", LIB_PATH)
 
-DSSM_ABI_VERSION = 1
+DSSM_ABI_VERSION = 2
 DSSM_MAX_LAYERS = 8
 DSSM_F32, DSSM_BF16 = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
- BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ, BUF_DENSE_TIMING, BUF_A, BUF_DA) = range(13)
+ BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
+BUF_A, BUF_DA = 11, 12
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
 GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS, GRAPH_WIRE_SHADOWS = 1, 2, 4, 8
 # dssm_plan_schedule bits (include/dssm.h DSSM_SCHED_*)
 SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_ADAM": 8,
               "WHOLEK": 16, "DW_IN_APPLY": 32, "SCATTER_IN_COS": 64, "DETERMINISTIC": 128}
+# dssm_plan_set_option ids (include/dssm.h DSSM_OPT_*)
+OPTIONS = {k: i for i, k in enumerate(["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "SCATTER_IN_COS",
+                                         "DW_IN_APPLY", "WIRE_GRAD_PASS", "CSC_RANK", "DETERMINISTIC",
+                                         "FUSED_W1_ADAM"])}
 
 
 class DssmError(RuntimeError):
@@ -71,8 +76,8 @@ _SIGS = {
     "dssm_plan_graph_launch": (C.c_int, [_P, C.c_int, _P]),
     "dssm_plan_graph_build_steps": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.c_int,
                                               C.c_int, _P, C.POINTER(C.c_int)]),
-    "dssm_plan_check": (C.c_int, [_P, _P]),
-    "dssm_plan_dense_enabled": (C.c_int, [_P]),
+    "dssm_plan_set_option": (C.c_int, [_P, C.c_int, C.c_int]),
+    "dssm_plan_get_option": (C.c_int, [_P, C.c_int]),
     "dssm_plan_fused_stats": (C.c_int, [_P]),
     "dssm_plan_schedule": (C.c_int, [_P]),
     "dssm_plan_set_adam_range": (C.c_int, [_P, C.c_int64, C.c_int64]),

@@ -24,7 +24,6 @@
 #include "launch.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace dssm {
 namespace {
@@ -95,7 +94,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
   const int n = a.n;
   const bool heavy = e - s > kLightEntries;
   if (heavy && a.item_blocks) return;  // updated by the heavy-item workgroups
-  if (e == s && (a.w1_flat || a.flat_elsewhere)) return;  // untouched: the flat roles' pass
+  if (e == s && a.w1_flat) return;  // untouched: the flat roles' pass
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
@@ -189,7 +188,9 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
 // A one-item column is updated right here; a longer column's items add their rows to the
 // gradient arena with fp32 atomics and arrive on the column's ticket: the last arrival takes
 // the row with atomic exchanges (read and clear at the coherence point), updates it and
-// re-arms the ticket.
+// re-arms the ticket.  Deterministic mode (heavy_slab): the items store their rows into the slab
+// instead (agent-scope stores, drained before the ticket) and the last arrival sums them in item
+// order with agent-scope loads, so the fp32 sum no longer depends on arrival order.
 template <typename TZ>
 __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb) {
   __shared__ float part[4][512];
@@ -217,6 +218,9 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const float v = part[0][i] + part[1][i] + part[2][i] + part[3][i];
         if (nit == 1) grow[c0 + i] = v;
+        else if (a.heavy_slab)
+          __hip_atomic_store(a.heavy_slab + (size_t)it * a.n + c0 + i, v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         else atomicAdd(a.g + (size_t)c * a.n + c0 + i, v);
       }
       __syncthreads();
@@ -234,9 +238,19 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       }
       __syncthreads();
       if (s_last) {
-        for (int j = threadIdx.x; j < a.n; j += blockDim.x)
-          grow[j] = __hip_atomic_exchange(a.g + (size_t)c * a.n + j, 0.f, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+        if (a.heavy_slab) {
+          const float* sl = a.heavy_slab + (size_t)(it - item.y) * a.n;
+          for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
+            float acc = 0.f;
+            for (int k = 0; k < nit; ++k)
+              acc += __hip_atomic_load(sl + (size_t)k * a.n + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            grow[j] = acc;
+          }
+        } else {
+          for (int j = threadIdx.x; j < a.n; j += blockDim.x)
+            grow[j] = __hip_atomic_exchange(a.g + (size_t)c * a.n + j, 0.f, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
         w1_row_from(a, c, grow, alpha);
       }
@@ -251,50 +265,20 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
 // only needs every other block to have READ them, which precedes their arrival) advances them
 // (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
 // the ticket.
-#ifdef DSSM_ADAM_WPE  // diagnostics builds: a minimum occupancy (waves per SIMD) for the step kernel
-#define DSSM_ADAM_ATTR __attribute__((amdgpu_waves_per_eu(DSSM_ADAM_WPE)))
-#else
-#define DSSM_ADAM_ATTR
-#endif
 template <typename TZ>
-__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
+__global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  // Block roles.  Dispatch is in block order: the heavy-item blocks (the longest dependent
-  // chains) come first; the W1-row gather blocks and the flat/dense streaming blocks follow,
-  // either contiguous (interleave == 0) or interleaved in proportion (Bresenham over the block
-  // index) so every CU runs latency-bound gathers beside HBM streaming from the start.
-  const int64_t nb = gridDim.x, b0 = blockIdx.x;
+  // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
+  // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
+  // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
+  const int b0 = blockIdx.x;
   const int nh = a.item_blocks, nw = a.w1_blocks;
-  const int nf = (int)nb - nh - nw;
-  bool is_heavy = b0 < nh;
-  int hcount = (int)(is_heavy ? b0 : nh);
-  int64_t j = b0 - hcount;  // index among the other roles
-  const int64_t nwf = nw + nf;
-  int wcount;
-  bool is_w1;
-  if (a.interleave >= 2) {
-    // 2: heavy items, flat/dense streaming, W1 rows; 3: flat/dense, heavy items, W1 rows
-    const int64_t f0 = a.interleave == 2 ? nh : 0, h0 = a.interleave == 2 ? 0 : nf;
-    const int64_t w0 = (int64_t)nh + nf;
-    is_heavy = b0 >= h0 && b0 < h0 + nh;
-    hcount = (int)(b0 - h0);
-    is_w1 = b0 >= w0;
-    wcount = (int)(b0 - w0);
-    j = (b0 - f0) + nw;  // flat/dense index = j - wcount below
-    if (!is_heavy && !is_w1) wcount = nw;
-  } else if (a.interleave) {
-    wcount = nwf ? (int)(j * nw / nwf) : 0;
-    is_w1 = !is_heavy && nwf && (j + 1) * nw / nwf > wcount;
-  } else {
-    is_w1 = !is_heavy && j < nw;
-    wcount = (int)(j < nw ? j : nw);
-  }
-  if (is_heavy) {
-    heavy_items<TZ>(a, alpha, hcount);
-  } else if (is_w1) {
-    const int b = wcount;
+  if (b0 < nh) {
+    heavy_items<TZ>(a, alpha, b0);
+  } else if (b0 < nh + nw) {
+    const int b = b0 - nh;
     // the next row's column range is loaded while this row is processed (one dependent load
     // fewer on each row's chain)
     const int stride = a.w1_blocks * 4;
@@ -316,7 +300,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       e = en;
     }
   } else {
-    const int bi = (int)(j - wcount);
+    const int bi = b0 - nh - nw;
     if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
       const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
       for (int64_t i = (int64_t)bi * blockDim.x + threadIdx.x; i < w4;
@@ -387,24 +371,9 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       if (u == ntop - 1) {
         a.st[0] = b1p * a.beta1;
         a.st[1] = b2p * a.beta2;
-        // every block has read this step's heavy-item count: re-arm it for the next step's scan
-        // (the next step's rank launch may already be running beside this one)
-        if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-  }
-}
-
-__global__ void k_noop() {}
-
-// beta1_power *= beta1; beta2_power *= beta2 (TF1.x AdamOptimizer._finish, fp32): the separate-
-// launch variant (A/B knob DSSM_ADAM_SEP_ADVANCE=1)
-__global__ void k_adam_advance(float* __restrict__ st, float beta1, float beta2, int* heavy_reset) {
-  if (threadIdx.x == 0) {
-    st[0] = st[0] * beta1;
-    st[1] = st[1] * beta2;
-    if (heavy_reset) *heavy_reset = 0;
   }
 }
 
@@ -468,32 +437,14 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if ((a.d4_begin < 0) || (a.d4_end < a.d4_begin)) return hipErrorInvalidValue;
   a.b1c = 1.0f - a.beta1;
   a.b2c = 1.0f - a.beta2;
-  static const int w1_cap = [] {
-    const char* e = std::getenv("DSSM_ADAM_W1_BLOCKS");
-    return e ? std::atoi(e) : kAdamW1Blocks;
-  }();
-  static const bool sep_advance = [] {
-    const char* e = std::getenv("DSSM_ADAM_SEP_ADVANCE");
-    return e && e[0] == '1';
-  }();
-  if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), w1_cap);
-  if (sep_advance || a.gout) a.ticket = nullptr;  // the gradient pass advances nothing
-  static const bool w1_flat_on = [] {
-    const char* e = std::getenv("DSSM_ADAM_W1_FLAT");
-    return !(e && e[0] == '0');
-  }();
-  static const int item_cap = [] {
-    const char* e = std::getenv("DSSM_ADAM_ITEM_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : kAdamItemBlocks;
-  }();
-  static const int interleave = [] {
-    const char* e = std::getenv("DSSM_ADAM_INTERLEAVE");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.interleave = interleave;
+  // 2048 W1-row gather blocks: measured against 1024 / 4096 (+2-4 us each)
+  if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), kAdamW1Blocks);
+  if (a.gout) a.ticket = nullptr;  // the gradient pass advances nothing
+  if (!a.ticket && !a.gout) return hipErrorInvalidValue;  // the step must advance the beta powers
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
-  else a.item_blocks = std::min(a.item_blocks, item_cap);
-  a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && w1_flat_on && (a.n % 4) == 0 && !a.flat_elsewhere) ? 1 : 0;
+  else a.item_blocks = std::min(a.item_blocks, kAdamItemBlocks);
+  // rows with no entry this step stream through the flat role instead of a wave per row
+  a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && (a.n % 4) == 0) ? 1 : 0;
   if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) +
                      (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
@@ -503,13 +454,6 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
-  static const bool gap_probe = [] {  // diagnostics: an empty launch after the step kernel
-    const char* e = std::getenv("DSSM_GAP_PROBE");
-    return e && e[0] == '1';
-  }();
-  if (gap_probe) hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
-  if (!a.ticket && !a.gout)
-    hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, s, a.st, a.beta1, a.beta2, a.heavy_reset);
   return hipGetLastError();
 }
 

@@ -60,11 +60,11 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
                                                   unsigned* __restrict__ tickets,
                                                   float* __restrict__ batch_mean,
                                                   float* __restrict__ batch_var,
-                                                  float* __restrict__ coef, int phase,
+                                                  float* __restrict__ coef,
                                                   double* __restrict__ zero, int nzero) {
-  // phase 0: partials + last-block finalize; 1: partials only; 2: finalize only (own launch)
+  // partials, then the last block to arrive finalizes
   // zero: fused-statistics accumulators of this step's later layers (bnfuse.h), cleared here
-  if (phase != 2 && zero) {
+  if (zero) {
     const int nb = gridDim.x * gridDim.y;
     for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * 1024 + threadIdx.x; i < nzero; i += nb * 1024)
       zero[i] = 0.0;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
   const int rb = blockIdx.y;
   const RowBlocks blk(tw);
   const size_t plane = (size_t)2 * ldz;
-  if (train && phase != 2) {
+  if (train) {
     int r0, r1, tower;
     blk.range(tw, rb, r0, r1, tower);
     float x[RPT];
@@ -117,7 +117,6 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
       part[((size_t)rb * 2) * ldz + c] = mu;
       part[((size_t)rb * 2 + 1) * ldz + c] = M2;
     }
-    if (phase == 1) return;
     if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
   } else if (rb != 0) {
     return;  // eval: one block per column chunk just builds the coefficients from the EMA
@@ -303,7 +302,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
                                                       const float* __restrict__ coef, BnGrads G,
                                                       float* __restrict__ part,
                                                       unsigned* __restrict__ tickets,
-                                                      float* __restrict__ bcoef, int phase) {
+                                                      float* __restrict__ bcoef) {
   __shared__ float s_a[NG][64], s_b[NG][64];
   __shared__ int s_flag;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -311,7 +310,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
   const int rb = blockIdx.y;
   const RowBlocks blk(tw);
   const size_t plane = (size_t)2 * ldz;
-  if (phase != 2) {
+  {
     int r0, r1, tower;
     blk.range(tw, rb, r0, r1, tower);
     float zz[RPT], dd[RPT];
@@ -345,8 +344,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
       part[((size_t)rb * 2 + 1) * ldz + c] = t2;
     }
   }
-  if (phase == 1) return;
-  if (phase == 0 && !last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
+  if (!last_block_arrival(&tickets[blockIdx.x], (unsigned)gridDim.y, &s_flag)) return;
   for (int tower = 0; tower < 2; ++tower) {
     const int first = tower == 0 ? 0 : blk.nq;
     const int count = tower == 0 ? blk.nq : blk.nd;
@@ -440,7 +438,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
                                                          const float* __restrict__ loss_part,
                                                          int loss_blocks,
                                                          float* __restrict__ loss_out,
-                                                         FlatSlice flat, int nwork, TnParams dw,
+                                                         int nwork, TnParams dw,
                                                          int dw_x, int dw_y, int dw_blocks) {
   __shared__ __attribute__((aligned(16))) float smem[kApplySmemFloats];
   // blocks [0, dw_blocks): the previous backward pair's dW split-K tiles (the longest chains,
@@ -457,12 +455,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   // partials (deferred finalize: no cross-workgroup ticket in the cosine launch) and dgamma /
   // dbeta, off the element blocks' critical path
   if (bid >= nwork) {
-    if (bid == nwork) {
-      if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
-      fs_materialize_bwd(b);
-    } else {
-      flat_untouched(flat, bid - nwork - 1);  // untouched W1 rows (flat.h)
-    }
+    if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
+    fs_materialize_bwd(b);
     return;
   }
   float (*sc)[6][kApplyMaxLd] = reinterpret_cast<float (*)[6][kApplyMaxLd]>(smem);  // mu rstd inv shift m1 m2
@@ -553,24 +547,17 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean, float* batch_var, float* partial,
-                               unsigned* tickets, float* coef, bool split, hipStream_t s,
-                               double* zero, int nzero) {
+                               unsigned* tickets, float* coef, hipStream_t s, double* zero,
+                               int nzero) {
   RowBlocks b(t);
   BnParams P;
   P.gamma[0] = gamma_q; P.gamma[1] = gamma_d;
   P.beta[0] = beta_q; P.beta[1] = beta_d;
   P.ema_mean[0] = ema_q_mean; P.ema_mean[1] = ema_d_mean;
   P.ema_var[0] = ema_q_var; P.ema_var[1] = ema_d_var;
-  if (split && train) {
-    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t,
-                       P, eps, decay, 1, partial, tickets, batch_mean, batch_var, coef, 1, zero, nzero);
-    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), 1), dim3(1024), 0, s, Z, ldz, n, t, P, eps,
-                       decay, 1, partial, tickets, batch_mean, batch_var, coef, 2, nullptr, 0);
-  } else {
-    hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s,
-                       Z, ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean,
-                       batch_var, coef, 0, zero, nzero);
-  }
+  hipLaunchKernelGGL(k_bn_stats, dim3(cdiv(ldz, 64), train ? b.total() : 1), dim3(1024), 0, s, Z,
+                     ldz, n, t, P, eps, decay, train ? 1 : 0, partial, tickets, batch_mean, batch_var,
+                     coef, zero, nzero);
   return hipGetLastError();
 }
 
@@ -590,20 +577,13 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, bool split, hipStream_t s) {
+                         void* dZ, bool dz_bf16, hipStream_t s) {
   RowBlocks b(t);
   BnGrads G;
   G.dgamma[0] = dgamma_q; G.dgamma[1] = dgamma_d;
   G.dbeta[0] = dbeta_q; G.dbeta[1] = dbeta_d;
-  if (split) {
-    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA,
-                       ldz, n, t, coef, G, partial, tickets, bcoef, 1);
-    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), 1), dim3(1024), 0, s, Z, dA, ldz, n, t,
-                       coef, G, partial, tickets, bcoef, 2);
-  } else {
-    hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA,
-                       ldz, n, t, coef, G, partial, tickets, bcoef, 0);
-  }
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA, ldz,
+                     n, t, coef, G, partial, tickets, bcoef);
   const int grid = ew_grid((size_t)t.rows * (ldz / 4));
   if (dz_bf16)
     hipLaunchKernelGGL(k_bn_bwd_apply<u16>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,
@@ -622,25 +602,16 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part, int loss_blocks,
-                                     float* loss_out,
-                                     const FlatSlice* flat, const TnParams* dw) {
+                                     float* loss_out, const TnParams* dw) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
-  static const int gmax = [] {
-    const char* e = std::getenv("DSSM_APPLY_GRID");
-    return e ? std::max(1, std::atoi(e)) : 1024;
-  }();
-  static const int gmax_dw = [] {  // element blocks beside hosted dW tiles
-    const char* e = std::getenv("DSSM_APPLY_GRID_DW");
-    return e ? std::max(1, std::atoi(e)) : 512;
-  }();
-  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? gmax_dw : gmax);
-  const FlatSlice fl = flat ? *flat : FlatSlice{};
+  // element workgroups: fewer beside hosted dW tiles, which share the CUs
+  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? 512 : 1024);
   if (dw && dw->k_per_split > 3 * 128) return hipErrorInvalidValue;  // tn_chunk_body<3>
   const TnParams p = dw ? *dw : TnParams{};
   const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
   const int dw_blocks = dw ? dw_x * dw_y * cdiv(p.K, p.k_per_split) : 0;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1 + fl.nblocks), dim3(256), 0, s, Z, dA,
-                     b, (u16*)dZ, loss_part, loss_blocks, loss_out, fl, grid, p, dw_x, dw_y, dw_blocks);
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, dA, b,
+                     (u16*)dZ, loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks);
   return hipGetLastError();
 }
 

@@ -15,9 +15,8 @@
 // The sums are fp64 accumulations of fp32 values: the result does not depend on the atomic
 // order beyond fp64 rounding, far below the fp32 outputs' resolution.  They are zeroed by the
 // first launch of the next train step (the CSC histogram, spmm.hip).  Same-address fp64 atomics
-// serialise (measured on MI355X: ~23 ns each; tools/micro/atomics.hip), so producers with many
-// workgroups spread their sums over fcopies / bcopies replicas (workgroup index mod copies)
-// that the consumers add up.
+// serialise (measured on MI355X: ~23 ns each; tools/micro/atomics.hip): producers keep the chains
+// short by summing many rows per workgroup before their one atomic per (statistic, column).
 #pragma once
 #include "common.h"
 
@@ -34,15 +33,11 @@ struct BnSide {
   float* coef;      // [4][2][ld]: mean, rstd, inv = gamma*rstd, shift = beta - mean*inv
   float* bmean;     // [2][n] batch moments (train)
   float* bvar;
-  double* fsum;     // fcopies x [2 towers][2][ld]: sum z, sum z^2 (replicas summed by consumers)
-  int fcopies;
-  double* bsum;     // bcopies x [2 towers][2][ld]: sum dy, sum dy*xhat
-  int bcopies;
+  double* fsum;     // [2 towers][2][ld]: sum z, sum z^2
+  double* bsum;     // [2 towers][2][ld]: sum dy, sum dy*xhat
   float* dgamma[2];
   float* dbeta[2];
 };
-
-constexpr int kMaxSumCopies = 8;  // replicas of an accumulator (producers spread their atomics)
 
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -64,16 +59,12 @@ __device__ __forceinline__ void fs_coef_from(const BnSide& b, int t, int c, doub
 }
 __device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu, float& var,
                                         float& rstd, float& inv, float& shift) {
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < b.fcopies; ++k) {
-    s += b.fsum[(size_t)k * 4 * b.ld + (t * 2) * b.ld + c];
-    q += b.fsum[(size_t)k * 4 * b.ld + (t * 2 + 1) * b.ld + c];
-  }
+  const double s = b.fsum[(t * 2) * b.ld + c], q = b.fsum[(t * 2 + 1) * b.ld + c];
   fs_coef_from(b, t, c, s, q, mu, var, rstd, inv, shift);
 }
 
 // Every thread of the workgroup derives the coefficients of items i = tid + nthreads*u
-// (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all replica loads in flight at once:
+// (u < NPER, i < 2*ld; tower i / ld, column i % ld) with all loads in flight at once:
 // load() issues the loads (call it before a kernel's bulk loads so these return first),
 // finish() calls out(tower, column, mu, rstd, inv, shift) (zeros for pad columns >= n).
 template <int NPER>
@@ -89,20 +80,13 @@ struct FsCoefStage {
       const int t = ic / b.ld, c = ic - t * b.ld;
       const int cn = c < b.n ? c : 0;
       off[u] = (t * 2) * b.ld + c;
-      s[u] = q[u] = 0.0;
       gm[u] = b.gamma[t][cn];
       bt[u] = b.beta[t][cn];
     }
 #pragma unroll
-    for (int k = 0; k < kMaxSumCopies; ++k) {
-      if (k < b.fcopies) {  // uniform
-        const double* base = b.fsum + (size_t)k * 4 * b.ld;
-#pragma unroll
-        for (int u = 0; u < NPER; ++u) {
-          s[u] += base[off[u]];
-          q[u] += base[off[u] + b.ld];
-        }
-      }
+    for (int u = 0; u < NPER; ++u) {
+      s[u] = b.fsum[off[u]];
+      q[u] = b.fsum[off[u] + b.ld];
     }
   }
   template <typename F>
@@ -217,14 +201,8 @@ __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
 
 // Backward means of column c, tower t: m1 = mean(dy), m2 = mean(dy*xhat).
 __device__ __forceinline__ void fs_bsums(const BnSide& b, int t, int c, double& s1, double& s2) {
-  s1 = s2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < kMaxSumCopies; ++k) {
-    if (k < b.bcopies) {  // uniform
-      s1 += b.bsum[(size_t)k * 4 * b.ld + (t * 2) * b.ld + c];
-      s2 += b.bsum[(size_t)k * 4 * b.ld + (t * 2 + 1) * b.ld + c];
-    }
-  }
+  s1 = b.bsum[(t * 2) * b.ld + c];
+  s2 = b.bsum[(t * 2 + 1) * b.ld + c];
 }
 __device__ __forceinline__ void fs_dcoef(const BnSide& b, int t, int c, float& m1, float& m2) {
   const double N = t == 0 ? b.rows_q : b.rows_d;

@@ -44,15 +44,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int split, BnSide fs, unsigned long long* tmp, FlatSlice flat,
-    CscScatter scat) {
-  unsigned long long* tm = (tmp && threadIdx.x == 0 && blockIdx.x == 1) ? tmp : nullptr;
-  int ti = 0;
-  auto stamp = [&]() {
-    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
-    ++ti;
-  };
-  stamp();
+    float* __restrict__ dy, int defer, BnSide fs, CscScatter scat) {
   constexpr int NT = 64 * NW;
   __shared__ float s_part[2][NW];
   __shared__ int s_flag;
@@ -85,8 +77,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
       const int xb = (int)blockIdx.x - nrow_blocks - 1;
       if (xb < 0) fs_materialize_fwd(fs);
-      else if (xb < flat.nblocks) flat_untouched(flat, xb);  // untouched W1 rows (flat.h)
-      else csc_scatter_role(scat, xb - flat.nblocks);     // the CSC transpose's scatter (csc.h)
+      else csc_scatter_role(scat, xb);  // the CSC transpose's scatter (csc.h)
       return;
     }
     fs_coef_stage<(2 * kCosMaxN + NT - 1) / NT>(fs, threadIdx.x, NT,
@@ -98,14 +89,11 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     });
     __syncthreads();
   }
-  stamp();
   float lj = 0.f, cj = 0.f;
   float bq1[EPL], bq2[EPL], bd1[EPL], bd2[EPL];  // FSC: this wave's backward sums per column
 #pragma unroll
   for (int e = 0; e < EPL; ++e) bq1[e] = bq2[e] = bd1[e] = bd2[e] = 0.f;
   if (j < bs) {
-    if (tm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
     if constexpr (FSC) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
@@ -203,7 +191,6 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     if (lane == 0) qnorm[j] = qn;
     lj = -logf(p[0]);
     cj = (amax == 0) ? 1.f : 0.f;
-    stamp();
     // ---- backward: d loss / d cos_sim[j,k] = (p_k - [k==0]) / BS (skipped without dy: eval)
     if (FSC || dy != nullptr) {
     float dq[EPL];
@@ -263,10 +250,9 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       double acc = 0.0;
 #pragma unroll
       for (int w = 0; w < NW; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
-      atomic_add_f64(fs.bsum + (size_t)(blockIdx.x % fs.bcopies) * 4 * ld + (size_t)st * ld + c, acc);
+      atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
     }
   }
-  stamp();
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block
   if (lane == 0) {
     s_part[0][wv] = lj;
@@ -283,11 +269,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     part[2 * blockIdx.x] = a;
     part[2 * blockIdx.x + 1] = b;
   }
-  if (tm) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
-  }
-  if (split) return;  // k_loss_finalize sums the partials in its own launch
+  if (defer) return;  // a later launch sums the partials (the backward's first, or k_loss_finalize)
   if (!last_block_arrival(ticket, nrow_blocks, &s_flag)) return;
   loss_finalize(part, nrow_blocks, bs, loss_out);
 }
@@ -304,31 +286,29 @@ size_t cosine_ws_floats(int bs) { return (size_t)2 * cdiv(bs, 4) + 64; }
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              unsigned long long* timing,
-                              const FlatSlice* flat, const CscScatter* scatter) {
+                              hipStream_t s, const BnSide* fused, bool defer_finalize,
+                              const CscScatter* scatter) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
   // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
   const int nw = cosine_waves(n, fused != nullptr);
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
   unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * cdiv(bs, 4) + 32);  // past either layout
-  const FlatSlice fl = (flat && fused) ? *flat : FlatSlice{};
   CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
   if (sc.nblocks) sc.nblocks = std::max(1, sc.nblocks * 4 / nw);  // sized in 4-wave workgroups
   if (scatter && !fused) return hipErrorInvalidValue;  // the role rides on the fused kernel only
-  // fused: + materialising, flat and scatter blocks
-  dim3 grid(blocks + (fused ? 1 : 0) + fl.nblocks + sc.nblocks), block(64 * nw);
+  // fused: + materialising and scatter blocks
+  dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
                        gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,   \
-                       (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc);                      \
+                       defer_finalize ? 1 : 0, fs, sc);                      \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
                        coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,        \
-                       (split || defer_finalize) ? 1 : 0, fs, timing, fl, sc)
+                       defer_finalize ? 1 : 0, fs, sc)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -340,8 +320,6 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #undef DSSM_COS
 #undef DSSM_COS2
 #undef DSSM_COS3
-  if (split && !defer_finalize)
-    hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
   return hipGetLastError();
 }
 

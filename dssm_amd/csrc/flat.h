@@ -1,10 +1,9 @@
 // The decay-only Adam update of W1's untouched rows (TF1.x ApplyAdam is dense,
-// so a row with no CSC entry this step still gets m, v decayed and p moved with g = 0).  Those
-// rows are read by nobody else during the step (the SpMM gathers present columns only), so the
-// update can ride as extra workgroups in the step's latency-bound launches that leave CUs and HBM
-// idle (the last NT GEMM, the cosine kernel, the first BN-backward apply) instead of in the Adam
-// launch; it needs only the batch's column pointers (k_csc_scan) and the step's beta powers, which
-// the Adam launch advances at its end.
+// so a row with no CSC entry this step still gets m, v decayed and p moved with g = 0): the Adam
+// launch's flat streaming role (adam.hip), every lane busy instead of a wave per row.  It needs only
+// the batch's column pointers and the step's beta powers.  (Spreading it as extra workgroups over
+// the step's latency-bound launches was measured slower: the host launches grew by more than the
+// Adam launch shrank, 205 -> 211 us/step.)
 #pragma once
 #include "common.h"
 

@@ -268,11 +268,9 @@ struct NtParams {
 struct NtFuse {
   int in_from_sums;  // BN_A: derive the A operand's coefficients from `in`'s sums
   BnSide in;
-  double* out_sum;   // out_copies x [2 towers][2][ldc] (tile index mod out_copies)
-  int out_copies;
+  double* out_sum;   // [2 towers][2][ldc]
   const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
-  unsigned long long* tm;  // optional phase stamps (diagnostics: DSSM_NT_TIMING=1)
   int lds_epi;             // whole-K tiles: C staged through LDS, stored as 16-B row segments
 };
 
@@ -460,7 +458,7 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
       for (int j = 0; j < 2; ++j) {
         const int c = wn * 32 + j * 16 + lane, n = bn + c;
         if (n < N) {
-          double* os = f.out_sum + (size_t)(ty % f.out_copies) * 4 * ldc;
+          double* os = f.out_sum;
           atomic_add_f64(os + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
           atomic_add_f64(os + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
         }
@@ -512,13 +510,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const int wm = w >> 1, wn = w & 1;
   const int bm = ty * 128, bn = tx * 64;
   const int tower = bm < a.row_split ? 0 : 1;
-  unsigned long long* tm = (f.tm && t == 0 && tx == 1 && ty == 1) ? f.tm : nullptr;
-  int ti = 0;
-  auto stamp = [&]() {
-    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
-    ++ti;
-  };
-  stamp();
   // the A operand's BN coefficient inputs (sums, gamma, beta) first: they return ahead of the
   // tile's bulk loads
   constexpr int NPC = (2 * kWkMaxK + 511) / 512;
@@ -573,7 +564,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         }
     }
   }
-  stamp();
   // ---- BN coefficients of the A operand (from the sums or the materialised coefficients)
   if constexpr (BN_A) {
     if (FS == 1 && f.in_from_sums) {
@@ -599,7 +589,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     }
     __syncthreads();
   }
-  stamp();
   // ---- LDS images (bf16); out-of-range groups zeroed here, after every load was issued
   const bool write_a = BN_A && a.a_out != nullptr && tx == 0;
   {
@@ -639,7 +628,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     }
   }
   __syncthreads();
-  stamp();
   // ---- MFMA over the whole K (fragments of the next k-step read ahead of this step's MFMAs)
   f32x4 acc[2][2];
 #pragma unroll
@@ -670,8 +658,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 #pragma unroll
     for (int j = 0; j < 2; ++j) bfr[j] = bnx[j];
   }
-  if (tm) { asm volatile("s_nop 0" :: "v"(acc[0][0][0]), "v"(acc[1][1][3])); }
-  stamp();
   // ---- epilogue
   // lds_epi: the tile's values go to LDS (the A panel's space, free once every wave is past its
   // last MFMA) and leave as 16-B row segments (full 256-B rows) instead of the accumulator
@@ -732,7 +718,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       if (n < N) {
         const double v = sRed[(0 * 64 + c) * 2 + st] + sRed[(1 * 64 + c) * 2 + st] +
                          sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
-        atomic_add_f64(f.out_sum + (size_t)(ty % f.out_copies) * 4 * ldc + (size_t)(tower * 2 + st) * ldc + n, v);
+        atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
       }
     }
   }
@@ -746,10 +732,6 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) =
             *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
     }
-  }
-  if (tm) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
   }
 }
 
@@ -765,14 +747,11 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
 // A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
 // EMA update) off the tiles' critical path.
 template <bool BN_A, int FS>
-__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles,
-                                                    FlatSlice flat) {
+__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
   WG_TL(a.N == 300 ? 0 : 1, 0);
   if ((int)blockIdx.x >= ntiles) {
-    const bool mat = BN_A && FS == 1 && f.in_from_sums;
-    if (mat && (int)blockIdx.x == ntiles) fs_materialize_fwd(f.in);
-    else flat_untouched(flat, (int)blockIdx.x - ntiles - (mat ? 1 : 0));
+    if (BN_A && FS == 1 && f.in_from_sums) fs_materialize_fwd(f.in);
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);
@@ -808,17 +787,9 @@ __device__ __forceinline__ bf16x8 tr_frag_s(const u16* tile, int ld, int row0, i
   return __builtin_bit_cast(bf16x8, r);
 }
 
-__device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, int tz, u16* smem,
-                                           unsigned long long* tmp = nullptr) {
+__device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, int tz, u16* smem) {
   const int M = p.M, N = p.N, lda = p.lda, ldb = p.ldb;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  unsigned long long* tm = (tmp && t == 0 && tx == 1 && ty == 1 && tz == 1) ? tmp : nullptr;
-  int ti = 0;
-  auto stamp = [&]() {
-    if (tm && ti < 16) tm[ti] = __builtin_amdgcn_s_memrealtime();
-    ++ti;
-  };
-  stamp();
   const int wm = w >> 1, wn = w & 1;
   const int bm = ty * 128, bn = tx * 64;
   const int kbeg = tz * p.k_per_split;
@@ -843,7 +814,6 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
     const bool ok = k < kend && bnn < ldb;
     rb[i] = *reinterpret_cast<const uint4*>(p.B + (ok ? (size_t)k * ldb + bnn : 0));
   }
-  stamp();
   // stage; the group holding m == Mload gets the virtual ones column, m > Mload zeros
   const bool aedge = am + 8 > Mload;
 #pragma unroll
@@ -870,14 +840,12 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
         (k < kend && bnn < ldb) ? rb[i] : make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
-  stamp();
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kc = min(kTwKc, ((kend - kbeg) + 31) & ~31);
-  if (tm) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   for (int ks = 0; ks < kc; ks += 32) {
     bf16x8 af[2], bfr[2];
 #pragma unroll
@@ -890,8 +858,6 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
-  if (tm) { asm volatile("s_nop 0" :: "v"(acc[0][0][0]), "v"(acc[1][1][3])); }
-  stamp();
   float* out = p.C + (size_t)tz * M * p.ldc;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -904,10 +870,6 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
         if (m < M && n < N) out[(size_t)m * p.ldc + n] = acc[i][j][r];
       }
     }
-  }
-  if (tm) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
   }
 }
 
@@ -924,7 +886,7 @@ __global__ __launch_bounds__(512) void k_bwd_pair_wk(NtParams a, NtFuse f, int n
     // XCD grouping of the dW tiles needs the dA range to end on a multiple of 8
     const int nr = (int)gridDim.x - nt_blocks;
     const int r = (nt_blocks % 8) ? b - nt_blocks : xcd_tile(b - nt_blocks, nr);
-    tn_wk_body(p, r % tn_x, (r / tn_x) % tn_y, r / (tn_x * tn_y), pw_smem, f.tm ? f.tm - 128 + 64 : nullptr);
+    tn_wk_body(p, r % tn_x, (r / tn_x) % tn_y, r / (tn_x * tn_y), pw_smem);
   }
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1042,12 +1004,9 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, int out_copies, hipStream_t s,
-                                    unsigned long long* timing,
-                                    const FlatSlice* flat) {
+                                    double* out_sum, hipStream_t s) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
-  dim3 grid(cdiv(ldc, 64), cdiv(M, 64)), block(256);
   const NtParams a{M, N, K, Z, lda, coef, row_split, (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out};
   NtFuse f{};
   if (in_from_sums) {
@@ -1055,26 +1014,15 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     f.in = *in_from_sums;
   }
   f.out_sum = out_sum;
-  f.out_copies = out_copies;
-  f.tm = timing;
-  static const int lds_epi = [] {
-    const char* e = std::getenv("DSSM_NT_LDS_EPI");
-    return e ? std::atoi(e) : 1;  // measured: 14.4 (on) vs 16.2 us (off) per NT launch
-  }();
-  f.lds_epi = lds_epi;
-  static const bool wk_on = [] {
-    const char* e = std::getenv("DSSM_NT_WHOLEK");
-    return !(e && e[0] == '0');
-  }();
-  if (wk_on && K <= kWkMaxK && (row_split % 128) == 0) {
+  f.lds_epi = 1;  // measured: 14.4 (LDS-staged epilogue) vs 16.2 us per NT launch
+  if (K <= kWkMaxK && (row_split % 128) == 0) {
     const int Kp = (K + 31) & ~31;
     const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 128);
-    const FlatSlice fl = flat ? *flat : FlatSlice{};
-    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0) + fl.nblocks),
-                       dim3(512), wk_smem_bytes(Kp, f.lds_epi), s, a, f, nx, ntiles, fl);
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0)),
+                       dim3(512), wk_smem_bytes(Kp, f.lds_epi), s, a, f, nx, ntiles);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((k_gemm_nt<true, 1>), grid, block, 0, s, a, f);
+  hipLaunchKernelGGL((k_gemm_nt<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 64)), dim3(256), 0, s, a, f);
   return hipGetLastError();
 }
 
@@ -1086,29 +1034,19 @@ hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float*
 
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
-                           double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
-                           int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits, unsigned long long* timing, TnParams* dw_out) {
+                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
+                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
+                           TnParams* dw_out) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
   const NtParams a{M, kin, n, dZ, lddz, nullptr, row_split, W, ldw, dA, ldda, nullptr, nullptr};
   NtFuse f{};
   f.out_sum = bsum_prev;
-  f.out_copies = bsum_copies;
-  f.tm = timing;
   f.zb = z_prev;
   f.coefb = coef_prev;
-  static const int pair_lds_epi = [] {
-    const char* e = std::getenv("DSSM_PAIR_LDS_EPI");
-    return e ? std::atoi(e) : 0;  // measured: 18.1 (off) vs 18.3 us (on) per pair launch
-  }();
-  f.lds_epi = pair_lds_epi;
-  static const bool wk_pair = [] {
-    const char* e = std::getenv("DSSM_PAIR_WHOLEK");
-    return !(e && e[0] == '0');
-  }();
-  if (wk_pair && n <= kWkMaxK && (row_split % 128) == 0 && lda_prev >= kin) {
+  f.lds_epi = 0;  // measured: 18.1 (register epilogue) vs 18.3 us (LDS-staged) per pair launch
+  if (n <= kWkMaxK && (row_split % 128) == 0 && lda_prev >= kin) {
     const int Kp = (n + 31) & ~31;
     const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 128);
     const int Mw = kin + 1;
@@ -1150,17 +1088,8 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kps};
   const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
   const int tn_blocks = tn_x * tn_y * nsplit;
-  static const bool split_pair = [] {  // diagnostics: the two GEMMs as separate launches
-    const char* e = std::getenv("DSSM_PAIR_SPLIT");
-    return e && e[0] == '1';
-  }();
-  if (split_pair) {
-    hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks), dim3(256), 0, s, a, f, nt_x, nt_blocks, p, tn_x, tn_y);
-    hipLaunchKernelGGL(k_gemm_tn, dim3(tn_x, tn_y, nsplit), dim3(256), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
-                       nt_blocks, p, tn_x, tn_y);
-  }
+  hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
+                     nt_blocks, p, tn_x, tn_y);
   *deferred_splits = 0;
   if (nsplit > 1) {
     if (defer) {

@@ -3,16 +3,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "flat.h"
 
 namespace dssm {
 
 struct BnSide;    // bnfuse.h
 struct TnParams;  // tn.h
 struct CscScatter;  // csc.h
-
-// split=true: cross-block finalize steps run as their own small launch instead of inside the
-// producing kernel behind an agent-scope release/acquire ticket.
 
 // Eval-mode (on_train=False) BN coefficients of every layer from the EMA shadows
 // (new_dssm.py:85-86): they depend on the parameters only, not on the batch, so the forward
@@ -50,7 +46,9 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero = nullptr,
                             int nzero = 0, bool rank_path = true, bool rank_only = false,
-                            bool reset_heavy = true);
+                            int* sort_row = nullptr, float* sort_val = nullptr);
+// sort_row / sort_val (deterministic mode; capacity as csc_row / csc_val, not with rank_only):
+// scratch for the scatter, whose output every column then gets in row order.
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
@@ -63,18 +61,15 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
                                CscScatter* scatter_out = nullptr);
 // scatter_out: the launch runs the BN1 sums alone and hands the scatter to *scatter_out (a role of
 // a later launch: launch_cosine_loss).
-// FC1 forward (bf16 W1 shadow, ldz <= 512) + BN1 per-tower column sums into fsum (bnfuse.h).
-hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
-                                 int rows, const uint16_t* W, int ldw, int n, const float* bias,
-                                 float* Z, int ldz, double* fsum, int row_split, int copies,
-                                 hipStream_t s);
 // dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row
 // is written (light rows summed, heavy rows zeroed) then heavy rows accumulated with atomics;
 // light=false: only the heavy rows are accumulated (into rows that must already be zero).
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
                       bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s,
-                      int* csc_scratch = nullptr);  // non-null: heavy items of the rank transpose
+                      int* csc_scratch = nullptr,   // non-null: heavy items of the rank transpose
+                      float* heavy_slab = nullptr);  // deterministic: [items][n] partial rows
+size_t csc_heavy_cap(int rows, int max_nnz);  // heavy work items one step can list
 
 // ---- dense GEMM (gemm.hip) ----
 enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
@@ -106,17 +101,14 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, int out_copies, hipStream_t s,
-                                    unsigned long long* timing = nullptr,
-    const FlatSlice* flat = nullptr);
+                                    double* out_sum, hipStream_t s);
 // Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
 // z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
 // defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
-                           double* bsum_prev, int bsum_copies, int row_split, const uint16_t* A_prev,
-                           int lda_prev, float* slab, float* gw, bool defer, hipStream_t s,
-                           int* deferred_splits, unsigned long long* timing = nullptr,
+                           double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
+                           float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
                            TnParams* dw_out = nullptr);
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
@@ -138,8 +130,8 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* ema_q_mean, float* ema_q_var, float* ema_d_mean,
                                float* ema_d_var, float eps, float decay, bool train,
                                float* batch_mean /*[2*n] or null*/, float* batch_var,
-                               float* partial, unsigned* tickets, float* coef, bool split,
-                               hipStream_t s, double* zero = nullptr, int nzero = 0);
+                               float* partial, unsigned* tickets, float* coef, hipStream_t s,
+                               double* zero = nullptr, int nzero = 0);
 // Fused-statistics forward sums of one layer (bnfuse.h): fsum [2 towers][2][ldz] += sum z, z^2.
 hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s);
 // Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
@@ -147,7 +139,7 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part = nullptr,
                                      int loss_blocks = 0, float* loss_out = nullptr,
-    const FlatSlice* flat = nullptr, const TnParams* dw = nullptr);
+                                     const TnParams* dw = nullptr);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);
@@ -156,7 +148,7 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, bool split, hipStream_t s);
+                         void* dZ, bool dz_bf16, hipStream_t s);
 
 // ---- cosine / loss (cosine.hip) ----
 // z: last-layer activations [R x ld] fp32: pre-BN when coef != null (BN+ReLU applied on the
@@ -166,9 +158,8 @@ size_t cosine_ws_floats(int bs);
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
-                              bool split, hipStream_t s, const BnSide* fused = nullptr,
-                              bool defer_finalize = false, unsigned long long* timing = nullptr,
-    const FlatSlice* flat = nullptr, const CscScatter* scatter = nullptr);
+                              hipStream_t s, const BnSide* fused = nullptr,
+                              bool defer_finalize = false, const CscScatter* scatter = nullptr);
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 // (queries per workgroup: kCosFusedWaves for the fused-statistics kernel at widths <= 128,
 // whose per-wave LDS slots then stay small; otherwise 4)
@@ -255,12 +246,9 @@ struct AdamStep {
   uint16_t* pwire;
   int64_t wire4;
   int64_t t4_begin, t4_end;
-  // role layout after the heavy-item blocks (0: contiguous, 1: interleaved; DSSM_ADAM_INTERLEAVE)
-  int interleave;
-  // zeroed once every block has read heavy_n (the next step's rank launch does not reset it)
-  int* heavy_reset;
-  // the untouched W1 rows were updated by FlatSlice roles earlier in the step (flat.h): skip them
-  int flat_elsewhere;
+  // deterministic mode: a multi-item heavy column's items store their partial rows here ([item][n],
+  // write-through) and its last arrival sums them in item order (no fp32 atomics)
+  float* heavy_slab;
   // gradient pass (data parallel, bf16 wire): the W1 roles compute dW1 rows (inline gather, heavy
   // items, zero for untouched rows) and write them as bf16 to gout (arena layout; the bias row as
   // fp32 into g) instead of updating parameters; no dense range, no beta-power advance

@@ -13,7 +13,6 @@
 #include "../../include/dssm.h"
 #include "common.h"
 #include "bnfuse.h"
-#include "dense.h"
 #include "launch.h"
 #include "tn.h"
 #include "csc.h"
@@ -35,10 +34,6 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
-constexpr int kSumCopies = 8;   // replicas allocated per fused-statistics accumulator (bnfuse.h)
-constexpr int kNtSumCopies = 1, kPairSumCopies = 1, kCosSumCopies = 1;  // used by each producer
-constexpr int kFsum0Copies = 8;  // max replicas of layer 1's sums when the SpMM produces them
-constexpr int kDenseMaxGrid = 1024;  // workgroups of the persistent dense kernels (one per CU)
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Layout {
@@ -58,11 +53,9 @@ struct Layout {
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
   size_t dw_slab[DSSM_MAX_LAYERS] = {}, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
-  // persistent dense-stack path (dense.hip), bf16 only
-  bool dense_ok = false;
-  int dense_kmax = 0, dense_splits = 0;
-  size_t dense_sums = 0, dense_sums_bytes = 0, dense_args = 0, dense_bar = 0, loss_part = 0,
-         dense_tickets = 0, dense_timing = 0;
+  size_t sort_row, sort_val, heavy_slab;  // deterministic mode: transpose scratch, heavy partial rows
+  // fp64 accumulators of the fused BN statistics (bnfuse.h), one zeroed region
+  size_t sums = 0, sums_bytes = 0;
   size_t fsum[DSSM_MAX_LAYERS] = {}, bsum[DSSM_MAX_LAYERS] = {};
   size_t ws = 0;
   int max_nnz = 0;
@@ -145,24 +138,11 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     Lt.shadowT[l] = (Lt.bf16 && l > 0) ? take((size_t)Lt.n[l] * Lt.ldp[l - 1] * 2) : 0;
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
-  {
-    int ld[DSSM_MAX_LAYERS], n[DSSM_MAX_LAYERS];
-    for (int l = 0; l < Lt.L; ++l) ld[l] = Lt.ldp[l], n[l] = Lt.n[l];
-    Lt.dense_ok = Lt.bf16 && dssm::dense_supported(Lt.L, n, ld, Lt.BS, Lt.NEG);
-    if (Lt.dense_ok) {
-      for (int l = 0; l < Lt.L; ++l) {
-        Lt.dense_kmax = std::max(Lt.dense_kmax, Lt.ldp[l]);
-        max_part = std::max(max_part, (size_t)(Lt.R / 64) * 2 * Lt.ldp[l]);
-      }
-      Lt.dense_splits = dssm::dense_dw_splits(Lt.R);
-    }
-  }
   Lt.partial = take(max_part * 4);
   // split-K slabs of dW_l (l >= 2), one per layer: in fused mode the Adam step sums them
   for (int l = 1; l < Lt.L; ++l)
     Lt.dw_slab[l] = take(
-        std::max<size_t>({dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16),
-                          (size_t)Lt.dense_splits * (Lt.in_dim[l] + 1) * Lt.n[l], (size_t)1}) * 4);
+        std::max<size_t>(dssm::gemm_dw_slab_floats(Lt.in_dim[l] + 1, Lt.n[l], Lt.R, Lt.bf16), 1) * 4);
   const size_t K = Lt.NEG + 1;
   Lt.cos_raw = take(K * Lt.BS * 4);
   Lt.cos_sim = take(K * Lt.BS * 4);
@@ -176,30 +156,25 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.csc_row = take(ent * 4);
   Lt.csc_val = take(ent * 4);
   Lt.csc_col = take(ent * 4);
+  Lt.sort_row = take(ent * 4);
+  Lt.sort_val = take(ent * 4);
+  Lt.heavy_slab = take(dssm::csc_heavy_cap(Lt.R, Lt.max_nnz) * Lt.n[0] * 4);
   // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
   Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
   if (Lt.bf16) {
-    // fp64 statistics accumulators of the fused-statistics per-op path and the dense kernels
-    // (one contiguous region: zeroed as a whole)
+    // fp64 [2 towers][2][ld] forward and backward accumulators per layer (fused statistics), one
+    // contiguous region zeroed as a whole by the step's first launch
     size_t sums = 0;
-    // kSumCopies replicas of every accumulator (producers spread same-address atomics)
-    for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
-    Lt.dense_sums = take(sums);
-    Lt.dense_sums_bytes = sums;
-    size_t o = Lt.dense_sums;
+    for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
+    Lt.sums = take(sums);
+    Lt.sums_bytes = sums;
+    size_t o = Lt.sums;
     for (int l = 0; l < Lt.L; ++l) {
       Lt.fsum[l] = o;
-      o += (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
+      o += (size_t)4 * Lt.ldp[l] * 8;
       Lt.bsum[l] = o;
-      o += (size_t)kSumCopies * 4 * Lt.ldp[l] * 8;
+      o += (size_t)4 * Lt.ldp[l] * 8;
     }
-  }
-  if (Lt.dense_ok) {
-    Lt.dense_args = take(sizeof(dssm::DenseArgs));
-    Lt.dense_bar = take(3 * 256);
-    Lt.loss_part = take((size_t)kDenseMaxGrid * 2 * 4);
-    Lt.dense_tickets = take(2 * 256);
-    Lt.dense_timing = take(4 * 64 * 8);
   }
   Lt.ws = w;
 }
@@ -220,55 +195,26 @@ struct dssm_plan {
   // the reduce-scatter / all-gather; arena elements [0, wire_end) are W1's rows
   uint16_t* gwire = nullptr;
   uint16_t* pwire = nullptr;
-  // dW1 into the wire by the gradient pass (DSSM_WIRE_GRAD_PASS=0: materialise + pack)
-  bool wire_grad_pass = true;
   int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
-  bool fused_w1_adam = true;   // single-GPU path: dW1 light rows computed inside Adam
-  // multi-step graphs: the next step's CSC rank launch runs on the side stream beside this step's
-  // Adam (DSSM_RANK_PREFETCH=1; measured slower: the cross-stream fork / join in the graph costs
-  // more than the rank launch it hides); the forward of that batch then skips its rank launch
-  bool rank_prefetch = false;
-  // untouched W1 rows' decay-only Adam update spread over the step's latency-bound launches
-  // (flat.h) instead of the Adam launch: only inside whole steps (train_step / step graphs), where
-  // Adam is sure to follow.  DSSM_FLAT_SPREAD=0 keeps it in Adam; "a,b,c" = workgroups given to
-  // the last NT GEMM, the cosine and the first BN-backward apply launches (0 skips a launch).
-  // Opt-in (DSSM_FLAT_SPREAD=a,b,c): measured slower -- Adam loses only ~6 us (its critical path
-  // is the W1-row gathers, not the streaming) while the host launches grow by more (205 -> 211).
-  bool flat_spread = false;
-  int flat_blocks[3] = {128, 256, 512};
-  bool in_full_step = false;  // set by train_step / step-graph capture
-  bool flat_this_step = false;  // the slices were enqueued: this step's Adam skips untouched rows
-  const int32_t* rank_prefetched = nullptr;
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
-  bool csc_pending = false;
   int dw_deferred[DSSM_MAX_LAYERS] = {};  // split count of dW_l left in its slab (fused mode)
-  // persistent dense-stack kernels (bf16; DSSM_DENSE=0 selects the per-op launches)
-  bool dense_on = false;
-  int dense_grid = 0;
-  size_t dense_smem = 0;
-  // CSC build on the launch stream (default: measured faster than overlapping it on the side
-  // stream, whose join costs a cross-queue wait and whose kernels contend with the forward's);
-  // DSSM_CSC_SIDE=1 restores the overlapped side-stream schedule.
-  bool csc_inline = true;
-  // CSC transpose by rank / multi-block scan / row-parallel scatter launches (spmm.hip);
-  // DSSM_CSC_LEGACY=1 selects the histogram / single-block scan / fill launches
-  bool csc_rank_path = true;
-  bool split_finalize = false;  // DSSM_SPLIT_FINALIZE=1: finalize steps as separate launches
-  // bf16 train steps with the BN statistics fused into the producing / consuming kernels
-  // (bnfuse.h); DSSM_FUSED_STATS=0 selects the separate statistics launches
-  bool fused_stats = false;
-  // fused-statistics steps: BN1 sums accumulated by the SpMM itself (16-row workgroups, 8
-  // accumulator replicas) instead of the separate statistics launch; DSSM_SPMM_STATS=1.
-  // Measured slower on MI355X at C2 (the 16-row workgroups cost more than the launch saves).
-  bool spmm_stats = false;
-  bool scatter_in_cos = true;  // DSSM_SCATTER_IN_COS=0: the CSC scatter beside the BN1 sums
-  bool dw_in_apply = true;  // DSSM_DW_IN_APPLY=0: dW_l tiles in the backward pair launch
-  bool nt_timing = false;  // DSSM_NT_TIMING=1: layer-2 NT GEMM phase stamps (BUF_DENSE_TIMING row 3)
-  int fsum0_copies = 1;  // DSSM_FSUM_COPIES (<= kFsum0Copies)
-  hipStream_t side = nullptr;  // CSC transpose overlaps the forward pass on this stream
-  hipEvent_t ev_batch = nullptr, ev_csc = nullptr;
+  // Schedule options (dssm_plan_set_option; never read from the environment).  Each names a
+  // measured-faster default and the alternative it replaced, kept for parity tests and shapes the
+  // default does not support.  Graphs captured earlier keep the schedule they were captured with.
+  int opt[DSSM_OPT_COUNT] = {
+      1,  // FUSED_STATS: BN statistics fused into producers / consumers (where supported)
+      1,  // MERGED_CSC: the rank transpose's scan / scatter ride in the forward's launches
+      1,  // HEAVY_IN_ADAM: dW1's heavy columns as work items of the Adam launch
+      1,  // SCATTER_IN_COS: the transpose's scatter as workgroups of the cosine launch
+      1,  // DW_IN_APPLY: dW_l split-K tiles inside the next BN-backward apply launch
+      1,  // WIRE_GRAD_PASS: data parallel bf16 wire: dW1 written straight into the wire
+      1,  // CSC_RANK: rank / scan / scatter transpose (0: histogram / fill launches)
+      0,  // DETERMINISTIC: fixed-order reductions, bit-identical repeated runs
+      1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
+  };
+  bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
   struct GraphSlot {
     hipGraphExec_t exec = nullptr;
@@ -320,59 +266,6 @@ struct dssm_plan {
   }
 
   template <typename T> T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
-  dssm::DenseArgs dense_args() const {
-    dssm::DenseArgs a{};
-    a.L = Lt.L;
-    a.R = Lt.R;
-    a.BS = Lt.BS;
-    a.NEG = Lt.NEG;
-    a.gamma_cos = cfg.gamma;
-    a.eps = cfg.bn_eps;
-    a.decay = cfg.ema_decay;
-    for (int l = 0; l < Lt.L; ++l) {
-      dssm::DenseLayer& d = a.ly[l];
-      const int n = Lt.n[l];
-      d.n = n;
-      d.ld = Lt.ldp[l];
-      d.Z = at<float>(Lt.Z[l]);
-      d.A = l < Lt.L - 1 ? at<uint16_t>(Lt.A[l]) : nullptr;
-      d.Y = l == Lt.L - 1 ? at<float>(Lt.A[l]) : nullptr;
-      d.dy = at<float>(Lt.dA[l]);
-      d.dZ = at<uint16_t>(Lt.dZ[l]);
-      d.W = at<uint16_t>(Lt.shadow[l]);
-      d.WT = l > 0 ? at<uint16_t>(Lt.shadowT[l]) : nullptr;
-      d.bias = bias(l);
-      for (int t = 0; t < 2; ++t) {
-        d.gamma[t] = p + Lt.bn_off[l][2 * t];
-        d.beta[t] = p + Lt.bn_off[l][2 * t + 1];
-        d.dgamma[t] = g + Lt.bn_off[l][2 * t];
-        d.dbeta[t] = g + Lt.bn_off[l][2 * t + 1];
-        d.ema_mean[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t) * n;
-        d.ema_var[t] = ema + Lt.ema_off[l] + (int64_t)(2 * t + 1) * n;
-      }
-      d.coef = at<float>(Lt.coef[l]);
-      d.fsum = at<double>(Lt.fsum[l]);
-      d.bsum = at<double>(Lt.bsum[l]);
-      d.bmean = at<float>(Lt.bmean[l]);
-      d.bvar = at<float>(Lt.bvar[l]);
-      d.gW = g + Lt.fc_off[l];
-      d.slab = l > 0 ? at<float>(Lt.dw_slab[l]) : nullptr;
-      d.splits = Lt.dense_splits;
-    }
-    a.cos_raw = at<float>(Lt.cos_raw);
-    a.cos_sim = at<float>(Lt.cos_sim);
-    a.prob = at<float>(Lt.prob);
-    a.qnorm = at<float>(Lt.qnorm);
-    a.loss = at<float>(Lt.loss);
-    a.loss_part = at<float>(Lt.loss_part);
-    a.tickets = at<unsigned>(Lt.dense_tickets);
-    a.bar = at<unsigned>(Lt.dense_bar);
-    const char* tv = std::getenv("DSSM_DENSE_TIMING");
-    a.timing = (tv && tv[0] == '1') ? at<unsigned long long>(Lt.dense_timing) : nullptr;
-    const char* ex = std::getenv("DSSM_DENSE_EXP");
-    a.exp = ex ? std::atoi(ex) : 0;
-    return a;
-  }
   const void* weight(int l) const {  // what the kernels read for W_l
     return Lt.bf16 ? (const void*)at<u16>(Lt.shadow[l]) : (const void*)(p + Lt.fc_off[l]);
   }
@@ -401,27 +294,21 @@ struct dssm_plan {
     b.bmean = at<float>(Lt.bmean[l]);
     b.bvar = at<float>(Lt.bvar[l]);
     b.fsum = at<double>(Lt.fsum[l]);
-    b.fcopies = fcopies(l);
-    b.bcopies = bcopies(l);
     b.bsum = at<double>(Lt.bsum[l]);
     return b;
   }
-  // replicas each fused accumulator is spread over, set by its producer's workgroup count
-  int fcopies(int l) const { return l == 0 ? (spmm_stats ? fsum0_copies : 1) : copies_nt; }
-  int bcopies(int l) const { return l == Lt.L - 1 ? copies_cos : copies_pair; }
-  int copies_nt = kNtSumCopies, copies_pair = kPairSumCopies, copies_cos = kCosSumCopies;
-  // heavy dW1 columns as work items inside the Adam launch (DSSM_HEAVY_IN_ADAM=0: own launch)
-  bool heavy_adam = true;
-  // rank transpose split across the fused-statistics forward (scan beside the SpMM, scatter
-  // beside BN1's sums); DSSM_MERGE_CSC=0 keeps its three launches together
-  bool merge_csc = true;
+  bool csc_rank_path() const { return on(DSSM_OPT_CSC_RANK) && dssm::csc_rank_supported(Lt.D); }
+  bool fused_w1_adam() const { return on(DSSM_OPT_FUSED_W1_ADAM); }
+  // deterministic mode: the fixed-order statistics launches (the fused fp64 atomic sums are
+  // order-dependent at fp64 rounding), every CSC column in row order, heavy dW1 rows through slabs
+  bool deterministic() const { return on(DSSM_OPT_DETERMINISTIC); }
+  bool fused_stats() const { return on(DSSM_OPT_FUSED_STATS) && !deterministic() && fused_stats_ok(); }
   bool merged_csc() const {
-    return merge_csc && fused_stats && !dense_on && !spmm_stats && csc_inline && csc_rank_path &&
-           dssm::csc_rank_supported(Lt.D) && (Lt.BS % 128) == 0;
+    return on(DSSM_OPT_MERGED_CSC) && fused_stats() && csc_rank_path() && (Lt.BS % 128) == 0;
   }
-  bool heavy_in_adam() const { return heavy_adam && csc_rank_path && dssm::csc_rank_supported(Lt.D); }
+  bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
   bool fused_stats_ok() const {
-    if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.dense_sums_bytes) return false;
+    if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
       if (Lt.ldp[l] > 512) return false;
     for (int l = 1; l < Lt.L; ++l)
@@ -445,41 +332,6 @@ struct dssm_plan {
     return s;
   }
 };
-
-// Whether this step spreads the untouched W1 rows' Adam update (flat.h), and slice k (0: last NT
-// GEMM, 1: cosine, 2: first BN-backward apply) of the [W1; b1] block's float4 range, split in
-// proportion to the workgroups each launch gives it.
-static bool flat_spread_on(const dssm_plan* P) {
-  return P->flat_spread && P->in_full_step && P->fused_w1_adam && P->heavy_in_adam() && P->merged_csc() &&
-         P->Lt.bf16 && (P->Lt.n[0] % 4) == 0 && (P->flat_blocks[0] + P->flat_blocks[1] + P->flat_blocks[2]) > 0;
-}
-
-static dssm::FlatSlice flat_slice(const dssm_plan* P, int k) {
-  const Layout& Lt = P->Lt;
-  const dssm_config& c = P->cfg;
-  dssm::FlatSlice f{};
-  f.p = P->p;
-  f.m = P->m;
-  f.v = P->v;
-  f.shadow = P->at<uint16_t>(Lt.shadow[0]);
-  f.ldsh = Lt.ldp[0];
-  f.n = Lt.n[0];
-  f.D = Lt.D;
-  f.col_ptr = P->at<int>(Lt.col_ptr);
-  f.st = P->at<float>(Lt.adam_state);
-  f.lr = c.lr;
-  f.b1c = 1.0f - c.beta1;
-  f.b2c = 1.0f - c.beta2;
-  f.eps = c.adam_eps;
-  const int64_t w4 = (int64_t)(Lt.D + 1) * Lt.n[0] / 4;
-  const int tot = P->flat_blocks[0] + P->flat_blocks[1] + P->flat_blocks[2];
-  int before = 0;
-  for (int i = 0; i < k; ++i) before += P->flat_blocks[i];
-  f.i4_begin = w4 * before / tot;
-  f.i4_end = w4 * (before + P->flat_blocks[k]) / tot;
-  f.nblocks = P->flat_blocks[k];
-  return f;
-}
 
 namespace dssm {
 int report_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
@@ -563,70 +415,10 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
   P->m = adam_m;
   P->v = adam_v;
   P->ema = ema;
-  if (const char* e = std::getenv("DSSM_SPLIT_FINALIZE")) P->split_finalize = e[0] == '1';
-  if (const char* e = std::getenv("DSSM_CSC_SIDE")) P->csc_inline = e[0] != '1';
-  if (const char* e = std::getenv("DSSM_CSC_LEGACY")) P->csc_rank_path = e[0] != '1';
-  P->fused_stats = P->fused_stats_ok();
-  if (const char* e = std::getenv("DSSM_FUSED_STATS")) P->fused_stats = P->fused_stats && e[0] != '0';
-  if (const char* e = std::getenv("DSSM_SPMM_STATS")) P->spmm_stats = e[0] == '1';
-  if (const char* e = std::getenv("DSSM_HEAVY_IN_ADAM")) P->heavy_adam = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_MERGE_CSC")) P->merge_csc = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_SUM_COPIES")) {  // "nt,pair,cos" (each 1..kSumCopies)
-    int a = 1, b = 1, c = 1;
-    if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
-      P->copies_nt = std::max(1, std::min(kSumCopies, a));
-      P->copies_pair = std::max(1, std::min(kSumCopies, b));
-      P->copies_cos = std::max(1, std::min(kSumCopies, c));
-    }
-  }
-  if (const char* e = std::getenv("DSSM_RANK_PREFETCH")) P->rank_prefetch = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_FLAT_SPREAD")) {
-    int a = 0, b = 0, c = 0;
-    if (e[0] == '0' && e[1] == 0) P->flat_spread = false;
-    else if (std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) {
-      P->flat_spread = true;
-      P->flat_blocks[0] = std::max(0, a);
-      P->flat_blocks[1] = std::max(0, b);
-      P->flat_blocks[2] = std::max(0, c);
-    }
-  }
-  if (const char* e = std::getenv("DSSM_WIRE_GRAD_PASS")) P->wire_grad_pass = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_SCATTER_IN_COS")) P->scatter_in_cos = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_DW_IN_APPLY")) P->dw_in_apply = e[0] != '0';
-  if (const char* e = std::getenv("DSSM_NT_TIMING")) P->nt_timing = e[0] == '1' && P->Lt.dense_ok;
-  if (const char* e = std::getenv("DSSM_FSUM_COPIES"))
-    P->fsum0_copies = std::max(1, std::min(kFsum0Copies, std::atoi(e)));
-  {
-    const float st[4] = {cfg->beta1, cfg->beta2, 0.f, 0.f};  // TF: beta*_power start at beta*
-    if (hipMemcpy(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice) != hipSuccess) {
-      delete P;
-      return fail(DSSM_E_HIP, "failed to initialise the device Adam state");
-    }
-  }
-  if (P->Lt.dense_ok) {
-    // opt-in until it outruns the per-op launches (DSSM_DENSE=1)
-    const char* e = std::getenv("DSSM_DENSE");
-    if (e && e[0] == '1') {
-      const Layout& Lt = P->Lt;
-      int ld[DSSM_MAX_LAYERS];
-      for (int l = 0; l < Lt.L; ++l) ld[l] = Lt.ldp[l];
-      P->dense_smem = dssm::dense_smem_bytes(ld, Lt.L);
-      P->dense_grid = std::min(dssm::dense_max_grid(P->dense_smem), kDenseMaxGrid);
-      if (P->dense_grid > 0) {
-        const dssm::DenseArgs a = P->dense_args();
-        if (hipMemcpy(P->ws + Lt.dense_args, &a, sizeof a, hipMemcpyHostToDevice) != hipSuccess) {
-          delete P;
-          return fail(DSSM_E_HIP, "failed to write the dense-kernel arguments");
-        }
-        P->dense_on = true;
-      }
-    }
-  }
-  if (hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&P->ev_batch, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&P->ev_csc, hipEventDisableTiming) != hipSuccess) {
+  const float st[4] = {cfg->beta1, cfg->beta2, 0.f, 0.f};  // TF: beta*_power start at beta*
+  if (hipMemcpy(P->ws + P->Lt.adam_state, st, sizeof st, hipMemcpyHostToDevice) != hipSuccess) {
     delete P;
-    return fail(DSSM_E_HIP, "failed to create the plan's side stream/events");
+    return fail(DSSM_E_HIP, "failed to initialise the device Adam state");
   }
   *out = P;
   return DSSM_OK;
@@ -636,10 +428,6 @@ int dssm_plan_destroy(dssm_plan* plan) {
   if (plan) {
     for (auto& p : plan->probe)
       for (hipEvent_t e : p.ev) hipEventDestroy(e);
-    if (plan->side) {
-      hipStreamSynchronize(plan->side);
-      hipStreamDestroy(plan->side);
-    }
     for (auto* g : plan->graphs) {
       if (g->exec) hipGraphExecDestroy(g->exec);
       for (auto& pr : g->ev)
@@ -647,11 +435,22 @@ int dssm_plan_destroy(dssm_plan* plan) {
           if (e) hipEventDestroy(e);
       delete g;
     }
-    if (plan->ev_batch) hipEventDestroy(plan->ev_batch);
-    if (plan->ev_csc) hipEventDestroy(plan->ev_csc);
   }
   delete plan;
   return DSSM_OK;
+}
+
+int dssm_plan_set_option(dssm_plan* P, int option, int value) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (option < 0 || option >= DSSM_OPT_COUNT) return fail(DSSM_E_INVALID, "unknown plan option");
+  if (P->capturing) return fail(DSSM_E_INVALID, "options cannot change during a graph capture");
+  P->opt[option] = value != 0;
+  return DSSM_OK;
+}
+
+int dssm_plan_get_option(const dssm_plan* P, int option) {
+  if (!P || option < 0 || option >= DSSM_OPT_COUNT) return -1;
+  return P->opt[option];
 }
 
 int dssm_plan_probe_enable(dssm_plan* P, int id, int max_samples) {
@@ -710,9 +509,6 @@ int dssm_plan_buffer(const dssm_plan* P, int id, int layer, void** ptr, size_t* 
       n = (size_t)Lt.R * Lt.ldp[layer] * (Lt.bf16 && layer < Lt.L - 1 ? 2 : 4);
       break;
     case DSSM_BUF_DA: off = Lt.dA[layer]; n = (size_t)Lt.R * Lt.ldp[layer] * 4; break;
-    case DSSM_BUF_DENSE_TIMING:
-      if (!Lt.dense_ok) return fail(DSSM_E_UNSUPPORTED, "no dense-kernel workspace in this plan");
-      off = Lt.dense_timing; n = 4 * 64 * 8; break;
     default: return fail(DSSM_E_INVALID, "unknown buffer id");
   }
   *ptr = P->ws + off;
@@ -744,48 +540,28 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   const Layout& Lt = P->Lt;
   const dssm_config& c = P->cfg;
   const dssm::BnTowers tw{Lt.BS, Lt.R};
+  const bool fused = train && P->fused_stats();
+  const bool merged = train && P->merged_csc();
   if (train) {
-    // The CSC transpose depends only on the batch: run it on the side stream, overlapped with
-    // the forward pass.  ev_batch orders it after everything already queued on `s` (including
-    // the previous step's consumers of the CSC arrays).
-    hipStream_t cs = P->csc_inline ? s : P->side;
-    if (!P->csc_inline) {
-      HIP_TRY(hipEventRecord(P->ev_batch, s));
-      HIP_TRY(hipStreamWaitEvent(P->side, P->ev_batch, 0));
-    }
-    P->probe_begin(DSSM_PROBE_CSC, cs);
-    // fused-statistics steps: the transpose's first launch also clears the step's BN sums (on
-    // the launch stream; the side-stream schedule clears them with a memset there instead)
-    const bool clear = P->fused_stats && !P->dense_on;
-    if (clear && !P->csc_inline)
-      HIP_TRY(hipMemsetAsync(P->ws + Lt.dense_sums, 0, Lt.dense_sums_bytes, s));
-    if (P->rank_prefetched == P->indptr && P->merged_csc()) {
-      P->rank_prefetched = nullptr;  // launched beside the previous step's Adam
-    } else
+    // The CSC transpose of the batch (dW1's operand).  Fused-statistics steps: its first launch
+    // also clears the step's BN sums; merged: its scan / scatter ride in later launches.
+    P->probe_begin(DSSM_PROBE_CSC, s);
     HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
-                                   P->at<int>(Lt.csc_col), cs,
-                                   clear && P->csc_inline ? P->at<double>(Lt.dense_sums) : nullptr,
-                                   clear && P->csc_inline ? (int)(Lt.dense_sums_bytes / 8) : 0,
-                                   P->csc_rank_path, P->merged_csc()));
-    P->probe_end(DSSM_PROBE_CSC, cs);
-    if (!P->csc_inline) {
-      HIP_TRY(hipEventRecord(P->ev_csc, P->side));
-      P->csc_pending = true;
-    }
+                                   P->at<int>(Lt.csc_col), s,
+                                   fused ? P->at<double>(Lt.sums) : nullptr,
+                                   fused ? (int)(Lt.sums_bytes / 8) : 0, P->csc_rank_path(), merged,
+                                   P->deterministic() ? P->at<int>(Lt.sort_row) : nullptr,
+                                   P->deterministic() ? P->at<float>(Lt.sort_val) : nullptr));
+    P->probe_end(DSSM_PROBE_CSC, s);
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
-  if (train && P->merged_csc()) {  // the SpMM rows share their launch with the column scan
+  if (merged) {  // the SpMM rows share their launch with the column scan
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
                                    P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
                                    P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
-  } else if (train && P->fused_stats && P->spmm_stats && !P->dense_on) {
-    HIP_TRY(dssm::launch_spmm_fwd_stats(P->indptr, P->indices, P->values, Lt.R,
-                                        P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
-                                        P->at<float>(Lt.Z[0]), Lt.ldp[0], P->at<double>(Lt.fsum[0]),
-                                        Lt.BS, P->fsum0_copies, s));
   } else {
     // eval: every layer's BN coefficients from the EMA, in the SpMM launch's extra workgroups
     dssm::EvalCoef ec{};
@@ -811,41 +587,30 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                 Lt.ldp[0], s, train ? nullptr : &ec));
   }
   P->probe_end(DSSM_PROBE_SPMM_FWD, s);
-  if (P->dense_on) {  // BN1 .. cosine + loss (+ dy_L and its BN partials) in one launch
-    HIP_TRY(dssm::launch_dense_fwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.ldp[Lt.L - 1],
-                                   Lt.dense_kmax, Lt.NEG, train != 0, P->dense_grid,
-                                   P->dense_smem, s));
-    P->fwd_train_done = train != 0;
-    return DSSM_OK;
-  }
-  if (train && P->fused_stats) {
-    // BN1 sums by their own launch (or, DSSM_SPMM_STATS=1, with the SpMM); each NT GEMM
-    // stages the previous layer's BN+ReLU and accumulates its own output's sums, the cosine
-    // kernel the last layer's backward sums (bnfuse.h)
-    // scatter_in_cos: the transpose's scatter rides in the cosine launch instead (csc.h)
+  if (fused) {
+    // BN1 sums by their own launch; each NT GEMM stages the previous layer's BN+ReLU and
+    // accumulates its own output's sums, the cosine kernel the last layer's backward sums
+    // (bnfuse.h).  Merged: the transpose's scatter rides beside the BN1 sums or, by default,
+    // in the cosine launch (csc.h).
     dssm::CscScatter scat{};
-    const bool scat_cos = P->merged_csc() && P->scatter_in_cos;
-    if (P->merged_csc())  // BN1 sums beside the transpose's scatter
+    const bool scat_cos = merged && P->on(DSSM_OPT_SCATTER_IN_COS);
+    if (merged)
       HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
                                         P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
                                         P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s,
                                         scat_cos ? &scat : nullptr));
-    else if (!P->spmm_stats)
+    else
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s));
-    const bool flat_on = flat_spread_on(P);
-    const dssm::FlatSlice fs0 = flat_slice(P, 0), fs1 = flat_slice(P, 1);
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
-          P->at<float>(Lt.coef[l - 1]), &in, Lt.BS,
-          P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l]), Lt.ldp[l],
-          P->bias(l), P->at<uint16_t>(Lt.A[l - 1]), P->at<double>(Lt.fsum[l]), P->fcopies(l), s,
-          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 192 : nullptr,
-          (flat_on && l == Lt.L - 1 && fs0.nblocks) ? &fs0 : nullptr));
+          P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1],
+          P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<uint16_t>(Lt.A[l - 1]),
+          P->at<double>(Lt.fsum[l]), s));
     }
     const int lL = Lt.L - 1;
     const dssm::BnSide last = P->bn_side(lL);
@@ -853,11 +618,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.Z[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG, c.gamma,
         P->at<float>(Lt.coef[lL]), P->at<float>(Lt.A[lL]), P->at<float>(Lt.cos_raw),
         P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
-        P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]),
-        P->split_finalize, s, &last, /*defer_finalize=*/true,
-        P->nt_timing ? P->at<unsigned long long>(Lt.dense_timing) : nullptr,
-        (flat_on && fs1.nblocks) ? &fs1 : nullptr, scat_cos ? &scat : nullptr));
-    P->flat_this_step = flat_on;
+        P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]), s, &last,
+        /*defer_finalize=*/true, scat_cos ? &scat : nullptr));
     P->fwd_train_done = true;
     P->fwd_fused = true;
     P->loss_pending = true;
@@ -867,13 +629,12 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   for (int l = 0; l < Lt.L; ++l) {
     float* ema = P->ema + Lt.ema_off[l];
     const int n = Lt.n[l];
-    if (train || P->dense_on)  // eval coefficients: written by the SpMM launch above
-    HIP_TRY(dssm::launch_bn_fwd_stats(
-        P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
-        P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
-        c.bn_eps, c.ema_decay, train != 0, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
-        P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]),
-        P->split_finalize, s));
+    if (train)  // eval coefficients: written by the SpMM launch above
+      HIP_TRY(dssm::launch_bn_fwd_stats(
+          P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->p + Lt.bn_off[l][0], P->p + Lt.bn_off[l][1],
+          P->p + Lt.bn_off[l][2], P->p + Lt.bn_off[l][3], ema, ema + n, ema + 2 * n, ema + 3 * n,
+          c.bn_eps, c.ema_decay, true, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
+          P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]), s));
     const bool last = l == Lt.L - 1;
     if (last && Lt.bf16) break;  // the cosine kernel applies the last BN+ReLU itself
     if (!last && P->wholek(l + 1)) {
@@ -904,7 +665,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
       P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
       P->at<float>(Lt.loss_j), P->at<float>(Lt.loss),
       train ? P->at<float>(Lt.dA[lL]) : nullptr,  // eval: no gradient
-      P->split_finalize, s));
+      s));
   P->fwd_train_done = train != 0;
   return DSSM_OK;
 }
@@ -916,14 +677,10 @@ static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s);
 // (unfused) or inside the Adam step (fused).
 static int dw1_backward(dssm_plan* P, hipStream_t s) {
   const Layout& Lt = P->Lt;
-  if (P->csc_pending) {
-    HIP_TRY(hipStreamWaitEvent(s, P->ev_csc, 0));
-    P->csc_pending = false;
-  }
   P->probe_begin(DSSM_PROBE_DW1, s);
   // fused single-GPU step with the rank transpose: the heavy columns are computed inside Adam
   // (the DW1 probe then brackets no kernel)
-  if (P->fused_w1_adam && P->heavy_in_adam()) {
+  if (P->fused_w1_adam() && P->heavy_in_adam()) {
     P->probe_end(DSSM_PROBE_DW1, s);
     return DSSM_OK;
   }
@@ -934,15 +691,14 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
   }
   HIP_TRY(dssm::launch_dw1(P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
                            P->at<int>(Lt.csc_col), Lt.D, Lt.R, Lt.max_nnz, P->ws + Lt.dZ[0],
-                           Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam, s,
-                           P->csc_rank_path && dssm::csc_rank_supported(Lt.D)
-                               ? P->at<int>(Lt.csc_scratch) : nullptr));
+                           Lt.bf16, Lt.ldp[0], Lt.n[0], P->g + Lt.fc_off[0], !P->fused_w1_adam(), s,
+                           P->csc_rank_path() ? P->at<int>(Lt.csc_scratch) : nullptr,
+                           P->deterministic() ? P->at<float>(Lt.heavy_slab) : nullptr));
   P->probe_end(DSSM_PROBE_DW1, s);
   return DSSM_OK;
 }
 
 static int backward_impl(dssm_plan* P, void* stream);
-
 
 int dssm_plan_backward(dssm_plan* P, void* stream) {
   if (int rc = backward_impl(P, stream)) return rc;
@@ -957,25 +713,17 @@ static int backward_impl(dssm_plan* P, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const Layout& Lt = P->Lt;
   const dssm::BnTowers tw{Lt.BS, Lt.R};
-  if (!P->grads_clean && P->fused_w1_adam) {
+  if (!P->grads_clean && P->fused_w1_adam()) {
     // backward() twice without an Adam step in between: re-zero the atomic-target blocks (only
     // the fused path leaves dW1's heavy rows to be cleared by Adam; otherwise dw1-light
     // overwrites every row before the heavy atomics).
     HIP_TRY(hipMemsetAsync(P->g, 0, sizeof(float) * (size_t)Lt.total, s));
   }
   P->grads_clean = false;
-  if (P->dense_on) {
-    // BN_L .. BN1 backward, dA GEMMs, dW_l (l >= 2) split-K, dZ1 in one launch; then dW1
-    const bool defer = P->fused_w1_adam;
-    HIP_TRY(dssm::launch_dense_bwd(P->at<dssm::DenseArgs>(Lt.dense_args), Lt.dense_kmax,
-                                   defer ? 1 : 0, P->dense_grid, P->dense_smem, s));
-    for (int l = 1; l < Lt.L; ++l) P->dw_deferred[l] = defer ? Lt.dense_splits : 0;
-    return dw1_backward(P, s);
-  }
   if (P->fwd_fused) {
     // BN_L apply from the cosine kernel's sums, then per layer one launch for dA_{l-1} (with
-    // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply
-    // dw_in_apply: the pair launches run their dA tiles only (one round) and each dW_l's tiles
+    // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply.
+    // DW_IN_APPLY: the pair launches run their dA tiles only (one round) and each dW_l's tiles
     // ride in the following apply launch (BN_{l-1}'s), whose element blocks leave CUs idle
     dssm::TnParams dw{};
     bool dw_pending = false;
@@ -983,13 +731,11 @@ static int backward_impl(dssm_plan* P, void* stream) {
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
-      const dssm::FlatSlice fs2 = flat_slice(P, 2);
       HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                               P->at<uint16_t>(Lt.dZ[l]), s,
                                               fin ? P->at<float>(Lt.loss_j) : nullptr,
-                                              dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true), P->at<float>(Lt.loss),
-                                              (fin && P->flat_this_step && fs2.nblocks) ? &fs2 : nullptr,
-                                              dw_pending ? &dw : nullptr));
+                                              dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true),
+                                              P->at<float>(Lt.loss), dw_pending ? &dw : nullptr));
       if (dw_pending && dw_reduce_to) {  // not deferred to Adam: the slabs summed right after
         const int nsplit = (dw.K + dw.k_per_split - 1) / dw.k_per_split;
         HIP_TRY(dssm::launch_splitk_reduce(dw.C, nsplit, (int64_t)dw.M * dw.N, dw_reduce_to, s));
@@ -998,18 +744,16 @@ static int backward_impl(dssm_plan* P, void* stream) {
       dw_reduce_to = nullptr;
       if (fin) P->loss_pending = false;
       if (l == 0) break;
-      const bool host_dw = P->dw_in_apply;
+      const bool host_dw = P->on(DSSM_OPT_DW_IN_APPLY);
       dw = dssm::TnParams{};  // filled by the pair launch when it hands its dW tiles over
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
-          P->bcopies(l - 1), Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
-          P->g + Lt.fc_off[l], P->fused_w1_adam, s, &P->dw_deferred[l],
-          (P->nt_timing && l == 1) ? P->at<unsigned long long>(Lt.dense_timing) + 128 : nullptr,
-          host_dw ? &dw : nullptr));
+          Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
+          P->g + Lt.fc_off[l], P->fused_w1_adam(), s, &P->dw_deferred[l], host_dw ? &dw : nullptr));
       dw_pending = host_dw && dw.C != nullptr;
-      if (dw_pending && !P->fused_w1_adam && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
+      if (dw_pending && !P->fused_w1_adam() && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
     }
     return dw1_backward(P, s);
   }
@@ -1020,15 +764,15 @@ static int backward_impl(dssm_plan* P, void* stream) {
                                 P->g + Lt.bn_off[l][1], P->g + Lt.bn_off[l][2],
                                 P->g + Lt.bn_off[l][3], P->at<float>(Lt.partial),
                                 P->at<unsigned>(Lt.tickets[l][1]), P->at<float>(Lt.bcoef[l]),
-                                P->ws + Lt.dZ[l], Lt.bf16, P->split_finalize, s));
+                                P->ws + Lt.dZ[l], Lt.bf16, s));
     if (l > 0) {
       const int kin = Lt.in_dim[l];
       float* gw = P->g + Lt.fc_off[l];
       HIP_TRY(dssm::launch_gemm(dssm::GEMM_DW, Lt.bf16, kin + 1, n, Lt.R, P->ws + Lt.A[l - 1],
                                 Lt.ldp[l - 1], P->ws + Lt.dZ[l], Lt.ldp[l], gw, n, nullptr, true,
                                 P->at<float>(Lt.dw_slab[l]), s,
-                                P->fused_w1_adam ? &P->dw_deferred[l] : nullptr));
-      if (!P->fused_w1_adam) P->dw_deferred[l] = 0;
+                                P->fused_w1_adam() ? &P->dw_deferred[l] : nullptr));
+      if (!P->fused_w1_adam()) P->dw_deferred[l] = 0;
       if (P->wholek(l))  // dA = dZ . W^T: the weight shadow rows are already k-contiguous
         HIP_TRY(dssm::launch_gemm_nt(Lt.R, kin, n, P->ws + Lt.dZ[l], Lt.ldp[l], false, nullptr,
                                      Lt.BS, P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l],
@@ -1065,6 +809,7 @@ static void fill_w1_roles(dssm_plan* P, dssm::AdamStep& a) {
     a.heavy_n = dssm::csc_heavy_count(scr, Lt.D, Lt.max_nnz);
     a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
     a.heavy_ticket = dssm::csc_heavy_tickets(scr, Lt.D, Lt.R, Lt.max_nnz);
+    a.heavy_slab = P->deterministic() ? P->at<float>(Lt.heavy_slab) : nullptr;
   }
 }
 
@@ -1072,7 +817,7 @@ static void fill_w1_roles(dssm_plan* P, dssm::AdamStep& a) {
 // into the gradient arena) by k_adam_step's W1 roles in gradient-pass mode, instead of the
 // materialising dW1 launches + the wire pack.
 static bool wire_gradient_pass(const dssm_plan* P) {
-  return P->gwire && !P->fused_w1_adam && P->heavy_in_adam() && P->wire_grad_pass;
+  return P->gwire && !P->fused_w1_adam() && P->heavy_in_adam() && P->on(DSSM_OPT_WIRE_GRAD_PASS);
 }
 
 static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s) {
@@ -1118,12 +863,12 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   a.clear_from = Lt.total;
   a.d4_begin = P->adam_begin / 4;
   a.d4_end = (P->adam_end >= 0 ? P->adam_end : Lt.total) / 4;
-  if (P->fused_w1_adam && (P->adam_begin != 0 || (P->adam_end >= 0 && P->adam_end != Lt.total)))
+  if (P->fused_w1_adam() && (P->adam_begin != 0 || (P->adam_end >= 0 && P->adam_end != Lt.total)))
     return fail(DSSM_E_INVALID, "a sharded Adam range needs the fused W1 Adam off");
   if (P->pwire) {
     // bf16 wire: the rank's W1 shard from the reduce-scattered wire (writing the parameter wire),
     // then the replicated fp32 tail [wire_end, total) with its shadows
-    if (P->fused_w1_adam) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
+    if (P->fused_w1_adam()) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
     const int64_t we = P->wire_end();
     a.d4_begin = std::min(P->adam_begin, we) / 4;
     a.d4_end = std::min(P->adam_end >= 0 ? P->adam_end : we, we) / 4;
@@ -1138,12 +883,10 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
     if (sh.count) sh.count -= 1;
   }
-  if (P->fused_w1_adam) {
+  if (P->fused_w1_adam()) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
     fill_w1_roles(P, a);
     a.d4_begin = rest / 4;
-    if (a.heavy_n) a.heavy_reset = const_cast<int*>(a.heavy_n);
-    a.flat_elsewhere = P->flat_this_step ? 1 : 0;  // the step's slices updated the untouched rows
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
@@ -1162,7 +905,6 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
   P->probe_end(DSSM_PROBE_ADAM, s);
   P->grads_clean = true;
-  P->flat_this_step = false;
   return DSSM_OK;
 }
 
@@ -1187,7 +929,7 @@ int dssm_plan_set_wire(dssm_plan* P, uint16_t* grad_wire, uint16_t* param_wire, 
   }
   if (!grad_wire || !param_wire) return fail(DSSM_E_INVALID, "both wires or neither");
   if (!P->Lt.bf16) return fail(DSSM_E_UNSUPPORTED, "the bf16 wire is a bf16-mode (perf) option");
-  if (P->fused_w1_adam) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
+  if (P->fused_w1_adam()) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
   if (P->Lt.fc_off[0] != 0 || count < P->wire_end())
     return fail(DSSM_E_INVALID, "wire buffers must hold dssm_plan_wire_extent() elements");
   if ((reinterpret_cast<uintptr_t>(grad_wire) | reinterpret_cast<uintptr_t>(param_wire)) & 7)
@@ -1205,39 +947,16 @@ int dssm_plan_wire_shadows(dssm_plan* P, void* stream) {
 }
 
 int dssm_plan_set_fused_w1_adam(dssm_plan* P, int on) {
-  if (!P) return fail(DSSM_E_INVALID, "null plan");
-  P->fused_w1_adam = on != 0;
-  return DSSM_OK;
+  return dssm_plan_set_option(P, DSSM_OPT_FUSED_W1_ADAM, on);
 }
 
 int dssm_plan_train_step(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
-  P->in_full_step = true;  // Adam follows: the untouched rows' update may ride in the step's launches
   int rc = dssm_plan_forward(P, 1, stream);
   if (!rc) rc = dssm_plan_backward(P, stream);
   if (!rc) rc = dssm_plan_adam(P, 1.0f, stream);
-  P->in_full_step = false;
-  P->flat_this_step = false;
   return rc;
 }
-
-int dssm_plan_check(dssm_plan* P, void* stream) {
-  if (!P) return fail(DSSM_E_INVALID, "null plan");
-  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  if (!P->dense_on) return DSSM_OK;
-  unsigned err = 0;
-  HIP_TRY(hipMemcpy(&err, P->ws + P->Lt.dense_bar + 128 * 4, 4, hipMemcpyDeviceToHost));
-  if (err) {
-    // re-arm the barrier and tickets, clear the statistics accumulators
-    HIP_TRY(hipMemset(P->ws + P->Lt.dense_bar, 0, 3 * 256));
-    HIP_TRY(hipMemset(P->ws + P->Lt.dense_tickets, 0, 2 * 256));
-    HIP_TRY(hipMemset(P->ws + P->Lt.dense_sums, 0, P->Lt.dense_sums_bytes));
-    return fail(DSSM_E_HIP, "dense kernel grid barrier timed out (results of that step are invalid)");
-  }
-  return DSSM_OK;
-}
-
-int dssm_plan_dense_enabled(dssm_plan* P) { return P && P->dense_on ? P->dense_grid : 0; }
 
 int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
@@ -1252,20 +971,21 @@ int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
 int dssm_plan_schedule(const dssm_plan* P) {
   if (!P) return 0;
   int f = 0;
-  const bool fs = P->fused_stats && !P->dense_on;
+  const bool fs = P->fused_stats();
   if (fs) f |= DSSM_SCHED_FUSED_STATS;
   if (P->merged_csc()) f |= DSSM_SCHED_MERGED_CSC;
   if (P->heavy_in_adam()) f |= DSSM_SCHED_HEAVY_IN_ADAM;
-  if (P->fused_w1_adam) f |= DSSM_SCHED_FUSED_W1_ADAM;
+  if (P->fused_w1_adam()) f |= DSSM_SCHED_FUSED_W1_ADAM;
   bool wk = P->Lt.L > 1;
   for (int l = 1; l < P->Lt.L; ++l) wk = wk && P->wholek(l);
   if (wk) f |= DSSM_SCHED_WHOLEK;
-  if (fs && P->dw_in_apply) f |= DSSM_SCHED_DW_IN_APPLY;
-  if (P->merged_csc() && P->scatter_in_cos) f |= DSSM_SCHED_SCATTER_IN_COS;
+  if (fs && P->on(DSSM_OPT_DW_IN_APPLY)) f |= DSSM_SCHED_DW_IN_APPLY;
+  if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
+  if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;
   return f;
 }
 
-int dssm_plan_fused_stats(dssm_plan* P) { return P && P->fused_stats && !P->dense_on ? 1 : 0; }
+int dssm_plan_fused_stats(dssm_plan* P) { return P && P->fused_stats() ? 1 : 0; }
 
 int dssm_plan_set_adam_state(dssm_plan* P, float beta1_power, float beta2_power, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
@@ -1296,7 +1016,7 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
     return fail(DSSM_E_INVALID, "graph parts: DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM | DSSM_GRAPH_SHADOWS"
                                 " | DSSM_GRAPH_WIRE_SHADOWS");
   if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
-  if (P->fused_w1_adam && parts != (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM))
+  if (P->fused_w1_adam() && parts != (DSSM_GRAPH_FWD_BWD | DSSM_GRAPH_ADAM))
     return fail(DSSM_E_INVALID, "with the fused W1 Adam a graph must hold the whole step");
   hipStream_t s = (hipStream_t)stream;
   auto* g = new dssm_plan::GraphSlot();
@@ -1318,14 +1038,11 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
   }
   P->capturing = g;
   int rc = DSSM_OK;
-  P->in_full_step = (parts & DSSM_GRAPH_FWD_BWD) && (parts & DSSM_GRAPH_ADAM);
   if (parts & DSSM_GRAPH_FWD_BWD) {
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
   }
   if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
-  P->in_full_step = false;
-  P->flat_this_step = false;
   if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
   if (!rc && (parts & DSSM_GRAPH_WIRE_SHADOWS)) rc = dssm_plan_wire_shadows(P, stream);
   P->capturing = nullptr;
@@ -1383,9 +1100,6 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   }
   P->capturing = g;
   int rc = DSSM_OK;
-  const bool prefetch = P->rank_prefetch && P->merged_csc() && P->fused_w1_adam && P->heavy_in_adam();
-  P->rank_prefetched = nullptr;
-  P->in_full_step = true;
   for (int i = 0; i < nsteps && !rc; ++i) {
     // probes (event-record nodes) ride in the first step only
     g->probes = with_probes != 0 && i == 0;
@@ -1394,36 +1108,8 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     P->values = values[i];
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
-    if (rc) break;
-    const bool pf = prefetch && i + 1 < nsteps;
-    if (pf) {
-      // step i+1's rank launch (its batch only; it also clears the BN sums, whose last reader,
-      // this step's backward, is complete) on the side stream beside this step's Adam, which
-      // re-arms the heavy-item count once every block has read it
-      const Layout& Lt = P->Lt;
-      hipError_t he = hipEventRecord(P->ev_batch, s);
-      if (he == hipSuccess) he = hipStreamWaitEvent(P->side, P->ev_batch, 0);
-      if (he == hipSuccess)
-        he = dssm::launch_csc_build(indptrs[i + 1], indices[i + 1], values[i + 1], Lt.R, Lt.D,
-                                    Lt.max_nnz, P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
-                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
-                                    P->at<int>(Lt.csc_col), P->side, P->at<double>(Lt.dense_sums),
-                                    (int)(Lt.dense_sums_bytes / 8), true, true, /*reset_heavy=*/false);
-      if (he == hipSuccess) he = hipEventRecord(P->ev_csc, P->side);
-      if (he != hipSuccess) {
-        rc = fail(DSSM_E_HIP, std::string("rank prefetch: ") + hipGetErrorString(he));
-        break;
-      }
-    }
-    rc = dssm_plan_adam(P, 1.0f, stream);
-    if (!rc && pf) {
-      if (hipStreamWaitEvent(s, P->ev_csc, 0) != hipSuccess) rc = fail(DSSM_E_HIP, "rank prefetch join");
-      P->rank_prefetched = indptrs[i + 1];
-    }
+    if (!rc) rc = dssm_plan_adam(P, 1.0f, stream);
   }
-  P->in_full_step = false;
-  P->flat_this_step = false;
-  P->rank_prefetched = nullptr;
   g->probes = with_probes != 0;
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();
@@ -1515,7 +1201,7 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
   unsigned* tickets = reinterpret_cast<unsigned*>(w + o1 + align256(4 * 2 * (size_t)ldz * 4));
   HIP_TRY(dssm::launch_bn_fwd_stats(Z, ldz, n, tw, gamma, beta, gamma, beta, ema_mean, ema_var,
                                     ema_mean, ema_var, eps, decay, train != 0, batch_mean,
-                                    batch_var, part, tickets, coef, false, s));
+                                    batch_var, part, tickets, coef, s));
   HIP_TRY(dssm::launch_bn_apply(Z, ldz, n, tw, coef, relu != 0, out, out_dtype == DSSM_BF16, s));
   return DSSM_OK;
 }
@@ -1527,7 +1213,7 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
       query_bs < 1 || neg < 1 || neg > 15 || n < 1 || n > 512 || ld < n)
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss: bad arguments");
   HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
-                                   cos_sim, prob, query_norm, ws, loss, dy, false,
+                                   cos_sim, prob, query_norm, ws, loss, dy,
                                    (hipStream_t)stream));
   return DSSM_OK;
 }

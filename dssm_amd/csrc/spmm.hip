@@ -104,65 +104,6 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
   spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne);
 }
 
-// FC1 forward + BN1 statistics (fused-statistics schedule, bnfuse.h): 16 rows per 1024-thread
-// workgroup (one tower: row_split % 16 == 0); every wave stages its row's z and z^2 in LDS,
-// the workgroup sums its 16 rows per column in fp64 and adds them to fsum[tower] with one atomic
-// per (column, statistic).
-constexpr int kSpmmStatRows = 16;
-template <typename TW, int RPW>
-__global__ __launch_bounds__(64 * kSpmmStatRows / RPW) void k_spmm_fwd_stats(
-    const int* __restrict__ indptr, const int* __restrict__ indices,
-    const float* __restrict__ values, int rows, const TW* __restrict__ W, int ldw, int n,
-    const float* __restrict__ bias, float* __restrict__ Z, int ldz, double* __restrict__ fsum,
-    int row_split, int copies) {
-  constexpr int NT = 64 * kSpmmStatRows / RPW;
-  extern __shared__ float red[];  // [waves][2][ldz]
-  const int wv = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * kSpmmStatRows;
-  const int lane = lane_id();
-  const int c = lane * 8;  // ldz <= 512: one 512-column pass
-  const int nvalid = (c < ldz) ? n - c : 0;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int row = row0 + wv * RPW + rr;
-    if (row >= rows) break;
-    float acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = (c + i < n) ? bias[c + i] : 0.f;
-    const int s = indptr[row], e = indptr[row + 1];
-    gather_accumulate(indices, values, s, e, W, ldw, c, nvalid, acc);
-    if (c < ldz) store8(Z + (size_t)row * ldz + c, acc);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s1[i] += acc[i];
-      s2[i] = __fmaf_rn(acc[i], acc[i], s2[i]);
-    }
-  }
-  if (c < ldz) {
-    float* r0 = red + (size_t)(wv * 2) * ldz + c;
-    float* r1 = r0 + ldz;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      r0[i] = s1[i];
-      r1[i] = s2[i];
-    }
-  }
-  __syncthreads();
-  const int tower = row0 < row_split ? 0 : 1;
-  // replica blockIdx % copies: spreads the same-address atomics (bnfuse.h)
-  fsum += (size_t)(blockIdx.x % copies) * 4 * ldz;
-  for (int i = threadIdx.x; i < 2 * n; i += NT) {
-    const int st = i / n, cc = i - st * n;
-    double a = 0.0;
-#pragma unroll
-    for (int w = 0; w < kSpmmStatRows / RPW; ++w) a += red[(size_t)(w * 2 + st) * ldz + cc];
-    __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + st) * ldz + cc, a, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // ---- CSR -> CSC ------------------------------------------------------------------------------
 // Blocks own contiguous row ranges; wave w of a block walks rows r0+w, r0+w+16, ... and its
 // lanes the row's entries (a row's columns are distinct, so a wave-instruction never collides).
@@ -679,6 +620,54 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
   }
 }
 
+// Deterministic mode: the transpose's entries of every column put in row order.  The scatter /
+// fill place a column's entries in an order set by atomics (per-block slot reservations, LDS
+// histogram arrival), which changes the fp32 summation order of dW1 from run to run; this pass
+// rewrites each column [col_ptr[c], col_ptr[c+1]) of (row_in, val_in) sorted by row into
+// (row_out, val_out).  One workgroup per column: the column's rows are set in an LDS bitmap
+// (window of kSortWin rows at a time; a row appears at most once per column) with its value
+// beside it, then the bitmap's block-wide prefix count gives every entry its slot.
+constexpr int kSortWin = 8192;  // rows per window: one 32-bit bitmap word per thread
+__global__ __launch_bounds__(256) void k_csc_sort_rows(const int* __restrict__ col_ptr, int rows,
+                                                       const int* __restrict__ row_in,
+                                                       const float* __restrict__ val_in,
+                                                       int* __restrict__ row_out,
+                                                       float* __restrict__ val_out) {
+  static_assert(kSortWin / 32 == 256, "one bitmap word per thread");
+  __shared__ unsigned bits[kSortWin / 32];
+  __shared__ float vals[kSortWin];
+  __shared__ int s_wave[4];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int s = col_ptr[c], e = col_ptr[c + 1];
+  if (s == e) return;  // uniform over the workgroup
+  int base = s;
+  for (int w0 = 0; w0 < rows; w0 += kSortWin) {
+    const int wn = min(kSortWin, rows - w0);
+    bits[t] = 0u;
+    __syncthreads();
+    for (int i = s + t; i < e; i += 256) {
+      const int r = row_in[i] - w0;
+      if (r >= 0 && r < wn) {
+        atomicOr(&bits[r >> 5], 1u << (r & 31));
+        vals[r] = val_in[i];
+      }
+    }
+    __syncthreads();
+    unsigned m = bits[t];
+    int tot;
+    int p = base + block_excl_scan<256>(__popc(m), s_wave, tot);
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      row_out[p] = w0 + t * 32 + b;
+      val_out[p] = vals[t * 32 + b];
+      ++p;
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+
 // ---- dW1 ---------------------------------------------------------------------------------------
 // Light columns (<= kLight entries): one wave sums and stores the whole row; heavy rows get 0
 // here (the heavy kernel adds into them afterwards).
@@ -687,12 +676,16 @@ __global__ __launch_bounds__(256) void k_dw1_light(const int* __restrict__ col_p
                                                    const int* __restrict__ csc_row,
                                                    const float* __restrict__ csc_val, int D,
                                                    const TZ* __restrict__ dZ, int lddz, int n,
-                                                   float* __restrict__ G) {
+                                                   float* __restrict__ G, int mode) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c > D) return;
   const int lane = lane_id();
   const int s = col_ptr[c], e = col_ptr[c + 1];
-  const bool heavy = e - s > kLightEntries;
+  // mode 0: light rows summed, heavy rows zeroed (the heavy kernels add into them); deterministic
+  // mode without the heavy-item list, one wave per column in CSC order: 1 every row, 2 the heavy
+  // rows only (the fused W1 Adam gathers the light ones itself)
+  if (mode == 2 && e - s <= kLightEntries) return;
+  const bool heavy = mode == 0 && e - s > kLightEntries;
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
     const int nvalid = n - cc;
@@ -757,7 +750,7 @@ __global__ __launch_bounds__(1024) void k_dw1_heavy_items(const int* __restrict_
                                                          const int* __restrict__ heavy_n,
                                                          const int2* __restrict__ items,
                                                          const TZ* __restrict__ dZ, int lddz, int n,
-                                                         float* __restrict__ G) {
+                                                         float* __restrict__ G, float* __restrict__ slab) {
   __shared__ float part[kHeavyWaves][512];
   const int wv = threadIdx.x >> 6, lane = lane_id();
   const int nitems = *heavy_n;
@@ -783,9 +776,32 @@ __global__ __launch_bounds__(1024) void k_dw1_heavy_items(const int* __restrict_
         for (int w = 0; w < kHeavyWaves; ++w) a += part[w][i];
         float* g = G + (size_t)c * n + c0 + i;
         if (single) *g = a;
+        else if (slab) slab[(size_t)it * n + c0 + i] = a;  // deterministic: summed in item order
         else atomicAdd(g, a);
       }
       __syncthreads();
+    }
+  }
+}
+
+// Deterministic mode: the multi-item heavy columns' rows from their items' partial rows, summed in
+// item order (one workgroup per column, at its first item).
+__global__ __launch_bounds__(256) void k_dw1_heavy_reduce(const int* __restrict__ col_ptr,
+                                                          const int* __restrict__ heavy_n,
+                                                          const int2* __restrict__ items, int n,
+                                                          const float* __restrict__ slab,
+                                                          float* __restrict__ G) {
+  const int nitems = *heavy_n;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int2 item = items[it];
+    if (item.y != 0) continue;
+    const int c = item.x;
+    const int nit = cdiv(col_ptr[c + 1] - col_ptr[c], kHeavyItem);
+    if (nit < 2) continue;
+    for (int j = threadIdx.x; j < n; j += 256) {
+      float a = 0.f;
+      for (int k = 0; k < nit; ++k) a += slab[(size_t)(it + k) * n + j];
+      G[(size_t)c * n + j] = a;
     }
   }
 }
@@ -811,27 +827,6 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
   else
     hipLaunchKernelGGL(k_spmm_fwd<float>, grid, block, 0, s, indptr, indices, values, rows,
                        (const float*)W, ldw, n, bias, Z, ldz, e, ne);
-  return hipGetLastError();
-}
-
-hipError_t launch_spmm_fwd_stats(const int* indptr, const int* indices, const float* values,
-                                 int rows, const uint16_t* W, int ldw, int n, const float* bias,
-                                 float* Z, int ldz, double* fsum, int row_split, int copies,
-                                 hipStream_t s) {
-  if (ldz > 512 || (row_split % kSpmmStatRows)) return hipErrorInvalidValue;
-  static const int rpw = [] {
-    const char* e = std::getenv("DSSM_SPMM_STATS_RPW");
-    return e ? std::atoi(e) : 2;
-  }();
-  const dim3 grid(cdiv(rows, kSpmmStatRows));
-#define DSSM_SPS(R)                                                                              \
-  hipLaunchKernelGGL((k_spmm_fwd_stats<u16, R>), grid, dim3(64 * kSpmmStatRows / R),              \
-                     (size_t)(kSpmmStatRows / R) * 2 * ldz * sizeof(float), s, indptr, indices,    \
-                     values, rows, (const u16*)W, ldw, n, bias, Z, ldz, fsum, row_split, copies)
-  if (rpw == 1) DSSM_SPS(1);
-  else if (rpw == 4) DSSM_SPS(4);
-  else DSSM_SPS(2);
-#undef DSSM_SPS
   return hipGetLastError();
 }
 
@@ -863,10 +858,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
   int* pos_tmp = scratch + 2 * (D + 1 + 64);
   const int nsum_x = cdiv(ldz, 64), nsum = nsum_x * cdiv(rows, kSumsRows);
   if (scatter_out) {
-    static const int nb = [] {
-      const char* e = std::getenv("DSSM_SCATTER_BLOCKS");
-      return e ? std::max(1, std::atoi(e)) : 384;
-    }();
+    constexpr int nb = 384;  // scatter workgroups beside the cosine launch
     *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                               csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
   }
@@ -897,7 +889,13 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
                             int D, int max_nnz, int* scratch, int* col_ptr, int* csc_row,
                             float* csc_val, int* csc_col, hipStream_t s, double* zero,
-                            int nzero, bool rank_path, bool rank_only, bool reset_heavy) {
+                            int nzero, bool rank_path, bool rank_only, int* sort_row,
+                            float* sort_val) {
+  // deterministic mode (sort_row != null): the scatter / fill write into (sort_row, sort_val),
+  // then k_csc_sort_rows puts every column in row order into (csc_row, csc_val)
+  if (sort_row && (!sort_val || rank_only)) return hipErrorInvalidValue;
+  int* out_row = sort_row ? sort_row : csc_row;
+  float* out_val = sort_row ? sort_val : csc_val;
   int* cnt = scratch;  // zero between steps (re-zeroed by k_csc_scan / k_csc_scatter)
   int* cursor = scratch + (D + 1 + 64);
   int* rank_tmp = cursor + (D + 1 + 64);
@@ -908,15 +906,13 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     const int rpb = cdiv(rows, kCscRankBlocks);
     const int grid = cdiv(rows, rpb);
     hipLaunchKernelGGL(k_csc_rank, dim3(grid), dim3(kTB), lds, s, indptr, indices, rows, D, rpb, cnt,
-                       rank_tmp, zero, nzero, reset_heavy ? heavy_n : nullptr);
+                       rank_tmp, zero, nzero, heavy_n);
     if (rank_only) return hipGetLastError();  // scan and scatter ride in later launches
     hipLaunchKernelGGL(k_csc_scan_multi, dim3(cdiv(D + 1, kScanMultiCols)), dim3(kTB), 0, s, cnt, D,
                        rows, col_ptr, heavy_n, heavy_items);
     hipLaunchKernelGGL(k_csc_scatter, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices, values,
-                       rows, D, col_ptr, rank_tmp, cnt, csc_row, csc_val, csc_col);
-    return hipGetLastError();
-  }
-  if (lds + (size_t)(cdiv(rows, max(1, min(32, cdiv(rows, 64)))) + 1) * sizeof(int) <= 156 * 1024) {
+                       rows, D, col_ptr, rank_tmp, cnt, out_row, out_val, csc_col);
+  } else if (lds + (size_t)(cdiv(rows, max(1, min(32, cdiv(rows, 64)))) + 1) * sizeof(int) <= 156 * 1024) {
     // Few fat blocks (one CU each: the LDS histogram takes 120 KB): enough to keep the transpose
     // short while leaving most CUs to the forward pass it overlaps on the main stream.
     const int nblk = max(1, min(32, cdiv(rows, 64)));
@@ -926,8 +922,8 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                        cnt, zero, nzero);
     hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
     hipLaunchKernelGGL(k_csc_fill, dim3(grid), dim3(kTB), lds + (size_t)(rpb + 1) * sizeof(int), s,
-                       indptr, indices, values, rows, D, rpb, cursor, col_ptr, rank_tmp, csc_row,
-                       csc_val, csc_col);
+                       indptr, indices, values, rows, D, rpb, cursor, col_ptr, rank_tmp, out_row,
+                       out_val, csc_col);
   } else {
     if (nzero) {
       const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(double), s);
@@ -938,15 +934,18 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                        cnt);
     hipLaunchKernelGGL(k_csc_scan, dim3(1), dim3(1024), 0, s, cnt, D, rows, col_ptr, cursor);
     hipLaunchKernelGGL(k_csc_fill_global, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
-                       values, rows, D, cursor, col_ptr, csc_row, csc_val, csc_col);
+                       values, rows, D, cursor, col_ptr, out_row, out_val, csc_col);
   }
+  if (sort_row)
+    hipLaunchKernelGGL(k_csc_sort_rows, dim3(D + 1), dim3(256), 0, s, col_ptr, rows, sort_row,
+                       sort_val, csc_row, csc_val);
   return hipGetLastError();
 }
 
 hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_val,
                       const int* csc_col, int D, int rows, int max_nnz, const void* dZ,
                       bool dz_bf16, int lddz, int n, float* G, bool light, hipStream_t s,
-                      int* scratch) {
+                      int* scratch, float* heavy_slab) {
   dim3 block(256);
   dim3 g1(cdiv(D + 1, 4));
   dim3 g2(max(1, cdiv(cdiv(max_nnz + rows, 64), 4)));
@@ -954,27 +953,30 @@ hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_v
   const int* heavy_n = scratch ? csc_heavy_count(scratch, D, max_nnz) : nullptr;
   const int2* items = scratch ? reinterpret_cast<const int2*>(heavy_n + 64) : nullptr;
   const int gi = 512;
-  if (dz_bf16) {
-    if (light)
-      hipLaunchKernelGGL(k_dw1_light<u16>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
-                         (const u16*)dZ, lddz, n, G);
-    if (items)
-      hipLaunchKernelGGL(k_dw1_heavy_items<u16>, dim3(gi), dim3(1024), 0, s, col_ptr, csc_row,
-                         csc_val, heavy_n, items, (const u16*)dZ, lddz, n, G);
-    else
-      hipLaunchKernelGGL(k_dw1_heavy<u16>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col, D,
-                         (const u16*)dZ, lddz, n, G);
-  } else {
-    if (light)
-      hipLaunchKernelGGL(k_dw1_light<float>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,
-                         (const float*)dZ, lddz, n, G);
-    if (items)
-      hipLaunchKernelGGL(k_dw1_heavy_items<float>, dim3(gi), dim3(1024), 0, s, col_ptr, csc_row,
-                         csc_val, heavy_n, items, (const float*)dZ, lddz, n, G);
-    else
-      hipLaunchKernelGGL(k_dw1_heavy<float>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col,
-                         D, (const float*)dZ, lddz, n, G);
+  // deterministic (heavy_slab != null): multi-item columns through the slab and an ordered sum;
+  // without the item list every column is summed by one wave
+  const bool serial = heavy_slab && !items;
+  const int mode = serial ? (light ? 1 : 2) : 0;
+#define DSSM_DW1(T)                                                                             \
+  if (light || serial)                                                                          \
+    hipLaunchKernelGGL(k_dw1_light<T>, g1, block, 0, s, col_ptr, csc_row, csc_val, D,           \
+                       (const T*)dZ, lddz, n, G, mode);                                         \
+  if (items) {                                                                                  \
+    hipLaunchKernelGGL(k_dw1_heavy_items<T>, dim3(gi), dim3(1024), 0, s, col_ptr, csc_row,      \
+                       csc_val, heavy_n, items, (const T*)dZ, lddz, n, G, heavy_slab);          \
+    if (heavy_slab)                                                                             \
+      hipLaunchKernelGGL(k_dw1_heavy_reduce, dim3(gi), dim3(256), 0, s, col_ptr, heavy_n,       \
+                         items, n, heavy_slab, G);                                              \
+  } else if (!serial) {                                                                         \
+    hipLaunchKernelGGL(k_dw1_heavy<T>, g2, block, 0, s, col_ptr, csc_row, csc_val, csc_col, D,  \
+                       (const T*)dZ, lddz, n, G);                                               \
   }
+  if (dz_bf16) {
+    DSSM_DW1(u16)
+  } else {
+    DSSM_DW1(float)
+  }
+#undef DSSM_DW1
   return hipGetLastError();
 }
 

@@ -303,13 +303,19 @@ class DSSM:
               "graph_probe_read")
         return float(ms.value)
 
-    def check(self, stream=None):
-        """Synchronize and raise if a persistent dense kernel reported a device-side failure."""
-        check(self.lib.dssm_plan_check(self._plan, stream_ptr(stream)), "plan_check")
+    def set_option(self, name: str, value: bool):
+        """Choose a schedule alternative (dssm_plan_set_option; OPTIONS in _lib): applies to the
+        steps enqueued and graphs captured afterwards.  The plan never reads the environment."""
+        check(self.lib.dssm_plan_set_option(self._plan, _lib.OPTIONS[name], 1 if value else 0),
+              f"set_option {name}")
+        if name == "FUSED_W1_ADAM":
+            self.fused_w1_adam = bool(value)
 
-    @property
-    def dense_persistent(self) -> bool:
-        return bool(self.lib.dssm_plan_dense_enabled(self._plan))
+    def get_option(self, name: str) -> bool:
+        v = int(self.lib.dssm_plan_get_option(self._plan, _lib.OPTIONS[name]))
+        if v < 0:
+            raise _lib.DssmError(f"bad option {name}")
+        return bool(v)
 
     @property
     def fused_stats(self) -> bool:

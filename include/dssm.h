@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DSSM_ABI_VERSION 1
+#define DSSM_ABI_VERSION 2
 #define DSSM_MAX_LAYERS 8
 
 enum { DSSM_OK = 0, DSSM_E_INVALID = -1, DSSM_E_HIP = -2, DSSM_E_RCCL = -3, DSSM_E_UNSUPPORTED = -4 };
@@ -72,9 +72,7 @@ enum {
   DSSM_BUF_BATCH_MEAN,      /* float[2*n_l]: batch mean, tower q then d (new_dssm.py:77) */
   DSSM_BUF_BATCH_VAR,       /* float[2*n_l] */
   DSSM_BUF_DZ,              /* dZ of layer `layer` (compute dtype, R*ldp) */
-  DSSM_BUF_DENSE_TIMING,    /* uint64[2][64] phase stamps of the persistent dense kernels
-                               (100 MHz clock; written only when DSSM_DENSE_TIMING=1) */
-  DSSM_BUF_A,               /* post-BN/ReLU activation of layer `layer` (R*ldp): the next product's
+  DSSM_BUF_A = 11,          /* post-BN/ReLU activation of layer `layer` (R*ldp): the next product's
                                operand, bf16 in bf16 mode; fp32 embeddings for the last layer */
   DSSM_BUF_DA,              /* float[R*ldp(n_l)] d loss / d A of layer `layer` (the last: dy) */
   DSSM_BUF_COUNT
@@ -119,12 +117,46 @@ int dssm_plan_backward(dssm_plan* plan, void* stream);
 int dssm_plan_adam(dssm_plan* plan, float grad_scale, void* stream);
 int dssm_plan_set_adam_state(dssm_plan* plan, float beta1_power, float beta2_power, void* stream);
 int dssm_plan_get_adam_state(dssm_plan* plan, float* beta1_power, float* beta2_power, void* stream);
-/* Single-GPU fast path (default on): backward leaves the light rows of dW1 un-materialized and
- * dssm_plan_adam computes them inline from the CSC transpose while updating W1, so a dense dW1 is
- * never written or re-read; the split-K partial slabs of dW_l (l >= 2) are likewise summed inside
- * the Adam step instead of by a reduce launch.  Turn it off when the gradient arena must hold
- * the full gradient (data-parallel all-reduce, or inspecting the gradients). */
+/* Single-GPU fast path (default on; = dssm_plan_set_option(DSSM_OPT_FUSED_W1_ADAM)): backward
+ * leaves the light rows of dW1 un-materialized and dssm_plan_adam computes them inline from the CSC
+ * transpose while updating W1, so a dense dW1 is never written or re-read; the split-K partial
+ * slabs of dW_l (l >= 2) are likewise summed inside the Adam step instead of by a reduce launch.
+ * Turn it off when the gradient arena must hold the full gradient (data-parallel exchange, or
+ * inspecting the gradients). */
 int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
+/* Schedule options.  The plan never reads the environment: every alternative schedule is chosen
+ * here, explicitly, and applies to the steps enqueued (or graphs captured) afterwards.  Defaults
+ * are the measured-fastest schedule; the alternatives stay for parity tests and
+ * for shapes the defaults do not support (a default the shape cannot run falls back by itself:
+ * dssm_plan_schedule() reports what a step runs).
+ *   FUSED_STATS     1: BN statistics fused into producers / consumers (bf16, BS % 64 == 0,
+ *                      widths <= 512); 0: separate fixed-order statistics launches
+ *   MERGED_CSC      1: the rank transpose's scan / scatter ride in the forward's launches
+ *                      (with FUSED_STATS, BS % 128 == 0)
+ *   HEAVY_IN_ADAM   1: dW1's heavy columns as work items inside the Adam launch
+ *   SCATTER_IN_COS  1: the transpose's scatter as workgroups of the cosine launch (with MERGED_CSC)
+ *   DW_IN_APPLY     1: dW_l split-K tiles inside the next BN-backward apply launch (FUSED_STATS)
+ *   WIRE_GRAD_PASS  1: data parallel bf16 wire: dW1 written straight into the wire
+ *   CSC_RANK        1: rank / scan / scatter transpose (D <= ~38k); 0: histogram / fill launches
+ *   DETERMINISTIC   0; 1: fixed-order reductions only (separate statistics launches, every CSC
+ *                      column in row order, heavy dW1 rows summed in item order): repeated runs
+ *                      from the same state and batches are bit-identical
+ *   FUSED_W1_ADAM   see dssm_plan_set_fused_w1_adam */
+enum {
+  DSSM_OPT_FUSED_STATS = 0,
+  DSSM_OPT_MERGED_CSC,
+  DSSM_OPT_HEAVY_IN_ADAM,
+  DSSM_OPT_SCATTER_IN_COS,
+  DSSM_OPT_DW_IN_APPLY,
+  DSSM_OPT_WIRE_GRAD_PASS,
+  DSSM_OPT_CSC_RANK,
+  DSSM_OPT_DETERMINISTIC,
+  DSSM_OPT_FUSED_W1_ADAM,
+  DSSM_OPT_COUNT
+};
+int dssm_plan_set_option(dssm_plan* plan, int option, int value);
+/* The option's value (0 / 1), or -1 for a bad plan / option. */
+int dssm_plan_get_option(const dssm_plan* plan, int option);
 /* Sharded optimizer step (data parallel, ZeRO-1 style): dssm_plan_adam updates only arena
  * elements [begin, end) (multiples of 4; [0, param_count) restores the full step) -- the rank's
  * shard of a reduce-scattered gradient -- together with the bf16 shadows of those elements.  The
@@ -173,16 +205,9 @@ int dssm_plan_graph_build_steps(dssm_plan* plan, const int32_t* const* indptrs,
 enum { DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC, DSSM_PROBE_COUNT };
 int dssm_plan_probe_enable(dssm_plan* plan, int probe_id, int max_samples);
 int dssm_plan_probe_read(dssm_plan* plan, int probe_id, float* total_ms, int* count);
-/* Synchronize the stream and report a device-side failure of the persistent dense kernels
- * (a grid barrier that timed out: the step's results are invalid; the barrier is re-armed). */
-int dssm_plan_check(dssm_plan* plan, void* stream);
-/* The persistent kernels' grid size (> 0) when the bf16 plan runs the dense stack as the two
- * persistent kernels (dense.hip), 0 when
- * it uses per-op launches (fp32 mode, unsupported shapes, or DSSM_DENSE=0). */
-int dssm_plan_dense_enabled(dssm_plan* plan);
-/* 1 when the plan's bf16 train steps run the per-op schedule with the batch-norm statistics
- * fused into the producing / consuming kernels (DSSM_FUSED_STATS, default on where supported:
- * bf16, query_bs % 64 == 0, widths <= 512), else 0. */
+/* 1 when the plan's bf16 train steps run with the batch-norm statistics fused into the producing /
+ * consuming kernels (DSSM_OPT_FUSED_STATS, default on where supported: bf16, query_bs % 64 == 0,
+ * widths <= 512, not DETERMINISTIC), else 0. */
 int dssm_plan_fused_stats(dssm_plan* plan);
 /* What a train step of this plan runs (bit set of DSSM_SCHED_*), for tests and reports that
  * must know which kernels produced a result. */

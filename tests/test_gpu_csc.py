@@ -1,5 +1,5 @@
 """The CSC transpose (spmm.hip: k_csc_rank -> k_csc_scan_multi -> k_csc_scatter) against the
-legacy histogram / single-block scan / fill launches (DSSM_CSC_LEGACY=1) it replaced.
+legacy histogram / single-block scan / fill launches (plan option CSC_RANK = 0) it replaced.
 
 The transpose is observed through what consumes it: dW1 = [X | 1]^T dZ1 (light columns summed
 one wave per column, heavy columns by 64-entry slices with fp32 atomics). Both transposes order
@@ -33,15 +33,8 @@ CASES = [
 def _model(case, legacy, p):
     from dssm_amd.model import DSSM
     D, widths, BS, NEG, _ = case
-    old = os.environ.get("DSSM_CSC_LEGACY")
-    os.environ["DSSM_CSC_LEGACY"] = "1" if legacy else "0"
-    try:
-        m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
-    finally:
-        if old is None:
-            os.environ.pop("DSSM_CSC_LEGACY")
-        else:
-            os.environ["DSSM_CSC_LEGACY"] = old
+    m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
+    m.set_option("CSC_RANK", not legacy)
     m.load_params(p)
     m.set_fused_w1_adam(False)
     return m
@@ -59,8 +52,6 @@ def test_rank_transpose_matches_legacy_transpose(case):
             m.set_batch(batch)
             m.forward(True)
             m.backward()
-        a.check()
-        b.check()
         torch.cuda.synchronize()
         assert a.loss_accuracy()[0] == b.loss_accuracy()[0]
         ga = a.named_grads()["W1"].cpu().numpy()

@@ -1,5 +1,5 @@
 """The fused-statistics per-op schedule (csrc/bnfuse.h, default for bf16 train steps) against the
-separate statistics launches (DSSM_FUSED_STATS=0) and the oracle.
+separate statistics launches (plan option FUSED_STATS = 0) and the oracle.
 
 The fused schedule computes the same batch-norm quantities from fp64 column sums (E[z^2] - mean^2)
 accumulated by the kernels that produce each layer, where the separate launches merge fp32
@@ -15,7 +15,6 @@ test_gpu_dense.py uses:
 
 Against the float64 oracle, the bf16 bars of test_gpu_parity apply.
 """
-import os
 import re
 
 import numpy as np
@@ -37,24 +36,13 @@ CASES = [
 ]
 
 
-def _model(case, fused: bool, p, spmm_stats: bool = False):
+def _model(case, fused: bool, p):
     from dssm_amd.model import DSSM
     D, widths, BS, NEG = case
-    saved = {k: os.environ.get(k) for k in ("DSSM_DENSE", "DSSM_FUSED_STATS", "DSSM_SPMM_STATS")}
-    os.environ["DSSM_DENSE"] = "0"
-    os.environ["DSSM_FUSED_STATS"] = "1" if fused else "0"
-    os.environ["DSSM_SPMM_STATS"] = "1" if spmm_stats else "0"
-    try:
-        m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
+    m.set_option("FUSED_STATS", fused)
     m.load_params(p)
     m.set_fused_w1_adam(False)
-    assert not m.dense_persistent
     assert m.fused_stats == fused
     return m
 
@@ -63,14 +51,13 @@ def _is_bias(k):
     return re.fullmatch(r"b\d+", k) is not None
 
 
-@pytest.mark.parametrize("spmm_stats", [False, True], ids=["bn1-launch", "bn1-in-spmm"])
 @pytest.mark.parametrize("case", CASES)
-def test_fused_stats_match_separate_launches_and_oracle(case, spmm_stats):
+def test_fused_stats_match_separate_launches_and_oracle(case):
     D, widths, BS, NEG = case
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
     p = O.init_params(cfg, seed=21)
     batch = synth_batch(D, BS, NEG, seed=99, mean_nnz=24)
-    a, b = _model(case, True, p, spmm_stats), _model(case, False, p)
+    a, b = _model(case, True, p), _model(case, False, p)
     for m in (a, b):
         m.set_batch(batch)
         m.forward(True)
@@ -142,19 +129,12 @@ def test_fused_stats_training_steps_track_separate_launches():
 
 def test_fused_stats_unsupported_batch_falls_back():
     from dssm_amd.model import DSSM
-    old = os.environ.pop("DSSM_DENSE", None)
-    os.environ["DSSM_DENSE"] = "0"
-    try:
-        m = DSSM(1000, (64, 32), 48, 4, dtype="bf16")  # 48 % 64 != 0: tiles would straddle towers
-        assert not m.fused_stats
-        m2 = DSSM(1000, (64, 32), 64, 4, dtype="bf16")
-        assert m2.fused_stats
-        m3 = DSSM(1000, (64, 32), 64, 4, dtype="fp32")
-        assert not m3.fused_stats
-    finally:
-        os.environ.pop("DSSM_DENSE", None)
-        if old is not None:
-            os.environ["DSSM_DENSE"] = old
+    m = DSSM(1000, (64, 32), 48, 4, dtype="bf16")  # 48 % 64 != 0: tiles would straddle towers
+    assert not m.fused_stats
+    m2 = DSSM(1000, (64, 32), 64, 4, dtype="bf16")
+    assert m2.fused_stats
+    m3 = DSSM(1000, (64, 32), 64, 4, dtype="fp32")
+    assert not m3.fused_stats
 
 
 def test_train_forward_without_backward_reports_its_loss():

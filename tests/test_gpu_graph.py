@@ -153,25 +153,3 @@ def test_multi_step_graph_matches_eager(case):
     d = (ea.params - gr.params).abs()
     assert float(d.max()) <= 2 * k * lr, float(d.max())
     assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
-
-
-def test_flat_spread_option_matches_default(monkeypatch):
-    """DSSM_FLAT_SPREAD (opt-in): the untouched W1 rows' Adam update rides in the step's NT GEMM /
-    cosine / BN-apply launches instead of the Adam launch -- same arithmetic (flat.h's adam1), so a
-    teacher-forced step matches the default schedule at the graph test's bar."""
-    D, widths, BS, NEG, dtype, fused = CASES[1]
-    lr = 0.01
-    _, _, ref = make(D, widths, BS, NEG, dtype, fused=fused)
-    monkeypatch.setenv("DSSM_FLAT_SPREAD", "64,128,256")
-    _, _, sp = make(D, widths, BS, NEG, dtype, fused=fused)
-    for i, hb in enumerate(_batches(D, BS, NEG, 3)):
-        _copy_state(sp, ref)
-        for m in (ref, sp):
-            m.set_batch(hb)
-            m.train_step()
-        torch.cuda.synchronize()
-        assert ref.loss_accuracy()[0] == sp.loss_accuracy()[0]
-        d = (ref.params - sp.params).abs()
-        assert float(d.max()) <= 2 * lr, (i, float(d.max()))
-        assert float((d <= 1e-5).float().mean()) >= 0.999
-        assert ref.beta_powers() == sp.beta_powers()

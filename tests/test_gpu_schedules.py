@@ -1,11 +1,11 @@
 """The step's launch schedules against each other (same arithmetic, different launches).
 
-Two placements of work are plan options, read when the plan is created:
+Two placements of work are plan options (dssm_plan_set_option):
 
-* DSSM_DW_IN_APPLY: dW_l's split-K tiles run in the BN_{l-1} backward-apply launch (default,
-  tn.h tn_chunk_body, 64 x 64 tiles) or in the backward pair launch (=0, 128 x 64 tiles);
-* DSSM_SCATTER_IN_COS: the CSC transpose's scatter runs as a role of the cosine launch
-  (default, csc.h) or beside the BN1 sums (=0).
+* DW_IN_APPLY: dW_l's split-K tiles run in the BN_{l-1} backward-apply launch (default,
+  tn.h tn_chunk_body, 64 x 64 tiles) or in the backward pair launch (0, 128 x 64 tiles);
+* SCATTER_IN_COS: the CSC transpose's scatter runs as a role of the cosine launch
+  (default, csc.h) or beside the BN1 sums (0).
 
 Both tile shapes sum every split in the same k order, and the scatter writes every entry to
 the slot its rank reserved, so the schedules compute the same step.  The check is teacher-forced
@@ -28,8 +28,8 @@ from tests.test_gpu_parity import make
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [{"DSSM_DW_IN_APPLY": "0"}, {"DSSM_SCATTER_IN_COS": "0"},
-            {"DSSM_DW_IN_APPLY": "0", "DSSM_SCATTER_IN_COS": "0"}]
+VARIANTS = [{"DW_IN_APPLY": False}, {"SCATTER_IN_COS": False},
+            {"DW_IN_APPLY": False, "SCATTER_IN_COS": False}]
 CASES = [
     # (D, widths, BS, NEG, fused); BS a multiple of 128: the whole-K backward pair path
     (5000, (300, 300, 128), 128, 4, True),
@@ -47,15 +47,13 @@ def _copy_state(dst, src):
 
 @pytest.mark.parametrize("variant", VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
 @pytest.mark.parametrize("case", CASES)
-def test_schedule_matches_default(case, variant, monkeypatch):
+def test_schedule_matches_default(case, variant):
     D, widths, BS, NEG, fused = case
     lr, steps = 0.01, 3
     _, _, ref = make(D, widths, BS, NEG, "bf16", fused=fused)
-    for k, x in variant.items():
-        monkeypatch.setenv(k, x)
     _, _, var = make(D, widths, BS, NEG, "bf16", fused=fused)
-    for k in variant:
-        monkeypatch.delenv(k)
+    for k, x in variant.items():
+        var.set_option(k, x)
     batches = [synth_batch(D, BS, NEG, seed=3000 + i, mean_nnz=32) for i in range(steps)]
     for i, hb in enumerate(batches):
         _copy_state(var, ref)

@@ -41,14 +41,14 @@ def _close(a, b):
 
 @pytest.mark.parametrize("bs", [BS, 128])
 @pytest.mark.parametrize("shard,grad_pass", [("all", "1"), ("first_half", "1"), ("all", "0")])
-def test_wire_step_matches_unwired(shard, grad_pass, bs, monkeypatch):
+def test_wire_step_matches_unwired(shard, grad_pass, bs):
     """grad_pass 1 (default): dW1 straight into the wire by k_adam_step's W1 roles; 0: materialised
     dW1 + k_wire_pack.  bs 128 (a multiple of 128) takes the whole-K backward pair, whose dW_l tiles
     ride in the apply launches with the slabs reduced after them (the data-parallel schedule)."""
     BS = bs
-    monkeypatch.setenv("DSSM_WIRE_GRAD_PASS", grad_pass)
     _, _, ref = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
     _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    m.set_option("WIRE_GRAD_PASS", grad_pass == "1")
     ext, gw, pw = _wired(m)
     end = ext if shard == "all" else (ext // 2) // 64 * 64
     m.set_adam_range(0, end)
