@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--batches", type=int, default=8, help="distinct staged batches per rank")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--allreduce", default="torch", choices=["torch", "rccl"])
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
+                    help="N>1 transport: rccl = libdssm.so's own RCCL communicator (default on GPUs), "
+                         "torch = torch.distributed collectives")
     ap.add_argument("--dp-mode", default="auto", choices=["auto", "zero", "allreduce"],
                     help="N>1 exchange: zero = reduce-scatter + sharded Adam + all-gather "
                          "(default with torch.distributed), allreduce = all-reduce + replicated Adam")
@@ -79,7 +81,7 @@ def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int) -> int:
 
 
 def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: int, rows: int,
-                   n1: int, range_elems: int = None, wire_elems: int = 0) -> int:
+                   n1: int, range_elems: int = None, wire_elems: int = 0, wire_parts: int = 1) -> int:
     """Algorithmic bytes of one k_adam_step launch.
 
     Every updated element streams p, m, v in and out (24 B).  Its gradient is read as fp32 (4 B),
@@ -87,7 +89,8 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
     gathers it from the CSC transpose instead, (index, value) 8 B + one bf16 dZ1 row (2 n1 B) per
     entry, over nnz + rows entries (the ones column gives db1) -- the SpMM-backward bytes of
     SURVEY §8(d) minus its dense dW1 write; (b) data-parallel bf16 wire: the rank's W1 shard
-    reads a bf16 gradient (2 B) and writes a bf16 parameter copy (2 B).  bf16 mode adds 2 B per
+    reads wire_parts bf16 partial gradients (2 B each: one per rank after the all-to-all) and
+    writes a bf16 parameter copy (2 B).  bf16 mode adds 2 B per
     weight element written to its shadows (W_l for l >= 2 also transposed: 4 B)."""
     if range_elems is None:
         range_elems = n_params
@@ -95,7 +98,7 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
     if fused:
         b += 4 * (n_params - w1_elems) + (nnz + rows) * (8 + 2 * n1)
     else:
-        b += 4 * (range_elems - wire_elems) + 4 * wire_elems
+        b += 4 * (range_elems - wire_elems) + (2 * wire_parts + 2) * wire_elems
     if bf16:
         sh_w1 = (w1_elems - n1) if fused else 0  # W1's shadow (bias row excluded); wired: from the wire
         sh_rest = sum(2 * WIDTHS[l - 1] * WIDTHS[l] for l in range(1, len(WIDTHS)))
@@ -105,24 +108,38 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
     return int(b)
 
 
-# probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py)
-PMC_KERNELS = {"adam": "k_adam_step<{t}>", "spmm_fwd": "k_spmm_scan<{t}>"}  # the SpMM rides in k_spmm_scan
+# probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py):
+# bf16 steps run the SpMM inside k_spmm_scan (merged transpose), fp32 steps as k_spmm_fwd
+PMC_KERNELS = {"bf16": {"adam": "k_adam_step<unsigned short>", "spmm_fwd": "k_spmm_scan<unsigned short>"},
+               "fp32": {"adam": "k_adam_step<float>", "spmm_fwd": "k_spmm_fwd<float>"}}
+# the workload a traffic summary without a "_workload" record was collected on (r01: the default
+# single-GPU bench line)
+DEFAULT_WORKLOAD = {"dtype": "bf16", "columns": "zipf", "feed": "device"}
 
 
-def pmc_traffic(dtype: str):
+def pmc_traffic(workload: dict):
     """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) from the newest
-    committed profiles/*_traffic.json; PMC counters cannot be read from inside the timed run."""
+    committed profiles/r*_traffic.json collected on THIS workload (dtype, column distribution,
+    feed); PMC counters cannot be read from inside the timed run.  No matching summary: none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-    if not files or dtype != "bf16":
-        return {}, None
-    d = json.load(open(files[-1]))
-    out = {}
-    for probe, kname in PMC_KERNELS.items():
-        k = kname.format(t="unsigned short")
-        if k in d:
-            out[probe] = d[k]["hbm_bytes"]
-    return out, os.path.relpath(files[-1], ROOT)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("_workload", DEFAULT_WORKLOAD) != workload:
+            continue
+        out = {probe: d[k]["hbm_bytes"] for probe, k in PMC_KERNELS[workload["dtype"]].items() if k in d}
+        return out, os.path.relpath(f, ROOT)
+    return {}, None
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(seconds: float):
@@ -312,9 +329,7 @@ def main():
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
-        dp = DataParallel(model, comm="rccl" if args.allreduce == "rccl" else "torch",
-                          mode="allreduce" if args.allreduce == "rccl" else args.dp_mode,
-                          wire=args.wire)
+        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire)
     rehearse = args.rehearse_world if world == 1 else 1
     if rehearse > 1:
         # rank 0's kernels of a W-rank bf16-wire step; the reduce-scatter / all-reduce / all-gather
@@ -325,6 +340,8 @@ def main():
         wires = [torch.zeros(shard * rehearse, dtype=torch.bfloat16, device=dev) for _ in range(2)]
         wires[1][:ext].copy_(model.params[:ext])
         model.set_wire(*wires)
+        stage = torch.zeros(shard * rehearse, dtype=torch.bfloat16, device=dev)  # the all-to-all's output
+        model.set_wire_stage(stage, rehearse, shard)
         model.set_adam_range(0, min(shard, ext))
 
     cols = ZipfColumns(D, uniform=args.columns == "uniform")
@@ -487,24 +504,27 @@ def main():
     n_params = int(model.n_params)
     w1_elems = (D + 1) * WIDTHS[0]
     fused = world == 1 and rehearse == 1
-    wire_elems, range_elems = 0, n_params
+    wire_elems, range_elems, wire_parts = 0, n_params, 1
     if dp is not None and dp.mode == "zero":
         if dp.wire == "bf16":
             wire_elems = max(0, dp.end - dp.begin)
             range_elems = wire_elems + (n_params - dp.extent)
+            wire_parts = world
         else:
             range_elems = max(0, dp.end - dp.begin)
     elif rehearse > 1:
         ext = D * WIDTHS[0]
         wire_elems = min(-(-ext // (64 * rehearse)) * 64, ext)
         range_elems = wire_elems + (n_params - ext)
+        wire_parts = rehearse
     kern = {
         "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
         "adam": (adam_alg_bytes(n_params, args.dtype == "bf16", fused, w1_elems, nnz_avg, rows,
-                                WIDTHS[0], range_elems, wire_elems), probes.get("adam", 0.0)),
+                                WIDTHS[0], range_elems, wire_elems, wire_parts), probes.get("adam", 0.0)),
     }
-    # the committed PMC summary profiles the default single-GPU step (fused Adam) only
-    traffic, traffic_src = pmc_traffic(args.dtype) if fused else ({}, None)
+    # committed PMC summaries profile single-GPU steps (fused Adam) of a named workload
+    workload = {"dtype": args.dtype, "columns": args.columns, "feed": args.feed}
+    traffic, traffic_src = pmc_traffic(workload) if fused else ({}, None)
     rl = {}
     for k, (byt, ms) in kern.items():
         gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -524,7 +544,8 @@ def main():
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
-                   "dp_exchange": (f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) if dp is not None else None,
+                   "dp_exchange": ((f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) + f" via {dp.comm}")
+                                  if dp is not None else None,
                    "feed": "host CSR -> pinned async H2D (native feeder), PCIe inside the timed region"
                            if feeder is not None else "device-resident staged batches"},
         "roofline": dict(rl[dominant], kernel=dominant),
@@ -542,14 +563,15 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"]["cpu_model"] = cpu_model()
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": repr(e)}
     if feeder is not None:
         feeder.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dp is not None and dp.comm is not None:
-        dp.comm.destroy()
+    if dp is not None:
+        dp.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -87,6 +87,7 @@ _SIGS = {
     "dssm_plan_wire_extent": (C.c_int64, [_P]),
     "dssm_plan_set_wire": (C.c_int, [_P, _P, _P, C.c_int64]),
     "dssm_plan_wire_shadows": (C.c_int, [_P, _P]),
+    "dssm_plan_set_wire_stage": (C.c_int, [_P, _P, C.c_int, C.c_int64]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),
     "dssm_plan_probe_read": (C.c_int, [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
     "dssm_spmm_csr_fwd": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,
@@ -141,6 +142,11 @@ _SIGS = {
     "dssm_comm_unique_id": (C.c_int, [_P]),
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),
+    "dssm_comm_world": (C.c_int, []),
+    "dssm_allreduce_sum": (C.c_int, [_P, C.c_int64, C.c_int, _P]),
+    "dssm_reduce_scatter_sum": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
+    "dssm_all_gather": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
+    "dssm_all_to_all": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_comm_destroy": (C.c_int, []),
 }
 

@@ -322,7 +322,18 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       const bool wired = i < a.wire4;
       float4 pp = ld_stream4(a.p + i * 4);
       float4 gg;
-      if (wired) {
+      if (wired && a.gstage) {
+        // one bf16 rounding per rank's gradient, the sum over ranks in fp32 (fixed rank order)
+        gg = make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint2* st = reinterpret_cast<const uint2*>(a.gstage) + (i - a.gbase4);
+        for (int k = 0; k < a.gparts; ++k) {
+          const uint2 q = st[(int64_t)k * (a.gstride / 4)];
+          gg.x += __uint_as_float(q.x << 16);
+          gg.y += __uint_as_float(q.x & 0xffff0000u);
+          gg.z += __uint_as_float(q.y << 16);
+          gg.w += __uint_as_float(q.y & 0xffff0000u);
+        }
+      } else if (wired) {
         const uint2 q = reinterpret_cast<const uint2*>(a.gwire)[i];
         gg = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                          __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));

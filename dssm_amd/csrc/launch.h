@@ -245,6 +245,11 @@ struct AdamStep {
   const uint16_t* gwire;
   uint16_t* pwire;
   int64_t wire4;
+  // all-to-all wire: the W1 gradient of float4 i (< wire4) is the fp32 sum of gparts bf16 partials
+  // gstage[k * gstride + 4 * (i - gbase4)] (k = 0, 1, ...: fixed order), instead of gwire[i]
+  const uint16_t* gstage;
+  int gparts;
+  int64_t gstride, gbase4;
   int64_t t4_begin, t4_end;
   // deterministic mode: a multi-item heavy column's items store their partial rows here ([item][n],
   // write-through) and its last arrival sums them in item order (no fp32 atomics)

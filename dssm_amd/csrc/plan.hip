@@ -195,6 +195,11 @@ struct dssm_plan {
   // the reduce-scatter / all-gather; arena elements [0, wire_end) are W1's rows
   uint16_t* gwire = nullptr;
   uint16_t* pwire = nullptr;
+  // all-to-all wire (dssm_plan_set_wire_stage): the rank's W1 shard gradient as gparts bf16
+  // partial copies (one per rank) gstride apart, summed in fp32 by the Adam launch
+  const uint16_t* gstage = nullptr;
+  int gparts = 0;
+  int64_t gstride = 0;
   int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
@@ -878,6 +883,14 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     a.gwire = P->gwire;
     a.pwire = P->pwire;
     a.wire4 = we / 4;
+    if (P->gstage) {
+      if (P->gstride < P->adam_end - P->adam_begin)
+        return fail(DSSM_E_INVALID, "wire stage stride shorter than the Adam range");
+      a.gstage = P->gstage;
+      a.gparts = P->gparts;
+      a.gstride = P->gstride;
+      a.gbase4 = P->adam_begin / 4;
+    }
     // the tail's gradient is consumed here; clear it (b1's row is the gradient pass's atomic target)
     if (wire_gradient_pass(P)) a.clear_from = we;
     for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
@@ -936,6 +949,22 @@ int dssm_plan_set_wire(dssm_plan* P, uint16_t* grad_wire, uint16_t* param_wire, 
     return fail(DSSM_E_INVALID, "wire buffers must be 8-byte aligned");
   P->gwire = grad_wire;
   P->pwire = param_wire;
+  return DSSM_OK;
+}
+
+int dssm_plan_set_wire_stage(dssm_plan* P, const uint16_t* stage, int parts, int64_t stride) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!stage) {
+    P->gstage = nullptr;
+    P->gparts = 0;
+    return DSSM_OK;
+  }
+  if (parts < 1 || parts > 64 || stride < 0 || (stride % 4) ||
+      (reinterpret_cast<uintptr_t>(stage) & 7))
+    return fail(DSSM_E_INVALID, "wire stage: 1..64 parts, stride a multiple of 4, 8-B aligned");
+  P->gstage = stage;
+  P->gparts = parts;
+  P->gstride = stride;
   return DSSM_OK;
 }
 
@@ -1219,13 +1248,27 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
 }
 
 // ---- RCCL ---------------------------------------------------------------------------------
+// The library's own communicator (one per process: one process per GPU).  Collectives are
+// enqueued on the caller's stream, between the step's graphs.
 static ncclComm_t g_comm = nullptr;
+static int g_rank = 0, g_world = 0;
+
+static bool nccl_type(int dtype, ncclDataType_t* t, size_t* es) {
+  if (dtype == DSSM_F32) { *t = ncclFloat32; *es = 4; return true; }
+  if (dtype == DSSM_BF16) { *t = ncclBfloat16; *es = 2; return true; }
+  return false;
+}
+
+#define RCCL_TRY(expr)                                                                    \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess) return fail(DSSM_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
 
 int dssm_comm_unique_id(void* out128) {
   if (!out128) return fail(DSSM_E_INVALID, "null id buffer");
   ncclUniqueId id;
-  ncclResult_t r = ncclGetUniqueId(&id);
-  if (r != ncclSuccess) return fail(DSSM_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  RCCL_TRY(ncclGetUniqueId(&id));
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   std::memcpy(out128, &id, 128);
   return DSSM_OK;
@@ -1242,14 +1285,71 @@ int dssm_comm_init(int rank, int world, const void* unique_id128) {
     g_comm = nullptr;
     return fail(DSSM_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
+  g_rank = rank;
+  g_world = world;
+  return DSSM_OK;
+}
+
+int dssm_comm_world(void) { return g_comm ? g_world : 0; }
+
+int dssm_allreduce_sum(void* buf, int64_t count, int dtype, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t;
+  size_t es;
+  if (!buf || count < 0 || !nccl_type(dtype, &t, &es)) return fail(DSSM_E_INVALID, "dssm_allreduce_sum: bad arguments");
+  RCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, t, ncclSum, g_comm, (hipStream_t)stream));
   return DSSM_OK;
 }
 
 int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream) {
+  return dssm_allreduce_sum(buf, count, DSSM_F32, stream);
+}
+
+int dssm_reduce_scatter_sum(const void* send, void* recv, int64_t count, int dtype, void* stream) {
   if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
-  ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, g_comm,
-                                 (hipStream_t)stream);
-  if (r != ncclSuccess) return fail(DSSM_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  ncclDataType_t t;
+  size_t es;
+  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es))
+    return fail(DSSM_E_INVALID, "dssm_reduce_scatter_sum: bad arguments");
+  RCCL_TRY(ncclReduceScatter(send, recv, (size_t)count, t, ncclSum, g_comm, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t;
+  size_t es;
+  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es))
+    return fail(DSSM_E_INVALID, "dssm_all_gather: bad arguments");
+  RCCL_TRY(ncclAllGather(send, recv, (size_t)count, t, g_comm, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t;
+  size_t es;
+  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es) || send == recv)
+    return fail(DSSM_E_INVALID, "dssm_all_to_all: bad arguments (distinct send / recv)");
+  hipStream_t s = (hipStream_t)stream;
+  const char* sp = static_cast<const char*>(send);
+  char* rp = static_cast<char*>(recv);
+  const size_t chunk = (size_t)count * es;
+  // the rank's own chunk by a device copy; every peer pair by one grouped send / recv (all xGMI
+  // links busy at once on a fully connected node: one step, not world - 1 ring steps)
+  HIP_TRY(hipMemcpyAsync(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk,
+                         hipMemcpyDeviceToDevice, s));
+  RCCL_TRY(ncclGroupStart());
+  for (int j = 0; j < g_world; ++j) {
+    if (j == g_rank) continue;
+    ncclResult_t r = ncclSend(sp + (size_t)j * chunk, (size_t)count, t, j, g_comm, s);
+    if (r == ncclSuccess) r = ncclRecv(rp + (size_t)j * chunk, (size_t)count, t, j, g_comm, s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return fail(DSSM_E_RCCL, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    }
+  }
+  RCCL_TRY(ncclGroupEnd());
   return DSSM_OK;
 }
 
@@ -1257,6 +1357,7 @@ int dssm_comm_destroy(void) {
   if (g_comm) {
     ncclCommDestroy(g_comm);
     g_comm = nullptr;
+    g_world = 0;
   }
   return DSSM_OK;
 }

@@ -253,6 +253,18 @@ class DSSM:
         n = min(grad_wire.numel(), param_wire.numel())
         check(self.lib.dssm_plan_set_wire(self._plan, ptr(grad_wire), ptr(param_wire), n), "set_wire")
 
+    def set_wire_stage(self, stage: Optional[torch.Tensor], parts: int = 0, stride: int = 0):
+        """All-to-all wire (dssm_plan_set_wire_stage): apply_adam() takes the shard's W1 gradient
+        as the fp32 sum of `parts` bf16 partials stage[k*stride : k*stride + shard] (None: off)."""
+        if stage is None:
+            check(self.lib.dssm_plan_set_wire_stage(self._plan, None, 0, 0), "set_wire_stage")
+            return
+        if stage.dtype != torch.bfloat16 or not stage.is_contiguous() or stage.device != self.device:
+            raise ValueError("the wire stage is a contiguous bf16 tensor on the model's device")
+        if stage.numel() < parts * stride:
+            raise ValueError("wire stage too small")
+        check(self.lib.dssm_plan_set_wire_stage(self._plan, ptr(stage), int(parts), int(stride)), "set_wire_stage")
+
     def wire_shadows(self, stream=None):
         check(self.lib.dssm_plan_wire_shadows(self._plan, stream_ptr(stream)), "wire_shadows")
 

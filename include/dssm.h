@@ -180,6 +180,14 @@ int dssm_plan_set_adam_range(dssm_plan* plan, int64_t begin, int64_t end);
 int64_t dssm_plan_wire_extent(const dssm_plan* plan);
 int dssm_plan_set_wire(dssm_plan* plan, uint16_t* grad_wire, uint16_t* param_wire, int64_t count);
 int dssm_plan_wire_shadows(dssm_plan* plan, void* stream);
+/* All-to-all variant of the bf16 wire (the default data-parallel exchange, dssm_amd/dist.py):
+ * instead of a reduce-scattered grad_wire (rounded to bf16 at every ring hop), dssm_plan_adam
+ * takes the W1 shard's gradient as the fp32 sum, in rank order, of `parts` bf16 partial gradients
+ * stage[k * stride + (e - begin)] (k < parts, e in the Adam range [begin, end), stride >= end -
+ * begin, a multiple of 4): each rank's own gradient rounded once, then accumulated in fp32.  The
+ * stage is what dssm_all_to_all() of every rank's grad_wire (chunks of `stride`) delivers.
+ * NULL: off (the reduce-scattered grad_wire is read). */
+int dssm_plan_set_wire_stage(dssm_plan* plan, const uint16_t* stage, int parts, int64_t stride);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, void* stream);
 
@@ -293,11 +301,24 @@ int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, vo
 int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, int cols, float* dx,
                   int lddx, void* stream);
 
-/* ---- data parallel (one RCCL all-reduce of the gradient arena per step) ----------------- */
-/* unique_id: 128 bytes from dssm_comm_unique_id() on rank 0, shared by the caller. */
+/* ---- data parallel: the library's RCCL communicator ----------------------
+ * One communicator per process (one process per GPU).  unique_id: 128 bytes from
+ * dssm_comm_unique_id() on rank 0, shared by the caller (dssm_amd/dist.py broadcasts it through
+ * torch.distributed's store: bootstrap only, no data).  Collectives are asynchronous on `stream`
+ * and replace the reference's single-process optimizer (new_dssm.py:215-217) when the batch is
+ * sharded over ranks; dtype DSSM_F32 or DSSM_BF16 (summed by RCCL in that type).  count is per rank
+ * (reduce-scatter: recv count, send holds world * count; all-gather: send count; all-to-all: the
+ * chunk each pair of ranks exchanges, chunk j of send goes to rank j and chunk j of recv comes from
+ * rank j; send != recv).  In-place reduce-scatter / all-gather: recv == send + rank * count /
+ * send == recv + rank * count. */
 int dssm_comm_unique_id(void* out128);
 int dssm_comm_init(int rank, int world, const void* unique_id128);
+int dssm_comm_world(void);  /* world size, 0 before dssm_comm_init */
+int dssm_allreduce_sum(void* buf, int64_t count, int dtype, void* stream);
 int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
+int dssm_reduce_scatter_sum(const void* send, void* recv, int64_t count, int dtype, void* stream);
+int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void* stream);
+int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream);
 int dssm_comm_destroy(void);
 
 /* ---- host data path (utils/utils.py:20-24, 45-61, 368-437; new_dssm.py:26-49) ---------------

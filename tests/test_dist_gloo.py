@@ -1,12 +1,17 @@
-"""Data-parallel path on CPU: world_size 2 over gloo.
+"""Data-parallel path on CPU: world_size 2 and 4 over gloo.
 
-Each rank runs `dssm_amd.dist.DataParallel` (the product's DP step: forward, backward, one
-all-reduce of the flat gradient arena, Adam with grad_scale = 1/world). Its shard comes from
-`dssm_amd.data.shard_batch`. The per-rank compute engine is the C/OpenMP restatement
+Each rank runs `dssm_amd.dist.DataParallel` (the product's DP step: forward, backward, the
+gradient exchange of its schedule, Adam with grad_scale = 1/world) with the torch.distributed
+transport (gloo); on GPUs the same schedules run on libdssm.so's RCCL communicator.  Its shard
+comes from `dssm_amd.data.shard_batch`. The per-rank compute engine is the C/OpenMP restatement
 (oracle/cpu_c), a test stand-in for the device plan, so the host-side DP logic runs without a GPU.
 
-Parity definition (§8e): the 2-rank step equals the oracle's mean of the per-shard gradients
-followed by one Adam step. Both ranks end bit-identical. Each rank's EMA is its own shard's
+Schedules: "allreduce" (one fp32 all-reduce, replicated Adam), "zero" with the fp32 wire
+(reduce-scatter, sharded Adam, all-gather) and "zero" with the bf16 all-to-all wire (every rank
+receives the bf16 gradients of its shard from every rank and sums them in fp32 in rank order).
+
+Parity definition (§8e): the N-rank step equals the oracle's mean of the per-shard gradients
+followed by one Adam step. All ranks end bit-identical. Each rank's EMA is its own shard's
 (local BN statistics).
 """
 import os
@@ -28,15 +33,15 @@ cpu_c = pytest.importorskip("oracle.cpu_c")
 if not cpu_c.available():
     pytest.skip("gcc/OpenMP unavailable", allow_module_level=True)
 
-D, WIDTHS, BS, NEG, WORLD = 600, [64, 32], 32, 4, 2
+D, WIDTHS, BS, NEG = 600, [64, 32], 32, 4
 
 
 class CpuEngine:
     """The DSSM model interface DataParallel drives (forward/backward/arenas/apply_adam, the
     optimizer range and the shadow refresh of the zero schedule)."""
 
-    def __init__(self, params):
-        self.cpu = cpu_c.CpuDSSM(D, WIDTHS, BS // WORLD, NEG, params, pad_to=64 * WORLD)
+    def __init__(self, params, world):
+        self.cpu = cpu_c.CpuDSSM(D, WIDTHS, BS // world, NEG, params, pad_to=64 * world)
         self.n_params = self.cpu.total
         self.params = torch.from_numpy(self.cpu.flat["p"])  # flat arenas (padded), shared memory
         self.grads = torch.from_numpy(self.cpu.flat["g"])
@@ -44,7 +49,7 @@ class CpuEngine:
         self.adam_v = torch.from_numpy(self.cpu.flat["v"])
         self.range = (0, self.n_params)
         self._train = None
-        self.gwire = self.pwire = None
+        self.gwire = self.pwire = self.stage = None
 
     # bf16 wire (include/dssm.h dssm_plan_set_wire): W1's rows, arena [0, D*WIDTHS[0])
     def wire_extent(self):
@@ -52,6 +57,9 @@ class CpuEngine:
 
     def set_wire(self, gw, pw):
         self.gwire, self.pwire = gw, pw
+
+    def set_wire_stage(self, stage, parts, stride):
+        self.stage, self.parts, self.stride = stage, parts, stride
 
     def wire_shadows(self):
         pass  # fp32 engine: the bf16 W1 shadow is the parameter wire itself
@@ -84,7 +92,13 @@ class CpuEngine:
         b, e = self.range
         if self.gwire is not None:
             ext = self.wire_extent()
-            self.grads[b:e] = self.gwire[b:e].float()
+            if self.stage is not None:  # the all-to-all's partials of this shard, fp32 sum in rank order
+                acc = torch.zeros(e - b, dtype=torch.float32)
+                for k in range(self.parts):
+                    acc += self.stage[k * self.stride:k * self.stride + (e - b)].float()
+                self.grads[b:e] = acc
+            else:
+                self.grads[b:e] = self.gwire[b:e].float()
         self.cpu.adam(grad_scale)
         for r, old in keep.items():
             if self.gwire is not None:
@@ -103,18 +117,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, port, out_dir, mode, wire="fp32"):
+def _worker(rank, port, out_dir, mode, wire, world):
     os.environ["OMP_NUM_THREADS"] = "2"
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         cfg = O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS, neg=NEG)
         p0 = O.init_params(cfg, seed=9)
         glob = synth_batch(D, BS, NEG, seed=1234, mean_nnz=16)
-        eng = CpuEngine(p0)
-        dp = DataParallel(eng, comm="torch", mode=mode, wire=wire)
-        assert dp.world == WORLD and dp.rank == rank and dp.mode == mode
+        eng = CpuEngine(p0, world)
+        dp = DataParallel(eng, comm="auto", mode=mode, wire=wire)
+        assert dp.world == world and dp.rank == rank and dp.mode == mode and dp.comm == "torch"
         assert dp.wire == (wire if mode == "zero" else "fp32")
-        eng.set_batch(shard_batch(glob, BS, NEG, rank, WORLD))
+        eng.set_batch(shard_batch(glob, BS, NEG, rank, world))
         dp.train_step()
         dp.gather_state()
         np.save(os.path.join(out_dir, f"p{rank}.npy"), eng.cpu.flat["p"][:eng.n_params])
@@ -125,20 +139,23 @@ def _worker(rank, port, out_dir, mode, wire="fp32"):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("mode,wire", [("allreduce", "fp32"), ("zero", "fp32"), ("zero", "bf16")])
-def test_data_parallel_two_ranks_gloo(mode, wire):
-    """allreduce: all-reduce + replicated Adam; zero: reduce-scatter + Adam on the rank's shard +
-    all-gather of the parameters, with W1's rows on an fp32 or a bf16 wire. All must give the
-    same step (the bf16 wire within Adam's insensitivity to gradient rounding: a first step
+def test_data_parallel_gloo(mode, wire, world):
+    """allreduce: all-reduce + replicated Adam; zero: Adam on the rank's shard + all-gather of the
+    parameters, W1's rows on an fp32 (reduce-scatter) or a bf16 all-to-all wire. All must give
+    the same step (the bf16 wire within Adam's insensitivity to gradient rounding: a first step
     moves each element by lr * sign(g) wherever |g| >> eps)."""
+    WORLD = world
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d, mode, wire), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, mode, wire, world), nprocs=WORLD, join=True)
         p = [np.load(os.path.join(d, f"p{r}.npy")) for r in range(WORLD)]
         m_ = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(WORLD)]
         ema = [np.load(os.path.join(d, f"ema{r}.npy")) for r in range(WORLD)]
         loss = [float(np.load(os.path.join(d, f"loss{r}.npy"))[0]) for r in range(WORLD)]
-    np.testing.assert_array_equal(p[0], p[1])  # identical parameters on every rank
-    np.testing.assert_array_equal(m_[0], m_[1])  # and identical (gathered) Adam state
+    for r in range(1, WORLD):
+        np.testing.assert_array_equal(p[0], p[r])  # identical parameters on every rank
+        np.testing.assert_array_equal(m_[0], m_[r])  # and identical (gathered) Adam state
 
     # oracle: mean of the per-shard gradients, then one Adam step
     cfg_l = O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS // WORLD, neg=NEG)

@@ -101,3 +101,37 @@ def test_wire_shadows_equal_fp32_refresh():
     m.forward(False)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(m.fetch("cos_sim_raw"), a)
+
+
+@pytest.mark.parametrize("parts", [2, 4, 8])
+def test_wire_stage_sums_rank_partials_in_fp32(parts):
+    """The all-to-all wire (dssm_plan_set_wire_stage, the default data-parallel exchange): Adam
+    takes the shard's W1 gradient as the fp32 sum, in rank order, of `parts` bf16 partials (what
+    dssm_all_to_all delivers).  Against the unwired Adam over the same range fed that fp32 sum,
+    the shard's parameters and Adam slots are bit-identical."""
+    _, _, ref = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    ext, gw, pw = _wired(m)
+    stride = -(-ext // (64 * parts)) * 64
+    s0, s1 = stride, min(2 * stride, ext)  # the shard of rank 1
+    stage = torch.zeros(parts * stride, dtype=torch.bfloat16, device=m.device)
+    gen = torch.Generator(device=m.device).manual_seed(5)
+    for k in range(parts):  # rank k's bf16 gradient of this shard
+        stage[k * stride:k * stride + (s1 - s0)] = (
+            torch.randn(s1 - s0, generator=gen, device=m.device) * 1e-3).to(torch.bfloat16)
+    m.set_wire_stage(stage, parts, stride)
+    m.set_adam_range(s0, s1)
+    ref.set_adam_range(s0, s1)
+    acc = torch.zeros(s1 - s0, dtype=torch.float32, device=m.device)
+    for k in range(parts):
+        acc += stage[k * stride:k * stride + (s1 - s0)].float()
+    ref.grads.zero_()
+    ref.grads[s0:s1] = acc
+    m.grads.zero_()
+    ref.apply_adam(1.0 / parts)
+    m.apply_adam(1.0 / parts)
+    torch.cuda.synchronize()
+    assert torch.equal(m.params[s0:s1], ref.params[s0:s1])
+    assert torch.equal(m.adam_m[s0:s1], ref.adam_m[s0:s1])
+    assert torch.equal(m.adam_v[s0:s1], ref.adam_v[s0:s1])
+    assert torch.equal(pw[s0:s1], m.params[s0:s1].to(torch.bfloat16))

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc/$c -o run \
-    -- python3 bench.py --steps ${STEPS:-20} --warmup 3 --cpu-baseline 0 --graph 0 --probes 0 --fwd-only 0 \
+    -- python3 bench.py --steps ${STEPS:-20} --warmup 3 --cpu-baseline 0 --graph 0 --probes 0 --fwd-only 0 ${BENCH_ARGS:-} \
     > gpurun_out/pmc/$c.log 2>&1 || exit $?
 done
 find gpurun_out/pmc -name "*counter_collection*"

@@ -3,7 +3,9 @@
 FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes of 16-B/lane streaming reads, so it
 is doubled; WRITE_SIZE is exact for 16-B/lane stores and float atomics.
-usage: python tools/pmc_traffic.py gpurun_out/pmc profiles/r01_traffic.json
+usage: python tools/pmc_traffic.py gpurun_out/pmc profiles/r02_traffic.json [dtype columns feed]
+The workload the counters were collected on (default bf16 zipf device: bench.py's defaults) is
+recorded as "_workload"; bench.py attaches the traffic only to a line of the same workload.
 """
 import csv
 import glob
@@ -29,7 +31,7 @@ def collect(root, counter):
     return vals
 
 
-def main(root, out):
+def main(root, out, dtype="bf16", columns="zipf", feed="device"):
     fetch, write = collect(root, "FETCH_SIZE"), collect(root, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
@@ -38,10 +40,11 @@ def main(root, out):
         res[k] = {"fetch_kib_raw": round(f, 1), "write_kib": round(w, 1),
                   "hbm_bytes": int(round((2 * f + w) * 1024)),
                   "launches": max(len(fetch.get(k, [])), len(write.get(k, [])))}
+    res["_workload"] = {"dtype": dtype, "columns": columns, "feed": feed}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes"]):
+    for k, v in sorted(((k, v) for k, v in res.items() if k != "_workload"), key=lambda kv: -kv[1]["hbm_bytes"]):
         print(f"{v['hbm_bytes'] / 1e6:10.2f} MB  {k}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:])
