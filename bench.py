@@ -131,6 +131,21 @@ def pmc_traffic(workload: dict):
     return {}, None
 
 
+def mfma_summary(dtype: str):
+    """Matrix-core use of the MFMA kernels (TFLOP/s vs the dense peak, busy share of the SIMD
+    cycles) from the newest committed profiles/r*_mfma*.json of this dtype (tools/mfma_util.py:
+    rocprofv3 SQ_INSTS_VALU_MFMA_MOPS_* / SQ_VALU_MFMA_BUSY_CYCLES over kernel-trace durations)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma*.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("_workload", {}).get("dtype") != dtype:
+            continue
+        ks = {k: {x: v[x] for x in ("tflops", "peak_tflops", "frac_of_peak", "mfma_busy", "flops_per_launch")
+                  if x in v} for k, v in d.items() if k != "_workload"}
+        return {"kernels": ks, "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -555,6 +570,9 @@ def main():
     }
     if args.columns != "zipf":
         out["config"]["columns"] = args.columns
+    mf = mfma_summary(args.dtype) if fused else None
+    if mf is not None:
+        out["mfma"] = mf
     if fwd is not None:
         out["fwd_only"] = fwd
     if rehearse > 1:
