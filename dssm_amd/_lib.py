@@ -29,7 +29,7 @@ SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_A
 # dssm_plan_set_option ids (include/dssm.h DSSM_OPT_*)
 OPTIONS = {k: i for i, k in enumerate(["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "SCATTER_IN_COS",
                                          "DW_IN_APPLY", "WIRE_GRAD_PASS", "CSC_RANK", "DETERMINISTIC",
-                                         "FUSED_W1_ADAM"])}
+                                         "FUSED_W1_ADAM", "RANK_IN_ADAM"])}
 
 
 class DssmError(RuntimeError):

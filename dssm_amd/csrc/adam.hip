@@ -25,6 +25,21 @@
 
 #include <algorithm>
 
+#ifndef DSSM_ADAM_ORDER
+#define DSSM_ADAM_ORDER 0
+#endif
+#ifndef DSSM_RANK_POS
+#define DSSM_RANK_POS 1
+#endif
+#ifndef DSSM_ADAM_LATE_PMV
+#define DSSM_ADAM_LATE_PMV 0
+#endif
+#ifdef DSSM_ADAM_WPE  // diagnostics builds: a minimum occupancy (waves per SIMD) for the step kernel
+#define DSSM_ADAM_ATTR __attribute__((amdgpu_waves_per_eu(DSSM_ADAM_WPE)))
+#else
+#define DSSM_ADAM_ATTR
+#endif
+
 namespace dssm {
 namespace {
 
@@ -101,11 +116,13 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     const int nvalid = n - cc;
     const size_t o = (size_t)c * n + cc;
     float P[8], M[8], V[8], G[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#if !DSSM_ADAM_LATE_PMV
     if (nvalid > 0 && !a.gout) {  // stream loads first: independent of the gather chain below
       ld_stream8(a.p + o, nvalid, P);
       ld_stream8(a.m + o, nvalid, M);
       ld_stream8(a.v + o, nvalid, V);
     }
+#endif
     if (heavy) {
       if (nvalid > 0) {
         load8(a.g + o, nvalid, G);
@@ -115,6 +132,13 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     } else {
       gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
     }
+#if DSSM_ADAM_LATE_PMV
+    if (nvalid > 0 && !a.gout) {  // after the gather: fewer live registers, higher occupancy
+      ld_stream8(a.p + o, nvalid, P);
+      ld_stream8(a.m + o, nvalid, M);
+      ld_stream8(a.v + o, nvalid, V);
+    }
+#endif
     if (nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
       const int k = nvalid >= 8 ? 8 : 4;
       if (c < a.D) {
@@ -266,19 +290,35 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
 // (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
 // the ticket.
 template <typename TZ>
-__global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
+__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
   // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
   // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
-  const int b0 = blockIdx.x;
-  const int nh = a.item_blocks, nw = a.w1_blocks;
-  if (b0 < nh) {
+  __shared__ unsigned s_rank[kRankHash];  // the hosted rank role's hash table
+  const int nr = a.rank.nblocks;
+  // where the hosted rank workgroups sit in dispatch order
+#if DSSM_RANK_POS == 0
+  const int rs = 0;
+#elif DSSM_RANK_POS == 1
+  const int rs = (int)gridDim.x - nr;
+#else
+  const int rs = a.item_blocks;
+#endif
+  const int bx = blockIdx.x;
+  const bool is_rank = bx >= rs && bx < rs + nr;
+  const int b0 = bx < rs ? bx : bx - nr;
+  const int nh = a.item_blocks, nw = a.w1_blocks, nd = a.dense_blocks;
+  // role order after the heavy items: W1 rows then streaming (0), or streaming first (1)
+  const bool w1_role = DSSM_ADAM_ORDER == 0 ? (b0 >= nh && b0 < nh + nw) : (b0 >= nh + nd);
+  if (is_rank) {
+    csc_rank_role(a.rank, bx - rs, s_rank);
+  } else if (b0 < nh) {
     heavy_items<TZ>(a, alpha, b0);
-  } else if (b0 < nh + nw) {
-    const int b = b0 - nh;
+  } else if (w1_role) {
+    const int b = DSSM_ADAM_ORDER == 0 ? b0 - nh : b0 - nh - nd;
     // the next row's column range is loaded while this row is processed (one dependent load
     // fewer on each row's chain)
     const int stride = a.w1_blocks * 4;
@@ -300,7 +340,7 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       e = en;
     }
   } else {
-    const int bi = b0 - nh - nw;
+    const int bi = DSSM_ADAM_ORDER == 0 ? b0 - nh - nw : b0 - nh;
     if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
       const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
       for (int64_t i = (int64_t)bi * blockDim.x + threadIdx.x; i < w4;
@@ -382,6 +422,7 @@ __global__ __launch_bounds__(256) void k_adam_step(AdamStep a) {
       if (u == ntop - 1) {
         a.st[0] = b1p * a.beta1;
         a.st[1] = b2p * a.beta2;
+        if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -460,7 +501,8 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) +
                      (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
-  dim3 grid(a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
+  if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
+  dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   if (dz_bf16)
     hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
   else

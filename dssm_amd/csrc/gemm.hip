@@ -477,50 +477,58 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NtParams a, NtFuse f) {
 }
 
 // ---- whole-K NT GEMM (K <= 352): one load round per tile -----------------------------------
-// 128 x 64 output tile per 512-thread workgroup (8 waves = 4 x 2 of 32 x 32), the tile's WHOLE K
-// panel of A (128 rows) and BT (64 rows) staged once: every global load of the tile is issued
-// before the first LDS write, so a tile costs one memory round trip instead of one per 64-deep
-// K step; the A panel is converted to bf16 (with BN+ReLU when BN_A) on the way into LDS.
-// 240 tiles at C2 (M 6144, N 300): one wave of workgroups over 256 CUs.  FS epilogues as
-// nt_body's (tiles never straddle the tower boundary: row_split % 128 == 0).
+// (32 WM) x 64 output tile per (128 WM)-thread workgroup (2 WM waves = WM x 2 of 32 x 32), the
+// tile's WHOLE K panel of A (32 WM rows) and BT (64 rows) staged once: every global load of the
+// tile is issued before the first LDS write, so a tile costs one memory round trip instead of
+// one per 64-deep K step; the A panel is converted to bf16 (with BN+ReLU when BN_A) on the way
+// into LDS.  WM = 4: 128-row tiles, 512 threads (240 tiles at C2, one per CU); WM = 2: 64-row
+// tiles, 256 threads, half the LDS, so two tiles share a CU and overlap their load / MFMA /
+// epilogue chains.  FS epilogues as nt_body's (tiles never straddle the tower boundary:
+// row_split % (32 WM) == 0).
 constexpr int kWkMaxK = 352;
-constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: 128 rows x Kp/8 / 512
+#ifndef DSSM_WK_ROWS
+#define DSSM_WK_ROWS 128
+#endif
+constexpr int kWkRows = DSSM_WK_ROWS;  // whole-K tile height of the forward / dA launches (64 or 128)
+constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: (32 WM) rows x Kp/8 / (128 WM)
 __host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
 // LDS: A / B panels, BN coefficients, then the column-sum reduction.  The LDS epilogue stages a
-// [128][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
-__host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi) {
-  const size_t panels = (size_t)(128 + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4;
-  return (lds_epi && panels < (size_t)128 * 68 * 4) ? (size_t)128 * 68 * 4 : panels;
+// [32 WM][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
+__host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi, int WM = 4) {
+  const size_t panels = (size_t)(32 * WM + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4;
+  const size_t epi = (size_t)32 * WM * 68 * 4;
+  return (lds_epi && panels < epi) ? epi : panels;
 }
-__host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0) {
-  return wk_red_offset(Kp, lds_epi) + 4 * 64 * 2 * 8;
+__host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM = 4) {
+  return wk_red_offset(Kp, lds_epi, WM) + (size_t)WM * 64 * 2 * 8;
 }
 
-template <bool BN_A, int FS>
+template <bool BN_A, int FS, int WM = 4>
 __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
                                            u16* wk_smem) {
+  constexpr int NT = 128 * WM, ROWS = 32 * WM, BT = NT / 64;  // threads, tile rows, B threads / row
   const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc;
   const int Kp = (K + 31) & ~31, LDK = wk_ldk(Kp);
-  u16* sA = wk_smem;                                     // [128][LDK]
-  u16* sB = sA + 128 * LDK;                              // [64][LDK]
+  u16* sA = wk_smem;                                     // [ROWS][LDK]
+  u16* sB = sA + ROWS * LDK;                             // [64][LDK]
   float* sCoef = reinterpret_cast<float*>(sB + 64 * LDK);  // [tower][inv|shift][Kp]
   double* sRed = reinterpret_cast<double*>(reinterpret_cast<char*>(wk_smem) +
-                                           wk_red_offset(Kp, f.lds_epi));  // [4 wm][64][2]
+                                           wk_red_offset(Kp, f.lds_epi, WM));  // [WM][64][2]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int bm = ty * 128, bn = tx * 64;
+  const int bm = ty * ROWS, bn = tx * 64;
   const int tower = bm < a.row_split ? 0 : 1;
   // the A operand's BN coefficient inputs (sums, gamma, beta) first: they return ahead of the
   // tile's bulk loads
-  constexpr int NPC = (2 * kWkMaxK + 511) / 512;
+  constexpr int NPC = (2 * kWkMaxK + NT - 1) / NT;
   FsCoefStage<NPC> cst;
   const bool from_sums = BN_A && FS == 1 && f.in_from_sums;
-  if (from_sums) cst.load(f.in, t, 512);
+  if (from_sums) cst.load(f.in, t, NT);
   // ---- every global load of the tile, issued first.  A: 4 threads per row (groups t%4 + 4i),
-  // B: 8 threads per row (groups t%8 + 8i): no divisions, 128-B row segments per 4 / 8 lanes.
+  // B: BT threads per row (groups t%BT + BT i): 128-B row segments per 4 / BT lanes.
   const int arow = t >> 2, ag0 = t & 3;
-  const int brow = t >> 3, bg0 = t & 7;
-  constexpr int NGA = kWkMaxG, NGB = (kWkMaxG + 1) / 2;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / 8)
+  const int brow = t / BT, bg0 = t % BT;
+  constexpr int NGA = kWkMaxG, NGB = (4 * kWkMaxG + BT - 1) / BT;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
   float4 fa[NGA][2];  // fp32 A groups (BN_A)
   uint4 ua[NGA];      // bf16 A groups
   uint4 ub[NGB];
@@ -542,7 +550,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     const size_t bbase = (size_t)(bok ? bn + brow : 0) * ldb;
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      const int kg = (bg0 + 8 * i) * 8;
+      const int kg = (bg0 + BT * i) * 8;
       ub[i] = *reinterpret_cast<const uint4*>(a.BT + ((bok && kg < ldb) ? bbase + kg : 0));
     }
   }
@@ -567,20 +575,20 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   // ---- BN coefficients of the A operand (from the sums or the materialised coefficients)
   if constexpr (BN_A) {
     if (FS == 1 && f.in_from_sums) {
-      cst.finish(f.in, t, 512, [&](int tw, int k, float, float, float inv, float sh) {
+      cst.finish(f.in, t, NT, [&](int tw, int k, float, float, float inv, float sh) {
         if (k < Kp) {
           sCoef[(tw * 2 + 0) * Kp + k] = inv;
           sCoef[(tw * 2 + 1) * Kp + k] = sh;
         }
       });
-      for (int i = t; i < 2 * (Kp - lda); i += 512) {  // K pad beyond the stored width
+      for (int i = t; i < 2 * (Kp - lda); i += NT) {  // K pad beyond the stored width
         const int tw = i / (Kp - lda), k = lda + i % (Kp - lda);
         sCoef[(tw * 2 + 0) * Kp + k] = 0.f;
         sCoef[(tw * 2 + 1) * Kp + k] = 0.f;
       }
     } else {
       const size_t plane = (size_t)2 * lda;
-      for (int i = t; i < 2 * Kp; i += 512) {
+      for (int i = t; i < 2 * Kp; i += NT) {
         const int tw = i / Kp, k = i - tw * Kp;
         const bool ok = k < lda;
         sCoef[(tw * 2 + 0) * Kp + k] = ok ? a.coef[2 * plane + (size_t)tw * lda + k] : 0.f;
@@ -621,7 +629,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     const bool bok = bn + brow < N;
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      const int kg = (bg0 + 8 * i) * 8;
+      const int kg = (bg0 + BT * i) * 8;
       if (kg < Kp)
         *reinterpret_cast<uint4*>(&sB[brow * LDK + kg]) =
             (bok && kg < ldb) ? ub[i] : make_uint4(0u, 0u, 0u, 0u);
@@ -663,7 +671,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   // last MFMA) and leave as 16-B row segments (full 256-B rows) instead of the accumulator
   // layout's 4-B scattered stores
   const bool lds_epi = f.lds_epi != 0;
-  float* sC = reinterpret_cast<float*>(sA);  // [128][68]
+  float* sC = reinterpret_cast<float*>(sA);  // [ROWS][68]
   constexpr int kCld = 68;
   if (lds_epi) __syncthreads();
   double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};
@@ -716,8 +724,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     if (t < 128) {
       const int c = t >> 1, st = t & 1, n = bn + c;
       if (n < N) {
-        const double v = sRed[(0 * 64 + c) * 2 + st] + sRed[(1 * 64 + c) * 2 + st] +
-                         sRed[(2 * 64 + c) * 2 + st] + sRed[(3 * 64 + c) * 2 + st];
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < WM; ++q) v += sRed[(q * 64 + c) * 2 + st];
         atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
       }
     }
@@ -726,8 +735,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     __syncthreads();
     const int ncols = min(64, ldc - bn);  // multiple of 8: ldc = ldp8(N)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = t + 512 * k, r = idx >> 4, q = (idx & 15) * 4;
+    for (int k = 0; k < 4; ++k) {  // ROWS x 16 float4 = 4 per thread
+      const int idx = t + NT * k, r = idx >> 4, q = (idx & 15) * 4;
       if (bm + r < M && q < ncols)
         *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) =
             *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
@@ -746,8 +755,8 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
 // Whole-K forward NT GEMM: blocks [0, ntiles) compute tiles (XCD-grouped row blocks); with the
 // A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
 // EMA update) off the tiles' critical path.
-template <bool BN_A, int FS>
-__global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
+template <bool BN_A, int FS, int WM>
+__global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
   WG_TL(a.N == 300 ? 0 : 1, 0);
   if ((int)blockIdx.x >= ntiles) {
@@ -755,7 +764,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);
-  nt_wk_body<BN_A, FS>(a, f, tile % nx, tile / nx, wk_smem);
+  nt_wk_body<BN_A, FS, WM>(a, f, tile % nx, tile / nx, wk_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -873,6 +882,20 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
   }
 }
 
+// Whole-K backward pair, dA tiles only (the dW_l tiles ride in the next BN-backward apply launch).
+template <int WM>
+__global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks) {
+  extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
+  WG_TL(a.K == 300 ? 3 : 2, 0);
+  const int tile = xcd_tile(blockIdx.x, nt_blocks);
+  nt_wk_body<false, 2, WM>(a, f, tile % nt_x, tile / nt_x, pw_smem);
+#ifdef DSSM_WG_TL
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  WG_TL(a.K == 300 ? 3 : 2, 1);
+#endif
+}
+
 // Whole-K backward pair: the dA tiles (nt_wk_body, FS == 2) first, then the dW chunk tiles.
 __global__ __launch_bounds__(512) void k_bwd_pair_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks,
                                                      TnParams p, int tn_x, int tn_y) {
@@ -881,7 +904,7 @@ __global__ __launch_bounds__(512) void k_bwd_pair_wk(NtParams a, NtFuse f, int n
   WG_TL(a.K == 300 ? 3 : 2, 0);
   if (b < nt_blocks) {
     const int tile = xcd_tile(b, nt_blocks);
-    nt_wk_body<false, 2>(a, f, tile % nt_x, tile / nt_x, pw_smem);
+    nt_wk_body<false, 2, 4>(a, f, tile % nt_x, tile / nt_x, pw_smem);
   } else {
     // XCD grouping of the dW tiles needs the dA range to end on a multiple of 8
     const int nr = (int)gridDim.x - nt_blocks;
@@ -1015,11 +1038,17 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   }
   f.out_sum = out_sum;
   f.lds_epi = 1;  // measured: 14.4 (LDS-staged epilogue) vs 16.2 us per NT launch
-  if (K <= kWkMaxK && (row_split % 128) == 0) {
+  if (K <= kWkMaxK && (row_split % 64) == 0) {
     const int Kp = (K + 31) & ~31;
-    const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 128);
-    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1>), dim3(ntiles + (in_from_sums ? 1 : 0)),
-                       dim3(512), wk_smem_bytes(Kp, f.lds_epi), s, a, f, nx, ntiles);
+    const int nx = cdiv(ldc, 64);
+#define DSSM_NTWK(WM)                                                                         \
+  {                                                                                           \
+    const int ntiles = nx * cdiv(M, 32 * WM);                                                 \
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),    \
+                       dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
+  }
+    if (kWkRows == 64 || (row_split % 128)) DSSM_NTWK(2) else DSSM_NTWK(4)
+#undef DSSM_NTWK
     return hipGetLastError();
   }
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 64)), dim3(256), 0, s, a, f);
@@ -1049,6 +1078,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   if (n <= kWkMaxK && (row_split % 128) == 0 && lda_prev >= kin) {
     const int Kp = (n + 31) & ~31;
     const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 128);
+    const int nt_blocks64 = nt_x * cdiv(M, 64);
     const int Mw = kin + 1;
     const int nsplit = cdiv(M, kTwKc);
     const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
@@ -1057,8 +1087,12 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
       // BN-backward apply launch (bn.hip), same splits and slabs.  Without defer the caller sums
       // the slabs (launch_splitk_reduce) after that launch.
       *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
-      hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi), s,
-                         a, f, nt_x, nt_blocks, *dw_out, 1, 1);
+      if (kWkRows == 64)
+        hipLaunchKernelGGL(k_pair_da_wk<2>, dim3(nt_blocks64), dim3(256), wk_smem_bytes(Kp, f.lds_epi, 2),
+                           s, a, f, nt_x, nt_blocks64);
+      else
+        hipLaunchKernelGGL(k_pair_da_wk<4>, dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi, 4),
+                           s, a, f, nt_x, nt_blocks);
       *deferred_splits = (defer && nsplit > 1) ? nsplit : 0;
       return hipGetLastError();
     }

@@ -3,12 +3,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "csc.h"
+
 
 namespace dssm {
 
 struct BnSide;    // bnfuse.h
 struct TnParams;  // tn.h
-struct CscScatter;  // csc.h
 
 // Eval-mode (on_train=False) BN coefficients of every layer from the EMA shadows
 // (new_dssm.py:85-86): they depend on the parameters only, not on the batch, so the forward
@@ -70,6 +71,9 @@ hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_v
                       int* csc_scratch = nullptr,   // non-null: heavy items of the rank transpose
                       float* heavy_slab = nullptr);  // deterministic: [items][n] partial rows
 size_t csc_heavy_cap(int rows, int max_nnz);  // heavy work items one step can list
+// the rank pass of launch_csc_build (rank_path) as a role of another launch (csc.h), same outputs
+CscRankRole csc_rank_role_args(const int* indptr, const int* indices, int rows, int D, int* scratch,
+                               double* zero, int nzero);
 
 // ---- dense GEMM (gemm.hip) ----
 enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
@@ -190,7 +194,13 @@ struct ShadowList {
 // One optimizer step over the arena (adam.hip).  st: device {beta1_power, beta2_power} of this
 // step, advanced by the kernel; ticket: kAdamTicketUints zero-initialised counters, re-armed by
 // the kernel.
-constexpr int kAdamW1Blocks = 2048;
+#ifndef DSSM_ADAM_W1B
+#define DSSM_ADAM_W1B 2048
+#endif
+#ifndef DSSM_ADAM_ITEMS
+#define DSSM_ADAM_ITEMS 512
+#endif
+constexpr int kAdamW1Blocks = DSSM_ADAM_W1B;
 constexpr int kAdamDenseBlocks = 2048;
 constexpr int kAdamSubTickets = 64;
 // ticket area: top counter + kAdamSubTickets counters, each on its own 256-B line
@@ -254,12 +264,17 @@ struct AdamStep {
   // deterministic mode: a multi-item heavy column's items store their partial rows here ([item][n],
   // write-through) and its last arrival sums them in item order (no fp32 atomics)
   float* heavy_slab;
+  // the NEXT step's CSC rank pass as the launch's first workgroups (csc.h; rank.nblocks == 0: none),
+  // with heavy_reset: the heavy-item count this step's scan filled, zeroed by the last block once
+  // every block has read it (the next step's rank launch, which would zero it, is skipped)
+  CscRankRole rank;
+  int* heavy_reset;
   // gradient pass (data parallel, bf16 wire): the W1 roles compute dW1 rows (inline gather, heavy
   // items, zero for untouched rows) and write them as bf16 to gout (arena layout; the bias row as
   // fp32 into g) instead of updating parameters; no dense range, no beta-power advance
   uint16_t* gout;
 };
-constexpr int kAdamItemBlocks = 512;  // persistent workgroups for the heavy W1 columns
+constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 // bf16 wire helpers (data parallel): wire[i] = bf16(g[i]) for i < n (n % 4 == 0); the W1 shadow

@@ -205,6 +205,12 @@ struct dssm_plan {
   bool loss_pending = false;  // its loss partials await the backward's first launch
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
   int dw_deferred[DSSM_MAX_LAYERS] = {};  // split count of dW_l left in its slab (fused mode)
+  // Multi-step graphs: the Adam launch of step i hosts step i+1's CSC rank pass (csc.h) when the
+  // next batch is known (host_rank_*); rank_done_for = that batch, whose forward then skips the
+  // transpose's first launch (the rank launch, 11 us at C2).
+  const int32_t* host_rank_indptr = nullptr;
+  const int32_t* host_rank_indices = nullptr;
+  const int32_t* rank_done_for = nullptr;
   // Schedule options (dssm_plan_set_option; never read from the environment).  Each names a
   // measured-faster default and the alternative it replaced, kept for parity tests and shapes the
   // default does not support.  Graphs captured earlier keep the schedule they were captured with.
@@ -218,6 +224,7 @@ struct dssm_plan {
       1,  // CSC_RANK: rank / scan / scatter transpose (0: histogram / fill launches)
       0,  // DETERMINISTIC: fixed-order reductions, bit-identical repeated runs
       1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
+      1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -551,6 +558,9 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     // The CSC transpose of the batch (dW1's operand).  Fused-statistics steps: its first launch
     // also clears the step's BN sums; merged: its scan / scatter ride in later launches.
     P->probe_begin(DSSM_PROBE_CSC, s);
+    const bool hosted = merged && P->rank_done_for == P->indptr;  // done by the last Adam launch
+    P->rank_done_for = nullptr;
+    if (!hosted)
     HIP_TRY(dssm::launch_csc_build(P->indptr, P->indices, P->values, Lt.R, Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr),
                                    P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
@@ -905,6 +915,17 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
       sh.count -= 1;
     }
   }
+  // the next step's rank pass as this launch's first workgroups (multi-step graphs)
+  if (P->host_rank_indptr && P->fused_w1_adam() && a.heavy_n && P->merged_csc() &&
+      Lt.D <= dssm::kRankMaxD) {
+    a.rank = dssm::csc_rank_role_args(P->host_rank_indptr, P->host_rank_indices, Lt.R, Lt.D,
+                                      P->at<int>(Lt.csc_scratch), P->at<double>(Lt.sums),
+                                      (int)(Lt.sums_bytes / 8));
+    a.heavy_reset = const_cast<int*>(a.heavy_n);
+    P->rank_done_for = P->host_rank_indptr;
+  }
+  P->host_rank_indptr = nullptr;
+  P->host_rank_indices = nullptr;
   for (int l = 1; l < Lt.L; ++l)
     if (P->dw_deferred[l] > 0) {  // dW_l still in its split-K slab: summed inside the step
       dssm::SlabSeg& sg = a.slabs.seg[a.slabs.count++];
@@ -1129,6 +1150,7 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   }
   P->capturing = g;
   int rc = DSSM_OK;
+  P->rank_done_for = nullptr;
   for (int i = 0; i < nsteps && !rc; ++i) {
     // probes (event-record nodes) ride in the first step only
     g->probes = with_probes != 0 && i == 0;
@@ -1137,8 +1159,14 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     P->values = values[i];
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
+    if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {  // step i+1's rank pass rides in this Adam
+      P->host_rank_indptr = indptrs[i + 1];
+      P->host_rank_indices = indices[i + 1];
+    }
     if (!rc) rc = dssm_plan_adam(P, 1.0f, stream);
   }
+  P->host_rank_indptr = P->host_rank_indices = nullptr;
+  P->rank_done_for = nullptr;
   g->probes = with_probes != 0;
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();

@@ -870,6 +870,13 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
 
 size_t csc_heavy_cap(int rows, int max_nnz) { return (size_t)(max_nnz + rows) / 32 + 64; }
 
+CscRankRole csc_rank_role_args(const int* indptr, const int* indices, int rows, int D, int* scratch,
+                               double* zero, int nzero) {
+  // cnt and the per-entry ranks where launch_csc_build keeps them
+  return CscRankRole{indptr, indices, rows, scratch, scratch + 2 * (D + 1 + 64), zero, nzero,
+                     cdiv(rows, kRankRoleRows)};
+}
+
 size_t csc_scratch_ints(int D, int rows, int max_nnz) {
   // cnt (D+1, padded) + cursor (D+1) + rank / position per entry (max_nnz) + heavy-item count
   // (64, padded) + heavy items (int2 each) + per-column heavy tickets (D+1, padded)

@@ -141,7 +141,10 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *   DETERMINISTIC   0; 1: fixed-order reductions only (separate statistics launches, every CSC
  *                      column in row order, heavy dW1 rows summed in item order): repeated runs
  *                      from the same state and batches are bit-identical
- *   FUSED_W1_ADAM   see dssm_plan_set_fused_w1_adam */
+ *   FUSED_W1_ADAM   see dssm_plan_set_fused_w1_adam
+ *   RANK_IN_ADAM    1: in multi-step graphs (dssm_plan_graph_build_steps) step i's Adam launch also
+ *                      runs step i+1's CSC rank pass (with MERGED_CSC and FUSED_W1_ADAM), so that
+ *                      step's forward skips the rank launch */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -152,6 +155,7 @@ enum {
   DSSM_OPT_CSC_RANK,
   DSSM_OPT_DETERMINISTIC,
   DSSM_OPT_FUSED_W1_ADAM,
+  DSSM_OPT_RANK_IN_ADAM,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);

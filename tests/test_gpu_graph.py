@@ -153,3 +153,41 @@ def test_multi_step_graph_matches_eager(case):
     d = (ea.params - gr.params).abs()
     assert float(d.max()) <= 2 * k * lr, float(d.max())
     assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
+
+
+@pytest.mark.parametrize("hosted", [True, False])
+def test_cycle_graph_with_rank_in_adam(hosted):
+    """RANK_IN_ADAM (default): in a multi-step graph, step i's Adam launch also runs step i+1's CSC
+    rank pass (csc.h csc_rank_role: LDS hash table per 12 rows) and that step skips its rank
+    launch.  BS = 128 takes the merged-transpose schedule the option needs; 4 steps, so three
+    rank passes ride in Adam launches.  Against eager steps at the multi-step bar above."""
+    D, widths, BS, NEG, lr, k = 5000, (300, 300, 128), 128, 4, 0.01, 4
+    _, _, ea = make(D, widths, BS, NEG, "bf16")
+    _, _, gr = make(D, widths, BS, NEG, "bf16")
+    gr.set_option("RANK_IN_ADAM", hosted)
+    assert gr.schedule()["MERGED_CSC"]
+    batches = _batches(D, BS, NEG, k)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        staged = [tuple(torch.from_numpy(x).cuda() for x in (hb.indptr, hb.indices, hb.values))
+                  for hb in batches]
+        gid = gr.graph_build_steps(staged)
+        losses = []
+        for ip, ix, vv in staged:
+            ea.set_batch(indptr=ip, indices=ix, values=vv)
+            ea.train_step()
+            torch.cuda.synchronize()
+            losses.append(ea.loss_accuracy()[0])
+        gr.graph_launch(gid)
+        torch.cuda.synchronize()
+    assert ea.beta_powers() == gr.beta_powers()
+    la, lg = losses[-1], gr.loss_accuracy()[0]
+    assert abs(la - lg) <= 1e-3 * abs(la) + 1e-6, (la, lg)
+    d = (ea.params - gr.params).abs()
+    assert float(d.max()) <= 2 * k * lr, float(d.max())
+    assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
+    # the graph can be replayed again (the hosted passes re-arm what they consume)
+    with torch.cuda.stream(s):
+        gr.graph_launch(gid)
+        torch.cuda.synchronize()
+    assert np.isfinite(gr.loss_accuracy()[0])

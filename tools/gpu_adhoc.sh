@@ -1,5 +1,7 @@
-set -u
+set -eu
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_api.py -q --timeout 120 --timeout-method thread > gpurun_out/pytest_wire.log 2>&1; tail -3 gpurun_out/pytest_wire.log
-HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 120 python -u tools/rccl_probe.py > gpurun_out/rccl_probe.log 2>&1; echo "probe rc=$?"; tail -20 gpurun_out/rccl_probe.log
+L=dssm_amd/libdssm
+timeout -k 10 300 python -u -m pytest tests/test_gpu_graph.py -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_rank.log 2>&1 || { tail -30 gpurun_out/pytest_rank.log; exit 1; }
+tail -1 gpurun_out/pytest_rank.log
+STEPS=400 bash tools/ab.sh "DSSM_LIB_PATH=$L.so" "DSSM_LIB_PATH=${L}_r32.so" "DSSM_LIB_PATH=${L}_r48.so" "DSSM_LIB_PATH=$L.so" "DSSM_LIB_PATH=${L}_r32.so" "DSSM_LIB_PATH=${L}_r48.so"

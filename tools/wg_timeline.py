@@ -32,6 +32,9 @@ for slot, name in enumerate(("nt L2 (N=300)", "nt L3 (N=128)", "pair L3", "pair 
     buf = np.zeros((2048, 2), np.uint64)
     assert f(slot, buf.ctypes.data, 2048) == 0
     n = int(np.sum(buf[:, 0] > 0))
+    if n == 0:
+        print(f"{name}: no stamps")
+        continue
     t = buf[:n].astype(np.int64)
     t0 = t[:, 0].min()
     st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
@@ -43,8 +46,8 @@ for slot, name in enumerate(("nt L2 (N=300)", "nt L3 (N=128)", "pair L3", "pair 
     print("   starts (us, by start order, every 16th):", " ".join(f"{x:.1f}" for x in st[order][::16]))
     print("   ends   (us, same WGs):                ", " ".join(f"{x:.1f}" for x in en[order][::16]))
 
-# k_adam_step: roles by block index (heavy items, W1 rows, flat/dense streaming); the launch
-# geometry is recomputed the way launch_adam_step sizes it
+# k_adam_step: roles by block index (heavy items, W1 rows, flat/dense streaming), as
+# k_adam_step assigns them
 g = lib.dssm_debug_adam_timeline
 g.restype = C.c_int
 g.argtypes = [C.c_void_p, C.c_int]
@@ -54,13 +57,10 @@ n = int(np.sum(buf[:, 0] > 0))
 t = buf[:n].astype(np.int64)
 t0 = t[:, 0].min()
 st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
-items, w1 = 512, 2048  # kAdamItemBlocks, kAdamW1Blocks: roles interleaved as k_adam_step assigns them
+items, w1 = 512, 2048  # kAdamItemBlocks, kAdamW1Blocks: roles contiguous in block order
 b = np.arange(n, dtype=np.int64)
-hc = b * items // n
-heavy = (b + 1) * items // n > hc
-j = b - hc
-wc = j * w1 // (n - items)
-w1r = ~heavy & ((j + 1) * w1 // (n - items) > wc)
+heavy = b < items
+w1r = (b >= items) & (b < items + w1)
 for name, sel in (("heavy items", heavy), ("W1 rows", w1r), ("flat/dense", ~heavy & ~w1r)):
     if not sel.any():
         continue
