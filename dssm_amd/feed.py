@@ -7,8 +7,8 @@ Mirrors the reference's pipeline with its names:
   libdssm.so (``dssm_text_clean``, ``dssm_vocab_*``); ``TextVectorizer`` has sklearn's
   fit / transform / get_feature_names / vocabulary_ surface and returns scipy CSR matrices, so
   ``pull_batch`` and ``convert_sparse_matrix_to_sparse_tensor`` (dssm_amd.data) work on them
-  unchanged.  The vectorizer is saved as a JSON feature list, not a pickle (save_vectorizer,
-  utils/utils.py:241-261).
+  unchanged.  ``save_vectorizer`` / ``load_vectorizer`` (utils/utils.py:241-261) write and read
+  the reference's file: a pickled scikit-learn CountVectorizer (dssm_amd.vecpickle).
 * ``get_data_set_comment`` (utils/utils.py:368-421): TSV lines ``prefix \\t title \\t label \\t mid
   \\t feed_id`` with label '1', one space-separated character per token, NEG negatives per query
   drawn from the other docs (doc != positive, query differs, no repeats).  The reference draws
@@ -31,6 +31,7 @@ import scipy.sparse as sps
 
 from . import _lib
 from ._lib import check
+from .vecpickle import dumps_count_vectorizer, loads_count_vectorizer
 
 
 def _cstrs(texts: Sequence[str]):
@@ -113,27 +114,49 @@ class TextVectorizer:
     def fit_transform(self, raw_documents):
         return self.fit(raw_documents).transform(raw_documents)
 
-    # save_vectorizer / load_vectorizer (utils/utils.py:241-261), as JSON
-    def save(self, path: str):
-        with open(path, "w", encoding="utf8") as f:
-            json.dump({"format": "dssm_amd.TextVectorizer/1", "features": self._names}, f, ensure_ascii=False)
+    # save_vectorizer / load_vectorizer (utils/utils.py:241-261)
+    def save(self, path: str, format: str = "pickle"):
+        """format="pickle" (default): the reference's file -- a pickled scikit-learn CountVectorizer
+        that its load_vectorizer reads (dssm_amd.vecpickle); "json": a feature list."""
+        if format == "pickle":
+            with open(path, "wb") as f:
+                f.write(dumps_count_vectorizer(self._names))
+        elif format == "json":
+            with open(path, "w", encoding="utf8") as f:
+                json.dump({"format": "dssm_amd.TextVectorizer/1", "features": self._names}, f,
+                          ensure_ascii=False)
+        else:
+            raise ValueError("format must be 'pickle' or 'json'")
+
+    @classmethod
+    def from_features(cls, features: Sequence[str]) -> "TextVectorizer":
+        """A fitted vectorizer whose column i is features[i]."""
+        v = cls()
+        for name in features:
+            check(v.lib.dssm_vocab_add(v._h, name.encode("utf8")), "vocab_add")
+        v._names = list(features)
+        return v
 
     @classmethod
     def load(cls, path: str) -> "TextVectorizer":
-        with open(path, encoding="utf8") as f:
-            d = json.load(f)
-        v = cls()
-        for name in d["features"]:
-            check(v.lib.dssm_vocab_add(v._h, name.encode("utf8")), "vocab_add")
-        v._names = list(d["features"])
-        return v
+        """Either format of ``save``: the reference's pickle (read by an allow-list unpickler that
+        resolves nothing but the CountVectorizer state, see dssm_amd.vecpickle) or JSON."""
+        with open(path, "rb") as f:
+            data = f.read()
+        if data.lstrip()[:1] == b"{":
+            feats = json.loads(data.decode("utf8"))["features"]
+        else:
+            feats, _params = loads_count_vectorizer(data)
+        return cls.from_features(feats)
 
 
-def save_vectorizer(vectorizer: TextVectorizer, path: str = "output/vectorizer_data.json"):
+def save_vectorizer(vectorizer: TextVectorizer, path: str = "output/vectorizer_data"):
+    """utils/utils.py:241-249: the pickled CountVectorizer the reference writes."""
     vectorizer.save(path)
 
 
-def load_vectorizer(path: str = "output/vectorizer_data.json") -> TextVectorizer:
+def load_vectorizer(path: str = "output/vectorizer_data") -> TextVectorizer:
+    """utils/utils.py:252-261 (also reads this module's JSON form)."""
     return TextVectorizer.load(path)
 
 
