@@ -107,6 +107,7 @@ _SIGS = {
     "dssm_vocab_size": (C.c_int64, [_P]),
     "dssm_vocab_name": (C.c_int, [_P, C.c_int64, C.c_char_p, C.c_size_t]),
     "dssm_vocab_add": (C.c_int, [_P, C.c_char_p]),
+    "dssm_crc32c": (C.c_uint32, [C.c_uint32, _P, C.c_size_t]),
     "dssm_vocab_transform": (C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int64, _P, _P, _P, C.c_int64,
                                        C.POINTER(C.c_int64)]),
     "dssm_feeder_create": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int64),

@@ -25,12 +25,13 @@ at import of the model (dssm_amd._lib.load).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Any, Dict, Iterable, Optional
 
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, tfckpt
 from .data import SparseTensorValue, feeds_to_csr
 from .metrics import StreamingAUC, dssm_labels
 from .model import DSSM
@@ -236,14 +237,28 @@ class Session:
 
 
 class Saver:
-    """tf.train.Saver stand-in (new_dssm.py:248,331): params, Adam slots, beta powers, EMA."""
+    """tf.train.Saver (new_dssm.py:248,331): params, Adam slots, beta powers and EMA shadows as a
+    TF1.x V2 checkpoint under the reference graph's variable names (dssm_amd/tfckpt.py).
+    ``save(sess, "model/model_1.ckpt")`` writes model_1.ckpt.index / .data-00000-of-00001 and the
+    directory's ``checkpoint`` file and returns the prefix, as TF does; ``restore`` also reads
+    the npz form (``format="npz"``)."""
+
+    def __init__(self, format: str = "tf"):
+        if format not in ("tf", "npz"):
+            raise ValueError("format must be 'tf' or 'npz'")
+        self.format = format
 
     def save(self, sess: Session, save_path: str) -> str:
-        path = save_path if save_path.endswith(".npz") else save_path + ".npz"
-        sess.graph.model.save(path)
-        return path
+        if self.format == "npz" or save_path.endswith(".npz"):
+            path = save_path if save_path.endswith(".npz") else save_path + ".npz"
+            sess.graph.model.save(path)
+            return path
+        return tfckpt.save_model(sess.graph.model, save_path)
 
     def restore(self, sess: Session, save_path: str):
+        if os.path.exists(save_path + ".index"):
+            tfckpt.restore_model(sess.graph.model, save_path)
+            return
         path = save_path if save_path.endswith(".npz") else save_path + ".npz"
         sess.graph.model.restore(path)
 

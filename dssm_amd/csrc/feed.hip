@@ -314,6 +314,21 @@ int dssm_vocab_add(dssm_vocab* v, const char* name) {  // restore a saved vocabu
   return DSSM_OK;
 }
 
+// CRC-32C (reflected polynomial 0x82F63B78) extending a finished CRC, as leveldb / TF's
+// crc32c::Extend: the TF checkpoint writer / reader (dssm_amd/tfckpt.py) checks every tensor with it.
+__attribute__((target("sse4.2"))) uint32_t dssm_crc32c(uint32_t crc, const void* data, size_t n) {
+  const unsigned char* p = static_cast<const unsigned char*>(data);
+  uint64_t l = ~crc;
+  for (; n && (reinterpret_cast<uintptr_t>(p) & 7); --n) l = __builtin_ia32_crc32qi((uint32_t)l, *p++);
+  for (; n >= 8; n -= 8, p += 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    l = __builtin_ia32_crc32di(l, w);
+  }
+  for (; n; --n) l = __builtin_ia32_crc32qi((uint32_t)l, *p++);
+  return ~(uint32_t)l;
+}
+
 // Counts per document (CSR, sorted columns; unknown tokens dropped like sklearn's transform).
 // Pass indices/values NULL to size: *nnz_out = total non-zeros (indptr filled either way).
 int dssm_vocab_transform(const dssm_vocab* v, const char* const* texts, int64_t n, int64_t* indptr,

@@ -343,6 +343,10 @@ int64_t dssm_vocab_size(const dssm_vocab* v);
 int dssm_vocab_name(const dssm_vocab* v, int64_t i, char* out, size_t cap);
 /* append a feature (restoring a saved vocabulary in id order) */
 int dssm_vocab_add(dssm_vocab* v, const char* name);
+/* CRC-32C (Castagnoli) of n host bytes, extending the finished CRC `crc` (0 to start): the checksum
+ * TF1.x's tf.train.Saver V2 checkpoints carry per tensor and per index block (new_dssm.py:248,331;
+ * dssm_amd/tfckpt.py).  SSE4.2 crc32 instructions, 8 bytes per step. */
+uint32_t dssm_crc32c(uint32_t crc, const void* data, size_t n);
 /* vectorizer.transform: indptr [n+1]; indices / values [cap] (NULL: count only) */
 int dssm_vocab_transform(const dssm_vocab* v, const char* const* texts, int64_t n, int64_t* indptr,
                          int32_t* indices, float* values, int64_t cap, int64_t* nnz_out);

@@ -155,3 +155,40 @@ def test_deterministic_fp32_matches_oracle():
     for k, g in grads.items():
         if not is_bias(k):
             grad_check(k, gg[k], g, 1e-4)
+
+
+def test_tf_checkpoint_resume_is_bit_identical(tmp_path):
+    """tf.train.Saver round trip (dssm_amd/tfckpt.py, new_dssm.py:248,331): save after two steps,
+    train two more, restore into a fresh model and replay them -- parameters, Adam slots, EMA and
+    beta powers end bit-identical (deterministic mode, so the replay has no atomics noise)."""
+    from dssm_amd import tfckpt
+    from dssm_amd.model import DSSM
+    D, widths, BS, NEG = SMALL
+    batches = [synth_batch(D, BS, NEG, seed=1000 + i) for i in range(4)]
+
+    def model():
+        m = DSSM(D, widths, BS, NEG, dtype="bf16", init=False)
+        m.set_option("DETERMINISTIC", True)
+        return m
+
+    a = model()
+    a.init_params(seed=5)
+    for b in batches[:2]:
+        a.set_batch(b)
+        a.train_step()
+    prefix = tfckpt.save_model(a, str(tmp_path / "model" / "model_1.ckpt"))
+    for b in batches[2:]:
+        a.set_batch(b)
+        a.train_step()
+    torch.cuda.synchronize()
+    c = model()
+    tfckpt.restore_model(c, tfckpt.latest_checkpoint(str(tmp_path / "model")))
+    assert c.global_step == 2
+    for b in batches[2:]:
+        c.set_batch(b)
+        c.train_step()
+    torch.cuda.synchronize()
+    n = a.n_params
+    for x, y in ((a.params, c.params), (a.adam_m, c.adam_m), (a.adam_v, c.adam_v), (a.ema, c.ema)):
+        assert torch.equal(x[:n] if x.numel() > n else x, y[:n] if y.numel() > n else y)
+    assert a.beta_powers() == c.beta_powers()
