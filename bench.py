@@ -204,25 +204,12 @@ def bench_rnn(args):
                       "parallelism": "dp1"},
            "final_loss": round(m.loss(), 3)}
     if args.cpu_baseline:
-        try:  # the NumPy restatement (oracle/, test infrastructure) timed on the host: bounded sample
-            from oracle import rnn_oracle as RO
-            cfg = RO.RnnConfig(nwords=V, emb=E, hidden=H, query_bs=BS, neg=NEG, seq_len=T, lr=1e-5)
-            p = {k: v.astype(np.float64) for k, v in m.named().items()}
-            opt = RO.Adam(cfg, m.named())
-            lens = np.full(m.R, T, np.int32)
-            n, t0 = 0, time.perf_counter()
-            while n < 1 or time.perf_counter() - t0 < min(args.cpu_seconds, 20.0):
-                mask = RO.dropout_mask(m.R, 2 * H, 0.5, 0, n + 1)
-                fw = RO.forward(cfg, p, batches[n % len(batches)], lens, mask, 0.5)
-                g = RO.backward(cfg, p, batches[n % len(batches)], lens, fw)
-                opt.step(p, g)
-                n += 1
-            el = time.perf_counter() - t0
-            out["cpu_baseline"] = {"value": round(BS * (NEG + 1) * n / el, 1), "unit": "pairs/s",
-                                   "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                                   "kind": "port",
-                                   "sample": f"{n} full steps of the NumPy float64 restatement "
-                                             f"(oracle/rnn_oracle.py) in {el:.1f}s"}
+        try:  # the C/OpenMP fp32 restatement (oracle/cpu_c/rnn_cpu.c, test infrastructure) on the host
+            from oracle import cpu_c
+            host = [b for b in batches]
+            out["cpu_baseline"] = cpu_c.rnn_time_steps(V, E, H, BS, NEG, T, m.named(), host, keep=0.5,
+                                                       budget_s=min(args.cpu_seconds, 20.0))
+            out["cpu_baseline"]["cpu_model"] = cpu_model()
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(out), flush=True)

@@ -18,18 +18,20 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "dssm_cpu.c")
+RNN_SRC = os.path.join(HERE, "rnn_cpu.c")  # the RNN tower's step (BASELINE config 4)
 OUT_DIR = os.path.join(os.path.dirname(HERE), "_build")
 LIB = os.path.join(OUT_DIR, "libdssm_cpu.so")
 MAXL = 8
 
 
 def build(force: bool = False) -> str:
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+    if (not force and os.path.exists(LIB)
+            and os.path.getmtime(LIB) >= max(os.path.getmtime(SRC), os.path.getmtime(RNN_SRC))):
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = LIB + f".tmp{os.getpid()}"
     subprocess.run(["gcc", "-O3", "-march=x86-64-v3", "-fopenmp", "-fPIC", "-shared", "-std=c11",
-                    "-D_POSIX_C_SOURCE=200112L", SRC, "-o", tmp, "-lm"], check=True)
+                    "-D_POSIX_C_SOURCE=200112L", SRC, RNN_SRC, "-o", tmp, "-lm"], check=True)
     os.replace(tmp, LIB)
     return LIB
 
@@ -54,6 +56,16 @@ class _Params(C.Structure):
                 ("bn_b", C.c_void_p * MAXL)]
 
 
+class _RnnCfg(C.Structure):
+    _fields_ = [("V", C.c_int), ("E", C.c_int), ("H", C.c_int), ("T", C.c_int), ("BS", C.c_int),
+                ("NEG", C.c_int), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
+                ("eps", C.c_float), ("gamma", C.c_float)]
+
+
+class _RnnParams(C.Structure):
+    _fields_ = [("emb", C.c_void_p), ("w", C.c_void_p * 4)]
+
+
 _lib = None
 
 
@@ -76,6 +88,18 @@ def _load():
                                        C.POINTER(_Params), C.POINTER(_Params), P, C.c_float]
         _lib.dssm_cpu_accuracy.restype = C.c_float
         _lib.dssm_cpu_accuracy.argtypes = [P]
+        _lib.rnn_cpu_ws_create.restype = P
+        _lib.rnn_cpu_ws_create.argtypes = [C.POINTER(_RnnCfg)]
+        _lib.rnn_cpu_ws_destroy.argtypes = [P]
+        _lib.rnn_cpu_forward_backward.restype = C.c_float
+        _lib.rnn_cpu_forward_backward.argtypes = [C.POINTER(_RnnCfg), C.POINTER(_RnnParams),
+                                                  C.POINTER(_RnnParams), P, P, P, P, C.c_float]
+        _lib.rnn_cpu_train_step.restype = C.c_float
+        _lib.rnn_cpu_train_step.argtypes = [C.POINTER(_RnnCfg), C.POINTER(_RnnParams), C.POINTER(_RnnParams),
+                                            C.POINTER(_RnnParams), C.POINTER(_RnnParams), P, P, P, P,
+                                            C.c_float, P]
+        _lib.rnn_cpu_output.restype = P
+        _lib.rnn_cpu_output.argtypes = [P]
     return _lib
 
 
@@ -224,3 +248,100 @@ def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 200)
             "kind": "port",
             "sample": f"{steps} full C2 training steps (fwd+bwd+dense Adam, BS={BS}, NEG={NEG}) of the "
                       f"C/OpenMP fp32 restatement (oracle/cpu_c) in {el:.1f}s on {_threads()} threads"}
+
+
+class CpuRnnDSSM:
+    """The RNN tower's step in C (rnn_cpu.c) over the oracle's parameter names (emb, {fw,bw}_{Wg,bg,
+    Wc,bc}); the GRU blocks are stored as [W; b] like the GPU arena."""
+
+    BLOCKS = ("fw_g", "fw_c", "bw_g", "bw_c")
+
+    def __init__(self, nwords, emb, hidden, query_bs, neg, seq_len, params, lr=1e-5, beta1=0.9,
+                 beta2=0.999, eps=1e-8, gamma=20.0):
+        self.lib = _load()
+        self.cfg = _RnnCfg(nwords, emb, hidden, seq_len, query_bs, neg, lr, beta1, beta2, eps, gamma)
+        self.E, self.H, self.R = emb, hidden, query_bs * (2 + neg)
+        K = emb + hidden
+        shapes = {"emb": (nwords, emb), "fw_g": (K + 1, 2 * hidden), "fw_c": (K + 1, hidden),
+                  "bw_g": (K + 1, 2 * hidden), "bw_c": (K + 1, hidden)}
+        self.arrays, self.structs = {}, {}
+        for role in ("p", "g", "m", "v"):
+            arr = {k: np.zeros(s, np.float32) for k, s in shapes.items()}
+            st = _RnnParams()
+            st.emb = _p(arr["emb"])
+            for i, k in enumerate(self.BLOCKS):
+                st.w[i] = _p(arr[k])
+            self.arrays[role], self.structs[role] = arr, st
+        self.set_params(params)
+        self.beta_powers = np.array([beta1, beta2], np.float32)
+        self.ws = self.lib.rnn_cpu_ws_create(C.byref(self.cfg))
+
+    def set_params(self, p):
+        a = self.arrays["p"]
+        a["emb"][...] = p["emb"]
+        for d in ("fw", "bw"):
+            a[f"{d}_g"][...] = np.concatenate([p[f"{d}_Wg"], p[f"{d}_bg"][None, :]], 0)
+            a[f"{d}_c"][...] = np.concatenate([p[f"{d}_Wc"], p[f"{d}_bc"][None, :]], 0)
+
+    def named(self, role: str) -> Dict[str, np.ndarray]:
+        a = self.arrays[role]
+        K = self.E + self.H
+        out = {"emb": a["emb"]}
+        for d in ("fw", "bw"):
+            out[f"{d}_Wg"], out[f"{d}_bg"] = a[f"{d}_g"][:K], a[f"{d}_g"][K]
+            out[f"{d}_Wc"], out[f"{d}_bc"] = a[f"{d}_c"][:K], a[f"{d}_c"][K]
+        return out
+
+    def _args(self, ids, lens, mask):
+        ids = np.ascontiguousarray(ids, np.int32)
+        lens = np.ascontiguousarray(lens, np.int32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.float32)
+        return ids, lens, m
+
+    def forward_backward(self, ids, lens, mask=None, keep=1.0, backward=True) -> float:
+        ids, lens, m = self._args(ids, lens, mask)
+        s = self.structs
+        return float(self.lib.rnn_cpu_forward_backward(C.byref(self.cfg), C.byref(s["p"]),
+                                                       C.byref(s["g"]) if backward else None, self.ws,
+                                                       _p(ids), _p(lens), None if m is None else _p(m),
+                                                       float(keep)))
+
+    def train_step(self, ids, lens, mask=None, keep=1.0) -> float:
+        ids, lens, m = self._args(ids, lens, mask)
+        s = self.structs
+        return float(self.lib.rnn_cpu_train_step(C.byref(self.cfg), C.byref(s["p"]), C.byref(s["g"]),
+                                                 C.byref(s["m"]), C.byref(s["v"]), self.ws, _p(ids), _p(lens),
+                                                 None if m is None else _p(m), float(keep),
+                                                 _p(self.beta_powers)))
+
+    def output(self) -> np.ndarray:
+        ptr = self.lib.rnn_cpu_output(self.ws)
+        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_float)), shape=(self.R, 2 * self.H)).copy()
+
+    def __del__(self):
+        try:
+            if getattr(self, "ws", None):
+                self.lib.rnn_cpu_ws_destroy(self.ws)
+                self.ws = None
+        except Exception:
+            pass
+
+
+def rnn_time_steps(nwords, emb, hidden, query_bs, neg, seq_len, params, batches, keep=0.5,
+                   budget_s: float = 15.0):
+    """Bounded timing of full RNN-tower steps (fwd + BPTT + Adam) on all host threads."""
+    from .. import rnn_oracle as RO
+    m = CpuRnnDSSM(nwords, emb, hidden, query_bs, neg, seq_len, params)
+    R = query_bs * (2 + neg)
+    lens = np.full(R, seq_len, np.int32)
+    masks = [RO.dropout_mask(R, 2 * hidden, keep, 0, i + 1) for i in range(2)]
+    m.train_step(batches[0], lens, masks[0], keep)  # untimed warm-up (page faults, thread pool)
+    n, t0 = 0, time.perf_counter()
+    while n < 1 or time.perf_counter() - t0 < budget_s:
+        m.train_step(batches[n % len(batches)], lens, masks[n % 2], keep)
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": round(query_bs * (neg + 1) * n / el, 1), "unit": "pairs/s", "cores": _threads(),
+            "kind": "port",
+            "sample": f"{n} full config-4 steps (fwd + BPTT + Adam, BS={query_bs}, T={seq_len}) of the "
+                      f"C/OpenMP fp32 restatement (oracle/cpu_c/rnn_cpu.c) in {el:.1f}s"}

@@ -65,3 +65,34 @@ def test_cpu_c_adam_step_teacher_forced():
         assert d.max() <= 2 * lr, k
     f = np.float32
     np.testing.assert_array_equal(m.beta_powers, np.array([f(0.9) * f(0.9), f(0.999) * f(0.999)], np.float32))
+
+
+@pytest.mark.parametrize("keep", [1.0, 0.5])
+def test_rnn_port_matches_oracle(keep):
+    """oracle/cpu_c/rnn_cpu.c (bench.py's config-4 cpu_baseline) against the float64 RNN oracle:
+    embeddings, summed loss, every gradient, then one TF1.x Adam step."""
+    from oracle import rnn_oracle as RO
+    cfg = RO.RnnConfig(nwords=300, emb=32, hidden=32, query_bs=16, neg=4, seq_len=7, lr=1e-3)
+    p = RO.init_params(cfg, seed=3)
+    ids, lens = RO.synth_ids(cfg, seed=5)
+    mask = RO.dropout_mask(cfg.rows, 2 * cfg.hidden, keep, seed=17, step=1)
+    m = cpu_c.CpuRnnDSSM(cfg.nwords, cfg.emb, cfg.hidden, cfg.query_bs, cfg.neg, cfg.seq_len, p, lr=cfg.lr)
+    loss = m.forward_backward(ids, lens, mask, keep)
+    p64 = {k: v.astype(np.float64) for k, v in p.items()}
+    ref = RO.forward(cfg, p64, ids, lens, mask, keep)
+    np.testing.assert_allclose(m.output(), ref["y0"], rtol=1e-4, atol=1e-5)
+    assert abs(loss - ref["loss"]) <= 1e-4 * abs(ref["loss"])
+    g = RO.backward(cfg, p64, ids, lens, ref)
+    got = m.named("g")
+    for k, gr in g.items():
+        assert np.abs(got[k] - gr).max() <= 1e-4 * np.abs(gr).max() + 1e-7, k
+    opt = RO.Adam(cfg, {k: v.copy() for k, v in p.items()})
+    pref = {k: v.copy() for k, v in p.items()}
+    opt.step(pref, {k: v.copy() for k, v in got.items()})
+    m2 = cpu_c.CpuRnnDSSM(cfg.nwords, cfg.emb, cfg.hidden, cfg.query_bs, cfg.neg, cfg.seq_len, p, lr=cfg.lr)
+    m2.train_step(ids, lens, mask, keep)
+    after = m2.named("p")
+    for k in pref:
+        assert np.abs(after[k] - pref[k]).max() <= 2 * cfg.lr, k
+        well = np.abs(g[k]) > 1e-3 * np.abs(g[k]).max()
+        assert np.abs(after[k] - pref[k])[well].max(initial=0.0) <= 1e-6, k

@@ -86,3 +86,26 @@ def test_rnn_trains():
         losses.append(m.loss())
     torch.cuda.synchronize()
     assert np.isfinite(losses).all() and losses[-1] < 0.5 * losses[0], losses[::5]
+
+
+def test_rnn_config4_full_size_matches_oracle():
+    """BASELINE.json config 4 at its full size (vocabulary 21,128, E = H = 128, T = 32, BS = 1024,
+    NEG = 4: 6144 rows), dropout 0.5 and ragged lengths in [1, 32]: the forward embeddings and the
+    summed loss, and every gradient, against the float64 oracle at the fp32 bars of the small cases
+    (32 recurrent steps of fp32 accumulation stay inside them)."""
+    case = dict(nwords=21128, emb=128, hidden=128, query_bs=1024, neg=4, seq_len=32)
+    cfg, p, m, ids, lens = _setup(case, 0.5)
+    m.forward(True)
+    torch.cuda.synchronize()
+    mask = R.dropout_mask(cfg.rows, 2 * cfg.hidden, 0.5, seed=17, step=1)
+    p64 = {k: v.astype(np.float64) for k, v in p.items()}
+    ref = R.forward(cfg, p64, ids, lens, mask, 0.5)
+    np.testing.assert_allclose(m.y0.cpu().numpy(), ref["y0"], rtol=1e-4, atol=1e-5)
+    assert abs(m.loss() - ref["loss"]) <= 1e-4 * abs(ref["loss"]), (m.loss(), ref["loss"])
+    m.backward()
+    torch.cuda.synchronize()
+    g = R.backward(cfg, p64, ids, lens, ref)
+    got = m.named(m.grads)
+    for k, gr in g.items():
+        err = np.abs(got[k] - gr).max()
+        assert err <= 1e-4 * np.abs(gr).max() + 1e-7, (k, err, np.abs(gr).max())
