@@ -52,3 +52,30 @@ def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 1000
             "cores": _threads(), "kind": "port",
             "sample": f"{steps} full C2 steps (fwd+bwd+dense Adam, BS={BS}) of the NumPy float32 "
                       f"oracle in {el:.1f}s"}
+
+
+def time_multiview_steps(cfg, params, feeds, budget_s: float = 15.0, max_steps: int = 10000):
+    """multi_view_dssm_v3 (BASELINE config 5) on the host: the oracle's forward / backward / Adam
+    (oracle/multiview_oracle.py) in float32 with scipy CSR inputs, so FC1 is a sparse product as in
+    the reference's tf.sparse_tensor_dense_matmul (archive/multi_view_dssm_v3.py:121-128).
+    feeds: [(user_csr, item_csr, view, rot)]; one untimed warm-up step."""
+    from . import multiview_oracle as MV
+    p = {k: np.array(v, np.float32) for k, v in params.items()}
+    adam = MV.Adam(cfg, p)
+
+    def step(i):
+        u, it, view, rot = feeds[i % len(feeds)]
+        fw = MV.forward(cfg, p, u, it, view, rot, dtype=np.float32, sparse=True)
+        adam.step(p, MV.backward(cfg, p, fw))
+    step(0)
+    steps, t0 = 0, time.perf_counter()
+    while steps < max_steps:
+        step(1 + steps)
+        steps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(steps * cfg.bs * (cfg.neg + 1) / el, 1), "unit": "pairs/s",
+            "cores": _threads(), "kind": "port",
+            "sample": f"{steps} full config-5 steps (user + active view fwd + bwd + Adam, BS={cfg.bs}) of "
+                      f"the NumPy float32 multi-view oracle with scipy CSR inputs in {el:.1f}s"}

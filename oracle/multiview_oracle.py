@@ -67,11 +67,19 @@ def tower(p, t, X):
     return {"X": X, "z1": z1, "a1": a1, "z2": z2, "y": np.maximum(z2, 0)}
 
 
-def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot):
-    p = {k: v.astype(np.float64) for k, v in p.items()}
+def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot, dtype=np.float64, sparse=False):
+    """dtype float64 with dense X: the parity oracle.  float32 with sparse (scipy CSR) X: the CPU
+    baseline's restatement (bench.py --model multiview)."""
+    p = {k: v.astype(dtype) for k, v in p.items()}
     dims = [cfg.user_d] + list(cfg.view_d)
-    u = tower(p, "user", _dense(user_csr, dims[0]))
-    it = tower(p, f"view{view}", _dense(item_csr, dims[view]))
+    if sparse:
+        import scipy.sparse as sps
+        X = [sps.csr_matrix((np.asarray(c[2], dtype), c[1], c[0]), shape=(cfg.bs, d))
+             for c, d in ((user_csr, dims[0]), (item_csr, dims[view]))]
+    else:
+        X = [_dense(user_csr, dims[0]), _dense(item_csr, dims[view])]
+    u = tower(p, "user", X[0])
+    it = tower(p, f"view{view}", X[1])
     BS, K = cfg.bs, cfg.neg + 1
     idx = np.empty((K, BS), np.int64)
     idx[0] = np.arange(BS)
@@ -88,7 +96,7 @@ def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot):
 
 
 def backward(cfg: MvConfig, p, fw) -> Dict[str, np.ndarray]:
-    p = {k: v.astype(np.float64) for k, v in p.items()}
+    p = {k: v.astype(fw["u"]["y"].dtype) for k, v in p.items()}
     BS, K, g = cfg.bs, cfg.neg + 1, cfg.gamma
     yq, doc, c, qn, dn, prob = fw["u"]["y"], fw["doc"], fw["cos"], fw["qn"], fw["dn"], fw["prob"]
     dcos = (prob - np.eye(K)[0][None, :]) * g
@@ -104,7 +112,7 @@ def backward(cfg: MvConfig, p, fw) -> Dict[str, np.ndarray]:
         dz2 = dy * (tw["z2"] > 0)
         grads[f"{t}_W2"], grads[f"{t}_b2"] = tw["a1"].T @ dz2, dz2.sum(0)
         dz1 = (dz2 @ p[f"{t}_W2"].T) * (tw["z1"] > 0)
-        grads[f"{t}_W1"], grads[f"{t}_b1"] = tw["X"].T @ dz1, dz1.sum(0)
+        grads[f"{t}_W1"], grads[f"{t}_b1"] = np.asarray(tw["X"].T @ dz1), dz1.sum(0)
     return grads
 
 

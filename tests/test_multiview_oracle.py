@@ -27,3 +27,21 @@ def test_multiview_gradients_fd():
             flat[i] = old
             num = (lp - lm) / (2 * h)
             assert abs(num - g[k].reshape(-1)[i]) <= 1e-6 + 1e-5 * abs(num), (k, i, num)
+
+
+def test_multiview_sparse_f32_matches_f64():
+    """The CPU baseline's restatement (float32, scipy CSR FC1) against the float64 dense oracle."""
+    cfg = M.MvConfig(user_d=300, view_d=[200, 250, 280], l1=24, l2=16, bs=64, neg=4)
+    p = M.init_params(cfg, 5)
+    rng = np.random.Generator(np.random.PCG64(6))
+    u = synth_rows(rng, ZipfColumns(300), cfg.bs, 12.0)
+    it = synth_rows(rng, ZipfColumns(280), cfg.bs, 12.0)
+    rot = M.rotations(cfg, 7)
+    f64 = M.forward(cfg, p, u, it, 3, rot)
+    f32 = M.forward(cfg, p, u, it, 3, rot, dtype=np.float32, sparse=True)
+    assert abs(f32["loss"] - f64["loss"]) <= 1e-4 * abs(f64["loss"])
+    np.testing.assert_allclose(f32["cos"], f64["cos"], atol=1e-5)
+    g64, g32 = M.backward(cfg, p, f64), M.backward(cfg, p, f32)
+    assert set(g64) == set(g32)
+    for k in g64:
+        assert np.abs(g32[k] - g64[k]).max() <= 1e-4 * np.abs(g64[k]).max(), k
