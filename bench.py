@@ -167,13 +167,14 @@ def bench_rnn(args):
     """BASELINE.json config 4 (the reference's dssm_rnn tower, dssm_rnn.py:100-218): word embeddings
     (21,128-token vocabulary, data/vocab.txt's size) -> bidirectional GRU(128) over 32 ids per row ->
     dropout 0.5 -> x20 cosine / softmax, BS=1024, NEG=4; fp32; synthetic ids (uniform, full
-    lengths as the reference feeds); one step = forward + BPTT + Adam.  Not the headline."""
+    lengths as the reference feeds); one step = forward + BPTT + Adam.  --dtype bf16 (default): the
+    MFMA recurrences of csrc/rnn_mfma.hip; fp32: the parity mode.  Not the headline."""
     import torch
     from dssm_amd.rnn import RnnDSSM
     V, E, H, T = 21128, 128, 128, 32
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    m = RnnDSSM(V, E, H, BS, NEG, T, lr=1e-5, keep_prob=0.5, device=dev)
+    m = RnnDSSM(V, E, H, BS, NEG, T, lr=1e-5, keep_prob=0.5, device=dev, dtype=args.dtype)
     m.init_params(0)
     rng = np.random.Generator(np.random.PCG64(4))
     batches = [rng.integers(1, V, size=(m.R, T)).astype(np.int32) for _ in range(4)]
@@ -197,7 +198,7 @@ def bench_rnn(args):
     out = {"metric": "query-doc pairs/sec (fwd+bwd), dssm_rnn tower (BASELINE config 4)",
            "value": round(BS * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": 1,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
            "data": "synthetic",
            "config": {"workload": "dssm_rnn: vocab 21128, emb 128, BiGRU(128), seq_len 32, dropout 0.5, "
                                   "BS=1024, NEG=4, fwd+BPTT+Adam", "global_batch": BS, "neg": NEG,
@@ -230,24 +231,43 @@ def bench_multiview(args):
     m.init_params(0)
     cols = ZipfColumns(Dv)
     rng = np.random.Generator(np.random.PCG64(7))
-    feeds = []
+    feeds, host_feeds = [], []
     for b in range(3):
         u = synth_rows(rng, cols, B, 32.0)
         it = synth_rows(rng, cols, B, 32.0)
         m.set_batch(u, it, b + 1)
         feeds.append((dict(m.batch), b + 1))
+        host_feeds.append((u, it, b + 1))
 
-    def step(i):
+    # Adam (user tower + active view, one k_adam_step launch each) is the dominant kernel: HIP events
+    # on the stream the model launches on (torch's current stream) bracket its two launches in every
+    # timed step
+    probes = []
+
+    def step(i, probe=False):
         m.batch, m.view = dict(feeds[i % 3][0]), feeds[i % 3][1]
-        m.train_step()
+        m.forward()
+        m.backward()
+        if probe:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        m.apply_adam()
+        if probe:
+            ev[1].record()
+            probes.append(ev)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(args.warmup + i, probe=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    adam_ms = float(np.mean([a.elapsed_time(b) for a, b in probes])) / 2  # per launch
+    tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
+    # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower
+    adam_bytes = int(28 * tower_params)
+    achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
     out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
            "value": round(B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": 1,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
@@ -256,7 +276,21 @@ def bench_multiview(args):
            "config": {"workload": "multi_view_dssm_v3: user + 3 views (30k sparse -> 300 -> 128), in-batch "
                                   "rotated negatives, BS=4096, NEG=4, fwd+bwd+Adam", "global_batch": B,
                       "neg": NEG, "parallelism": "dp1"},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
+                        "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5)},
            "final_loss": round(m.loss(), 3)}
+    if args.cpu_baseline:
+        try:  # the NumPy float32 restatement (oracle/, test infrastructure) on the host
+            from oracle import cpu_port
+            from oracle.multiview_oracle import MvConfig
+            cfg = MvConfig(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05)
+            host = [(u, it, v, m.rot) for u, it, v in host_feeds]
+            out["cpu_baseline"] = cpu_port.time_multiview_steps(cfg, m.named(), host,
+                                                                budget_s=min(args.cpu_seconds, 20.0))
+            out["cpu_baseline"]["cpu_model"] = cpu_model()
+        except Exception as e:
+            out["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(out), flush=True)
 
 

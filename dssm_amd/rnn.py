@@ -6,7 +6,9 @@ bidirectional GRU (GRUCell(hidden), shared by query / positive / negative inputs
 softmax -> loss = -sum_j log p[j, 0] (summed over queries, :214) -> AdamOptimizer(lr) (:218).
 
 Everything runs through libdssm.so (csrc/rnn.hip for the tower and its Adam, csrc/cosine.hip's
-loss kernel shared with the BoW path); torch tensors are device storage only.
+loss kernel shared with the BoW path); torch tensors are device storage only.  dtype "fp32" (the
+parity mode: fp32 FMA recurrences) or "bf16" (the perf mode, csrc/rnn_mfma.hip: the recurrences on
+bf16 MFMA with register-resident weights, fp32 states / master weights / gradients / Adam).
 
 Parameters live in one flat fp32 arena: the embedding table [nwords x E] first (its Adam update
 uses TF1's IndexedSlices form), then per direction the GRU blocks [Wg; bg] ((E+H+1) x 2H) and
@@ -33,7 +35,7 @@ class RnnDSSM:
     def __init__(self, nwords: int, emb: int, hidden: int, query_bs: int, neg: int = 4,
                  seq_len: int = 10, lr: float = 1e-5, keep_prob: float = 0.5, gamma: float = 20.0,
                  beta1: float = 0.9, beta2: float = 0.999, adam_eps: float = 1e-8, device=None,
-                 seed: int = 0):
+                 seed: int = 0, dtype: str = "fp32"):
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.V, self.E, self.H = int(nwords), int(emb), int(hidden)
@@ -56,10 +58,19 @@ class RnnDSSM:
         self.adam_m = torch.zeros(off, dtype=f32, device=dev)
         self.adam_v = torch.zeros(off, dtype=f32, device=dev)
         self.adam_state = torch.tensor([beta1, beta2] + [0.0] * 62, dtype=f32, device=dev)
-        ws = self.lib.dssm_rnn_ws_floats(self.R, self.T, self.E, self.H)
-        if ws == 0:
-            raise ValueError("unsupported RNN shape (E, H multiples of 4; E+H <= 512; H <= 256)")
-        self.ws = torch.zeros(int(ws), dtype=f32, device=dev)
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError("dtype is 'fp32' or 'bf16'")
+        self.dtype = dtype
+        if dtype == "bf16":
+            if not self.lib.dssm_rnn_bf16_supported(self.E, self.H):
+                raise ValueError("bf16 RNN: (E, H) in {(128, 128), (64, 128), (32, 32)}")
+            ws = self.lib.dssm_rnn_bf16_ws_bytes(self.R, self.T, self.E, self.H, self.V)
+            self.ws = torch.zeros(int(ws), dtype=torch.uint8, device=dev)
+        else:
+            ws = self.lib.dssm_rnn_ws_floats(self.R, self.T, self.E, self.H)
+            if ws == 0:
+                raise ValueError("unsupported RNN shape (E, H multiples of 4; E+H <= 512; H <= 256)")
+            self.ws = torch.zeros(int(ws), dtype=f32, device=dev)
         R2 = (self.R, 2 * H)
         self.y0 = torch.zeros(R2, dtype=f32, device=dev)
         self.y = torch.zeros(R2, dtype=f32, device=dev)
@@ -140,10 +151,16 @@ class RnnDSSM:
     def forward(self, train: bool = True, keep: Optional[float] = None, stream=None):
         s = stream_ptr(stream)
         keep = (self.keep if keep is None else float(keep)) if train else 1.0
-        check(self.lib.dssm_rnn_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
-                                         ptr(self._block(self.params, "emb")), self.E, self.H,
-                                         self._w(self.params), ptr(self.ws), ptr(self.y0), 2 * self.H, s),
-              "rnn_forward")
+        if self.dtype == "bf16":
+            check(self.lib.dssm_rnn_bf16_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
+                                                  ptr(self._block(self.params, "emb")), self.V, self.E, self.H,
+                                                  self._w(self.params), ptr(self.ws), ptr(self.y0), 2 * self.H,
+                                                  s), "rnn_bf16_forward")
+        else:
+            check(self.lib.dssm_rnn_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
+                                             ptr(self._block(self.params, "emb")), self.E, self.H,
+                                             self._w(self.params), ptr(self.ws), ptr(self.y0), 2 * self.H, s),
+                  "rnn_forward")
         if train:
             self._drop_step += 1
         self._keep_used = keep
@@ -164,10 +181,16 @@ class RnnDSSM:
                                         self._keep_used, self.seed, self._drop_step, float(self.BS), s),
               "dropout_bwd")
         gw = (C.c_void_p * 4)(*[ptr(self._block(self.grads, n)) for n in ("fw_g", "fw_c", "bw_g", "bw_c")])
-        check(self.lib.dssm_rnn_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.E, self.H,
-                                          self._w(self.params), ptr(self.dy), 2 * self.H, ptr(self.ws),
-                                          ptr(self._block(self.grads, "emb")), self.V * self.E, gw, s),
-              "rnn_backward")
+        if self.dtype == "bf16":
+            check(self.lib.dssm_rnn_bf16_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.V, self.E,
+                                                   self.H, self._w(self.params), ptr(self.dy), 2 * self.H,
+                                                   ptr(self.ws), ptr(self._block(self.grads, "emb")), gw, s),
+                  "rnn_bf16_backward")
+        else:
+            check(self.lib.dssm_rnn_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.E, self.H,
+                                              self._w(self.params), ptr(self.dy), 2 * self.H, ptr(self.ws),
+                                              ptr(self._block(self.grads, "emb")), self.V * self.E, gw, s),
+                  "rnn_backward")
 
     def apply_adam(self, stream=None):
         check(self.lib.dssm_rnn_adam(ptr(self.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),

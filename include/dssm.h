@@ -387,6 +387,18 @@ int dssm_rnn_dropout(const float* x, float* y, int rows, int cols, int ld, float
 int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int E, int H,
                       const float* const* w, const float* dy, int lddy, float* ws, float* demb,
                       int64_t demb_elems, float* const* gw, void* stream);
+/* bf16 perf mode of the same tower (csrc/rnn_mfma.hip): the recurrences on v_mfma_f32_16x16x32_bf16
+ * with each direction's weights resident in VGPRs (bf16 copies of the fp32 w[4] made by the
+ * kernels), fp32 states / accumulation / gradients, bf16 step caches in ws.  Same arguments and
+ * outputs as the fp32 calls plus V (the embedding table's rows, for its bf16 copy in ws).
+ * Shapes: (E, H) in {(128, 128), (64, 128), (32, 32)} (dssm_rnn_bf16_supported). */
+int dssm_rnn_bf16_supported(int E, int H);
+size_t dssm_rnn_bf16_ws_bytes(int R, int T, int E, int H, int V);
+int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
+                          int E, int H, const float* const* w, void* ws, float* y, int ldy, void* stream);
+int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
+                           const float* const* w, const float* dy, int lddy, void* ws, float* demb,
+                           float* const* gw, void* stream);
 /* AdamOptimizer (dssm_rnn.py:218) over a flat arena: [0, n_sparse) the embedding table (TF1's
  * deduplicated IndexedSlices update, m*b1 + (1-b1) g form), the rest dense ApplyAdam; state =
  * device {beta1_power, beta2_power}, advanced after the update. */
