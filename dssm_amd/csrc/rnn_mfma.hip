@@ -45,8 +45,11 @@ struct Geo {
   static constexpr int LDA = K + 8, LDR = H + 8, LDG = 2 * H + 8;  // LDS row strides (u16)
 };
 
-__device__ __forceinline__ float fsig(float x) { return 1.0f / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 1.0f - 2.0f / (__expf(2.0f * x) + 1.0f); }
+// v_exp_f32 + v_rcp_f32 (1 ulp): the IEEE division sequence was half of the forward's VALU work
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
+}
 
 __device__ __forceinline__ unsigned pk2(float a, float b) {
   return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
@@ -132,17 +135,22 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
       len_r[m][i] = sLen[16 * m + 4 * lg + i];
       hs[m][i] = 0.f;
     }
-  // x_0 and h_{-1} = 0
-  uint4 xr[XPT];
-#pragma unroll
-  for (int i = 0; i < XPT; ++i) {
-    const int q = tid + i * NT;
-    if (q < NXQ) {
-      const int row = q / EC8, c8 = q - row * EC8;
-      xr[i] = *reinterpret_cast<const uint4*>(emb16 + (size_t)tok(sIds, sLen, row, 0, T, dir) * E + c8 * 8);
-      *reinterpret_cast<uint4*>(&sA[row * LDA + c8 * 8]) = xr[i];
-    }
-  }
+  // x_0 and h_{-1} = 0.  A thread stages at most two 16-B chunks of x per step (x0, x1: named
+  // registers, not an array, so nothing is indexed at run time)
+  static_assert(XPT <= 2, "x staging: at most two chunks per thread");
+  auto xsrc = [&](int q, int t) {
+    const int row = q / EC8, c8 = q - row * EC8;
+    return reinterpret_cast<const uint4*>(emb16 + (size_t)tok(sIds, sLen, row, t, T, dir) * E + c8 * 8);
+  };
+  auto xdst = [&](int q) {
+    const int row = q / EC8, c8 = q - row * EC8;
+    return reinterpret_cast<uint4*>(&sA[row * LDA + c8 * 8]);
+  };
+  const int q0 = tid, q1 = tid + NT;
+  const bool has0 = q0 < NXQ, has1 = XPT > 1 && q1 < NXQ;
+  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;
+  if (has0) *xdst(q0) = *xsrc(q0, 0);
+  if (has1) *xdst(q1) = *xsrc(q1, 0);
   for (int i = tid; i < M * HC8; i += NT) {
     const int row = i / HC8, c8 = i - row * HC8;
     *reinterpret_cast<uint4*>(&sA[row * LDA + E + c8 * 8]) = make_uint4(0, 0, 0, 0);
@@ -154,15 +162,8 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
   for (int t = 0; t < T; ++t) {
     // next step's input rows in flight during this step
     if (t + 1 < T) {
-#pragma unroll
-      for (int i = 0; i < XPT; ++i) {
-        const int q = tid + i * NT;
-        if (q < NXQ) {
-          const int row = q / EC8, c8 = q - row * EC8;
-          xr[i] = *reinterpret_cast<const uint4*>(emb16 + (size_t)tok(sIds, sLen, row, t + 1, T, dir) * E +
-                                                  c8 * 8);
-        }
-      }
+      if (has0) x0 = *xsrc(q0, t + 1);
+      if (has1) x1 = *xsrc(q1, t + 1);
     }
     // P1: gates and the candidate's x part
     f32x4 ar[MT], au[MT], ac[MT];
@@ -192,18 +193,14 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
         sR[(16 * m + 4 * lg + i) * LDR + gcol] = f2bf(rv * hs[m][i]);
       }
     __syncthreads();
-    // save [x_t | h_{t-1}] and r*h_{t-1}; the x slots take x_{t+1} (same thread, same chunk)
+    // save [x_t | h_{t-1}] and r*h_{t-1}
     const size_t rowbase = (size_t)dir * plane + (size_t)t * R + r0;
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int q = tid + i * NT;
-      if (q < NXQ) {
-        const int row = q / EC8, c8 = q - row * EC8;
-        uint4* p = reinterpret_cast<uint4*>(&sA[row * LDA + c8 * 8]);
-        if (row < nrow) *reinterpret_cast<uint4*>(XH + (rowbase + row) * K + c8 * 8) = *p;
-        if (t + 1 < T) *p = xr[i];
-      }
-    }
+    auto save_x = [&](int q) {
+      const int row = q / EC8, c8 = q - row * EC8;
+      if (row < nrow) *reinterpret_cast<uint4*>(XH + (rowbase + row) * K + c8 * 8) = *xdst(q);
+    };
+    if (has0) save_x(q0);
+    if (has1) save_x(q1);
     for (int i = tid; i < M * HC8; i += NT) {
       const int row = i / HC8, c8 = i - row * HC8;
       if (row < nrow) {
@@ -222,6 +219,11 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
         ac[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bC[XC + c], ac[m], 0, 0, 0);
       }
     __syncthreads();
+    // x_{t+1} into the x slots, free since the barrier (its loads had the whole step to land)
+    if (t + 1 < T) {
+      if (has0) *xdst(q0) = x0;
+      if (has1) *xdst(q1) = x1;
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       float cv[4], h0[4];
@@ -254,22 +256,24 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
 }
 
 // ---- BPTT --------------------------------------------------------------------------------------
-// Same grid.  dout [R x ldo] fp32.  Writes DG [dir][t][R][2H] = (dr, du) and DC [dir][t][R][H]
-// (u16; zero at a row's padding steps) and adds dx into demb (fp32 atomics).
+// Same grid.  dout [R x ldo] fp32.  Writes DG [dir][t][R][2H] = (dr, du), DC [dir][t][R][H] and the
+// input gradient DX [dir][t][R][E] (u16; zero at a row's padding steps).  The embedding gradient is
+// DX summed per token afterwards (k_emb_grad), not scattered with atomics here: 50M fp32 atomic adds
+// per config-4 step would run at the chip's ~1.3 TB/s atomic rate (MI355X_MICROARCH.md).
 template <int E, int H, int MT>
 __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
     GruDimsB d, const int* __restrict__ ids, const int* __restrict__ lens, const float* __restrict__ wg_fw,
     const float* __restrict__ wc_fw, const float* __restrict__ wg_bw, const float* __restrict__ wc_bw,
     const float* __restrict__ dout, int ldo, const u16* __restrict__ GF, u16* __restrict__ DG,
-    u16* __restrict__ DC, float* __restrict__ demb) {
+    u16* __restrict__ DC, u16* __restrict__ DX) {
   using G = Geo<E, H, MT>;
   constexpr int HC = G::HC, NW = G::NW, NT = G::NT, M = G::M, LDR = G::LDR, LDG = G::LDG;
-  constexpr int HC8 = H / 8;
+  constexpr int HC8 = H / 8, EC8 = E / 8, LDX = E + 8;
   __shared__ __attribute__((aligned(16))) u16 sC[M * LDR];  // dc
   __shared__ __attribute__((aligned(16))) u16 sG[M * LDG];  // [dr | du]
+  __shared__ __attribute__((aligned(16))) u16 sX[M * LDX];  // dx
   extern __shared__ int sDyn[];
   int* sLen = sDyn;
-  int* sIds = sDyn + M;
 
   const int T = d.T, R = d.R, dir = blockIdx.y;
   const float* Wg = dir ? wg_bw : wg_fw;
@@ -277,11 +281,12 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lc = lane & 15, lg = lane >> 4;
   const int r0 = blockIdx.x * M, nrow = min(M, R - r0);
   for (int i = tid; i < M; i += NT) sLen[i] = i < nrow ? lens[r0 + i] : 0;
-  for (int i = tid; i < M * T; i += NT) sIds[i] = i < nrow * T ? ids[(size_t)r0 * T + i] : 0;
 
   // transposed products: B[k = gate/candidate column][n = input column] = W[n][k] (contiguous)
   const int gcol = 16 * w + lc;
-  const bool hasx = 16 * w < E;  // wave-uniform: this wave also owns x columns 16w..16w+15
+  // wave-uniform: this wave also owns x columns 16w..16w+15 (every wave when E >= H: a constant, so
+  // the conditional MFMAs on ax compile without accumulator copies)
+  const bool hasx = (E >= H) || 16 * w < E;
   const int kh = E + gcol, kx = hasx ? gcol : 0;
   bf16x8 c1h[HC], c1x[HC], c2h[2 * HC], c2x[2 * HC];
 #pragma unroll
@@ -406,18 +411,298 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
 #pragma unroll
       for (int i = 0; i < 4; ++i) dh[m][i] = dhp[m][i] + a2[m][i];
     if (hasx) {
-      using gfloat = __attribute__((address_space(1))) float;
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * m + 4 * lg + i;
-          if (t < sLen[row])
-            __hip_atomic_fetch_add((gfloat*)(demb + (size_t)tok(sIds, sLen, row, t, T, dir) * E + gcol),
-                                   ax[m][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int i = 0; i < 4; ++i) sX[(16 * m + 4 * lg + i) * LDX + kx] = f2bf(ax[m][i]);
     }
     __syncthreads();
+    // dx rows out (the next step's sX writes come after two more barriers)
+    for (int i = tid; i < M * EC8; i += NT) {
+      const int row = i / EC8, c8 = i - row * EC8;
+      if (row < nrow)
+        *reinterpret_cast<uint4*>(DX + (rowbase + row) * E + c8 * 8) =
+            *reinterpret_cast<const uint4*>(&sX[row * LDX + c8 * 8]);
+    }
+  }
+}
+
+// ---- embedding gradient: dx summed per token -------------------------------------------------
+// The batch's active (row, position) pairs bucketed by token (count, one-workgroup scan, fill), then
+// one wave per token sums its positions' dx rows of both directions (fw at step s, bw at step
+// len - 1 - s) in fp32 and writes the token's whole gradient row (zero for absent tokens).
+__global__ void k_tok_count(const int* __restrict__ ids, const int* __restrict__ lens, int R, int T,
+                            int* __restrict__ cnt) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * T; i += gridDim.x * blockDim.x) {
+    const int r = i / T, p = i - r * T;
+    if (p < lens[r]) atomicAdd(&cnt[ids[i]], 1);
+  }
+}
+
+// exclusive scan of cnt[0, V) (V <= 32768) by one workgroup: the counts are loaded coalesced into
+// LDS (dynamic, V ints), each thread scans its contiguous slice, a shuffle scan per wave and a scan
+// of the 16 wave totals join the slices
+__global__ __launch_bounds__(1024) void k_tok_scan(const int* __restrict__ cnt, int V, int* __restrict__ start,
+                                                   int* __restrict__ cursor) {
+  extern __shared__ int sc[];
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, per = (V + 1023) / 1024, b = min(V, t * per),
+            e = min(V, b + per);
+  for (int i = t; i < V; i += 1024) sc[i] = cnt[i];
+  __syncthreads();
+  int s = 0;
+  for (int i = b; i < e; ++i) s += sc[i];
+  int x = s;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  int off = 0;
+  for (int i = 0; i < wv; ++i) off += wsum[i];
+  int run = off + x - s;
+  for (int i = b; i < e; ++i) {
+    const int c = sc[i];
+    sc[i] = run;
+    run += c;
+  }
+  __syncthreads();
+  for (int i = t; i < V; i += 1024) {
+    start[i] = sc[i];
+    cursor[i] = sc[i];
+  }
+  if (t == 1023) start[V] = off + x;
+}
+
+__global__ void k_tok_fill(const int* __restrict__ ids, const int* __restrict__ lens, int R, int T,
+                           int* __restrict__ cursor, int* __restrict__ pos) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * T; i += gridDim.x * blockDim.x) {
+    const int r = i / T, p = i - r * T;
+    if (p < lens[r]) pos[atomicAdd(&cursor[ids[i]], 1)] = i;
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void k_emb_grad(const int* __restrict__ start, const int* __restrict__ pos,
+                                                  const int* __restrict__ lens, int R, int T, int V,
+                                                  const u16* __restrict__ DX, float* __restrict__ demb) {
+  constexpr int CPL = E >= 128 ? E / 64 : 1;  // columns per lane
+  static_assert(CPL <= 2, "E <= 128");
+  const int lane = threadIdx.x & 63;
+  const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const bool on = lane * CPL < E;
+  const int c = on ? lane * CPL : 0;  // idle lanes (E = 32) read column 0 and write nothing
+  const size_t plane = (size_t)T * R;
+  float a0 = 0.f, a1 = 0.f;
+  const int b = start[v], n = start[v + 1] - b;
+  // 64 entries at a time: lane l resolves entry l's two row offsets, then every lane walks the
+  // entries with the offsets broadcast, the row loads of different entries independent
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    const int cnt = min(64, n - j0);
+    int ofw = 0, obw = 0;  // element offsets / E (rows of DX)
+    if (lane < cnt) {
+      const int i = pos[b + j0 + lane], r = i / T, p = i - r * T, L = lens[r];
+      ofw = p * R + r;
+      obw = (int)plane + (L - 1 - p) * R + r;
+    }
+    auto add = [&](int k) {
+      const u16* fw = DX + (size_t)__shfl(ofw, k) * E + c;
+      const u16* bw = DX + (size_t)__shfl(obw, k) * E + c;
+      if constexpr (CPL == 2) {
+        const unsigned x = *reinterpret_cast<const unsigned*>(fw), y = *reinterpret_cast<const unsigned*>(bw);
+        a0 += lo16(x) + lo16(y);
+        a1 += hi16(x) + hi16(y);
+      } else {
+        a0 += bf2f(*fw) + bf2f(*bw);
+      }
+    };
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {  // four entries' loads in flight together
+      add(k);
+      add(k + 1);
+      add(k + 2);
+      add(k + 3);
+    }
+    for (; k < cnt; ++k) add(k);
+  }
+  if (on) {
+    demb[(size_t)v * E + c] = a0;
+    if constexpr (CPL == 2) demb[(size_t)v * E + c + 1] = a1;
+  }
+}
+
+// ---- weight gradients ---------------------------------------------------------------------------
+// dW = Z^T dP over all T*R (step, row) pairs of a direction, with Z, dP the row-major bf16 step caches
+// ([x | h] or r*h, and [dr | du] or dc): a reduction over ~2e5 rows into a few 128 x 128 tiles.
+// One launch covers every output tile of both directions x S row splits.  A workgroup (8 waves, 2 x 4
+// of 64 x 32) streams its split's 64-row slabs of the two 128-column panels into LDS as plain
+// 16-B row chunks (XOR-swizzled chunk order) and takes BOTH MFMA operands k-contiguous with
+// ds_read_b64_tr_b16 (two per 16x16x32 fragment) -- the transpose the row-major caches need happens in
+// the LDS read, conflict-free.  The bias gradient (column sums of dP) rides on the B fragments of the
+// first row of waves.  Partials go to a [split][tile][129][128] slab; a second launch sums the splits
+// in fixed order into the arena.
+struct DwTile {
+  const u16* A;
+  const u16* B;
+  float* dest;  // row drow0 of the destination block, ld ldd
+  float* bias;  // null: no bias row from this tile
+  int lda, ldb, m0, mlen, n0, nlen, ldd, drow0;
+};
+constexpr int kDwMaxTiles = 16, kDwSlabRows = 129;
+struct DwArgs {
+  DwTile t[kDwMaxTiles];
+  int ntiles, TR, splits, kps;
+  float* slab;
+};
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef short v8s_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+__device__ __forceinline__ int dw_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int dw_off(int row, int ch) { return row * 128 + 8 * (ch ^ dw_sw(row)); }
+
+// fragment of a [64 k][128 col] swizzled image: lane (g, i) gets col c0 + i, rows kk0 + 8g + 0..7
+__device__ __forceinline__ bf16x8 dw_frag(const u16* S, int kk0, int c0, int g, int q, int p) {
+  const int r0 = kk0 + 8 * g + q, ch = (c0 >> 3) + (p >> 1), sub = 4 * (p & 1);
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(S + dw_off(r0, ch) + sub));
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(S + dw_off(r0 + 4, ch) + sub));
+  const v8s_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(512) void k_rnn_dw(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 sA[2][64 * 128];
+  __shared__ __attribute__((aligned(16))) u16 sB[2][64 * 128];
+  const int W = a.splits * a.ntiles;
+  // the tiles of one row split on one XCD (round-robin dispatch): they share the split's panels in L2
+  const int L = (W % 8 == 0) ? (int)(blockIdx.x % 8) * (W / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int ti = L % a.ntiles, split = L / a.ntiles;
+  // the tile record read in place from the kernarg segment (a dynamic index into the by-value
+  // argument would copy it to scratch)
+  const DwTile& T = ((const DwArgs*)__builtin_amdgcn_kernarg_segment_ptr())->t[ti];
+  const int kbeg = split * a.kps, kend = min(a.TR, kbeg + a.kps);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+
+  // two register sets: the global loads of slab s + 2 are issued while slab s is multiplied, so each
+  // has a whole iteration to land before its LDS store at the end of iteration s + 1
+  struct Set {
+    uint4 a0, a1, b0, b1;
+  };
+  const int ch = tid & 15, row0 = tid >> 4;  // chunk e = tid + 512 s: row row0 + 32 s, chunk ch
+  const bool okm = ch * 8 < T.mlen, okn = ch * 8 < T.nlen;
+  const u16* pa = T.A + T.m0 + ch * 8;
+  const u16* pb = T.B + T.n0 + ch * 8;
+  const int lda = T.lda, ldb = T.ldb;
+  auto ld1 = [&](const u16* base, int ld, bool okc, int k) {
+    // a value select, not a select of addresses (that would put the zero vector on scratch)
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (okc && k < kend) v = *reinterpret_cast<const uint4*>(base + (size_t)k * ld);
+    return v;
+  };
+  auto load = [&](int k0) {
+    Set r;
+    r.a0 = ld1(pa, lda, okm, k0 + row0);
+    r.a1 = ld1(pa, lda, okm, k0 + row0 + 32);
+    r.b0 = ld1(pb, ldb, okn, k0 + row0);
+    r.b1 = ld1(pb, ldb, okn, k0 + row0 + 32);
+    return r;
+  };
+  const int o0 = dw_off(row0, ch), o1 = dw_off(row0 + 32, ch);
+  auto store = [&](int buf, const Set& r) {
+    *reinterpret_cast<uint4*>(&sA[buf][o0]) = r.a0;
+    *reinterpret_cast<uint4*>(&sA[buf][o1]) = r.a1;
+    *reinterpret_cast<uint4*>(&sB[buf][o0]) = r.b0;
+    *reinterpret_cast<uint4*>(&sB[buf][o1]) = r.b1;
+  };
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[2] = {0.f, 0.f};
+  const bool dobias = T.bias != nullptr && wm == 0;  // wave-uniform
+
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      bf16x8 af[4], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = dw_frag(sA[buf], 32 * kc, wm * 64 + 16 * i, g, q, p);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = dw_frag(sB[buf], 32 * kc, wn * 32 + 16 * j, g, q, p);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (dobias) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum[j] += (float)bfr[j][e];
+      }
+    }
+  };
+  const int nst = kbeg < kend ? (kend - kbeg + 63) / 64 : 0;
+  Set r0{}, r1{};
+  if (nst > 0) r0 = load(kbeg);
+  if (nst > 1) r1 = load(kbeg + 64);
+  if (nst > 0) store(0, r0);
+  __syncthreads();
+  // iteration s: multiply slab s (LDS buffer s & 1), load slab s + 2 into set s & 1, store slab s + 1
+  // (set (s + 1) & 1) into the other buffer; unrolled by two so the sets stay in registers
+  for (int s = 0; s < nst; s += 2) {
+    if (s + 2 < nst) r0 = load(kbeg + 64 * (s + 2));
+    compute(0);
+    if (s + 1 < nst) store(1, r1);
+    __syncthreads();
+    if (s + 1 >= nst) break;
+    if (s + 3 < nst) r1 = load(kbeg + 64 * (s + 3));
+    compute(1);
+    if (s + 2 < nst) store(0, r0);
+    __syncthreads();
+  }
+  float* out = a.slab + ((size_t)split * a.ntiles + ti) * kDwSlabRows * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(size_t)(wm * 64 + 16 * i + 4 * g + r) * 128 + wn * 32 + 16 * j + li] = acc[i][j][r];
+  if (dobias) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v = bsum[j];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (g == 0) out[(size_t)128 * 128 + wn * 32 + 16 * j + li] = v;
+    }
+  }
+}
+
+// sum the splits in fixed order into the destinations (rows < mlen, columns < nlen; row 128 = bias)
+__global__ __launch_bounds__(256) void k_rnn_dw_reduce(DwArgs a) {
+  const int per_tile = kDwSlabRows * 32;  // float4 groups
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.ntiles * per_tile; e += gridDim.x * blockDim.x) {
+    const int ti = e / per_tile, rem = e - ti * per_tile, row = rem >> 5, c4 = (rem & 31) * 4;
+    const DwTile& T = ((const DwArgs*)__builtin_amdgcn_kernarg_segment_ptr())->t[ti];
+    if (c4 >= T.nlen) continue;
+    if (row < 128 ? row >= T.mlen : T.bias == nullptr) continue;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < a.splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(
+          a.slab + (((size_t)sp * a.ntiles + ti) * kDwSlabRows + row) * 128 + c4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float* d = row < 128 ? T.dest + (size_t)(T.drow0 + row) * T.ldd + T.n0 + c4 : T.bias + T.n0 + c4;
+    *reinterpret_cast<float4*>(d) = s;
   }
 }
 
@@ -430,8 +715,11 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 }
 
 // ---- workspace and dispatch -------------------------------------------------------------------
+constexpr int kDwMaxSplits = 64;
+
 struct WsB {
-  u16 *XH, *RH, *GF, *DG, *DC, *emb16;
+  u16 *XH, *RH, *GF, *DG, *DC, *DX, *emb16;
+  int *cnt, *start, *cursor, *pos;
   float* slab;
   size_t bytes;
 };
@@ -452,15 +740,18 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
   w.GF = (u16*)take(2 * (size_t)T * NB * 16 * H * 4 * 2);
   w.DG = (u16*)take(2 * TR * 2 * H * 2);
   w.DC = (u16*)take(2 * TR * H * 2);
+  w.DX = (u16*)take(2 * TR * E * 2);
   w.emb16 = (u16*)take((size_t)V * E * 2);
-  const size_t slab = std::max({gemm_dw_slab_floats((int)K + 1, 2 * H, (int)TR, true),
-                                gemm_dw_slab_floats(E, H, (int)TR, true),
-                                gemm_dw_slab_floats(H + 1, H, (int)TR, true)});
-  w.slab = (float*)take(slab * 4 + 64);
+  w.cnt = (int*)take(((size_t)V + 1) * 4);
+  w.start = (int*)take(((size_t)V + 1) * 4);
+  w.cursor = (int*)take(((size_t)V + 1) * 4);
+  w.pos = (int*)take(TR * 4);
+  w.slab = (float*)take((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128 * 4);
   w.bytes = off;
   return w;
 }
 
+// (the vocabulary is bounded separately: V <= 32768 for k_tok_scan)
 bool shape_ok(int E, int H) { return (E == 128 && H == 128) || (E == 64 && H == 128) || (E == 32 && H == 32); }
 
 // sequences per workgroup: fewest rounds of the 256 CUs (one workgroup per CU), then the fewest
@@ -492,9 +783,9 @@ template <int E, int H, int MT>
 void launch_bwd_t(const GruDimsB& d, const int* ids, const int* lens, const float* const* w, const float* dy,
                   int lddy, const WsB& ws, float* demb, hipStream_t s) {
   constexpr int M = 16 * MT;
-  const size_t dyn = sizeof(int) * (size_t)M * (1 + d.T);
+  const size_t dyn = sizeof(int) * (size_t)M;
   hipLaunchKernelGGL((k_gru_bwd_mfma<E, H, MT>), dim3((d.R + M - 1) / M, 2), dim3(Geo<E, H, MT>::NT), dyn, s, d,
-                     ids, lens, w[0], w[1], w[2], w[3], dy, lddy, ws.GF, ws.DG, ws.DC, demb);
+                     ids, lens, w[0], w[1], w[2], w[3], dy, lddy, ws.GF, ws.DG, ws.DC, ws.DX);
 }
 
 template <int E, int H>
@@ -532,13 +823,13 @@ extern "C" {
 int dssm_rnn_bf16_supported(int E, int H) { return dssm::shape_ok(E, H) ? 1 : 0; }
 
 size_t dssm_rnn_bf16_ws_bytes(int R, int T, int E, int H, int V) {
-  if (R <= 0 || T <= 0 || V <= 0 || !dssm::shape_ok(E, H)) return 0;
+  if (R <= 0 || T <= 0 || V <= 0 || V > 32768 || !dssm::shape_ok(E, H)) return 0;
   return dssm::ws_layout(nullptr, R, T, E, H, V).bytes;
 }
 
 int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
                           int E, int H, const float* const* w, void* ws, float* y, int ldy, void* stream) {
-  if (!ids || !lens || !emb || !w || !ws || !y || R <= 0 || T <= 0 || V <= 0 || !dssm::shape_ok(E, H) ||
+  if (!ids || !lens || !emb || !w || !ws || !y || R <= 0 || T <= 0 || V <= 0 || V > 32768 || !dssm::shape_ok(E, H) ||
       ldy < 2 * H)
     return rerr_b(DSSM_E_INVALID, "rnn_bf16_forward: bad argument or unsupported (E, H)");
   hipStream_t s = (hipStream_t)stream;
@@ -561,13 +852,19 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream) {
-  if (!ids || !lens || !w || !dy || !ws || !demb || !gw || R <= 0 || T <= 0 || V <= 0 ||
+  if (!ids || !lens || !w || !dy || !ws || !demb || !gw || R <= 0 || T <= 0 || V <= 0 || V > 32768 ||
       !dssm::shape_ok(E, H) || lddy < 2 * H)
     return rerr_b(DSSM_E_INVALID, "rnn_bf16_backward: bad argument or unsupported (E, H)");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(demb, 0, sizeof(float) * (size_t)V * E, s) != hipSuccess)
-    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: hipMemsetAsync");
   const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
+  // the batch's positions bucketed by token (for the embedding gradient after the BPTT)
+  if (hipMemsetAsync(L.cnt, 0, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
+    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: hipMemsetAsync");
+  const int gpos = std::max(1, std::min((R * T + 255) / 256, 2048));
+  hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt);
+  hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start,
+                     L.cursor);
+  hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cursor, L.pos);
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   if (E == 128)
@@ -576,22 +873,49 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
     dssm::dispatch_bwd<64, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else
     dssm::dispatch_bwd<32, 32>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
-  // [W; b] gradients: split-K bf16 TN GEMMs over all T*R (step, row) pairs; the ones row = bias.
-  //   dWg = [x | h]^T [dr | du];  dWc = [x ; r*h]^T dc in two row blocks (x rows, then state rows + bias)
+  const dim3 gemb((V + 3) / 4);
+  if (E == 128)
+    hipLaunchKernelGGL(dssm::k_emb_grad<128>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
+  else if (E == 64)
+    hipLaunchKernelGGL(dssm::k_emb_grad<64>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
+  else
+    hipLaunchKernelGGL(dssm::k_emb_grad<32>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
+  // [W; b] gradients, both directions in one launch (k_rnn_dw) + a fixed-order split reduce:
+  //   dWg = [x | h]^T [dr | du] (+ bias = column sums),  dWc rows [0, E) = x^T dc (+ bias),
+  //   dWc rows [E, E+H) = (r*h)^T dc
   const int K = E + H, TR = T * R;
-  const size_t half = (size_t)TR;
+  dssm::DwArgs A{};
+  int n = 0;
   for (int dir = 0; dir < 2; ++dir) {
-    const u16* XH = L.XH + half * dir * K;
-    hipError_t e = dssm::launch_gemm(dssm::GEMM_DW, true, K + 1, 2 * H, TR, XH, K, L.DG + half * dir * 2 * H,
-                                     2 * H, gw[2 * dir], 2 * H, nullptr, true, L.slab, s, nullptr);
-    if (e == hipSuccess)
-      e = dssm::launch_gemm(dssm::GEMM_DW, true, E, H, TR, XH, K, L.DC + half * dir * H, H, gw[2 * dir + 1], H,
-                            nullptr, false, L.slab, s, nullptr);
-    if (e == hipSuccess)
-      e = dssm::launch_gemm(dssm::GEMM_DW, true, H + 1, H, TR, L.RH + half * dir * H, H, L.DC + half * dir * H,
-                            H, gw[2 * dir + 1] + (size_t)E * H, H, nullptr, true, L.slab, s, nullptr);
-    if (e != hipSuccess) return rerr_b(DSSM_E_HIP, hipGetErrorString(e));
+    const size_t half = (size_t)TR * dir;
+    const u16* XH = L.XH + half * K;
+    const u16* RH = L.RH + half * H;
+    const u16* DG = L.DG + half * 2 * H;
+    const u16* DC = L.DC + half * H;
+    float* gg = gw[2 * dir];
+    float* gc = gw[2 * dir + 1];
+    for (int mb = 0; mb < K; mb += 128)
+      for (int nb = 0; nb < 2 * H; nb += 128)
+        A.t[n++] = dssm::DwTile{XH, DG, gg, mb == 0 ? gg + (size_t)K * 2 * H : nullptr, K, 2 * H, mb,
+                                std::min(128, K - mb), nb, std::min(128, 2 * H - nb), 2 * H, mb};
+    for (int mb = 0; mb < E; mb += 128)
+      for (int nb = 0; nb < H; nb += 128)
+        A.t[n++] = dssm::DwTile{XH, DC, gc, mb == 0 ? gc + (size_t)K * H : nullptr, K, H, mb,
+                                std::min(128, E - mb), nb, std::min(128, H - nb), H, mb};
+    for (int mb = 0; mb < H; mb += 128)
+      for (int nb = 0; nb < H; nb += 128)
+        A.t[n++] = dssm::DwTile{RH, DC, gc, nullptr, H, H, mb, std::min(128, H - mb), nb, std::min(128, H - nb), H,
+                                E + mb};
   }
+  A.ntiles = n;
+  A.TR = TR;
+  A.splits = std::max(1, std::min({dssm::kDwMaxSplits, (384 + n - 1) / n, (TR + 63) / 64}));
+  A.splits += A.splits & 1;  // even: with 12 tiles (E = H = 128) the XCD grouping needs splits * ntiles % 8 == 0
+  A.splits = std::min(A.splits, dssm::kDwMaxSplits);
+  A.kps = ((TR + A.splits - 1) / A.splits + 63) / 64 * 64;
+  A.slab = L.slab;
+  hipLaunchKernelGGL(dssm::k_rnn_dw, dim3(A.splits * n), dim3(512), 0, s, A);
+  hipLaunchKernelGGL(dssm::k_rnn_dw_reduce, dim3((n * dssm::kDwSlabRows * 32 + 255) / 256), dim3(256), 0, s, A);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
 }

@@ -391,7 +391,7 @@ int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int
  * with each direction's weights resident in VGPRs (bf16 copies of the fp32 w[4] made by the
  * kernels), fp32 states / accumulation / gradients, bf16 step caches in ws.  Same arguments and
  * outputs as the fp32 calls plus V (the embedding table's rows, for its bf16 copy in ws).
- * Shapes: (E, H) in {(128, 128), (64, 128), (32, 32)} (dssm_rnn_bf16_supported). */
+ * Shapes: (E, H) in {(128, 128), (64, 128), (32, 32)} (dssm_rnn_bf16_supported), V <= 32768. */
 int dssm_rnn_bf16_supported(int E, int H);
 size_t dssm_rnn_bf16_ws_bytes(int R, int T, int E, int H, int V);
 int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
