@@ -187,12 +187,12 @@ def bench_rnn(args):
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    probe = args.dtype == "bf16" and args.probes
+    if probe:  # HIP events around every timed BPTT launch, on the stream it runs on (libdssm.so)
+        m.lib.dssm_rnn_bf16_probe(args.steps)
     t0 = time.perf_counter()
-    ev[0].record()
     for i in range(args.steps):
         step(args.warmup + i)
-    ev[1].record()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out = {"metric": "query-doc pairs/sec (fwd+bwd), dssm_rnn tower (BASELINE config 4)",
@@ -204,6 +204,21 @@ def bench_rnn(args):
                                   "BS=1024, NEG=4, fwd+BPTT+Adam", "global_batch": BS, "neg": NEG,
                       "parallelism": "dp1"},
            "final_loss": round(m.loss(), 3)}
+    if probe:
+        import ctypes as C
+        avg, cnt = C.c_double(), C.c_int()
+        m.lib.dssm_rnn_bf16_probe_read(C.byref(avg), C.byref(cnt))
+        m.lib.dssm_rnn_bf16_probe(0)
+        # BPTT algorithmic bytes: per (direction, step, row, hidden column) the
+        # (r, u, c, h_{t-1}) cache read (8 B) and dr, du, dc written (6 B); dx written per input
+        # column (2 B); the incoming final-state gradient (fp32)
+        R = m.R
+        bptt = 2 * T * R * (H * 14 + E * 2) + R * 2 * H * 4
+        ms = avg.value
+        out["roofline"] = {"bound": "hbm", "achieved": round(bptt / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(bptt / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": None, "kernel": "k_gru_bwd_mfma", "bytes_per_launch": bptt,
+                           "avg_ms": round(ms, 5), "launches": cnt.value}
     if args.cpu_baseline:
         try:  # the C/OpenMP fp32 restatement (oracle/cpu_c/rnn_cpu.c, test infrastructure) on the host
             from oracle import cpu_c

@@ -15,9 +15,10 @@
 //   P2  (r*h) · Wc_h              -> c = tanh(...), h' = u h + (1 - u) c (carried past the length)
 // The BPTT kernel mirrors it with the transposed products (dc · Wc^T, [dr | du] · Wg^T), the
 // lane-local gate derivatives and the embedding gradient as fp32 atomics from the x columns.
-// Saved for the backward: [x_t | h_{t-1}] and r*h_{t-1} row-major (the weight-gradient GEMMs'
-// A operands) and (r, u, c, h_{t-1}) in the accumulator layout (read back by the same lane of
-// the BPTT kernel as two 16-B loads); BPTT writes [dr | du] and dc row-major for the GEMMs.
+// Saved for the backward: h_{t-1} and r*h_{t-1} row-major and the step's token per row (the
+// weight-gradient kernel's A operands; x_t is re-gathered from the bf16 embedding copy by token), and
+// (r, u, c, h_{t-1}) in the accumulator layout (read back by the same lane of the BPTT kernel as two
+// 16-B loads); BPTT writes [dr | du], dc and dx row-major.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -86,14 +87,15 @@ __device__ __forceinline__ int tok(const int* sIds, const int* sLen, int row, in
 
 // ---- forward -----------------------------------------------------------------------------------
 // grid (ceil(R / M), 2 directions), NT threads.  Wg: [(K+1) x 2H], Wc: [(K+1) x H] fp32 (last row
-// bias).  XH [dir][t][R][K], RH [dir][t][R][H] (u16), GF [dir][t][NB][NW][64][16] (u16), out [R x ldo]
-// fp32 final states (fw in [0, H), bw in [H, 2H)).
+// bias).  HS, RH [dir][t][R][H] (u16: h_{t-1}, r*h_{t-1}), TOK [dir][t][R] (int: the token of x_t),
+// GA [dir][t][NB][NW][64][8] (u16: r, u), GC [dir][t][NB][NW][64][8] (u16: c, h_{t-1}), out [R x ldo] fp32 final
+// states (fw in [0, H), bw in [H, 2H)).
 template <int E, int H, int MT>
 __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
     GruDimsB d, const int* __restrict__ ids, const int* __restrict__ lens, const u16* __restrict__ emb16,
     const float* __restrict__ wg_fw, const float* __restrict__ wc_fw, const float* __restrict__ wg_bw,
-    const float* __restrict__ wc_bw, u16* __restrict__ XH, u16* __restrict__ RH, u16* __restrict__ GF,
-    float* __restrict__ out, int ldo) {
+    const float* __restrict__ wc_bw, u16* __restrict__ HS, u16* __restrict__ RH, int* __restrict__ TOK,
+    u16* __restrict__ GA, u16* __restrict__ GC, float* __restrict__ out, int ldo) {
   using G = Geo<E, H, MT>;
   constexpr int K = G::K, KC = G::KC, XC = G::XC, HC = G::HC, NW = G::NW, NT = G::NT, M = G::M;
   constexpr int LDA = G::LDA, LDR = G::LDR;
@@ -193,18 +195,13 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
         sR[(16 * m + 4 * lg + i) * LDR + gcol] = f2bf(rv * hs[m][i]);
       }
     __syncthreads();
-    // save [x_t | h_{t-1}] and r*h_{t-1}
+    // save x_t's token, h_{t-1} and r*h_{t-1}
     const size_t rowbase = (size_t)dir * plane + (size_t)t * R + r0;
-    auto save_x = [&](int q) {
-      const int row = q / EC8, c8 = q - row * EC8;
-      if (row < nrow) *reinterpret_cast<uint4*>(XH + (rowbase + row) * K + c8 * 8) = *xdst(q);
-    };
-    if (has0) save_x(q0);
-    if (has1) save_x(q1);
+    for (int row = tid; row < nrow; row += NT) TOK[rowbase + row] = tok(sIds, sLen, row, t, T, dir);
     for (int i = tid; i < M * HC8; i += NT) {
       const int row = i / HC8, c8 = i - row * HC8;
       if (row < nrow) {
-        *reinterpret_cast<uint4*>(XH + (rowbase + row) * K + E + c8 * 8) =
+        *reinterpret_cast<uint4*>(HS + (rowbase + row) * H + c8 * 8) =
             *reinterpret_cast<const uint4*>(&sA[row * LDA + E + c8 * 8]);
         *reinterpret_cast<uint4*>(RH + (rowbase + row) * H + c8 * 8) =
             *reinterpret_cast<const uint4*>(&sR[row * LDR + c8 * 8]);
@@ -237,11 +234,12 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
       }
       const int blk = r0 / 16 + m;
       if (blk < NB) {
-        uint4* g = reinterpret_cast<uint4*>(
-            GF + ((((size_t)dir * T + t) * NB + blk) * NW + w) * 1024 + (size_t)lane * 16);
-        g[0] = make_uint4(pk2(ar[m][0], ar[m][1]), pk2(ar[m][2], ar[m][3]), pk2(au[m][0], au[m][1]),
-                          pk2(au[m][2], au[m][3]));
-        g[1] = make_uint4(pk2(cv[0], cv[1]), pk2(cv[2], cv[3]), pk2(h0[0], h0[1]), pk2(h0[2], h0[3]));
+        const size_t f = (((size_t)dir * T + t) * NB + blk) * NW + w;
+        *reinterpret_cast<uint4*>(GA + f * 512 + (size_t)lane * 8) =
+            make_uint4(pk2(ar[m][0], ar[m][1]), pk2(ar[m][2], ar[m][3]), pk2(au[m][0], au[m][1]),
+                       pk2(au[m][2], au[m][3]));
+        *reinterpret_cast<uint4*>(GC + f * 512 + (size_t)lane * 8) =
+            make_uint4(pk2(cv[0], cv[1]), pk2(cv[2], cv[3]), pk2(h0[0], h0[1]), pk2(h0[2], h0[3]));
       }
     }
     __syncthreads();
@@ -264,8 +262,8 @@ template <int E, int H, int MT>
 __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
     GruDimsB d, const int* __restrict__ ids, const int* __restrict__ lens, const float* __restrict__ wg_fw,
     const float* __restrict__ wc_fw, const float* __restrict__ wg_bw, const float* __restrict__ wc_bw,
-    const float* __restrict__ dout, int ldo, const u16* __restrict__ GF, u16* __restrict__ DG,
-    u16* __restrict__ DC, u16* __restrict__ DX) {
+    const float* __restrict__ dout, int ldo, const u16* __restrict__ GA, const u16* __restrict__ GC,
+    u16* __restrict__ DG, u16* __restrict__ DC, u16* __restrict__ DX) {
   using G = Geo<E, H, MT>;
   constexpr int HC = G::HC, NW = G::NW, NT = G::NT, M = G::M, LDR = G::LDR, LDG = G::LDG;
   constexpr int HC8 = H / 8, EC8 = E / 8, LDX = E + 8;
@@ -311,24 +309,27 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
     }
   const size_t plane = (size_t)T * R;
   const int NB = (R + 15) / 16;
-  auto gf_ptr = [&](int t, int m) {
-    const int blk = min(r0 / 16 + m, NB - 1);
-    return reinterpret_cast<const uint4*>(GF + ((((size_t)dir * T + t) * NB + blk) * NW + w) * 1024 +
-                                          (size_t)lane * 16);
-  };
-  // (r, u, c, h_{t-1}) of the current step, packed; the previous step's are loaded into the same
+  // (r, u), (c) and h_{t-1} of the current step, packed; the previous step's are loaded into the same
   // registers once P1's epilogue has used them, and stay in flight across P2 and the stores
-  uint4 gf[MT][2];
+  struct Cache {
+    uint4 ru, ch;  // (r, u), (c, h_{t-1})
+  };
+  auto load_cache = [&](int t, int m) {
+    const int blk = min(r0 / 16 + m, NB - 1);
+    const size_t f = (((size_t)dir * T + t) * NB + blk) * NW + w;
+    Cache x;
+    x.ru = *reinterpret_cast<const uint4*>(GA + f * 512 + (size_t)lane * 8);
+    x.ch = *reinterpret_cast<const uint4*>(GC + f * 512 + (size_t)lane * 8);
+    return x;
+  };
+  Cache gf[MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    gf[m][0] = gf_ptr(T - 1, m)[0];
-    gf[m][1] = gf_ptr(T - 1, m)[1];
-  }
+  for (int m = 0; m < MT; ++m) gf[m] = load_cache(T - 1, m);
   for (int t = T - 1; t >= 0; --t) {
     float dhp[MT][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const uint4 g0 = gf[m][0], g1 = gf[m][1];
+      const uint4 g0 = gf[m].ru, g1 = gf[m].ch;
       const float uv[4] = {lo16(g0.z), hi16(g0.z), lo16(g0.w), hi16(g0.w)};
       const float cv[4] = {lo16(g1.x), hi16(g1.x), lo16(g1.y), hi16(g1.y)};
       const float h0[4] = {lo16(g1.z), hi16(g1.z), lo16(g1.w), hi16(g1.w)};
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
       }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const uint4 g0 = gf[m][0], g1 = gf[m][1];
+      const uint4 g0 = gf[m].ru, g1 = gf[m].ch;
       const float rv[4] = {lo16(g0.x), hi16(g0.x), lo16(g0.y), hi16(g0.y)};
       const float h0[4] = {lo16(g1.z), hi16(g1.z), lo16(g1.w), hi16(g1.w)};
 #pragma unroll
@@ -374,10 +375,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
     }
     if (t > 0) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        gf[m][0] = gf_ptr(t - 1, m)[0];
-        gf[m][1] = gf_ptr(t - 1, m)[1];
-      }
+      for (int m = 0; m < MT; ++m) gf[m] = load_cache(t - 1, m);
     }
     __syncthreads();
     // save dc and [dr | du] for the weight-gradient GEMMs
@@ -544,12 +542,16 @@ __global__ __launch_bounds__(256) void k_emb_grad(const int* __restrict__ start,
 // the LDS read, conflict-free.  The bias gradient (column sums of dP) rides on the B fragments of the
 // first row of waves.  Partials go to a [split][tile][129][128] slab; a second launch sums the splits
 // in fixed order into the arena.
+// A's columns [0, ex) are x: gathered as rows tok[k] of the bf16 embedding copy emb ([V x ex]);
+// columns [ex, ...) are column (c - ex) of the row-major A (ex = 0: a plain A).
 struct DwTile {
   const u16* A;
   const u16* B;
   float* dest;  // row drow0 of the destination block, ld ldd
   float* bias;  // null: no bias row from this tile
-  int lda, ldb, m0, mlen, n0, nlen, ldd, drow0;
+  const int* tok;
+  const u16* emb;
+  int lda, ldb, m0, mlen, n0, nlen, ldd, drow0, ex;
 };
 constexpr int kDwMaxTiles = 16, kDwSlabRows = 129;
 struct DwArgs {
@@ -595,19 +597,33 @@ __global__ __launch_bounds__(512) void k_rnn_dw(DwArgs a) {
   };
   const int ch = tid & 15, row0 = tid >> 4;  // chunk e = tid + 512 s: row row0 + 32 s, chunk ch
   const bool okm = ch * 8 < T.mlen, okn = ch * 8 < T.nlen;
-  const u16* pa = T.A + T.m0 + ch * 8;
+  const int col = T.m0 + ch * 8;
+  const bool xcol = col < T.ex;  // this thread's A chunk is a gathered embedding chunk
+  const u16* pa = xcol ? T.emb + col : T.A + (col - T.ex);
   const u16* pb = T.B + T.n0 + ch * 8;
-  const int lda = T.lda, ldb = T.ldb;
+  const int lda = xcol ? T.ex : T.lda, ldb = T.ldb;
+  const int* tok = T.tok;
   auto ld1 = [&](const u16* base, int ld, bool okc, int k) {
     // a value select, not a select of addresses (that would put the zero vector on scratch)
     uint4 v = make_uint4(0, 0, 0, 0);
     if (okc && k < kend) v = *reinterpret_cast<const uint4*>(base + (size_t)k * ld);
     return v;
   };
+  // gathered chunks: the tokens of a load's rows were fetched by the previous load (loads are issued
+  // in increasing k0, 64 rows apart), so the embedding gather waits on no dependent load
+  auto tok1 = [&](int k) { return (xcol && okm && k < kend) ? tok[k] : 0; };
+  int tk0 = tok1(kbeg + row0), tk1 = tok1(kbeg + row0 + 32);
+  auto lda1 = [&](int k, int tk) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (okm && k < kend) v = *reinterpret_cast<const uint4*>(pa + (size_t)(xcol ? tk : k) * lda);
+    return v;
+  };
   auto load = [&](int k0) {
     Set r;
-    r.a0 = ld1(pa, lda, okm, k0 + row0);
-    r.a1 = ld1(pa, lda, okm, k0 + row0 + 32);
+    r.a0 = lda1(k0 + row0, tk0);
+    r.a1 = lda1(k0 + row0 + 32, tk1);
+    tk0 = tok1(k0 + 64 + row0);
+    tk1 = tok1(k0 + 64 + row0 + 32);
     r.b0 = ld1(pb, ldb, okn, k0 + row0);
     r.b1 = ld1(pb, ldb, okn, k0 + row0 + 32);
     return r;
@@ -718,8 +734,8 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 constexpr int kDwMaxSplits = 64;
 
 struct WsB {
-  u16 *XH, *RH, *GF, *DG, *DC, *DX, *emb16;
-  int *cnt, *start, *cursor, *pos;
+  u16 *HS, *RH, *GA, *GC, *DG, *DC, *DX, *emb16;
+  int *TOK, *cnt, *start, *cursor, *pos;
   float* slab;
   size_t bytes;
 };
@@ -727,7 +743,7 @@ struct WsB {
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
-  const size_t TR = (size_t)T * R, K = (size_t)E + H, NB = (R + 15) / 16;
+  const size_t TR = (size_t)T * R, NB = (R + 15) / 16;
   WsB w{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -735,9 +751,11 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
     off += al256(bytes);
     return p;
   };
-  w.XH = (u16*)take(2 * TR * K * 2);
+  w.HS = (u16*)take(2 * TR * H * 2);
   w.RH = (u16*)take(2 * TR * H * 2);
-  w.GF = (u16*)take(2 * (size_t)T * NB * 16 * H * 4 * 2);
+  w.TOK = (int*)take(2 * TR * 4);
+  w.GA = (u16*)take(2 * (size_t)T * NB * 16 * H * 2 * 2);
+  w.GC = (u16*)take(2 * (size_t)T * NB * 16 * H * 2 * 2);
   w.DG = (u16*)take(2 * TR * 2 * H * 2);
   w.DC = (u16*)take(2 * TR * H * 2);
   w.DX = (u16*)take(2 * TR * E * 2);
@@ -776,7 +794,7 @@ void launch_fwd_t(const GruDimsB& d, const int* ids, const int* lens, const u16*
   constexpr int M = 16 * MT;
   const size_t dyn = sizeof(int) * (size_t)M * (1 + d.T);
   hipLaunchKernelGGL((k_gru_fwd_mfma<E, H, MT>), dim3((d.R + M - 1) / M, 2), dim3(Geo<E, H, MT>::NT), dyn, s, d,
-                     ids, lens, emb16, w[0], w[1], w[2], w[3], ws.XH, ws.RH, ws.GF, y, ldy);
+                     ids, lens, emb16, w[0], w[1], w[2], w[3], ws.HS, ws.RH, ws.TOK, ws.GA, ws.GC, y, ldy);
 }
 
 template <int E, int H, int MT>
@@ -785,7 +803,7 @@ void launch_bwd_t(const GruDimsB& d, const int* ids, const int* lens, const floa
   constexpr int M = 16 * MT;
   const size_t dyn = sizeof(int) * (size_t)M;
   hipLaunchKernelGGL((k_gru_bwd_mfma<E, H, MT>), dim3((d.R + M - 1) / M, 2), dim3(Geo<E, H, MT>::NT), dyn, s, d,
-                     ids, lens, w[0], w[1], w[2], w[3], dy, lddy, ws.GF, ws.DG, ws.DC, ws.DX);
+                     ids, lens, w[0], w[1], w[2], w[3], dy, lddy, ws.GA, ws.GC, ws.DG, ws.DC, ws.DX);
 }
 
 template <int E, int H>
@@ -814,8 +832,15 @@ void dispatch_bwd(int mt, const GruDimsB& d, const int* ids, const int* lens, co
 }  // namespace dssm
 
 // ---- C-ABI -------------------------------------------------------------------------------------
+#include <vector>
 namespace {
 int rerr_b(int code, const char* m) { return dssm::report_error(code, m); }
+// HIP-event probes around the BPTT launch (bench.py's roofline: the launch's duration measured on
+// the stream it runs on, inside the timed region)
+struct BpttProbe {
+  std::vector<hipEvent_t> ev;  // pairs
+  int used = 0;
+} g_probe;
 }
 
 extern "C" {
@@ -867,12 +892,15 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cursor, L.pos);
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
+  const bool probe = g_probe.used < (int)g_probe.ev.size() / 2;
+  if (probe) hipEventRecord(g_probe.ev[2 * g_probe.used], s);
   if (E == 128)
     dssm::dispatch_bwd<128, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else if (E == 64)
     dssm::dispatch_bwd<64, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else
     dssm::dispatch_bwd<32, 32>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
+  if (probe) hipEventRecord(g_probe.ev[2 * g_probe.used++ + 1], s);
   const dim3 gemb((V + 3) / 4);
   if (E == 128)
     hipLaunchKernelGGL(dssm::k_emb_grad<128>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
@@ -888,29 +916,33 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   int n = 0;
   for (int dir = 0; dir < 2; ++dir) {
     const size_t half = (size_t)TR * dir;
-    const u16* XH = L.XH + half * K;
+    const u16* HS = L.HS + half * H;
+    const int* TK = L.TOK + half;
     const u16* RH = L.RH + half * H;
     const u16* DG = L.DG + half * 2 * H;
     const u16* DC = L.DC + half * H;
     float* gg = gw[2 * dir];
     float* gc = gw[2 * dir + 1];
+    // [x | h] = embedding rows by token (columns < E) and the h_{t-1} cache
     for (int mb = 0; mb < K; mb += 128)
       for (int nb = 0; nb < 2 * H; nb += 128)
-        A.t[n++] = dssm::DwTile{XH, DG, gg, mb == 0 ? gg + (size_t)K * 2 * H : nullptr, K, 2 * H, mb,
-                                std::min(128, K - mb), nb, std::min(128, 2 * H - nb), 2 * H, mb};
+        A.t[n++] = dssm::DwTile{HS, DG, gg, mb == 0 ? gg + (size_t)K * 2 * H : nullptr, TK, L.emb16, H, 2 * H, mb,
+                                std::min(128, K - mb), nb, std::min(128, 2 * H - nb), 2 * H, mb, E};
     for (int mb = 0; mb < E; mb += 128)
       for (int nb = 0; nb < H; nb += 128)
-        A.t[n++] = dssm::DwTile{XH, DC, gc, mb == 0 ? gc + (size_t)K * H : nullptr, K, H, mb,
-                                std::min(128, E - mb), nb, std::min(128, H - nb), H, mb};
+        A.t[n++] = dssm::DwTile{HS, DC, gc, mb == 0 ? gc + (size_t)K * H : nullptr, TK, L.emb16, H, H, mb,
+                                std::min(128, E - mb), nb, std::min(128, H - nb), H, mb, E};
     for (int mb = 0; mb < H; mb += 128)
       for (int nb = 0; nb < H; nb += 128)
-        A.t[n++] = dssm::DwTile{RH, DC, gc, nullptr, H, H, mb, std::min(128, H - mb), nb, std::min(128, H - nb), H,
-                                E + mb};
+        A.t[n++] = dssm::DwTile{RH, DC, gc, nullptr, nullptr, nullptr, H, H, mb, std::min(128, H - mb), nb,
+                                std::min(128, H - nb), H, E + mb, 0};
   }
   A.ntiles = n;
   A.TR = TR;
-  A.splits = std::max(1, std::min({dssm::kDwMaxSplits, (384 + n - 1) / n, (TR + 63) / 64}));
-  A.splits += A.splits & 1;  // even: with 12 tiles (E = H = 128) the XCD grouping needs splits * ntiles % 8 == 0
+  // about two workgroups per CU (64 KB of LDS each) in one round
+  A.splits = std::max(1, std::min({dssm::kDwMaxSplits, 512 / n, (TR + 63) / 64}));
+  A.splits -= A.splits & 1;  // even: with 12 tiles (E = H = 128) the XCD grouping needs splits * ntiles % 8 == 0
+  A.splits = std::max(A.splits, 1);
   A.splits = std::min(A.splits, dssm::kDwMaxSplits);
   A.kps = ((TR + A.splits - 1) / A.splits + 63) / 64 * 64;
   A.slab = L.slab;
@@ -918,6 +950,33 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   hipLaunchKernelGGL(dssm::k_rnn_dw_reduce, dim3((n * dssm::kDwSlabRows * 32 + 255) / 256), dim3(256), 0, s, A);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_rnn_bf16_probe(int n_max) {
+  for (hipEvent_t e : g_probe.ev) hipEventDestroy(e);
+  g_probe.ev.clear();
+  g_probe.used = 0;
+  for (int i = 0; i < 2 * n_max; ++i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return rerr_b(DSSM_E_HIP, "rnn_bf16_probe: hipEventCreate");
+    g_probe.ev.push_back(e);
+  }
+  return DSSM_OK;
+}
+
+int dssm_rnn_bf16_probe_read(double* avg_ms, int* count) {
+  if (!avg_ms || !count) return rerr_b(DSSM_E_INVALID, "rnn_bf16_probe_read: bad argument");
+  double tot = 0.0;
+  for (int i = 0; i < g_probe.used; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(g_probe.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_probe.ev[2 * i], g_probe.ev[2 * i + 1]) != hipSuccess)
+      return rerr_b(DSSM_E_HIP, "rnn_bf16_probe_read: event");
+    tot += ms;
+  }
+  *count = g_probe.used;
+  *avg_ms = g_probe.used ? tot / g_probe.used : 0.0;
+  return DSSM_OK;
 }
 
 }  // extern "C"

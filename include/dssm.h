@@ -399,6 +399,10 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream);
+/* Timing probes (benchmarks): record HIP events around the next n_max BPTT launches (n_max = 0:
+ * off); read the average launch duration of the recorded ones (synchronizes on their events). */
+int dssm_rnn_bf16_probe(int n_max);
+int dssm_rnn_bf16_probe_read(double* avg_ms, int* count);
 /* AdamOptimizer (dssm_rnn.py:218) over a flat arena: [0, n_sparse) the embedding table (TF1's
  * deduplicated IndexedSlices update, m*b1 + (1-b1) g form), the rest dense ApplyAdam; state =
  * device {beta1_power, beta2_power}, advanced after the update. */
