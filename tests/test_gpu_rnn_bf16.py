@@ -3,8 +3,9 @@ recurrences with register-resident weights) against the bf16-emulating NumPy ora
 (oracle/rnn_oracle.py emulate="bf16": the same operand rounding points, float64 elsewhere) on the same
 seeded inputs, including BASELINE.json config 4's full size with ragged lengths and dropout.
 
-Bars (written here, bf16 mode): final states |err| <= 2e-3 (states lie in (-1, 1)); summed loss
-relative <= 1e-3; every gradient ||err|| <= 1e-2 ||g|| with cosine >= 0.9999.  Rounding-boundary flips
+Bars (written here, bf16 mode): final states |err| <= 1e-4 (states lie in (-1, 1); measured <= 1.2e-5);
+summed loss relative <= 2e-4; every gradient ||err|| <= 5e-3 ||g|| (measured <= 1.9e-3) with cosine
+>= 0.99999.  Rounding-boundary flips
 of the bf16 state operand between the fp32 kernel and the float64 oracle are what the bars absorb;
 the un-emulated float64 oracle is reported beside them (the bf16 mode's own error)."""
 import numpy as np
@@ -44,8 +45,8 @@ def _check(cfg, p, m, ids, lens, keep):
     err_y = np.abs(y0 - ref["y0"]).max()
     plain = R.forward(cfg, p64, ids, lens, mask, keep)
     print(f"y0 max|err| vs emulated {err_y:.2e}, vs float64 {np.abs(y0 - plain['y0']).max():.2e}")
-    assert err_y <= 2e-3, err_y
-    assert abs(m.loss() - ref["loss"]) <= 1e-3 * abs(ref["loss"]), (m.loss(), ref["loss"])
+    assert err_y <= 1e-4, err_y
+    assert abs(m.loss() - ref["loss"]) <= 2e-4 * abs(ref["loss"]), (m.loss(), ref["loss"])
     m.backward()
     torch.cuda.synchronize()
     g = R.backward(cfg, p64, ids, lens, ref)
@@ -58,7 +59,7 @@ def _check(cfg, p, m, ids, lens, keep):
         gp = g_plain[k].ravel()
         rel_plain = np.linalg.norm(a - gp) / max(np.linalg.norm(gp), 1e-30)
         print(f"{k}: rel {rel:.2e} cos {cos:.6f} (vs float64: rel {rel_plain:.2e})")
-        assert rel <= 1e-2 and cos >= 0.9999, (k, rel, cos)
+        assert rel <= 5e-3 and cos >= 0.99999, (k, rel, cos)
 
 
 @pytest.mark.parametrize("case", CASES)
