@@ -8,8 +8,8 @@
 // layer's BN+ReLU on the fly when given the pre-BN activations (and writes the embeddings out),
 // computes norms/dots by wave reductions, softmax/loss redundantly in every lane, and writes the
 // gradient of every embedding row it owns (each doc row belongs to exactly one query: no
-// atomics).  The per-block loss/accuracy partials are summed by the last block to finish
-// (agent-scope ticket), in fixed order.
+// atomics).  The per-block loss/accuracy partials are summed in fixed order by a later launch
+// (the backward's first, or k_loss_finalize).
 #include <algorithm>
 
 #include "bnfuse.h"
@@ -43,14 +43,11 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
-    float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
-    float* __restrict__ dy, int defer, BnSide fs, CscScatter scat) {
+    float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat) {
   constexpr int NT = 64 * NW;
   __shared__ float s_part[2][NW];
-  __shared__ int s_flag;
   __shared__ float s_co[FSC ? 2 * 4 * kCosMaxN : 1];     // [tower][mu|rstd|inv|shift][c]
   __shared__ float s_bs[FSC ? NW * 4 * EPL * 64 : 1];    // [wave][sq1|sq2|sd1|sd2][c]
-  (void)s_flag;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int j = blockIdx.x * NW + wv;
   const int K = neg + 1;
@@ -269,9 +266,6 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     part[2 * blockIdx.x] = a;
     part[2 * blockIdx.x + 1] = b;
   }
-  if (defer) return;  // a later launch sums the partials (the backward's first, or k_loss_finalize)
-  if (!last_block_arrival(ticket, nrow_blocks, &s_flag)) return;
-  loss_finalize(part, nrow_blocks, bs, loss_out);
 }
 
 __global__ __launch_bounds__(64) void k_loss_finalize(const float* __restrict__ part, int nblk,
@@ -289,10 +283,9 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               hipStream_t s, const BnSide* fused, bool defer_finalize,
                               const CscScatter* scatter) {
   if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
-  // ws: [partials 2*blocks floats][ticket] (ticket zero on first use; re-armed by the kernel)
+  // ws: the per-workgroup loss / accuracy partials (2 floats each)
   const int nw = cosine_waves(n, fused != nullptr);
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
-  unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * cdiv(bs, 4) + 32);  // past either layout
   CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
   if (sc.nblocks) sc.nblocks = std::max(1, sc.nblocks * 4 / nw);  // sized in 4-wave workgroups
   if (scatter && !fused) return hipErrorInvalidValue;  // the role rides on the fused kernel only
@@ -300,15 +293,17 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
+  // The loss partials are always summed by a later launch: a second tiny launch here when the
+  // caller does not defer.  (The in-kernel alternative, an agent-scope release + ticket in EVERY
+  // workgroup so that the last one can sum, writes back the XCD's L2 once per workgroup -- the dy
+  // rows the kernel has just written.)
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
-                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,   \
-                       defer_finalize ? 1 : 0, fs, sc);                      \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc);        \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, ticket, loss_out, dy,        \
-                       defer_finalize ? 1 : 0, fs, sc)
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -320,6 +315,8 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #undef DSSM_COS
 #undef DSSM_COS2
 #undef DSSM_COS3
+  if (!defer_finalize)
+    hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
   return hipGetLastError();
 }
 

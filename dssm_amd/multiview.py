@@ -5,7 +5,9 @@ The reference's archive/multi_view_dssm_v3.py:107-241: a user tower and three it
 positives and in-batch rotations of them as the NEG negatives (Make_Negative_Item), x20 cosine,
 softmax, summed loss, Adam on the user tower and the active view.
 
-Composed from libdssm.so's functional C-ABI (include/dssm.h): dssm_spmm_csr_fwd /
+The user tower and the active item view run concurrently (the item tower on a second stream that
+forks from and joins the caller's stream): each tower's launches are latency-bound, so the two
+chains overlap on the CUs.  Composed from libdssm.so's functional C-ABI (include/dssm.h): dssm_spmm_csr_fwd /
 dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2), dssm_relu / dssm_relu_bwd,
 dssm_rows_gather / dssm_rows_scatter_add (the rotation as an index map and its backward),
 dssm_cosine_softmax_loss (shared with the BoW path), dssm_adam_step.  fp32; torch tensors are
@@ -72,9 +74,11 @@ class MultiViewDSSM:
         self.dysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)
         self.merged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         self.dmerged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
-        self.dz2 = torch.zeros((BS, self.ld2), dtype=f32, device=dev)
-        self.da1 = torch.zeros((BS, self.ld1), dtype=f32, device=dev)
-        self.dz1 = torch.zeros((BS, self.ld1), dtype=f32, device=dev)
+        # per-tower backward scratch: the two towers run concurrently (user tower on the caller's
+        # stream, the item tower on self.aux)
+        self.dz2 = {k: torch.zeros((BS, self.ld2), dtype=f32, device=dev) for k in ("u", "i")}
+        self.da1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
+        self.dz1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         K = self.neg + 1
         self.cos_raw = torch.zeros(K * BS, dtype=f32, device=dev)
         self.cos_sim = torch.zeros(BS * K, dtype=f32, device=dev)
@@ -83,7 +87,8 @@ class MultiViewDSSM:
         self.loss_buf = torch.zeros(2, dtype=f32, device=dev)
         self.cos_ws = torch.zeros(2 * (-(-BS // 4)) + 64, dtype=f32, device=dev)
         slab = max(self.lib.dssm_dense_bwd_slab_floats(BS, self.l1, self.l2, _lib.DSSM_F32), 1)
-        self.slab = torch.zeros(int(slab), dtype=f32, device=dev)
+        self.slab = {k: torch.zeros(int(slab), dtype=f32, device=dev) for k in ("u", "i")}
+        self.aux = torch.cuda.Stream(device=dev)
         # one CSC-transpose workspace per tower (zero on first use, kept zero by the calls)
         self.spmm_ws = {t: torch.zeros(int(self.lib.dssm_spmm_bwd_ws_bytes(BS, d, self.max_nnz)),
                                        dtype=torch.uint8, device=dev) for t, d in zip(TOWERS, self.dims)}
@@ -171,11 +176,20 @@ class MultiViewDSSM:
                                       self.l1, self.l2, ptr(w2[self.l1]), ptr(y_rows), self.ld2, s), "dense_fwd")
         check(self.lib.dssm_relu(ptr(y_rows), self.ld2, self.bs, self.l2, ptr(y_rows), self.ld2, s), "relu")
 
+    def _fork(self, stream):
+        """The item tower's stream joins the caller's stream here."""
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.aux.wait_stream(main)
+        return main
+
     def forward(self, stream=None):
-        s = stream_ptr(stream)
+        main = self._fork(stream)
+        s, sa = stream_ptr(main), stream_ptr(self.aux)
         BS = self.bs
+        # the towers are independent until the cosine: the item tower runs beside the user tower
         self._tower_fwd("u", "user", self.ysrc[:BS], s)
-        self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], s)
+        self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], sa)
+        main.wait_stream(self.aux)
         R = BS * (2 + self.neg)
         check(self.lib.dssm_rows_gather(ptr(self.ysrc), self.ld2, ptr(self.map), R, self.l2, ptr(self.merged),
                                         self.ld2, s), "gather")
@@ -188,28 +202,33 @@ class MultiViewDSSM:
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w2 = self._block(self.params, f"{tower}_2")
+        dz2, da1, dz1 = self.dz2[key], self.da1[key], self.dz1[key]
         check(self.lib.dssm_relu_bwd(ptr(y_rows), self.ld2, ptr(dy_rows), self.ld2, self.bs, self.l2,
-                                     ptr(self.dz2), self.ld2, s), "relu_bwd")
+                                     ptr(dz2), self.ld2, s), "relu_bwd")
         check(self.lib.dssm_dense_bwd(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
-                                      self.l1, self.l2, ptr(self.dz2), self.ld2, ptr(self.da1), self.ld1,
-                                      ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab), s), "dense_bwd")
-        check(self.lib.dssm_relu_bwd(ptr(self.a1[key]), self.ld1, ptr(self.da1), self.ld1, self.bs, self.l1,
-                                     ptr(self.dz1), self.ld1, s), "relu_bwd")
-        check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(self.dz1),
+                                      self.l1, self.l2, ptr(dz2), self.ld2, ptr(da1), self.ld1,
+                                      ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
+              "dense_bwd")
+        check(self.lib.dssm_relu_bwd(ptr(self.a1[key]), self.ld1, ptr(da1), self.ld1, self.bs, self.l1,
+                                     ptr(dz1), self.ld1, s), "relu_bwd")
+        check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(dz1),
                                            _lib.DSSM_F32, self.ld1, self.l1,
                                            ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),
                                            s), "spmm_bwd")
 
     def backward(self, stream=None):
-        s = stream_ptr(stream)
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s = stream_ptr(main)
         BS, R = self.bs, self.bs * (2 + self.neg)
         # the cosine kernel's d(mean loss)/dy x BS = d(summed loss)/dy (multi_view_dssm_v3.py:234)
         check(self.lib.dssm_rnn_dropout(ptr(self.dmerged), ptr(self.dmerged), R, self.l2, self.ld2, 1.0, 0, 0,
                                         float(BS), s), "scale")
         check(self.lib.dssm_rows_scatter_add(ptr(self.dmerged), self.ld2, ptr(self.map), R, self.l2,
                                              ptr(self.dysrc), self.ld2, 2 * BS, s), "scatter")
+        self._fork(main)
         self._tower_bwd("u", "user", self.ysrc[:BS], self.dysrc[:BS], s)
-        self._tower_bwd("i", f"view{self.view}", self.ysrc[BS:], self.dysrc[BS:], s)
+        self._tower_bwd("i", f"view{self.view}", self.ysrc[BS:], self.dysrc[BS:], stream_ptr(self.aux))
+        main.wait_stream(self.aux)
 
     def apply_adam(self, stream=None):
         s = stream_ptr(stream)
