@@ -232,6 +232,7 @@ struct dssm_plan {
     hipGraphExec_t exec = nullptr;
     hipEvent_t ev[DSSM_PROBE_COUNT][2] = {};
     bool probes = false;
+    unsigned probe_mask = ~0u;  // while capturing: which probe ids record event nodes
   };
   std::vector<GraphSlot*> graphs;
   GraphSlot* capturing = nullptr;
@@ -259,7 +260,7 @@ struct dssm_plan {
 
   void probe_begin(int id, hipStream_t s) {
     if (capturing) {
-      if (capturing->probes) graph_event_node(s, capturing->ev[id][0]);
+      if (capturing->probes && (capturing->probe_mask >> id & 1)) graph_event_node(s, capturing->ev[id][0]);
       return;
     }
     Probe& p = probe[id];
@@ -267,7 +268,7 @@ struct dssm_plan {
   }
   void probe_end(int id, hipStream_t s) {
     if (capturing) {
-      if (capturing->probes) graph_event_node(s, capturing->ev[id][1]);
+      if (capturing->probes && (capturing->probe_mask >> id & 1)) graph_event_node(s, capturing->ev[id][1]);
       return;
     }
     Probe& p = probe[id];
@@ -1152,8 +1153,11 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   int rc = DSSM_OK;
   P->rank_done_for = nullptr;
   for (int i = 0; i < nsteps && !rc; ++i) {
-    // probes (event-record nodes) ride in the first step only
-    g->probes = with_probes != 0 && i == 0;
+    // probes (event-record nodes): the transpose / SpMM / dW1 ones in the first step (the only one
+    // with its own rank launch when the rank pass rides in Adam), the Adam one in the last step (the
+    // only Adam launch hosting no rank pass: it times the optimizer alone)
+    g->probes = with_probes != 0 && (i == 0 || i == nsteps - 1);
+    g->probe_mask = (i == 0 ? ~(1u << DSSM_PROBE_ADAM) : 0u) | (i == nsteps - 1 ? 1u << DSSM_PROBE_ADAM : 0u);
     P->indptr = indptrs[i];
     P->indices = indices[i];
     P->values = values[i];
@@ -1168,6 +1172,7 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   P->host_rank_indptr = P->host_rank_indices = nullptr;
   P->rank_done_for = nullptr;
   g->probes = with_probes != 0;
+  g->probe_mask = ~0u;
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();
   hipGraph_t graph = nullptr;
