@@ -100,7 +100,9 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
   constexpr int K = G::K, KC = G::KC, XC = G::XC, HC = G::HC, NW = G::NW, NT = G::NT, M = G::M;
   constexpr int LDA = G::LDA, LDR = G::LDR;
   constexpr int EC8 = E / 8, HC8 = H / 8, NXQ = M * EC8, XPT = (NXQ + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) u16 sA[M * LDA];  // [x_t | h_{t-1}]
+  // [x_t | h_{t-1}], double-buffered by step parity: step t reads sA[t & 1] and fills sA[(t+1) & 1],
+  // so the step needs two barriers (after the gates' r*h, after the state update), not three
+  __shared__ __attribute__((aligned(16))) u16 sA[2][M * LDA];
   __shared__ __attribute__((aligned(16))) u16 sR[M * LDR];  // r * h_{t-1}
   extern __shared__ int sDyn[];                              // lens [M], ids [M][T]
   int* sLen = sDyn;
@@ -144,24 +146,26 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
     const int row = q / EC8, c8 = q - row * EC8;
     return reinterpret_cast<const uint4*>(emb16 + (size_t)tok(sIds, sLen, row, t, T, dir) * E + c8 * 8);
   };
-  auto xdst = [&](int q) {
+  auto xdst = [&](u16* A, int q) {
     const int row = q / EC8, c8 = q - row * EC8;
-    return reinterpret_cast<uint4*>(&sA[row * LDA + c8 * 8]);
+    return reinterpret_cast<uint4*>(&A[row * LDA + c8 * 8]);
   };
   const int q0 = tid, q1 = tid + NT;
   const bool has0 = q0 < NXQ, has1 = XPT > 1 && q1 < NXQ;
   uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;
-  if (has0) *xdst(q0) = *xsrc(q0, 0);
-  if (has1) *xdst(q1) = *xsrc(q1, 0);
+  if (has0) *xdst(sA[0], q0) = *xsrc(q0, 0);
+  if (has1) *xdst(sA[0], q1) = *xsrc(q1, 0);
   for (int i = tid; i < M * HC8; i += NT) {
     const int row = i / HC8, c8 = i - row * HC8;
-    *reinterpret_cast<uint4*>(&sA[row * LDA + E + c8 * 8]) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(&sA[0][row * LDA + E + c8 * 8]) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
 
   const size_t plane = (size_t)T * R;
   const int NB = (R + 15) / 16;
   for (int t = 0; t < T; ++t) {
+    u16* A = sA[t & 1];
+    u16* An = sA[(t + 1) & 1];
     // next step's input rows in flight during this step
     if (t + 1 < T) {
       if (has0) x0 = *xsrc(q0, t + 1);
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
     for (int c = 0; c < KC; ++c) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const bf16x8 a = lds_frag(&sA[(16 * m + lc) * LDA + 32 * c + 8 * lg]);
+        const bf16x8 a = lds_frag(&A[(16 * m + lc) * LDA + 32 * c + 8 * lg]);
         ar[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bR[c], ar[m], 0, 0, 0);
         au[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bU[c], au[m], 0, 0, 0);
         if (c < XC) ac[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bC[c], ac[m], 0, 0, 0);
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
       const int row = i / HC8, c8 = i - row * HC8;
       if (row < nrow) {
         *reinterpret_cast<uint4*>(HS + (rowbase + row) * H + c8 * 8) =
-            *reinterpret_cast<const uint4*>(&sA[row * LDA + E + c8 * 8]);
+            *reinterpret_cast<const uint4*>(&A[row * LDA + E + c8 * 8]);
         *reinterpret_cast<uint4*>(RH + (rowbase + row) * H + c8 * 8) =
             *reinterpret_cast<const uint4*>(&sR[row * LDR + c8 * 8]);
       }
@@ -215,11 +219,11 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
         const bf16x8 a = lds_frag(&sR[(16 * m + lc) * LDR + 32 * c + 8 * lg]);
         ac[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bC[XC + c], ac[m], 0, 0, 0);
       }
-    __syncthreads();
-    // x_{t+1} into the x slots, free since the barrier (its loads had the whole step to land)
+    // x_{t+1} and h_t into the other buffer (last read by step t-1, before the previous barrier);
+    // the x loads had the whole step to land
     if (t + 1 < T) {
-      if (has0) *xdst(q0) = x0;
-      if (has1) *xdst(q1) = x1;
+      if (has0) *xdst(An, q0) = x0;
+      if (has1) *xdst(An, q1) = x1;
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_fwd_mfma(
         h0[i] = hs[m][i];
         const float uv = au[m][i];
         if (t < len_r[m][i]) hs[m][i] = uv * h0[i] + (1.0f - uv) * cv[i];
-        sA[(16 * m + 4 * lg + i) * LDA + E + gcol] = f2bf(hs[m][i]);
+        An[(16 * m + 4 * lg + i) * LDA + E + gcol] = f2bf(hs[m][i]);
       }
       const int blk = r0 / 16 + m;
       if (blk < NB) {
@@ -267,9 +271,11 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
   using G = Geo<E, H, MT>;
   constexpr int HC = G::HC, NW = G::NW, NT = G::NT, M = G::M, LDR = G::LDR, LDG = G::LDG;
   constexpr int HC8 = H / 8, EC8 = E / 8, LDX = E + 8;
-  __shared__ __attribute__((aligned(16))) u16 sC[M * LDR];  // dc
-  __shared__ __attribute__((aligned(16))) u16 sG[M * LDG];  // [dr | du]
-  __shared__ __attribute__((aligned(16))) u16 sX[M * LDX];  // dx
+  // dc, [dr | du] and dx tiles, double-buffered by step parity: two barriers per step (the next
+  // step writes the other buffers), dx rows of step t stored after the first barrier of step t-1
+  __shared__ __attribute__((aligned(16))) u16 sCb[2][M * LDR];
+  __shared__ __attribute__((aligned(16))) u16 sGb[2][M * LDG];
+  __shared__ __attribute__((aligned(16))) u16 sXb[2][M * LDX];
   extern __shared__ int sDyn[];
   int* sLen = sDyn;
 
@@ -325,7 +331,20 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
   Cache gf[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) gf[m] = load_cache(T - 1, m);
+  auto store_dx = [&](int t) {
+    const u16* sX = sXb[t & 1];
+    const size_t rb = (size_t)dir * plane + (size_t)t * R + r0;
+    for (int i = tid; i < M * EC8; i += NT) {
+      const int row = i / EC8, c8 = i - row * EC8;
+      if (row < nrow)
+        *reinterpret_cast<uint4*>(DX + (rb + row) * E + c8 * 8) =
+            *reinterpret_cast<const uint4*>(&sX[row * LDX + c8 * 8]);
+    }
+  };
   for (int t = T - 1; t >= 0; --t) {
+    u16* sC = sCb[t & 1];
+    u16* sG = sGb[t & 1];
+    u16* sX = sXb[t & 1];
     float dhp[MT][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -346,6 +365,7 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
       }
     }
     __syncthreads();
+    if (t + 1 < T) store_dx(t + 1);  // written before this barrier, rewritten after the next one
     // P1: dc · Wc^T -> state part (the reset gate's and the state's gradient through r*h) and x part
     f32x4 ah[MT], ax[MT];
 #pragma unroll
@@ -414,15 +434,9 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
 #pragma unroll
         for (int i = 0; i < 4; ++i) sX[(16 * m + 4 * lg + i) * LDX + kx] = f2bf(ax[m][i]);
     }
-    __syncthreads();
-    // dx rows out (the next step's sX writes come after two more barriers)
-    for (int i = tid; i < M * EC8; i += NT) {
-      const int row = i / EC8, c8 = i - row * EC8;
-      if (row < nrow)
-        *reinterpret_cast<uint4*>(DX + (rowbase + row) * E + c8 * 8) =
-            *reinterpret_cast<const uint4*>(&sX[row * LDX + c8 * 8]);
-    }
   }
+  __syncthreads();
+  store_dx(0);
 }
 
 // ---- embedding gradient: dx summed per token -------------------------------------------------
@@ -893,14 +907,14 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   const bool probe = g_probe.used < (int)g_probe.ev.size() / 2;
-  if (probe) hipEventRecord(g_probe.ev[2 * g_probe.used], s);
+  if (probe) (void)hipEventRecord(g_probe.ev[2 * g_probe.used], s);
   if (E == 128)
     dssm::dispatch_bwd<128, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else if (E == 64)
     dssm::dispatch_bwd<64, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else
     dssm::dispatch_bwd<32, 32>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
-  if (probe) hipEventRecord(g_probe.ev[2 * g_probe.used++ + 1], s);
+  if (probe) (void)hipEventRecord(g_probe.ev[2 * g_probe.used++ + 1], s);
   const dim3 gemb((V + 3) / 4);
   if (E == 128)
     hipLaunchKernelGGL(dssm::k_emb_grad<128>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
@@ -953,7 +967,7 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
 }
 
 int dssm_rnn_bf16_probe(int n_max) {
-  for (hipEvent_t e : g_probe.ev) hipEventDestroy(e);
+  for (hipEvent_t e : g_probe.ev) (void)hipEventDestroy(e);
   g_probe.ev.clear();
   g_probe.used = 0;
   for (int i = 0; i < 2 * n_max; ++i) {
