@@ -239,15 +239,23 @@ def bench_multiview(args):
     fp32, synthetic Zipf trigram rows; the active view cycles 1, 2, 3 over the staged batches.
     One step = forward + backward + Adam (user tower + active view).  Not the headline."""
     import torch
+    import torch.distributed as dist
     from dssm_amd.data import ZipfColumns, synth_rows
-    from dssm_amd.multiview import MultiViewDSSM
+    from dssm_amd.multiview import MultiViewDataParallel, MultiViewDSSM
     B, Dv, L1, L2 = 4096, 30000, 300, 128
-    dev = torch.device("cuda", 0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count()) if args.backend == "gloo" else local  # gloo: rehearsal
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:  # config 5 on N GPUs: BS users per rank, gradient all-reduce (weak scaling)
+        dist.init_process_group(args.backend, device_id=dev if args.backend == "nccl" else None)
     m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev)
     m.init_params(0)
+    dp = MultiViewDataParallel(m, comm=args.comm) if world > 1 else None
     cols = ZipfColumns(Dv)
-    rng = np.random.Generator(np.random.PCG64(7))
+    rng = np.random.Generator(np.random.PCG64(7 + rank))
     feeds, host_feeds = [], []
     for b in range(3):
         u = synth_rows(rng, cols, B, 32.0)
@@ -274,7 +282,9 @@ def bench_multiview(args):
     with torch.cuda.stream(stream):
         for i in range(max(args.warmup, 3)):
             eager(i)
-            m.apply_adam()
+            if dp is not None:
+                dp.exchange()
+            m.apply_adam(grad_scale=1.0 / world)
         torch.cuda.synchronize()
         if args.graph:
             for i in range(3):
@@ -284,7 +294,7 @@ def bench_multiview(args):
                     m.forward()
                     m.backward()
                 with torch.cuda.graph(g2, stream=stream):
-                    m.apply_adam()
+                    m.apply_adam(grad_scale=1.0 / world)
                 fb_graphs.append(g1)
                 adam_graphs.append(g2)
 
@@ -293,41 +303,53 @@ def bench_multiview(args):
             fb_graphs[i % 3].replay()
         else:
             eager(i)
+        if dp is not None:
+            dp.exchange()  # between the graphs: RCCL all-reduce of the trained towers' gradients
         if probe:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         if args.graph:
             adam_graphs[i % 3].replay()
         else:
-            m.apply_adam()
+            m.apply_adam(grad_scale=1.0 / world)
         if probe:
             ev[1].record()
             probes.append(ev)
     torch.cuda.set_stream(stream)
     torch.cuda.synchronize()
+    if dp is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, probe=True)
     torch.cuda.synchronize()
+    if dp is not None:
+        dist.barrier()
     el = time.perf_counter() - t0
+    if dp is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
     adam_ms = float(np.mean([a.elapsed_time(b) for a, b in probes])) / 2  # per launch
     tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
     # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower
     adam_bytes = int(28 * tower_params)
     achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
     out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
-           "value": round(B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": 1,
+           "value": round(world * B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic",
            "config": {"workload": "multi_view_dssm_v3: user + 3 views (30k sparse -> 300 -> 128), in-batch "
-                                  "rotated negatives, BS=4096, NEG=4, fwd+bwd+Adam", "global_batch": B,
-                      "neg": NEG, "parallelism": "dp1", "launch": "hipgraph" if args.graph else "eager"},
+                                  "rotated negatives, BS=4096 per GPU, NEG=4, fwd+bwd+Adam", "global_batch": B * world,
+                      "neg": NEG, "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph else "eager",
+                      "dp_exchange": dp.comm if dp is not None else None},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
                         "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5)},
            "final_loss": round(m.loss(), 3)}
-    if args.cpu_baseline:
+    if args.cpu_baseline and rank == 0 and world == 1:
         try:  # the NumPy float32 restatement (oracle/, test infrastructure) on the host
             from oracle import cpu_port
             from oracle.multiview_oracle import MvConfig
@@ -338,7 +360,11 @@ def bench_multiview(args):
             out["cpu_baseline"]["cpu_model"] = cpu_model()
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dp is not None:
+        dp.close()
+        dist.destroy_process_group()
 
 
 def fwd_only(model, staged, args, stream):

@@ -230,13 +230,16 @@ class MultiViewDSSM:
         self._tower_bwd("i", f"view{self.view}", self.ysrc[BS:], self.dysrc[BS:], stream_ptr(self.aux))
         main.wait_stream(self.aux)
 
-    def apply_adam(self, stream=None):
+    def trained_ranges(self):
+        """Arena ranges the step updates: the user tower and the active view."""
+        return [self.layout[t] for t in ("user", f"view{self.view}")]
+
+    def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
-        for k, t in enumerate(("user", f"view{self.view}")):
-            b, e = self.layout[t]
+        for k, (b, e) in enumerate(self.trained_ranges()):
             check(self.lib.dssm_adam_step(ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]),
                                           ptr(self.adam_v[b:e]), e - b, self.lr, 0.9, 0.999, 1e-8,
-                                          ptr(self.adam_state), 1.0, k == 1, s), "adam")
+                                          ptr(self.adam_state), grad_scale, k == 1, s), "adam")
         self.global_step += 1
 
     def train_step(self, stream=None):
@@ -246,3 +249,63 @@ class MultiViewDSSM:
 
     def loss(self) -> float:
         return float(self.loss_buf[0].item()) * self.bs
+
+
+class MultiViewDataParallel:
+    """BASELINE config 5 across GPUs: one process per GPU, each rank trains on its own batch of BS
+    users (weak scaling) with the same active view; after the backward the gradients of the user
+    tower and the active view are summed over the ranks (fp32 all-reduce on libdssm.so's RCCL
+    communicator, or torch.distributed: dssm_amd.dist transports, self-tested at start-up) and every
+    rank applies the same Adam step with grad_scale = 1/world, the mean of the per-rank gradients,
+    so the ranks stay bit-identical.  (The reference's loss is a sum over its BS users; averaging
+    over ranks keeps the per-step update of the single-GPU step.)"""
+
+    def __init__(self, model: MultiViewDSSM, comm: str = "auto"):
+        import torch.distributed as dist
+        from .dist import LibTransport, TorchTransport
+        self.model = model
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.tx = None
+        if self.world == 1:
+            return
+        cands = []
+        if comm in ("auto", "rccl") and dist.get_backend() == "nccl":
+            cands.append(LibTransport)
+        cands.append(TorchTransport)
+        for cls in cands:
+            try:
+                tx = cls(self.rank, self.world)
+                z = torch.full((64,), float(self.rank + 1), device=model.device)
+                tx.all_reduce(z)
+                ok = bool(torch.equal(z, torch.full_like(z, float(self.world * (self.world + 1) // 2))))
+            except Exception:
+                tx, ok = None, False
+            flag = torch.tensor([1.0 if ok else 0.0], device=model.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if flag.item() == 1.0:
+                self.tx = tx
+                return
+            if tx is not None:
+                tx.destroy()
+        raise RuntimeError("no working all-reduce transport")
+
+    @property
+    def comm(self) -> str:
+        return self.tx.name if self.tx is not None else "none"
+
+    def exchange(self):
+        if self.world > 1:
+            for b, e in self.model.trained_ranges():
+                self.tx.all_reduce(self.model.grads[b:e])
+
+    def train_step(self):
+        self.model.forward()
+        self.model.backward()
+        self.exchange()
+        self.model.apply_adam(grad_scale=1.0 / self.world)
+
+    def close(self):
+        if self.tx is not None:
+            self.tx.destroy()
+            self.tx = None
