@@ -133,6 +133,18 @@ def pmc_traffic(workload: dict):
     return {}, None
 
 
+def model_profile(kind: str, model: str, kernel: str):
+    """The newest committed profiles/r*_<kind>_*.json collected on a non-headline row (its
+    "_workload" names the bench.py --model) and its record of one kernel: HBM bytes per launch
+    ("traffic": tools/pmc_traffic.py) or matrix-core use ("mfma": tools/mfma_util.py)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_*.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("_workload", {}).get("model") == model and kernel in d:
+            return d[kernel], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def mfma_summary(dtype: str):
     """Matrix-core use of the MFMA kernels (TFLOP/s vs the dense peak, busy share of the SIMD
     cycles) from the newest committed profiles/r*_mfma*.json of this dtype (tools/mfma_util.py:
@@ -140,7 +152,7 @@ def mfma_summary(dtype: str):
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma*.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("_workload", {}).get("dtype") != dtype:
+        if d.get("_workload", {}).get("dtype") != dtype or "model" in d.get("_workload", {}):
             continue
         ks = {k: {x: v[x] for x in ("tflops", "peak_tflops", "frac_of_peak", "mfma_busy", "flops_per_launch")
                   if x in v} for k, v in d.items() if k != "_workload"}
@@ -221,6 +233,13 @@ def bench_rnn(args):
                            "unit": "GB/s", "frac": round(bptt / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "traffic": None, "kernel": "k_gru_bwd_mfma", "bytes_per_launch": bptt,
                            "avg_ms": round(ms, 5), "launches": cnt.value}
+        t, src = model_profile("traffic", "rnn", "k_gru_bwd_mfma<128, 128, 3>")
+        if t is not None:
+            out["roofline"].update(traffic=t["hbm_bytes"], traffic_source=src)
+        mf = {k: model_profile("mfma", "rnn", k) for k in ("k_gru_fwd_mfma<128, 128, 3>",
+                                                          "k_gru_bwd_mfma<128, 128, 3>", "k_rnn_dw")}
+        out["mfma"] = {k.split("<")[0]: {x: v[x] for x in ("tflops", "frac_of_peak", "mfma_busy") if x in v}
+                       for k, (v, _) in mf.items() if v is not None} or None
     if args.cpu_baseline:
         try:  # the C/OpenMP fp32 restatement (oracle/cpu_c/rnn_cpu.c, test infrastructure) on the host
             from oracle import cpu_c
@@ -349,6 +368,9 @@ def bench_multiview(args):
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
                         "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5)},
            "final_loss": round(m.loss(), 3)}
+    t, src = model_profile("traffic", "multiview", "k_rnn_adam")
+    if t is not None:
+        out["roofline"].update(traffic=t["hbm_bytes"], traffic_source=src)
     if args.cpu_baseline and rank == 0 and world == 1:
         try:  # the NumPy float32 restatement (oracle/, test infrastructure) on the host
             from oracle import cpu_port

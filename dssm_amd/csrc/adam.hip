@@ -31,6 +31,12 @@
 #ifndef DSSM_RANK_POS
 #define DSSM_RANK_POS 1
 #endif
+#ifndef DSSM_ADAM_PRE_IDX
+#define DSSM_ADAM_PRE_IDX 1
+#endif
+#ifndef DSSM_ADAM_GATHER_U  // rows in flight in the W1-row role's gather batches
+#define DSSM_ADAM_GATHER_U 4
+#endif
 #ifndef DSSM_ADAM_LATE_PMV
 #define DSSM_ADAM_LATE_PMV 0
 #endif
@@ -103,8 +109,25 @@ __device__ __forceinline__ float4 slab_grad4(const SlabList& sl, int64_t i, cons
 
 // One wave updates row c of [W1; b1] (CSC column c): light rows' gradient is gathered inline
 // from the CSC transpose and dZ1, heavy rows' gradient (k_dw1_heavy) is read and cleared.
+// A light row's CSC entries (index, value), lane j holding entry j: loaded one row ahead of the
+// row's gather (DSSM_ADAM_PRE_IDX), so the row's chain starts at the dZ1 loads.
+struct RowEntries {
+  int i;
+  float v;
+};
+__device__ __forceinline__ RowEntries row_entries(const AdamStep& a, int s, int e) {
+  RowEntries r{0, 0.f};
+  const int lane = lane_id();
+  if (e - s <= kLightEntries && lane < e - s) {
+    r.i = a.csc_row[s + lane];
+    r.v = a.csc_val[s + lane];
+  }
+  return r;
+}
+
 template <typename TZ>
-__device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha) {
+__device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha,
+                                       const RowEntries* pre = nullptr) {
   const int lane = lane_id();
   const int n = a.n;
   const bool heavy = e - s > kLightEntries;
@@ -130,7 +153,8 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
         if (nvalid > 4) *reinterpret_cast<float4*>(a.g + o + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     } else {
-      gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
+      if (pre) gather_batch<TZ, 2, DSSM_ADAM_GATHER_U>(pre->i, pre->v, e - s, dZ, a.lddz, cc, nvalid, G);
+      else gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, G);
     }
 #if DSSM_ADAM_LATE_PMV
     if (nvalid > 0 && !a.gout) {  // after the gather: fewer live registers, higher occupancy
@@ -322,12 +346,36 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
     // the next row's column range is loaded while this row is processed (one dependent load
     // fewer on each row's chain)
     const int stride = a.w1_blocks * 4;
-    int c = b * 4 + (threadIdx.x >> 6);
+    int c = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar row state
     int s = 0, e = 0;
     if (c <= a.D) {
       s = a.col_ptr[c];
       e = a.col_ptr[c + 1];
     }
+#if DSSM_ADAM_PRE_IDX
+    // two rows ahead: the column range; one row ahead: the light row's CSC entries
+    int sn = 0, en = 0;
+    if (c + stride <= a.D) {
+      sn = a.col_ptr[c + stride];
+      en = a.col_ptr[c + stride + 1];
+    }
+    RowEntries ent = row_entries(a, s, e);
+    for (; c <= a.D; c += stride) {
+      const int c2 = c + 2 * stride;
+      int s2 = 0, e2 = 0;
+      if (c2 <= a.D) {
+        s2 = a.col_ptr[c2];
+        e2 = a.col_ptr[c2 + 1];
+      }
+      const RowEntries next = row_entries(a, sn, en);
+      w1_row<TZ>(a, c, s, e, alpha, &ent);
+      s = sn;
+      e = en;
+      sn = s2;
+      en = e2;
+      ent = next;
+    }
+#else
     for (; c <= a.D; c += stride) {
       const int cn = c + stride;
       int sn = 0, en = 0;
@@ -339,6 +387,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       s = sn;
       e = en;
     }
+#endif
   } else {
     const int bi = DSSM_ADAM_ORDER == 0 ? b0 - nh - nw : b0 - nh;
     if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero

@@ -148,7 +148,23 @@ __device__ __forceinline__ void loss_reduce(const float* __restrict__ part, int 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (wv == 0) {
     float a = 0.f, b = 0.f;
-    for (int i = lane; i < nblk; i += 64) {
+    int i = lane;
+    // eight partials' loads in flight per lane before the (in-order) adds: the launch is one
+    // wave, so its time is the load latency chain
+    for (; i + 7 * 64 < nblk; i += 8 * 64) {
+      float pa[8], pb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        pa[k] = part[2 * (i + 64 * k)];
+        pb[k] = part[2 * (i + 64 * k) + 1];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a += pa[k];
+        b += pb[k];
+      }
+    }
+    for (; i < nblk; i += 64) {
       a += part[2 * i];
       b += part[2 * i + 1];
     }

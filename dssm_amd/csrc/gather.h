@@ -38,27 +38,17 @@ template <> struct RawRow8<float> {
   }
 };
 
-// Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc.  All 64 lanes must be
-// active (the index broadcast reads every lane's register; v_readlane ignores EXEC); lanes with
-// nvalid <= 0 only skip their loads.
+// One batch of cnt <= 64 entries whose (index, value) pairs lane j already holds in my_i, my_v.
+// All 64 lanes must be active (the index broadcast reads every lane's register; v_readlane
+// ignores EXEC); lanes with nvalid <= 0 only skip their loads.
 // REM: rows in flight in the remainder (< U) loop: 2 for the short CSC columns of dW1 (most light
 // columns have a handful of entries: their chain is the remainder), 1 for the SpMM's ~32-entry rows
 // (measured: the wider remainder costs it occupancy).
-template <typename T, int REM = 1>
-__device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
-                                                  const float* __restrict__ val, int s, int e,
-                                                  const T* __restrict__ M, int ldm, int c,
-                                                  int nvalid, float (&acc)[8]) {
-  constexpr int U = sizeof(T) == 2 ? 8 : 4;  // rows in flight per lane
-  const int lane = lane_id();
-  for (int base = s; base < e; base += 64) {
-    const int cnt = min(64, e - base);
-    int my_i = 0;
-    float my_v = 0.f;
-    if (lane < cnt) {
-      my_i = idx[base + lane];
-      my_v = val[base + lane];
-    }
+// U: rows in flight per lane in the main loop.
+template <typename T, int REM = 1, int U = sizeof(T) == 2 ? 8 : 4>
+__device__ __forceinline__ void gather_batch(int my_i, float my_v, int cnt, const T* __restrict__ M,
+                                             int ldm, int c, int nvalid, float (&acc)[8]) {
+  {
     int j = 0;
     for (; j + U <= cnt; j += U) {
       RawRow8<T> x[U];
@@ -92,6 +82,25 @@ __device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
         x.fma(v, acc);
       }
     }
+  }
+}
+
+// Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc (gather_batch per 64).
+template <typename T, int REM = 1>
+__device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
+                                                  const float* __restrict__ val, int s, int e,
+                                                  const T* __restrict__ M, int ldm, int c,
+                                                  int nvalid, float (&acc)[8]) {
+  const int lane = lane_id();
+  for (int base = s; base < e; base += 64) {
+    const int cnt = min(64, e - base);
+    int my_i = 0;
+    float my_v = 0.f;
+    if (lane < cnt) {
+      my_i = idx[base + lane];
+      my_v = val[base + lane];
+    }
+    gather_batch<T, REM>(my_i, my_v, cnt, M, ldm, c, nvalid, acc);
   }
 }
 

@@ -45,7 +45,7 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
                                           const TW* __restrict__ W, int ldw, int n,
                                           const float* __restrict__ bias, float* __restrict__ Z,
                                           int ldz, int b) {
-  const int row = b * 4 + (threadIdx.x >> 6);
+  const int row = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
@@ -513,7 +513,7 @@ __device__ __forceinline__ void scatter_rows(const int* __restrict__ indptr,
                                              int* __restrict__ csc_row, float* __restrict__ csc_val,
                                              int* __restrict__ csc_col, int b, int nb) {
   for (int c = b * 256 + threadIdx.x; c < D; c += nb * 256) cnt[c] = 0;
-  const int row = b * 4 + (threadIdx.x >> 6);
+  const int row = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
                                                          int* __restrict__ csc_row,
                                                          float* __restrict__ csc_val,
                                                          int* __restrict__ csc_col) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
   const int lane = lane_id();
   const int s = indptr[row], e = indptr[row + 1];
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void k_dw1_light(const int* __restrict__ col_p
                                                    const float* __restrict__ csc_val, int D,
                                                    const TZ* __restrict__ dZ, int lddz, int n,
                                                    float* __restrict__ G, int mode) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int c = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (c > D) return;
   const int lane = lane_id();
   const int s = col_ptr[c], e = col_ptr[c + 1];

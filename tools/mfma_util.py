@@ -12,7 +12,7 @@ GRBM_GUI_ACTIVE (GPU-active cycles of the dispatch).  Per kernel:
                     launch's SIMD-cycles the matrix cores were busy (rocprofv3's MfmaUtil divides by
                     GRBM_GUI_ACTIVE, which on gfx950 sums the 8 XCDs and includes the counter
                     pass's serialisation, so it is not used)
-usage: python tools/mfma_util.py <counter dir> <kernel_stats.csv> <out.json> [bf16|fp32]
+usage: python tools/mfma_util.py <counter dir> <kernel_stats.csv> <out.json> [bf16|fp32 [model]]
 """
 import csv
 import glob
@@ -32,7 +32,7 @@ def short(name):
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
 
-def main(root, stats_csv, out, dtype="bf16"):
+def main(root, stats_csv, out, dtype="bf16", model=None):
     mops_name = "SQ_INSTS_VALU_MFMA_MOPS_" + ("BF16" if dtype == "bf16" else "F32")
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
@@ -42,6 +42,8 @@ def main(root, stats_csv, out, dtype="bf16"):
     for r in csv.DictReader(open(stats_csv)):
         dur[short(r["Name"])] = float(r["AverageNs"])
     res = {"_workload": {"dtype": dtype}}
+    if model:  # a non-headline row (bench.py --model)
+        res["_workload"]["model"] = model
     for k, c in vals.items():
         mops = c.get(mops_name, [])
         if not mops or sum(mops) == 0:
