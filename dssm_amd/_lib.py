@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("DSSM_LIB_PATH", LIB_PATH)
 DSSM_ABI_VERSION = 2
 DSSM_MAX_LAYERS = 8
 DSSM_F32, DSSM_BF16 = 0, 1
+DSSM_ACT_NONE, DSSM_ACT_RELU = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
  BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
 BUF_A, BUF_DA = 11, 12
@@ -94,6 +95,10 @@ _SIGS = {
                                     C.c_int, _P]),
     "dssm_dense_fwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
                                  _P, C.c_int, _P]),
+    "dssm_spmm_csr_fwd_act": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,
+                                        C.c_int, C.c_int, _P]),
+    "dssm_dense_fwd_act": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
+                                     _P, C.c_int, C.c_int, _P]),
     "dssm_bn_ws_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "dssm_bn_relu_fwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float,
                                    C.c_float, C.c_int, C.c_int, _P, C.c_int, _P, _P, _P, _P]),
@@ -140,6 +145,8 @@ _SIGS = {
     "dssm_dense_bwd_slab_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "dssm_dense_bwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
                                  _P, C.c_int, _P, _P, _P]),
+    "dssm_dense_bwd_masked": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
+                                        C.c_int, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_bn_relu_bwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float, C.c_int, _P,
                                    C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,

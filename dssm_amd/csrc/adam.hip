@@ -37,6 +37,9 @@
 #ifndef DSSM_ADAM_GATHER_U  // rows in flight in the W1-row role's gather batches
 #define DSSM_ADAM_GATHER_U 4
 #endif
+#ifndef DSSM_ADAM_HEAVY_U  // rows in flight in the heavy items' gather batches
+#define DSSM_ADAM_HEAVY_U 8
+#endif
 #ifndef DSSM_ADAM_LATE_PMV
 #define DSSM_ADAM_LATE_PMV 0
 #endif
@@ -239,11 +242,18 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
 // re-arms the ticket.  Deterministic mode (heavy_slab): the items store their rows into the slab
 // instead (agent-scope stores, drained before the ticket) and the last arrival sums them in item
 // order with agent-scope loads, so the fp32 sum no longer depends on arrival order.
+// LDS of one heavy-item workgroup: the 4 waves' partial rows, the summed row, the last-arrival flag
+struct HeavyLds {
+  float part[4][512];
+  float grow[512];
+  int last;
+};
+
 template <typename TZ>
-__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb) {
-  __shared__ float part[4][512];
-  __shared__ float grow[512];
-  __shared__ int s_last;
+__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb, HeavyLds& L) {
+  float(&part)[4][512] = L.part;
+  float(&grow)[512] = L.grow;
+  int& s_last = L.last;
   const int wv = threadIdx.x >> 6, lane = lane_id();
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
   const int nitems = *a.heavy_n;
@@ -258,7 +268,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       const int cc = c0 + lane * 8;
       const int nvalid = a.n - cc;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (s < e) gather_accumulate<TZ, 2>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, acc);
+      if (s < e) gather_accumulate<TZ, 2, DSSM_ADAM_HEAVY_U>(a.csc_row, a.csc_val, s, e, dZ, a.lddz, cc, nvalid, acc);
 #pragma unroll
       for (int i = 0; i < 8; ++i) part[wv][lane * 8 + i] = acc[i];
       __syncthreads();
@@ -321,7 +331,12 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
   // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
   // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
-  __shared__ unsigned s_rank[kRankHash];  // the hosted rank role's hash table
+  // one LDS block shared by the two roles that use LDS (the hosted rank role's hash table, the
+  // heavy items' rows): 16.4 instead of 26.6 KB per workgroup, so LDS no longer caps the launch at
+  // 6 workgroups per CU
+  constexpr size_t kLdsBytes = sizeof(unsigned) * kRankHash > sizeof(HeavyLds) ? sizeof(unsigned) * kRankHash
+                                                                                : sizeof(HeavyLds);
+  __shared__ __align__(16) unsigned char s_lds[kLdsBytes];
   const int nr = a.rank.nblocks;
   // where the hosted rank workgroups sit in dispatch order
 #if DSSM_RANK_POS == 0
@@ -338,9 +353,9 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   // role order after the heavy items: W1 rows then streaming (0), or streaming first (1)
   const bool w1_role = DSSM_ADAM_ORDER == 0 ? (b0 >= nh && b0 < nh + nw) : (b0 >= nh + nd);
   if (is_rank) {
-    csc_rank_role(a.rank, bx - rs, s_rank);
+    csc_rank_role(a.rank, bx - rs, reinterpret_cast<unsigned*>(s_lds));
   } else if (b0 < nh) {
-    heavy_items<TZ>(a, alpha, b0);
+    heavy_items<TZ>(a, alpha, b0, *reinterpret_cast<HeavyLds*>(s_lds));
   } else if (w1_role) {
     const int b = DSSM_ADAM_ORDER == 0 ? b0 - nh : b0 - nh - nd;
     // the next row's column range is loaded while this row is processed (one dependent load

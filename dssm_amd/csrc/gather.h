@@ -86,7 +86,7 @@ __device__ __forceinline__ void gather_batch(int my_i, float my_v, int cnt, cons
 }
 
 // Accumulate sum_j val_j * M[idx_j, c..c+8) for entries [s, e) into acc (gather_batch per 64).
-template <typename T, int REM = 1>
+template <typename T, int REM = 1, int U = sizeof(T) == 2 ? 8 : 4>
 __device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
                                                   const float* __restrict__ val, int s, int e,
                                                   const T* __restrict__ M, int ldm, int c,
@@ -100,7 +100,7 @@ __device__ __forceinline__ void gather_accumulate(const int* __restrict__ idx,
       my_i = idx[base + lane];
       my_v = val[base + lane];
     }
-    gather_batch<T, REM>(my_i, my_v, cnt, M, ldm, c, nvalid, acc);
+    gather_batch<T, REM, U>(my_i, my_v, cnt, M, ldm, c, nvalid, acc);
   }
 }
 

@@ -89,7 +89,10 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
                                               int lda, const T* __restrict__ B, int ldb,
                                               float* __restrict__ C, int ldc,
                                               const float* __restrict__ bias, int ones_row,
-                                              int k_per_split) {
+                                              int k_per_split, int relu,
+                                              const float* __restrict__ mask, int ldmask) {
+  // relu (FWD): the layer's ReLU in the epilogue; mask (DA): dA zeroed where mask <= 0 (the ReLU
+  // backward through the layer's input activation, ReluGrad)
   constexpr bool TA = (MODE == GEMM_DW);
   constexpr bool TB = (MODE == GEMM_DA);
   constexpr int BK = Cfg<T>::BK;
@@ -224,9 +227,12 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
         const float v = acc[i][j][r];
         if (m >= M) continue;
         if constexpr (MODE == GEMM_FWD) {
-          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? v + bias[n] : 0.f;
+          float x = v + (n < N ? bias[n] : 0.f);
+          if (relu) x = fmaxf(x, 0.f);
+          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? x : 0.f;
         } else if constexpr (MODE == GEMM_DA) {
-          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? v : 0.f;
+          const bool keep = n < N && (!mask || mask[(size_t)m * ldmask + n] > 0.f);
+          if (n < ldc) out[(size_t)m * ldc + n] = keep ? v : 0.f;
         } else {
           if (n < N) out[(size_t)m * ldc + n] = v;
         }
@@ -968,7 +974,7 @@ int dw_splits(int M, int N, int K, int BK) {
 template <typename T>
 hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, const T* B, int ldb,
                     float* C, int ldc, const float* bias, bool ones_row, float* slab,
-                    hipStream_t s, int* deferred_splits) {
+                    hipStream_t s, int* deferred_splits, int relu, const float* mask, int ldmask) {
   dim3 block(256);
   constexpr int BK = Cfg<T>::BK;
   if (mode == GEMM_DW) {
@@ -983,10 +989,10 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
                                     ones_row ? 1 : 0, kps});
       else
         hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb,
-                           target, ldc, bias, ones_row ? 1 : 0, kps);
+                           target, ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0);
     } else {
       hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
-                         ldc, bias, ones_row ? 1 : 0, kps);
+                         ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0);
     }
     if (deferred_splits) *deferred_splits = splits > 1 ? splits : 0;
     if (splits > 1 && !deferred_splits) {
@@ -999,10 +1005,10 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
     const int kps = cdiv(K, BK) * BK;
     if (mode == GEMM_FWD)
       hipLaunchKernelGGL((k_gemm<T, GEMM_FWD>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C,
-                         ldc, bias, 0, kps);
+                         ldc, bias, 0, kps, relu, nullptr, 0);
     else
       hipLaunchKernelGGL((k_gemm<T, GEMM_DA>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C,
-                         ldc, bias, 0, kps);
+                         ldc, bias, 0, kps, 0, mask, ldmask);
   }
   return hipGetLastError();
 }
@@ -1145,12 +1151,13 @@ size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
 
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
-                       float* slab, hipStream_t s, int* deferred_splits) {
+                       float* slab, hipStream_t s, int* deferred_splits, int relu,
+                       const float* mask, int ldmask) {
   if (bf16)
     return launch_t<u16>(mode, M, N, K, (const u16*)A, lda, (const u16*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s, deferred_splits);
+                         ones_row, slab, s, deferred_splits, relu, mask, ldmask);
   return launch_t<float>(mode, M, N, K, (const float*)A, lda, (const float*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s, deferred_splits);
+                         ones_row, slab, s, deferred_splits, relu, mask, ldmask);
 }
 
 }  // namespace dssm

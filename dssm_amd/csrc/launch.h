@@ -31,7 +31,7 @@ int eval_coef_blocks(const EvalCoef& e);
 // eval_coef_blocks(*ec) extra workgroups write the eval BN coefficients.
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s, const EvalCoef* ec = nullptr);
+                           int ldz, hipStream_t s, const EvalCoef* ec = nullptr, bool relu = false);
 // CSR -> CSC transpose of X with a virtual all-ones column D appended (its dW row = db1).
 // scratch: csc_scratch_ints() ints, zero on first use (kept zero between calls);
 // col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
@@ -80,15 +80,17 @@ enum GemmMode { GEMM_FWD = 0, GEMM_DA = 1, GEMM_DW = 2 };
 constexpr int kMaxDwSplits = 32;
 // Workspace floats the DW split-K partial slabs need for an (M x N) output over K rows.
 size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16);
-// FWD: C[M x ldc] = A[M x K] * B[K x N] + bias (cols >= N written 0)
-// DA : C[M x ldc] = A[M x K] * B^T where B is [N x K] (ld ldb)
+// FWD: C[M x ldc] = A[M x K] * B[K x N] + bias (cols >= N written 0), then ReLU when relu != 0
+// DA : C[M x ldc] = A[M x K] * B^T where B is [N x K] (ld ldb); with mask [M x ldmask], elements
+//      where mask <= 0 are written 0 (ReluGrad through the layer input)
 // DW : C[M x N] = A^T * B, A is [K x M] (ld lda) with a virtual ones row at m == M-1 when
 //      ones_row != 0; B is [K x N]; split-K over the K (rows) dimension into `slab`
 //      (gemm_dw_slab_floats) then a fixed-order reduce into C (ldc must equal N).
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
                        const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
                        float* slab, hipStream_t s,
-                       int* deferred_splits = nullptr);
+                       int* deferred_splits = nullptr, int relu = 0, const float* mask = nullptr,
+                       int ldmask = 0);
 
 // bf16 "NT" GEMM: C[M x ldc] = A . B + bias, B given k-contiguous as BT [N x ldb]
 // (BT[n][k] = B[k][n]).  bn_a: A = relu(Z*inv + shift) from fp32 Z [M x lda] with BN coefficients

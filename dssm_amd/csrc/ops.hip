@@ -3,7 +3,8 @@
 // towers) instead of the fused training-step plan.
 //   dssm_spmm_csr_bwd_w : [dW1; db1] = [X | 1]^T dZ1 (TF's SparseTensorDenseMatMul gradient,
 //                         dense), via the plan's CSC transpose + dW1 kernels
-//   dssm_dense_bwd      : dA = dZ W^T and [dW; db] = [A | 1]^T dZ (tf.matmul + bias autodiff)
+//   dssm_dense_bwd      : dA = dZ W^T and [dW; db] = [A | 1]^T dZ (tf.matmul + bias autodiff);
+//                         _masked: dA zeroed where the layer input (a ReLU output) is <= 0
 //   dssm_bn_relu_bwd    : batch-statistics batch_normalization + ReLU backward (new_dssm.py:62-88)
 #include <hip/hip_runtime.h>
 
@@ -224,11 +225,12 @@ size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype) {
   return dssm::gemm_dw_slab_floats(K + 1, N, M, dtype == DSSM_BF16);
 }
 
-int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
-                   const void* dZ, int lddz, float* dA, int ldda, float* dWb, float* slab, void* stream) {
+int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                          const void* dZ, int lddz, float* dA, int ldda, const float* mask, int ldmask,
+                          float* dWb, float* slab, void* stream) {
   if (!A || !W || !dZ || !dWb || M <= 0 || K <= 0 || N <= 0 || lda < K || ldw < N || lddz < N ||
       (dA && ldda < K) || (dtype != DSSM_F32 && dtype != DSSM_BF16) || (lda % 4) || (ldw % 4) ||
-      (lddz % 4))
+      (lddz % 4) || (mask && (!dA || ldmask < K)))
     return oerr(DSSM_E_INVALID, "dense_bwd: bad argument");
   if (dssm_dense_bwd_slab_floats(M, K, N, dtype) && !slab)
     return oerr(DSSM_E_INVALID, "dense_bwd: this shape needs a split-K slab");
@@ -237,11 +239,17 @@ int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, in
   hipError_t e = hipSuccess;
   if (dA)
     e = dssm::launch_gemm(dssm::GEMM_DA, bf, M, K, N, dZ, lddz, W, ldw, dA, ldda, nullptr, false, nullptr,
-                          s, nullptr);
+                          s, nullptr, 0, mask, ldmask);
   if (e == hipSuccess)
     e = dssm::launch_gemm(dssm::GEMM_DW, bf, K + 1, N, M, A, lda, dZ, lddz, dWb, N, nullptr, true, slab, s,
                           nullptr);
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                   const void* dZ, int lddz, float* dA, int ldda, float* dWb, float* slab, void* stream) {
+  return dssm_dense_bwd_masked(A, lda, W, ldw, dtype, M, K, N, dZ, lddz, dA, ldda, nullptr, 0, dWb, slab,
+                               stream);
 }
 
 int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamma, const float* beta,

@@ -1217,27 +1217,41 @@ int dssm_plan_graph_probe_read(dssm_plan* P, int graph_id, int probe_id, float* 
 }
 
 // ---- functional entry points ------------------------------------------------------------
-int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
-                      const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
-                      int ldz, void* stream) {
+int dssm_spmm_csr_fwd_act(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                          const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
+                          int ldz, int act, void* stream) {
   if (!indptr || !W || !bias || !Z || rows < 0 || n < 4 || (n % 4) || ldz < n || (ldz % 8) ||
-      ldw < n || (ldw % 4))
+      ldw < n || (ldw % 4) || (act != DSSM_ACT_NONE && act != DSSM_ACT_RELU))
     return fail(DSSM_E_INVALID, "dssm_spmm_csr_fwd: bad arguments (n%4==0, ldz%8==0, ldw>=n)");
   if (w_dtype == DSSM_BF16 && ldw < ldp8(n))
     return fail(DSSM_E_INVALID, "bf16 W needs ldw >= round_up(n, 8) with zero pads");
   HIP_TRY(dssm::launch_spmm_fwd(indptr, indices, values, rows, W, w_dtype == DSSM_BF16, ldw, n,
-                                bias, Z, ldz, (hipStream_t)stream));
+                                bias, Z, ldz, (hipStream_t)stream, nullptr, act == DSSM_ACT_RELU));
+  return DSSM_OK;
+}
+
+int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                      const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
+                      int ldz, void* stream) {
+  return dssm_spmm_csr_fwd_act(indptr, indices, values, rows, W, w_dtype, ldw, n, bias, Z, ldz,
+                               DSSM_ACT_NONE, stream);
+}
+
+int dssm_dense_fwd_act(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                       const float* bias, float* Z, int ldz, int act, void* stream) {
+  if (!A || !W || !bias || !Z || M < 0 || K < 1 || N < 1 || lda < K || ldw < N || ldz < N ||
+      (lda % 8) || (ldw % 4) || (ldz % 4) || (dtype == DSSM_BF16 && (ldw % 8)) ||
+      (act != DSSM_ACT_NONE && act != DSSM_ACT_RELU))
+    return fail(DSSM_E_INVALID, "dssm_dense_fwd: bad arguments");
+  HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, dtype == DSSM_BF16, M, N, K, A, lda, W, ldw, Z, ldz,
+                            bias, false, nullptr, (hipStream_t)stream, nullptr,
+                            act == DSSM_ACT_RELU ? 1 : 0));
   return DSSM_OK;
 }
 
 int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                    const float* bias, float* Z, int ldz, void* stream) {
-  if (!A || !W || !bias || !Z || M < 0 || K < 1 || N < 1 || lda < K || ldw < N || ldz < N ||
-      (lda % 8) || (ldw % 4) || (ldz % 4) || (dtype == DSSM_BF16 && (ldw % 8)))
-    return fail(DSSM_E_INVALID, "dssm_dense_fwd: bad arguments");
-  HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, dtype == DSSM_BF16, M, N, K, A, lda, W, ldw, Z, ldz,
-                            bias, false, nullptr, (hipStream_t)stream));
-  return DSSM_OK;
+  return dssm_dense_fwd_act(A, lda, W, ldw, dtype, M, K, N, bias, Z, ldz, DSSM_ACT_NONE, stream);
 }
 
 size_t dssm_bn_ws_bytes(int rows, int ldz) {

@@ -44,7 +44,7 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
                                           const float* __restrict__ values, int rows,
                                           const TW* __restrict__ W, int ldw, int n,
                                           const float* __restrict__ bias, float* __restrict__ Z,
-                                          int ldz, int b) {
+                                          int ldz, int b, bool relu = false) {
   const int row = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
   const int lane = lane_id();
@@ -56,6 +56,10 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = (c + i < n) ? bias[c + i] : 0.f;
     gather_accumulate(indices, values, s, e, W, ldw, c, nvalid, acc);
+    if (relu) {  // the layer's ReLU fused (functional API: FC1 + tf.nn.relu)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaxf(acc[i], 0.f);
+    }
     if (c < ldz) store8(Z + (size_t)row * ldz + c, acc);
   }
 }
@@ -96,12 +100,12 @@ __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr
                                                   const TW* __restrict__ W, int ldw, int n,
                                                   const float* __restrict__ bias,
                                                   float* __restrict__ Z, int ldz, EvalCoef ec,
-                                                  int ne) {
+                                                  int ne, int relu) {
   if ((int)blockIdx.x < ne) {
     eval_coef_item(ec, (int)blockIdx.x * 256 + threadIdx.x);
     return;
   }
-  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne);
+  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne, relu != 0);
 }
 
 // ---- CSR -> CSC ------------------------------------------------------------------------------
@@ -816,17 +820,17 @@ int eval_coef_blocks(const EvalCoef& e) {
 
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s, const EvalCoef* ec) {
+                           int ldz, hipStream_t s, const EvalCoef* ec, bool relu) {
   EvalCoef e{};
   const int ne = ec ? eval_coef_blocks(*ec) : 0;
   if (ec) e = *ec;
   dim3 grid(ne + cdiv(rows, 4)), block(256);
   if (w_bf16)
     hipLaunchKernelGGL(k_spmm_fwd<u16>, grid, block, 0, s, indptr, indices, values, rows,
-                       (const u16*)W, ldw, n, bias, Z, ldz, e, ne);
+                       (const u16*)W, ldw, n, bias, Z, ldz, e, ne, relu ? 1 : 0);
   else
     hipLaunchKernelGGL(k_spmm_fwd<float>, grid, block, 0, s, indptr, indices, values, rows,
-                       (const float*)W, ldw, n, bias, Z, ldz, e, ne);
+                       (const float*)W, ldw, n, bias, Z, ldz, e, ne, relu ? 1 : 0);
   return hipGetLastError();
 }
 

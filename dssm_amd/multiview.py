@@ -8,7 +8,9 @@ softmax, summed loss, Adam on the user tower and the active view.
 The user tower and the active item view run concurrently (the item tower on a second stream that
 forks from and joins the caller's stream): each tower's launches are latency-bound, so the two
 chains overlap on the CUs.  Composed from libdssm.so's functional C-ABI (include/dssm.h): dssm_spmm_csr_fwd /
-dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2), dssm_relu / dssm_relu_bwd,
+dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2) with the ReLUs in their epilogues
+(dssm_spmm_csr_fwd_act / dssm_dense_fwd_act, dssm_dense_bwd_masked: FC1's ReLU backward on dA1),
+dssm_relu_bwd (FC2's ReLU backward),
 dssm_rows_gather / dssm_rows_scatter_add (the rotation as an index map and its backward),
 dssm_cosine_softmax_loss (shared with the BoW path), dssm_adam_step.  fp32; torch tensors are
 device storage only.
@@ -68,7 +70,6 @@ class MultiViewDSSM:
         self.adam_v = torch.zeros(off, dtype=f32, device=dev)
         self.adam_state = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
         BS, R = self.bs, self.bs * (2 + self.neg)
-        self.z1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         self.a1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         self.ysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)   # [user_y; item_y]
         self.dysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)
@@ -77,7 +78,6 @@ class MultiViewDSSM:
         # per-tower backward scratch: the two towers run concurrently (user tower on the caller's
         # stream, the item tower on self.aux)
         self.dz2 = {k: torch.zeros((BS, self.ld2), dtype=f32, device=dev) for k in ("u", "i")}
-        self.da1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         self.dz1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         K = self.neg + 1
         self.cos_raw = torch.zeros(K * BS, dtype=f32, device=dev)
@@ -168,13 +168,13 @@ class MultiViewDSSM:
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w1, w2 = self._block(self.params, f"{tower}_1"), self._block(self.params, f"{tower}_2")
-        check(self.lib.dssm_spmm_csr_fwd(ptr(ip), ptr(ix), ptr(vv), self.bs, ptr(w1), _lib.DSSM_F32, self.l1,
-                                         self.l1, ptr(w1[d]), ptr(self.z1[key]), self.ld1, s), "spmm_fwd")
-        check(self.lib.dssm_relu(ptr(self.z1[key]), self.ld1, self.bs, self.l1, ptr(self.a1[key]), self.ld1, s),
-              "relu")
-        check(self.lib.dssm_dense_fwd(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
-                                      self.l1, self.l2, ptr(w2[self.l1]), ptr(y_rows), self.ld2, s), "dense_fwd")
-        check(self.lib.dssm_relu(ptr(y_rows), self.ld2, self.bs, self.l2, ptr(y_rows), self.ld2, s), "relu")
+        # FC + ReLU in one launch each (the ReLU in the producers' epilogues)
+        check(self.lib.dssm_spmm_csr_fwd_act(ptr(ip), ptr(ix), ptr(vv), self.bs, ptr(w1), _lib.DSSM_F32, self.l1,
+                                             self.l1, ptr(w1[d]), ptr(self.a1[key]), self.ld1, _lib.DSSM_ACT_RELU, s),
+              "spmm_fwd")
+        check(self.lib.dssm_dense_fwd_act(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
+                                          self.l1, self.l2, ptr(w2[self.l1]), ptr(y_rows), self.ld2,
+                                          _lib.DSSM_ACT_RELU, s), "dense_fwd")
 
     def _fork(self, stream):
         """The item tower's stream joins the caller's stream here."""
@@ -202,15 +202,15 @@ class MultiViewDSSM:
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w2 = self._block(self.params, f"{tower}_2")
-        dz2, da1, dz1 = self.dz2[key], self.da1[key], self.dz1[key]
+        dz2, dz1 = self.dz2[key], self.dz1[key]
         check(self.lib.dssm_relu_bwd(ptr(y_rows), self.ld2, ptr(dy_rows), self.ld2, self.bs, self.l2,
                                      ptr(dz2), self.ld2, s), "relu_bwd")
-        check(self.lib.dssm_dense_bwd(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
-                                      self.l1, self.l2, ptr(dz2), self.ld2, ptr(da1), self.ld1,
-                                      ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
+        # dA1 with FC1's ReLU backward fused (masked by a1 = relu(z1) > 0): dz1 directly
+        check(self.lib.dssm_dense_bwd_masked(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32,
+                                             self.bs, self.l1, self.l2, ptr(dz2), self.ld2, ptr(dz1), self.ld1,
+                                             ptr(self.a1[key]), self.ld1,
+                                             ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
               "dense_bwd")
-        check(self.lib.dssm_relu_bwd(ptr(self.a1[key]), self.ld1, ptr(da1), self.ld1, self.bs, self.l1,
-                                     ptr(dz1), self.ld1, s), "relu_bwd")
         check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(dz1),
                                            _lib.DSSM_F32, self.ld1, self.l1,
                                            ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),

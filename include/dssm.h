@@ -246,10 +246,18 @@ int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, floa
 int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
                       const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
                       int ldz, void* stream);
+/* Epilogue activations of the functional forwards (the FC layer + tf.nn.relu of
+ * archive/multi_view_dssm_v3.py:120-139 in one launch). */
+enum { DSSM_ACT_NONE = 0, DSSM_ACT_RELU = 1 };
+int dssm_spmm_csr_fwd_act(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                          const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
+                          int ldz, int act, void* stream);
 /* add_layer (archive/dssm_v3.py:44-53) on device: Z[M x ldz] = A[M x lda] . W[K x ldw] + bias,
  * inputs of dtype `dtype`, fp32 accumulate and output. */
 int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                    const float* bias, float* Z, int ldz, void* stream);
+int dssm_dense_fwd_act(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                       const float* bias, float* Z, int ldz, int act, void* stream);
 /* batch_normalization (new_dssm.py:62-88) + ReLU over rows [row0, row0+rows) of Z (one tower).
  * train!=0: batch moments, EMA update of ema_mean/ema_var; train==0: uses the EMA.
  * out: [rows x ldz] of out_dtype; batch_mean/var may be NULL.  ws: >= dssm_bn_ws_bytes(),
@@ -282,6 +290,11 @@ int dssm_spmm_csr_bwd_w(const int32_t* indptr, const int32_t* indices, const flo
 size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype);
 int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                    const void* dZ, int lddz, float* dA, int ldda, float* dWb, float* slab, void* stream);
+/* dssm_dense_bwd with the ReLU backward of the layer's input fused into dA: dA = (dZ W^T) where
+ * mask [M x ldmask] > 0, else 0 (mask = the ReLU output that was the layer's input A; ReluGrad). */
+int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                          const void* dZ, int lddz, float* dA, int ldda, const float* mask, int ldmask,
+                          float* dWb, float* slab, void* stream);
 /* batch_normalization + ReLU backward with batch statistics (new_dssm.py:62-88, :134-136; ReLU'(0) =
  * 0): from the forward's Z, gamma, beta and batch mean / biased variance (dssm_bn_relu_fwd's
  * batch_mean / batch_var), dout -> dz, dgamma, dbeta.  relu = 0: plain batch norm. */

@@ -78,6 +78,61 @@ def test_dense_bwd(dt):
     _close(dWb.cpu().numpy(), A1.T @ dZ.astype(np.float64), tol)
 
 
+def test_dense_bwd_masked_and_fused_relu_forwards():
+    """dssm_dense_bwd_masked (ReluGrad through the layer input fused into dA: exact zeros where the
+    mask is <= 0, the plain dA elsewhere, same dW), dssm_dense_fwd_act / dssm_spmm_csr_fwd_act with
+    DSSM_ACT_RELU against the unfused entry points + dssm_relu (bit-identical: the same arithmetic
+    with the max in the epilogue)."""
+    lib = _lib.load()
+    M, K, N = 1024, 300, 128
+    rng = np.random.Generator(np.random.PCG64(5))
+    lda, ldw = 304, 128
+    A = torch.zeros((M, lda), device="cuda")
+    A[:, :K] = torch.from_numpy(np.maximum(rng.standard_normal((M, K)), 0).astype(np.float32)).cuda()
+    W = torch.from_numpy(rng.standard_normal((K + 1, ldw)).astype(np.float32) * 0.1).cuda()
+    dZ = torch.from_numpy(rng.standard_normal((M, ldw)).astype(np.float32)).cuda()
+    slab = torch.zeros(max(1, lib.dssm_dense_bwd_slab_floats(M, K, N, _lib.DSSM_F32)), device="cuda")
+    s = _lib.stream_ptr()
+    dA, dWb = torch.zeros((M, lda), device="cuda"), torch.zeros((K + 1, N), device="cuda")
+    check(lib.dssm_dense_bwd(ptr(A), lda, ptr(W), ldw, _lib.DSSM_F32, M, K, N, ptr(dZ), ldw, ptr(dA), lda,
+                             ptr(dWb), ptr(slab), s), "dense_bwd")
+    dAm, dWbm = torch.zeros((M, lda), device="cuda"), torch.zeros((K + 1, N), device="cuda")
+    check(lib.dssm_dense_bwd_masked(ptr(A), lda, ptr(W), ldw, _lib.DSSM_F32, M, K, N, ptr(dZ), ldw, ptr(dAm),
+                                    lda, ptr(A), lda, ptr(dWbm), ptr(slab), s), "dense_bwd_masked")
+    torch.cuda.synchronize()
+    assert torch.equal(dWbm, dWb)
+    assert torch.equal(dAm[:, :K], torch.where(A[:, :K] > 0, dA[:, :K], torch.zeros_like(dA[:, :K])))
+    assert float((A[:, :K] <= 0).float().mean()) > 0.3  # the mask does cut
+    # the masked form rejects a mask without dA
+    assert lib.dssm_dense_bwd_masked(ptr(A), lda, ptr(W), ldw, _lib.DSSM_F32, M, K, N, ptr(dZ), ldw, None,
+                                     lda, ptr(A), lda, ptr(dWbm), ptr(slab), s) != 0
+    # forward GEMM + ReLU
+    Z, Zr = torch.zeros((M, ldw), device="cuda"), torch.zeros((M, ldw), device="cuda")
+    check(lib.dssm_dense_fwd(ptr(A), lda, ptr(W), ldw, _lib.DSSM_F32, M, K, N, ptr(W[K]), ptr(Z), ldw, s), "fwd")
+    check(lib.dssm_relu(ptr(Z), ldw, M, N, ptr(Z), ldw, s), "relu")
+    check(lib.dssm_dense_fwd_act(ptr(A), lda, ptr(W), ldw, _lib.DSSM_F32, M, K, N, ptr(W[K]), ptr(Zr), ldw,
+                                 _lib.DSSM_ACT_RELU, s), "fwd_act")
+    torch.cuda.synchronize()
+    assert torch.equal(Z, Zr) and float((Zr[:, :N] == 0).float().mean()) > 0.3
+    ref = torch.relu(A[:, :K].double() @ W[:K, :N].double() + W[K, :N].double())
+    assert float((Zr[:, :N].double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    # sparse FC1 + ReLU
+    D, n = 5000, 300
+    ip, ix, vv = synth_rows(rng, ZipfColumns(D), M, 24.0)
+    t = [torch.from_numpy(x).cuda() for x in (ip, ix, vv)]
+    W1 = torch.from_numpy(rng.standard_normal((D + 1, n)).astype(np.float32) * 0.1).cuda()
+    Y, Yr = torch.zeros((M, lda), device="cuda"), torch.zeros((M, lda), device="cuda")
+    check(lib.dssm_spmm_csr_fwd(ptr(t[0]), ptr(t[1]), ptr(t[2]), M, ptr(W1), _lib.DSSM_F32, n, n, ptr(W1[D]),
+                                ptr(Y), lda, s), "spmm")
+    check(lib.dssm_relu(ptr(Y), lda, M, n, ptr(Y), lda, s), "relu")
+    check(lib.dssm_spmm_csr_fwd_act(ptr(t[0]), ptr(t[1]), ptr(t[2]), M, ptr(W1), _lib.DSSM_F32, n, n,
+                                    ptr(W1[D]), ptr(Yr), lda, _lib.DSSM_ACT_RELU, s), "spmm_act")
+    torch.cuda.synchronize()
+    assert torch.equal(Y[:, :n], Yr[:, :n])
+    assert lib.dssm_spmm_csr_fwd_act(ptr(t[0]), ptr(t[1]), ptr(t[2]), M, ptr(W1), _lib.DSSM_F32, n, n,
+                                     ptr(W1[D]), ptr(Yr), lda, 7, s) != 0
+
+
 @pytest.mark.parametrize("relu", [1, 0])
 def test_bn_relu_bwd(relu):
     lib = _lib.load()
