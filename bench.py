@@ -124,9 +124,9 @@ def pmc_traffic(workload: dict):
     committed profiles/r*_traffic.json collected on THIS workload (dtype, column distribution,
     feed); PMC counters cannot be read from inside the timed run.  No matching summary: none."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic*.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("_workload", DEFAULT_WORKLOAD) != workload:
+        if d.get("_workload", DEFAULT_WORKLOAD) != workload:  # (other rows' files name their model)
             continue
         out = {probe: d[k]["hbm_bytes"] for probe, k in PMC_KERNELS[workload["dtype"]].items() if k in d}
         return out, os.path.relpath(f, ROOT)
