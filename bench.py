@@ -283,10 +283,9 @@ def bench_multiview(args):
         feeds.append((dict(m.batch), b + 1))
         host_feeds.append((u, it, b + 1))
 
-    # Adam (user tower + active view, one k_adam_step launch each) is the dominant kernel: HIP events
-    # on the stream the model launches on (torch's current stream) bracket its two launches in every
-    # timed step
-    probes = []
+    # Adam (user tower + active view, one optimizer launch each) is the dominant kernel: libdssm's
+    # dssm_adam_probe records HIP events around each launch on the stream it runs on (inside the
+    # captured Adam graphs: event-record nodes timing every replay, read for the latest)
     # hipGraph replay (--graph 1): per staged feed one graph for forward + backward (both towers'
     # streams, fork / join captured) and one for the two Adam launches, so the ~30 host calls of a
     # step (ctypes + stream bookkeeping, about as long as the GPU work) leave the timed loop; the
@@ -306,6 +305,7 @@ def bench_multiview(args):
             m.apply_adam(grad_scale=1.0 / world)
         torch.cuda.synchronize()
         if args.graph:
+            m.lib.dssm_adam_probe(6)  # the 3 Adam graphs' 2 launches each
             for i in range(3):
                 m.batch, m.view = dict(feeds[i][0]), feeds[i][1]
                 g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -317,31 +317,27 @@ def bench_multiview(args):
                 fb_graphs.append(g1)
                 adam_graphs.append(g2)
 
-    def step(i, probe=False):
+    def step(i):
         if args.graph:
             fb_graphs[i % 3].replay()
         else:
             eager(i)
         if dp is not None:
             dp.exchange()  # between the graphs: RCCL all-reduce of the trained towers' gradients
-        if probe:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
         if args.graph:
             adam_graphs[i % 3].replay()
         else:
             m.apply_adam(grad_scale=1.0 / world)
-        if probe:
-            ev[1].record()
-            probes.append(ev)
     torch.cuda.set_stream(stream)
+    if not args.graph:
+        m.lib.dssm_adam_probe(2 * args.steps)
     torch.cuda.synchronize()
     if dp is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, probe=True)
+        step(args.warmup + i)
     torch.cuda.synchronize()
     if dp is not None:
         dist.barrier()
@@ -350,7 +346,12 @@ def bench_multiview(args):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    adam_ms = float(np.mean([a.elapsed_time(b) for a, b in probes])) / 2  # per launch
+    import ctypes as C
+    avg, cnt = C.c_double(), C.c_int()
+    from dssm_amd._lib import check
+    check(m.lib.dssm_adam_probe_read(C.byref(avg), C.byref(cnt)), "adam_probe_read")
+    m.lib.dssm_adam_probe(0)
+    adam_ms = avg.value  # per launch
     tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
     # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower
     adam_bytes = int(28 * tower_params)
@@ -366,7 +367,7 @@ def bench_multiview(args):
                       "dp_exchange": dp.comm if dp is not None else None},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
-                        "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5)},
+                        "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5), "launches": cnt.value},
            "final_loss": round(m.loss(), 3)}
     t, src = model_profile("traffic", "multiview", "k_rnn_adam")
     if t is not None:

@@ -278,6 +278,8 @@ struct AdamStep {
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
+// a timing probe's event (plan.hip): hipEventRecord, or an event-record node while s is capturing
+void record_probe_event(hipStream_t s, hipEvent_t e);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
 // bf16 wire helpers (data parallel): wire[i] = bf16(g[i]) for i < n (n % 4 == 0); the W1 shadow
 // rows from the all-gathered bf16 parameter wire (row length cols, shadow stride ld)

@@ -347,6 +347,27 @@ struct dssm_plan {
 };
 
 namespace dssm {
+// A timing probe's event on stream s: a plain record, or while s is capturing, an explicit
+// event-record node after the capture frontier (hipEventRecord on a capturing stream only marks a
+// fork / join point).  Shared by the functional API's probes (rnn.hip, rnn_mfma.hip).
+void record_probe_event(hipStream_t s, hipEvent_t e) {
+  hipStreamCaptureStatus st;
+  if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive) {
+    unsigned long long id;
+    hipGraph_t g;
+    const hipGraphNode_t* deps;
+    size_t nd;
+    if (hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &nd) != hipSuccess) return;
+    hipGraphNode_t node;
+    if (hipGraphAddEventRecordNode(&node, g, deps, nd, e) != hipSuccess) return;
+    hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+    return;
+  }
+  (void)hipEventRecord(e, s);
+}
+}  // namespace dssm
+
+namespace dssm {
 int report_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 }  // namespace dssm
 

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/dssm.h"
 #include "common.h"
@@ -366,6 +367,13 @@ bool dims_ok(int R, int T, int E, int H) {
   return R > 0 && T > 0 && E > 0 && H > 0 && E + H <= dssm::kMaxK && H <= dssm::kMaxH && (E % 4) == 0 &&
          (H % 4) == 0;
 }
+// HIP-event probes around dssm_adam_step's optimizer launch (bench.py's multi-view roofline: the
+// launch's duration measured on the stream it runs on; recorded inside a graph capture they become
+// event-record nodes, which time each captured launch's latest replay)
+struct AdamProbe {
+  std::vector<hipEvent_t> ev;  // pairs
+  int used = 0;
+} g_adam_probe;
 }  // namespace
 
 extern "C" {
@@ -478,9 +486,39 @@ extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int6
   if (!p || !g || !m || !v || !state || n < 0) return rerr(DSSM_E_INVALID, "adam_step: bad argument");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+  const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
+  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, (int64_t)0, n, state, lr,
                      beta1, beta2, eps, grad_scale);
+  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]);
   if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+extern "C" int dssm_adam_probe(int n_max) {
+  for (hipEvent_t e : g_adam_probe.ev) (void)hipEventDestroy(e);
+  g_adam_probe.ev.clear();
+  g_adam_probe.used = 0;
+  for (int i = 0; i < 2 * n_max; ++i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return rerr(DSSM_E_HIP, "adam_probe: hipEventCreate");
+    g_adam_probe.ev.push_back(e);
+  }
+  return DSSM_OK;
+}
+
+extern "C" int dssm_adam_probe_read(double* avg_ms, int* count) {
+  if (!avg_ms || !count) return rerr(DSSM_E_INVALID, "adam_probe_read: bad argument");
+  double tot = 0.0;
+  for (int i = 0; i < g_adam_probe.used; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(g_adam_probe.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_adam_probe.ev[2 * i], g_adam_probe.ev[2 * i + 1]) != hipSuccess)
+      return rerr(DSSM_E_HIP, "adam_probe_read: event");
+    tot += ms;
+  }
+  *count = g_adam_probe.used;
+  *avg_ms = g_adam_probe.used ? tot / g_adam_probe.used : 0.0;
+  return DSSM_OK;
 }

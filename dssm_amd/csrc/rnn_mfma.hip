@@ -907,14 +907,14 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   const bool probe = g_probe.used < (int)g_probe.ev.size() / 2;
-  if (probe) (void)hipEventRecord(g_probe.ev[2 * g_probe.used], s);
+  if (probe) dssm::record_probe_event(s, g_probe.ev[2 * g_probe.used]);
   if (E == 128)
     dssm::dispatch_bwd<128, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else if (E == 64)
     dssm::dispatch_bwd<64, 128>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
   else
     dssm::dispatch_bwd<32, 32>(mt, d, ids, lens, w, dy, lddy, L, demb, s);
-  if (probe) (void)hipEventRecord(g_probe.ev[2 * g_probe.used++ + 1], s);
+  if (probe) dssm::record_probe_event(s, g_probe.ev[2 * g_probe.used++ + 1]);
   const dim3 gemb((V + 3) / 4);
   if (E == 128)
     hipLaunchKernelGGL(dssm::k_emb_grad<128>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);

@@ -307,6 +307,10 @@ int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamm
  * when advance != 0 (an optimizer step spanning several calls advances on its last one). */
 int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                    float beta2, float eps, float* state, float grad_scale, int advance, void* stream);
+/* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
+ * averages the recorded launches (in a captured graph, each launch's latest replay). */
+int dssm_adam_probe(int n_max);
+int dssm_adam_probe_read(double* avg_ms, int* count);
 /* Row gather / scatter-add (Merge_Negative_Doc by index, its backward): dst[r] = src[map[r]];
  * dst[map[r]] += src[r] over r < n after dst (dst_rows x ldd) is cleared.  fp32. */
 int dssm_rows_gather(const float* src, int lds, const int32_t* map, int n, int cols, float* dst, int ldd,
