@@ -172,9 +172,14 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(seconds: float):
-    """Time the CPU port of the step (oracle/, test infrastructure) on a bounded sample."""
+    """Time the CPU port of the step (oracle/, test infrastructure) on a bounded sample, and the
+    NumPy float32 oracle on a shorter one as the secondary number."""
     from oracle import cpu_port
-    return cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds)
+    out = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds)
+    if "C/OpenMP" in out.get("sample", ""):
+        sec = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=min(5.0, seconds / 3), use_c=False)
+        out["numpy_oracle"] = {k: sec[k] for k in ("value", "unit", "cores", "sample")}
+    return out
 
 
 def bench_rnn(args):

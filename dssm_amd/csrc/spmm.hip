@@ -26,6 +26,10 @@
 #include "launch.h"
 #include "csc.h"
 
+#ifndef DSSM_SPMM_U  // rows in flight per lane in the SpMM's gather batches
+#define DSSM_SPMM_U 8
+#endif
+
 namespace dssm {
 namespace {
 
@@ -55,7 +59,7 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = (c + i < n) ? bias[c + i] : 0.f;
-    gather_accumulate(indices, values, s, e, W, ldw, c, nvalid, acc);
+    gather_accumulate<TW, 1, DSSM_SPMM_U>(indices, values, s, e, W, ldw, c, nvalid, acc);
     if (relu) {  // the layer's ReLU fused (functional API: FC1 + tf.nn.relu)
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = fmaxf(acc[i], 0.f);

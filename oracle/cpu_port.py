@@ -25,14 +25,17 @@ def _threads():
     return os.cpu_count() or 1
 
 
-def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000):
+def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000, use_c: bool = True):
+    """use_c=False times the NumPy float32 oracle even when the C port is built (SURVEY §8(d)'s
+    secondary CPU number)."""
     from dssm_amd.data import ZipfColumns, synth_batch  # synthetic batches only (host numpy)
-    try:
-        from . import cpu_c
-        if cpu_c.available():
-            return cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
-    except ImportError:
-        pass
+    if use_c:
+        try:
+            from . import cpu_c
+            if cpu_c.available():
+                return cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
+        except ImportError:
+            pass
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
     p = O.init_params(cfg, seed=0)
     ema = O.make_ema(cfg)
