@@ -1,0 +1,53 @@
+"""bench.py's measurement plumbing on the CPU (no GPU run): the committed profile summaries it
+attaches to a line are the ones collected on THAT line's workload, the algorithmic-byte formulas
+match DESIGN.md §5, and the committed bench lines keep the driver's JSON contract."""
+import json
+import os
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_traffic_lookup_matches_workload():
+    t, src = bench.pmc_traffic({"dtype": "bf16", "columns": "zipf", "feed": "device"})
+    assert src and set(t) <= {"adam", "spmm_fwd"} and t["adam"] > 0
+    d = json.load(open(os.path.join(ROOT, src)))
+    assert d["_workload"] == {"dtype": "bf16", "columns": "zipf", "feed": "device"}
+    t32, src32 = bench.pmc_traffic({"dtype": "fp32", "columns": "zipf", "feed": "device"})
+    assert src32 != src and json.load(open(os.path.join(ROOT, src32)))["_workload"]["dtype"] == "fp32"
+    # a workload nobody profiled gets no traffic, never another workload's
+    assert bench.pmc_traffic({"dtype": "bf16", "columns": "zipf", "feed": "host"}) == ({}, None)
+
+
+def test_model_profiles_are_not_taken_for_the_headline():
+    mf = bench.mfma_summary("bf16")
+    assert mf is not None and "model" not in json.load(open(os.path.join(ROOT, mf["source"])))["_workload"]
+    assert not any(k.startswith(("k_gru", "k_rnn")) for k in mf["kernels"])
+    v, src = bench.model_profile("traffic", "rnn", "k_gru_bwd_mfma<128, 128, 3>")
+    assert v is not None and json.load(open(os.path.join(ROOT, src)))["_workload"]["model"] == "rnn"
+    assert bench.model_profile("traffic", "nosuchmodel", "k_rnn_adam") == (None, None)
+
+
+def test_algorithmic_bytes():
+    # SpMM forward: 4(R+1) + NNZ*8 + NNZ*L1*2 + R*L1*4 at the C2 shapes, bf16
+    assert bench.spmm_alg_bytes(196608, 6144, 300, 2) == 4 * 6145 + 196608 * 8 + 196608 * 600 + 6144 * 1200
+    # fused single-GPU Adam: 24 B per parameter + the gathered [W1; b1] gradient rows + the shadows
+    n_params, w1 = 9132040, 30001 * 300
+    b = bench.adam_alg_bytes(n_params, True, True, w1, 197742, 6144, 300, n_params, 0, 1)
+    assert 3.5e8 < b < 3.7e8
+
+
+@pytest.mark.parametrize("name", ["r02_bench_bf16", "r02_bench_fp32", "r02_bench_rnn", "r02_bench_multiview"])
+def test_committed_lines_keep_the_contract(name):
+    d = json.loads(open(os.path.join(ROOT, "profiles", name + ".json")).read().strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    r = d["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and 0 < r["frac"] < 1
+    assert abs(r["achieved"] / r["peak"] - r["frac"]) < 1e-3
+    assert abs(r["bytes_per_launch"] / (r["avg_ms"] * 1e-3) / 1e9 - r["achieved"]) <= 1e-3 * r["achieved"] + 0.1
+    assert "workload" in d["config"]
