@@ -144,6 +144,8 @@ _SIGS = {
                                       _P, _P, _P]),
     "dssm_adam_probe": (C.c_int, [C.c_int]),
     "dssm_adam_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    "dssm_rows_gather_sum": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_float, _P, C.c_int, _P,
+                                       C.c_int, _P]),
     "dssm_dense_bwd_slab_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "dssm_dense_bwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
                                  _P, C.c_int, _P, _P, _P]),

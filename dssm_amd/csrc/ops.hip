@@ -128,6 +128,23 @@ __global__ void k_rows_scatter_add(const float* __restrict__ src, int lds, const
   }
 }
 
+// dst[r] = scale * sum of src rows idx[offs[r] .. offs[r+1]) in list order (the scatter-add's
+// inverse: fixed order, no atomics, no clearing pass); with mask, zero where mask[r] <= 0 (ReluGrad)
+__global__ void k_rows_gather_sum(const float* __restrict__ src, int lds, const int* __restrict__ offs,
+                                  const int* __restrict__ idx, int n, int cols, float scale,
+                                  const float* __restrict__ mask, int ldm, float* __restrict__ dst, int ldd) {
+  const int64_t total = (int64_t)n * cols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    float acc = 0.f;
+    for (int j = offs[r]; j < offs[r + 1]; ++j) acc += src[(size_t)idx[j] * lds + c];
+    acc *= scale;
+    if (mask && !(mask[(size_t)r * ldm + c] > 0.f)) acc = 0.f;
+    dst[(size_t)r * ldd + c] = acc;
+  }
+}
+
 __global__ void k_relu(const float* __restrict__ x, int ldx, int rows, int cols, float* __restrict__ y,
                        int ldy) {
   const int64_t total = (int64_t)rows * cols;
@@ -173,6 +190,15 @@ int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, 
     return oerr(DSSM_E_HIP, "rows_scatter_add: hipMemsetAsync");
   hipLaunchKernelGGL(k_rows_scatter_add, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, s, src, lds, map, n,
                      cols, dst, ldd);
+  return hip_status();
+}
+
+int dssm_rows_gather_sum(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
+                         float scale, const float* mask, int ldm, float* dst, int ldd, void* stream) {
+  if (!src || !offs || !idx || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols || (mask && ldm < cols))
+    return oerr(DSSM_E_INVALID, "rows_gather_sum: bad argument");
+  hipLaunchKernelGGL(k_rows_gather_sum, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, (hipStream_t)stream, src,
+                     lds, offs, idx, n, cols, scale, mask, ldm, dst, ldd);
   return hip_status();
 }
 

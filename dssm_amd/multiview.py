@@ -10,8 +10,8 @@ forks from and joins the caller's stream): each tower's launches are latency-bou
 chains overlap on the CUs.  Composed from libdssm.so's functional C-ABI (include/dssm.h): dssm_spmm_csr_fwd /
 dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2) with the ReLUs in their epilogues
 (dssm_spmm_csr_fwd_act / dssm_dense_fwd_act, dssm_dense_bwd_masked: FC1's ReLU backward on dA1),
-dssm_relu_bwd (FC2's ReLU backward),
-dssm_rows_gather / dssm_rows_scatter_add (the rotation as an index map and its backward),
+dssm_rows_gather_sum (the rotation's gradient x BS with FC2's ReLU backward),
+dssm_rows_gather (the rotation as an index map),
 dssm_cosine_softmax_loss (shared with the BoW path), dssm_adam_step.  fp32; torch tensors are
 device storage only.
 
@@ -72,12 +72,11 @@ class MultiViewDSSM:
         BS, R = self.bs, self.bs * (2 + self.neg)
         self.a1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         self.ysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)   # [user_y; item_y]
-        self.dysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)
+        self.dz2src = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)  # FC2's dz, [user; item]
         self.merged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         self.dmerged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         # per-tower backward scratch: the two towers run concurrently (user tower on the caller's
         # stream, the item tower on self.aux)
-        self.dz2 = {k: torch.zeros((BS, self.ld2), dtype=f32, device=dev) for k in ("u", "i")}
         self.dz1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         K = self.neg + 1
         self.cos_raw = torch.zeros(K * BS, dtype=f32, device=dev)
@@ -146,7 +145,15 @@ class MultiViewDSSM:
         i = np.tile(np.arange(self.neg), BS)
         m.append(BS + (j + np.array(rot)[i]) % BS)
         self.rot = rot
-        self.map = torch.from_numpy(np.concatenate(m).astype(np.int32)).to(self.device)
+        mp = np.concatenate(m).astype(np.int32)
+        self.map = torch.from_numpy(mp).to(self.device)
+        # its inverse (each of the 2BS source rows: the merged rows it feeds, ascending) for the
+        # backward's fixed-order gather-sum
+        order = np.argsort(mp, kind="stable").astype(np.int32)
+        offs = np.zeros(2 * BS + 1, np.int32)
+        np.cumsum(np.bincount(mp, minlength=2 * BS), out=offs[1:])
+        self.inv_idx = torch.from_numpy(order).to(self.device)
+        self.inv_offs = torch.from_numpy(offs).to(self.device)
 
     # ---- feed ---------------------------------------------------------------------------------
     def set_batch(self, user_csr, item_csr, view: int):
@@ -198,13 +205,11 @@ class MultiViewDSSM:
                                                 ptr(self.qnorm), ptr(self.loss_buf), ptr(self.dmerged),
                                                 ptr(self.cos_ws), s), "cosine")
 
-    def _tower_bwd(self, key, tower, y_rows, dy_rows, s):
+    def _tower_bwd(self, key, tower, dz2, s):
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w2 = self._block(self.params, f"{tower}_2")
-        dz2, dz1 = self.dz2[key], self.dz1[key]
-        check(self.lib.dssm_relu_bwd(ptr(y_rows), self.ld2, ptr(dy_rows), self.ld2, self.bs, self.l2,
-                                     ptr(dz2), self.ld2, s), "relu_bwd")
+        dz1 = self.dz1[key]
         # dA1 with FC1's ReLU backward fused (masked by a1 = relu(z1) > 0): dz1 directly
         check(self.lib.dssm_dense_bwd_masked(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32,
                                              self.bs, self.l1, self.l2, ptr(dz2), self.ld2, ptr(dz1), self.ld1,
@@ -221,13 +226,14 @@ class MultiViewDSSM:
         s = stream_ptr(main)
         BS, R = self.bs, self.bs * (2 + self.neg)
         # the cosine kernel's d(mean loss)/dy x BS = d(summed loss)/dy (multi_view_dssm_v3.py:234)
-        check(self.lib.dssm_rnn_dropout(ptr(self.dmerged), ptr(self.dmerged), R, self.l2, self.ld2, 1.0, 0, 0,
-                                        float(BS), s), "scale")
-        check(self.lib.dssm_rows_scatter_add(ptr(self.dmerged), self.ld2, ptr(self.map), R, self.l2,
-                                             ptr(self.dysrc), self.ld2, 2 * BS, s), "scatter")
+        # Merge_Negative_Doc's gradient, the x BS and FC2's ReLU backward in one launch: dz2 of both
+        # towers = BS * (sum of the merged rows each source row feeds) where y > 0
+        check(self.lib.dssm_rows_gather_sum(ptr(self.dmerged), self.ld2, ptr(self.inv_offs), ptr(self.inv_idx),
+                                            2 * BS, self.l2, float(BS), ptr(self.ysrc), self.ld2, ptr(self.dz2src),
+                                            self.ld2, s), "gather_sum")
         self._fork(main)
-        self._tower_bwd("u", "user", self.ysrc[:BS], self.dysrc[:BS], s)
-        self._tower_bwd("i", f"view{self.view}", self.ysrc[BS:], self.dysrc[BS:], stream_ptr(self.aux))
+        self._tower_bwd("u", "user", self.dz2src[:BS], s)
+        self._tower_bwd("i", f"view{self.view}", self.dz2src[BS:], stream_ptr(self.aux))
         main.wait_stream(self.aux)
 
     def trained_ranges(self):

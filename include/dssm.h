@@ -317,6 +317,11 @@ int dssm_rows_gather(const float* src, int lds, const int32_t* map, int n, int c
                      void* stream);
 int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, int cols, float* dst,
                           int ldd, int dst_rows, void* stream);
+/* The scatter-add's inverse form (Merge_Negative_Doc's gradient without atomics): dst[r] = scale *
+ * sum over j in [offs[r], offs[r+1]) of src[idx[j]], summed in list order, for r < n; with mask
+ * (ld ldm) the result is 0 where mask[r] <= 0 (the ReLU backward of the rows' forward output). */
+int dssm_rows_gather_sum(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
+                         float scale, const float* mask, int ldm, float* dst, int ldd, void* stream);
 /* tf.nn.relu and its gradient (ReluGrad: dx = y > 0 ? dy : 0); y may alias x. */
 int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, void* stream);
 int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, int cols, float* dx,

@@ -133,6 +133,36 @@ def test_dense_bwd_masked_and_fused_relu_forwards():
                                      ptr(W1[D]), ptr(Yr), lda, 7, s) != 0
 
 
+def test_rows_gather_sum_is_the_scatter_add_inverse():
+    """dssm_rows_gather_sum over the inverse of a map == scale x dssm_rows_scatter_add over the map
+    (up to summation order), masked by ReluGrad where a mask is given."""
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(9))
+    n_src, n, cols, ld = 300, 1500, 128, 128
+    mp = rng.integers(0, n_src, n).astype(np.int32)
+    order = np.argsort(mp, kind="stable").astype(np.int32)
+    offs = np.zeros(n_src + 1, np.int32)
+    np.cumsum(np.bincount(mp, minlength=n_src), out=offs[1:])
+    src = torch.from_numpy(rng.standard_normal((n, ld)).astype(np.float32)).cuda()
+    mask = torch.from_numpy(rng.standard_normal((n_src, ld)).astype(np.float32)).cuda()
+    t_map, t_idx, t_off = (torch.from_numpy(x).cuda() for x in (mp, order, offs))
+    ref = torch.zeros((n_src, ld), device="cuda")
+    s = _lib.stream_ptr()
+    check(lib.dssm_rows_scatter_add(ptr(src), ld, ptr(t_map), n, cols, ptr(ref), ld, n_src, s), "scatter_add")
+    got, gotm = torch.zeros_like(ref), torch.zeros_like(ref)
+    check(lib.dssm_rows_gather_sum(ptr(src), ld, ptr(t_off), ptr(t_idx), n_src, cols, 3.0, None, 0, ptr(got), ld, s),
+          "gather_sum")
+    check(lib.dssm_rows_gather_sum(ptr(src), ld, ptr(t_off), ptr(t_idx), n_src, cols, 3.0, ptr(mask), ld, ptr(gotm),
+                                   ld, s), "gather_sum masked")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got, 3.0 * ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gotm, torch.where(mask > 0, 3.0 * ref, torch.zeros_like(ref)), rtol=1e-5, atol=1e-5)
+    # a source row no merged row maps to gets exact zeros
+    empty = np.flatnonzero(np.bincount(mp, minlength=n_src) == 0)
+    if empty.size:
+        assert float(got[torch.from_numpy(empty).cuda()].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("relu", [1, 0])
 def test_bn_relu_bwd(relu):
     lib = _lib.load()
