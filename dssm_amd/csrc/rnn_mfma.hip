@@ -745,6 +745,9 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 }
 
 // ---- workspace and dispatch -------------------------------------------------------------------
+#ifndef DSSM_RNN_DW_WGS  // workgroups of one k_rnn_dw launch (tiles x row splits): 2 per CU
+#define DSSM_RNN_DW_WGS 512
+#endif
 constexpr int kDwMaxSplits = 64;
 
 struct WsB {
@@ -954,7 +957,7 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   A.ntiles = n;
   A.TR = TR;
   // about two workgroups per CU (64 KB of LDS each) in one round
-  A.splits = std::max(1, std::min({dssm::kDwMaxSplits, 512 / n, (TR + 63) / 64}));
+  A.splits = std::max(1, std::min({dssm::kDwMaxSplits, DSSM_RNN_DW_WGS / n, (TR + 63) / 64}));
   A.splits -= A.splits & 1;  // even: with 12 tiles (E = H = 128) the XCD grouping needs splits * ntiles % 8 == 0
   A.splits = std::max(A.splits, 1);
   A.splits = std::min(A.splits, dssm::kDwMaxSplits);
