@@ -346,6 +346,10 @@ struct dssm_plan {
   }
 };
 
+#ifndef DSSM_GRAPH_UPLOAD
+#define DSSM_GRAPH_UPLOAD 1
+#endif
+
 namespace dssm {
 // A timing probe's event on stream s: a plain record, or while s is capturing, an explicit
 // event-record node after the capture frontier (hipEventRecord on a capturing stream only marks a
@@ -1135,6 +1139,10 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
     delete g;
     return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
   }
+#if DSSM_GRAPH_UPLOAD
+  // upload the executable graph now (without running it), so its first launch pays no upload
+  (void)hipGraphUpload(g->exec, s);
+#endif
   P->graphs.push_back(g);
   *graph_id = (int)P->graphs.size() - 1;
   return DSSM_OK;
@@ -1177,8 +1185,10 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     // probes (event-record nodes): the transpose / SpMM / dW1 ones in the first step (the only one
     // with its own rank launch when the rank pass rides in Adam), the Adam one in the last step (the
     // only Adam launch hosting no rank pass: it times the optimizer alone)
-    g->probes = with_probes != 0 && (i == 0 || i == nsteps - 1);
-    g->probe_mask = (i == 0 ? ~(1u << DSSM_PROBE_ADAM) : 0u) | (i == nsteps - 1 ? 1u << DSSM_PROBE_ADAM : 0u);
+    // (with_probes == 2: the Adam probe alone)
+    g->probes = with_probes != 0 && ((i == 0 && with_probes != 2) || i == nsteps - 1);
+    g->probe_mask = (i == 0 && with_probes != 2 ? ~(1u << DSSM_PROBE_ADAM) : 0u) |
+                    (i == nsteps - 1 ? 1u << DSSM_PROBE_ADAM : 0u);
     P->indptr = indptrs[i];
     P->indices = indices[i];
     P->values = values[i];
@@ -1214,6 +1224,10 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     delete g;
     return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
   }
+#if DSSM_GRAPH_UPLOAD
+  // upload the executable graph now (without running it), so its first launch pays no upload
+  (void)hipGraphUpload(g->exec, s);
+#endif
   P->graphs.push_back(g);
   *graph_id = (int)P->graphs.size() - 1;
   return DSSM_OK;

@@ -287,10 +287,12 @@ class DSSM:
         self._graphs[gid.value] = (parts, self._batch_refs)  # keep the batch tensors alive
         return gid.value
 
-    def graph_build_steps(self, batches, probes: bool = False, stream=None) -> int:
+    def graph_build_steps(self, batches, probes=False, stream=None) -> int:
         """Capture len(batches) whole training steps back to back into ONE graph, step i on the
         device CSR batch (indptr, indices, values) = batches[i]; a replay runs all of them (the
-        host launch boundary is paid once per replay, not once per step)."""
+        host launch boundary is paid once per replay, not once per step).  probes: True = every
+        probe (transpose / SpMM / dW1 in the first step, Adam in the last), "adam" = the Adam probe
+        alone (two event-record nodes instead of eight)."""
         sp = stream_ptr(stream)
         if not sp:
             raise ValueError("graph capture needs a non-default stream (torch.cuda.Stream())")
@@ -298,7 +300,8 @@ class DSSM:
         arr = [(C.c_void_p * n)(*[ptr(b[k]) for b in batches]) for k in range(3)]
         gid = C.c_int()
         check(self.lib.dssm_plan_graph_build_steps(self._plan, arr[0], arr[1], arr[2], n,
-                                                   1 if probes else 0, sp, C.byref(gid)),
+                                                   2 if probes == "adam" else (1 if probes else 0), sp,
+                                                   C.byref(gid)),
               "graph_build_steps")
         self._graphs[gid.value] = (_lib.GRAPH_FWD_BWD | _lib.GRAPH_ADAM, tuple(batches), n)
         return gid.value

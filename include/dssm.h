@@ -206,7 +206,8 @@ int dssm_plan_graph_build(dssm_plan* plan, int parts, float grad_scale, int with
 int dssm_plan_graph_launch(dssm_plan* plan, int graph_id, void* stream);
 /* nsteps whole training steps (forward + backward + Adam, as dssm_plan_train_step) captured
  * back to back into ONE graph, step i on batch (indptrs[i], indices[i], values[i]): a replay
- * runs them with no host launch boundary between steps.  Probes record the first step only.
+ * runs them with no host launch boundary between steps.  with_probes 1: the transpose / SpMM /
+ * dW1 probes record the first step, the Adam probe the last; 2: the Adam probe alone.
  * The plan's current batch is left as it was. */
 int dssm_plan_graph_build_steps(dssm_plan* plan, const int32_t* const* indptrs,
                                 const int32_t* const* indices, const float* const* values,
