@@ -203,15 +203,29 @@ def bench_rnn(args):
     def step(i):
         m.ids = staged[i % len(staged)]
         m.train_step()
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
     probe = args.dtype == "bf16" and args.probes
     if probe:  # HIP events around every timed BPTT launch, on the stream it runs on (libdssm.so)
         m.lib.dssm_rnn_bf16_probe(args.steps)
+    region = None
+    if args.graph and args.steps <= 256:
+        # the timed region as ONE graph of exactly K steps (each captured step keeps its own dropout
+        # mask index); the BPTT probes become event-record nodes around each captured BPTT launch
+        region = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(region, stream=stream):
+            for i in range(args.steps):
+                step(args.warmup + i)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    if region is not None:
+        region.replay()
+    else:
+        for i in range(args.steps):
+            step(args.warmup + i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out = {"metric": "query-doc pairs/sec (fwd+bwd), dssm_rnn tower (BASELINE config 4)",
@@ -221,7 +235,8 @@ def bench_rnn(args):
            "data": "synthetic",
            "config": {"workload": "dssm_rnn: vocab 21128, emb 128, BiGRU(128), seq_len 32, dropout 0.5, "
                                   "BS=1024, NEG=4, fwd+BPTT+Adam", "global_batch": BS, "neg": NEG,
-                      "parallelism": "dp1"},
+                      "parallelism": "dp1", "launch": "hipgraph: one graph of K steps" if region is not None
+                      else "eager"},
            "final_loss": round(m.loss(), 3)}
     if probe:
         import ctypes as C
@@ -295,7 +310,7 @@ def bench_multiview(args):
     # streams, fork / join captured) and one for the two Adam launches, so the ~30 host calls of a
     # step (ctypes + stream bookkeeping, about as long as the GPU work) leave the timed loop; the
     # Adam probes bracket the Adam graph's replay on the stream it runs on
-    fb_graphs, adam_graphs = [], []
+    fb_graphs, adam_graphs, region = [], [], None
     stream = torch.cuda.Stream()
 
     def eager(i):
@@ -309,7 +324,20 @@ def bench_multiview(args):
                 dp.exchange()
             m.apply_adam(grad_scale=1.0 / world)
         torch.cuda.synchronize()
-        if args.graph:
+        if args.graph and dp is None and args.steps <= 256:
+            # one GPU: the whole timed region as ONE graph of exactly K steps (no launch gaps between
+            # steps); the Adam probe records the last step's two optimizer launches
+            region = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(region, stream=stream):
+                for i in range(args.steps):
+                    j = args.warmup + i
+                    m.batch, m.view = dict(feeds[j % 3][0]), feeds[j % 3][1]
+                    m.forward()
+                    m.backward()
+                    if i == args.steps - 1:
+                        m.lib.dssm_adam_probe(2)
+                    m.apply_adam(grad_scale=1.0)
+        elif args.graph:
             m.lib.dssm_adam_probe(6)  # the 3 Adam graphs' 2 launches each
             for i in range(3):
                 m.batch, m.view = dict(feeds[i][0]), feeds[i][1]
@@ -341,8 +369,11 @@ def bench_multiview(args):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    if region is not None:
+        region.replay()
+    else:
+        for i in range(args.steps):
+            step(args.warmup + i)
     torch.cuda.synchronize()
     if dp is not None:
         dist.barrier()
@@ -368,7 +399,8 @@ def bench_multiview(args):
            "data": "synthetic",
            "config": {"workload": "multi_view_dssm_v3: user + 3 views (30k sparse -> 300 -> 128), in-batch "
                                   "rotated negatives, BS=4096 per GPU, NEG=4, fwd+bwd+Adam", "global_batch": B * world,
-                      "neg": NEG, "parallelism": f"dp{world}", "launch": "hipgraph" if args.graph else "eager",
+                      "neg": NEG, "parallelism": f"dp{world}",
+                      "launch": ("hipgraph: one graph of K steps" if region is not None else "hipgraph") if args.graph else "eager",
                       "dp_exchange": dp.comm if dp is not None else None},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
