@@ -568,21 +568,31 @@ def main():
         graphs = []
         # Probes (graph event-record nodes cost a few us each) ride in batch 0's graph only, so
         # they are sampled once per len(staged) steps inside the timed region.
+        split = world > 1 or rehearse > 1
+        shadow_part = 0
+        if dp is not None and dp.mode == "zero":
+            shadow_part = _lib.GRAPH_WIRE_SHADOWS if dp.wire == "bf16" else _lib.GRAPH_SHADOWS
+        elif rehearse > 1:
+            shadow_part = _lib.GRAPH_WIRE_SHADOWS
+        # data parallel: per batch the plain fwd+bwd graph (the run's first step) and one that first
+        # refreshes the shadows from the previous step's update (no collective between the two, so
+        # one graph boundary fewer per step); the shadow-only graph leaves the state consistent after
+        # the timed region
+        merged = []
         for b, (ip, ix, vv) in enumerate(staged):
             model.set_batch(indptr=ip, indices=ix, values=vv)
-            pr = bool(args.probes) and b == 0 and (world > 1 or rehearse > 1 or not args.multi_step)
-            if world > 1 or rehearse > 1:
+            # the probes ride in the graph of the timed region's first step (batch W mod len(staged))
+            pr = bool(args.probes) and b == args.warmup % len(staged) and (world > 1 or rehearse > 1 or
+                                                                           not args.multi_step)
+            if split:
                 graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
+                if shadow_part:
+                    merged.append(model.graph_build(_lib.GRAPH_FWD_BWD | shadow_part, probes=pr))
             else:
                 graphs.append(model.graph_build(probes=pr))
-        split = world > 1 or rehearse > 1
         adam_graph = (model.graph_build(_lib.GRAPH_ADAM, 1.0 / max(world, rehearse), probes=bool(args.probes))
                       if split else None)
-        shadow_graph = None
-        if dp is not None and dp.mode == "zero":
-            shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS if dp.wire == "bf16" else _lib.GRAPH_SHADOWS)
-        elif rehearse > 1:
-            shadow_graph = model.graph_build(_lib.GRAPH_WIRE_SHADOWS)
+        shadow_graph = model.graph_build(shadow_part) if shadow_part else None
 
         # single GPU: the staged batches' steps also captured back to back into one graph, replayed
         # once per full cycle of len(staged) steps (one host launch boundary per cycle); the
@@ -623,15 +633,14 @@ def main():
                 model.graph_launch(partial[n % len(staged)])
 
         def step(i):
-            model.graph_launch(graphs[i % len(graphs)])
+            # steps after the first start with the previous step's shadow refresh (merged graph)
+            model.graph_launch((merged if merged and i > 0 else graphs)[i % len(graphs)])
             if split:
                 if dp is not None:
                     dp.exchange_before_adam()
                 model.graph_launch(adam_graph)
-                if shadow_graph is not None:
-                    if dp is not None:
-                        dp.exchange_after_adam()
-                    model.graph_launch(shadow_graph)
+                if shadow_graph is not None and dp is not None:
+                    dp.exchange_after_adam()
     else:
         def step(i):
             ip, ix, vv = staged[i % len(staged)]
@@ -667,6 +676,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.graph and feeder is None and split and shadow_graph is not None:
+        model.graph_launch(shadow_graph)  # untimed: the last step's shadow refresh
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -683,7 +694,9 @@ def main():
         if args.graph:  # last replay of every staged-batch graph, all inside the timed region
             g = adam_graph if (name == "adam" and adam_graph is not None) else (
                 (region[args.steps] if name == "adam" else probe_graph) if args.steps in region else
-                (cycle if args.steps >= len(staged) else partial[args.steps]) if cycle is not None else graphs[0])
+                (cycle if args.steps >= len(staged) else partial[args.steps]) if cycle is not None else
+                (graphs[0] if feeder is not None else
+                 (merged if split and merged and args.warmup > 0 else graphs)[args.warmup % len(graphs)]))
             probes[name] = model.graph_probe_read(g, pid)
         else:
             tot, cnt = model.probe_read(pid)

@@ -1114,13 +1114,22 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
   }
   P->capturing = g;
   int rc = DSSM_OK;
-  if (parts & DSSM_GRAPH_FWD_BWD) {
+  // a shadow part with FWD_BWD and no ADAM: the previous step's shadow refresh, then this step's
+  // forward + backward (data parallel: one graph boundary fewer per step, the refresh and the next
+  // forward have no collective between them)
+  const bool shadows_first = (parts & DSSM_GRAPH_FWD_BWD) && !(parts & DSSM_GRAPH_ADAM) &&
+                             (parts & (DSSM_GRAPH_SHADOWS | DSSM_GRAPH_WIRE_SHADOWS));
+  auto shadow_parts = [&]() {
+    if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
+    if (!rc && (parts & DSSM_GRAPH_WIRE_SHADOWS)) rc = dssm_plan_wire_shadows(P, stream);
+  };
+  if (shadows_first) shadow_parts();
+  if (!rc && (parts & DSSM_GRAPH_FWD_BWD)) {
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
   }
   if (!rc && (parts & DSSM_GRAPH_ADAM)) rc = dssm_plan_adam(P, grad_scale, stream);
-  if (!rc && (parts & DSSM_GRAPH_SHADOWS)) rc = dssm_plan_sync_shadows(P, stream);
-  if (!rc && (parts & DSSM_GRAPH_WIRE_SHADOWS)) rc = dssm_plan_wire_shadows(P, stream);
+  if (!shadows_first) shadow_parts();
   P->capturing = nullptr;
   std::string err = rc ? g_err : std::string();
   hipGraph_t graph = nullptr;

@@ -197,7 +197,10 @@ int dssm_plan_train_step(dssm_plan* plan, void* stream);
 
 /* hipGraph capture of a step for the CURRENT batch pointers (dssm_plan_set_batch): parts =
  * DSSM_GRAPH_FWD_BWD and/or DSSM_GRAPH_ADAM and/or DSSM_GRAPH_SHADOWS (data-parallel runs launch
- * the gradient collective between the first two).  Replays then cost one launch per step.  with_probes: the graph records the timing
+ * the gradient collective between the first two).  Parts run in the order FWD_BWD, ADAM, the shadow
+ * parts, except that a graph of FWD_BWD plus a shadow part WITHOUT ADAM runs the shadow refresh first
+ * (the previous step's, then this step's forward + backward: data parallel saves a graph boundary per
+ * step).  Replays then cost one launch per step.  with_probes: the graph records the timing
  * probes' events (read back for its last replay with dssm_plan_graph_probe_read).  stream must
  * not be the default stream.  Graphs are owned by the plan. */
 enum { DSSM_GRAPH_FWD_BWD = 1, DSSM_GRAPH_ADAM = 2, DSSM_GRAPH_SHADOWS = 4, DSSM_GRAPH_WIRE_SHADOWS = 8 };

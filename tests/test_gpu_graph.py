@@ -201,3 +201,37 @@ def test_cycle_graph_with_rank_in_adam(hosted):
         gr.graph_launch(gid)
         torch.cuda.synchronize()
     assert np.isfinite(gr.loss_accuracy()[0])
+
+
+def test_shadows_first_graph_matches_separate_graphs():
+    """A graph of FWD_BWD + a shadow part without ADAM runs the shadow refresh FIRST (bench.py's
+    data-parallel flow: the previous step's refresh merged with the next forward + backward).
+    Deterministic unfused bf16 steps: [fwd+bwd, Adam, shadows] x 3 with separate graphs equals
+    fwd+bwd, Adam, then [shadows+fwd+bwd, Adam] x 2 and a final shadows graph, bit for bit."""
+    D, widths, BS, NEG = 3000, (128, 128, 64), 64, 4
+    batches = _batches(D, BS, NEG, 3)
+    s = torch.cuda.Stream()
+    out = []
+    with torch.cuda.stream(s):
+        staged = [tuple(torch.from_numpy(x).cuda() for x in (hb.indptr, hb.indices, hb.values)) for hb in batches]
+        for merged in (False, True):
+            _, _, m = make(D, widths, BS, NEG, "bf16", fused=False)
+            m.set_option("DETERMINISTIC", True)
+            plain, comb = [], []
+            for ip, ix, vv in staged:
+                m.set_batch(indptr=ip, indices=ix, values=vv)
+                plain.append(m.graph_build(_lib.GRAPH_FWD_BWD))
+                comb.append(m.graph_build(_lib.GRAPH_FWD_BWD | _lib.GRAPH_SHADOWS))
+            adam = m.graph_build(_lib.GRAPH_ADAM)
+            sh = m.graph_build(_lib.GRAPH_SHADOWS)
+            for i in range(3):
+                m.graph_launch(comb[i] if merged and i > 0 else plain[i])
+                m.graph_launch(adam)
+                if not merged:
+                    m.graph_launch(sh)
+            if merged:
+                m.graph_launch(sh)
+            torch.cuda.synchronize()
+            out.append((m.params.clone(), m.loss_accuracy()[0]))
+    assert out[0][1] == out[1][1]
+    assert torch.equal(out[0][0], out[1][0])
