@@ -672,6 +672,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
+    host_launch = time.perf_counter() - t0  # host time to submit the timed region's launches
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -760,6 +761,7 @@ def main():
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,
         "final_loss": round(loss, 5), "final_accuracy": round(acc, 4),
+        "host_launch_ms": round(1e3 * host_launch, 3),
     }
     if args.columns != "zipf":
         out["config"]["columns"] = args.columns
