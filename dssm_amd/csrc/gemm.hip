@@ -560,6 +560,14 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       ub[i] = *reinterpret_cast<const uint4*>(a.BT + ((bok && kg < ldb) ? bbase + kg : 0));
     }
   }
+  // the epilogue's bias columns, loaded with the operands (a load issued after the MFMA loop would
+  // put its latency into the epilogue)
+  float bcol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = bn + wn * 32 + j * 16 + (lane & 15);
+    bcol[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
+  }
   float zb[2][2][4], cb[2][4];  // FS == 2: the epilogue's pre-BN values and coefficients
   if constexpr (FS == 2) {
     const size_t plane = (size_t)2 * ldc;
@@ -691,7 +699,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m < M && n < ldc) {
           const float v = acc[i][j][r];
-          const float x = (n < N) ? (a.bias ? v + a.bias[n] : v) : 0.f;
+          const float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
           if (lds_epi)
             sC[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * kCld + wn * 32 + j * 16 + (lane & 15)] = x;
           else
