@@ -107,6 +107,14 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
   const int kbeg = blockIdx.z * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int Mload = ones_row ? M - 1 : M;
+  float bcol[2] = {0.f, 0.f};  // GEMM_FWD: the epilogue's bias columns, loaded ahead of the K loop
+  if constexpr (MODE == GEMM_FWD) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+      bcol[j] = n < N ? bias[n] : 0.f;
+    }
+  }
 
   T ra[G][8], rb[G][8];
   auto load = [&](int k0) {
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
         const float v = acc[i][j][r];
         if (m >= M) continue;
         if constexpr (MODE == GEMM_FWD) {
-          float x = v + (n < N ? bias[n] : 0.f);
+          float x = v + bcol[j];
           if (relu) x = fmaxf(x, 0.f);
           if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? x : 0.f;
         } else if constexpr (MODE == GEMM_DA) {
@@ -289,6 +297,12 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
   const int bm = ty * 64, bn = tx * 64;
   const int tower = bm < a.row_split ? 0 : 1;
   const bool write_a = BN_A && a.a_out != nullptr && tx == 0;
+  float bcol[2];  // the epilogue's bias columns, loaded ahead of the K loop
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = bn + wn * 32 + j * 16 + (lane & 15);
+    bcol[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
+  }
   // BN_A: the layer's (inv, shift) for both towers staged in LDS once; the raw fp32 Z loads of
   // the next K-step stay in flight across this step's MFMAs and are transformed in store().
   if constexpr (BN_A) {
@@ -425,7 +439,7 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
         const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m < M && n < ldc) {
           const float v = acc[i][j][r];
-          const float x = (n < N) ? (a.bias ? v + a.bias[n] : v) : 0.f;
+          const float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
           a.C[(size_t)m * ldc + n] = x;
           if constexpr (FS == 1) {
             cs[j] += x;
