@@ -175,8 +175,28 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // GEMM_DA with a mask: the epilogue's 16 mask values per lane loaded behind the first K-step's
+  // operands and kept as bits (bit (i*2+j)*4+r: keep), not loaded after the K loop
+  unsigned keep_bits = 0xffffu;
   if (kbeg < kend) {
     load(kbeg);
+    if constexpr (MODE == GEMM_DA) {
+      if (mask) {
+        keep_bits = 0u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = bn + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+              const bool k = m < M && n < N && mask[(size_t)m * ldmask + n] > 0.f;
+              keep_bits |= (k ? 1u : 0u) << ((i * 2 + j) * 4 + r);
+            }
+          }
+      }
+    }
     store(0);
   }
   __syncthreads();
@@ -239,7 +259,8 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
           if (relu) x = fmaxf(x, 0.f);
           if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? x : 0.f;
         } else if constexpr (MODE == GEMM_DA) {
-          const bool keep = n < N && (!mask || mask[(size_t)m * ldmask + n] > 0.f);
+          const bool keep = n < N && (kbeg < kend ? ((keep_bits >> ((i * 2 + j) * 4 + r)) & 1u)
+                                                  : (!mask || mask[(size_t)m * ldmask + n] > 0.f));
           if (n < ldc) out[(size_t)m * ldc + n] = keep ? v : 0.f;
         } else {
           if (n < N) out[(size_t)m * ldc + n] = v;
