@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--columns", default="zipf", choices=["zipf", "uniform"],
                     help="column-id distribution of the synthetic batches (SURVEY 8d: Zipf(1.1) headline, "
                          "uniform variant)")
+    ap.add_argument("--fp32-line", type=int, default=1,
+                    help="N=1 bf16 headline: also time the fp32 parity mode (the reference's precision, "
+                         "new_dssm.py:111-114) over the same K / W in a child process and report it as "
+                         "the line's fp32_mode key")
     ap.add_argument("--fwd-only", type=int, default=1,
                     help="also time the forward alone (eval mode: EMA-BN forward + cosine + loss, "
                          "new_dssm.py:274-285) over the staged batches, N=1")
@@ -180,6 +184,26 @@ def cpu_baseline(seconds: float):
         sec = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=min(5.0, seconds / 3), use_c=False)
         out["numpy_oracle"] = {k: sec[k] for k in ("value", "unit", "cores", "sample")}
     return out
+
+
+def fp32_mode_line(args) -> dict:
+    """The fp32 parity mode (fp32 weights, activations and MFMA 16x16x4 f32) of the same C2
+    workload, K timed steps after W warm-up steps, timed by this script in a child process (a
+    fresh plan and arenas; the child prints its own line, summarised here)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--dtype", "fp32", "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--batches", str(args.batches), "--cpu-baseline", "0",
+           "--fwd-only", "0", "--fp32-line", "0", "--probes", str(args.probes)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"exit {r.returncode}: {r.stderr[-400:]}"}
+        d = json.loads(lines[-1])
+    except Exception as e:  # reported, never fatal for the headline
+        return {"error": repr(e)}
+    keep = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "roofline", "kernels_ms", "final_loss")
+    return {k: d[k] for k in keep if k in d}
 
 
 def bench_rnn(args):
@@ -561,47 +585,44 @@ def main():
                 feeder.next(model, next_batch=(i + 1) % args.batches)
                 model.graph_launch(gslots[feeder._cur])
                 feeder.done()
+    elif args.graph and dp is not None:
+        # data parallel: per staged batch a captured fwd+bwd graph (and the variant that first
+        # rebuilds the shadows from the previous step's all-gathered update), one Adam graph, the
+        # exchange's collectives between them (dssm_amd.dist.DataParallel.build_graphs)
+        dp.build_graphs(staged, probe_batch=(args.warmup % len(staged)) if args.probes else None)
+        graphs, adam_graph, cycle, region, probe_graph, split = None, None, None, {}, None, True
+
+        def run_steps(i0, n):
+            for i in range(i0, i0 + n):
+                dp.graph_step(i)
     elif args.graph:
-        # One captured step per staged batch (the batch pointers are baked into the graph); with
-        # N>1 the all-reduce runs between the fwd+bwd graph and the Adam graph.  Timing probes
-        # are event nodes inside the graphs (their last replay is read after the timed region).
+        # One captured step per staged batch (the batch pointers are baked into the graph).  Timing
+        # probes are event nodes inside the graphs (their last replay is read after the timed region).
         graphs = []
         # Probes (graph event-record nodes cost a few us each) ride in batch 0's graph only, so
         # they are sampled once per len(staged) steps inside the timed region.
-        split = world > 1 or rehearse > 1
-        shadow_part = 0
-        if dp is not None and dp.mode == "zero":
-            shadow_part = _lib.GRAPH_WIRE_SHADOWS if dp.wire == "bf16" else _lib.GRAPH_SHADOWS
-        elif rehearse > 1:
-            shadow_part = _lib.GRAPH_WIRE_SHADOWS
-        # data parallel: per batch the plain fwd+bwd graph (the run's first step) and one that first
-        # refreshes the shadows from the previous step's update (no collective between the two, so
-        # one graph boundary fewer per step); the shadow-only graph leaves the state consistent after
-        # the timed region
+        split = rehearse > 1
+        shadow_part = _lib.GRAPH_WIRE_SHADOWS if rehearse > 1 else 0
+        # rehearsal: per batch the plain fwd+bwd graph (the run's first step) and one that first
+        # refreshes the shadows from the previous step's update (one graph boundary fewer per step)
         merged = []
         for b, (ip, ix, vv) in enumerate(staged):
             model.set_batch(indptr=ip, indices=ix, values=vv)
             # the probes ride in the graph of the timed region's first step (batch W mod len(staged))
-            pr = bool(args.probes) and b == args.warmup % len(staged) and (world > 1 or rehearse > 1 or
-                                                                           not args.multi_step)
+            pr = bool(args.probes) and b == args.warmup % len(staged) and (rehearse > 1 or not args.multi_step)
             if split:
                 graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
-                if shadow_part:
-                    merged.append(model.graph_build(_lib.GRAPH_FWD_BWD | shadow_part, probes=pr))
+                merged.append(model.graph_build(_lib.GRAPH_FWD_BWD | shadow_part, probes=pr))
             else:
                 graphs.append(model.graph_build(probes=pr))
-        adam_graph = (model.graph_build(_lib.GRAPH_ADAM, 1.0 / max(world, rehearse), probes=bool(args.probes))
+        adam_graph = (model.graph_build(_lib.GRAPH_ADAM, 1.0 / rehearse, probes=bool(args.probes))
                       if split else None)
         shadow_graph = model.graph_build(shadow_part) if shadow_part else None
 
-        # single GPU: the staged batches' steps also captured back to back into one graph, replayed
-        # once per full cycle of len(staged) steps (one host launch boundary per cycle); the
-        # warm-up and the timed region each start at batch 0, and their last partial cycle (K mod
-        # len(staged) steps) is one more multi-step graph of the first batches, so every step of
-        # both runs inside a multi-step graph
-        # a run of up to MAX_REGION_STEPS steps (the warm-up, the timed region) is ONE multi-step
-        # graph of exactly that many steps over the batches in order (one launch, one separate rank
-        # launch: a second, partial graph would add its own launch gap and rank launch)
+        # single GPU: a run of up to MAX_REGION_STEPS steps (the warm-up, the timed region) is ONE
+        # multi-step graph of exactly that many steps over the batches in order (one launch, one
+        # separate rank launch: a second, partial graph would add its own launch gap and rank
+        # launch); longer runs replay a cycle graph of len(staged) steps plus a partial one.
         # Its only probe is the Adam one (the roofline's kernel: two event-record nodes; the eight
         # of the full set cost ~3.7 us/step at K = 20); the secondary probes (transpose, SpMM, dW1)
         # time one untimed replay of a probed cycle after the timed region.
@@ -636,11 +657,7 @@ def main():
             # steps after the first start with the previous step's shadow refresh (merged graph)
             model.graph_launch((merged if merged and i > 0 else graphs)[i % len(graphs)])
             if split:
-                if dp is not None:
-                    dp.exchange_before_adam()
                 model.graph_launch(adam_graph)
-                if shadow_graph is not None and dp is not None:
-                    dp.exchange_after_adam()
     else:
         def step(i):
             ip, ix, vv = staged[i % len(staged)]
@@ -677,7 +694,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if args.graph and feeder is None and split and shadow_graph is not None:
+    if dp is not None and args.graph:
+        dp.settle()  # untimed: the last step's shadow refresh
+    elif args.graph and feeder is None and split and shadow_graph is not None:
         model.graph_launch(shadow_graph)  # untimed: the last step's shadow refresh
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -692,6 +711,12 @@ def main():
         model.graph_launch(probe_graph)  # untimed: the secondary probes' replay
         torch.cuda.synchronize()
     for name, pid in (probe_ids if args.probes else ()):
+        if args.graph and dp is not None:  # the timed region's first step's graphs, the Adam graph
+            plain, merged_g, adam_g = dp.graph_ids()
+            g = adam_g if name == "adam" else (merged_g if merged_g and args.warmup > 0 else plain)[
+                args.warmup % len(plain)]
+            probes[name] = model.graph_probe_read(g, pid)
+            continue
         if args.graph:  # last replay of every staged-batch graph, all inside the timed region
             g = adam_graph if (name == "adam" and adam_graph is not None) else (
                 (region[args.steps] if name == "adam" else probe_graph) if args.steps in region else
@@ -753,8 +778,8 @@ def main():
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
-                   "dp_exchange": ((f"{dp.mode}/{dp.wire}" if dp.mode == "zero" else dp.mode) + f" via {dp.comm}")
-                                  if dp is not None else None,
+                   "dp_exchange": dp.schedule if dp is not None else None,
+                   "dp_fallbacks": dp.fallbacks if dp is not None else None,
                    "feed": "host CSR -> pinned async H2D (native feeder), PCIe inside the timed region"
                            if feeder is not None else "device-resident staged batches"},
         "roofline": dict(rl[dominant], kernel=dominant),
@@ -773,6 +798,9 @@ def main():
     if rehearse > 1:
         out["rehearsal"] = {"world": rehearse, "collectives": "omitted",
                             "note": "rank 0's compute share of an N-rank bf16-wire step; not a headline number"}
+    if (args.fp32_line and rank == 0 and world == 1 and rehearse == 1 and args.dtype == "bf16"
+            and feeder is None and args.columns == "zipf"):
+        out["fp32_mode"] = fp32_mode_line(args)
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

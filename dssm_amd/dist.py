@@ -29,13 +29,16 @@ Transports for the same collectives:
   through torch.distributed once (bootstrap only);
 * "torch": torch.distributed (gloo on the CPU tests; the "nccl" backend = RCCL as a fallback).
 
-Every collective the chosen schedule uses is self-tested at start-up on small exact patterns
-(every rank must agree); a failing library transport falls back to torch.distributed, a failing
-in-place schedule to "allreduce".
+Every collective the chosen schedule uses (SCHEDULE_OPS) is self-tested at start-up on small exact
+patterns and every rank must agree.  With comm="auto" a failing library transport falls back to
+torch.distributed and a failing zero schedule (mode="auto") is demoted to "allreduce"; each such
+fallback is warned about and listed in DataParallel.fallbacks (bench.py puts it in its JSON line).
+comm="rccl" and mode="zero" are strict: a failure raises on every rank instead.
 """
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -53,56 +56,81 @@ def _dtype_id(t: torch.Tensor) -> int:
 
 
 class TorchTransport:
-    """torch.distributed collectives (gloo on CPU; nccl = RCCL as a fallback)."""
+    """torch.distributed collectives: "nccl" (= RCCL) on GPUs as a fallback, gloo on the CPU tests.
+    gloo with device tensors (world-2 rehearsals sharing one GPU) stages every collective through
+    host memory, so each op keeps the same in-place semantics as the device transports."""
     name = "torch"
 
     def __init__(self, rank: int, world: int):
         self.rank, self.world = rank, world
         self.nccl = dist.get_backend() == "nccl"
 
+    def _host(self, fn, *ts):
+        """Run fn on host copies of device tensors (gloo), then copy the results back."""
+        if self.nccl or not any(t.is_cuda for t in ts):
+            fn(*ts)
+            return
+        hs = [t.cpu() for t in ts]
+        fn(*hs)
+        for t, h in zip(ts, hs):
+            t.copy_(h)
+
     def all_reduce(self, t):
-        dist.all_reduce(t)
+        self._host(dist.all_reduce, t)
 
     def reduce_scatter_(self, t, shard: int):
         """Sum over ranks; the rank's shard lands in place in its own copy of t."""
-        mine = t[self.rank * shard:(self.rank + 1) * shard]
         if self.nccl:
+            mine = t[self.rank * shard:(self.rank + 1) * shard]
             dist.reduce_scatter_tensor(mine, t)  # in place: output == input + rank * count
         else:
-            dist.all_reduce(t)  # gloo: the shard of the full sum is the same bytes
+            self._host(dist.all_reduce, t)  # gloo: the shard of the full sum is the same bytes
 
     def all_gather_(self, t, shard: int):
-        mine = t[self.rank * shard:(self.rank + 1) * shard]
         if self.nccl:
+            mine = t[self.rank * shard:(self.rank + 1) * shard]
             dist.all_gather_into_tensor(t, mine)  # in place: input == output + rank * count
-        else:
-            parts = list(t.view(self.world, shard).unbind(0))
-            got = [torch.empty_like(x) for x in parts]
-            dist.all_gather(got, mine.clone())
+            return
+
+        def gather(x):
+            parts = list(x.view(self.world, shard).unbind(0))
+            got = [torch.empty_like(p) for p in parts]
+            dist.all_gather(got, parts[self.rank].clone())
             for dst, src in zip(parts, got):
                 dst.copy_(src)
+        self._host(gather, t)
 
     def all_to_all(self, send, recv):
-        dist.all_to_all_single(recv, send)
+        self._host(lambda s, r: dist.all_to_all_single(r, s), send, recv)
 
     def destroy(self):
         pass
 
 
 class LibTransport:
-    """libdssm.so's RCCL communicator: collectives enqueued on the current stream, no torch op."""
+    """libdssm.so's RCCL communicator: collectives enqueued on the current stream, no torch op.
+
+    Bootstrap: rank 0 creates the 128-byte unique id and broadcasts (status, id) through
+    torch.distributed, so a failure on rank 0 reaches every rank in the same collective and all of
+    them raise together (DataParallel's transport selection then agrees on the next candidate)."""
     name = "rccl"
+    capturable = True  # RCCL calls may be captured into a hipGraph
 
     def __init__(self, rank: int, world: int):
         self.rank, self.world = rank, world
         lib = _lib.load()
         self.lib = lib
         buf = (C.c_char * 128)()
+        status, msg = True, ""
         if rank == 0:
-            check(lib.dssm_comm_unique_id(buf), "comm_unique_id")
-        obj = [bytes(buf)]
+            if lib.dssm_comm_unique_id(buf) != 0:
+                status, msg = False, lib.dssm_last_error().decode()
+        obj = [(status, msg, bytes(buf))]
         dist.broadcast_object_list(obj, src=0)
-        buf = (C.c_char * 128).from_buffer_copy(obj[0])
+        status, msg, raw = obj[0]
+        if not status:
+            raise _lib.DssmError(f"rank 0 could not create the RCCL unique id: {msg}")
+        buf = (C.c_char * 128).from_buffer_copy(raw)
         check(lib.dssm_comm_init(rank, world, buf), "comm_init")
 
     def all_reduce(self, t):
@@ -126,6 +154,92 @@ class LibTransport:
         self.lib.dssm_comm_destroy()
 
 
+# The collectives (op, dtype) each exchange schedule runs: only these are self-tested.
+SCHEDULE_OPS = {
+    ("allreduce", "fp32"): (("all_reduce", torch.float32),),
+    ("zero", "fp32"): (("reduce_scatter", torch.float32), ("all_gather", torch.float32)),
+    ("zero", "bf16"): (("all_to_all", torch.bfloat16), ("all_reduce", torch.float32),
+                       ("all_gather", torch.bfloat16), ("all_gather", torch.float32)),
+}
+
+
+def selftest(tx, ops, device, rank: int, world: int) -> bool:
+    """Small tensors with known contents (every partial sum exact in bf16) through the given
+    collectives, before any capture."""
+    w, r, k = world, rank, 64
+    try:
+        ok = True
+        for op, dt in ops:
+            if op == "reduce_scatter":
+                x = (torch.arange(w * k, device=device) % 4 + 4 * r).to(dt)
+                tx.reduce_scatter_(x, k)
+                ref = ((torch.arange(r * k, (r + 1) * k, device=device) % 4) * w + 4 * sum(range(w))).to(dt)
+                ok = ok and bool(torch.equal(x[r * k:(r + 1) * k], ref))
+            elif op == "all_gather":
+                y = torch.zeros(w * k, dtype=dt, device=device)
+                y[r * k:(r + 1) * k] = r + 1
+                tx.all_gather_(y, k)
+                ok = ok and bool(torch.equal(y, torch.arange(1, w + 1, device=device).to(dt).repeat_interleave(k)))
+            elif op == "all_to_all":
+                s = (torch.arange(w, device=device) + 8 * r).to(dt).repeat_interleave(k)  # chunk j: j + 8r
+                d = torch.zeros_like(s)
+                tx.all_to_all(s, d)
+                want = (torch.arange(w, device=device) * 8 + r).to(dt).repeat_interleave(k)  # from j: r + 8j
+                ok = ok and bool(torch.equal(d, want))
+            elif op == "all_reduce":
+                z = torch.full((k,), float(r + 1), dtype=dt, device=device)
+                tx.all_reduce(z)
+                ok = ok and bool(torch.equal(z, torch.full((k,), float(w * (w + 1) // 2), dtype=dt, device=device)))
+            else:
+                raise ValueError(op)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        return ok
+    except Exception:
+        return False
+
+
+def agree(ok: bool, device) -> bool:
+    """True on every rank iff ok on every rank (one MIN all-reduce)."""
+    flag = torch.tensor([1.0 if ok else 0.0], device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item() == 1.0)
+
+
+def select_transport(rank: int, world: int, device, comm: str, ops) -> "tuple":
+    """The first candidate transport that every rank can build and that passes the self-test of
+    `ops` on every rank: the library's RCCL communicator on GPUs under the nccl backend (comm
+    "auto" / "rccl"), then torch.distributed (comm "auto" / "torch").  comm="rccl" is strict: no
+    fallback, a failure raises on every rank.  Returns (transport or None, [fallback notes])."""
+    if comm not in ("auto", "rccl", "torch"):
+        raise ValueError("comm: 'auto', 'rccl' or 'torch'")
+    gpu = device.type == "cuda" and dist.get_backend() == "nccl"
+    cands = []
+    if comm in ("auto", "rccl") and gpu:
+        cands.append(LibTransport)
+    if comm == "torch" or (comm == "auto"):
+        cands.append(TorchTransport)
+    notes = []
+    for cls in cands:
+        err = ""
+        try:
+            tx = cls(rank, world)
+        except Exception as e:  # noqa: BLE001 - every rank learns the outcome through agree()
+            ok, tx, err = False, None, repr(e)
+        else:
+            ok = selftest(tx, ops, device, rank, world)
+            if not ok:
+                err = "self-test mismatch"
+        if agree(ok, device):
+            return tx, notes
+        if tx is not None:
+            tx.destroy()
+        notes.append(f"{cls.name} transport failed ({err or 'on another rank'})")
+    if comm == "rccl":
+        raise RuntimeError("comm='rccl' requested but libdssm.so's RCCL transport failed: " + "; ".join(notes))
+    return None, notes
+
+
 def shard_bounds(n_pad: int, n: int, rank: int, world: int):
     """Rank's optimizer shard of an arena of n elements padded to n_pad (equal shards)."""
     s = n_pad // world
@@ -136,10 +250,15 @@ class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
     def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto"):
+        """comm: "auto" (the library's RCCL communicator on GPUs, torch.distributed as the
+        self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
+        zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
+        fallback taken is listed in .fallbacks and warned about."""
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         npad = model.params.numel()
+        strict_mode = mode == "zero"
         if mode == "auto":
             mode = "zero" if (self.world > 1 and npad % (64 * self.world) == 0) else "allreduce"
         if mode == "zero" and npad % (64 * self.world):
@@ -153,9 +272,10 @@ class DataParallel:
             raise ValueError("wire: 'bf16' or 'fp32'")
         self.wire = wire if self.mode == "zero" else "fp32"
         self.tx = None
+        self.fallbacks = []
         if self.world > 1:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
-            self.tx = self._transport(comm)
+            self.tx = self._transport(comm, strict_mode)
         self.grad_wire = self.param_wire = self.stage = None
         if self.mode == "zero" and self.wire == "bf16":
             ext = model.wire_extent()
@@ -179,64 +299,29 @@ class DataParallel:
     def comm(self) -> str:
         return self.tx.name if self.tx is not None else "none"
 
-    def _transport(self, comm: str):
-        """The library's RCCL communicator on GPUs (comm "auto" / "rccl"), torch.distributed
-        otherwise; each candidate must pass the self-test of the collectives it will run."""
-        cands = []
-        gpu = self.model.params.is_cuda and dist.get_backend() == "nccl"
-        if comm in ("auto", "rccl") and gpu:
-            cands.append(LibTransport)
-        if comm in ("auto", "torch") or not cands:
-            cands.append(TorchTransport)
-        for cls in cands:
-            try:
-                tx = cls(self.rank, self.world)
-            except Exception:
-                ok, tx = False, None
-            else:
-                ok = self._selftest(tx)
-            if self._agree(ok):
-                return tx
-            if tx is not None:
-                tx.destroy()
-        if self.mode == "zero":
-            self.mode, self.wire = "allreduce", "fp32"  # last resort: one all-reduce
-        return TorchTransport(self.rank, self.world)
+    @property
+    def schedule(self) -> str:
+        """What the exchange runs, e.g. "zero/bf16 via rccl" (bench.py's config.dp_exchange)."""
+        s = f"{self.mode}/{self.wire}" if self.mode == "zero" else self.mode
+        return f"{s} via {self.comm}"
 
-    def _agree(self, ok: bool) -> bool:
-        flag = torch.tensor([1.0 if ok else 0.0], device=self.model.params.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item() == 1.0)
-
-    def _selftest(self, tx) -> bool:
-        """Small tensors with known contents (every partial sum exact in bf16) through every
-        collective this schedule uses, before any capture."""
+    def _transport(self, comm: str, strict_mode: bool):
+        """The transport for this schedule (select_transport); with no working transport a
+        non-strict zero schedule is demoted to "allreduce" (one fp32 all-reduce), whose smaller
+        set of collectives is tried again.  Every fallback is recorded and warned about."""
         dev = self.model.params.device
-        w, r, k = self.world, self.rank, 64
-        try:
-            ok = True
-            for dt in (torch.float32, torch.bfloat16):
-                x = (torch.arange(w * k, device=dev) % 4 + 4 * r).to(dt)
-                tx.reduce_scatter_(x, k)
-                ref = ((torch.arange(r * k, (r + 1) * k, device=dev) % 4) * w + 4 * sum(range(w))).to(dt)
-                ok = ok and bool(torch.equal(x[r * k:(r + 1) * k], ref))
-                y = torch.zeros(w * k, dtype=dt, device=dev)
-                y[r * k:(r + 1) * k] = r + 1
-                tx.all_gather_(y, k)
-                ok = ok and bool(torch.equal(y, torch.arange(1, w + 1, device=dev).to(dt).repeat_interleave(k)))
-                s = (torch.arange(w, device=dev) + 8 * r).to(dt).repeat_interleave(k)  # chunk j: j + 8r
-                d = torch.zeros_like(s)
-                tx.all_to_all(s, d)
-                want = (torch.arange(w, device=dev) * 8 + r).to(dt).repeat_interleave(k)  # from rank j: r + 8j
-                ok = ok and bool(torch.equal(d, want))
-                z = torch.full((k,), float(r + 1), dtype=dt, device=dev)
-                tx.all_reduce(z)
-                ok = ok and bool(torch.equal(z, torch.full((k,), float(w * (w + 1) // 2), dtype=dt, device=dev)))
-            if dev.type == "cuda":
-                torch.cuda.synchronize(dev)
-            return ok
-        except Exception:
-            return False
+        tx, notes = select_transport(self.rank, self.world, dev, comm, SCHEDULE_OPS[(self.mode, self.wire)])
+        self.fallbacks += notes
+        if tx is None and self.mode == "zero" and not strict_mode:
+            self.fallbacks.append(f"zero/{self.wire} schedule demoted to allreduce")
+            self.mode, self.wire = "allreduce", "fp32"
+            tx, notes = select_transport(self.rank, self.world, dev, comm, SCHEDULE_OPS[("allreduce", "fp32")])
+            self.fallbacks += notes
+        if tx is None:
+            raise RuntimeError("no working transport for the data-parallel exchange: " + "; ".join(self.fallbacks))
+        for note in self.fallbacks:
+            warnings.warn(f"DataParallel: {note}", RuntimeWarning, stacklevel=3)
+        return tx
 
     # ---- collectives ----------------------------------------------------------------------
     def exchange_before_adam(self):
@@ -287,6 +372,51 @@ class DataParallel:
         if self.mode == "zero":
             self.exchange_after_adam()
             self.refresh_shadows()
+
+    # ---- captured steps (bench.py's timed path) ----------------------------------------------
+    def build_graphs(self, staged, probe_batch=None):
+        """Capture, per staged device batch (indptr, indices, values), the forward + backward as a
+        hipGraph (plus, under the zero schedule, a variant that first rebuilds the weight shadows
+        from the previous step's all-gathered update: one graph boundary fewer per step), and one
+        Adam graph.  graph_step() replays them with the exchange's collectives between the graphs.
+        probe_batch: the batch whose graphs carry the plan's timing probes."""
+        from . import _lib
+        m = self.model
+        shadow = 0
+        if self.mode == "zero" and getattr(m, "dtype", "fp32") == "bf16":
+            shadow = _lib.GRAPH_WIRE_SHADOWS if self.wire == "bf16" else _lib.GRAPH_SHADOWS
+        self._g_plain, self._g_merged = [], []
+        for b, (ip, ix, vv) in enumerate(staged):
+            m.set_batch(indptr=ip, indices=ix, values=vv)
+            pr = b == probe_batch
+            self._g_plain.append(m.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
+            if shadow:
+                self._g_merged.append(m.graph_build(_lib.GRAPH_FWD_BWD | shadow, probes=pr))
+        self._g_adam = m.graph_build(_lib.GRAPH_ADAM, 1.0 / self.world, probes=probe_batch is not None)
+        self._g_shadow = m.graph_build(shadow) if shadow else None
+        self._shadows_pending = False
+
+    def graph_step(self, i: int):
+        """One step on staged batch i (mod the staged count) from the captured graphs."""
+        m = self.model
+        n = len(self._g_plain)
+        m.graph_launch((self._g_merged if self._shadows_pending else self._g_plain)[i % n])
+        self.exchange_before_adam()
+        m.graph_launch(self._g_adam)
+        if self.mode == "zero":
+            self.exchange_after_adam()
+            self._shadows_pending = self._g_shadow is not None
+
+    def settle(self):
+        """Rebuild the weight shadows a last graph_step left pending (the next graph_step would
+        have done it first thing): after the timed region, before reading or saving the model."""
+        if getattr(self, "_shadows_pending", False):
+            self.model.graph_launch(self._g_shadow)
+            self._shadows_pending = False
+
+    def graph_ids(self):
+        """(plain fwd+bwd graphs, merged graphs, Adam graph): for reading the timing probes."""
+        return self._g_plain, self._g_merged, self._g_adam
 
     def close(self):
         if self.tx is not None:

@@ -268,33 +268,21 @@ class MultiViewDataParallel:
 
     def __init__(self, model: MultiViewDSSM, comm: str = "auto"):
         import torch.distributed as dist
-        from .dist import LibTransport, TorchTransport
+        from .dist import SCHEDULE_OPS, select_transport
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.tx = None
+        self.fallbacks = []
         if self.world == 1:
             return
-        cands = []
-        if comm in ("auto", "rccl") and dist.get_backend() == "nccl":
-            cands.append(LibTransport)
-        cands.append(TorchTransport)
-        for cls in cands:
-            try:
-                tx = cls(self.rank, self.world)
-                z = torch.full((64,), float(self.rank + 1), device=model.device)
-                tx.all_reduce(z)
-                ok = bool(torch.equal(z, torch.full_like(z, float(self.world * (self.world + 1) // 2))))
-            except Exception:
-                tx, ok = None, False
-            flag = torch.tensor([1.0 if ok else 0.0], device=model.device)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if flag.item() == 1.0:
-                self.tx = tx
-                return
-            if tx is not None:
-                tx.destroy()
-        raise RuntimeError("no working all-reduce transport")
+        self.tx, self.fallbacks = select_transport(self.rank, self.world, model.device, comm,
+                                                   SCHEDULE_OPS[("allreduce", "fp32")])
+        if self.tx is None:
+            raise RuntimeError("no working all-reduce transport: " + "; ".join(self.fallbacks))
+        for note in self.fallbacks:
+            import warnings
+            warnings.warn(f"MultiViewDataParallel: {note}", RuntimeWarning, stacklevel=2)
 
     @property
     def comm(self) -> str:

@@ -25,6 +25,18 @@ def _threads():
     return os.cpu_count() or 1
 
 
+def host_cpus() -> dict:
+    """What the host offers the baseline: the threads used, the process's affinity-mask size, the
+    machine's CPU count (nproc) and OMP_NUM_THREADS.  On the GPU box OMP_NUM_THREADS is the box's
+    CPU share (16 per GPU), set by the harness and left as it is; nproc counts the whole machine."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"threads_used": _threads(), "affinity_cpus": aff, "nproc": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000, use_c: bool = True):
     """use_c=False times the NumPy float32 oracle even when the C port is built (SURVEY §8(d)'s
     secondary CPU number)."""
@@ -33,7 +45,9 @@ def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 1000
         try:
             from . import cpu_c
             if cpu_c.available():
-                return cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
+                out = cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
+                out["host"] = host_cpus()
+                return out
         except ImportError:
             pass
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
@@ -52,7 +66,7 @@ def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 1000
             break
     el = time.perf_counter() - t0
     return {"value": round(steps * BS * (NEG + 1) / el, 1), "unit": "pairs/s",
-            "cores": _threads(), "kind": "port",
+            "cores": _threads(), "kind": "port", "host": host_cpus(),
             "sample": f"{steps} full C2 steps (fwd+bwd+dense Adam, BS={BS}) of the NumPy float32 "
                       f"oracle in {el:.1f}s"}
 
@@ -79,6 +93,6 @@ def time_multiview_steps(cfg, params, feeds, budget_s: float = 15.0, max_steps: 
             break
     el = time.perf_counter() - t0
     return {"value": round(steps * cfg.bs * (cfg.neg + 1) / el, 1), "unit": "pairs/s",
-            "cores": _threads(), "kind": "port",
+            "cores": _threads(), "kind": "port", "host": host_cpus(),
             "sample": f"{steps} full config-5 steps (user + active view fwd + bwd + Adam, BS={cfg.bs}) of "
                       f"the NumPy float32 multi-view oracle with scipy CSR inputs in {el:.1f}s"}

@@ -1,0 +1,120 @@
+"""libdssm.so's own RCCL communicator (include/dssm.h dssm_comm_* / dssm_allreduce_sum /
+dssm_reduce_scatter_sum / dssm_all_gather / dssm_all_to_all; csrc/plan.hip) executed on the GPU.
+
+RCCL refuses two ranks on one device, so on the one-GPU box the communicator runs at world size 1
+(ncclCommInitRank with one rank): every collective then executes its real RCCL code path and its
+result is exactly known.  Covered: the bootstrap (dssm_amd.dist.LibTransport: rank 0's unique id
+broadcast through torch.distributed as a (status, id) pair), every collective in fp32 and bf16
+through LibTransport, the schedule self-tests of DataParallel (SCHEDULE_OPS), and the collectives
+captured into a hipGraph and replayed (the data-parallel step graph captures them).  The N>1
+exchange itself is covered by tests/test_gpu_dp_bow.py (two ranks over gloo on this GPU) and
+tests/test_dist_gloo.py (CPU); the reference has no data parallelism."""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tx():
+    from dssm_amd.dist import LibTransport
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    torch.cuda.set_device(0)
+    t = LibTransport(0, 1)
+    assert t.lib.dssm_comm_world() == 1
+    yield t
+    t.destroy()
+    assert t.lib.dssm_comm_world() == 0
+    dist.destroy_process_group()
+
+
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+def _pattern(n, dt, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randint(-512, 512, (n,), generator=g).float() / 8).to(dt).cuda()
+
+
+@pytest.mark.parametrize("dt", DTYPES, ids=["fp32", "bf16"])
+def test_collectives_world1_exact(tx, dt):
+    n = 4096 + 64
+    x = _pattern(n, dt, 1)
+    ref = x.clone()
+    tx.all_reduce(x)  # one rank: the sum is the buffer itself
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    y = _pattern(n, dt, 2)
+    ref = y.clone()
+    tx.reduce_scatter_(y, n)  # in place: recv = send + rank * count
+    tx.all_gather_(y, n)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    s, d = _pattern(n, dt, 3), torch.zeros(n, dtype=dt, device="cuda")
+    tx.all_to_all(s, d)
+    torch.cuda.synchronize()
+    assert torch.equal(d, s)
+    # distinct send / recv buffers are required by the all-to-all
+    from dssm_amd._lib import DssmError
+    with pytest.raises(DssmError):
+        tx.all_to_all(s, s)
+
+
+@pytest.mark.parametrize("sched", [("allreduce", "fp32"), ("zero", "fp32"), ("zero", "bf16")],
+                         ids=lambda s: "/".join(s))
+def test_schedule_selftests_world1(tx, sched):
+    from dssm_amd.dist import SCHEDULE_OPS, selftest
+    assert selftest(tx, SCHEDULE_OPS[sched], torch.device("cuda", 0), 0, 1)
+
+
+def test_collectives_captured_in_graph(tx):
+    """The four collectives captured into one hipGraph on a side stream and replayed twice: each
+    replay re-runs them on the buffers' current contents."""
+    n = 2048
+    a = torch.zeros(n, device="cuda")
+    b = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+    c = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+    out = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        tx.all_reduce(a)
+        tx.reduce_scatter_(b, n)
+        tx.all_gather_(b, n)
+        tx.all_to_all(c, out)
+    for seed in (5, 6):
+        a.copy_(_pattern(n, torch.float32, seed))
+        b.copy_(_pattern(n, torch.bfloat16, seed + 10))
+        c.copy_(_pattern(n, torch.bfloat16, seed + 20))
+        ra, rb, rc = a.clone(), b.clone(), c.clone()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(a, ra) and torch.equal(b, rb) and torch.equal(out, rc)
+
+
+def test_strict_rccl_without_nccl_backend_raises():
+    """comm="rccl" is strict: under a backend other than nccl (here: the module's gloo group, if
+    still initialised, else a fresh one) the library transport is not a candidate and the
+    selection raises instead of falling back silently."""
+    from dssm_amd.dist import SCHEDULE_OPS, select_transport
+    made = False
+    if not dist.is_initialized():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        made = True
+    try:
+        with pytest.raises(RuntimeError):
+            select_transport(0, 1, torch.device("cuda", 0), "rccl", SCHEDULE_OPS[("allreduce", "fp32")])
+    finally:
+        if made:
+            dist.destroy_process_group()
