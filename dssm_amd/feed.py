@@ -15,6 +15,9 @@ Mirrors the reference's pipeline with its names:
   them with ``random.random()`` into a ``set`` (order depends on the string hash seed, SURVEY
   Appendix B.3) and can loop forever; here they come from a seeded PCG64 in draw order, and a
   query with too few eligible docs raises.
+* ``get_data_by_dssm2`` (utils/data_input.py:53-60,121-161): the alternative BoW loader over a
+  fixed character vocabulary (``load_vocab``, ``DataInputConfig``: the attributes it needs from
+  dssm_rnn/config.py), float32 CSR query / doc_pos / doc_neg matrices for ``pull_batch``.
 * ``Feeder``: the step's combined CSR [q; pos; neg] of batch b assembled from the three CSR
   matrices by a native worker thread into pinned memory and copied on its own HIP stream
   (``dssm_feeder_*``), double-buffered so batch b+1's H2D overlaps step b; ``DSSM.set_batch``
@@ -230,6 +233,79 @@ def sample_negatives_reference(query: Sequence[str], doc: Sequence[str], neg: in
                 raise ValueError(f"query {i}: fewer than NEG={neg} eligible negative docs")
         out.extend(picked)
     return out
+
+
+# ---- utils/data_input.py: BoW feeds over a fixed vocabulary (the dssm_rnn configs) -----------
+def load_vocab(file_path: str) -> dict:
+    """dssm_rnn/config.py:5-11: token -> line number of a vocabulary file (data/vocab.txt)."""
+    word_dict = {}
+    with open(file_path, encoding="utf8") as f:
+        for idx, word in enumerate(f.readlines()):
+            word_dict[word.strip()] = idx
+    return word_dict
+
+
+class DataInputConfig:
+    """The attributes utils/data_input.py reads from its config (dssm_rnn/config.py:26-29,51):
+    vocab_map, nwords, unk, pad, max_seq_len."""
+
+    def __init__(self, vocab_path: str = None, vocab_map: dict = None, unk: str = "[UNK]",
+                 pad: str = "[PAD]", max_seq_len: int = 10):
+        if vocab_map is None:
+            vocab_map = load_vocab(vocab_path)
+        self.vocab_map = vocab_map
+        self.nwords = len(vocab_map)
+        self.unk, self.pad, self.max_seq_len = unk, pad, max_seq_len
+
+
+def convert_seq2bow(query: str, conf: DataInputConfig) -> dict:
+    """utils/data_input.py:53-60: character counts over the vocabulary, out-of-vocabulary
+    characters counted at [UNK]; returned sparse ({id: count}) instead of an nwords-long vector."""
+    vm, unk = conf.vocab_map, conf.vocab_map[conf.unk]
+    out = {}
+    for w in query:
+        i = vm.get(w, unk)
+        out[i] = out.get(i, 0) + 1
+    return out
+
+
+def _bow_csr(rows, nwords: int) -> sps.csr_matrix:
+    """float32 CSR of {id: count} rows, column indices ascending (the layout csr_matrix gives the
+    reference's dense rows)."""
+    indptr = np.zeros(len(rows) + 1, np.int32)
+    idx, val = [], []
+    for r, d in enumerate(rows):
+        ks = sorted(d)
+        idx.extend(ks)
+        val.extend(d[k] for k in ks)
+        indptr[r + 1] = len(idx)
+    return sps.csr_matrix((np.asarray(val, np.float32), np.asarray(idx, np.int32), indptr),
+                          shape=(len(rows), nwords))
+
+
+def get_data_by_dssm2(file_path: str, conf: DataInputConfig) -> dict:
+    """utils/data_input.py:121-161: TSV lines ``prefix \t query_prediction (JSON) \t title \t tag
+    \t label``; label '0' lines are skipped; the negatives are the predicted queries other than the
+    title (iteration order of the JSON object), and a line is kept only with at least 4 of them, of
+    which the first 4 are used.  Returns {'query', 'doc_pos', 'doc_neg'}: float32 CSR count matrices
+    over conf.nwords columns, doc_neg rows 4j..4j+3 belonging to query j -- the matrices pull_batch
+    (dssm_amd.data) slices."""
+    q, pos, neg = [], [], []
+    with open(file_path, encoding="utf8") as f:
+        for line in f:
+            spline = line.strip().split("\t")
+            if len(spline) < 4:
+                continue
+            prefix, query_pred, title, tag, label = spline
+            if label == "0":
+                continue
+            cur = [convert_seq2bow(each, conf) for each in json.loads(query_pred) if each != title]
+            if len(cur) >= 4:
+                q.append(convert_seq2bow(prefix, conf))
+                pos.append(convert_seq2bow(title, conf))
+                neg.extend(cur[:4])
+    return {"query": _bow_csr(q, conf.nwords), "doc_pos": _bow_csr(pos, conf.nwords),
+            "doc_neg": _bow_csr(neg, conf.nwords)}
 
 
 class Feeder:

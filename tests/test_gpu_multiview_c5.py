@@ -1,0 +1,70 @@
+"""Multi-view DSSM at BASELINE config 5's size (archive/multi_view_dssm_v3.py:107-241): one user
+tower and three item views, 30k-wide sparse inputs, FC 300 -> 128, BS = 4096, NEG = 4 -- the shape
+`bench.py --model multiview` times -- against the float64 oracle (oracle/multiview_oracle.py,
+scipy CSR inputs) on the same Zipf batches, for active views 1 and 3:
+* loss (summed over the batch, as the reference) rel <= 1e-5; every cosine <= 1e-4 rel + 1e-5;
+* every gradient of the user tower and the active view <= 1e-4 * max|g| (the other views get none);
+* one teacher-forced Adam step (the oracle's TF1.x ApplyAdam on the GPU's gradients): <= 1e-6 on
+  well-conditioned elements (|g| > 1e-3 max|g|), <= 2 lr everywhere, untouched views unchanged."""
+import numpy as np
+import pytest
+import torch
+
+from dssm_amd.data import ZipfColumns, synth_rows
+from dssm_amd.multiview import MultiViewDSSM
+from oracle import multiview_oracle as M
+
+pytestmark = pytest.mark.gpu
+
+CFG = M.MvConfig(user_d=30000, view_d=[30000, 30000, 30000], l1=300, l2=128, bs=4096, neg=4, lr=0.05)
+
+
+def _setup(view):
+    cfg = CFG
+    p = M.init_params(cfg, 5)
+    rot = M.rotations(cfg, 7)
+    m = MultiViewDSSM(cfg.user_d, cfg.view_d, cfg.l1, cfg.l2, cfg.bs, cfg.neg, lr=cfg.lr, rotations=rot)
+    m.load_params(p)
+    rng = np.random.Generator(np.random.PCG64(40 + view))
+    u = synth_rows(rng, ZipfColumns(cfg.user_d), cfg.bs, 32.0)
+    it = synth_rows(rng, ZipfColumns(cfg.view_d[view - 1]), cfg.bs, 32.0)
+    m.set_batch(u, it, view)
+    return cfg, p, rot, m, u, it
+
+
+@pytest.mark.parametrize("view", [1, 3])
+def test_multiview_config5_matches_oracle(view):
+    cfg, p, rot, m, u, it = _setup(view)
+    m.forward()
+    m.backward()
+    torch.cuda.synchronize()
+    fw = M.forward(cfg, p, u, it, view, rot, dtype=np.float64, sparse=True)
+    assert abs(m.loss() - fw["loss"]) <= 1e-5 * abs(fw["loss"]), (m.loss(), fw["loss"])
+    cos = m.cos_raw.cpu().numpy().reshape(cfg.neg + 1, cfg.bs).T
+    np.testing.assert_allclose(cos, fw["cos"], rtol=1e-4, atol=1e-5)
+    g = M.backward(cfg, p, fw)
+    got = m.named(m.grads)
+    errs = {}
+    for k, ref in g.items():
+        errs[k] = float(np.abs(got[k] - ref).max() / np.abs(ref).max())
+    print("config-5 view", view, {k: f"{v:.2e}" for k, v in errs.items()})
+    assert all(v <= 1e-4 for v in errs.values()), errs
+    for k, v in got.items():  # views without a gradient this step
+        if not k.startswith(("user", f"view{view}")):
+            assert not np.any(v), k
+
+    # one teacher-forced Adam step on the GPU's own gradients
+    gg = {k: v for k, v in got.items() if k.startswith(("user", f"view{view}"))}
+    pref = {k: v.copy() for k, v in p.items()}
+    M.Adam(cfg, pref).step(pref, gg)
+    m.apply_adam()
+    torch.cuda.synchronize()
+    after = m.named()
+    for k in pref:
+        d = np.abs(after[k] - pref[k])
+        assert d.max() <= 2 * cfg.lr, (k, d.max())
+        if k in gg:
+            well = np.abs(gg[k]) > 1e-3 * np.abs(gg[k]).max()
+            assert d[well].max(initial=0.0) <= 1e-6, (k, d[well].max(initial=0.0))
+        else:
+            assert d.max() == 0.0, k

@@ -18,33 +18,36 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-CFG = dict(user_d=2000, view_d=[1800, 1900, 2000], l1=64, l2=32, bs=64, neg=4)
+CFGS = {"toy": dict(user_d=2000, view_d=[1800, 1900, 2000], l1=64, l2=32, bs=64, neg=4, nnz=12.0),
+        # BASELINE config 5 per rank (bench.py --model multiview): 30k views, 300 -> 128, BS = 4096
+        "config5": dict(user_d=30000, view_d=[30000, 30000, 30000], l1=300, l2=128, bs=4096, neg=4, nnz=32.0)}
 VIEW = 2
 
 
-def _batch(rank):
+def _batch(cfg, rank):
     from dssm_amd.data import ZipfColumns, synth_rows
     rng = np.random.Generator(np.random.PCG64(100 + rank))
-    u = synth_rows(rng, ZipfColumns(CFG["user_d"]), CFG["bs"], 12.0)
-    it = synth_rows(rng, ZipfColumns(CFG["view_d"][VIEW - 1]), CFG["bs"], 12.0)
+    u = synth_rows(rng, ZipfColumns(cfg["user_d"]), cfg["bs"], cfg["nnz"])
+    it = synth_rows(rng, ZipfColumns(cfg["view_d"][VIEW - 1]), cfg["bs"], cfg["nnz"])
     return u, it
 
 
-def _model():
+def _model(cfg):
     from dssm_amd.multiview import MultiViewDSSM
-    m = MultiViewDSSM(CFG["user_d"], CFG["view_d"], CFG["l1"], CFG["l2"], CFG["bs"], CFG["neg"], lr=0.01,
+    m = MultiViewDSSM(cfg["user_d"], cfg["view_d"], cfg["l1"], cfg["l2"], cfg["bs"], cfg["neg"], lr=0.01,
                       device=torch.device("cuda", 0))
     m.init_params(4)
     return m
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, name):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
     try:
         from dssm_amd.multiview import MultiViewDataParallel
         torch.cuda.set_device(0)
-        m = _model()
-        m.set_batch(*_batch(rank), VIEW)
+        cfg = CFGS[name]
+        m = _model(cfg)
+        m.set_batch(*_batch(cfg, rank), VIEW)
         dp = MultiViewDataParallel(m, comm="auto")
         assert dp.world == 2 and dp.comm == "torch"
         m.forward()
@@ -60,19 +63,21 @@ def _worker(rank, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_multiview_dp_world2_matches_mean_gradient_step():
+@pytest.mark.parametrize("name", list(CFGS))
+def test_multiview_dp_world2_matches_mean_gradient_step(name):
+    cfg = CFGS[name]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(port, d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(port, d, name), nprocs=2, join=True)
         r0, r1 = (np.load(os.path.join(d, f"r{r}.npz")) for r in (0, 1))
         # one process: each batch's gradient, their sum, one Adam step on the mean
-        m = _model()
+        m = _model(cfg)
         gs = []
         for rank in (0, 1):
             m.grads.zero_()
-            m.set_batch(*_batch(rank), VIEW)
+            m.set_batch(*_batch(cfg, rank), VIEW)
             m.forward()
             m.backward()
             torch.cuda.synchronize()
