@@ -55,9 +55,22 @@ def parse():
                     help="N=1 graph mode: one graph holding a step per staged batch (replayed per cycle)")
     ap.add_argument("--probes", type=int, default=1, help="HIP-event kernel probes in the timed region")
     ap.add_argument("--rehearse-world", type=int, default=1,
-                    help="analysis only (N=1): run rank 0's share of a W-rank zero/bf16-wire step "
-                         "(unfused dW1, wire pack, 1/W Adam shard, wire shadows) with the "
-                         "collectives omitted, to time the per-rank compute of the N>1 path")
+                    help="analysis only (N=1): rank 0's share of a W-rank zero/bf16-wire step (the data-"
+                         "parallel step graph, chunked gradient pass / Adam / shadow rebuild) with each "
+                         "collective replaced per --rehearse-comm")
+    ap.add_argument("--rehearse-comm", default="model", choices=["model", "copy"],
+                    help="rehearsal collectives: model = a kernel holding the comm stream for the modelled "
+                         "link time (--link-latency-us + bytes sent / --link-gbps); copy = a device copy of "
+                         "the same bytes")
+    ap.add_argument("--link-gbps", type=float, default=350.0,
+                    help="modelled xGMI egress per GPU for --rehearse-comm model (GB/s)")
+    ap.add_argument("--link-latency-us", type=float, default=10.0,
+                    help="modelled fixed cost per collective for --rehearse-comm model (us)")
+    ap.add_argument("--dp-chunks", type=int, default=1,
+                    help="N>1 bf16 wire: W1's rows exchanged in this many pieces (with --dp-overlap each "
+                         "piece's collectives overlap the next piece's kernels)")
+    ap.add_argument("--dp-overlap", type=int, default=0,
+                    help="N>1 captured step: the collectives on a second captured stream (fork / join edges)")
     ap.add_argument("--model", default="bow", choices=["bow", "rnn", "multiview"],
                     help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4); "
                          "multiview: multi_view_dssm_v3 (config 5)")
@@ -522,20 +535,16 @@ def main():
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
-        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire)
+        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks,
+                          overlap=bool(args.dp_overlap))
     rehearse = args.rehearse_world if world == 1 else 1
     if rehearse > 1:
-        # rank 0's kernels of a W-rank bf16-wire step; the reduce-scatter / all-reduce / all-gather
-        # that would sit between the graphs are left out (analysis of the N>1 compute share)
+        # rank 0's kernels of a W-rank bf16-wire step in the data-parallel step graph, each
+        # collective replaced by a modelled link time or a device copy (analysis of the N>1 path)
         model.set_fused_w1_adam(False)
-        ext = model.wire_extent()
-        shard = -(-ext // (64 * rehearse)) * 64
-        wires = [torch.zeros(shard * rehearse, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        wires[1][:ext].copy_(model.params[:ext])
-        model.set_wire(*wires)
-        stage = torch.zeros(shard * rehearse, dtype=torch.bfloat16, device=dev)  # the all-to-all's output
-        model.set_wire_stage(stage, rehearse, shard)
-        model.set_adam_range(0, min(shard, ext))
+        nw = model.dp_wire_size(rehearse, args.dp_chunks)
+        wires = [torch.zeros(nw, dtype=torch.bfloat16, device=dev) for _ in range(3)]
+        model.set_dp_wire(rehearse, 0, args.dp_chunks, *wires)
 
     cols = ZipfColumns(D, uniform=args.columns == "uniform")
     staged = []
@@ -578,13 +587,45 @@ def main():
             feeder.done()
         torch.cuda.synchronize()
         feeder.start(0)
-        graphs, adam_graph, cycle, region, probe_graph = gslots, None, None, {}, None
+        graphs, adam_graph, cycle, region, probe_graph, split = gslots, None, None, {}, None, False
 
         def run_steps(i0, n):
             for i in range(i0, i0 + n):
                 feeder.next(model, next_batch=(i + 1) % args.batches)
                 model.graph_launch(gslots[feeder._cur])
                 feeder.done()
+    elif args.graph and (rehearse > 1 or (dp is not None and dp.capturable)):
+        # data parallel on the library's RCCL communicator (or its one-GPU rehearsal): the warm-up
+        # and the timed region are each ONE graph of exactly that many whole steps, collectives
+        # included (dssm_plan_graph_build_dp_steps: per step the chunked gradient pass, all-to-all,
+        # Adam, all-gather and shadow rebuild overlapping on two streams; step i+1's rank pass in
+        # step i's Adam); longer runs replay a cycle of len(staged) steps plus a partial one
+        MAX_REGION_STEPS = 256
+        comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2}[args.rehearse_comm]
+
+        def dp_graph(batches, probes=False):
+            if rehearse == 1:
+                return dp.build_region(batches, probes=probes)
+            return model.graph_build_dp_steps(batches, 1.0 / rehearse, comm=comm_mode, link_gbps=args.link_gbps,
+                                              latency_us=args.link_latency_us, overlap=bool(args.dp_overlap),
+                                              probes=probes)
+        graphs, adam_graph, probe_graph, split, partial, cycle, region = None, None, None, True, {}, None, {}
+        for n in {args.warmup, args.steps} - {0}:
+            if n <= MAX_REGION_STEPS:
+                region[n] = dp_graph([staged[i % len(staged)] for i in range(n)], probes=bool(args.probes))
+        if max(args.warmup, args.steps) > MAX_REGION_STEPS:
+            cycle = dp_graph(staged, probes=bool(args.probes))
+            for r in {args.warmup % len(staged), args.steps % len(staged)} - {0}:
+                partial[r] = dp_graph(staged[:r], probes=bool(args.probes))
+
+        def run_steps(i0, n):
+            if n in region:
+                model.graph_launch(region[n])
+                return
+            for _ in range(n // len(staged)):
+                model.graph_launch(cycle)
+            if n % len(staged):
+                model.graph_launch(partial[n % len(staged)])
     elif args.graph and dp is not None:
         # data parallel: per staged batch a captured fwd+bwd graph (and the variant that first
         # rebuilds the shadows from the previous step's all-gathered update), one Adam graph, the
@@ -601,23 +642,12 @@ def main():
         graphs = []
         # Probes (graph event-record nodes cost a few us each) ride in batch 0's graph only, so
         # they are sampled once per len(staged) steps inside the timed region.
-        split = rehearse > 1
-        shadow_part = _lib.GRAPH_WIRE_SHADOWS if rehearse > 1 else 0
-        # rehearsal: per batch the plain fwd+bwd graph (the run's first step) and one that first
-        # refreshes the shadows from the previous step's update (one graph boundary fewer per step)
-        merged = []
+        split, adam_graph = False, None
         for b, (ip, ix, vv) in enumerate(staged):
             model.set_batch(indptr=ip, indices=ix, values=vv)
             # the probes ride in the graph of the timed region's first step (batch W mod len(staged))
-            pr = bool(args.probes) and b == args.warmup % len(staged) and (rehearse > 1 or not args.multi_step)
-            if split:
-                graphs.append(model.graph_build(_lib.GRAPH_FWD_BWD, probes=pr))
-                merged.append(model.graph_build(_lib.GRAPH_FWD_BWD | shadow_part, probes=pr))
-            else:
-                graphs.append(model.graph_build(probes=pr))
-        adam_graph = (model.graph_build(_lib.GRAPH_ADAM, 1.0 / rehearse, probes=bool(args.probes))
-                      if split else None)
-        shadow_graph = model.graph_build(shadow_part) if shadow_part else None
+            pr = bool(args.probes) and b == args.warmup % len(staged) and not args.multi_step
+            graphs.append(model.graph_build(probes=pr))
 
         # single GPU: a run of up to MAX_REGION_STEPS steps (the warm-up, the timed region) is ONE
         # multi-step graph of exactly that many steps over the batches in order (one launch, one
@@ -654,10 +684,7 @@ def main():
                 model.graph_launch(partial[n % len(staged)])
 
         def step(i):
-            # steps after the first start with the previous step's shadow refresh (merged graph)
-            model.graph_launch((merged if merged and i > 0 else graphs)[i % len(graphs)])
-            if split:
-                model.graph_launch(adam_graph)
+            model.graph_launch(graphs[i % len(graphs)])
     else:
         def step(i):
             ip, ix, vv = staged[i % len(staged)]
@@ -695,9 +722,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dp is not None and args.graph:
-        dp.settle()  # untimed: the last step's shadow refresh
-    elif args.graph and feeder is None and split and shadow_graph is not None:
-        model.graph_launch(shadow_graph)  # untimed: the last step's shadow refresh
+        dp.settle()  # untimed: a last split-graph step's shadow refresh (none after a captured region)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -711,6 +736,12 @@ def main():
         model.graph_launch(probe_graph)  # untimed: the secondary probes' replay
         torch.cuda.synchronize()
     for name, pid in (probe_ids if args.probes else ()):
+        if args.graph and split and region is not None and (rehearse > 1 or dp.capturable):
+            if name == "adam":  # the data-parallel region: its last step's Adam chunks
+                g = region[args.steps] if args.steps in region else (
+                    cycle if args.steps % len(staged) == 0 else partial[args.steps % len(staged)])
+                probes[name] = model.graph_probe_read(g, pid)
+            continue
         if args.graph and dp is not None:  # the timed region's first step's graphs, the Adam graph
             plain, merged_g, adam_g = dp.graph_ids()
             g = adam_g if name == "adam" else (merged_g if merged_g and args.warmup > 0 else plain)[
@@ -718,11 +749,9 @@ def main():
             probes[name] = model.graph_probe_read(g, pid)
             continue
         if args.graph:  # last replay of every staged-batch graph, all inside the timed region
-            g = adam_graph if (name == "adam" and adam_graph is not None) else (
-                (region[args.steps] if name == "adam" else probe_graph) if args.steps in region else
-                (cycle if args.steps >= len(staged) else partial[args.steps]) if cycle is not None else
-                (graphs[0] if feeder is not None else
-                 (merged if split and merged and args.warmup > 0 else graphs)[args.warmup % len(graphs)]))
+            g = ((region[args.steps] if name == "adam" else probe_graph) if args.steps in region else
+                 (cycle if args.steps >= len(staged) else partial[args.steps]) if cycle is not None else
+                 (graphs[0] if feeder is not None else graphs[args.warmup % len(graphs)]))
             probes[name] = model.graph_probe_read(g, pid)
         else:
             tot, cnt = model.probe_read(pid)
@@ -747,9 +776,9 @@ def main():
         else:
             range_elems = max(0, dp.end - dp.begin)
     elif rehearse > 1:
-        ext = D * WIDTHS[0]
-        wire_elems = min(-(-ext // (64 * rehearse)) * 64, ext)
-        range_elems = wire_elems + (n_params - ext)
+        geo = model.dp_geometry()
+        wire_elems = geo["shard_end"] - geo["shard_begin"]
+        range_elems = wire_elems + (n_params - geo["extent"])
         wire_parts = rehearse
     kern = {
         "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
@@ -796,8 +825,16 @@ def main():
     if fwd is not None:
         out["fwd_only"] = fwd
     if rehearse > 1:
-        out["rehearsal"] = {"world": rehearse, "collectives": "omitted",
-                            "note": "rank 0's compute share of an N-rank bf16-wire step; not a headline number"}
+        out["rehearsal"] = {"world": rehearse, "chunks": args.dp_chunks, "overlap": bool(args.dp_overlap),
+                            "collectives": ({"model": f"modelled: {args.link_latency_us} us + bytes sent / "
+                                                      f"{args.link_gbps} GB/s per collective",
+                                             "copy": "device copies of the same bytes"}[args.rehearse_comm]),
+                            "note": "rank 0 of an N-rank bf16-wire step on one GPU; not a headline number"}
+    if dp is not None:
+        out["config"]["dp_chunks"] = dp.chunks
+        out["config"]["dp_overlap"] = dp.overlap
+        out["config"]["dp_launch"] = ("one graph per region, collectives captured" if dp.capturable and args.graph
+                                      else "split graphs, host-issued collectives" if args.graph else "eager")
     if (args.fp32_line and rank == 0 and world == 1 and rehearse == 1 and args.dtype == "bf16"
             and feeder is None and args.columns == "zipf"):
         out["fp32_mode"] = fp32_mode_line(args)

@@ -86,9 +86,13 @@ _SIGS = {
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
     "dssm_plan_wire_extent": (C.c_int64, [_P]),
-    "dssm_plan_set_wire": (C.c_int, [_P, _P, _P, C.c_int64]),
+    "dssm_plan_dp_wire_size": (C.c_int64, [_P, C.c_int, C.c_int]),
+    "dssm_plan_set_dp_wire": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int64]),
+    "dssm_plan_dp_geometry": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "dssm_plan_wire_shadows": (C.c_int, [_P, _P]),
-    "dssm_plan_set_wire_stage": (C.c_int, [_P, _P, C.c_int, C.c_int64]),
+    "dssm_plan_graph_build_dp_steps": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.c_int,
+                                                 C.c_float, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, _P,
+                                                 C.POINTER(C.c_int)]),
     "dssm_plan_probe_enable": (C.c_int, [_P, C.c_int, C.c_int]),
     "dssm_plan_probe_read": (C.c_int, [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
     "dssm_spmm_csr_fwd": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P,

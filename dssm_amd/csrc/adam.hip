@@ -118,6 +118,24 @@ struct RowEntries {
   int i;
   float v;
 };
+
+// gradient pass by wire chunks (a.wchunk >= 0): is row c (c == D: b1's row, last chunk) in it
+__device__ __forceinline__ bool in_chunk(const AdamStep& a, int c) {
+  if (a.wchunk < 0) return true;
+  if (c >= a.D) return a.wchunk == a.geo.wp - 1;
+  return (c / a.geo.ws) % a.geo.wp == a.wchunk;
+}
+// the W1-row role's v-th row: every row [0, D] (wchunk < 0) or the chunk's rows, b1's row last
+// (-1: a slot past W1's rows)
+__device__ __forceinline__ int w1_role_rows(const AdamStep& a) {
+  return a.wchunk < 0 ? a.D + 1 : a.geo.ww * a.geo.ws + 1;
+}
+__device__ __forceinline__ int w1_role_row(const AdamStep& a, int v) {
+  if (a.wchunk < 0) return v;
+  const int nv = a.geo.ww * a.geo.ws;
+  if (v == nv) return a.wchunk == a.geo.wp - 1 ? a.D : -1;
+  return wire_chunk_row(a.geo, a.wchunk, v, a.D);
+}
 __device__ __forceinline__ RowEntries row_entries(const AdamStep& a, int s, int e) {
   RowEntries r{0, 0.f};
   const int lane = lane_id();
@@ -169,15 +187,16 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     if (nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
       const int k = nvalid >= 8 ? 8 : 4;
       if (c < a.D) {
+        u16* q = a.gout + wire_row_off(a.geo, c) + cc;
         uint2 lo;
         lo.x = pack2bf(G[0], G[1]);
         lo.y = pack2bf(G[2], G[3]);
-        *reinterpret_cast<uint2*>(a.gout + o) = lo;
+        *reinterpret_cast<uint2*>(q) = lo;
         if (k == 8) {
           uint2 hi;
           hi.x = pack2bf(G[4], G[5]);
           hi.y = pack2bf(G[6], G[7]);
-          *reinterpret_cast<uint2*>(a.gout + o + 4) = hi;
+          *reinterpret_cast<uint2*>(q + 4) = hi;
         }
       } else {
         *reinterpret_cast<float4*>(a.g + o) = make_float4(G[0], G[1], G[2], G[3]);
@@ -216,10 +235,10 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
 // Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
 __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
   if (a.gout) {  // gradient pass
+    const int64_t wo = c < a.D ? wire_row_off(a.geo, c) : 0;
     for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
-      const size_t o = (size_t)c * a.n + j;
-      if (c < a.D) a.gout[o] = f2bf(grow[j]);
-      else a.g[o] = grow[j];
+      if (c < a.D) a.gout[wo + j] = f2bf(grow[j]);
+      else a.g[(size_t)c * a.n + j] = grow[j];
     }
     return;
   }
@@ -260,6 +279,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
   for (int it = hb; it < nitems; it += a.item_blocks) {
     const int2 item = a.heavy_items[it];
     const int c = item.x;
+    if (!in_chunk(a, c)) continue;  // uniform over the workgroup
     const int cs = a.col_ptr[c], ce = a.col_ptr[c + 1];
     const int i0 = cs + item.y * kHeavyItem;
     const int s = min(ce, i0 + wv * (kHeavyItem / 4)), e = min(ce, s + kHeavyItem / 4);
@@ -360,45 +380,45 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
     const int b = DSSM_ADAM_ORDER == 0 ? b0 - nh : b0 - nh - nd;
     // the next row's column range is loaded while this row is processed (one dependent load
     // fewer on each row's chain)
+    // rows by slot v (wave-uniform: scalar row state); every row, or one wire chunk's rows
     const int stride = a.w1_blocks * 4;
-    int c = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar row state
-    int s = 0, e = 0;
-    if (c <= a.D) {
-      s = a.col_ptr[c];
-      e = a.col_ptr[c + 1];
-    }
+    const int nv = w1_role_rows(a);
+    int v = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto range = [&](int vv, int& rs, int& re) {
+      const int c = vv < nv ? w1_role_row(a, vv) : -1;
+      rs = re = 0;
+      if (c >= 0) {
+        rs = a.col_ptr[c];
+        re = a.col_ptr[c + 1];
+      }
+      return c;
+    };
+    int s, e;
+    int c = range(v, s, e);
 #if DSSM_ADAM_PRE_IDX
     // two rows ahead: the column range; one row ahead: the light row's CSC entries
-    int sn = 0, en = 0;
-    if (c + stride <= a.D) {
-      sn = a.col_ptr[c + stride];
-      en = a.col_ptr[c + stride + 1];
-    }
+    int sn, en;
+    int cn = range(v + stride, sn, en);
     RowEntries ent = row_entries(a, s, e);
-    for (; c <= a.D; c += stride) {
-      const int c2 = c + 2 * stride;
-      int s2 = 0, e2 = 0;
-      if (c2 <= a.D) {
-        s2 = a.col_ptr[c2];
-        e2 = a.col_ptr[c2 + 1];
-      }
+    for (; v < nv; v += stride) {
+      int s2, e2;
+      const int c2 = range(v + 2 * stride, s2, e2);
       const RowEntries next = row_entries(a, sn, en);
-      w1_row<TZ>(a, c, s, e, alpha, &ent);
+      if (c >= 0) w1_row<TZ>(a, c, s, e, alpha, &ent);
+      c = cn;
       s = sn;
       e = en;
+      cn = c2;
       sn = s2;
       en = e2;
       ent = next;
     }
 #else
-    for (; c <= a.D; c += stride) {
-      const int cn = c + stride;
-      int sn = 0, en = 0;
-      if (cn <= a.D) {
-        sn = a.col_ptr[cn];
-        en = a.col_ptr[cn + 1];
-      }
-      w1_row<TZ>(a, c, s, e, alpha);
+    for (; v < nv; v += stride) {
+      int sn, en;
+      const int cn = range(v + stride, sn, en);
+      if (c >= 0) w1_row<TZ>(a, c, s, e, alpha);
+      c = cn;
       s = sn;
       e = en;
     }
@@ -406,12 +426,15 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   } else {
     const int bi = DSSM_ADAM_ORDER == 0 ? b0 - nh - nw : b0 - nh;
     if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
-      const int64_t w4 = (int64_t)(a.D + 1) * a.n / 4;
+      const int nv = w1_role_rows(a) - 1;  // W1 rows only (b1's row is never untouched)
+      const int q = a.n / 4;
+      const int64_t w4 = (int64_t)nv * q;
       for (int64_t i = (int64_t)bi * blockDim.x + threadIdx.x; i < w4;
            i += (int64_t)a.dense_blocks * blockDim.x) {
-        const int c = (int)((i * 4) / a.n);
-        if (a.col_ptr[c + 1] != a.col_ptr[c]) continue;
-        if (c < a.D) reinterpret_cast<uint2*>(a.gout)[i] = make_uint2(0u, 0u);
+        const int vr = (int)(i / q);
+        const int c = w1_role_row(a, vr);
+        if (c < 0 || c >= a.D || a.col_ptr[c + 1] != a.col_ptr[c]) continue;
+        reinterpret_cast<uint2*>(a.gout + wire_row_off(a.geo, c))[i - (int64_t)vr * q] = make_uint2(0u, 0u);
       }
     } else if (a.w1_flat) {
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
@@ -459,7 +482,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
         uint2 q;
         q.x = pack2bf(pp.x, pp.y);
         q.y = pack2bf(pp.z, pp.w);
-        reinterpret_cast<uint2*>(a.pwire)[i] = q;
+        reinterpret_cast<uint2*>(a.pwire)[i + a.pwire_off4] = q;
       } else if (a.sh.count) {
         write_shadow4(a.sh, i * 4, pp);
       }
@@ -514,30 +537,45 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
   }
 }
 
+// the wire's W1 rows from the materialised fp32 gradient (one 4-element group per thread)
 __global__ __launch_bounds__(256) void k_wire_pack(const float* __restrict__ g, u16* __restrict__ w,
-                                                   int64_t n4) {
+                                                   int D, WireGeo geo) {
+  const int q = geo.n / 4;
+  const int64_t n4 = (int64_t)D * q;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / q);
     const float4 v = reinterpret_cast<const float4*>(g)[i];
-    uint2 q;
-    q.x = pack2bf(v.x, v.y);
-    q.y = pack2bf(v.z, v.w);
-    reinterpret_cast<uint2*>(w)[i] = q;
+    uint2 o;
+    o.x = pack2bf(v.x, v.y);
+    o.y = pack2bf(v.z, v.w);
+    reinterpret_cast<uint2*>(w + wire_row_off(geo, r))[i - (int64_t)r * q] = o;
   }
 }
 
-// W1 shadow rows [rows x ld] from the bf16 parameter wire (rows of g.cols, at g.offset): one
-// 4-element group per thread (cols % 4 == 0, so a group never straddles two rows)
-__global__ __launch_bounds__(256) void k_wire_shadow(const u16* __restrict__ w, ShadowSeg g) {
-  const int64_t n4 = g.rows * g.cols / 4;
+// W1 shadow rows [rows x ld] from the bf16 parameter wire (row length g.cols == geo.n; W1 at
+// arena offset 0): every row, or one chunk's rows; one 4-element group per thread
+__global__ __launch_bounds__(256) void k_wire_shadow(const u16* __restrict__ w, ShadowSeg g, WireGeo geo,
+                                                     int chunk) {
+  const int q = g.cols / 4;
+  const int nrows = chunk < 0 ? (int)g.rows : geo.ww * geo.ws;
+  const int64_t n4 = (int64_t)nrows * q;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t rel = i * 4;
-    const int64_t r = rel / g.cols;
-    const int c = (int)(rel - r * g.cols);
-    *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) =
-        *reinterpret_cast<const uint2*>(w + g.offset + rel);
+    const int v = (int)(i / q);
+    const int r = chunk < 0 ? v : wire_chunk_row(geo, chunk, v, (int)g.rows);
+    if (r < 0) continue;
+    const int c = (int)(i - (int64_t)v * q) * 4;
+    *reinterpret_cast<uint2*>(g.ptr + (int64_t)r * g.ld + c) =
+        *reinterpret_cast<const uint2*>(w + wire_row_off(geo, r) + c);
   }
+}
+
+// the data-parallel rehearsal's modelled collective: one wave holds the stream for `ticks` of the
+// 100 MHz real-time counter
+__global__ void k_spin(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
 }
 
 int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -554,16 +592,18 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   a.b1c = 1.0f - a.beta1;
   a.b2c = 1.0f - a.beta2;
   // 2048 W1-row gather blocks: measured against 1024 / 4096 (+2-4 us each)
-  if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(a.D + 1, 4), kAdamW1Blocks);
-  if (a.gout) a.ticket = nullptr;  // the gradient pass advances nothing
-  if (!a.ticket && !a.gout) return hipErrorInvalidValue;  // the step must advance the beta powers
+  const int w1_rows = a.wchunk < 0 ? a.D + 1 : a.geo.ww * a.geo.ws + 1;
+  if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(w1_rows, 4), kAdamW1Blocks);
+  if (a.gout || a.no_advance) a.ticket = nullptr;  // the gradient pass / a non-final chunk advance nothing
+  if (!a.ticket && !a.gout && !a.no_advance) return hipErrorInvalidValue;  // a step advances the beta powers
+  if (a.wchunk >= 0 && (!a.gout || !a.geo.ww || a.wchunk >= a.geo.wp)) return hipErrorInvalidValue;
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, kAdamItemBlocks);
   // rows with no entry this step stream through the flat role instead of a wave per row
   a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && (a.n % 4) == 0) ? 1 : 0;
   if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
-  const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) +
-                     (a.w1_flat ? (int64_t)(a.D + 1) * a.n / 4 : 0);
+  const int64_t flat_rows = a.wchunk < 0 ? (int64_t)a.D + 1 : (int64_t)a.geo.ww * a.geo.ws;
+  const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + (a.w1_flat ? flat_rows * a.n / 4 : 0);
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
@@ -574,16 +614,23 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_wire_pack(const float* g, uint16_t* wire, int64_t n, hipStream_t s) {
-  if (n % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_wire_pack, dim3(grid_for(n / 4)), dim3(256), 0, s, g, wire, n / 4);
+hipError_t launch_wire_pack(const float* g, uint16_t* wire, int D, WireGeo geo, hipStream_t s) {
+  if (geo.n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wire_pack, dim3(grid_for((int64_t)D * geo.n / 4)), dim3(256), 0, s, g, wire, D, geo);
   return hipGetLastError();
 }
 
-hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s) {
-  if (seg.cols % 4) return hipErrorInvalidValue;
-  const int64_t n4 = seg.rows * seg.cols / 4;
-  hipLaunchKernelGGL(k_wire_shadow, dim3(grid_for(n4)), dim3(256), 0, s, wire, seg);
+hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, WireGeo geo, int chunk, hipStream_t s) {
+  if (seg.cols % 4 || seg.cols != geo.n || (chunk >= 0 && (!geo.ww || chunk >= geo.wp)))
+    return hipErrorInvalidValue;
+  const int64_t rows = chunk < 0 ? seg.rows : (int64_t)geo.ww * geo.ws;
+  hipLaunchKernelGGL(k_wire_shadow, dim3(grid_for(rows * seg.cols / 4)), dim3(256), 0, s, wire, seg, geo, chunk);
+  return hipGetLastError();
+}
+
+hipError_t launch_spin(double ns, hipStream_t s) {
+  const unsigned long long ticks = ns > 0 ? (unsigned long long)(ns / 10.0 + 0.5) : 0ull;
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks);
   return hipGetLastError();
 }
 

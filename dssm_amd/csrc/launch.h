@@ -218,6 +218,26 @@ struct SlabList {
   int count;
   SlabSeg seg[8];
 };
+// Data-parallel wire layout (dssm_plan_set_dp_wire): W1's rows [0, D) in sub-chunks of s rows;
+// rank j's optimizer shard is rows [j*chunks*s, (j+1)*chunks*s) and its sub-chunk p holds rows
+// (j*chunks + p)*s + [0, s).  The wire stores sub-chunk (p, j) at ((p*world + j)*s)*n, so the
+// collectives of chunk p (all-to-all of the gradient, all-gather of the parameters) each move one
+// contiguous block of world * s * n elements.  chunks == 1: the wire is the arena's own layout.
+struct WireGeo {
+  int ww, wp, ws;  // world, chunks, rows per sub-chunk (ww == 0: identity)
+  int n;           // row length (W1's width)
+};
+__host__ __device__ inline int64_t wire_row_off(const WireGeo& g, int row) {
+  if (!g.ww) return (int64_t)row * g.n;
+  const int j = row / (g.ws * g.wp), p = (row / g.ws) % g.wp, s = row % g.ws;
+  return ((int64_t)(p * g.ww + j) * g.ws + s) * g.n;
+}
+// row of chunk `chunk`'s v-th row slot (v < ww * ws), -1 past W1's rows
+__host__ __device__ inline int wire_chunk_row(const WireGeo& g, int chunk, int v, int D) {
+  const int c = ((v / g.ws) * g.wp + chunk) * g.ws + v % g.ws;
+  return c < D ? c : -1;
+}
+
 struct AdamStep {
   float* p;
   float* g;
@@ -250,7 +270,7 @@ struct AdamStep {
   const int* heavy_n;
   const int2* heavy_items;
   unsigned* heavy_ticket;
-  // data-parallel bf16 wire (dssm_plan_set_wire): float4 index i < wire4 takes its gradient from
+  // data-parallel bf16 wire (dssm_plan_set_dp_wire): float4 index i < wire4 takes its gradient from
   // the reduce-scattered bf16 gradient wire and writes bf16(p) to the parameter wire (the
   // all-gather's input) instead of the shadows; a second dense range [t4_begin, t4_end) (the
   // replicated fp32 tail) follows [d4_begin, d4_end)
@@ -272,18 +292,26 @@ struct AdamStep {
   CscRankRole rank;
   int* heavy_reset;
   // gradient pass (data parallel, bf16 wire): the W1 roles compute dW1 rows (inline gather, heavy
-  // items, zero for untouched rows) and write them as bf16 to gout (arena layout; the bias row as
-  // fp32 into g) instead of updating parameters; no dense range, no beta-power advance
+  // items, zero for untouched rows) and write them as bf16 to gout (wire layout below; the bias row
+  // as fp32 into g) instead of updating parameters; no dense range, no beta-power advance
   uint16_t* gout;
+  // chunked wire geometry (WireGeo; ww == 0: the wire is laid out as the arena)
+  WireGeo geo;
+  int wchunk = -1;     // gradient pass: only the rows of this chunk (-1: every row)
+  int64_t pwire_off4;  // the dense range's parameter-wire float4 index = i + pwire_off4
+  int no_advance;      // a chunk of a chunked Adam step other than the last: no beta-power advance
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 // a timing probe's event (plan.hip): hipEventRecord, or an event-record node while s is capturing
 void record_probe_event(hipStream_t s, hipEvent_t e);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
-// bf16 wire helpers (data parallel): wire[i] = bf16(g[i]) for i < n (n % 4 == 0); the W1 shadow
-// rows from the all-gathered bf16 parameter wire (row length cols, shadow stride ld)
-hipError_t launch_wire_pack(const float* g, uint16_t* wire, int64_t n, hipStream_t s);
-hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s);
+// bf16 wire helpers (data parallel): the wire's W1 rows = bf16(g) (rows [0, D) of row length
+// geo.n); the W1 shadow rows from the all-gathered bf16 parameter wire (chunk: that chunk's rows
+// only, -1: all)
+hipError_t launch_wire_pack(const float* g, uint16_t* wire, int D, WireGeo geo, hipStream_t s);
+hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, WireGeo geo, int chunk, hipStream_t s);
+// one workgroup spinning for `ns` nanoseconds (the data-parallel rehearsal's modelled collective)
+hipError_t launch_spin(double ns, hipStream_t s);
 
 }  // namespace dssm

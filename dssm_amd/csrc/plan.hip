@@ -3,10 +3,12 @@
 // behind the Python add_layer / batch_normalization / cosine API, and the RCCL communicator.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -191,16 +193,27 @@ struct dssm_plan {
   const float* values = nullptr;
   bool fwd_train_done = false;
   int64_t adam_begin = 0, adam_end = -1;  // sharded optimizer range (dssm_plan_set_adam_range)
-  // data-parallel bf16 wire (dssm_plan_set_wire): W1 gradient / parameter copies exchanged by
-  // the reduce-scatter / all-gather; arena elements [0, wire_end) are W1's rows
+  // data-parallel bf16 wire (dssm_plan_set_dp_wire, layout dssm::WireGeo): the gradient pass
+  // writes every rank's W1 rows into gwire, the all-to-all delivers this rank's shard from every
+  // rank into gstage (summed in fp32, rank order, by the Adam launch), Adam writes bf16(W1) of the
+  // shard into pwire, which the all-gather completes; arena elements [0, wire_end) are W1's rows
   uint16_t* gwire = nullptr;
   uint16_t* pwire = nullptr;
-  // all-to-all wire (dssm_plan_set_wire_stage): the rank's W1 shard gradient as gparts bf16
-  // partial copies (one per rank) gstride apart, summed in fp32 by the Adam launch
   const uint16_t* gstage = nullptr;
-  int gparts = 0;
-  int64_t gstride = 0;
+  dssm::WireGeo geo{};
+  int dp_rank = 0;
+  bool dp_defer_gradpass = false;  // the data-parallel graph builder launches the chunks itself
+  // the data-parallel graph builder's hook around each Adam chunk launch (stream waits / event
+  // records while capturing): (chunk, after)
+  std::function<int(int, bool)> dp_hook;
+  hipStream_t comm_stream = nullptr;  // the data-parallel graphs' collective stream
   int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
+  int64_t sub_elems() const { return (int64_t)geo.ws * geo.n; }
+  // rows [r0, r1) of this rank's sub-chunk p (r1 <= r0: none past W1's rows)
+  void dp_chunk_rows(int p, int& r0, int& r1) const {
+    r0 = std::min((dp_rank * geo.wp + p) * geo.ws, Lt.D);
+    r1 = std::min(r0 + geo.ws, Lt.D);
+  }
   bool fwd_fused = false;  // the last train forward ran the fused-statistics schedule
   bool loss_pending = false;  // its loss partials await the backward's first launch
   bool grads_clean = true;     // atomic-target gradient blocks are zero (Adam clears them)
@@ -233,6 +246,7 @@ struct dssm_plan {
     hipEvent_t ev[DSSM_PROBE_COUNT][2] = {};
     bool probes = false;
     unsigned probe_mask = ~0u;  // while capturing: which probe ids record event nodes
+    std::vector<hipEvent_t> xev;  // fork / join events of a multi-stream capture
   };
   std::vector<GraphSlot*> graphs;
   GraphSlot* capturing = nullptr;
@@ -471,8 +485,10 @@ int dssm_plan_destroy(dssm_plan* plan) {
       for (auto& pr : g->ev)
         for (hipEvent_t e : pr)
           if (e) hipEventDestroy(e);
+      for (hipEvent_t e : g->xev) hipEventDestroy(e);
       delete g;
     }
+    if (plan->comm_stream) hipStreamDestroy(plan->comm_stream);
   }
   delete plan;
   return DSSM_OK;
@@ -712,7 +728,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
 }
 
 static bool wire_gradient_pass(const dssm_plan* P);
-static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s);
+static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s, int chunk);
 
 // dW1 = X^T dZ1 from the batch's CSC transpose: heavy columns here, light columns either here
 // (unfused) or inside the Adam step (fused).
@@ -726,7 +742,9 @@ static int dw1_backward(dssm_plan* P, hipStream_t s) {
     return DSSM_OK;
   }
   if (wire_gradient_pass(P)) {
-    if (int rc = launch_wire_gradient_pass(P, s)) return rc;
+    if (!P->dp_defer_gradpass)
+      for (int c = 0; c < P->geo.wp; ++c)
+        if (int rc = launch_wire_gradient_pass(P, s, c)) return rc;
     P->probe_end(DSSM_PROBE_DW1, s);
     return DSSM_OK;
   }
@@ -744,7 +762,7 @@ static int backward_impl(dssm_plan* P, void* stream);
 int dssm_plan_backward(dssm_plan* P, void* stream) {
   if (int rc = backward_impl(P, stream)) return rc;
   if (P->gwire && !wire_gradient_pass(P))  // data parallel: the W1 gradient rows leave as bf16
-    HIP_TRY(dssm::launch_wire_pack(P->g, P->gwire, P->wire_end(), (hipStream_t)stream));
+    HIP_TRY(dssm::launch_wire_pack(P->g, P->gwire, P->Lt.D, P->geo, (hipStream_t)stream));
   return DSSM_OK;
 }
 
@@ -861,7 +879,7 @@ static bool wire_gradient_pass(const dssm_plan* P) {
   return P->gwire && !P->fused_w1_adam() && P->heavy_in_adam() && P->on(DSSM_OPT_WIRE_GRAD_PASS);
 }
 
-static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s) {
+static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s, int chunk) {
   dssm::AdamStep a{};
   a.p = P->p;
   a.g = P->g;
@@ -877,6 +895,36 @@ static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s) {
   fill_w1_roles(P, a);
   a.shadow = nullptr;
   a.gout = P->gwire;
+  a.geo = P->geo;
+  a.wchunk = P->geo.wp > 1 ? chunk : -1;
+  HIP_TRY(dssm::launch_adam_step(a, P->Lt.bf16, s));
+  return DSSM_OK;
+}
+
+// One launch of the data-parallel Adam step: this rank's W1 sub-chunk c (its gradient the fp32
+// sum of the world's bf16 partials in the stage, its bf16 parameters into the wire); the last
+// chunk also updates the replicated tail, hosts any rank role and advances the beta powers.
+static int dp_adam_chunk(dssm_plan* P, const dssm::AdamStep& base, int c, hipStream_t s) {
+  dssm::AdamStep a = base;
+  const bool last = c == P->geo.wp - 1;
+  int r0, r1;
+  P->dp_chunk_rows(c, r0, r1);
+  const int n = P->geo.n;
+  a.d4_begin = (int64_t)r0 * n / 4;
+  a.d4_end = (int64_t)std::max(r0, r1) * n / 4;
+  const int64_t sub = P->sub_elems();
+  a.gstage = P->gstage + (int64_t)c * P->geo.ww * sub;
+  a.gbase4 = a.d4_begin;
+  a.pwire_off4 = ((int64_t)c * P->geo.ww + P->dp_rank) * sub / 4 - a.d4_begin;
+  if (!last) {
+    a.t4_begin = a.t4_end = 0;
+    a.no_advance = 1;
+    a.clear_from = P->Lt.total;
+    a.sh.count = 0;
+    a.slabs.count = 0;
+    a.rank = dssm::CscRankRole{};
+    a.heavy_reset = nullptr;
+  }
   HIP_TRY(dssm::launch_adam_step(a, P->Lt.bf16, s));
   return DSSM_OK;
 }
@@ -906,27 +954,20 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   a.d4_end = (P->adam_end >= 0 ? P->adam_end : Lt.total) / 4;
   if (P->fused_w1_adam() && (P->adam_begin != 0 || (P->adam_end >= 0 && P->adam_end != Lt.total)))
     return fail(DSSM_E_INVALID, "a sharded Adam range needs the fused W1 Adam off");
+  if (P->pwire && P->fused_w1_adam()) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
   if (P->pwire) {
-    // bf16 wire: the rank's W1 shard from the reduce-scattered wire (writing the parameter wire),
-    // then the replicated fp32 tail [wire_end, total) with its shadows
-    if (P->fused_w1_adam()) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
+    // bf16 wire: the rank's W1 shard, sub-chunk by sub-chunk, from the all-to-all's stage (writing
+    // the parameter wire); the last launch also takes the replicated fp32 tail [wire_end, total)
+    // with its shadows and advances the beta powers
     const int64_t we = P->wire_end();
-    a.d4_begin = std::min(P->adam_begin, we) / 4;
-    a.d4_end = std::min(P->adam_end >= 0 ? P->adam_end : we, we) / 4;
-    if (a.d4_end < a.d4_begin) a.d4_end = a.d4_begin;
     a.t4_begin = we / 4;
     a.t4_end = Lt.total / 4;
     a.gwire = P->gwire;
     a.pwire = P->pwire;
     a.wire4 = we / 4;
-    if (P->gstage) {
-      if (P->gstride < P->adam_end - P->adam_begin)
-        return fail(DSSM_E_INVALID, "wire stage stride shorter than the Adam range");
-      a.gstage = P->gstage;
-      a.gparts = P->gparts;
-      a.gstride = P->gstride;
-      a.gbase4 = P->adam_begin / 4;
-    }
+    a.gstage = P->gstage;
+    a.gparts = P->geo.ww;
+    a.gstride = P->sub_elems();
     // the tail's gradient is consumed here; clear it (b1's row is the gradient pass's atomic target)
     if (wire_gradient_pass(P)) a.clear_from = we;
     for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
@@ -941,13 +982,16 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
       sh.count -= 1;
     }
   }
-  // the next step's rank pass as this launch's first workgroups (multi-step graphs)
-  if (P->host_rank_indptr && P->fused_w1_adam() && a.heavy_n && P->merged_csc() &&
+  // the next step's rank pass as workgroups of this step's (last) launch (multi-step graphs); the
+  // heavy-item count it re-arms was consumed by this launch's W1 roles (fused) or the backward's
+  // gradient pass (data parallel)
+  int* heavy_n = P->heavy_in_adam() ? dssm::csc_heavy_count(P->at<int>(Lt.csc_scratch), Lt.D, Lt.max_nnz) : nullptr;
+  if (P->host_rank_indptr && (P->fused_w1_adam() || wire_gradient_pass(P)) && heavy_n && P->merged_csc() &&
       Lt.D <= dssm::kRankMaxD) {
     a.rank = dssm::csc_rank_role_args(P->host_rank_indptr, P->host_rank_indices, Lt.R, Lt.D,
                                       P->at<int>(Lt.csc_scratch), P->at<double>(Lt.sums),
                                       (int)(Lt.sums_bytes / 8));
-    a.heavy_reset = const_cast<int*>(a.heavy_n);
+    a.heavy_reset = heavy_n;
     P->rank_done_for = P->host_rank_indptr;
   }
   P->host_rank_indptr = nullptr;
@@ -962,7 +1006,17 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     }
   a.sh = sh;
   P->probe_begin(DSSM_PROBE_ADAM, s);
-  HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
+  if (P->pwire) {
+    for (int c = 0; c < P->geo.wp; ++c) {
+      if (P->dp_hook)
+        if (int rc = P->dp_hook(c, false)) return rc;
+      if (int rc = dp_adam_chunk(P, a, c, s)) return rc;
+      if (P->dp_hook)
+        if (int rc = P->dp_hook(c, true)) return rc;
+    }
+  } else {
+    HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
+  }
   P->probe_end(DSSM_PROBE_ADAM, s);
   P->grads_clean = true;
   return DSSM_OK;
@@ -981,44 +1035,73 @@ int dssm_plan_set_adam_range(dssm_plan* P, int64_t begin, int64_t end) {
 
 int64_t dssm_plan_wire_extent(const dssm_plan* P) { return P ? P->wire_end() : -1; }
 
-int dssm_plan_set_wire(dssm_plan* P, uint16_t* grad_wire, uint16_t* param_wire, int64_t count) {
+static dssm::WireGeo dp_geo(const dssm_plan* P, int world, int chunks) {
+  dssm::WireGeo g{};
+  g.ww = world;
+  g.wp = chunks;
+  g.ws = (P->Lt.D + world * chunks - 1) / (world * chunks);
+  g.n = P->Lt.n[0];
+  return g;
+}
+
+int64_t dssm_plan_dp_wire_size(const dssm_plan* P, int world, int chunks) {
+  if (!P || world < 1 || chunks < 1) return -1;
+  const dssm::WireGeo g = dp_geo(P, world, chunks);
+  return (int64_t)g.ww * g.wp * g.ws * g.n;
+}
+
+int dssm_plan_set_dp_wire(dssm_plan* P, int world, int rank, int chunks, uint16_t* grad_wire,
+                          const uint16_t* stage, uint16_t* param_wire, int64_t count) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
-  if (!grad_wire && !param_wire) {
+  if (P->capturing) return fail(DSSM_E_INVALID, "the wire cannot change during a graph capture");
+  if (!grad_wire && !param_wire && !stage) {
     P->gwire = P->pwire = nullptr;
+    P->gstage = nullptr;
+    P->geo = dssm::WireGeo{};
     return DSSM_OK;
   }
-  if (!grad_wire || !param_wire) return fail(DSSM_E_INVALID, "both wires or neither");
+  if (!grad_wire || !param_wire || !stage) return fail(DSSM_E_INVALID, "grad_wire, stage and param_wire, or none");
   if (!P->Lt.bf16) return fail(DSSM_E_UNSUPPORTED, "the bf16 wire is a bf16-mode (perf) option");
   if (P->fused_w1_adam()) return fail(DSSM_E_INVALID, "the bf16 wire needs the fused W1 Adam off");
-  if (P->Lt.fc_off[0] != 0 || count < P->wire_end())
-    return fail(DSSM_E_INVALID, "wire buffers must hold dssm_plan_wire_extent() elements");
-  if ((reinterpret_cast<uintptr_t>(grad_wire) | reinterpret_cast<uintptr_t>(param_wire)) & 7)
+  if (world < 1 || rank < 0 || rank >= world || chunks < 1 || chunks > 64)
+    return fail(DSSM_E_INVALID, "dp wire: 0 <= rank < world, 1 <= chunks <= 64");
+  if (world > 1 && stage == grad_wire) return fail(DSSM_E_INVALID, "the stage is the all-to-all's output");
+  if (P->Lt.fc_off[0] != 0 || (P->Lt.n[0] % 4))
+    return fail(DSSM_E_UNSUPPORTED, "the wire needs W1 at arena offset 0 and a width multiple of 4");
+  if (count < dssm_plan_dp_wire_size(P, world, chunks))
+    return fail(DSSM_E_INVALID, "wire buffers must hold dssm_plan_dp_wire_size() elements");
+  if ((reinterpret_cast<uintptr_t>(grad_wire) | reinterpret_cast<uintptr_t>(param_wire) |
+       reinterpret_cast<uintptr_t>(stage)) & 7)
     return fail(DSSM_E_INVALID, "wire buffers must be 8-byte aligned");
   P->gwire = grad_wire;
   P->pwire = param_wire;
+  P->gstage = stage;
+  P->geo = dp_geo(P, world, chunks);
+  P->dp_rank = rank;
   return DSSM_OK;
 }
 
-int dssm_plan_set_wire_stage(dssm_plan* P, const uint16_t* stage, int parts, int64_t stride) {
-  if (!P) return fail(DSSM_E_INVALID, "null plan");
-  if (!stage) {
-    P->gstage = nullptr;
-    P->gparts = 0;
-    return DSSM_OK;
-  }
-  if (parts < 1 || parts > 64 || stride < 0 || (stride % 4) ||
-      (reinterpret_cast<uintptr_t>(stage) & 7))
-    return fail(DSSM_E_INVALID, "wire stage: 1..64 parts, stride a multiple of 4, 8-B aligned");
-  P->gstage = stage;
-  P->gparts = parts;
-  P->gstride = stride;
+int dssm_plan_dp_geometry(const dssm_plan* P, int64_t* out) {
+  if (!P || !out) return fail(DSSM_E_INVALID, "null argument");
+  if (!P->pwire) return fail(DSSM_E_INVALID, "no wire set (dssm_plan_set_dp_wire)");
+  const dssm::WireGeo& g = P->geo;
+  const int64_t r0 = std::min<int64_t>((int64_t)P->dp_rank * g.wp * g.ws, P->Lt.D);
+  const int64_t r1 = std::min<int64_t>(r0 + (int64_t)g.wp * g.ws, P->Lt.D);
+  out[0] = g.ww;
+  out[1] = g.wp;
+  out[2] = g.ws;
+  out[3] = P->sub_elems();
+  out[4] = r0 * g.n;  // this rank's W1 shard in the arena: [out[4], out[5])
+  out[5] = r1 * g.n;
+  out[6] = P->wire_end();
+  out[7] = P->Lt.total;
   return DSSM_OK;
 }
 
 int dssm_plan_wire_shadows(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
-  if (!P->pwire) return fail(DSSM_E_INVALID, "no wire set (dssm_plan_set_wire)");
-  HIP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], (hipStream_t)stream));
+  if (!P->pwire) return fail(DSSM_E_INVALID, "no wire set (dssm_plan_set_dp_wire)");
+  HIP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, -1, (hipStream_t)stream));
   return DSSM_OK;
 }
 
@@ -1416,20 +1499,17 @@ int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void
   return DSSM_OK;
 }
 
-int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream) {
-  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
-  ncclDataType_t t;
-  size_t es;
-  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es) || send == recv)
-    return fail(DSSM_E_INVALID, "dssm_all_to_all: bad arguments (distinct send / recv)");
-  hipStream_t s = (hipStream_t)stream;
+// all-to-all as the rank's own chunk by a device copy plus one grouped send / recv per peer (all
+// xGMI links busy at once on a fully connected node: one step, not world - 1 ring steps).  (RCCL's
+// ncclAllToAll crashed in hipGraph capture at world 1 on this image; the grouped form captures.)
+static int all_to_all_impl(const void* send, void* recv, int64_t count, ncclDataType_t t, size_t es,
+                           hipStream_t s) {
   const char* sp = static_cast<const char*>(send);
   char* rp = static_cast<char*>(recv);
   const size_t chunk = (size_t)count * es;
-  // the rank's own chunk by a device copy; every peer pair by one grouped send / recv (all xGMI
-  // links busy at once on a fully connected node: one step, not world - 1 ring steps)
   HIP_TRY(hipMemcpyAsync(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk,
                          hipMemcpyDeviceToDevice, s));
+  if (g_world == 1) return DSSM_OK;
   RCCL_TRY(ncclGroupStart());
   for (int j = 0; j < g_world; ++j) {
     if (j == g_rank) continue;
@@ -1441,6 +1521,197 @@ int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void
     }
   }
   RCCL_TRY(ncclGroupEnd());
+  return DSSM_OK;
+}
+
+int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t;
+  size_t es;
+  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es) || send == recv)
+    return fail(DSSM_E_INVALID, "dssm_all_to_all: bad arguments (distinct send / recv)");
+  return all_to_all_impl(send, recv, count, t, es, (hipStream_t)stream);
+}
+
+// ---- the data-parallel step graph (include/dssm.h dssm_plan_graph_build_dp_steps) -----------
+// One collective of the exchange on the comm stream cs: the library's RCCL communicator (comm 0),
+// a device copy of the same bytes (comm 1) or a kernel holding cs for the modelled link time (2).
+struct DpComm {
+  int mode;
+  double gbps, latency_ns;
+};
+static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hipStream_t cs) {
+  const int64_t sub = P->sub_elems();
+  const int W = P->geo.ww;
+  const int64_t blk = (int64_t)W * sub;  // chunk's elements in each wire
+  const size_t tail = (size_t)(P->Lt.total - P->wire_end());
+  float* tg = P->g + P->wire_end();
+  // bytes this rank sends: all-to-all / all-gather (W-1) * sub bf16; all-reduce (ring) 2(W-1)/W fp32
+  const double bytes = kind == 2 ? 2.0 * (W - 1) / W * tail * 4 : (double)(W - 1) * sub * 2;
+  if (k.mode == 2) {
+    HIP_TRY(dssm::launch_spin(k.latency_ns + bytes / k.gbps, cs));
+    return DSSM_OK;
+  }
+  uint16_t* gw = P->gwire + chunk * blk;
+  uint16_t* st = const_cast<uint16_t*>(P->gstage) + chunk * blk;
+  uint16_t* pw = P->pwire + chunk * blk;
+  if (k.mode == 1) {  // same bytes through HBM (the tail's copy is skipped: 0.5 MB)
+    if (kind == 0) HIP_TRY(hipMemcpyAsync(st, gw, blk * 2, hipMemcpyDeviceToDevice, cs));
+    if (kind == 1) HIP_TRY(hipMemcpyAsync(st, pw, blk * 2, hipMemcpyDeviceToDevice, cs));
+    return DSSM_OK;
+  }
+  if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs);
+  if (kind == 1) RCCL_TRY(ncclAllGather(pw + (int64_t)P->dp_rank * sub, pw, (size_t)sub, ncclBfloat16, g_comm, cs));
+  if (kind == 2) RCCL_TRY(ncclAllReduce(tg, tg, tail, ncclFloat32, ncclSum, g_comm, cs));
+  return DSSM_OK;
+}
+
+int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, const int32_t* const* indices,
+                                   const float* const* values, int nsteps, float grad_scale, int comm,
+                                   float link_gbps, float latency_us, int overlap, int with_probes,
+                                   void* stream, int* graph_id) {
+  if (!P || !graph_id || !indptrs || !indices || !values || nsteps < 1)
+    return fail(DSSM_E_INVALID, "null argument or nsteps < 1");
+  if (!stream) return fail(DSSM_E_INVALID, "graph capture needs a non-default stream");
+  if (P->capturing) return fail(DSSM_E_INVALID, "already capturing");
+  if (!P->pwire || !wire_gradient_pass(P))
+    return fail(DSSM_E_INVALID, "the data-parallel graph needs the bf16 wire (dssm_plan_set_dp_wire) and the "
+                                "wire gradient pass (HEAVY_IN_ADAM, WIRE_GRAD_PASS)");
+  if (comm < 0 || comm > 2 || (comm == 2 && !(link_gbps > 0.f)))
+    return fail(DSSM_E_INVALID, "comm: 0 RCCL, 1 device copies, 2 modelled (link_gbps > 0)");
+  if (comm == 0 && (!g_comm || g_world != P->geo.ww || g_rank != P->dp_rank))
+    return fail(DSSM_E_INVALID, "comm 0 needs dssm_comm_init with the wire's world and rank");
+  if (comm == 0 && P->geo.ww > 1 && P->gstage == P->gwire)
+    return fail(DSSM_E_INVALID, "the all-to-all needs a stage distinct from grad_wire");
+  for (int i = 0; i < nsteps; ++i)
+    if (!indptrs[i] || (P->Lt.max_nnz && (!indices[i] || !values[i])))
+      return fail(DSSM_E_INVALID, "null batch pointer");
+  hipStream_t s = (hipStream_t)stream;
+  // overlap: the collectives on a second captured stream (fork / join edges between the two);
+  // otherwise every node on the capture stream, in dependency order
+  if (overlap && !P->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&P->comm_stream, hipStreamNonBlocking));
+  hipStream_t cs = overlap ? P->comm_stream : s;
+  const DpComm k{comm, (double)link_gbps, 1e3 * (double)latency_us};
+  const int C = P->geo.wp;
+  auto* g = new dssm_plan::GraphSlot();
+  g->probes = with_probes != 0;
+  // events: per step and chunk gradient-pass / all-to-all / Adam / all-gather, + the tail's
+  const int per_step = 4 * C + 1;
+  g->xev.resize((size_t)per_step * nsteps, nullptr);
+  for (auto& e : g->xev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      for (hipEvent_t x : g->xev)
+        if (x) hipEventDestroy(x);
+      delete g;
+      return fail(DSSM_E_HIP, "hipEventCreate failed");
+    }
+  if (g->probes)
+    for (auto& pr : g->ev)
+      for (hipEvent_t& e : pr) (void)hipEventCreate(&e);
+  const int32_t* keep_ip = P->indptr;
+  const int32_t* keep_ix = P->indices;
+  const float* keep_v = P->values;
+  const bool was_fwd = P->fwd_train_done;
+  P->grads_clean = true;
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    for (hipEvent_t x : g->xev) hipEventDestroy(x);
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
+  }
+  P->capturing = g;
+  P->dp_defer_gradpass = true;
+  P->rank_done_for = nullptr;
+  int rc = DSSM_OK;
+  auto rec = [&](hipEvent_t e, hipStream_t st) { return cs == s ? hipSuccess : hipEventRecord(e, st); };
+  auto wait = [&](hipStream_t st, hipEvent_t e) { return cs == s ? hipSuccess : hipStreamWaitEvent(st, e, 0); };
+#define DP_TRY(expr)                                                                              \
+  do {                                                                                            \
+    if (!rc) {                                                                                    \
+      hipError_t e_ = (expr);                                                                     \
+      if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    }                                                                                             \
+  } while (0)
+  for (int i = 0; i < nsteps && !rc; ++i) {
+    hipEvent_t* ev = g->xev.data() + (size_t)i * per_step;
+    hipEvent_t *e_gp = ev, *e_a2a = ev + C, *e_adam = ev + 2 * C, *e_ag = ev + 3 * C, e_tail = ev[4 * C];
+    g->probes = with_probes != 0 && i == nsteps - 1;
+    g->probe_mask = 1u << DSSM_PROBE_ADAM;
+    P->indptr = indptrs[i];
+    P->indices = indices[i];
+    P->values = values[i];
+    rc = dssm_plan_forward(P, 1, stream);
+    if (!rc) rc = dssm_plan_backward(P, stream);
+    // gradient pass chunk by chunk; each chunk's all-to-all on the comm stream as soon as it lands
+    for (int c = 0; c < C && !rc; ++c) {
+      if (!rc) rc = launch_wire_gradient_pass(P, s, C > 1 ? c : -1);
+      DP_TRY(rec(e_gp[c], s));
+      DP_TRY(wait(cs, e_gp[c]));
+      if (!rc) rc = dp_collective(P, k, 0, c, cs);
+      DP_TRY(rec(e_a2a[c], cs));
+    }
+    if (!rc) rc = dp_collective(P, k, 2, 0, cs);  // the fp32 tail (b1's row: the last chunk's pass)
+    DP_TRY(rec(e_tail, cs));
+    // Adam chunk c once its all-to-all is in; each chunk's all-gather as soon as its Adam is done
+    if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {
+      P->host_rank_indptr = indptrs[i + 1];
+      P->host_rank_indices = indices[i + 1];
+    }
+    P->dp_hook = [&](int c, bool after) -> int {
+      if (!after) {
+        if (wait(s, e_a2a[c]) != hipSuccess) return fail(DSSM_E_HIP, "hipStreamWaitEvent");
+        if (c == C - 1 && wait(s, e_tail) != hipSuccess) return fail(DSSM_E_HIP, "hipStreamWaitEvent");
+        return DSSM_OK;
+      }
+      if (rec(e_adam[c], s) != hipSuccess || wait(cs, e_adam[c]) != hipSuccess)
+        return fail(DSSM_E_HIP, "hipEventRecord / hipStreamWaitEvent");
+      if (int r = dp_collective(P, k, 1, c, cs)) return r;
+      if (rec(e_ag[c], cs) != hipSuccess) return fail(DSSM_E_HIP, "hipEventRecord");
+      return DSSM_OK;
+    };
+    if (!rc) rc = dssm_plan_adam(P, grad_scale, stream);
+    P->dp_hook = nullptr;
+    // W1's shadow rebuilt chunk by chunk as the all-gathers land (the next forward's operand)
+    for (int c = 0; c < C && !rc; ++c) {
+      DP_TRY(wait(s, e_ag[c]));
+      DP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s));
+    }
+  }
+#undef DP_TRY
+  P->dp_hook = nullptr;
+  P->dp_defer_gradpass = false;
+  P->host_rank_indptr = P->host_rank_indices = nullptr;
+  P->rank_done_for = nullptr;
+  g->probes = with_probes != 0;
+  g->probe_mask = ~0u;
+  P->capturing = nullptr;
+  std::string err = rc ? g_err : std::string();
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(s, &graph);
+  P->indptr = keep_ip;
+  P->indices = keep_ix;
+  P->values = keep_v;
+  P->grads_clean = true;
+  P->fwd_train_done = was_fwd;
+  if (rc || e != hipSuccess || !graph) {
+    if (graph) hipGraphDestroy(graph);
+    for (hipEvent_t x : g->xev) hipEventDestroy(x);
+    delete g;
+    return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  }
+  e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    for (hipEvent_t x : g->xev) hipEventDestroy(x);
+    delete g;
+    return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+#if DSSM_GRAPH_UPLOAD
+  (void)hipGraphUpload(g->exec, s);
+#endif
+  P->graphs.push_back(g);
+  *graph_id = (int)P->graphs.size() - 1;
   return DSSM_OK;
 }
 

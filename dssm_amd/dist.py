@@ -13,7 +13,7 @@ Two exchange schedules over the flat fp32 arenas:
   updated shards are all-gathered.  The wire ("wire" argument) is
   - "bf16" (default for a bf16 model): the backward writes bf16(dW1) into a gradient wire; an
     ALL-TO-ALL delivers to every rank the bf16 gradients of ITS shard from every rank, which the
-    Adam launch sums in fp32 in rank order (dssm_plan_set_wire_stage: one bf16 rounding per
+    Adam launch sums in fp32 in rank order (dssm_plan_set_dp_wire: one bf16 rounding per
     rank's gradient, no rounding per ring hop as a bf16 reduce-scatter would add); Adam writes
     bf16(W1) of the shard into a parameter wire that is all-gathered, and W1's bf16 shadow is
     rebuilt from it.  The small tail ([extent, n_params): b1, W2.., BN) is all-reduced in fp32
@@ -249,7 +249,8 @@ def shard_bounds(n_pad: int, n: int, rank: int, world: int):
 class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
-    def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto"):
+    def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto", chunks: int = 1,
+                 overlap: bool = False):
         """comm: "auto" (the library's RCCL communicator on GPUs, torch.distributed as the
         self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
         zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
@@ -277,20 +278,21 @@ class DataParallel:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
             self.tx = self._transport(comm, strict_mode)
         self.grad_wire = self.param_wire = self.stage = None
+        self.chunks, self.overlap = 1, bool(overlap)
         if self.mode == "zero" and self.wire == "bf16":
-            ext = model.wire_extent()
-            self.extent = ext
-            self.shard = -(-ext // (64 * self.world)) * 64
-            self.begin, self.end = self.rank * self.shard, min((self.rank + 1) * self.shard, ext)
-            n = self.shard * self.world
+            # the W1 rows in `chunks` pieces (include/dssm.h dssm_plan_set_dp_wire): chunk p of each
+            # collective is one contiguous block of world * sub elements
+            self.chunks = max(1, int(chunks))
+            n = model.dp_wire_size(self.world, self.chunks)
             dev = model.params.device
             self.grad_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
             self.param_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
             self.stage = torch.zeros(n, dtype=torch.bfloat16, device=dev)
-            self.param_wire[:ext].copy_(model.params[:ext])
-            model.set_wire(self.grad_wire, self.param_wire)
-            model.set_wire_stage(self.stage, self.world, self.shard)
-            model.set_adam_range(self.begin, max(self.begin, self.end))
+            model.set_dp_wire(self.world, self.rank, self.chunks, self.grad_wire, self.stage, self.param_wire)
+            geo = model.dp_geometry()
+            self.extent, self.sub = geo["extent"], geo["sub"]
+            self.begin, self.end = geo["shard_begin"], geo["shard_end"]
+            self.shard = self.chunks * self.sub  # W1 elements per rank (the last rank's padded)
         elif self.mode == "zero":
             self.begin, self.end, self.shard = shard_bounds(npad, model.n_params, self.rank, self.world)
             model.set_adam_range(self.begin, max(self.begin, self.end))
@@ -331,14 +333,20 @@ class DataParallel:
         if self.mode != "zero":
             self.tx.all_reduce(g)
         elif self.wire == "bf16":
-            self.tx.all_to_all(self.grad_wire, self.stage)  # every rank's bf16 slice of MY shard
+            blk = self.world * self.sub
+            for p in range(self.chunks):  # chunk p: every rank's bf16 slice of MY shard's sub-chunk p
+                self.tx.all_to_all(self.grad_wire[p * blk:(p + 1) * blk], self.stage[p * blk:(p + 1) * blk])
             self.tx.all_reduce(g[self.extent:self.model.n_params])  # the fp32 tail, replicated
         else:
             self.tx.reduce_scatter_(g, self.shard)
 
     def exchange_after_adam(self):
-        if self.mode == "zero":
-            self.tx.all_gather_(self.param_wire if self.wire == "bf16" else self.model.params, self.shard)
+        if self.mode == "zero" and self.wire == "bf16":
+            blk = self.world * self.sub
+            for p in range(self.chunks):
+                self.tx.all_gather_(self.param_wire[p * blk:(p + 1) * blk], self.sub)
+        elif self.mode == "zero":
+            self.tx.all_gather_(self.model.params, self.shard)
 
     def refresh_shadows(self):
         if self.wire == "bf16":
@@ -353,7 +361,8 @@ class DataParallel:
             return
         if self.wire == "bf16":
             # W1's fp32 rows (parameters too: other ranks' shards are stale on this one) through
-            # a padded staging buffer; the tail is replicated already
+            # a padded staging buffer (rank r's shard: rows [r, r+1) * chunks * S); the tail is
+            # replicated already
             ext = self.extent
             for t in (self.model.params, self.model.adam_m, self.model.adam_v):
                 buf = torch.zeros(self.shard * self.world, dtype=t.dtype, device=t.device)
@@ -374,6 +383,22 @@ class DataParallel:
             self.refresh_shadows()
 
     # ---- captured steps (bench.py's timed path) ----------------------------------------------
+    @property
+    def capturable(self) -> bool:
+        """Whole steps, collectives included, can be captured into one graph: the library's RCCL
+        transport with the zero / bf16-wire schedule (dssm_plan_graph_build_dp_steps)."""
+        return getattr(self.tx, "capturable", False) and self.mode == "zero" and self.wire == "bf16"
+
+    def build_region(self, batches, probes: bool = False) -> int:
+        """len(batches) whole data-parallel steps as ONE graph: per step the forward, backward, the
+        gradient pass chunk by chunk with each chunk's all-to-all on a second stream as it lands,
+        Adam chunk by chunk, each chunk's all-gather behind its Adam, the shadow rebuild per
+        gathered chunk; step i+1's CSC rank pass inside step i's Adam.  Replay: model.graph_launch."""
+        if not self.capturable:
+            raise RuntimeError(f"the {self.schedule} exchange cannot be captured (needs zero/bf16 via rccl)")
+        return self.model.graph_build_dp_steps(batches, 1.0 / self.world, comm=0, overlap=self.overlap,
+                                               probes=probes)
+
     def build_graphs(self, staged, probe_batch=None):
         """Capture, per staged device batch (indptr, indices, values), the forward + backward as a
         hipGraph (plus, under the zero schedule, a variant that first rebuilds the weight shadows

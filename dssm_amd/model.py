@@ -235,35 +235,46 @@ class DSSM:
         check(self.lib.dssm_plan_adam(self._plan, float(grad_scale), stream_ptr(stream)), "adam")
         self.global_step += 1
 
-    # ---- data-parallel bf16 wire (include/dssm.h dssm_plan_set_wire) ---------------------------
+    # ---- data-parallel bf16 wire (include/dssm.h dssm_plan_set_dp_wire) --------------------------
     def wire_extent(self) -> int:
         """Arena elements [0, extent) that cross the links as bf16 (W1's rows)."""
         return int(self.lib.dssm_plan_wire_extent(self._plan))
 
-    def set_wire(self, grad_wire: Optional[torch.Tensor], param_wire: Optional[torch.Tensor]):
-        """Attach (or detach, with None) the bf16 gradient / parameter wires: backward() then ends
-        by packing W1's gradient rows into grad_wire, apply_adam() reads the rank's W1 shard from
-        it and writes bf16 parameters into param_wire, wire_shadows() rebuilds W1's shadow from it."""
-        if grad_wire is None and param_wire is None:
-            check(self.lib.dssm_plan_set_wire(self._plan, None, None, 0), "set_wire")
+    def dp_wire_size(self, world: int, chunks: int = 1) -> int:
+        """Elements each wire buffer needs for this world size and chunk count."""
+        n = int(self.lib.dssm_plan_dp_wire_size(self._plan, int(world), int(chunks)))
+        if n < 0:
+            raise ValueError("world and chunks must be >= 1")
+        return n
+
+    def set_dp_wire(self, world: int = 1, rank: int = 0, chunks: int = 1, grad_wire=None, stage=None,
+                    param_wire=None):
+        """Attach (or detach, all None) the bf16 wire of a world-size `world` exchange in `chunks`
+        pieces: backward() then ends by writing every rank's W1 gradient rows into grad_wire, the
+        caller all-to-alls chunk p of grad_wire into chunk p of stage, apply_adam() updates this
+        rank's W1 shard from the fp32 sum of the stage's partials and writes bf16(W1) of it into
+        param_wire, the caller all-gathers param_wire chunk by chunk, wire_shadows() rebuilds W1's
+        shadow from it.  Layout: dp_geometry()."""
+        if grad_wire is None and stage is None and param_wire is None:
+            check(self.lib.dssm_plan_set_dp_wire(self._plan, 1, 0, 1, None, None, None, 0), "set_dp_wire")
+            self._wires = None
             return
-        for t in (grad_wire, param_wire):
+        for t in (grad_wire, stage, param_wire):
             if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.device != self.device:
                 raise ValueError("wires are contiguous bf16 tensors on the model's device")
-        n = min(grad_wire.numel(), param_wire.numel())
-        check(self.lib.dssm_plan_set_wire(self._plan, ptr(grad_wire), ptr(param_wire), n), "set_wire")
+        n = min(grad_wire.numel(), stage.numel(), param_wire.numel())
+        check(self.lib.dssm_plan_set_dp_wire(self._plan, int(world), int(rank), int(chunks), ptr(grad_wire),
+                                             ptr(stage), ptr(param_wire), n), "set_dp_wire")
+        self._wires = (grad_wire, stage, param_wire)
 
-    def set_wire_stage(self, stage: Optional[torch.Tensor], parts: int = 0, stride: int = 0):
-        """All-to-all wire (dssm_plan_set_wire_stage): apply_adam() takes the shard's W1 gradient
-        as the fp32 sum of `parts` bf16 partials stage[k*stride : k*stride + shard] (None: off)."""
-        if stage is None:
-            check(self.lib.dssm_plan_set_wire_stage(self._plan, None, 0, 0), "set_wire_stage")
-            return
-        if stage.dtype != torch.bfloat16 or not stage.is_contiguous() or stage.device != self.device:
-            raise ValueError("the wire stage is a contiguous bf16 tensor on the model's device")
-        if stage.numel() < parts * stride:
-            raise ValueError("wire stage too small")
-        check(self.lib.dssm_plan_set_wire_stage(self._plan, ptr(stage), int(parts), int(stride)), "set_wire_stage")
+    def dp_geometry(self) -> Dict[str, int]:
+        """The wire layout (dssm_plan_dp_geometry): world, chunks, rows per sub-chunk, elements per
+        rank and chunk ('sub'), this rank's W1 shard [shard_begin, shard_end) in the arena, the wire
+        extent and the parameter count."""
+        out = (C.c_int64 * 8)()
+        check(self.lib.dssm_plan_dp_geometry(self._plan, out), "dp_geometry")
+        keys = ("world", "chunks", "rows", "sub", "shard_begin", "shard_end", "extent", "n_params")
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def wire_shadows(self, stream=None):
         check(self.lib.dssm_plan_wire_shadows(self._plan, stream_ptr(stream)), "wire_shadows")
@@ -303,6 +314,26 @@ class DSSM:
                                                    2 if probes == "adam" else (1 if probes else 0), sp,
                                                    C.byref(gid)),
               "graph_build_steps")
+        self._graphs[gid.value] = (_lib.GRAPH_FWD_BWD | _lib.GRAPH_ADAM, tuple(batches), n)
+        return gid.value
+
+    def graph_build_dp_steps(self, batches, grad_scale: float, comm: int = 0, link_gbps: float = 0.0,
+                             latency_us: float = 0.0, overlap: bool = False, probes: bool = False,
+                             stream=None) -> int:
+        """len(batches) data-parallel steps on the bf16 wire (set_dp_wire) in ONE graph, collectives
+        included (dssm_plan_graph_build_dp_steps); overlap: the collectives on a second captured
+        stream beside the chunks' kernels.  comm 0: the library's RCCL communicator; 1 / 2: one-GPU
+        rehearsals (device copies / a modelled link time of latency_us + bytes / link_gbps)."""
+        sp = stream_ptr(stream)
+        if not sp:
+            raise ValueError("graph capture needs a non-default stream (torch.cuda.Stream())")
+        n = len(batches)
+        arr = [(C.c_void_p * n)(*[ptr(b[k]) for b in batches]) for k in range(3)]
+        gid = C.c_int()
+        check(self.lib.dssm_plan_graph_build_dp_steps(self._plan, arr[0], arr[1], arr[2], n, float(grad_scale),
+                                                      int(comm), float(link_gbps), float(latency_us),
+                                                      1 if overlap else 0, 1 if probes else 0, sp, C.byref(gid)),
+              "graph_build_dp_steps")
         self._graphs[gid.value] = (_lib.GRAPH_FWD_BWD | _lib.GRAPH_ADAM, tuple(batches), n)
         return gid.value
 

@@ -169,29 +169,49 @@ int dssm_plan_get_option(const dssm_plan* plan, int option);
 int dssm_plan_set_adam_range(dssm_plan* plan, int64_t begin, int64_t end);
 /* Data-parallel bf16 wire (perf mode; replaces the fp32 gradient all-reduce of the reference's
  * single-process optimizer, new_dssm.py:215-217, when the batch is sharded over ranks).  W1's rows
- * -- arena elements [0, dssm_plan_wire_extent()) -- cross the links as bf16:
- *   - dssm_plan_backward ends by writing grad_wire[i] = bf16(grad[i]) for those elements (the
- *     caller reduce-scatters grad_wire in place);
- *   - dssm_plan_adam then updates the adam-range shard of W1 from grad_wire (x grad_scale) and
- *     writes bf16(param) of the shard into param_wire (the caller all-gathers it), and updates
- *     the replicated fp32 tail [extent, param_count) -- b1, W2.., BN -- from the fp32 gradient
- *     arena (the caller all-reduces that tail first) with its shadows;
+ * -- arena elements [0, dssm_plan_wire_extent()) -- cross the links as bf16, in `chunks` pieces so
+ * the collectives of one piece overlap the kernels of the next (dssm_plan_graph_build_dp_steps):
+ *   - rank j's optimizer shard is W1 rows [j*chunks*S, (j+1)*chunks*S) (S = ceil(D / (world *
+ *     chunks)) rows per sub-chunk; dssm_plan_dp_geometry); the wires hold sub-chunk (p, j) -- rows
+ *     (j*chunks + p)*S + [0, S) -- at element ((p*world + j)*S)*n, so chunk p of every collective
+ *     is one contiguous block of world*S*n elements (chunks == 1: the arena's own layout);
+ *   - dssm_plan_backward ends by writing every rank's W1 gradient rows as bf16 into grad_wire (the
+ *     caller all-to-alls chunk p of grad_wire into chunk p of stage);
+ *   - dssm_plan_adam updates this rank's shard with the fp32 sum, in rank order, of the world's
+ *     bf16 partials in stage (x grad_scale: each rank's gradient rounded to bf16 once), writes
+ *     bf16(param) of the shard into param_wire (the caller all-gathers chunk p of it, in place),
+ *     and updates the replicated fp32 tail [extent, param_count) -- b1, W2.., BN -- from the fp32
+ *     gradient arena (the caller all-reduces that tail first) with its shadows;
  *   - dssm_plan_wire_shadows (graph part DSSM_GRAPH_WIRE_SHADOWS) rewrites W1's bf16 shadow from
  *     the all-gathered param_wire.
  * W1's fp32 master rows outside the rank's shard are then stale (all-gather them for a
- * checkpoint).  count: elements of each wire (>= extent; the caller pads to equal shards).
- * Both NULL: off.  Needs bf16 mode and the fused W1 Adam off. */
+ * checkpoint).  count: elements of each buffer (>= dssm_plan_dp_wire_size(world, chunks)).  stage
+ * may be grad_wire at world 1 (the all-to-all is then the identity).  All NULL: off.  Needs bf16
+ * mode and the fused W1 Adam off. */
 int64_t dssm_plan_wire_extent(const dssm_plan* plan);
-int dssm_plan_set_wire(dssm_plan* plan, uint16_t* grad_wire, uint16_t* param_wire, int64_t count);
+int64_t dssm_plan_dp_wire_size(const dssm_plan* plan, int world, int chunks);
+int dssm_plan_set_dp_wire(dssm_plan* plan, int world, int rank, int chunks, uint16_t* grad_wire,
+                          const uint16_t* stage, uint16_t* param_wire, int64_t count);
+/* out[8] = {world, chunks, S, S*n (elements per rank per chunk), shard begin, shard end (this rank's W1
+ * arena elements), extent, param_count}. */
+int dssm_plan_dp_geometry(const dssm_plan* plan, int64_t* out);
 int dssm_plan_wire_shadows(dssm_plan* plan, void* stream);
-/* All-to-all variant of the bf16 wire (the default data-parallel exchange, dssm_amd/dist.py):
- * instead of a reduce-scattered grad_wire (rounded to bf16 at every ring hop), dssm_plan_adam
- * takes the W1 shard's gradient as the fp32 sum, in rank order, of `parts` bf16 partial gradients
- * stage[k * stride + (e - begin)] (k < parts, e in the Adam range [begin, end), stride >= end -
- * begin, a multiple of 4): each rank's own gradient rounded once, then accumulated in fp32.  The
- * stage is what dssm_all_to_all() of every rank's grad_wire (chunks of `stride`) delivers.
- * NULL: off (the reduce-scattered grad_wire is read). */
-int dssm_plan_set_wire_stage(dssm_plan* plan, const uint16_t* stage, int parts, int64_t stride);
+/* nsteps data-parallel training steps on the bf16 wire captured into ONE graph, step i on batch
+ * (indptrs[i], ...), each step: forward, backward, the gradient pass (chunk by chunk), each chunk's
+ * all-to-all, the fp32 tail all-reduce, Adam chunk by chunk, each chunk's all-gather, the shadow
+ * rebuild per gathered chunk; step i+1's CSC rank pass rides in step i's Adam (with RANK_IN_ADAM).
+ * overlap 0: every node on `stream` in that order; 1: the collectives on a second captured stream,
+ * each chunk's collective as soon as its rows are written / updated (fork / join edges).
+ * comm: 0 = the library's RCCL communicator (dssm_comm_init; world / rank must match the wire's);
+ * 1 = rehearsal on one GPU, each collective replaced by a device copy of its bytes; 2 = rehearsal,
+ * each collective replaced by a kernel that holds its stream for latency_us + (bytes this rank
+ * sends) / link_gbps (GB/s) -- the exchange's modelled time on the links.  with_probes: the Adam
+ * probe brackets the last step's Adam launches. */
+int dssm_plan_graph_build_dp_steps(dssm_plan* plan, const int32_t* const* indptrs,
+                                   const int32_t* const* indices, const float* const* values,
+                                   int nsteps, float grad_scale, int comm, float link_gbps,
+                                   float latency_us, int overlap, int with_probes, void* stream,
+                                   int* graph_id);
 /* forward(train) + backward + adam: one sess.run(train_step) (new_dssm.py:267). */
 int dssm_plan_train_step(dssm_plan* plan, void* stream);
 

@@ -51,15 +51,35 @@ class CpuEngine:
         self._train = None
         self.gwire = self.pwire = self.stage = None
 
-    # bf16 wire (include/dssm.h dssm_plan_set_wire): W1's rows, arena [0, D*WIDTHS[0])
+    # bf16 wire (include/dssm.h dssm_plan_set_dp_wire): W1's rows, arena [0, D*WIDTHS[0]), laid
+    # out by sub-chunks: rank j's shard is rows [j*P*S, (j+1)*P*S), sub-chunk (p, j) at ((p*W+j)*S)*n
     def wire_extent(self):
         return D * WIDTHS[0]  # the port's arena starts with W1 [D x L1], like the device layout
 
-    def set_wire(self, gw, pw):
-        self.gwire, self.pwire = gw, pw
+    def _geo(self, world, chunks):
+        return world, chunks, -(-D // (world * chunks)), WIDTHS[0]
 
-    def set_wire_stage(self, stage, parts, stride):
-        self.stage, self.parts, self.stride = stage, parts, stride
+    def dp_wire_size(self, world, chunks):
+        w, p, rows, n = self._geo(world, chunks)
+        return w * p * rows * n
+
+    def set_dp_wire(self, world, rank, chunks, gw, st, pw):
+        self.gwire, self.stage, self.pwire = gw, st, pw
+        self.geo, self.wrank = self._geo(world, chunks), rank
+        w, p, rows, n = self.geo
+        r0 = min(rank * p * rows, D)
+        self.range = (r0 * n, min(r0 + p * rows, D) * n)
+
+    def dp_geometry(self):
+        w, p, rows, n = self.geo
+        b, e = self.range
+        return {"world": w, "chunks": p, "rows": rows, "sub": rows * n, "shard_begin": b, "shard_end": e,
+                "extent": self.wire_extent(), "n_params": self.n_params}
+
+    def _wpos(self, row):
+        w, p, rows, n = self.geo
+        j, c, s = row // (rows * p), (row // rows) % p, row % rows
+        return ((c * w + j) * rows + s) * n
 
     def wire_shadows(self):
         pass  # fp32 engine: the bf16 W1 shadow is the parameter wire itself
@@ -81,24 +101,27 @@ class CpuEngine:
 
     def backward(self):
         self.loss = self.cpu.forward_backward(self.batch, train=self._train, backward=True)
-        if self.gwire is not None:  # the plan's backward ends by packing W1's gradient rows
-            ext = self.wire_extent()
-            self.gwire[:ext] = self.grads[:ext].to(torch.bfloat16)
+        if self.gwire is not None:  # the plan's backward ends by writing W1's gradient rows
+            n = WIDTHS[0]
+            for row in range(D):
+                o = self._wpos(row)
+                self.gwire[o:o + n] = self.grads[row * n:(row + 1) * n].to(torch.bfloat16)
 
     def apply_adam(self, grad_scale=1.0):
         # a range step is the full step with the elements outside [begin, end) left as they were
-        # (with the wire: [begin, end) from the bf16 gradient wire plus the replicated tail)
+        # (with the wire: [begin, end) from the all-to-all's stage plus the replicated tail)
         keep = {r: self.cpu.flat[r].copy() for r in ("p", "m", "v")}
         b, e = self.range
         if self.gwire is not None:
             ext = self.wire_extent()
-            if self.stage is not None:  # the all-to-all's partials of this shard, fp32 sum in rank order
-                acc = torch.zeros(e - b, dtype=torch.float32)
-                for k in range(self.parts):
-                    acc += self.stage[k * self.stride:k * self.stride + (e - b)].float()
-                self.grads[b:e] = acc
-            else:
-                self.grads[b:e] = self.gwire[b:e].float()
+            w, p, rows, n = self.geo
+            for row in range(b // n, e // n):  # the world's bf16 partials of my rows, fp32 sum in rank order
+                c, sr = (row // rows) % p, row % rows
+                acc = torch.zeros(n, dtype=torch.float32)
+                for k in range(w):
+                    o = ((c * w + k) * rows + sr) * n
+                    acc += self.stage[o:o + n].float()
+                self.grads[row * n:(row + 1) * n] = acc
         self.cpu.adam(grad_scale)
         for r, old in keep.items():
             if self.gwire is not None:
@@ -108,7 +131,10 @@ class CpuEngine:
                 self.cpu.flat[r][:b] = old[:b]
                 self.cpu.flat[r][e:] = old[e:]
         if self.pwire is not None:
-            self.pwire[b:e] = self.params[b:e].to(torch.bfloat16)
+            n = WIDTHS[0]
+            for row in range(b // n, e // n):
+                o = self._wpos(row)
+                self.pwire[o:o + n] = self.params[row * n:(row + 1) * n].to(torch.bfloat16)
 
 
 def _free_port():
@@ -117,7 +143,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, port, out_dir, mode, wire, world):
+def _worker(rank, port, out_dir, mode, wire, world, chunks):
     os.environ["OMP_NUM_THREADS"] = "2"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -125,7 +151,7 @@ def _worker(rank, port, out_dir, mode, wire, world):
         p0 = O.init_params(cfg, seed=9)
         glob = synth_batch(D, BS, NEG, seed=1234, mean_nnz=16)
         eng = CpuEngine(p0, world)
-        dp = DataParallel(eng, comm="auto", mode=mode, wire=wire)
+        dp = DataParallel(eng, comm="auto", mode=mode, wire=wire, chunks=chunks)
         assert dp.world == world and dp.rank == rank and dp.mode == mode and dp.comm == "torch"
         assert dp.wire == (wire if mode == "zero" else "fp32")
         eng.set_batch(shard_batch(glob, BS, NEG, rank, world))
@@ -140,15 +166,16 @@ def _worker(rank, port, out_dir, mode, wire, world):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("mode,wire", [("allreduce", "fp32"), ("zero", "fp32"), ("zero", "bf16")])
-def test_data_parallel_gloo(mode, wire, world):
+@pytest.mark.parametrize("mode,wire,chunks", [("allreduce", "fp32", 1), ("zero", "fp32", 1), ("zero", "bf16", 1),
+                                              ("zero", "bf16", 3)])
+def test_data_parallel_gloo(mode, wire, chunks, world):
     """allreduce: all-reduce + replicated Adam; zero: Adam on the rank's shard + all-gather of the
     parameters, W1's rows on an fp32 (reduce-scatter) or a bf16 all-to-all wire. All must give
     the same step (the bf16 wire within Adam's insensitivity to gradient rounding: a first step
     moves each element by lr * sign(g) wherever |g| >> eps)."""
     WORLD = world
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d, mode, wire, world), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, mode, wire, world, chunks), nprocs=WORLD, join=True)
         p = [np.load(os.path.join(d, f"p{r}.npy")) for r in range(WORLD)]
         m_ = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(WORLD)]
         ema = [np.load(os.path.join(d, f"ema{r}.npy")) for r in range(WORLD)]

@@ -1,15 +1,23 @@
-"""Data-parallel bf16 wire kernels on one GPU (include/dssm.h dssm_plan_set_wire).
+"""Data-parallel bf16 wire on one GPU (include/dssm.h dssm_plan_set_dp_wire, dssm_amd/dist.py).
 
-The collectives are the caller's (dssm_amd/dist.py, covered over gloo in test_dist_gloo.py);
-what runs on the device is checked here with world = 1, where the reduce-scatter and
-all-gather are identities:
-* backward() ends by packing bf16(dW1) into the gradient wire (exactly torch's RNE rounding of
-  the materialized fp32 gradient);
-* Adam over a W1 shard reads the wire, updates the shard only, writes bf16(W1) into the
-  parameter wire, and updates the fp32 tail (b1, W2.., BN) as the unwired step does;
-* wire_shadows() rebuilds W1's bf16 shadow: a forward after it equals one after the fp32
-  shadow refresh.
-"""
+The wire carries W1's rows in `chunks` pieces: rank j's optimizer shard is rows [j*P*S, (j+1)*P*S)
+and sub-chunk (p, j) -- rows (j*P + p)*S + [0, S) -- sits at ((p*world + j)*S)*n, so chunk p of
+every collective is one contiguous block.  Checked here:
+* backward() writes bf16(dW1) of every row into the grad wire at its layout position (the gradient
+  pass's rows against the materialised gradient of the unwired step, to bf16 rounding);
+* Adam over this rank's shard takes the fp32 sum, in rank order, of the stage's bf16 partials
+  (bit-identical to the unwired Adam fed that sum), writes bf16(W1) of the shard into the
+  parameter wire at its layout position and leaves the other rows alone; the replicated fp32 tail
+  updates as the unwired step does;
+* wire_shadows() rebuilds W1's bf16 shadow: a forward after it equals one after the fp32 refresh;
+* the data-parallel step graph (dssm_plan_graph_build_dp_steps: forward, backward, the chunked
+  gradient pass, the collectives on a second stream, chunked Adam, chunked shadow rebuild) at
+  world 1, with the library's RCCL communicator (comm 0) and the device-copy rehearsal (comm 1),
+  against the same steps run eagerly; the modelled-link rehearsal (comm 2) runs.
+At world 1 the all-to-all and all-gather are identities; the exchange between ranks is covered by
+tests/test_gpu_dp_bow.py (world 2 over gloo) and tests/test_dist_gloo.py (CPU)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 import torch
@@ -22,15 +30,28 @@ pytestmark = pytest.mark.gpu
 D, WIDTHS, BS, NEG, LR = 5000, (300, 300, 128), 96, 4, 0.01
 
 
-def _wired(m):
-    ext = m.wire_extent()
-    assert ext == D * WIDTHS[0]
-    n = -(-ext // 512) * 512
+def _wires(m, world, rank, chunks, same_stage=False):
+    n = m.dp_wire_size(world, chunks)
     gw = torch.zeros(n, dtype=torch.bfloat16, device=m.device)
+    st = gw if same_stage else torch.zeros(n, dtype=torch.bfloat16, device=m.device)
     pw = torch.zeros(n, dtype=torch.bfloat16, device=m.device)
-    pw[:ext].copy_(m.params[:ext])
-    m.set_wire(gw, pw)
-    return ext, gw, pw
+    m.set_dp_wire(world, rank, chunks, gw, st, pw)
+    return gw, st, pw, m.dp_geometry()
+
+
+def _rows(geo, wire, D_=D):
+    """The wire's W1 rows in arena order ([D x n] view) from its sub-chunk layout."""
+    w, p, S, n = geo["world"], geo["chunks"], geo["rows"], geo["sub"] // geo["rows"]
+    out = torch.empty(D_, n, dtype=wire.dtype, device=wire.device)
+    for j in range(w):
+        for c in range(p):
+            r0 = (j * p + c) * S
+            if r0 >= D_:
+                continue
+            r1 = min(r0 + S, D_)
+            o = (c * w + j) * S * n
+            out[r0:r1] = wire[o:o + (r1 - r0) * n].view(r1 - r0, n)
+    return out
 
 
 def _close(a, b):
@@ -39,55 +60,47 @@ def _close(a, b):
     assert float((d <= 1e-5).float().mean()) >= 0.999, float((d <= 1e-5).float().mean())
 
 
-@pytest.mark.parametrize("bs", [BS, 128])
-@pytest.mark.parametrize("shard,grad_pass", [("all", "1"), ("first_half", "1"), ("all", "0")])
-def test_wire_step_matches_unwired(shard, grad_pass, bs):
-    """grad_pass 1 (default): dW1 straight into the wire by k_adam_step's W1 roles; 0: materialised
-    dW1 + k_wire_pack.  bs 128 (a multiple of 128) takes the whole-K backward pair, whose dW_l tiles
-    ride in the apply launches with the slabs reduced after them (the data-parallel schedule)."""
-    BS = bs
+@pytest.mark.parametrize("chunks", [1, 3])
+@pytest.mark.parametrize("grad_pass", ["1", "0"])
+def test_wire_step_world1_matches_unwired(chunks, grad_pass):
+    """World 1 (stage = grad wire: the all-to-all is the identity).  grad_pass 1 (default): dW1
+    straight into the wire by k_adam_step's W1 roles, chunk by chunk; 0: materialised dW1 +
+    k_wire_pack."""
     _, _, ref = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
     _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
     m.set_option("WIRE_GRAD_PASS", grad_pass == "1")
-    ext, gw, pw = _wired(m)
-    end = ext if shard == "all" else (ext // 2) // 64 * 64
-    m.set_adam_range(0, end)
-    p0, m0 = m.params.clone(), m.adam_m.clone()
+    gw, st, pw, geo = _wires(m, 1, 0, chunks, same_stage=True)
+    ext, n1 = m.wire_extent(), WIDTHS[0]
+    assert ext == D * n1 and (geo["shard_begin"], geo["shard_end"]) == (0, ext)
     hb = synth_batch(D, BS, NEG, seed=77, mean_nnz=32)
     for x in (ref, m):
         x.set_batch(hb)
         x.forward(True)
         x.backward()
     torch.cuda.synchronize()
-    if grad_pass == "0":
-        assert torch.equal(gw[:ext], m.grads[:ext].to(torch.bfloat16))
-    else:  # the pass leaves the arena's W1 rows alone; the wire holds bf16(dW1), b1's row is fp32
+    g_rows = _rows(geo, gw).float().reshape(-1)
+    g_ref = ref.grads[:ext]
+    if grad_pass == "0":  # exactly RNE bf16 of this model's materialised gradient
+        assert torch.equal(g_rows, m.grads[:ext].to(torch.bfloat16).float())
+    else:  # the pass leaves the arena's W1 rows alone; b1's row is fp32 in the arena
         assert float(m.grads[:ext].abs().max()) == 0.0
-        g_ref = ref.grads[:ext]
-        torch.testing.assert_close(gw[:ext].float(), g_ref, rtol=2 ** -7, atol=1e-6 * float(g_ref.abs().max()))
-        # b1's row (fp32, in the arena): under batch-stat BN dloss/db1 is exactly 0 and both sides
-        # hold the same bf16-dZ1 summation noise (test_oracle.py), up to float-atomic order
-        n1 = WIDTHS[0]
+        torch.testing.assert_close(g_rows, g_ref, rtol=2 ** -7, atol=1e-6 * float(g_ref.abs().max()))
         b_m, b_r = m.grads[ext:ext + n1], ref.grads[ext:ext + n1]
         assert float((b_m - b_r).abs().max()) <= 1e-4 * float(b_r.abs().max()) + 1e-7
     ref.apply_adam(1.0)
     m.apply_adam(1.0)
     torch.cuda.synchronize()
     n = m.n_params
-    _close(m.params[:end], ref.params[:end])
+    _close(m.params[:ext], ref.params[:ext])
     _close(m.params[ext:n], ref.params[ext:n])
     torch.testing.assert_close(m.adam_m[ext:n], ref.adam_m[ext:n], rtol=1e-3, atol=1e-6)
-    assert torch.equal(pw[:end], m.params[:end].to(torch.bfloat16))
-    if end < ext:  # outside the shard: untouched
-        assert torch.equal(m.params[end:ext], p0[end:ext])
-        assert torch.equal(m.adam_m[end:ext], m0[end:ext])
+    assert torch.equal(_rows(geo, pw).reshape(-1), m.params[:ext].to(torch.bfloat16))
     assert m.beta_powers() == ref.beta_powers()
 
 
 def test_wire_shadows_equal_fp32_refresh():
     _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
-    ext, gw, pw = _wired(m)
-    m.set_adam_range(0, ext)
+    _wires(m, 1, 0, 2, same_stage=True)
     hb = synth_batch(D, BS, NEG, seed=78, mean_nnz=32)
     m.set_batch(hb)
     m.forward(True)
@@ -103,35 +116,123 @@ def test_wire_shadows_equal_fp32_refresh():
     np.testing.assert_array_equal(m.fetch("cos_sim_raw"), a)
 
 
-@pytest.mark.parametrize("parts", [2, 4, 8])
-def test_wire_stage_sums_rank_partials_in_fp32(parts):
-    """The all-to-all wire (dssm_plan_set_wire_stage, the default data-parallel exchange): Adam
-    takes the shard's W1 gradient as the fp32 sum, in rank order, of `parts` bf16 partials (what
-    dssm_all_to_all delivers).  Against the unwired Adam over the same range fed that fp32 sum,
-    the shard's parameters and Adam slots are bit-identical."""
+@pytest.mark.parametrize("world,chunks", [(2, 1), (4, 2), (8, 3)])
+def test_stage_sums_rank_partials_in_fp32(world, chunks):
+    """Rank 1 of `world`: Adam takes each of its shard's W1 rows as the fp32 sum, in rank order, of
+    the world's bf16 partials in the stage (what the chunked all-to-all delivers).  Against the
+    unwired Adam over the same rows fed that fp32 sum, the shard's parameters and Adam slots are
+    bit-identical, the parameter wire holds bf16 of them at their layout positions, and every other
+    W1 row is untouched."""
     _, _, ref = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
     _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
-    ext, gw, pw = _wired(m)
-    stride = -(-ext // (64 * parts)) * 64
-    s0, s1 = stride, min(2 * stride, ext)  # the shard of rank 1
-    stage = torch.zeros(parts * stride, dtype=torch.bfloat16, device=m.device)
+    rank = 1
+    gw, st, pw, geo = _wires(m, world, rank, chunks)
+    S, n = geo["rows"], WIDTHS[0]
+    b0, b1 = geo["shard_begin"], geo["shard_end"]
     gen = torch.Generator(device=m.device).manual_seed(5)
-    for k in range(parts):  # rank k's bf16 gradient of this shard
-        stage[k * stride:k * stride + (s1 - s0)] = (
-            torch.randn(s1 - s0, generator=gen, device=m.device) * 1e-3).to(torch.bfloat16)
-    m.set_wire_stage(stage, parts, stride)
-    m.set_adam_range(s0, s1)
-    ref.set_adam_range(s0, s1)
-    acc = torch.zeros(s1 - s0, dtype=torch.float32, device=m.device)
-    for k in range(parts):
-        acc += stage[k * stride:k * stride + (s1 - s0)].float()
+    st.copy_((torch.randn(st.numel(), generator=gen, device=m.device) * 1e-3).to(torch.bfloat16))
+    acc = torch.zeros(b1 - b0, dtype=torch.float32, device=m.device)
+    for row in range(b0 // n, b1 // n):
+        c, s = (row // S) % chunks, row % S
+        for k in range(world):
+            o = ((c * world + k) * S + s) * n
+            acc[(row * n - b0):(row * n - b0) + n] += st[o:o + n].float()
+    ref.set_adam_range(b0, b1)
     ref.grads.zero_()
-    ref.grads[s0:s1] = acc
+    ref.grads[b0:b1] = acc
     m.grads.zero_()
-    ref.apply_adam(1.0 / parts)
-    m.apply_adam(1.0 / parts)
+    p0, m0 = m.params.clone(), m.adam_m.clone()
+    ref.apply_adam(1.0 / world)
+    m.apply_adam(1.0 / world)
     torch.cuda.synchronize()
-    assert torch.equal(m.params[s0:s1], ref.params[s0:s1])
-    assert torch.equal(m.adam_m[s0:s1], ref.adam_m[s0:s1])
-    assert torch.equal(m.adam_v[s0:s1], ref.adam_v[s0:s1])
-    assert torch.equal(pw[s0:s1], m.params[s0:s1].to(torch.bfloat16))
+    for x, y in ((m.params, ref.params), (m.adam_m, ref.adam_m), (m.adam_v, ref.adam_v)):
+        assert torch.equal(x[b0:b1], y[b0:b1])
+    pr = _rows(geo, pw).reshape(-1)
+    assert torch.equal(pr[b0:b1], m.params[b0:b1].to(torch.bfloat16))
+    ext = m.wire_extent()
+    assert torch.equal(m.params[:b0], p0[:b0]) and torch.equal(m.params[b1:ext], p0[b1:ext])
+    assert torch.equal(m.adam_m[:b0], m0[:b0]) and torch.equal(m.adam_m[b1:ext], m0[b1:ext])
+
+
+@pytest.fixture()
+def comm_world1():
+    """libdssm.so's RCCL communicator at world 1, bootstrapped directly (no torch.distributed)."""
+    from dssm_amd import _lib
+    lib = _lib.load()
+    made = False
+    if lib.dssm_comm_world() == 0:
+        buf = (C.c_char * 128)()
+        _lib.check(lib.dssm_comm_unique_id(buf), "comm_unique_id")
+        _lib.check(lib.dssm_comm_init(0, 1, buf), "comm_init")
+        made = True
+    assert lib.dssm_comm_world() == 1
+    yield
+    if made:
+        lib.dssm_comm_destroy()
+
+
+def _staged(seeds):
+    out = []
+    for sd in seeds:
+        b = synth_batch(D, BS, NEG, seed=sd, mean_nnz=32)
+        out.append(tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)))
+    return out
+
+
+@pytest.mark.parametrize("comm,overlap", [(0, False), (0, True), (1, True)])
+def test_dp_step_graph_world1_matches_eager(comm, overlap, comm_world1):
+    """Three captured data-parallel steps (comm 0: RCCL at world 1; comm 1: device copies) against
+    the same three steps run eagerly on the same wire (all-to-all = copy, all-gather = identity)."""
+    chunks, steps = 3, 3
+    runs = []
+    for mode in ("graph", "eager"):
+        _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+        gw, st, pw, geo = _wires(m, 1, 0, chunks)
+        runs.append((m, gw, st, pw))
+    batches = _staged([300 + i for i in range(steps)])
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        m, gw, st, pw = runs[0]
+        gid = m.graph_build_dp_steps(batches, 1.0, comm=comm, overlap=overlap)
+        m.graph_launch(gid)
+        e, egw, est, epw = runs[1]
+        for ip, ix, vv in batches:
+            e.set_batch(indptr=ip, indices=ix, values=vv)
+            e.forward(True)
+            e.backward()
+            est.copy_(egw)  # the all-to-all at world 1
+            e.apply_adam(1.0)
+            e.wire_shadows()
+    torch.cuda.synchronize()
+    # the two runs differ by float-atomic order (CSC entry order; the graph's rank pass rides in Adam),
+    # which from fresh Adam slots flips the lr * sign(g) update of rounding-level gradients
+    assert m.loss_accuracy()[0] == pytest.approx(e.loss_accuracy()[0], rel=1e-3)
+    _close(m.params[:m.n_params], e.params[:e.n_params])
+    torch.testing.assert_close(m.adam_m, e.adam_m, rtol=1e-2, atol=1e-6)
+    assert m.beta_powers() == e.beta_powers()
+    # the replayed graph left the shadows rebuilt from its last all-gather: same forward as a refresh
+    ip, ix, vv = batches[0]
+    m.set_batch(indptr=ip, indices=ix, values=vv)
+    m.forward(False)
+    torch.cuda.synchronize()
+    a = m.fetch("cos_sim_raw").copy()
+    m.sync_shadows()
+    m.forward(False)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(m.fetch("cos_sim_raw"), a, rtol=0, atol=2e-2)
+
+
+def test_dp_step_graph_modelled_links_runs():
+    """The modelled-link rehearsal (comm 2, world 8 on one GPU: the collectives are spin kernels on
+    the comm stream) captures and replays; each replay advances the beta powers once per step."""
+    _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+    _wires(m, 8, 0, 4)
+    b1, b2 = m.beta_powers()
+    batches = _staged([400, 401])
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gid = m.graph_build_dp_steps(batches, 1.0 / 8, comm=2, link_gbps=350.0, latency_us=10.0, overlap=True)
+        m.graph_launch(gid)
+    torch.cuda.synchronize()
+    nb1, nb2 = m.beta_powers()
+    assert nb1 == pytest.approx(b1 * 0.9 * 0.9, rel=1e-6) and nb2 == pytest.approx(b2 * 0.999 * 0.999, rel=1e-6)
