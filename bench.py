@@ -87,6 +87,10 @@ def parse():
                     help="N=1 bf16 headline: also time the fp32 parity mode (the reference's precision, "
                          "new_dssm.py:111-114) over the same K / W in a child process and report it as "
                          "the line's fp32_mode key")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="plan option DETERMINISTIC: run-to-run bit-identical steps (not the headline)")
+    ap.add_argument("--det-line", type=int, default=1,
+                    help="also time the deterministic mode (child process) and report it beside the line")
     ap.add_argument("--fwd-only", type=int, default=1,
                     help="also time the forward alone (eval mode: EMA-BN forward + cosine + loss, "
                          "new_dssm.py:274-285) over the staged batches, N=1")
@@ -203,10 +207,21 @@ def fp32_mode_line(args) -> dict:
     """The fp32 parity mode (fp32 weights, activations and MFMA 16x16x4 f32) of the same C2
     workload, K timed steps after W warm-up steps, timed by this script in a child process (a
     fresh plan and arenas; the child prints its own line, summarised here)."""
+    return child_mode_line(args, ["--dtype", "fp32"])
+
+
+def deterministic_mode_line(args) -> dict:
+    """The same bf16 C2 workload under the plan option DETERMINISTIC (fused statistics summed in a
+    fixed order, CSC columns in row order, heavy dW1 rows in item order: run-to-run bit-identical,
+    tests/test_gpu_deterministic.py), timed in a child process as fp32_mode_line."""
+    return child_mode_line(args, ["--deterministic", "1"])
+
+
+def child_mode_line(args, extra) -> dict:
     import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--dtype", "fp32", "--steps", str(args.steps),
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--batches", str(args.batches), "--cpu-baseline", "0",
-           "--fwd-only", "0", "--fp32-line", "0", "--probes", str(args.probes)]
+           "--fwd-only", "0", "--fp32-line", "0", "--det-line", "0", "--probes", str(args.probes)] + extra
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -215,7 +230,8 @@ def fp32_mode_line(args) -> dict:
         d = json.loads(lines[-1])
     except Exception as e:  # reported, never fatal for the headline
         return {"error": repr(e)}
-    keep = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "roofline", "kernels_ms", "final_loss")
+    keep = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "roofline", "kernels_ms", "final_loss",
+            "schedule")
     return {k: d[k] for k in keep if k in d}
 
 
@@ -532,6 +548,8 @@ def main():
     from dssm_amd.data import ZipfColumns, synth_batch
 
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
+    if args.deterministic:
+        model.set_option("DETERMINISTIC", True)
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
@@ -561,6 +579,39 @@ def main():
     probe_ids = (("spmm_fwd", _lib.PROBE_SPMM_FWD), ("adam", _lib.PROBE_ADAM),
                  ("dw1", _lib.PROBE_DW1), ("csc_build", _lib.PROBE_CSC))
 
+
+    # data parallel on the library's RCCL communicator (or its one-GPU rehearsal): the warm-up and
+    # the timed region are each ONE graph of exactly that many whole steps, collectives included
+    # (dssm_plan_graph_build_dp_steps; step i+1's rank pass in step i's Adam); longer runs replay a
+    # cycle of len(staged) steps plus a partial one.  A capture the runtime refuses falls back to
+    # split graphs with host-issued collectives, recorded in the line.
+    region_graphs, dp_capture_error = None, None
+    if args.graph and args.feed == "device" and (rehearse > 1 or (dp is not None and dp.capturable)):
+        MAX_REGION_STEPS = 256
+        comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2}[args.rehearse_comm]
+
+        def dp_graph(batches, probes=False):
+            if rehearse == 1:
+                return dp.build_region(batches, probes=probes)
+            return model.graph_build_dp_steps(batches, 1.0 / rehearse, comm=comm_mode, link_gbps=args.link_gbps,
+                                              latency_us=args.link_latency_us, overlap=bool(args.dp_overlap),
+                                              probes=probes)
+        try:
+            reg, cyc, part = {}, None, {}
+            for n in {args.warmup, args.steps} - {0}:
+                if n <= MAX_REGION_STEPS:
+                    reg[n] = dp_graph([staged[i % len(staged)] for i in range(n)], probes=bool(args.probes))
+            if max(args.warmup, args.steps) > MAX_REGION_STEPS:
+                cyc = dp_graph(staged, probes=bool(args.probes))
+                for r in {args.warmup % len(staged), args.steps % len(staged)} - {0}:
+                    part[r] = dp_graph(staged[:r], probes=bool(args.probes))
+            region_graphs = (reg, cyc, part)
+        except Exception as e:
+            if rehearse > 1:
+                raise
+            dp_capture_error = repr(e)
+            print(f"bench: the data-parallel step graph could not be captured ({e}); split graphs instead",
+                  file=sys.stderr, flush=True)
 
     feeder = None
     if args.feed == "host":
@@ -594,29 +645,10 @@ def main():
                 feeder.next(model, next_batch=(i + 1) % args.batches)
                 model.graph_launch(gslots[feeder._cur])
                 feeder.done()
-    elif args.graph and (rehearse > 1 or (dp is not None and dp.capturable)):
-        # data parallel on the library's RCCL communicator (or its one-GPU rehearsal): the warm-up
-        # and the timed region are each ONE graph of exactly that many whole steps, collectives
-        # included (dssm_plan_graph_build_dp_steps: per step the chunked gradient pass, all-to-all,
-        # Adam, all-gather and shadow rebuild overlapping on two streams; step i+1's rank pass in
-        # step i's Adam); longer runs replay a cycle of len(staged) steps plus a partial one
-        MAX_REGION_STEPS = 256
-        comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2}[args.rehearse_comm]
-
-        def dp_graph(batches, probes=False):
-            if rehearse == 1:
-                return dp.build_region(batches, probes=probes)
-            return model.graph_build_dp_steps(batches, 1.0 / rehearse, comm=comm_mode, link_gbps=args.link_gbps,
-                                              latency_us=args.link_latency_us, overlap=bool(args.dp_overlap),
-                                              probes=probes)
-        graphs, adam_graph, probe_graph, split, partial, cycle, region = None, None, None, True, {}, None, {}
-        for n in {args.warmup, args.steps} - {0}:
-            if n <= MAX_REGION_STEPS:
-                region[n] = dp_graph([staged[i % len(staged)] for i in range(n)], probes=bool(args.probes))
-        if max(args.warmup, args.steps) > MAX_REGION_STEPS:
-            cycle = dp_graph(staged, probes=bool(args.probes))
-            for r in {args.warmup % len(staged), args.steps % len(staged)} - {0}:
-                partial[r] = dp_graph(staged[:r], probes=bool(args.probes))
+    elif region_graphs is not None:
+        graphs, adam_graph, probe_graph, split, partial, cycle, region = (None, None, None, True,
+                                                                          region_graphs[2], region_graphs[1],
+                                                                          region_graphs[0])
 
         def run_steps(i0, n):
             if n in region:
@@ -736,7 +768,7 @@ def main():
         model.graph_launch(probe_graph)  # untimed: the secondary probes' replay
         torch.cuda.synchronize()
     for name, pid in (probe_ids if args.probes else ()):
-        if args.graph and split and region is not None and (rehearse > 1 or dp.capturable):
+        if args.graph and region_graphs is not None:
             if name == "adam":  # the data-parallel region: its last step's Adam chunks
                 g = region[args.steps] if args.steps in region else (
                     cycle if args.steps % len(staged) == 0 else partial[args.steps % len(staged)])
@@ -815,6 +847,7 @@ def main():
         "kernels_ms": {k: round(v, 5) for k, v in probes.items()},
         "rooflines": rl,
         "final_loss": round(loss, 5), "final_accuracy": round(acc, 4),
+        "schedule": sorted(k for k, v in model.schedule().items() if v),
         "host_launch_ms": round(1e3 * host_launch, 3),
     }
     if args.columns != "zipf":
@@ -833,11 +866,16 @@ def main():
     if dp is not None:
         out["config"]["dp_chunks"] = dp.chunks
         out["config"]["dp_overlap"] = dp.overlap
-        out["config"]["dp_launch"] = ("one graph per region, collectives captured" if dp.capturable and args.graph
+        out["config"]["dp_launch"] = ("one graph per region, collectives captured" if region_graphs is not None
                                       else "split graphs, host-issued collectives" if args.graph else "eager")
+        if dp_capture_error:
+            out["config"]["dp_capture_error"] = dp_capture_error
     if (args.fp32_line and rank == 0 and world == 1 and rehearse == 1 and args.dtype == "bf16"
             and feeder is None and args.columns == "zipf"):
         out["fp32_mode"] = fp32_mode_line(args)
+    if (args.det_line and not args.deterministic and rank == 0 and world == 1 and rehearse == 1
+            and args.dtype == "bf16" and feeder is None and args.columns == "zipf"):
+        out["deterministic_mode"] = deterministic_mode_line(args)
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

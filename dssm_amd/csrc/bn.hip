@@ -218,7 +218,7 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
 // atomic per (column, statistic) per 256-row block; no partials, no finalize (the consumer
 // derives the coefficients).
 __global__ __launch_bounds__(1024) void k_bn_sums(const float* __restrict__ Z, int ldz, int ncol,
-                                                 BnTowers tw, double* __restrict__ fsum) {
+                                                 BnTowers tw, double* __restrict__ fsum, DetAcc det) {
   __shared__ double s_a[NG][64], s_b[NG][64];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -245,8 +245,19 @@ __global__ __launch_bounds__(1024) void k_bn_sums(const float* __restrict__ Z, i
     double a = 0.0;
 #pragma unroll
     for (int k = 0; k < NG; ++k) a += g == 0 ? s_a[k][lane] : s_b[k][lane];
-    __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + g) * ldz + c, a, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    if (det.slab) {  // deterministic: this row block's slab row, the other tower zero
+      double* row = det.slab + (size_t)blockIdx.y * 4 * ldz;
+      row[(size_t)(tower * 2 + g) * ldz + c] = a;
+      row[(size_t)((1 - tower) * 2 + g) * ldz + c] = 0.0;
+    } else {
+      __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + g) * ldz + c, a, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (det.slab) {
+    __shared__ int s_last;
+    if (det_arrive(det.ticket + blockIdx.x, gridDim.y, &s_last))
+      det_reduce(det.slab, gridDim.y, ldz, blockIdx.x * 64, min((int)blockIdx.x * 64 + 64, ncol), fsum);
   }
 }
 
@@ -594,9 +605,11 @@ hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowe
   return hipGetLastError();
 }
 
-hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s) {
+hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s,
+                          const DetAcc* det) {
   RowBlocks b(t);
-  hipLaunchKernelGGL(k_bn_sums, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t, fsum);
+  hipLaunchKernelGGL(k_bn_sums, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t, fsum,
+                     det ? *det : DetAcc{});
   return hipGetLastError();
 }
 

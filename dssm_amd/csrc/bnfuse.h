@@ -22,6 +22,16 @@
 
 namespace dssm {
 
+// Deterministic mode (DSSM_OPT_DETERMINISTIC) of the fused statistics.  Instead of fp64 atomics
+// (exact up to fp64 rounding, whose order then varies), producer row r of a launch stores its
+// per-column partials of the accumulator [2 towers][2][ld] into slab row r -- zeros for the tower
+// it does not cover -- and arrives on the ticket of its column tile; the workgroup that arrives
+// last sums the rows in row order (fixed) into the accumulator with plain stores.
+struct DetAcc {
+  double* slab;      // [rows][4][ld] (null: atomics)
+  unsigned* ticket;  // one per column tile, zero-initialised, re-armed by the last arrival
+};
+
 struct BnSide {
   int n, ld;        // width, padded row stride
   int rows_q, rows_d;  // rows of the query / doc tower (row_split, rows - row_split)
@@ -37,10 +47,45 @@ struct BnSide {
   double* bsum;     // [2 towers][2][ld]: sum dy, sum dy*xhat
   float* dgamma[2];
   float* dbeta[2];
+  DetAcc fdet, bdet;  // deterministic mode: the producers' slabs of fsum / bsum (slab null: atomics)
 };
 
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every storing thread's slab stores drained, then one lane's release + arrival on ticket[tile]:
+// true (block-uniform) in the workgroup that arrived last of `expected`; it has acquired the other
+// rows (MI355X_MICROARCH.md, inter-workgroup visibility: producer drain + release, consumer acquire).
+__device__ __forceinline__ bool det_arrive(unsigned* ticket, unsigned expected, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == expected - 1;
+    if (last) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// The last arrival's fixed-order sum: out[k * ld + c] = sum over rows r < nrows (in order) of
+// slab[(r * 4 + k) * ld + c], for k < 4 and c in [c0, c1).
+__device__ __forceinline__ void det_reduce(const double* slab, int nrows, int ld, int c0, int c1, double* out) {
+  const int w = c1 - c0;
+  for (int i = threadIdx.x; i < 4 * w; i += blockDim.x) {
+    const int k = i / w, c = c0 + i - k * w;
+    double a = 0.0;
+    for (int r = 0; r < nrows; ++r) a += slab[((size_t)r * 4 + k) * ld + c];
+    out[(size_t)k * ld + c] = a;
+  }
 }
 
 // Forward coefficients of column c (< n), tower t, from the step's sums s = sum z, q = sum z^2
@@ -125,7 +170,8 @@ constexpr int kSumsRows = 128;
 template <int NT>
 __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int ldz, int ncol,
                                               int row_split, int rows, double* __restrict__ fsum,
-                                              int bx, int by, double (*s_red)[NT / 64][64]) {
+                                              int bx, int by, double (*s_red)[NT / 64][64],
+                                              DetAcc det = DetAcc{}, int nby = 0) {
   constexpr int NG = NT / 64, RPT = kSumsRows / NG;
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = bx * 64 + lane;
@@ -151,7 +197,18 @@ __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int l
     double a = 0.0;
 #pragma unroll
     for (int k = 0; k < NG; ++k) a += s_red[g][k][lane];
-    atomic_add_f64(fsum + (size_t)(tower * 2 + g) * ldz + c, a);
+    if (det.slab) {  // this row block's partials, the other tower's zero (deterministic mode)
+      double* row = det.slab + (size_t)by * 4 * ldz;
+      row[(size_t)(tower * 2 + g) * ldz + c] = a;
+      row[(size_t)((1 - tower) * 2 + g) * ldz + c] = 0.0;
+    } else {
+      atomic_add_f64(fsum + (size_t)(tower * 2 + g) * ldz + c, a);
+    }
+  }
+  if (det.slab) {
+    __shared__ int s_last;
+    if (det_arrive(det.ticket + bx, (unsigned)nby, &s_last))
+      det_reduce(det.slab, nby, ldz, bx * 64, min(bx * 64 + 64, ncol), fsum);
   }
 }
 

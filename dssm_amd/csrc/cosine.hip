@@ -247,7 +247,15 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       double acc = 0.0;
 #pragma unroll
       for (int w = 0; w < NW; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
-      atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
+      if (fs.bdet.slab)  // deterministic: this workgroup's slab row (both towers: [tower * 2 + stat])
+        fs.bdet.slab[((size_t)blockIdx.x * 4 + st) * ld + c] = acc;
+      else
+        atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
+    }
+    if (fs.bdet.slab) {
+      __shared__ int s_last;
+      if (det_arrive(fs.bdet.ticket, (unsigned)nrow_blocks, &s_last))
+        det_reduce(fs.bdet.slab, nrow_blocks, ld, 0, n, fs.bsum);
     }
   }
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block

@@ -307,6 +307,8 @@ struct NtFuse {
   const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
   int lds_epi;             // whole-K tiles: C staged through LDS, stored as 16-B row segments
+  DetAcc det;              // deterministic mode: out_sum by slab rows + fixed-order last-arrival sum
+  int det_rows;            // the launch's row tiles (arrivals per column tile)
 };
 
 template <bool BN_A, int FS>
@@ -499,11 +501,24 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
       for (int j = 0; j < 2; ++j) {
         const int c = wn * 32 + j * 16 + lane, n = bn + c;
         if (n < N) {
-          double* os = f.out_sum;
-          atomic_add_f64(os + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
-          atomic_add_f64(os + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
+          if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
+            double* row = f.det.slab + (size_t)ty * 4 * ldc;
+            row[(size_t)(tower * 2) * ldc + n] = cs[j] + sRed[c * 2];
+            row[(size_t)(tower * 2 + 1) * ldc + n] = cq[j] + sRed[c * 2 + 1];
+            row[(size_t)((1 - tower) * 2) * ldc + n] = 0.0;
+            row[(size_t)((1 - tower) * 2 + 1) * ldc + n] = 0.0;
+          } else {
+            double* os = f.out_sum;
+            atomic_add_f64(os + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
+            atomic_add_f64(os + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
+          }
         }
       }
+    }
+    if (f.det.slab) {
+      __shared__ int s_det;
+      if (det_arrive(f.det.ticket + tx, (unsigned)f.det_rows, &s_det))
+        det_reduce(f.det.slab, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum);
     }
   }
 }
@@ -776,8 +791,19 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         double v = 0.0;
 #pragma unroll
         for (int q = 0; q < WM; ++q) v += sRed[(q * 64 + c) * 2 + st];
-        atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
+        if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
+          double* row = f.det.slab + (size_t)ty * 4 * ldc;
+          row[(size_t)(tower * 2 + st) * ldc + n] = v;
+          row[(size_t)((1 - tower) * 2 + st) * ldc + n] = 0.0;
+        } else {
+          atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
+        }
       }
+    }
+    if (f.det.slab) {
+      __shared__ int s_det;
+      if (det_arrive(f.det.ticket + tx, (unsigned)f.det_rows, &s_det))
+        det_reduce(f.det.slab, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum);
     }
   }
   if (lds_epi) {
@@ -1076,7 +1102,7 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s) {
+                                    double* out_sum, hipStream_t s, const DetAcc* det) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
   const NtParams a{M, N, K, Z, lda, coef, row_split, (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out};
@@ -1087,11 +1113,13 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   }
   f.out_sum = out_sum;
   f.lds_epi = 1;  // measured: 14.4 (LDS-staged epilogue) vs 16.2 us per NT launch
+  if (det) f.det = *det;
   if (K <= kWkMaxK && (row_split % 64) == 0) {
     const int Kp = (K + 31) & ~31;
     const int nx = cdiv(ldc, 64);
 #define DSSM_NTWK(WM)                                                                         \
   {                                                                                           \
+    f.det_rows = cdiv(M, 32 * WM);                                                            \
     const int ntiles = nx * cdiv(M, 32 * WM);                                                 \
     hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),    \
                        dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
@@ -1100,6 +1128,7 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
 #undef DSSM_NTWK
     return hipGetLastError();
   }
+  f.det_rows = cdiv(M, 64);
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 64)), dim3(256), 0, s, a, f);
   return hipGetLastError();
 }
@@ -1114,7 +1143,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
                            float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
-                           TnParams* dw_out) {
+                           TnParams* dw_out, const DetAcc* det) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
@@ -1124,6 +1153,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   f.zb = z_prev;
   f.coefb = coef_prev;
   f.lds_epi = 0;  // measured: 18.1 (register epilogue) vs 18.3 us (LDS-staged) per pair launch
+  if (det) f.det = *det;
   if (n <= kWkMaxK && (row_split % 128) == 0 && lda_prev >= kin) {
     const int Kp = (n + 31) & ~31;
     const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 128);
@@ -1136,6 +1166,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
       // BN-backward apply launch (bn.hip), same splits and slabs.  Without defer the caller sums
       // the slabs (launch_splitk_reduce) after that launch.
       *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
+      f.det_rows = cdiv(M, kWkRows == 64 ? 64 : 128);
       if (kWkRows == 64)
         hipLaunchKernelGGL(k_pair_da_wk<2>, dim3(nt_blocks64), dim3(256), wk_smem_bytes(Kp, f.lds_epi, 2),
                            s, a, f, nt_x, nt_blocks64);
@@ -1148,6 +1179,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
     const int tn_x = cdiv(n, 64), tn_y = cdiv(Mw, 128);
     const int tn_blocks = tn_x * tn_y * nsplit;
     const size_t smem = std::max(wk_smem_bytes(Kp, f.lds_epi), tw_smem_bytes());
+    f.det_rows = cdiv(M, 128);
     hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks + tn_blocks), dim3(512), smem, s, a, f, nt_x,
                        nt_blocks, p, tn_x, tn_y);
     *deferred_splits = 0;
@@ -1171,6 +1203,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   const TnParams p{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kps};
   const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
   const int tn_blocks = tn_x * tn_y * nsplit;
+  f.det_rows = cdiv(M, 64);
   hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
                      nt_blocks, p, tn_x, tn_y);
   *deferred_splits = 0;

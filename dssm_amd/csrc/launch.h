@@ -9,6 +9,7 @@
 namespace dssm {
 
 struct BnSide;    // bnfuse.h
+struct DetAcc;    // bnfuse.h
 struct TnParams;  // tn.h
 
 // Eval-mode (on_train=False) BN coefficients of every layer from the EMA shadows
@@ -50,6 +51,10 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                             int* sort_row = nullptr, float* sort_val = nullptr);
 // sort_row / sort_val (deterministic mode; capacity as csc_row / csc_val, not with rank_only):
 // scratch for the scatter, whose output every column then gets in row order.
+// Every column [col_ptr[c], col_ptr[c+1]) of (row_in, val_in) into (row_out, val_out) in row order
+// (deterministic mode of the merged transpose, after its scatter).
+hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
+                           int* row_out, float* val_out, hipStream_t s);
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
@@ -59,7 +64,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s,
-                               CscScatter* scatter_out = nullptr);
+                               CscScatter* scatter_out = nullptr, const DetAcc* det = nullptr);
 // scatter_out: the launch runs the BN1 sums alone and hands the scatter to *scatter_out (a role of
 // a later launch: launch_cosine_loss).
 // dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row
@@ -107,7 +112,7 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s);
+                                    double* out_sum, hipStream_t s, const DetAcc* det = nullptr);
 // Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
 // z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
 // defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
@@ -115,7 +120,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
                            int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
                            float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
-                           TnParams* dw_out = nullptr);
+                           TnParams* dw_out = nullptr, const DetAcc* det = nullptr);
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
 // caller then sums the slabs into gw with launch_splitk_reduce.
@@ -139,7 +144,8 @@ hipError_t launch_bn_fwd_stats(const float* Z, int ldz, int n, BnTowers t, const
                                float* partial, unsigned* tickets, float* coef, hipStream_t s,
                                double* zero = nullptr, int nzero = 0);
 // Fused-statistics forward sums of one layer (bnfuse.h): fsum [2 towers][2][ldz] += sum z, z^2.
-hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s);
+hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s,
+                          const DetAcc* det = nullptr);
 // Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
 // also writes b.dgamma / b.dbeta.
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,

@@ -59,6 +59,9 @@ struct Layout {
   // fp64 accumulators of the fused BN statistics (bnfuse.h), one zeroed region
   size_t sums = 0, sums_bytes = 0;
   size_t fsum[DSSM_MAX_LAYERS] = {}, bsum[DSSM_MAX_LAYERS] = {};
+  // deterministic mode of the fused statistics (bnfuse.h DetAcc): producer slabs and tickets
+  size_t fslab[DSSM_MAX_LAYERS] = {}, bslab[DSSM_MAX_LAYERS] = {}, det_ticket[DSSM_MAX_LAYERS] = {};
+  int det_rows = 0;
   size_t ws = 0;
   int max_nnz = 0;
 };
@@ -170,6 +173,14 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
     Lt.sums = take(sums);
     Lt.sums_bytes = sums;
+    // producer rows of any fused-statistics launch: 64-row tiles bound them all
+    Lt.det_rows = (int)((R + 63) / 64) + 2;
+    for (int l = 0; l < Lt.L; ++l) {
+      const size_t slab = (size_t)Lt.det_rows * 4 * Lt.ldp[l] * 8;
+      Lt.fslab[l] = take(slab);
+      Lt.bslab[l] = take(slab);
+      Lt.det_ticket[l] = take(2 * 8 * 64);  // [fwd | bwd][column tile], one 64-B line each
+    }
     size_t o = Lt.sums;
     for (int l = 0; l < Lt.L; ++l) {
       Lt.fsum[l] = o;
@@ -322,14 +333,19 @@ struct dssm_plan {
     b.bvar = at<float>(Lt.bvar[l]);
     b.fsum = at<double>(Lt.fsum[l]);
     b.bsum = at<double>(Lt.bsum[l]);
+    if (deterministic() && Lt.det_rows) {
+      unsigned* tk = at<unsigned>(Lt.det_ticket[l]);
+      b.fdet = dssm::DetAcc{at<double>(Lt.fslab[l]), tk};
+      b.bdet = dssm::DetAcc{at<double>(Lt.bslab[l]), tk + 8 * 16};
+    }
     return b;
   }
   bool csc_rank_path() const { return on(DSSM_OPT_CSC_RANK) && dssm::csc_rank_supported(Lt.D); }
   bool fused_w1_adam() const { return on(DSSM_OPT_FUSED_W1_ADAM); }
-  // deterministic mode: the fixed-order statistics launches (the fused fp64 atomic sums are
-  // order-dependent at fp64 rounding), every CSC column in row order, heavy dW1 rows through slabs
+  // deterministic mode: fused statistics summed in a fixed order (bnfuse.h DetAcc slabs instead of
+  // fp64 atomics), every CSC column in row order, heavy dW1 rows through per-item slabs
   bool deterministic() const { return on(DSSM_OPT_DETERMINISTIC); }
-  bool fused_stats() const { return on(DSSM_OPT_FUSED_STATS) && !deterministic() && fused_stats_ok(); }
+  bool fused_stats() const { return on(DSSM_OPT_FUSED_STATS) && fused_stats_ok(); }
   bool merged_csc() const {
     return on(DSSM_OPT_MERGED_CSC) && fused_stats() && csc_rank_path() && (Lt.BS % 128) == 0;
   }
@@ -609,8 +625,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                    P->at<int>(Lt.csc_col), s,
                                    fused ? P->at<double>(Lt.sums) : nullptr,
                                    fused ? (int)(Lt.sums_bytes / 8) : 0, P->csc_rank_path(), merged,
-                                   P->deterministic() ? P->at<int>(Lt.sort_row) : nullptr,
-                                   P->deterministic() ? P->at<float>(Lt.sort_val) : nullptr));
+                                   P->deterministic() && !merged ? P->at<int>(Lt.sort_row) : nullptr,
+                                   P->deterministic() && !merged ? P->at<float>(Lt.sort_val) : nullptr));
     P->probe_end(DSSM_PROBE_CSC, s);
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
@@ -651,23 +667,29 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     // in the cosine launch (csc.h).
     dssm::CscScatter scat{};
     const bool scat_cos = merged && P->on(DSSM_OPT_SCATTER_IN_COS);
+    const bool det = P->deterministic();
+    // deterministic: the scatter writes the sort scratch, then every column is put in row order
+    int* scat_row = det ? P->at<int>(Lt.sort_row) : P->at<int>(Lt.csc_row);
+    float* scat_val = det ? P->at<float>(Lt.sort_val) : P->at<float>(Lt.csc_val);
+    const dssm::BnSide b0 = P->bn_side(0);
     if (merged)
       HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
-                                        P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row),
-                                        P->at<float>(Lt.csc_val), P->at<int>(Lt.csc_col), s,
-                                        scat_cos ? &scat : nullptr));
+                                        P->at<int>(Lt.col_ptr), scat_row, scat_val,
+                                        P->at<int>(Lt.csc_col), s, scat_cos ? &scat : nullptr,
+                                        det ? &b0.fdet : nullptr));
     else
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
-                                   P->at<double>(Lt.fsum[0]), s));
+                                   P->at<double>(Lt.fsum[0]), s, det ? &b0.fdet : nullptr));
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
+      const dssm::BnSide out = P->bn_side(l);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<uint16_t>(Lt.A[l - 1]),
-          P->at<double>(Lt.fsum[l]), s));
+          P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr));
     }
     const int lL = Lt.L - 1;
     const dssm::BnSide last = P->bn_side(lL);
@@ -677,6 +699,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
         P->at<float>(Lt.loss_j), P->at<float>(Lt.loss), P->at<float>(Lt.dA[lL]), s, &last,
         /*defer_finalize=*/true, scat_cos ? &scat : nullptr));
+    if (merged && det)
+      HIP_TRY(dssm::launch_csc_sort(P->at<int>(Lt.col_ptr), Lt.R, Lt.D, P->at<int>(Lt.sort_row),
+                                    P->at<float>(Lt.sort_val), P->at<int>(Lt.csc_row),
+                                    P->at<float>(Lt.csc_val), s));
     P->fwd_train_done = true;
     P->fwd_fused = true;
     P->loss_pending = true;
@@ -804,13 +830,15 @@ static int backward_impl(dssm_plan* P, void* stream) {
       if (fin) P->loss_pending = false;
       if (l == 0) break;
       const bool host_dw = P->on(DSSM_OPT_DW_IN_APPLY);
+      const dssm::BnSide bprev = P->bn_side(l - 1);
       dw = dssm::TnParams{};  // filled by the pair launch when it hands its dW tiles over
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
           Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
-          P->g + Lt.fc_off[l], P->fused_w1_adam(), s, &P->dw_deferred[l], host_dw ? &dw : nullptr));
+          P->g + Lt.fc_off[l], P->fused_w1_adam(), s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
+          P->deterministic() ? &bprev.bdet : nullptr));
       dw_pending = host_dw && dw.C != nullptr;
       if (dw_pending && !P->fused_w1_adam() && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
     }

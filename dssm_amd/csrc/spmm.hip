@@ -590,11 +590,11 @@ __global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ 
                                                       int* __restrict__ cnt,
                                                       int* __restrict__ csc_row,
                                                       float* __restrict__ csc_val,
-                                                      int* __restrict__ csc_col) {
+                                                      int* __restrict__ csc_col, DetAcc det) {
   __shared__ double s_red[2][4][64];
   const int b = blockIdx.x;
   if (b < nsum)
-    bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red);
+    bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red, det, nsum / nsum_x);
   else
     scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val,
                  csc_col, b - nsum, (int)gridDim.x - nsum);
@@ -648,6 +648,13 @@ __global__ __launch_bounds__(256) void k_csc_sort_rows(const int* __restrict__ c
   const int c = blockIdx.x, t = threadIdx.x;
   const int s = col_ptr[c], e = col_ptr[c + 1];
   if (s == e) return;  // uniform over the workgroup
+  if (e - s == 1) {    // a single entry is in order
+    if (t == 0) {
+      row_out[s] = row_in[s];
+      val_out[s] = val_in[s];
+    }
+    return;
+  }
   int base = s;
   for (int w0 = 0; w0 < rows; w0 += kSortWin) {
     const int wn = min(kSortWin, rows - w0);
@@ -859,7 +866,8 @@ hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* 
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
-                               float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out) {
+                               float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out,
+                               const DetAcc* det) {
   (void)max_nnz;
   if (row_split % kSumsRows) return hipErrorInvalidValue;
   int* cnt = scratch;
@@ -872,7 +880,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
   }
   hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n, row_split,
                      fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
-                     csc_row, csc_val, csc_col);
+                     csc_row, csc_val, csc_col, det ? *det : DetAcc{});
   return hipGetLastError();
 }
 
@@ -899,6 +907,13 @@ unsigned* csc_heavy_tickets(int* scratch, int D, int rows, int max_nnz) {
 
 int* csc_heavy_count(int* scratch, int D, int max_nnz) {
   return scratch + 2 * (D + 1 + 64) + max_nnz + 64;
+}
+
+hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
+                           int* row_out, float* val_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_csc_sort_rows, dim3(D + 1), dim3(256), 0, s, col_ptr, rows, row_in, val_in, row_out,
+                     val_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_csc_build(const int* indptr, const int* indices, const float* values, int rows,
