@@ -259,8 +259,8 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
 // gradient arena with fp32 atomics and arrive on the column's ticket: the last arrival takes
 // the row with atomic exchanges (read and clear at the coherence point), updates it and
 // re-arms the ticket.  Deterministic mode (heavy_slab): the items store their rows into the slab
-// instead (agent-scope stores, drained before the ticket) and the last arrival sums them in item
-// order with agent-scope loads, so the fp32 sum no longer depends on arrival order.
+// instead (released before the ticket, acquired by the last arrival) and the last arrival sums
+// them in item order, so the fp32 sum no longer depends on arrival order.
 // LDS of one heavy-item workgroup: the 4 waves' partial rows, the summed row, the last-arrival flag
 struct HeavyLds {
   float part[4][512];
@@ -306,16 +306,27 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
     if (nit == 1) {
       w1_row_from(a, c, grow, alpha);
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(a.heavy_ticket + c, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == (unsigned)nit - 1;
-        if (s_last) __hip_atomic_store(a.heavy_ticket + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // Deterministic mode: the slab rows are released before this workgroup's arrival and the
+      // last arrival acquires before reading them (common.h).  Atomics mode: every access to the
+      // column's row is a device-scope atomic performed at the coherence point, so the drained adds
+      // need no L2 write-back (an agent-scope release here writes back the XCD's L2 per item:
+      // measured +20 us on the Adam launch).
+      bool last;
+      if (a.heavy_slab) {
+        last = last_block_arrival(a.heavy_ticket + c, (unsigned)nit, &s_last);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const unsigned t = __hip_atomic_fetch_add(a.heavy_ticket + c, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+          s_last = t == (unsigned)nit - 1;
+          if (s_last) __hip_atomic_store(a.heavy_ticket + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        last = s_last != 0;
       }
-      __syncthreads();
-      if (s_last) {
+      if (last) {
         if (a.heavy_slab) {
           const float* sl = a.heavy_slab + (size_t)(it - item.y) * a.n;
           for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
@@ -358,7 +369,8 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
                                                                                 : sizeof(HeavyLds);
   __shared__ __align__(16) unsigned char s_lds[kLdsBytes];
   const int nr = a.rank.nblocks;
-  // where the hosted rank workgroups sit in dispatch order
+  // where the hosted rank workgroups sit in dispatch order (build knob DSSM_RANK_POS): 1 (default)
+  // last, after the streaming blocks; 0 first; 2 right after the heavy items
 #if DSSM_RANK_POS == 0
   const int rs = 0;
 #elif DSSM_RANK_POS == 1

@@ -256,8 +256,8 @@ __global__ __launch_bounds__(1024) void k_bn_sums(const float* __restrict__ Z, i
   }
   if (det.slab) {
     __shared__ int s_last;
-    if (det_arrive(det.ticket + blockIdx.x, gridDim.y, &s_last))
-      det_reduce(det.slab, gridDim.y, ldz, blockIdx.x * 64, min((int)blockIdx.x * 64 + 64, ncol), fsum);
+    det_publish(det, blockIdx.x, blockIdx.y, gridDim.y, ldz, blockIdx.x * 64, min((int)blockIdx.x * 64 + 64, ncol),
+                fsum, &s_last);
   }
 }
 
@@ -608,6 +608,7 @@ hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowe
 hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fsum, hipStream_t s,
                           const DetAcc* det) {
   RowBlocks b(t);
+  if (det && det->slab && (b.total() > det->cap || cdiv(ldz, 64) > kDetTiles)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_sums, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, ldz, n, t, fsum,
                      det ? *det : DetAcc{});
   return hipGetLastError();

@@ -25,12 +25,23 @@ namespace dssm {
 // Deterministic mode (DSSM_OPT_DETERMINISTIC) of the fused statistics.  Instead of fp64 atomics
 // (exact up to fp64 rounding, whose order then varies), producer row r of a launch stores its
 // per-column partials of the accumulator [2 towers][2][ld] into slab row r -- zeros for the tower
-// it does not cover -- and arrives on the ticket of its column tile; the workgroup that arrives
-// last sums the rows in row order (fixed) into the accumulator with plain stores.
+// it does not cover -- and the rows are summed by a two-level tree fixed by row index
+// (det_publish): the last arrival of each group of consecutive rows sums them in order into a
+// level-2 row, the last group's arrival sums the level-2 rows in order into the accumulator.
+// Most of the summing happens while other producers still run; the launch's tail is one short sum.
+constexpr int kDetTiles = 8;     // column tiles of 64 (ld <= 512)
+constexpr int kDetTickets = 32;  // tickets per column tile: [0] level 2, [1 + g] group g
 struct DetAcc {
-  double* slab;      // [rows][4][ld] (null: atomics)
-  unsigned* ticket;  // one per column tile, zero-initialised, re-armed by the last arrival
+  double* slab;      // [cap + cap / 8 + 1][4][ld]: level-1 rows, then level-2 rows (null: atomics)
+  unsigned* ticket;  // [kDetTiles][kDetTickets], zero-initialised, re-armed by the last arrivals
+  int cap;           // level-1 rows (producer rows of one launch) the slab holds
 };
+// rows per level-1 group for a launch of `nrows` producer rows (at most kDetTickets - 1 groups)
+__host__ __device__ inline int det_group(int nrows) {
+  const int g = (nrows + kDetTickets - 2) / (kDetTickets - 1);
+  return g > 8 ? g : 8;
+}
+__host__ __device__ inline size_t det_slab_rows(int cap) { return (size_t)cap + cap / 8 + 1; }
 
 struct BnSide {
   int n, ld;        // width, padded row stride
@@ -76,16 +87,41 @@ __device__ __forceinline__ bool det_arrive(unsigned* ticket, unsigned expected, 
   return *s_flag != 0;
 }
 
-// The last arrival's fixed-order sum: out[k * ld + c] = sum over rows r < nrows (in order) of
-// slab[(r * 4 + k) * ld + c], for k < 4 and c in [c0, c1).
-__device__ __forceinline__ void det_reduce(const double* slab, int nrows, int ld, int c0, int c1, double* out) {
+// Fixed-order sum of nr consecutive slab rows from row r0: dst[k * ld + c] = sum over rows (in
+// order) of src[((r0 + r) * 4 + k) * ld + c], k < 4, c in [c0, c1); 16 loads in flight per thread.
+__device__ __forceinline__ void det_sum_rows(const double* src, int r0, int nr, int ld, int c0, int c1,
+                                             double* dst) {
   const int w = c1 - c0;
   for (int i = threadIdx.x; i < 4 * w; i += blockDim.x) {
     const int k = i / w, c = c0 + i - k * w;
+    const double* p = src + ((size_t)r0 * 4 + k) * ld + c;
     double a = 0.0;
-    for (int r = 0; r < nrows; ++r) a += slab[((size_t)r * 4 + k) * ld + c];
-    out[(size_t)k * ld + c] = a;
+    for (int r = 0; r < nr; r += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = r + u < nr ? p[(size_t)(r + u) * 4 * ld] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a += v[u];
+    }
+    dst[(size_t)k * ld + c] = a;
   }
+}
+
+// Producer `row` of `nrows` (block-uniform call) has stored its slab row for column tile `tile`
+// (columns [c0, c1)): arrive, and sum what this workgroup arrived last for (module comment).
+__device__ __forceinline__ void det_publish(const DetAcc& d, int tile, int row, int nrows, int ld, int c0, int c1,
+                                            double* out, int* s_flag) {
+  unsigned* tk = d.ticket + tile * kDetTickets;
+  const int G = det_group(nrows), ng = (nrows + G - 1) / G;
+  if (ng == 1) {
+    if (det_arrive(tk, (unsigned)nrows, s_flag)) det_sum_rows(d.slab, 0, nrows, ld, c0, c1, out);
+    return;
+  }
+  const int g = row / G, gn = min(G, nrows - g * G);
+  if (!det_arrive(tk + 1 + g, (unsigned)gn, s_flag)) return;
+  double* lvl2 = d.slab + (size_t)nrows * 4 * ld;
+  det_sum_rows(d.slab, g * G, gn, ld, c0, c1, lvl2 + (size_t)g * 4 * ld);
+  if (det_arrive(tk, (unsigned)ng, s_flag)) det_sum_rows(lvl2, 0, ng, ld, c0, c1, out);
 }
 
 // Forward coefficients of column c (< n), tower t, from the step's sums s = sum z, q = sum z^2
@@ -207,8 +243,7 @@ __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int l
   }
   if (det.slab) {
     __shared__ int s_last;
-    if (det_arrive(det.ticket + bx, (unsigned)nby, &s_last))
-      det_reduce(det.slab, nby, ldz, bx * 64, min(bx * 64 + 64, ncol), fsum);
+    det_publish(det, bx, by, nby, ldz, bx * 64, min(bx * 64 + 64, ncol), fsum, &s_last);
   }
 }
 

@@ -254,8 +254,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     }
     if (fs.bdet.slab) {
       __shared__ int s_last;
-      if (det_arrive(fs.bdet.ticket, (unsigned)nrow_blocks, &s_last))
-        det_reduce(fs.bdet.slab, nrow_blocks, ld, 0, n, fs.bsum);
+      det_publish(fs.bdet, 0, blockIdx.x, nrow_blocks, ld, 0, n, fs.bsum, &s_last);
     }
   }
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block
@@ -301,6 +300,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
+  if (fs.bdet.slab && (cdiv(bs, nw) > fs.bdet.cap || ld > 64 * kDetTiles)) return hipErrorInvalidValue;
   // The loss partials are always summed by a later launch: a second tiny launch here when the
   // caller does not defer.  (The in-kernel alternative, an agent-scope release + ticket in EVERY
   // workgroup so that the last one can sum, writes back the XCD's L2 once per workgroup -- the dy

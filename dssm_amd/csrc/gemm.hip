@@ -517,8 +517,7 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
     }
     if (f.det.slab) {
       __shared__ int s_det;
-      if (det_arrive(f.det.ticket + tx, (unsigned)f.det_rows, &s_det))
-        det_reduce(f.det.slab, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum);
+      det_publish(f.det, tx, ty, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum, &s_det);
     }
   }
 }
@@ -802,8 +801,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     }
     if (f.det.slab) {
       __shared__ int s_det;
-      if (det_arrive(f.det.ticket + tx, (unsigned)f.det_rows, &s_det))
-        det_reduce(f.det.slab, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum);
+      det_publish(f.det, tx, ty, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum, &s_det);
     }
   }
   if (lds_epi) {
@@ -1099,6 +1097,11 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
   return hipGetLastError();
 }
 
+// deterministic statistics: the launch's producer rows fit the slab, its column tiles the tickets
+static bool det_fits(const NtFuse& f, int ld) {
+  return !f.det.slab || (f.det_rows <= f.det.cap && cdiv(ld, 64) <= kDetTiles);
+}
+
 hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
                                     int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
@@ -1120,6 +1123,7 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
 #define DSSM_NTWK(WM)                                                                         \
   {                                                                                           \
     f.det_rows = cdiv(M, 32 * WM);                                                            \
+    if (!det_fits(f, ldc)) return hipErrorInvalidValue;                                       \
     const int ntiles = nx * cdiv(M, 32 * WM);                                                 \
     hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),    \
                        dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
@@ -1129,6 +1133,7 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     return hipGetLastError();
   }
   f.det_rows = cdiv(M, 64);
+  if (!det_fits(f, ldc)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 64)), dim3(256), 0, s, a, f);
   return hipGetLastError();
 }
@@ -1167,6 +1172,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
       // the slabs (launch_splitk_reduce) after that launch.
       *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
       f.det_rows = cdiv(M, kWkRows == 64 ? 64 : 128);
+      if (!det_fits(f, ldda)) return hipErrorInvalidValue;
       if (kWkRows == 64)
         hipLaunchKernelGGL(k_pair_da_wk<2>, dim3(nt_blocks64), dim3(256), wk_smem_bytes(Kp, f.lds_epi, 2),
                            s, a, f, nt_x, nt_blocks64);
@@ -1180,6 +1186,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
     const int tn_blocks = tn_x * tn_y * nsplit;
     const size_t smem = std::max(wk_smem_bytes(Kp, f.lds_epi), tw_smem_bytes());
     f.det_rows = cdiv(M, 128);
+    if (!det_fits(f, ldda)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bwd_pair_wk, dim3(nt_blocks + tn_blocks), dim3(512), smem, s, a, f, nt_x,
                        nt_blocks, p, tn_x, tn_y);
     *deferred_splits = 0;
@@ -1204,6 +1211,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
   const int tn_blocks = tn_x * tn_y * nsplit;
   f.det_rows = cdiv(M, 64);
+  if (!det_fits(f, ldda)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
                      nt_blocks, p, tn_x, tn_y);
   *deferred_splits = 0;

@@ -292,7 +292,8 @@ struct AdamStep {
   // deterministic mode: a multi-item heavy column's items store their partial rows here ([item][n],
   // write-through) and its last arrival sums them in item order (no fp32 atomics)
   float* heavy_slab;
-  // the NEXT step's CSC rank pass as the launch's first workgroups (csc.h; rank.nblocks == 0: none),
+  // the NEXT step's CSC rank pass as extra workgroups (csc.h; rank.nblocks == 0: none), LAST in
+  // dispatch order by default (build knob DSSM_RANK_POS in adam.hip: 0 first, 2 after the heavy items),
   // with heavy_reset: the heavy-item count this step's scan filled, zeroed by the last block once
   // every block has read it (the next step's rank launch, which would zero it, is skipped)
   CscRankRole rank;

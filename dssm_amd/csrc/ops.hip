@@ -247,6 +247,25 @@ int dssm_spmm_csr_bwd_w(const int32_t* indptr, const int32_t* indices, const flo
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
+int dssm_csc_transpose(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                       int max_nnz, int row_order, int32_t* col_ptr, int32_t* csc_row, float* csc_val,
+                       int32_t* csc_col, void* ws, void* stream) {
+  if (!indptr || !col_ptr || !csc_row || !csc_val || !csc_col || !ws || rows <= 0 || D <= 0 || max_nnz < 0 ||
+      (max_nnz && (!indices || !values)))
+    return oerr(DSSM_E_INVALID, "csc_transpose: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const SpmmWs w = spmm_ws(rows, D, max_nnz);
+  char* b = static_cast<char*>(ws);
+  int* scratch = reinterpret_cast<int*>(b + w.scratch);
+  // row order: the transpose lands in the workspace's arrays, the row sort writes the caller's
+  int* srow = row_order ? reinterpret_cast<int*>(b + w.row) : nullptr;
+  float* sval = row_order ? reinterpret_cast<float*>(b + w.val) : nullptr;
+  const hipError_t e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, csc_row,
+                                              csc_val, csc_col, s, nullptr, 0, dssm::csc_rank_supported(D), false,
+                                              srow, sval);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
 size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype) {
   return dssm::gemm_dw_slab_floats(K + 1, N, M, dtype == DSSM_BF16);
 }

@@ -173,13 +173,14 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
     Lt.sums = take(sums);
     Lt.sums_bytes = sums;
-    // producer rows of any fused-statistics launch: 64-row tiles bound them all
+    // producer rows of any fused-statistics launch: 64-row tiles bound them all (the launchers
+    // check), plus the reduction tree's level-2 rows (bnfuse.h det_publish)
     Lt.det_rows = (int)((R + 63) / 64) + 2;
     for (int l = 0; l < Lt.L; ++l) {
-      const size_t slab = (size_t)Lt.det_rows * 4 * Lt.ldp[l] * 8;
+      const size_t slab = dssm::det_slab_rows(Lt.det_rows) * 4 * Lt.ldp[l] * 8;
       Lt.fslab[l] = take(slab);
       Lt.bslab[l] = take(slab);
-      Lt.det_ticket[l] = take(2 * 8 * 64);  // [fwd | bwd][column tile], one 64-B line each
+      Lt.det_ticket[l] = take(2 * dssm::kDetTiles * dssm::kDetTickets * 4);  // [fwd | bwd][tile][ticket]
     }
     size_t o = Lt.sums;
     for (int l = 0; l < Lt.L; ++l) {
@@ -335,8 +336,8 @@ struct dssm_plan {
     b.bsum = at<double>(Lt.bsum[l]);
     if (deterministic() && Lt.det_rows) {
       unsigned* tk = at<unsigned>(Lt.det_ticket[l]);
-      b.fdet = dssm::DetAcc{at<double>(Lt.fslab[l]), tk};
-      b.bdet = dssm::DetAcc{at<double>(Lt.bslab[l]), tk + 8 * 16};
+      b.fdet = dssm::DetAcc{at<double>(Lt.fslab[l]), tk, Lt.det_rows};
+      b.bdet = dssm::DetAcc{at<double>(Lt.bslab[l]), tk + dssm::kDetTiles * dssm::kDetTickets, Lt.det_rows};
     }
     return b;
   }

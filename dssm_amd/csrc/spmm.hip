@@ -632,54 +632,185 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
 // fill place a column's entries in an order set by atomics (per-block slot reservations, LDS
 // histogram arrival), which changes the fp32 summation order of dW1 from run to run; this pass
 // rewrites each column [col_ptr[c], col_ptr[c+1]) of (row_in, val_in) sorted by row into
-// (row_out, val_out).  One workgroup per column: the column's rows are set in an LDS bitmap
-// (window of kSortWin rows at a time; a row appears at most once per column) with its value
-// beside it, then the bitmap's block-wide prefix count gives every entry its slot.
-constexpr int kSortWin = 8192;  // rows per window: one 32-bit bitmap word per thread
-__global__ __launch_bounds__(256) void k_csc_sort_rows(const int* __restrict__ col_ptr, int rows,
-                                                       const int* __restrict__ row_in,
-                                                       const float* __restrict__ val_in,
-                                                       int* __restrict__ row_out,
-                                                       float* __restrict__ val_out) {
-  static_assert(kSortWin / 32 == 256, "one bitmap word per thread");
-  __shared__ unsigned bits[kSortWin / 32];
-  __shared__ float vals[kSortWin];
-  __shared__ int s_wave[4];
-  const int c = blockIdx.x, t = threadIdx.x;
-  const int s = col_ptr[c], e = col_ptr[c + 1];
-  if (s == e) return;  // uniform over the workgroup
-  if (e - s == 1) {    // a single entry is in order
-    if (t == 0) {
+// (row_out, val_out).  Workgroup b takes columns b + k * grid, k < kSortWaves (one workgroup per column
+// left the launch dominated by 30k workgroup dispatches: most columns hold a handful of entries):
+// * up to kSortWaveMax entries: one WAVE per column.  Its rows are set in the wave's LDS bitmap (a
+//   window of kSortWin rows at a time; a row appears at most once per column), a wave prefix count
+//   of the bitmap words gives every entry its slot, and each lane writes its own entries there;
+// * longer (the Zipf-hot columns): afterwards the whole workgroup per column, the same scheme over
+//   all the waves' bitmap words (a kSortWinWg-row window); the virtual ones column is already in
+//   row order (slot col_ptr[D] + row) and is copied.
+// A column holding a row twice (a CSR row with a repeated column: never from CountVectorizer, but
+// legal input) shows as fewer bits than entries in a window; it is then ranked by (row, value bits,
+// input slot) in O(n^2) work instead -- equal keys are identical entries, so the output is still a
+// function of the batch alone.
+constexpr int kSortWaves = 8;
+constexpr int kSortNT = 64 * kSortWaves;
+constexpr int kSortWords = 4;                        // bitmap words per lane
+constexpr int kSortWin = 64 * 32 * kSortWords;       // rows per window of a wave
+constexpr int kSortWinWg = kSortWaves * kSortWin;    // rows per window of the workgroup
+constexpr int kSortWaveMax = 512;
+
+// rank of entry i among [s, e) by (row, value bits, slot): the duplicate-row fallback
+__device__ __forceinline__ int sort_rank_slow(const int* __restrict__ row_in, const float* __restrict__ val_in,
+                                              int s, int e, int i, int ri, unsigned bi) {
+  int p = s;
+  for (int j = s; j < e; ++j) {
+    const int rj = row_in[j];
+    const unsigned bj = __float_as_uint(val_in[j]);
+    p += rj < ri || (rj == ri && (bj < bi || (bj == bi && j < i)));
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict__ col_ptr, int D, int rows,
+                                                           const int* __restrict__ row_in,
+                                                           const float* __restrict__ val_in,
+                                                           int* __restrict__ row_out,
+                                                           float* __restrict__ val_out) {
+  __shared__ unsigned bits[kSortWaves * 64 * kSortWords];
+  __shared__ int wpre[kSortWaves * 64 * kSortWords];
+  __shared__ int s_wave[kSortWaves];
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  unsigned* wbits = bits + wv * 64 * kSortWords;
+  int* wp = wpre + wv * 64 * kSortWords;
+  {
+    const int c = blockIdx.x + wv * gridDim.x;  // strided: hot columns of nearby ids spread out
+    const int s = c <= D ? col_ptr[c] : 0, e = c <= D ? col_ptr[c + 1] : 0;
+    if (e - s == 1 && lane == 0) {  // in order
       row_out[s] = row_in[s];
       val_out[s] = val_in[s];
     }
-    return;
-  }
-  int base = s;
-  for (int w0 = 0; w0 < rows; w0 += kSortWin) {
-    const int wn = min(kSortWin, rows - w0);
-    bits[t] = 0u;
-    __syncthreads();
-    for (int i = s + t; i < e; i += 256) {
-      const int r = row_in[i] - w0;
-      if (r >= 0 && r < wn) {
-        atomicOr(&bits[r >> 5], 1u << (r & 31));
-        vals[r] = val_in[i];
+    // the window loop's bounds stay workgroup-uniform (barriers); other waves idle through it
+    const bool sort = e - s > 1 && e - s <= kSortWaveMax;
+    bool dup = false;  // wave-uniform
+    int base = s;
+    for (int w0 = 0; w0 < rows; w0 += kSortWin) {
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) wbits[lane * kSortWords + j] = 0u;
+      __syncthreads();
+      int nin = 0;  // the column's entries in this window (duplicates: more than its bits)
+      if (sort)
+        for (int i = s + lane; i < e; i += 64) {
+          const int r = row_in[i] - w0;
+          if (r >= 0 && r < kSortWin) {
+            atomicOr(&wbits[r >> 5], 1u << (r & 31));
+            ++nin;
+          }
+        }
+      __syncthreads();
+      unsigned m[kSortWords];
+      int own = 0;
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) {
+        m[j] = wbits[lane * kSortWords + j];
+        own += __popc(m[j]);
       }
+      int inc = own;  // wave inclusive scan of the lanes' counts
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+      }
+      int run = inc - own;
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) {
+        wp[lane * kSortWords + j] = run;
+        run += __popc(m[j]);
+      }
+      const int total = __shfl(inc, 63, 64);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) nin += __shfl_xor(nin, d, 64);
+      dup = dup || nin != total;
+      __syncthreads();
+      if (sort && !dup)
+        for (int i = s + lane; i < e; i += 64) {
+          const int rr = row_in[i], r = rr - w0;
+          if (r >= 0 && r < kSortWin) {
+            const int wd = r >> 5;
+            const int p = base + wp[wd] + __popc(wbits[wd] & ((1u << (r & 31)) - 1u));
+            row_out[p] = rr;
+            val_out[p] = val_in[i];
+          }
+        }
+      base += total;
+      __syncthreads();
     }
-    __syncthreads();
-    unsigned m = bits[t];
-    int tot;
-    int p = base + block_excl_scan<256>(__popc(m), s_wave, tot);
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      row_out[p] = w0 + t * 32 + b;
-      val_out[p] = vals[t * 32 + b];
-      ++p;
+    if (sort && dup)
+      for (int i = s + lane; i < e; i += 64) {
+        const int ri = row_in[i];
+        const float vi = val_in[i];
+        const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
+        row_out[p] = ri;
+        val_out[p] = vi;
+      }
+  }
+  // the long columns of this workgroup, one at a time with every wave
+  for (int k = 0; k < kSortWaves; ++k) {
+    const int c = blockIdx.x + k * gridDim.x;
+    if (c > D) break;  // uniform
+    const int s = col_ptr[c], e = col_ptr[c + 1];
+    if (e - s <= kSortWaveMax) continue;
+    if (c == D) {  // the ones column: slot col_ptr[D] + row already
+      for (int i = s + t; i < e; i += kSortNT) {
+        row_out[i] = row_in[i];
+        val_out[i] = val_in[i];
+      }
+      continue;
     }
-    base += tot;
-    __syncthreads();
+    bool dup = false;
+    int base = s;
+    for (int w0 = 0; w0 < rows; w0 += kSortWinWg) {
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) bits[t * kSortWords + j] = 0u;
+      __syncthreads();
+      int nin = 0;
+      for (int i = s + t; i < e; i += kSortNT) {
+        const int r = row_in[i] - w0;
+        if (r >= 0 && r < kSortWinWg) {
+          atomicOr(&bits[r >> 5], 1u << (r & 31));
+          ++nin;
+        }
+      }
+      __syncthreads();
+      unsigned m[kSortWords];
+      int own = 0;
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) {
+        m[j] = bits[t * kSortWords + j];
+        own += __popc(m[j]);
+      }
+      int total, nin_total;
+      int run = block_excl_scan<kSortNT>(own, s_wave, total);
+      (void)block_excl_scan<kSortNT>(nin, s_wave, nin_total);
+#pragma unroll
+      for (int j = 0; j < kSortWords; ++j) {
+        wpre[t * kSortWords + j] = run;
+        run += __popc(m[j]);
+      }
+      dup = dup || nin_total != total;
+      __syncthreads();
+      if (!dup)
+        for (int i = s + t; i < e; i += kSortNT) {
+          const int rr = row_in[i], r = rr - w0;
+          if (r >= 0 && r < kSortWinWg) {
+            const int wd = r >> 5;
+            const int p = base + wpre[wd] + __popc(bits[wd] & ((1u << (r & 31)) - 1u));
+            row_out[p] = rr;
+            val_out[p] = val_in[i];
+          }
+        }
+      base += total;
+      __syncthreads();
+    }
+    if (dup)
+      for (int i = s + t; i < e; i += kSortNT) {
+        const int ri = row_in[i];
+        const float vi = val_in[i];
+        const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
+        row_out[p] = ri;
+        val_out[p] = vi;
+      }
   }
 }
 
@@ -873,6 +1004,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
   int* cnt = scratch;
   int* pos_tmp = scratch + 2 * (D + 1 + 64);
   const int nsum_x = cdiv(ldz, 64), nsum = nsum_x * cdiv(rows, kSumsRows);
+  if (det && det->slab && (cdiv(rows, kSumsRows) > det->cap || nsum_x > kDetTiles)) return hipErrorInvalidValue;
   if (scatter_out) {
     constexpr int nb = 384;  // scatter workgroups beside the cosine launch
     *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
@@ -911,8 +1043,8 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 
 hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
                            int* row_out, float* val_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_csc_sort_rows, dim3(D + 1), dim3(256), 0, s, col_ptr, rows, row_in, val_in, row_out,
-                     val_out);
+  hipLaunchKernelGGL(k_csc_sort_rows, dim3(cdiv(D + 1, kSortWaves)), dim3(kSortNT), 0, s, col_ptr, D,
+                     rows, row_in, val_in, row_out, val_out);
   return hipGetLastError();
 }
 
@@ -967,8 +1099,8 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                        values, rows, D, cursor, col_ptr, out_row, out_val, csc_col);
   }
   if (sort_row)
-    hipLaunchKernelGGL(k_csc_sort_rows, dim3(D + 1), dim3(256), 0, s, col_ptr, rows, sort_row,
-                       sort_val, csc_row, csc_val);
+    hipLaunchKernelGGL(k_csc_sort_rows, dim3(cdiv(D + 1, kSortWaves)), dim3(kSortNT), 0, s, col_ptr,
+                       D, rows, sort_row, sort_val, csc_row, csc_val);
   return hipGetLastError();
 }
 

@@ -65,6 +65,9 @@ class RnnDSSM:
             if not self.lib.dssm_rnn_bf16_supported(self.E, self.H):
                 raise ValueError("bf16 RNN: (E, H) in {(128, 128), (64, 128), (32, 32)}")
             ws = self.lib.dssm_rnn_bf16_ws_bytes(self.R, self.T, self.E, self.H, self.V)
+            if ws == 0 or self.V > 32768:
+                raise ValueError(f"bf16 RNN: vocabulary of {self.V} words exceeds the embedding-gradient "
+                                 "token scan's 32768-word limit (use dtype='fp32')")
             self.ws = torch.zeros(int(ws), dtype=torch.uint8, device=dev)
         else:
             ws = self.lib.dssm_rnn_ws_floats(self.R, self.T, self.E, self.H)

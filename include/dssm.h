@@ -308,6 +308,15 @@ size_t dssm_spmm_bwd_ws_bytes(int rows, int D, int max_nnz);
 int dssm_spmm_csr_bwd_w(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
                         int D, int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* dWb,
                         void* ws, void* stream);
+/* The CSC transpose [X | 1]^T that the weight gradient above gathers over: column c
+ * (< D) holds the batch entries of trigram c, column D the virtual ones column (row r at slot
+ * col_ptr[D] + r).  col_ptr [D + 2], csc_row / csc_val / csc_col [max_nnz + rows].  row_order != 0:
+ * every column's entries in ascending row order (the deterministic mode's transpose; scipy's
+ * tocsc() order); 0: per-column order set by atomics.  ws: dssm_spmm_bwd_ws_bytes() bytes,
+ * zero-filled before first use. */
+int dssm_csc_transpose(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                       int max_nnz, int row_order, int32_t* col_ptr, int32_t* csc_row, float* csc_val,
+                       int32_t* csc_col, void* ws, void* stream);
 /* add_layer / tf.matmul(x, W) + b autodiff (new_dssm.py:146-148): dA [M x ldda] = dZ W^T (dA may be
  * NULL), dWb [(K+1) x N] = [A | 1]^T dZ (row K = db).  A [M x lda], W [K x ldw], dZ [M x lddz] of
  * dtype; fp32 accumulation; slab: dssm_dense_bwd_slab_floats() floats (split-K partials). */

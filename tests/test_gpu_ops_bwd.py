@@ -49,6 +49,64 @@ def test_spmm_csr_bwd_w(D, rows, n, dt):
         _close(out.cpu().numpy(), X.T @ dZ.astype(np.float64), 1e-5)
 
 
+def _csc_expected(ip, ix, vv, rows, D):
+    """[X | 1]^T as CSC with every column in ascending row order (ties: value bits), NumPy."""
+    r = np.repeat(np.arange(rows, dtype=np.int64), np.diff(ip))
+    c = np.concatenate([ix.astype(np.int64), np.full(rows, D)])
+    rr = np.concatenate([r, np.arange(rows)])
+    v = np.concatenate([vv, np.ones(rows, np.float32)])
+    order = np.lexsort((v.view(np.uint32), rr, c))
+    ptr = np.zeros(D + 2, np.int64)
+    np.add.at(ptr, c + 1, 1)
+    return np.cumsum(ptr), rr[order], v[order], c[order]
+
+
+@pytest.mark.parametrize("D,rows,dups", [(30000, 6144, False), (5000, 9000, False), (700, 64, False),
+                                         (3000, 4096, True)])
+@pytest.mark.parametrize("row_order", [1, 0])
+def test_csc_transpose(D, rows, dups, row_order):
+    """dssm_csc_transpose: row_order 1 (the deterministic mode's wave-per-column row sort, one and two
+    8192-row windows) equals NumPy's row-ordered transpose exactly; row_order 0 holds the same
+    entries per column.  `dups`: CSR rows repeating a column (a hot one included), the sort's
+    (row, value, slot) ranking path."""
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(7))
+    ip, ix, vv = synth_rows(rng, ZipfColumns(D), rows, 24.0)
+    if dups:  # every 7th row repeats its first column with another value, every 11th column 0 twice
+        parts = []
+        for r in range(rows):
+            cols, vals = list(ix[ip[r]:ip[r + 1]]), list(vv[ip[r]:ip[r + 1]])
+            if r % 7 == 0:
+                cols.append(cols[0]), vals.append(5.0)
+            if r % 11 == 0:
+                cols += [0, 0]
+                vals += [1.0, 7.0]
+            parts.append((cols, vals))
+        ip = np.concatenate([[0], np.cumsum([len(c) for c, _ in parts])]).astype(np.int32)
+        ix = np.concatenate([c for c, _ in parts]).astype(np.int32)
+        vv = np.concatenate([v for _, v in parts]).astype(np.float32)
+    max_nnz = int(ip[-1])
+    ptr_e, row_e, val_e, col_e = _csc_expected(ip, ix, vv, rows, D)
+    ws = torch.zeros(lib.dssm_spmm_bwd_ws_bytes(rows, D, max_nnz), dtype=torch.uint8, device="cuda")
+    t = [torch.from_numpy(x).cuda() for x in (ip, ix, vv)]
+    ent = max_nnz + rows
+    cp = torch.zeros(D + 2, dtype=torch.int32, device="cuda")
+    cr, cc = (torch.zeros(ent, dtype=torch.int32, device="cuda") for _ in range(2))
+    cv = torch.zeros(ent, dtype=torch.float32, device="cuda")
+    for _ in range(2):  # the scratch must be re-armed by the call itself
+        check(lib.dssm_csc_transpose(ptr(t[0]), ptr(t[1]), ptr(t[2]), rows, D, max_nnz, row_order, ptr(cp),
+                                     ptr(cr), ptr(cv), ptr(cc), ptr(ws), _lib.stream_ptr()), "csc_transpose")
+        torch.cuda.synchronize()
+        gp, gr, gv, gc = (x.cpu().numpy() for x in (cp, cr, cv, cc))
+        assert np.array_equal(gp, ptr_e)
+        assert np.array_equal(gc, col_e)
+        if row_order:
+            assert np.array_equal(gr, row_e) and np.array_equal(gv.view(np.uint32), val_e.view(np.uint32))
+        else:
+            o = np.lexsort((gv.view(np.uint32), gr, gc))
+            assert np.array_equal(gr[o], row_e) and np.array_equal(gv[o], val_e)
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_dense_bwd(dt):
     lib = _lib.load()
