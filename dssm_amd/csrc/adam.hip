@@ -146,7 +146,7 @@ __device__ __forceinline__ RowEntries row_entries(const AdamStep& a, int s, int 
   return r;
 }
 
-template <typename TZ>
+template <typename TZ, bool WIRE>
 __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha,
                                        const RowEntries* pre = nullptr) {
   const int lane = lane_id();
@@ -161,7 +161,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     const size_t o = (size_t)c * n + cc;
     float P[8], M[8], V[8], G[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #if !DSSM_ADAM_LATE_PMV
-    if (nvalid > 0 && !a.gout) {  // stream loads first: independent of the gather chain below
+    if (nvalid > 0 && !(WIRE && a.gout)) {  // stream loads first: independent of the gather chain below
       ld_stream8(a.p + o, nvalid, P);
       ld_stream8(a.m + o, nvalid, M);
       ld_stream8(a.v + o, nvalid, V);
@@ -184,7 +184,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
       ld_stream8(a.v + o, nvalid, V);
     }
 #endif
-    if (nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
+    if (WIRE && nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
       const int k = nvalid >= 8 ? 8 : 4;
       if (c < a.D) {
         u16* q = a.gout + wire_row_off(a.geo, c) + cc;
@@ -233,8 +233,9 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
 }
 
 // Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
+template <bool WIRE>
 __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
-  if (a.gout) {  // gradient pass
+  if (WIRE && a.gout) {  // gradient pass
     const int64_t wo = c < a.D ? wire_row_off(a.geo, c) : 0;
     for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
       if (c < a.D) a.gout[wo + j] = f2bf(grow[j]);
@@ -268,7 +269,7 @@ struct HeavyLds {
   int last;
 };
 
-template <typename TZ>
+template <typename TZ, bool WIRE>
 __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb, HeavyLds& L) {
   float(&part)[4][512] = L.part;
   float(&grow)[512] = L.grow;
@@ -279,7 +280,8 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
   for (int it = hb; it < nitems; it += a.item_blocks) {
     const int2 item = a.heavy_items[it];
     const int c = item.x;
-    if (!in_chunk(a, c)) continue;  // uniform over the workgroup
+    if constexpr (WIRE)
+      if (!in_chunk(a, c)) continue;  // uniform over the workgroup
     const int cs = a.col_ptr[c], ce = a.col_ptr[c + 1];
     const int i0 = cs + item.y * kHeavyItem;
     const int s = min(ce, i0 + wv * (kHeavyItem / 4)), e = min(ce, s + kHeavyItem / 4);
@@ -304,7 +306,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       __syncthreads();
     }
     if (nit == 1) {
-      w1_row_from(a, c, grow, alpha);
+      w1_row_from<WIRE>(a, c, grow, alpha);
     } else {
       // Deterministic mode: the slab rows are released before this workgroup's arrival and the
       // last arrival acquires before reading them (common.h).  Atomics mode: every access to the
@@ -341,7 +343,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
                                             __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        w1_row_from(a, c, grow, alpha);
+        w1_row_from<WIRE>(a, c, grow, alpha);
       }
     }
     __syncthreads();
@@ -354,7 +356,10 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
 // only needs every other block to have READ them, which precedes their arrival) advances them
 // (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
 // the ticket.
-template <typename TZ>
+// WIRE: the data-parallel variants (gradient pass, chunked rows, bf16 wire / stage in the dense
+// range); the single-GPU step compiles without them (their row remapping and per-element wire tests
+// in the W1 and streaming loops cost the fused step 16 us: 57.5 -> 75 us measured)
+template <typename TZ, bool WIRE>
 __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
@@ -387,57 +392,85 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   if (is_rank) {
     csc_rank_role(a.rank, bx - rs, reinterpret_cast<unsigned*>(s_lds));
   } else if (b0 < nh) {
-    heavy_items<TZ>(a, alpha, b0, *reinterpret_cast<HeavyLds*>(s_lds));
+    heavy_items<TZ, WIRE>(a, alpha, b0, *reinterpret_cast<HeavyLds*>(s_lds));
   } else if (w1_role) {
     const int b = DSSM_ADAM_ORDER == 0 ? b0 - nh : b0 - nh - nd;
     // the next row's column range is loaded while this row is processed (one dependent load
     // fewer on each row's chain)
-    // rows by slot v (wave-uniform: scalar row state); every row, or one wire chunk's rows
     const int stride = a.w1_blocks * 4;
-    const int nv = w1_role_rows(a);
-    int v = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    auto range = [&](int vv, int& rs, int& re) {
-      const int c = vv < nv ? w1_role_row(a, vv) : -1;
-      rs = re = 0;
-      if (c >= 0) {
-        rs = a.col_ptr[c];
-        re = a.col_ptr[c + 1];
+    if constexpr (!WIRE) {
+      // every row [0, D]; c stays wave-uniform (scalar row state: a lane-varying form of this loop,
+      // a row-slot remapping through a lambda, measured 57.5 -> 75 us)
+      int c = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      int s = 0, e = 0;
+      if (c <= a.D) {
+        s = a.col_ptr[c];
+        e = a.col_ptr[c + 1];
       }
-      return c;
-    };
-    int s, e;
-    int c = range(v, s, e);
 #if DSSM_ADAM_PRE_IDX
-    // two rows ahead: the column range; one row ahead: the light row's CSC entries
-    int sn, en;
-    int cn = range(v + stride, sn, en);
-    RowEntries ent = row_entries(a, s, e);
-    for (; v < nv; v += stride) {
-      int s2, e2;
-      const int c2 = range(v + 2 * stride, s2, e2);
-      const RowEntries next = row_entries(a, sn, en);
-      if (c >= 0) w1_row<TZ>(a, c, s, e, alpha, &ent);
-      c = cn;
-      s = sn;
-      e = en;
-      cn = c2;
-      sn = s2;
-      en = e2;
-      ent = next;
-    }
+      // two rows ahead: the column range; one row ahead: the light row's CSC entries
+      int sn = 0, en = 0;
+      if (c + stride <= a.D) {
+        sn = a.col_ptr[c + stride];
+        en = a.col_ptr[c + stride + 1];
+      }
+      RowEntries ent = row_entries(a, s, e);
+      for (; c <= a.D; c += stride) {
+        const int c2 = c + 2 * stride;
+        int s2 = 0, e2 = 0;
+        if (c2 <= a.D) {
+          s2 = a.col_ptr[c2];
+          e2 = a.col_ptr[c2 + 1];
+        }
+        const RowEntries next = row_entries(a, sn, en);
+        w1_row<TZ, false>(a, c, s, e, alpha, &ent);
+        s = sn;
+        e = en;
+        sn = s2;
+        en = e2;
+        ent = next;
+      }
 #else
-    for (; v < nv; v += stride) {
-      int sn, en;
-      const int cn = range(v + stride, sn, en);
-      if (c >= 0) w1_row<TZ>(a, c, s, e, alpha);
-      c = cn;
-      s = sn;
-      e = en;
-    }
+      for (; c <= a.D; c += stride) {
+        const int cn = c + stride;
+        int sn = 0, en = 0;
+        if (cn <= a.D) {
+          sn = a.col_ptr[cn];
+          en = a.col_ptr[cn + 1];
+        }
+        w1_row<TZ, false>(a, c, s, e, alpha);
+        s = sn;
+        e = en;
+      }
 #endif
+    } else {
+      // rows by slot v: every row, or one wire chunk's rows (w1_role_row); wave-uniform
+      const int nv = w1_role_rows(a);
+      int v = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      auto range = [&](int vv, int& rs, int& re) {
+        const int c = __builtin_amdgcn_readfirstlane(vv < nv ? w1_role_row(a, vv) : -1);
+        rs = re = 0;
+        if (c >= 0) {
+          rs = a.col_ptr[c];
+          re = a.col_ptr[c + 1];
+        }
+        return c;
+      };
+      int s, e;
+      int c = range(v, s, e);
+      int sn, en;
+      int cn = range(v + stride, sn, en);
+      for (; v < nv; v += stride) {
+        if (c >= 0) w1_row<TZ, true>(a, c, s, e, alpha);
+        c = cn;
+        s = sn;
+        e = en;
+        cn = range(v + 2 * stride, sn, en);
+      }
+    }
   } else {
     const int bi = DSSM_ADAM_ORDER == 0 ? b0 - nh - nw : b0 - nh;
-    if (a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
+    if (WIRE && a.w1_flat && a.gout) {  // gradient pass: an untouched row's gradient is zero
       const int nv = w1_role_rows(a) - 1;  // W1 rows only (b1's row is never untouched)
       const int q = a.n / 4;
       const int64_t w4 = (int64_t)nv * q;
@@ -458,10 +491,10 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
     for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < na + nt;
          j += (int64_t)a.dense_blocks * blockDim.x) {
       const int64_t i = j < na ? a.d4_begin + j : a.t4_begin + (j - na);
-      const bool wired = i < a.wire4;
+      const bool wired = WIRE && i < a.wire4;
       float4 pp = ld_stream4(a.p + i * 4);
       float4 gg;
-      if (wired && a.gstage) {
+      if (WIRE && wired && a.gstage) {
         // one bf16 rounding per rank's gradient, the sum over ranks in fp32 (fixed rank order)
         gg = make_float4(0.f, 0.f, 0.f, 0.f);
         const uint2* st = reinterpret_cast<const uint2*>(a.gstage) + (i - a.gbase4);
@@ -472,7 +505,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
           gg.z += __uint_as_float(q.y << 16);
           gg.w += __uint_as_float(q.y & 0xffff0000u);
         }
-      } else if (wired) {
+      } else if (WIRE && wired) {
         const uint2 q = reinterpret_cast<const uint2*>(a.gwire)[i];
         gg = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                          __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
@@ -490,7 +523,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       st_stream4(a.v + i * 4, vv);
       if (i * 4 >= a.clear_from)
         reinterpret_cast<float4*>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (wired) {
+      if (WIRE && wired) {
         uint2 q;
         q.x = pack2bf(pp.x, pp.y);
         q.y = pack2bf(pp.z, pp.w);
@@ -619,10 +652,16 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
-  if (dz_bf16)
-    hipLaunchKernelGGL(k_adam_step<u16>, grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL(k_adam_step<float>, grid, block, 0, s, a);
+  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire;
+#define DSSM_ADAM_LAUNCH(TZ)                                                         \
+  if (wire) hipLaunchKernelGGL((k_adam_step<TZ, true>), grid, block, 0, s, a);       \
+  else hipLaunchKernelGGL((k_adam_step<TZ, false>), grid, block, 0, s, a)
+  if (dz_bf16) {
+    DSSM_ADAM_LAUNCH(u16);
+  } else {
+    DSSM_ADAM_LAUNCH(float);
+  }
+#undef DSSM_ADAM_LAUNCH
   return hipGetLastError();
 }
 
