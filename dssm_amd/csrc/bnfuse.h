@@ -265,29 +265,40 @@ __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
       em[u] = b.ema_mean[t][cn];
       ev[u] = b.ema_var[t][cn];
     }
-    int u = 0;
-    st.finish(b, base + threadIdx.x, blockDim.x,
-              [&](int t, int c, float mu, float rstd, float inv, float shift) {
-      const size_t o = (size_t)t * b.ld + c;
-      b.coef[o] = mu;
-      b.coef[plane + o] = rstd;
-      b.coef[2 * plane + o] = inv;
-      b.coef[3 * plane + o] = shift;
-      if (c < b.n) {
-        // biased batch variance back from rstd would lose bits: recompute it from the sums
-        const double N = t == 0 ? b.rows_q : b.rows_d;
-        const double m = st.s[u] / N;
-        const double v = st.q[u] / N - m * m;
-        const float var = (float)(v > 0.0 ? v : 0.0);
-        b.bmean[t * b.n + c] = mu;
-        b.bvar[t * b.n + c] = var;
-        // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
-        const float one_m = 1.0f - b.decay;
-        b.ema_mean[t][c] = em[u] - (em[u] - mu) * one_m;
-        b.ema_var[t][c] = ev[u] - (ev[u] - var) * one_m;
+    // the coefficient arithmetic of FsCoefStage::finish, unrolled here so that the sums are read by
+    // compile-time index (a counter in finish's callback indexed them at run time: scratch memory
+    // for every workgroup of the producing launch)
+#pragma unroll
+    for (int u = 0; u < NPER; ++u) {
+      const int i = base + threadIdx.x + blockDim.x * u;
+      if (i < 2 * b.ld) {
+        const int t = i / b.ld, c = i - t * b.ld;
+        float mu = 0.f, var = 0.f, rstd = 0.f, inv = 0.f, shift = 0.f;
+        if (c < b.n) {
+          const double N = t == 0 ? b.rows_q : b.rows_d;
+          const double m = st.s[u] / N;
+          const double v = st.q[u] / N - m * m;
+          mu = (float)m;
+          var = (float)(v > 0.0 ? v : 0.0);
+          rstd = 1.0f / sqrtf(var + b.eps);
+          inv = rstd * st.gm[u];
+          shift = st.bt[u] - mu * inv;
+        }
+        const size_t o = (size_t)t * b.ld + c;
+        b.coef[o] = mu;
+        b.coef[plane + o] = rstd;
+        b.coef[2 * plane + o] = inv;
+        b.coef[3 * plane + o] = shift;
+        if (c < b.n) {
+          b.bmean[t * b.n + c] = mu;
+          b.bvar[t * b.n + c] = var;
+          // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
+          const float one_m = 1.0f - b.decay;
+          b.ema_mean[t][c] = em[u] - (em[u] - mu) * one_m;
+          b.ema_var[t][c] = ev[u] - (ev[u] - var) * one_m;
+        }
       }
-      ++u;
-    });
+    }
   }
 }
 

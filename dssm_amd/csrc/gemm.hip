@@ -25,10 +25,12 @@ namespace {
 
 constexpr int BM = 64, BN = 64;
 
-// Diagnostics build only (-DDSSM_WG_TL): per-workgroup start / end stamps (s_memrealtime,
+// Diagnostics build only (-DDSSM_WG_TL): per-workgroup start / end / phase stamps (s_memrealtime,
 // 100 MHz) of the dense GEMM launches, read back by dssm_debug_wg_timeline (tools/wg_timeline.py).
 #ifdef DSSM_WG_TL
-__device__ unsigned long long g_wg_tl[4][2048][2];
+constexpr int kTlStamps = 6;  // 0 start, 1 end; NT / pair tiles: 2 operands landed, 3 LDS images
+                              // written, 4 MFMA done, 5 statistics published
+__device__ unsigned long long g_wg_tl[4][2048][kTlStamps];
 #define WG_TL(slot, idx)                                                                    \
   do {                                                                                      \
     if (threadIdx.x == 0)                                                                   \
@@ -580,7 +582,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const bool from_sums = BN_A && FS == 1 && f.in_from_sums;
   if (from_sums) cst.load(f.in, t, NT);
   // ---- every global load of the tile, issued first.  A: 4 threads per row (groups t%4 + 4i),
-  // B: BT threads per row (groups t%BT + BT i): 128-B row segments per 4 / BT lanes.
+  // B: BT threads per row (groups t%BT + BT i): 128-B row segments per 4 / BT lanes.  (8 threads
+  // per row with whole-line instructions measured the same: the fetch is not line-rate bound.)
   const int arow = t >> 2, ag0 = t & 3;
   const int brow = t / BT, bg0 = t % BT;
   constexpr int NGA = kWkMaxG, NGB = (4 * kWkMaxG + BT - 1) / BT;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
@@ -635,6 +638,11 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         }
     }
   }
+#ifdef DSSM_WG_TL
+  const int tl_slot = FS == 1 ? (a.N == 300 ? 0 : 1) : (a.K == 300 ? 3 : 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  WG_TL(tl_slot, 2);
+#endif
   // ---- BN coefficients of the A operand (from the sums or the materialised coefficients)
   if constexpr (BN_A) {
     if (FS == 1 && f.in_from_sums) {
@@ -699,6 +707,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     }
   }
   __syncthreads();
+#ifdef DSSM_WG_TL
+  WG_TL(tl_slot, 3);
+#endif
   // ---- MFMA over the whole K (fragments of the next k-step read ahead of this step's MFMAs)
   f32x4 acc[2][2];
 #pragma unroll
@@ -729,6 +740,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 #pragma unroll
     for (int j = 0; j < 2; ++j) bfr[j] = bnx[j];
   }
+#ifdef DSSM_WG_TL
+  WG_TL(tl_slot, 4);
+#endif
   // ---- epilogue
   // lds_epi: the tile's values go to LDS (the A panel's space, free once every wave is past its
   // last MFMA) and leave as 16-B row segments (full 256-B rows) instead of the accumulator
@@ -804,6 +818,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       det_publish(f.det, tx, ty, f.det_rows, ldc, bn, min(bn + 64, N), f.out_sum, &s_det);
     }
   }
+#ifdef DSSM_WG_TL
+  WG_TL(tl_slot, 5);
+#endif
   if (lds_epi) {
     __syncthreads();
     const int ncols = min(64, ldc - bn);  // multiple of 8: ldc = ldp8(N)
@@ -1249,7 +1266,7 @@ hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void
 #ifdef DSSM_WG_TL
 extern "C" int dssm_debug_wg_timeline(int slot, unsigned long long* out, int n) {
   if (slot < 0 || slot >= 4 || n > 2048) return -1;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_wg_tl), sizeof(unsigned long long) * 2 * n,
-                             sizeof(unsigned long long) * 2 * 2048 * slot) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_wg_tl), sizeof(unsigned long long) * dssm::kTlStamps * n,
+                             sizeof(unsigned long long) * dssm::kTlStamps * 2048 * slot) == hipSuccess ? 0 : -2;
 }
 #endif

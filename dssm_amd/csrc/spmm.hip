@@ -560,6 +560,13 @@ __global__ __launch_bounds__(256) void k_csc_scatter(const int* __restrict__ ind
 // launch each instead of two: a kernel boundary saved, and the small scan / scatter work fills the
 // gaps of the latency-bound SpMM / sums.  The scan and sums workgroups come first.
 constexpr int kScanSmallNT = 256;
+#ifndef DSSM_SCAN_LAST
+#define DSSM_SCAN_LAST 0
+#endif
+#ifdef DSSM_WG_TL
+// Diagnostics build only: per-wave start / end stamps of the training SpMM's row waves (row index)
+__device__ unsigned long long g_spmm_tl[8192][2];
+#endif
 template <typename TW>
 __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indptr,
                                                    const int* __restrict__ indices,
@@ -573,10 +580,32 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
                                                    int2* __restrict__ heavy_items, int nscan) {
   __shared__ int s_wave[kScanSmallNT / 64];
   __shared__ int s_hbase;
+#if DSSM_SCAN_LAST  // the scan workgroups after the row workgroups in dispatch order
+  const int nrow_blocks = (int)gridDim.x - nscan;
+  if ((int)blockIdx.x >= nrow_blocks)
+    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x - nrow_blocks, s_wave,
+                             &s_hbase);
+  else {
+    const int rb = blockIdx.x;
+#else
   if ((int)blockIdx.x < nscan)
     scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x, s_wave, &s_hbase);
-  else
-    spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, blockIdx.x - nscan);
+  else {
+    const int rb = blockIdx.x - nscan;
+#endif
+#ifdef DSSM_WG_TL
+    const int row = rb * 4 + (threadIdx.x >> 6);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, rb);
+#ifdef DSSM_WG_TL
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0 && row < rows && row < 8192) {
+      g_spmm_tl[row][0] = t0;
+      g_spmm_tl[row][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ Z, int ldz, int ncol,
@@ -1143,3 +1172,11 @@ hipError_t launch_dw1(const int* col_ptr, const int* csc_row, const float* csc_v
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_WG_TL
+extern "C" int dssm_debug_spmm_timeline(unsigned long long* out, int n) {
+  if (n > 8192) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_spmm_tl), sizeof(unsigned long long) * 2 * n, 0) == hipSuccess
+             ? 0 : -2;
+}
+#endif

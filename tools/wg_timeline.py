@@ -19,6 +19,7 @@ from dssm_amd.model import DSSM
 D, W, BS, NEG = 30000, (300, 300, 128), 1024, 4
 m = DSSM(D, W, BS, NEG, dtype="bf16")
 b = synth_batch(D, BS, NEG, seed=1000, cols=ZipfColumns(D))
+batch = b
 m.set_batch(b)
 for _ in range(5):
     m.train_step()
@@ -29,13 +30,28 @@ f.restype = C.c_int
 f.argtypes = [C.c_int, C.c_void_p, C.c_int]
 grids = {0: 5 * 48, 1: 2 * 48, 2: None, 3: None}
 for slot, name in enumerate(("nt L2 (N=300)", "nt L3 (N=128)", "pair L3", "pair L2")):
-    buf = np.zeros((2048, 2), np.uint64)
+    buf = np.zeros((2048, 6), np.uint64)
     assert f(slot, buf.ctypes.data, 2048) == 0
     n = int(np.sum(buf[:, 0] > 0))
     if n == 0:
         print(f"{name}: no stamps")
         continue
     t = buf[:n].astype(np.int64)
+    ph = t[:, 2:6]
+    if (ph > 0).all():  # phase stamps (tiles only; the materialising block has none)
+        rel = (ph - t[:, :1]) * 0.01
+        tiles = (t[:, 2] > 0)
+        print(f"{name}: phase medians from WG start (us): operands landed {np.median(rel[:, 0]):.2f}, "
+              f"LDS images {np.median(rel[:, 1]):.2f}, MFMA done {np.median(rel[:, 2]):.2f}, "
+              f"stats published {np.median(rel[:, 3]):.2f}, end {np.median((t[:, 1] - t[:, 0]) * 0.01):.2f}")
+    else:
+        ok = t[:, 2] > 0
+        if ok.any():
+            rel = (t[ok][:, 2:6] - t[ok][:, :1]) * 0.01
+            print(f"{name}: phase medians over {int(ok.sum())} tiles (us): operands landed {np.median(rel[:, 0]):.2f}, "
+                  f"LDS images {np.median(rel[:, 1]):.2f}, MFMA done {np.median(rel[:, 2]):.2f}, "
+                  f"stats published {np.median(rel[:, 3]):.2f}, end {np.median((t[ok][:, 1] - t[ok][:, 0]) * 0.01):.2f}")
+    t = t[:, :2]
     t0 = t[:, 0].min()
     st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
     dur = en - st
@@ -70,3 +86,36 @@ for name, sel in (("heavy items", heavy), ("W1 rows", w1r), ("flat/dense", ~heav
 print(f"adam span {en.max():.1f} us over {n} blocks")
 hist = np.histogram(en, bins=12)[0]
 print("  block ends histogram (12 bins over the span):", hist.tolist())
+
+# SpMM row waves: duration against the row's nnz
+h = lib.dssm_debug_spmm_timeline
+h.restype = C.c_int
+h.argtypes = [C.c_void_p, C.c_int]
+R = m.rows if hasattr(m, "rows") else 6144
+buf = np.zeros((R, 2), np.uint64)
+assert h(buf.ctypes.data, R) == 0
+t = buf.astype(np.int64)
+t0 = t[:, 0].min()
+st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
+nnz = np.diff(batch.indptr)[:R]
+d = en - st
+print(f"spmm rows: span {en.max():.1f} us; start spread {st.max():.1f}; wave duration median {np.median(d):.2f} "
+      f"max {d.max():.2f}; nnz median {np.median(nnz)} max {nnz.max()}")
+for lo, hi in ((0, 24), (24, 32), (32, 40), (40, 48), (48, 200)):
+    sel = (nnz >= lo) & (nnz < hi)
+    if sel.any():
+        print(f"   nnz [{lo},{hi}): {int(sel.sum())} rows, duration median {np.median(d[sel]):.2f} max {d[sel].max():.2f}, "
+              f"end median {np.median(en[sel]):.2f} max {en[sel].max():.2f}")
+hist = np.histogram(st, bins=10)[0]
+print("   wave starts histogram (10 bins):", hist.tolist(), f"over {st.max():.1f} us")
+late = np.where(st > 2.0)[0]
+if late.size:
+    print(f"   late-starting rows: {late.size}, rows {late.min()}..{late.max()}, "
+          f"blocks {sorted(set((late // 4).tolist()))[:40]}")
+print("   duration percentiles 50/90/99/max:", [round(float(np.percentile(d, q)), 2) for q in (50, 90, 99, 100)])
+blk = np.arange(R) // 4
+for name, key in (("xcd (block % 8)", blk % 8), ("block // 256", blk // 256)):
+    print(f"   by {name}:", " ".join(f"{int(k)}:{np.median(d[key == k]):.1f}/{np.percentile(d[key == k], 99):.1f}"
+                                      for k in np.unique(key)))
+slow = np.argsort(d)[-12:]
+print("   slowest rows:", [(int(r), int(nnz[r]), round(float(st[r]), 1), round(float(d[r]), 1)) for r in slow])
