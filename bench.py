@@ -133,8 +133,12 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
 
 # probe name -> kernel name in the rocprofv3 PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py):
 # bf16 steps run the SpMM inside k_spmm_scan (merged transpose), fp32 steps as k_spmm_fwd
-PMC_KERNELS = {"bf16": {"adam": "k_adam_step<unsigned short>", "spmm_fwd": "k_spmm_scan<unsigned short>"},
-               "fp32": {"adam": "k_adam_step<float>", "spmm_fwd": "k_spmm_fwd<float>"}}
+# (the step kernel's single-GPU variant is k_adam_step<T, false> since round 3; older summaries
+# name it k_adam_step<T>)
+PMC_KERNELS = {"bf16": {"adam": ("k_adam_step<unsigned short, false>", "k_adam_step<unsigned short>"),
+                        "spmm_fwd": ("k_spmm_scan<unsigned short>",)},
+               "fp32": {"adam": ("k_adam_step<float, false>", "k_adam_step<float>"),
+                        "spmm_fwd": ("k_spmm_fwd<float>",)}}
 # the workload a traffic summary without a "_workload" record was collected on (r01: the default
 # single-GPU bench line)
 DEFAULT_WORKLOAD = {"dtype": "bf16", "columns": "zipf", "feed": "device"}
@@ -149,7 +153,12 @@ def pmc_traffic(workload: dict):
         d = json.load(open(f))
         if d.get("_workload", DEFAULT_WORKLOAD) != workload:  # (other rows' files name their model)
             continue
-        out = {probe: d[k]["hbm_bytes"] for probe, k in PMC_KERNELS[workload["dtype"]].items() if k in d}
+        out = {}
+        for probe, names in PMC_KERNELS[workload["dtype"]].items():
+            for k in names:
+                if k in d:
+                    out[probe] = d[k]["hbm_bytes"]
+                    break
         return out, os.path.relpath(f, ROOT)
     return {}, None
 

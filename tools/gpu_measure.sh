@@ -6,7 +6,7 @@
 set -eu
 mkdir -p gpurun_out/m
 export TMPDIR=/tmp
-B="python3 bench.py --cpu-baseline 0"
+B="python3 bench.py --cpu-baseline 0 --fp32-line 0 --det-line 0"
 for dt in ${DTYPES:-bf16 fp32}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/m/kt_$dt -o run \
     -- $B --dtype $dt --steps 48 --warmup 8 --fwd-only 0 > gpurun_out/m/kt_$dt.log 2>&1
