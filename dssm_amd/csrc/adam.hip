@@ -89,6 +89,12 @@ __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, f
   }
 }
 
+__device__ __forceinline__ bool in_slabs(const SlabList& sl, int64_t i) {
+  for (int s = 0; s < sl.count; ++s)
+    if (i >= sl.seg[s].offset && i < sl.seg[s].offset + sl.seg[s].count) return true;
+  return false;
+}
+
 // Gradient of element i..i+3: from a deferred split-K slab (fixed split order, as
 // k_splitk_reduce would have summed it) or from the arena.
 __device__ __forceinline__ float4 slab_grad4(const SlabList& sl, int64_t i, const float* g) {
@@ -488,6 +494,13 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       flat_untouched(f, bi);
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
+    if (WIRE && a.slab_to_g) {  // gradient pass: g = the deferred split-K slabs' sums (fixed order)
+      for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < nt; j += (int64_t)a.dense_blocks * blockDim.x) {
+        const int64_t i = a.t4_begin + j;
+        if (in_slabs(a.slabs, i * 4))
+          reinterpret_cast<float4*>(a.g)[i] = slab_grad4(a.slabs, i * 4, a.g);
+      }
+    } else
     for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < na + nt;
          j += (int64_t)a.dense_blocks * blockDim.x) {
       const int64_t i = j < na ? a.d4_begin + j : a.t4_begin + (j - na);
@@ -642,6 +655,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (a.gout || a.no_advance) a.ticket = nullptr;  // the gradient pass / a non-final chunk advance nothing
   if (!a.ticket && !a.gout && !a.no_advance) return hipErrorInvalidValue;  // a step advances the beta powers
   if (a.wchunk >= 0 && (!a.gout || !a.geo.ww || a.wchunk >= a.geo.wp)) return hipErrorInvalidValue;
+  if (a.slab_to_g && (!a.gout || a.d4_end != a.d4_begin)) return hipErrorInvalidValue;  // gradient pass only
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;
   else a.item_blocks = std::min(a.item_blocks, kAdamItemBlocks);
   // rows with no entry this step stream through the flat role instead of a wave per row
@@ -652,7 +666,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
-  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire;
+  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g;
 #define DSSM_ADAM_LAUNCH(TZ)                                                         \
   if (wire) hipLaunchKernelGGL((k_adam_step<TZ, true>), grid, block, 0, s, a);       \
   else hipLaunchKernelGGL((k_adam_step<TZ, false>), grid, block, 0, s, a)

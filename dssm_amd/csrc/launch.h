@@ -307,6 +307,9 @@ struct AdamStep {
   int wchunk = -1;     // gradient pass: only the rows of this chunk (-1: every row)
   int64_t pwire_off4;  // the dense range's parameter-wire float4 index = i + pwire_off4
   int no_advance;      // a chunk of a chunked Adam step other than the last: no beta-power advance
+  // gradient pass: the dense role sums the deferred split-K slabs (slabs) of [t4_begin, t4_end) into
+  // the gradient arena instead of updating parameters (the tail's all-reduce then sends the sums)
+  int slab_to_g;
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);

@@ -814,6 +814,8 @@ static int backward_impl(dssm_plan* P, void* stream) {
     dssm::TnParams dw{};
     bool dw_pending = false;
     float* dw_reduce_to = nullptr;
+    // dW_l's split-K slabs summed later: by the fused Adam step, or by the wire gradient pass
+    const bool defer_slabs = P->fused_w1_adam() || wire_gradient_pass(P);
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
@@ -838,10 +840,10 @@ static int backward_impl(dssm_plan* P, void* stream) {
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
           Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
-          P->g + Lt.fc_off[l], P->fused_w1_adam(), s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
+          P->g + Lt.fc_off[l], defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
           P->deterministic() ? &bprev.bdet : nullptr));
       dw_pending = host_dw && dw.C != nullptr;
-      if (dw_pending && !P->fused_w1_adam() && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
+      if (dw_pending && !defer_slabs && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
     }
     return dw1_backward(P, s);
   }
@@ -926,7 +928,31 @@ static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s, int chunk) {
   a.gout = P->gwire;
   a.geo = P->geo;
   a.wchunk = P->geo.wp > 1 ? chunk : -1;
+  // the pass of b1's row (the last chunk) also sums the deferred dW_l split-K slabs into the
+  // gradient arena (no separate reduce launches; the tail's all-reduce follows this launch)
+  if (chunk < 0 || chunk == P->geo.wp - 1) {
+    const Layout& Lt = P->Lt;
+    int64_t lo = Lt.total, hi = 0;
+    for (int l = 1; l < Lt.L; ++l)
+      if (P->dw_deferred[l] > 0) {
+        dssm::SlabSeg& sg = a.slabs.seg[a.slabs.count++];
+        sg.offset = Lt.fc_off[l];
+        sg.count = (int64_t)(Lt.in_dim[l] + 1) * Lt.n[l];
+        sg.splits = P->dw_deferred[l];
+        sg.slab = P->at<float>(Lt.dw_slab[l]);
+        lo = std::min(lo, sg.offset);
+        hi = std::max(hi, sg.offset + sg.count);
+      }
+    if (a.slabs.count) {
+      if ((lo % 4) || (hi % 4)) return fail(DSSM_E_INVALID, "dW slab segments must be 4-aligned");
+      a.slab_to_g = 1;
+      a.t4_begin = lo / 4;
+      a.t4_end = hi / 4;
+    }
+  }
   HIP_TRY(dssm::launch_adam_step(a, P->Lt.bf16, s));
+  if (a.slab_to_g)
+    for (int l = 1; l < P->Lt.L; ++l) P->dw_deferred[l] = 0;  // the arena holds dW_l now
   return DSSM_OK;
 }
 
