@@ -582,8 +582,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const bool from_sums = BN_A && FS == 1 && f.in_from_sums;
   if (from_sums) cst.load(f.in, t, NT);
   // ---- every global load of the tile, issued first.  A: 4 threads per row (groups t%4 + 4i),
-  // B: BT threads per row (groups t%BT + BT i): 128-B row segments per 4 / BT lanes.  (8 threads
-  // per row with whole-line instructions measured the same: the fetch is not line-rate bound.)
+  // B: BT threads per row (groups t%BT + BT i): 128-B row segments per 4 / BT lanes.  (Measured
+  // neutral in round 3: 8 threads per row with whole-line instructions, and a per-column-tile
+  // rotation of the K groups' issue order.)
   const int arow = t >> 2, ag0 = t & 3;
   const int brow = t / BT, bg0 = t % BT;
   constexpr int NGA = kWkMaxG, NGB = (4 * kWkMaxG + BT - 1) / BT;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
@@ -838,8 +839,13 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 // round-robin dispatch places on one XCD (speed only, never correctness: any placement computes
 // the same tiles).  Consecutive tiles share their A rows (a row block's column tiles) or their
 // batch-row chunk (dW), so those re-reads hit that XCD's L2 instead of the Infinity Cache.
+// (measured in round 3 with the grouping off: +4.5 us/step, so the row block's A panel is shared
+// through the XCD's L2)
+#ifndef DSSM_XCD_TILE
+#define DSSM_XCD_TILE 1
+#endif
 __device__ __forceinline__ int xcd_tile(int b, int n) {
-  return (n % 8) ? b : (b % 8) * (n / 8) + b / 8;
+  return (!DSSM_XCD_TILE || (n % 8)) ? b : (b % 8) * (n / 8) + b / 8;
 }
 
 // Whole-K forward NT GEMM: blocks [0, ntiles) compute tiles (XCD-grouped row blocks); with the
