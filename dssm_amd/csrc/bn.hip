@@ -456,7 +456,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   // first in dispatch order); they read dZ of the layer above and the forward's activations, so
   // they are independent of this launch's own work
   if ((int)blockIdx.x < dw_blocks) {
-    const int r = blockIdx.x;
+    // XCD-grouped: the tiles of one batch-row chunk share its A / dZ sub-panels through one L2
+#ifndef DSSM_XCD_DW_APPLY
+#define DSSM_XCD_DW_APPLY 1
+#endif
+    const int r = DSSM_XCD_DW_APPLY ? xcd_tile(blockIdx.x, dw_blocks) : (int)blockIdx.x;
     u16* sA = reinterpret_cast<u16*>(smem);
     tn_chunk_body<3>(dw, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y), sA, sA + 2 * kTnTile);
     return;
