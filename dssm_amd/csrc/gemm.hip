@@ -105,8 +105,14 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int bm = blockIdx.y * BM, bn = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * k_per_split;
+  // XCD-grouped tile order over the whole grid (x fastest): consecutive tiles share a row block's
+  // A panel (FWD / DA) or a split's batch-row chunk (DW), so they run on one XCD
+  const int gx = gridDim.x, gxy = gridDim.x * gridDim.y;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int tile = xcd_tile(lin, gxy * gridDim.z);
+  const int tbx = tile % gx, tby = (tile % gxy) / gx, tbz = tile / gxy;
+  const int bm = tby * BM, bn = tbx * BN;
+  const int kbeg = tbz * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int Mload = ones_row ? M - 1 : M;
   float bcol[2] = {0.f, 0.f};  // GEMM_FWD: the epilogue's bias columns, loaded ahead of the K loop
@@ -245,7 +251,7 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 
   // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
   float* out = C;
-  if constexpr (MODE == GEMM_DW) out = C + (size_t)blockIdx.z * M * ldc;  // this split's slab
+  if constexpr (MODE == GEMM_DW) out = C + (size_t)tbz * M * ldc;  // this split's slab
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll

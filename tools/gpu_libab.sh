@@ -10,6 +10,6 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
     DSSM_LIB_PATH=$PWD/$lib timeout -k 10 200 python3 bench.py --steps ${STEPS:-400} --warmup 40 \
       --cpu-baseline 0 --fwd-only 0 ${BENCH_ARGS:-} > gpurun_out/libab.json 2> gpurun_out/libab.err || {
       echo "[$lib] failed rc=$?"; tail -5 gpurun_out/libab.err; exit 1; }
-    python3 -c "import json; d=json.load(open('gpurun_out/libab.json')); print('$lib', d['ms_per_step'], d['value'], d['kernels_ms'])"
+    python3 -c "import json; d=json.load(open('gpurun_out/libab.json')); print('$lib', d['ms_per_step'], d['value'], d.get('kernels_ms'))"
   done
 done
