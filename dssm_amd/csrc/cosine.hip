@@ -38,6 +38,19 @@ constexpr int kCosMaxN = 512;
 // NW: waves (queries) per workgroup.  The fused kernel uses 16: each workgroup adds its backward
 // sums with one fp64 atomic per (statistic, column), and the 64-deep same-address chains (instead
 // of 256-deep at 4 waves) no longer trail the launch.
+#ifdef DSSM_WG_TL
+// Diagnostics build only: per-workgroup start / end stamps of the fused cosine launch (its query
+// blocks, the materialising block, the CSC scatter blocks), read by dssm_debug_cos_timeline
+__device__ unsigned long long g_cos_tl[1024][8];  // 0 start 1 end, 2..6 phases (query blocks)
+#define COS_TL(idx)                                                                               \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_cos_tl[blockIdx.x][idx] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define COS_TL(idx) \
+  do {              \
+  } while (0)
+#endif
 template <int EPL, int KM, bool FSC, int NW>
 __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
@@ -45,6 +58,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat) {
   constexpr int NT = 64 * NW;
+  COS_TL(0);
   __shared__ float s_part[2][NW];
   __shared__ float s_co[FSC ? 2 * 4 * kCosMaxN : 1];     // [tower][mu|rstd|inv|shift][c]
   __shared__ float s_bs[FSC ? NW * 4 * EPL * 64 : 1];    // [wave][sq1|sq2|sd1|sd2][c]
@@ -75,8 +89,17 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       const int xb = (int)blockIdx.x - nrow_blocks - 1;
       if (xb < 0) fs_materialize_fwd(fs);
       else csc_scatter_role(scat, xb);  // the CSC transpose's scatter (csc.h)
+#ifdef DSSM_WG_TL
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      COS_TL(1);
+#endif
       return;
     }
+#ifdef DSSM_WG_TL
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    COS_TL(2);
+#endif
     fs_coef_stage<(2 * kCosMaxN + NT - 1) / NT>(fs, threadIdx.x, NT,
                                           [&](int t, int c, float mu, float rs, float inv, float sh) {
       s_co[(t * 4 + 0) * kCosMaxN + c] = mu;
@@ -86,6 +109,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     });
     __syncthreads();
   }
+  COS_TL(3);
   float lj = 0.f, cj = 0.f;
   float bq1[EPL], bq2[EPL], bd1[EPL], bd2[EPL];  // FSC: this wave's backward sums per column
 #pragma unroll
@@ -188,6 +212,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     if (lane == 0) qnorm[j] = qn;
     lj = -logf(p[0]);
     cj = (amax == 0) ? 1.f : 0.f;
+    COS_TL(4);
     // ---- backward: d loss / d cos_sim[j,k] = (p_k - [k==0]) / BS (skipped without dy: eval)
     if (FSC || dy != nullptr) {
     float dq[EPL];
@@ -231,6 +256,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     }
     }  // backward
   }
+  COS_TL(5);
   if constexpr (FSC) {
     // workgroup sums of the NW waves (fp64) -> the layer's backward accumulators
 #pragma unroll
@@ -257,6 +283,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       det_publish(fs.bdet, 0, blockIdx.x, nrow_blocks, ld, 0, n, fs.bsum, &s_last);
     }
   }
+  COS_TL(6);
   // ---- loss / accuracy: per-block partials, fixed-order sum by the last block
   if (lane == 0) {
     s_part[0][wv] = lj;
@@ -273,6 +300,11 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     part[2 * blockIdx.x] = a;
     part[2 * blockIdx.x + 1] = b;
   }
+#ifdef DSSM_WG_TL
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  COS_TL(1);
+#endif
 }
 
 __global__ __launch_bounds__(64) void k_loss_finalize(const float* __restrict__ part, int nblk,
@@ -335,3 +367,11 @@ hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out,
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_WG_TL
+extern "C" int dssm_debug_cos_timeline(unsigned long long* out, int n) {
+  if (n > 1024) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_cos_tl), sizeof(unsigned long long) * 8 * n, 0) == hipSuccess
+             ? 0 : -2;
+}
+#endif

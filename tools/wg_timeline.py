@@ -119,3 +119,25 @@ for name, key in (("xcd (block % 8)", blk % 8), ("block // 256", blk // 256)):
                                       for k in np.unique(key)))
 slow = np.argsort(d)[-12:]
 print("   slowest rows:", [(int(r), int(nnz[r]), round(float(st[r]), 1), round(float(d[r]), 1)) for r in slow])
+
+# fused cosine launch: query blocks, then the materialising block, then the CSC scatter blocks
+h = lib.dssm_debug_cos_timeline
+h.restype = C.c_int
+h.argtypes = [C.c_void_p, C.c_int]
+buf = np.zeros((1024, 8), np.uint64)
+assert h(buf.ctypes.data, 1024) == 0
+n = int(np.sum(buf[:, 0] > 0))
+t = buf[:n].astype(np.int64)
+nq0 = BS // 16
+ph = (t[:nq0, 2:7] - t[:nq0, :1]) * 0.01
+print("cosine query-block phase medians from start (us): rows landed %.2f, coefficients %.2f, forward %.2f, "
+      "backward %.2f, statistics %.2f, end %.2f" % tuple(list(np.median(ph, axis=0)) + [np.median((t[:nq0, 1] - t[:nq0, 0]) * 0.01)]))
+t = t[:, :2]
+t0 = t[:, 0].min()
+st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
+nq = BS // 16
+for name, sel in (("query blocks", slice(0, nq)), ("materialise", slice(nq, nq + 1)), ("scatter blocks", slice(nq + 1, n))):
+    d = en[sel] - st[sel]
+    if d.size:
+        print(f"cosine {name}: {d.size} blocks, start {st[sel].min():.1f}..{st[sel].max():.1f}, end "
+              f"{en[sel].min():.1f}..{en[sel].max():.1f} us, duration median {np.median(d):.2f} max {d.max():.2f}")
