@@ -204,11 +204,11 @@ __global__ __launch_bounds__(1024) void k_bn_stats(const float* __restrict__ Z, 
           var = P.ema_var[tower][c];
         }
         const float rstd = 1.0f / sqrtf(var + eps);
-        const float inv = rstd * P.gamma[tower][c];
+        const float inv = rstd * pick2(P.gamma, tower)[c];
         coef[o] = mu;
         coef[plane + o] = rstd;
         coef[2 * plane + o] = inv;
-        coef[3 * plane + o] = P.beta[tower][c] - mu * inv;
+        coef[3 * plane + o] = pick2(P.beta, tower)[c] - mu * inv;
       }
     }
   }

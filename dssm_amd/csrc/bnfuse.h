@@ -61,6 +61,14 @@ struct BnSide {
   DetAcc fdet, bdet;  // deterministic mode: the producers' slabs of fsum / bsum (slab null: atomics)
 };
 
+// Element t (0 / 1) of a two-pointer array of a kernel argument, as a select of the two (uniform)
+// pointers: indexing the array with a lane-varying t makes the compiler fetch the pointer from the
+// argument segment with a vector load, a dependent round trip before the data load.
+template <typename P>
+__device__ __forceinline__ P pick2(P const (&a)[2], int t) {
+  return t ? a[1] : a[0];
+}
+
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -135,8 +143,8 @@ __device__ __forceinline__ void fs_coef_from(const BnSide& b, int t, int c, doub
   mu = (float)m;
   var = (float)(v > 0.0 ? v : 0.0);
   rstd = 1.0f / sqrtf(var + b.eps);
-  inv = rstd * b.gamma[t][c];
-  shift = b.beta[t][c] - mu * inv;
+  inv = rstd * pick2(b.gamma, t)[c];
+  shift = pick2(b.beta, t)[c] - mu * inv;
 }
 __device__ __forceinline__ void fs_coef(const BnSide& b, int t, int c, float& mu, float& var,
                                         float& rstd, float& inv, float& shift) {
@@ -161,8 +169,8 @@ struct FsCoefStage {
       const int t = ic / b.ld, c = ic - t * b.ld;
       const int cn = c < b.n ? c : 0;
       off[u] = (t * 2) * b.ld + c;
-      gm[u] = b.gamma[t][cn];
-      bt[u] = b.beta[t][cn];
+      gm[u] = pick2(b.gamma, t)[cn];
+      bt[u] = pick2(b.beta, t)[cn];
     }
 #pragma unroll
     for (int u = 0; u < NPER; ++u) {
@@ -262,8 +270,8 @@ __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
       const int ic = i < 2 * b.ld ? i : 0;
       const int t = ic / b.ld, c = ic - t * b.ld;
       const int cn = c < b.n ? c : 0;
-      em[u] = b.ema_mean[t][cn];
-      ev[u] = b.ema_var[t][cn];
+      em[u] = pick2(b.ema_mean, t)[cn];
+      ev[u] = pick2(b.ema_var, t)[cn];
     }
     // the coefficient arithmetic of FsCoefStage::finish, unrolled here so that the sums are read by
     // compile-time index (a counter in finish's callback indexed them at run time: scratch memory
@@ -294,8 +302,8 @@ __device__ __forceinline__ void fs_materialize_fwd(const BnSide& b) {
           b.bvar[t * b.n + c] = var;
           // ExponentialMovingAverage(decay).apply: shadow -= (shadow - value) * (1 - decay)
           const float one_m = 1.0f - b.decay;
-          b.ema_mean[t][c] = em[u] - (em[u] - mu) * one_m;
-          b.ema_var[t][c] = ev[u] - (ev[u] - var) * one_m;
+          pick2(b.ema_mean, t)[c] = em[u] - (em[u] - mu) * one_m;
+          pick2(b.ema_var, t)[c] = ev[u] - (ev[u] - var) * one_m;
         }
       }
     }
@@ -321,8 +329,8 @@ __device__ __forceinline__ void fs_materialize_bwd(const BnSide& b) {
     const int t = i / b.n, c = i - t * b.n;
     double s1, s2;
     fs_bsums(b, t, c, s1, s2);
-    b.dbeta[t][c] = (float)s1;
-    b.dgamma[t][c] = (float)s2;
+    pick2(b.dbeta, t)[c] = (float)s1;
+    pick2(b.dgamma, t)[c] = (float)s2;
   }
 }
 
