@@ -623,7 +623,10 @@ hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSi
                                      float* loss_out, const TnParams* dw) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
   // element workgroups: fewer beside hosted dW tiles, which share the CUs
-  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? 512 : 1024);
+#ifndef DSSM_APPLY_GRID_DW
+#define DSSM_APPLY_GRID_DW 512
+#endif
+  const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? DSSM_APPLY_GRID_DW : 1024);
   if (dw && dw->k_per_split > 3 * 128) return hipErrorInvalidValue;  // tn_chunk_body<3>
   const TnParams p = dw ? *dw : TnParams{};
   const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
