@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--fwd-only", type=int, default=1,
                     help="also time the forward alone (eval mode: EMA-BN forward + cosine + loss, "
                          "new_dssm.py:274-285) over the staged batches, N=1")
+    ap.add_argument("--idle-before-warmup", type=float, default=0.0,
+                    help="analysis only: seconds of host sleep between the graph builds and the warm-up")
+    ap.add_argument("--busy-before-warmup", type=float, default=0.0,
+                    help="analysis only: seconds of dense matmul load between the graph builds and the warm-up")
     return ap.parse_args()
 
 
@@ -747,6 +751,16 @@ def main():
         def run_steps(i0, n):
             for i in range(i0, i0 + n):
                 step(i)
+    if args.idle_before_warmup > 0:  # analysis only: host idle time between the graph builds and the warm-up
+        time.sleep(args.idle_before_warmup)
+    if args.busy_before_warmup > 0:  # analysis only: a dense matmul load right before the warm-up
+        xa = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+        tb = time.perf_counter()
+        while time.perf_counter() - tb < args.busy_before_warmup:
+            for _ in range(8):
+                xa = (xa @ xa).clamp_(-1, 1)
+            torch.cuda.synchronize()
+        del xa
     run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if not args.graph and args.probes:
