@@ -605,8 +605,12 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       const int kg = (ag0 + 4 * i) * 8;
       const size_t off = (rok && kg < lda) ? rbase + kg : 0;
       if constexpr (BN_A) {
+#ifdef DSSM_EXP_ZB16
+        ua[i] = *reinterpret_cast<const uint4*>((const u16*)a.A + off);
+#else
         fa[i][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
         fa[i][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
+#endif
       } else {
         ua[i] = *reinterpret_cast<const uint4*>((const u16*)a.A + off);
       }
@@ -689,8 +693,16 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
           if (ok) {
             const float* ci = &sCoef[(tower * 2) * Kp + kg];
             const float* ch = ci + Kp;
+#ifdef DSSM_EXP_ZB16
+            const uint4 u = ua[i];
+            const float z[8] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u),
+                                __uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)};
+#else
             const float z[8] = {fa[i][0].x, fa[i][0].y, fa[i][0].z, fa[i][0].w,
                                 fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
+#endif
             float y[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);

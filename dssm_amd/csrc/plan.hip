@@ -212,6 +212,10 @@ struct dssm_plan {
   uint16_t* gwire = nullptr;
   uint16_t* pwire = nullptr;
   const uint16_t* gstage = nullptr;
+  // the captured data-parallel graph's steps after the first (one wire chunk): the forward's SpMM
+  // reads W1 straight from the all-gathered parameter wire (row stride geo.n) instead of the shadow
+  // the k_wire_shadow launch would rebuild from it; the region's last step still rebuilds the shadow
+  const uint16_t* w1_wire = nullptr;
   dssm::WireGeo geo{};
   int dp_rank = 0;
   bool dp_defer_gradpass = false;  // the data-parallel graph builder launches the chunks itself
@@ -306,9 +310,13 @@ struct dssm_plan {
 
   template <typename T> T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
   const void* weight(int l) const {  // what the kernels read for W_l
+    if (l == 0 && w1_wire) return w1_wire;
     return Lt.bf16 ? (const void*)at<u16>(Lt.shadow[l]) : (const void*)(p + Lt.fc_off[l]);
   }
-  int weight_ld(int l) const { return Lt.bf16 ? Lt.ldp[l] : Lt.n[l]; }
+  int weight_ld(int l) const {
+    if (l == 0 && w1_wire) return geo.n;
+    return Lt.bf16 ? Lt.ldp[l] : Lt.n[l];
+  }
   // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
   bool wholek(int l) const { return Lt.bf16 && l > 0 && Lt.ldp[l - 1] <= 512; }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
@@ -633,7 +641,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   if (merged) {  // the SpMM rows share their launch with the column scan
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
-                                   P->at<uint16_t>(Lt.shadow[0]), Lt.ldp[0], Lt.n[0], P->bias(0),
+                                   (const uint16_t*)P->weight(0), P->weight_ld(0), Lt.n[0], P->bias(0),
                                    P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
   } else {
@@ -1621,6 +1629,8 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   return DSSM_OK;
 }
 
+static int Lt_n0(const dssm_plan* P) { return P->Lt.n[0]; }
+
 int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, const int32_t* const* indices,
                                    const float* const* values, int nsteps, float grad_scale, int comm,
                                    float link_gbps, float latency_us, int overlap, int with_probes,
@@ -1727,12 +1737,19 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     };
     if (!rc) rc = dssm_plan_adam(P, grad_scale, stream);
     P->dp_hook = nullptr;
-    // W1's shadow rebuilt chunk by chunk as the all-gathers land (the next forward's operand)
+    // W1's shadow rebuilt chunk by chunk as the all-gathers land (the next forward's operand).  With
+    // one chunk the wire already holds W1 row-major: the region's next step reads it directly
+    // (w1_wire) and only the last step rebuilds the shadow, which the next region's first step and
+    // the eval forward read.
+    const bool direct = C == 1 && P->geo.n == Lt_n0(P) && i + 1 < nsteps;
     for (int c = 0; c < C && !rc; ++c) {
       DP_TRY(wait(s, e_ag[c]));
-      DP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s));
+      if (!direct)
+        DP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s));
     }
+    P->w1_wire = direct ? P->pwire : nullptr;
   }
+  P->w1_wire = nullptr;
 #undef DP_TRY
   P->dp_hook = nullptr;
   P->dp_defer_gradpass = false;

@@ -179,11 +179,13 @@ def _staged(seeds):
     return out
 
 
-@pytest.mark.parametrize("comm,overlap", [(0, False), (0, True), (1, True)])
-def test_dp_step_graph_world1_matches_eager(comm, overlap, comm_world1):
+@pytest.mark.parametrize("comm,overlap,chunks", [(0, False, 3), (0, True, 3), (1, True, 3), (0, False, 1)])
+def test_dp_step_graph_world1_matches_eager(comm, overlap, chunks, comm_world1):
     """Three captured data-parallel steps (comm 0: RCCL at world 1; comm 1: device copies) against
-    the same three steps run eagerly on the same wire (all-to-all = copy, all-gather = identity)."""
-    chunks, steps = 3, 3
+    the same three steps run eagerly on the same wire (all-to-all = copy, all-gather = identity).
+    With one chunk, steps 2 and 3 of the graph read W1 straight from the parameter wire (no shadow
+    rebuild between the steps)."""
+    steps = 3
     runs = []
     for mode in ("graph", "eager"):
         _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
