@@ -94,9 +94,6 @@ def parse():
     ap.add_argument("--fwd-only", type=int, default=1,
                     help="also time the forward alone (eval mode: EMA-BN forward + cosine + loss, "
                          "new_dssm.py:274-285) over the staged batches, N=1")
-    ap.add_argument("--zb16", type=int, default=0,
-                    help="plan option ZB16: the hidden layers' pre-BN activations stored as bf16 (bf16 mode; "
-                         "not the headline: it doubles the bf16 mode's loss error against fp32, DESIGN 3)")
     ap.add_argument("--idle-before-warmup", type=float, default=0.0,
                     help="analysis only: seconds of host sleep between the graph builds and the warm-up")
     ap.add_argument("--busy-before-warmup", type=float, default=0.0,
@@ -104,10 +101,10 @@ def parse():
     return ap.parse_args()
 
 
-def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int, s_out: int = 4) -> int:
+def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int) -> int:
     """indptr + (index, value) per nnz + one gathered W1 row (n1*s_w) per nnz
-    + one Z1 output row per input row (fp32; bf16 under the plan option ZB16: s_out = 2)."""
-    return 4 * (rows + 1) + nnz * (4 + 4) + nnz * n1 * s_w + rows * n1 * s_out
+    + fp32 Z1 output row per input row."""
+    return 4 * (rows + 1) + nnz * (4 + 4) + nnz * n1 * s_w + rows * n1 * 4
 
 
 def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: int, rows: int,
@@ -566,8 +563,6 @@ def main():
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
     if args.deterministic:
         model.set_option("DETERMINISTIC", True)
-    if args.zb16:
-        model.set_option("ZB16", True)
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
@@ -841,8 +836,7 @@ def main():
         range_elems = wire_elems + (n_params - geo["extent"])
         wire_parts = rehearse
     kern = {
-        "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w, 2 if model.schedule().get("ZB16") else 4),
-                     probes.get("spmm_fwd", 0.0)),
+        "spmm_fwd": (spmm_alg_bytes(nnz_avg, rows, WIDTHS[0], s_w), probes.get("spmm_fwd", 0.0)),
         "adam": (adam_alg_bytes(n_params, args.dtype == "bf16", fused, w1_elems, nnz_avg, rows,
                                 WIDTHS[0], range_elems, wire_elems, wire_parts), probes.get("adam", 0.0)),
     }

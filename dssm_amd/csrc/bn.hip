@@ -443,16 +443,7 @@ constexpr int kApplyMaxLd = 512;
 // tiles of the dW blocks (tn.h)
 static_assert(kTnTile * 2 >= 128 * kTnLd, "a 128-row sub-chunk per operand");
 constexpr int kApplySmemFloats = 2 * 6 * kApplyMaxLd > kTnTile * 2 ? 2 * 6 * kApplyMaxLd : kTnTile * 2;
-// 4 pre-BN values at element offset o: fp32, or bf16 (plan option ZB16)
-__device__ __forceinline__ float4 load_z4(const void* Z, bool zb16, size_t o) {
-  if (zb16) {
-    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const u16*>(Z) + o);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-  }
-  return *reinterpret_cast<const float4*>(static_cast<const float*>(Z) + o);
-}
-__global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const void* __restrict__ Z, int zb16,
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
                                                          u16* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
@@ -495,7 +486,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const void* __restrict_
   if (i0 < total) {
     const int r = (int)(i0 / q);
     const int c = (int)(i0 - (size_t)r * q) * 4;
-    z0 = load_z4(Z, zb16 != 0, (size_t)r * ld + c);
+    z0 = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
     da0 = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
   }
   {  // coefficients of all 2*ld (tower, column) items: every load in flight at once
@@ -533,7 +524,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const void* __restrict_
     const int t = r < b.rows_q ? 0 : 1;
     float4 z = z0, da = da0;
     if (i != i0) {
-      z = load_z4(Z, zb16 != 0, (size_t)r * ld + c);
+      z = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
       da = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
     }
     const float zz[4] = {z.x, z.y, z.z, z.w}, dd[4] = {da.x, da.y, da.z, da.w};
@@ -627,7 +618,7 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
   return hipGetLastError();
 }
 
-hipError_t launch_bn_bwd_apply_fused(const void* Z, bool zb16, const float* dA, const BnSide& b, uint16_t* dZ,
+hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part, int loss_blocks,
                                      float* loss_out, const TnParams* dw) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
@@ -640,7 +631,7 @@ hipError_t launch_bn_bwd_apply_fused(const void* Z, bool zb16, const float* dA, 
   const TnParams p = dw ? *dw : TnParams{};
   const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
   const int dw_blocks = dw ? dw_x * dw_y * cdiv(p.K, p.k_per_split) : 0;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, zb16 ? 1 : 0, dA, b,
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, dA, b,
                      (u16*)dZ, loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks);
   return hipGetLastError();
 }

@@ -211,10 +211,8 @@ __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthr
 // Per-tower column sums of z and z^2 of one kSumsRows x 64 block (NT threads: NT/64 row groups),
 // fp64 atomics into fsum [2 towers][2][ldz]; blocks never straddle the tower boundary.
 constexpr int kSumsRows = 128;
-__device__ __forceinline__ float zval(const float* Z, size_t i) { return Z[i]; }
-__device__ __forceinline__ float zval(const u16* Z, size_t i) { return bf2f(Z[i]); }
-template <int NT, typename TZ>
-__device__ __forceinline__ void bn_sums_block(const TZ* __restrict__ Z, int ldz, int ncol,
+template <int NT>
+__device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int ldz, int ncol,
                                               int row_split, int rows, double* __restrict__ fsum,
                                               int bx, int by, double (*s_red)[NT / 64][64],
                                               DetAcc det = DetAcc{}, int nby = 0) {
@@ -227,7 +225,7 @@ __device__ __forceinline__ void bn_sums_block(const TZ* __restrict__ Z, int ldz,
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {  // all loads issued before any arithmetic
     const int r = r0 + g + NG * i;
-    x[i] = zval(Z, (size_t)(r < r1 ? r : r0) * ldz + (c < ldz ? c : 0));
+    x[i] = Z[(size_t)(r < r1 ? r : r0) * ldz + (c < ldz ? c : 0)];
   }
   double s = 0.0, q = 0.0;
 #pragma unroll

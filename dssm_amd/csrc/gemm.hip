@@ -312,13 +312,11 @@ struct NtFuse {
   int in_from_sums;  // BN_A: derive the A operand's coefficients from `in`'s sums
   BnSide in;
   double* out_sum;   // [2 towers][2][ldc]
-  const void* zb;    // FS == 2: pre-BN activations of the output layer [M x ldc] (fp32, or bf16: zb16)
-  int zb16;
+  const float* zb;   // FS == 2: pre-BN activations of the output layer [M x ldc]
   const float* coefb;  // FS == 2: its coefficients [4][2][ldc]
   int lds_epi;             // whole-K tiles: C staged through LDS, stored as 16-B row segments
   DetAcc det;              // deterministic mode: out_sum by slab rows + fixed-order last-arrival sum
   int det_rows;            // the launch's row tiles (arrivals per column tile)
-  int c16;                 // whole-K forward: C stored as bf16 (plan option ZB16), rounded before its sums
 };
 
 template <bool BN_A, int FS>
@@ -371,7 +369,7 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-          zb[i][j][r] = static_cast<const float*>(f.zb)[(size_t)(m < M ? m : 0) * ldc + (okn ? n : 0)];
+          zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * ldc + (okn ? n : 0)];
         }
     }
   }
@@ -568,8 +566,7 @@ __host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM 
   return wk_red_offset(Kp, lds_epi, WM) + (size_t)WM * 64 * 2 * 8;
 }
 
-// A16 (BN_A): the pre-BN activations Z are bf16 (plan option ZB16), half the A panel's bytes.
-template <bool BN_A, int FS, int WM = 4, bool A16 = false>
+template <bool BN_A, int FS, int WM = 4>
 __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
                                            u16* wk_smem) {
   constexpr int NT = 128 * WM, ROWS = 32 * WM, BT = NT / 64;  // threads, tile rows, B threads / row
@@ -607,7 +604,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     for (int i = 0; i < NGA; ++i) {
       const int kg = (ag0 + 4 * i) * 8;
       const size_t off = (rok && kg < lda) ? rbase + kg : 0;
-      if constexpr (BN_A && !A16) {
+      if constexpr (BN_A) {
         fa[i][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
         fa[i][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
       } else {
@@ -644,8 +641,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-          const size_t zo = (size_t)(m < M ? m : 0) * ldc + (n < N ? n : 0);
-          zb[i][j][r] = f.zb16 ? bf2f(static_cast<const u16*>(f.zb)[zo]) : static_cast<const float*>(f.zb)[zo];
+          zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * ldc + (n < N ? n : 0)];
         }
     }
   }
@@ -693,17 +689,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
           if (ok) {
             const float* ci = &sCoef[(tower * 2) * Kp + kg];
             const float* ch = ci + Kp;
-            float z[8];
-            if constexpr (A16) {
-              const uint4 u = ua[i];
-              z[0] = __uint_as_float(u.x << 16); z[1] = __uint_as_float(u.x & 0xffff0000u);
-              z[2] = __uint_as_float(u.y << 16); z[3] = __uint_as_float(u.y & 0xffff0000u);
-              z[4] = __uint_as_float(u.z << 16); z[5] = __uint_as_float(u.z & 0xffff0000u);
-              z[6] = __uint_as_float(u.w << 16); z[7] = __uint_as_float(u.w & 0xffff0000u);
-            } else {
-              z[0] = fa[i][0].x; z[1] = fa[i][0].y; z[2] = fa[i][0].z; z[3] = fa[i][0].w;
-              z[4] = fa[i][1].x; z[5] = fa[i][1].y; z[6] = fa[i][1].z; z[7] = fa[i][1].w;
-            }
+            const float z[8] = {fa[i][0].x, fa[i][0].y, fa[i][0].z, fa[i][0].w,
+                                fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
             float y[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
@@ -782,12 +769,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m < M && n < ldc) {
           const float v = acc[i][j][r];
-          float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
-          if (f.c16) x = bf2f(f2bf(x));  // bf16 output: the statistics describe the stored value
+          const float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
           if (lds_epi)
             sC[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * kCld + wn * 32 + j * 16 + (lane & 15)] = x;
-          else if (f.c16)
-            reinterpret_cast<u16*>(a.C)[(size_t)m * ldc + n] = f2bf(x);
           else
             a.C[(size_t)m * ldc + n] = x;
           if constexpr (FS == 1) {
@@ -850,17 +834,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 #pragma unroll
     for (int k = 0; k < 4; ++k) {  // ROWS x 16 float4 = 4 per thread
       const int idx = t + NT * k, r = idx >> 4, q = (idx & 15) * 4;
-      if (bm + r < M && q < ncols) {
-        const float4 v = *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
-        if (f.c16) {
-          uint2 h;
-          h.x = pack2bf(v.x, v.y);
-          h.y = pack2bf(v.z, v.w);
-          *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(a.C) + (size_t)(bm + r) * ldc + bn + q) = h;
-        } else {
-          *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) = v;
-        }
-      }
+      if (bm + r < M && q < ncols)
+        *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) =
+            *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
     }
   }
 }
@@ -869,7 +845,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 // Whole-K forward NT GEMM: blocks [0, ntiles) compute tiles (XCD-grouped row blocks); with the
 // A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
 // EMA update) off the tiles' critical path.
-template <bool BN_A, int FS, int WM, bool A16 = false>
+template <bool BN_A, int FS, int WM>
 __global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
   WG_TL(a.N == 300 ? 0 : 1, 0);
@@ -878,7 +854,7 @@ __global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, i
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);
-  nt_wk_body<BN_A, FS, WM, A16>(a, f, tile % nx, tile / nx, wk_smem);
+  nt_wk_body<BN_A, FS, WM>(a, f, tile % nx, tile / nx, wk_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1143,16 +1119,14 @@ static bool det_fits(const NtFuse& f, int ld) {
   return !f.det.slab || (f.det_rows <= f.det.cap && cdiv(ld, 64) <= kDetTiles);
 }
 
-hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const void* Z, int lda, const float* coef,
+hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
-                                    int ldb, void* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s, const DetAcc* det, bool z_bf16,
-                                    bool c_bf16) {
+                                    int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
+                                    double* out_sum, hipStream_t s, const DetAcc* det) {
   if ((lda % 8) || (ldb % 8) || K > lda || K > ldb || lda > kNtMaxK || (row_split % 64))
     return hipErrorInvalidValue;
-  const NtParams a{M, N, K, Z, lda, coef, row_split, (const u16*)BT, ldb, (float*)C, ldc, bias, (u16*)a_out};
+  const NtParams a{M, N, K, Z, lda, coef, row_split, (const u16*)BT, ldb, C, ldc, bias, (u16*)a_out};
   NtFuse f{};
-  f.c16 = c_bf16 ? 1 : 0;
   if (in_from_sums) {
     f.in_from_sums = 1;
     f.in = *in_from_sums;
@@ -1168,19 +1142,15 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const void* Z, int lda,
     f.det_rows = cdiv(M, 32 * WM);                                                            \
     if (!det_fits(f, ldc)) return hipErrorInvalidValue;                                       \
     const int ntiles = nx * cdiv(M, 32 * WM);                                                 \
-    if (z_bf16)                                                                               \
-      hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM, true>), dim3(ntiles + (in_from_sums ? 1 : 0)), \
-                         dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
-    else                                                                                      \
-      hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),  \
-                         dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
+    hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),    \
+                       dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
   }
     if (kWkRows == 64 || (row_split % 128)) DSSM_NTWK(2) else DSSM_NTWK(4)
 #undef DSSM_NTWK
     return hipGetLastError();
   }
   f.det_rows = cdiv(M, 64);
-  if (!det_fits(f, ldc) || z_bf16 || c_bf16) return hipErrorInvalidValue;  // bf16 Z: whole-K tiles only
+  if (!det_fits(f, ldc)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_gemm_nt<true, 1>), dim3(cdiv(ldc, 64), cdiv(M, 64)), dim3(256), 0, s, a, f);
   return hipGetLastError();
 }
@@ -1192,10 +1162,10 @@ hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float*
 }
 
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
-                           int ldw, float* dA, int ldda, const void* z_prev, const float* coef_prev,
+                           int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
                            float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
-                           TnParams* dw_out, const DetAcc* det, bool zprev_bf16) {
+                           TnParams* dw_out, const DetAcc* det) {
   if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || (row_split % 64))
     return hipErrorInvalidValue;
   // dA_{l-1} = dZ_l . W_l^T (the weight shadow rows are k-contiguous), BN_{l-1} bwd sums fused
@@ -1203,7 +1173,6 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   NtFuse f{};
   f.out_sum = bsum_prev;
   f.zb = z_prev;
-  f.zb16 = zprev_bf16 ? 1 : 0;
   f.coefb = coef_prev;
   f.lds_epi = 0;  // measured: 18.1 (register epilogue) vs 18.3 us (LDS-staged) per pair launch
   if (det) f.det = *det;
@@ -1259,7 +1228,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
   const int tn_x = cdiv(n, BN), tn_y = cdiv(Mw, BM);
   const int tn_blocks = tn_x * tn_y * nsplit;
   f.det_rows = cdiv(M, 64);
-  if (!det_fits(f, ldda) || zprev_bf16) return hipErrorInvalidValue;  // bf16 z_prev: whole-K tiles only
+  if (!det_fits(f, ldda)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bwd_pair, dim3(nt_blocks + tn_blocks), dim3(256), 0, s, a, f, nt_x,
                      nt_blocks, p, tn_x, tn_y);
   *deferred_splits = 0;

@@ -58,11 +58,9 @@ hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_i
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
-                            const uint16_t* W, int ldw, int n, const float* bias, void* Z, int ldz,
-                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s,
-                            bool zb16 = false);
-// zb16: Z is bf16 (plan option ZB16: the hidden layers' pre-BN activations stored as bf16)
-hipError_t launch_sums_scatter(const void* Z, bool zb16, int ldz, int n, int row_split, double* fsum,
+                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s);
+hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s,
@@ -111,22 +109,18 @@ hipError_t launch_gemm_nt(int M, int N, int K, const void* A, int lda, bool bn_a
 // forward NT GEMM of layer l with BN_{l-1}+ReLU staged on the A operand, whose coefficients come
 // from `coef` or, when in_from_sums != null, from that layer's sums (and are materialised by
 // one workgroup); the output's per-tower column sums (with bias) are added to out_sum.
-hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const void* Z, int lda, const float* coef,
+hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda, const float* coef,
                                     const BnSide* in_from_sums, int row_split, const uint16_t* BT,
-                                    int ldb, void* C, int ldc, const float* bias, uint16_t* a_out,
-                                    double* out_sum, hipStream_t s, const DetAcc* det = nullptr,
-                                    bool z_bf16 = false, bool c_bf16 = false);
-// z_bf16 / c_bf16 (plan option ZB16): the input pre-BN activations Z / the output C are bf16 at the
-// same row strides (C rounded to bf16 before its column sums: the statistics describe the stored values).
+                                    int ldb, float* C, int ldc, const float* bias, uint16_t* a_out,
+                                    double* out_sum, hipStream_t s, const DetAcc* det = nullptr);
 // Backward of layer l in one launch: dA_{l-1} = dZ_l . W_l^T (+ BN_{l-1} backward sums from
 // z_prev / coef_prev into bsum_prev) and dW_l = [A_{l-1}; 1]^T . dZ_l (split-K into slab;
 // defer: the splits are left for the Adam step, *deferred_splits = count; else reduced into gw).
 hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, const uint16_t* W,
-                           int ldw, float* dA, int ldda, const void* z_prev, const float* coef_prev,
+                           int ldw, float* dA, int ldda, const float* z_prev, const float* coef_prev,
                            double* bsum_prev, int row_split, const uint16_t* A_prev, int lda_prev,
                            float* slab, float* gw, bool defer, hipStream_t s, int* deferred_splits,
-                           TnParams* dw_out = nullptr, const DetAcc* det = nullptr,
-                           bool zprev_bf16 = false);
+                           TnParams* dw_out = nullptr, const DetAcc* det = nullptr);
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
 // caller then sums the slabs into gw with launch_splitk_reduce.
@@ -154,7 +148,7 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
                           const DetAcc* det = nullptr);
 // Fused-statistics backward apply: dZ (bf16) of layer b from Z, dA and b's backward sums;
 // also writes b.dgamma / b.dbeta.
-hipError_t launch_bn_bwd_apply_fused(const void* Z, bool zb16, const float* dA, const BnSide& b, uint16_t* dZ,
+hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part = nullptr,
                                      int loss_blocks = 0, float* loss_out = nullptr,
                                      const TnParams* dw = nullptr);

@@ -254,7 +254,6 @@ struct dssm_plan {
       0,  // DETERMINISTIC: fixed-order reductions, bit-identical repeated runs
       1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
       1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
-      0,  // ZB16: hidden layers' pre-BN activations stored as bf16 (fused statistics + merged CSC)
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -360,8 +359,6 @@ struct dssm_plan {
     return on(DSSM_OPT_MERGED_CSC) && fused_stats() && csc_rank_path() && (Lt.BS % 128) == 0;
   }
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
-  // layer l's pre-BN activations are bf16 (ZB16: the hidden layers of the fused, merged schedule)
-  bool zb16(int l) const { return on(DSSM_OPT_ZB16) && merged_csc() && l < Lt.L - 1; }
   bool fused_stats_ok() const {
     if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -645,8 +642,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   if (merged) {  // the SpMM rows share their launch with the column scan
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
                                    (const uint16_t*)P->weight(0), P->weight_ld(0), Lt.n[0], P->bias(0),
-                                   P->ws + Lt.Z[0], Lt.ldp[0], Lt.D, Lt.max_nnz,
-                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s, P->zb16(0)));
+                                   P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
+                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
   } else {
     // eval: every layer's BN coefficients from the EMA, in the SpMM launch's extra workgroups
     dssm::EvalCoef ec{};
@@ -685,7 +682,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     float* scat_val = det ? P->at<float>(Lt.sort_val) : P->at<float>(Lt.csc_val);
     const dssm::BnSide b0 = P->bn_side(0);
     if (merged)
-      HIP_TRY(dssm::launch_sums_scatter(P->ws + Lt.Z[0], P->zb16(0), Lt.ldp[0], Lt.n[0], Lt.BS,
+      HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
                                         P->at<int>(Lt.col_ptr), scat_row, scat_val,
@@ -698,10 +695,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
       const dssm::BnSide in = P->bn_side(l - 1);
       const dssm::BnSide out = P->bn_side(l);
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
-          Lt.R, Lt.n[l], Lt.n[l - 1], P->ws + Lt.Z[l - 1], Lt.ldp[l - 1],
+          Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1],
-          P->ws + Lt.Z[l], Lt.ldp[l], P->bias(l), P->at<uint16_t>(Lt.A[l - 1]),
-          P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr, P->zb16(l - 1), P->zb16(l)));
+          P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<uint16_t>(Lt.A[l - 1]),
+          P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr));
     }
     const int lL = Lt.L - 1;
     const dssm::BnSide last = P->bn_side(lL);
@@ -830,7 +827,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
-      HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->ws + Lt.Z[l], P->zb16(l), P->at<float>(Lt.dA[l]), b,
+      HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                               P->at<uint16_t>(Lt.dZ[l]), s,
                                               fin ? P->at<float>(Lt.loss_j) : nullptr,
                                               dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true),
@@ -849,10 +846,10 @@ static int backward_impl(dssm_plan* P, void* stream) {
       HIP_TRY(dssm::launch_bwd_pair(
           Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
           P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
-          P->ws + Lt.Z[l - 1], P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
+          P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
           Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
           P->g + Lt.fc_off[l], defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
-          P->deterministic() ? &bprev.bdet : nullptr, P->zb16(l - 1)));
+          P->deterministic() ? &bprev.bdet : nullptr));
       dw_pending = host_dw && dw.C != nullptr;
       if (dw_pending && !defer_slabs && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
     }
@@ -1207,7 +1204,6 @@ int dssm_plan_schedule(const dssm_plan* P) {
   if (fs && P->on(DSSM_OPT_DW_IN_APPLY)) f |= DSSM_SCHED_DW_IN_APPLY;
   if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
   if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;
-  if (P->zb16(0)) f |= DSSM_SCHED_ZB16;
   return f;
 }
 

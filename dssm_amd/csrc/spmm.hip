@@ -48,7 +48,7 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
                                           const float* __restrict__ values, int rows,
                                           const TW* __restrict__ W, int ldw, int n,
                                           const float* __restrict__ bias, float* __restrict__ Z,
-                                          int ldz, int b, bool relu = false, bool zb16 = false) {
+                                          int ldz, int b, bool relu = false) {
   const int row = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
   const int lane = lane_id();
@@ -64,12 +64,7 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = fmaxf(acc[i], 0.f);
     }
-    if (c < ldz) {
-      if (zb16)  // bf16 pre-BN activations (plan option ZB16): Z holds u16 at the same row stride
-        store8(reinterpret_cast<u16*>(Z) + (size_t)row * ldz + c, acc);
-      else
-        store8(Z + (size_t)row * ldz + c, acc);
-    }
+    if (c < ldz) store8(Z + (size_t)row * ldz + c, acc);
   }
 }
 
@@ -582,8 +577,7 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
                                                    const int* __restrict__ cnt, int D,
                                                    int* __restrict__ col_ptr,
                                                    int* __restrict__ heavy_n,
-                                                   int2* __restrict__ heavy_items, int nscan,
-                                                   int zb16) {
+                                                   int2* __restrict__ heavy_items, int nscan) {
   __shared__ int s_wave[kScanSmallNT / 64];
   __shared__ int s_hbase;
 #if DSSM_SCAN_LAST  // the scan workgroups after the row workgroups in dispatch order
@@ -603,7 +597,7 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
     const int row = rb * 4 + (threadIdx.x >> 6);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, rb, false, zb16 != 0);
+    spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, rb);
 #ifdef DSSM_WG_TL
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((threadIdx.x & 63) == 0 && row < rows && row < 8192) {
@@ -614,7 +608,7 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
   }
 }
 
-__global__ __launch_bounds__(256) void k_sums_scatter(const void* __restrict__ Z, int zb16, int ldz, int ncol,
+__global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ Z, int ldz, int ncol,
                                                       int row_split, double* __restrict__ fsum,
                                                       int nsum_x, int nsum,
                                                       const int* __restrict__ indptr,
@@ -629,12 +623,7 @@ __global__ __launch_bounds__(256) void k_sums_scatter(const void* __restrict__ Z
   __shared__ double s_red[2][4][64];
   const int b = blockIdx.x;
   if (b < nsum)
-    if (zb16)
-      bn_sums_block<256>(static_cast<const u16*>(Z), ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x,
-                         s_red, det, nsum / nsum_x);
-    else
-      bn_sums_block<256>(static_cast<const float*>(Z), ldz, ncol, row_split, rows, fsum, b % nsum_x,
-                         b / nsum_x, s_red, det, nsum / nsum_x);
+    bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red, det, nsum / nsum_x);
   else
     scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val,
                  csc_col, b - nsum, (int)gridDim.x - nsum);
@@ -1022,19 +1011,19 @@ bool csc_rank_supported(int D) {
 }
 
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
-                            const uint16_t* W, int ldw, int n, const float* bias, void* Z, int ldz,
-                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s, bool zb16) {
+                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s) {
   int* cnt = scratch;
   int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
   int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const int nscan = cdiv(D + 1, kScanSmallNT * 4);
   hipLaunchKernelGGL(k_spmm_scan<u16>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
-                     values, rows, (const u16*)W, ldw, n, bias, (float*)Z, ldz, cnt, D, col_ptr, heavy_n,
-                     heavy_items, nscan, zb16 ? 1 : 0);
+                     values, rows, (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
+                     heavy_items, nscan);
   return hipGetLastError();
 }
 
-hipError_t launch_sums_scatter(const void* Z, bool zb16, int ldz, int n, int row_split, double* fsum,
+hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out,
@@ -1050,8 +1039,7 @@ hipError_t launch_sums_scatter(const void* Z, bool zb16, int ldz, int n, int row
     *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                               csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
   }
-  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z,
-                     zb16 ? 1 : 0, ldz, n, row_split,
+  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n, row_split,
                      fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                      csc_row, csc_val, csc_col, det ? *det : DetAcc{});
   return hipGetLastError();

@@ -68,8 +68,7 @@ enum {
   DSSM_BUF_PROB,            /* float[BS*(NEG+1)] softmax (new_dssm.py:206) */
   DSSM_BUF_QUERY_NORM,      /* float[BS] query_norm_single (new_dssm.py:187) */
   DSSM_BUF_EMBED,           /* float[R*ldp(n_L)] embeddings: rows [q; pos; neg] (new_dssm.py:156-158) */
-  DSSM_BUF_Z,               /* float[R*ldp(n_l)] pre-BN activations of layer `layer` (bf16 at the
-                               same row stride for l < L-1 when the schedule has DSSM_SCHED_ZB16) */
+  DSSM_BUF_Z,               /* float[R*ldp(n_l)] pre-BN activations of layer `layer` */
   DSSM_BUF_BATCH_MEAN,      /* float[2*n_l]: batch mean, tower q then d (new_dssm.py:77) */
   DSSM_BUF_BATCH_VAR,       /* float[2*n_l] */
   DSSM_BUF_DZ,              /* dZ of layer `layer` (compute dtype, R*ldp) */
@@ -145,11 +144,7 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *   FUSED_W1_ADAM   see dssm_plan_set_fused_w1_adam
  *   RANK_IN_ADAM    1: in multi-step graphs (dssm_plan_graph_build_steps) step i's Adam launch also
  *                      runs step i+1's CSC rank pass (with MERGED_CSC and FUSED_W1_ADAM), so that
- *                      step's forward skips the rank launch
- *   ZB16            0; 1: with FUSED_STATS and MERGED_CSC, the hidden layers' pre-BN activations Z_l
- *                      (l < L) are stored as bf16 (the SpMM / forward NT epilogues round them, the
- *                      column sums are of the rounded values, every consumer reads bf16); the last
- *                      layer's stays fp32.  0: fp32 Z everywhere */
+ *                      step's forward skips the rank launch */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -161,7 +156,6 @@ enum {
   DSSM_OPT_DETERMINISTIC,
   DSSM_OPT_FUSED_W1_ADAM,
   DSSM_OPT_RANK_IN_ADAM,
-  DSSM_OPT_ZB16,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);
@@ -261,8 +255,7 @@ enum {
   DSSM_SCHED_WHOLEK = 16,          /* layers >= 2 on the whole-K bf16 NT / backward-pair GEMMs */
   DSSM_SCHED_DW_IN_APPLY = 32,     /* dW_l split-K tiles inside the next BN-backward apply launch */
   DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
-  DSSM_SCHED_DETERMINISTIC = 128,  /* fixed-order reductions: bit-identical repeated runs */
-  DSSM_SCHED_ZB16 = 256            /* hidden layers' pre-BN activations stored as bf16 */
+  DSSM_SCHED_DETERMINISTIC = 128   /* fixed-order reductions: bit-identical repeated runs */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
 /* The fused-statistics train forward leaves the loss / accuracy reduction to the backward's first

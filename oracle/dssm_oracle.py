@@ -52,8 +52,8 @@ def bf16_round(x) -> np.ndarray:
 
 
 def _rw(a, emulate):
-    """Operand as the matrix cores see it: bf16 under ``emulate`` "bf16" / "bf16z", unchanged otherwise."""
-    return bf16_round(a) if emulate in ("bf16", "bf16z") else a
+    """Operand as the matrix cores see it: bf16 under ``emulate == "bf16"``, unchanged otherwise."""
+    return bf16_round(a) if emulate == "bf16" else a
 
 
 @dataclasses.dataclass
@@ -239,9 +239,7 @@ def forward(cfg: OracleConfig, params, ema, batch, train: bool = True, dtype=np.
     reference is fp32 throughout, new_dssm.py:111-114): every weight W_l is read as its bf16
     shadow, and each hidden layer's post-BN/ReLU activation is rounded to bf16 before it feeds
     the next layer's product (the last layer's embeddings stay fp32).  Everything else --
-    BN statistics, cosine, softmax, loss -- is computed as in fp32 mode.  ``emulate="bf16z"`` adds
-    the plan option ZB16 (include/dssm.h): each hidden layer's pre-BN activation Z_l is rounded to
-    bf16 before its statistics and normalisation (the last layer's stays fp32)."""
+    BN statistics, cosine, softmax, loss -- is computed as in fp32 mode."""
     dt = dtype
     X = csr_matrix(batch["indptr"], batch["indices"], batch["values"], cfg.rows, cfg.trigram_d, dt)
     cache = {"X": X, "layers": [], "emulate": emulate}
@@ -251,8 +249,6 @@ def forward(cfg: OracleConfig, params, ema, batch, train: bool = True, dtype=np.
         W = _rw(params[f"W{l}"], emulate).astype(dt)
         b = params[f"b{l}"].astype(dt)
         Z = (X @ W if l == 1 else A @ W) + b
-        if emulate == "bf16z" and l < cfg.n_layers:
-            Z = bf16_round(Z).astype(dt)  # stored as bf16 (ZB16)
         lc = bn_relu_forward(cfg, Z, params, l, ema, new_ema if train else None, dt)
         lc["A_in"] = A
         A = lc["A"]

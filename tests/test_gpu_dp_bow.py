@@ -221,8 +221,7 @@ def test_bow_data_parallel_world2(mode, wire):
     v0 = {k: v.cpu().numpy().astype(np.float64) for k, v in e.named_adam()[1].items()}
     gsum = None
     for r in range(WORLD):
-        emu = "bf16z" if e.schedule().get("ZB16") else "bf16"  # + bf16 hidden pre-BN activations
-        cache, _ = O.forward(cfg, p0, O.make_ema(cfg), _shard(1, r).as_dict(), True, np.float64, emulate=emu)
+        cache, _ = O.forward(cfg, p0, O.make_ema(cfg), _shard(1, r).as_dict(), True, np.float64, emulate="bf16")
         lr_ = abs(float(res[1, r]["loss"][0]) - cache["loss"]) / abs(cache["loss"])
         errs[f"loss_rank{r}_vs_oracle"] = (lr_, 1e-4)
         g = O.backward(cfg, p0, cache, np.float64)
