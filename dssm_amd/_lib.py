@@ -146,6 +146,8 @@ _SIGS = {
     "dssm_spmm_bwd_ws_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "dssm_spmm_csr_bwd_w": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                       _P, _P, _P]),
+    "dssm_cosine_softmax_loss_mapped": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_float, _P, _P,
+                                                  _P, _P, _P, _P, _P, _P]),
     "dssm_csc_transpose": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P]),
     "dssm_adam_probe": (C.c_int, [C.c_int]),
     "dssm_adam_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),

@@ -51,12 +51,15 @@ __device__ unsigned long long g_cos_tl[1024][8];  // 0 start 1 end, 2..6 phases 
   do {              \
   } while (0)
 #endif
-template <int EPL, int KM, bool FSC, int NW>
+// MAP: the merged row r of [q; pos; neg] is read from z row rmap[r] (the multi-view model's in-batch
+// rotation as an index map instead of a gathered copy); dy stays in the merged layout.
+template <int EPL, int KM, bool FSC, int NW, bool MAP = false>
 __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
-    float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat) {
+    float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat,
+    const int* __restrict__ rmap) {
   constexpr int NT = 64 * NW;
   COS_TL(0);
   __shared__ float s_part[2][NW];
@@ -71,17 +74,21 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
   // coefficient): query row + K doc rows
   float q[EPL], d[KM][EPL], zq[EPL], zd[FSC ? KM : 1][EPL];
   if (j < bs && (int)blockIdx.x < nrow_blocks) {
+    int src[1 + KM];  // the source rows (MAP: wave-uniform map reads)
+    src[0] = MAP ? rmap[j] : j;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) src[1 + k] = k < K ? (MAP ? rmap[doc_row(j, k, bs, neg)] : doc_row(j, k, bs, neg)) : 0;
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const int c = lane + 64 * e;
-      q[e] = (c < n) ? z[(size_t)j * ld + c] : 0.f;
+      q[e] = (c < n) ? z[(size_t)src[0] * ld + c] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < KM; ++k)
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
         const int c = lane + 64 * e;
-        d[k][e] = (k < K && c < n) ? z[(size_t)doc_row(j, k, bs, neg) * ld + c] : 0.f;
+        d[k][e] = (k < K && c < n) ? z[(size_t)src[1 + k] * ld + c] : 0.f;
       }
   }
   if constexpr (FSC) {
@@ -320,8 +327,8 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              const CscScatter* scatter) {
-  if (neg + 1 > MAXK || n > kCosMaxN) return hipErrorInvalidValue;
+                              const CscScatter* scatter, const int* rmap) {
+  if (neg + 1 > MAXK || n > kCosMaxN || (rmap && (fused || coef || y_out))) return hipErrorInvalidValue;
   // ws: the per-workgroup loss / accuracy partials (2 floats each)
   const int nw = cosine_waves(n, fused != nullptr);
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
@@ -340,10 +347,13 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
-                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc);        \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr); \
+  else if (rmap)                                                                                \
+    hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, true>), grid, block, 0, s, z, ld, n, bs, neg, gamma, \
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap);         \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc)
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \

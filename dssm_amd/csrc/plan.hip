@@ -1472,6 +1472,18 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
   return DSSM_OK;
 }
 
+int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_map, int n, int query_bs, int neg,
+                                    float gamma, float* cos_sim_raw, float* cos_sim, float* prob,
+                                    float* query_norm, float* loss, float* dy, float* ws, void* stream) {
+  if (!y || !row_map || !cos_sim_raw || !cos_sim || !prob || !query_norm || !loss || !dy || !ws ||
+      query_bs < 1 || neg < 1 || neg > 15 || n < 1 || n > 512 || ld < n)
+    return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss_mapped: bad arguments");
+  HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
+                                   cos_sim, prob, query_norm, ws, loss, dy, (hipStream_t)stream, nullptr,
+                                   false, nullptr, row_map));
+  return DSSM_OK;
+}
+
 int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
                              float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
                              float* loss, float* dy, float* ws, void* stream) {

@@ -11,8 +11,8 @@ chains overlap on the CUs.  Composed from libdssm.so's functional C-ABI (include
 dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2) with the ReLUs in their epilogues
 (dssm_spmm_csr_fwd_act / dssm_dense_fwd_act, dssm_dense_bwd_masked: FC1's ReLU backward on dA1),
 dssm_rows_gather_sum (the rotation's gradient x BS with FC2's ReLU backward),
-dssm_rows_gather (the rotation as an index map),
-dssm_cosine_softmax_loss (shared with the BoW path), dssm_adam_step.  fp32; torch tensors are
+dssm_cosine_softmax_loss_mapped (the cosine kernel shared with the BoW path, reading the rotation's
+merged rows through an index map), dssm_adam_step.  fp32; torch tensors are
 device storage only.
 
 The reference chooses the view with a Python comparison against a placeholder at graph build, so
@@ -73,7 +73,6 @@ class MultiViewDSSM:
         self.a1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
         self.ysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)   # [user_y; item_y]
         self.dz2src = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)  # FC2's dz, [user; item]
-        self.merged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         self.dmerged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         # per-tower backward scratch: the two towers run concurrently (user tower on the caller's
         # stream, the item tower on self.aux)
@@ -197,13 +196,11 @@ class MultiViewDSSM:
         self._tower_fwd("u", "user", self.ysrc[:BS], s)
         self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], sa)
         main.wait_stream(self.aux)
-        R = BS * (2 + self.neg)
-        check(self.lib.dssm_rows_gather(ptr(self.ysrc), self.ld2, ptr(self.map), R, self.l2, ptr(self.merged),
-                                        self.ld2, s), "gather")
-        check(self.lib.dssm_cosine_softmax_loss(ptr(self.merged), self.ld2, self.l2, BS, self.neg, self.gamma,
-                                                ptr(self.cos_raw), ptr(self.cos_sim), ptr(self.prob),
-                                                ptr(self.qnorm), ptr(self.loss_buf), ptr(self.dmerged),
-                                                ptr(self.cos_ws), s), "cosine")
+        # Make_Negative_Item's merged rows read through the index map by the cosine kernel itself
+        check(self.lib.dssm_cosine_softmax_loss_mapped(ptr(self.ysrc), self.ld2, ptr(self.map), self.l2, BS,
+                                                       self.neg, self.gamma, ptr(self.cos_raw), ptr(self.cos_sim),
+                                                       ptr(self.prob), ptr(self.qnorm), ptr(self.loss_buf),
+                                                       ptr(self.dmerged), ptr(self.cos_ws), s), "cosine")
 
     def _tower_bwd(self, key, tower, dz2, s):
         ip, ix, vv = self.batch[key]

@@ -298,6 +298,12 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
 int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
                              float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
                              float* loss, float* dy, float* ws, void* stream);
+/* The same with the rows read through a map: merged row r of [q; pos; neg] is y row row_map[r]
+ * (multi_view_dssm_v3's in-batch rotated negatives, Make_Negative_Item, without a gathered copy);
+ * dy [R x ld] is in the merged layout. */
+int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_map, int n, int query_bs, int neg,
+                                    float gamma, float* cos_sim_raw, float* cos_sim, float* prob,
+                                    float* query_norm, float* loss, float* dy, float* ws, void* stream);
 
 /* ---- functional backward (the per-op gradients; the plan fuses them) ---------------------- */
 /* tf.sparse_tensor_dense_matmul's weight gradient (new_dssm.py:124-126 autodiff, dense like
