@@ -4,7 +4,7 @@ set -eu
 mkdir -p gpurun_out/mv
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_multiview.py tests/test_gpu_multiview_c5.py tests/test_gpu_multiview_dp.py \
-  tests/test_gpu_api.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/mv/tests.log 2>&1 \
+  tests/test_gpu_api.py tests/test_gpu_parity.py tests/test_gpu_rnn.py -x -q --timeout 200 --timeout-method thread > gpurun_out/mv/tests.log 2>&1 \
   || { tail -30 gpurun_out/mv/tests.log; exit 1; }
 tail -2 gpurun_out/mv/tests.log
 for r in 1 2; do
