@@ -1641,8 +1641,6 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   return DSSM_OK;
 }
 
-static int Lt_n0(const dssm_plan* P) { return P->Lt.n[0]; }
-
 int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, const int32_t* const* indices,
                                    const float* const* values, int nsteps, float grad_scale, int comm,
                                    float link_gbps, float latency_us, int overlap, int with_probes,
@@ -1753,7 +1751,7 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     // one chunk the wire already holds W1 row-major: the region's next step reads it directly
     // (w1_wire) and only the last step rebuilds the shadow, which the next region's first step and
     // the eval forward read.
-    const bool direct = C == 1 && P->geo.n == Lt_n0(P) && i + 1 < nsteps;
+    const bool direct = C == 1 && P->geo.n == P->Lt.n[0] && i + 1 < nsteps;
     for (int c = 0; c < C && !rc; ++c) {
       DP_TRY(wait(s, e_ag[c]));
       if (!direct)
