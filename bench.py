@@ -67,10 +67,8 @@ def parse():
     ap.add_argument("--link-latency-us", type=float, default=10.0,
                     help="modelled fixed cost per collective for --rehearse-comm model (us)")
     ap.add_argument("--dp-chunks", type=int, default=1,
-                    help="N>1 bf16 wire: W1's rows exchanged in this many pieces (with --dp-overlap each "
-                         "piece's collectives overlap the next piece's kernels)")
-    ap.add_argument("--dp-overlap", type=int, default=0,
-                    help="N>1 captured step: the collectives on a second captured stream (fork / join edges)")
+                    help="N>1 bf16 wire: W1's rows exchanged in this many pieces (1: the parameter wire is "
+                         "read by the next step's SpMM directly)")
     ap.add_argument("--model", default="bow", choices=["bow", "rnn", "multiview"],
                     help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4); "
                          "multiview: multi_view_dssm_v3 (config 5)")
@@ -566,8 +564,7 @@ def main():
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
-        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks,
-                          overlap=bool(args.dp_overlap))
+        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks)
     rehearse = args.rehearse_world if world == 1 else 1
     if rehearse > 1:
         # rank 0's kernels of a W-rank bf16-wire step in the data-parallel step graph, each
@@ -607,8 +604,7 @@ def main():
             if rehearse == 1:
                 return dp.build_region(batches, probes=probes)
             return model.graph_build_dp_steps(batches, 1.0 / rehearse, comm=comm_mode, link_gbps=args.link_gbps,
-                                              latency_us=args.link_latency_us, overlap=bool(args.dp_overlap),
-                                              probes=probes)
+                                              latency_us=args.link_latency_us, probes=probes)
         try:
             reg, cyc, part = {}, None, {}
             for n in {args.warmup, args.steps} - {0}:
@@ -881,14 +877,13 @@ def main():
     if fwd is not None:
         out["fwd_only"] = fwd
     if rehearse > 1:
-        out["rehearsal"] = {"world": rehearse, "chunks": args.dp_chunks, "overlap": bool(args.dp_overlap),
+        out["rehearsal"] = {"world": rehearse, "chunks": args.dp_chunks,
                             "collectives": ({"model": f"modelled: {args.link_latency_us} us + bytes sent / "
                                                       f"{args.link_gbps} GB/s per collective",
                                              "copy": "device copies of the same bytes"}[args.rehearse_comm]),
                             "note": "rank 0 of an N-rank bf16-wire step on one GPU; not a headline number"}
     if dp is not None:
         out["config"]["dp_chunks"] = dp.chunks
-        out["config"]["dp_overlap"] = dp.overlap
         out["config"]["dp_launch"] = ("one graph per region, collectives captured" if region_graphs is not None
                                       else "split graphs, host-issued collectives" if args.graph else "eager")
         if dp_capture_error:

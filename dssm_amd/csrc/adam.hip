@@ -693,6 +693,35 @@ hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, WireGeo geo, 
   return hipGetLastError();
 }
 
+// Device-to-device copy as a kernel node (the data-parallel graphs' own-chunk all-to-all copy and the
+// copy rehearsal): ordered like every other kernel of the captured stream.  16-B lanes when both
+// pointers and the size allow it, else 4-B, else bytes.
+__global__ __launch_bounds__(256) void k_copy_bytes(void* __restrict__ dst, const void* __restrict__ src,
+                                                    size_t bytes, int width) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (width == 16) {
+    for (size_t i = t; i < bytes / 16; i += stride)
+      static_cast<uint4*>(dst)[i] = static_cast<const uint4*>(src)[i];
+  } else if (width == 4) {
+    for (size_t i = t; i < bytes / 4; i += stride)
+      static_cast<unsigned*>(dst)[i] = static_cast<const unsigned*>(src)[i];
+  } else {
+    for (size_t i = t; i < bytes; i += stride)
+      static_cast<unsigned char*>(dst)[i] = static_cast<const unsigned char*>(src)[i];
+  }
+}
+
+hipError_t launch_copy_bytes(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  const uintptr_t a = (uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes;
+  const int width = (a % 16 == 0) ? 16 : (a % 4 == 0) ? 4 : 1;
+  const size_t items = bytes / width;
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_copy_bytes, dim3(grid), dim3(256), 0, s, dst, src, bytes, width);
+  return hipGetLastError();
+}
+
 hipError_t launch_spin(double ns, hipStream_t s) {
   const unsigned long long ticks = ns > 0 ? (unsigned long long)(ns / 10.0 + 0.5) : 0ull;
   hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks);

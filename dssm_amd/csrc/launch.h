@@ -325,5 +325,7 @@ hipError_t launch_wire_pack(const float* g, uint16_t* wire, int D, WireGeo geo, 
 hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, WireGeo geo, int chunk, hipStream_t s);
 // one workgroup spinning for `ns` nanoseconds (the data-parallel rehearsal's modelled collective)
 hipError_t launch_spin(double ns, hipStream_t s);
+// device-to-device copy as a kernel (captured graphs: ordered like the neighbouring kernel nodes)
+hipError_t launch_copy_bytes(void* dst, const void* src, size_t bytes, hipStream_t s);
 
 }  // namespace dssm

@@ -1582,8 +1582,7 @@ static int all_to_all_impl(const void* send, void* recv, int64_t count, ncclData
   const char* sp = static_cast<const char*>(send);
   char* rp = static_cast<char*>(recv);
   const size_t chunk = (size_t)count * es;
-  HIP_TRY(hipMemcpyAsync(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk,
-                         hipMemcpyDeviceToDevice, s));
+  HIP_TRY(dssm::launch_copy_bytes(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk, s));
   if (g_world == 1) return DSSM_OK;
   RCCL_TRY(ncclGroupStart());
   for (int j = 0; j < g_world; ++j) {
@@ -1631,8 +1630,8 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   uint16_t* st = const_cast<uint16_t*>(P->gstage) + chunk * blk;
   uint16_t* pw = P->pwire + chunk * blk;
   if (k.mode == 1) {  // same bytes through HBM (the tail's copy is skipped: 0.5 MB)
-    if (kind == 0) HIP_TRY(hipMemcpyAsync(st, gw, blk * 2, hipMemcpyDeviceToDevice, cs));
-    if (kind == 1) HIP_TRY(hipMemcpyAsync(st, pw, blk * 2, hipMemcpyDeviceToDevice, cs));
+    if (kind == 0) HIP_TRY(dssm::launch_copy_bytes(st, gw, blk * 2, cs));
+    if (kind == 1) HIP_TRY(dssm::launch_copy_bytes(st, pw, blk * 2, cs));
     return DSSM_OK;
   }
   if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs);
@@ -1652,6 +1651,9 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   if (!P->pwire || !wire_gradient_pass(P))
     return fail(DSSM_E_INVALID, "the data-parallel graph needs the bf16 wire (dssm_plan_set_dp_wire) and the "
                                 "wire gradient pass (HEAVY_IN_ADAM, WIRE_GRAD_PASS)");
+  if (overlap)
+    return fail(DSSM_E_INVALID, "overlap: removed (the two-stream variant measured slower than the one-stream "
+                                "graph and its captured RCCL steps raced at world 1; DESIGN 6)");
   if (comm < 0 || comm > 2 || (comm == 2 && !(link_gbps > 0.f)))
     return fail(DSSM_E_INVALID, "comm: 0 RCCL, 1 device copies, 2 modelled (link_gbps > 0)");
   if (comm == 0 && (!g_comm || g_world != P->geo.ww || g_rank != P->dp_rank))

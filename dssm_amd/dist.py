@@ -278,7 +278,9 @@ class DataParallel:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
             self.tx = self._transport(comm, strict_mode)
         self.grad_wire = self.param_wire = self.stage = None
-        self.chunks, self.overlap = 1, bool(overlap)
+        if overlap:  # removed in round 3: slower, and its two-stream RCCL graph raced
+            raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
+        self.chunks, self.overlap = 1, False
         if self.mode == "zero" and self.wire == "bf16":
             # the W1 rows in `chunks` pieces (include/dssm.h dssm_plan_set_dp_wire): chunk p of each
             # collective is one contiguous block of world * sub elements

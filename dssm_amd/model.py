@@ -321,8 +321,8 @@ class DSSM:
                              latency_us: float = 0.0, overlap: bool = False, probes: bool = False,
                              stream=None) -> int:
         """len(batches) data-parallel steps on the bf16 wire (set_dp_wire) in ONE graph, collectives
-        included (dssm_plan_graph_build_dp_steps); overlap: the collectives on a second captured
-        stream beside the chunks' kernels.  comm 0: the library's RCCL communicator; 1 / 2: one-GPU
+        included (dssm_plan_graph_build_dp_steps); overlap must be False (the two-stream variant was
+        removed in round 3).  comm 0: the library's RCCL communicator; 1 / 2: one-GPU
         rehearsals (device copies / a modelled link time of latency_us + bytes / link_gbps)."""
         sp = stream_ptr(stream)
         if not sp:

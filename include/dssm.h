@@ -200,8 +200,8 @@ int dssm_plan_wire_shadows(dssm_plan* plan, void* stream);
  * (indptrs[i], ...), each step: forward, backward, the gradient pass (chunk by chunk), each chunk's
  * all-to-all, the fp32 tail all-reduce, Adam chunk by chunk, each chunk's all-gather, the shadow
  * rebuild per gathered chunk; step i+1's CSC rank pass rides in step i's Adam (with RANK_IN_ADAM).
- * overlap 0: every node on `stream` in that order; 1: the collectives on a second captured stream,
- * each chunk's collective as soon as its rows are written / updated (fork / join edges).
+ * overlap must be 0: every node on `stream` in that order (the two-stream variant, collectives on a
+ * second captured stream, measured slower and raced under RCCL at world 1; removed in round 3).
  * comm: 0 = the library's RCCL communicator (dssm_comm_init; world / rank must match the wire's);
  * 1 = rehearsal on one GPU, each collective replaced by a device copy of its bytes; 2 = rehearsal,
  * each collective replaced by a kernel that holds its stream for latency_us + (bytes this rank

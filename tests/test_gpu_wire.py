@@ -179,8 +179,8 @@ def _staged(seeds):
     return out
 
 
-@pytest.mark.parametrize("comm,overlap,chunks", [(0, False, 3), (0, True, 3), (1, True, 3), (0, False, 1)])
-def test_dp_step_graph_world1_matches_eager(comm, overlap, chunks, comm_world1):
+@pytest.mark.parametrize("comm,chunks", [(0, 3), (1, 3), (0, 1)])
+def test_dp_step_graph_world1_matches_eager(comm, chunks, comm_world1):
     """Three captured data-parallel steps (comm 0: RCCL at world 1; comm 1: device copies) against
     the same three steps run eagerly on the same wire (all-to-all = copy, all-gather = identity).
     With one chunk, steps 2 and 3 of the graph read W1 straight from the parameter wire (no shadow
@@ -195,7 +195,7 @@ def test_dp_step_graph_world1_matches_eager(comm, overlap, chunks, comm_world1):
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         m, gw, st, pw = runs[0]
-        gid = m.graph_build_dp_steps(batches, 1.0, comm=comm, overlap=overlap)
+        gid = m.graph_build_dp_steps(batches, 1.0, comm=comm)
         m.graph_launch(gid)
         e, egw, est, epw = runs[1]
         for ip, ix, vv in batches:
@@ -233,7 +233,9 @@ def test_dp_step_graph_modelled_links_runs():
     batches = _staged([400, 401])
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        gid = m.graph_build_dp_steps(batches, 1.0 / 8, comm=2, link_gbps=350.0, latency_us=10.0, overlap=True)
+        with pytest.raises(RuntimeError):  # the two-stream variant was removed
+            m.graph_build_dp_steps(batches, 1.0 / 8, comm=2, link_gbps=350.0, latency_us=10.0, overlap=True)
+        gid = m.graph_build_dp_steps(batches, 1.0 / 8, comm=2, link_gbps=350.0, latency_us=10.0)
         m.graph_launch(gid)
     torch.cuda.synchronize()
     nb1, nb2 = m.beta_powers()

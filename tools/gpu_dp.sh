@@ -17,7 +17,5 @@ done <<'LIST'
 --rehearse-world 8 --rehearse-comm model --link-gbps 1e9 --link-latency-us 0
 --rehearse-world 8 --rehearse-comm model
 --rehearse-world 8 --rehearse-comm copy
---rehearse-world 8 --dp-chunks 4 --dp-overlap 1 --rehearse-comm model
---rehearse-world 8 --dp-chunks 2 --dp-overlap 1 --rehearse-comm model
 --rehearse-world 2 --rehearse-comm model
 LIST
