@@ -169,8 +169,8 @@ int dssm_plan_get_option(const dssm_plan* plan, int option);
 int dssm_plan_set_adam_range(dssm_plan* plan, int64_t begin, int64_t end);
 /* Data-parallel bf16 wire (perf mode; replaces the fp32 gradient all-reduce of the reference's
  * single-process optimizer, new_dssm.py:215-217, when the batch is sharded over ranks).  W1's rows
- * -- arena elements [0, dssm_plan_wire_extent()) -- cross the links as bf16, in `chunks` pieces so
- * the collectives of one piece overlap the kernels of the next (dssm_plan_graph_build_dp_steps):
+ * -- arena elements [0, dssm_plan_wire_extent()) -- cross the links as bf16, in `chunks` pieces
+ * (dssm_plan_graph_build_dp_steps; with one piece the next step's SpMM reads the parameter wire):
  *   - rank j's optimizer shard is W1 rows [j*chunks*S, (j+1)*chunks*S) (S = ceil(D / (world *
  *     chunks)) rows per sub-chunk; dssm_plan_dp_geometry); the wires hold sub-chunk (p, j) -- rows
  *     (j*chunks + p)*S + [0, S) -- at element ((p*world + j)*S)*n, so chunk p of every collective

@@ -11,7 +11,7 @@ every collective is one contiguous block.  Checked here:
   updates as the unwired step does;
 * wire_shadows() rebuilds W1's bf16 shadow: a forward after it equals one after the fp32 refresh;
 * the data-parallel step graph (dssm_plan_graph_build_dp_steps: forward, backward, the chunked
-  gradient pass, the collectives on a second stream, chunked Adam, chunked shadow rebuild) at
+  gradient pass, the collectives, chunked Adam, chunked shadow rebuild, all on one stream) at
   world 1, with the library's RCCL communicator (comm 0) and the device-copy rehearsal (comm 1),
   against the same steps run eagerly; the modelled-link rehearsal (comm 2) runs.
 At world 1 the all-to-all and all-gather are identities; the exchange between ranks is covered by
