@@ -10,8 +10,12 @@ on the host and staged in HBM before the timed region; each step just points the
 next staged batch (no copy).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
-   N>1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+   N>1 as a plain process: bench.py starts its N ranks itself (a child torch.distributed.run on
+   127.0.0.1, before any GPU call); or under the launcher directly:
+         python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
            --master-port P bench.py --gpus N --steps K --warmup W
+   N>1 defaults to the library's RCCL transport, strict (no timed fallback), and ends with a
+   cross-rank digest of parameters / Adam state (dp_check in the line).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -42,9 +46,11 @@ def parse():
                          "graph-launch gap and the cycle's one separate rank launch: 183.9 -> 180.6 us/step vs 8)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "torch"],
-                    help="N>1 transport: rccl = libdssm.so's own RCCL communicator (default on GPUs), "
-                         "torch = torch.distributed collectives")
+    ap.add_argument("--comm", default=None, choices=["auto", "rccl", "torch"],
+                    help="N>1 transport: rccl = libdssm.so's own RCCL communicator (the default under the "
+                         "nccl backend, strict: a failure raises instead of timing a fallback), torch = "
+                         "torch.distributed collectives (the default under gloo), auto = rccl with a "
+                         "self-tested torch fallback")
     ap.add_argument("--dp-mode", default="auto", choices=["auto", "zero", "allreduce"],
                     help="N>1 exchange: zero = reduce-scatter + sharded Adam + all-gather "
                          "(default with torch.distributed), allreduce = all-reduce + replicated Adam")
@@ -96,7 +102,69 @@ def parse():
                     help="analysis only: seconds of host sleep between the graph builds and the warm-up")
     ap.add_argument("--busy-before-warmup", type=float, default=0.0,
                     help="analysis only: seconds of dense matmul load between the graph builds and the warm-up")
-    return ap.parse_args()
+    ap.add_argument("--dp-check", type=int, default=1,
+                    help="N>1: after the timed region, gather the sharded optimizer state and compare a "
+                         "digest of every rank's parameters / Adam m / v (reported as dp_check)")
+    args = ap.parse_args()
+    if args.comm is None:  # N>1 default: strict library RCCL on GPUs, so a fallback is never timed
+        args.comm = "rccl" if args.backend == "nccl" else "torch"
+    return args
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started as a plain process: launch the N ranks as a child
+    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1) with the same
+    arguments and return its exit code.  Runs before anything touches the GPU (no HIP call, no
+    torch.cuda query), so the parent never holds a device context; rank 0 prints the line."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the only kind the host driver has)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    child = subprocess.Popen(cmd, env=env)
+
+    def forward(sig, _frame):  # the driver's timeout reaches the ranks too
+        child.send_signal(sig)
+    for s in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s, forward)
+    return child.wait()
+
+
+def dp_check(model, dp, dev) -> dict:
+    """Cross-rank self-check after the timed region: every rank's fp32 parameters, Adam m and v
+    (sharded rows gathered first: gather_state) and TF beta powers are hashed; the data-parallel
+    step keeps them bit-identical by construction.  EMA shadows are rank-local."""
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    if hasattr(dp, "gather_state"):
+        dp.gather_state()
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+    n = int(getattr(model, "n_params", model.params.numel()))
+    h = hashlib.sha256()
+    finite = True
+    for t in (model.params[:n], model.adam_m[:n], model.adam_v[:n]):
+        a = t.detach().cpu().numpy()
+        finite = finite and bool(np.isfinite(a).all())
+        h.update(a.tobytes())
+    if hasattr(model, "beta_powers"):
+        h.update(np.asarray(model.beta_powers(), np.float32).tobytes())
+    mine = (h.hexdigest(), finite)
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, mine)
+    return {"world": len(got), "ranks_identical": all(g[0] == got[0][0] for g in got),
+            "finite": all(g[1] for g in got), "digest": got[0][0][:16],
+            "what": "sha256 of fp32 params, Adam m, v (+ beta powers) after gather_state, per rank"}
 
 
 def spmm_alg_bytes(nnz: int, rows: int, n1: int, s_w: int) -> int:
@@ -417,6 +485,7 @@ def bench_multiview(args):
     def step(i):
         if args.graph:
             fb_graphs[i % 3].replay()
+            m.view = feeds[i % 3][1]  # the replayed feed's active view: the ranges the exchange sums
         else:
             eager(i)
         if dp is not None:
@@ -473,6 +542,8 @@ def bench_multiview(args):
     t, src = model_profile("traffic", "multiview", "k_rnn_adam")
     if t is not None:
         out["roofline"].update(traffic=t["hbm_bytes"], traffic_source=src)
+    if dp is not None and args.dp_check:
+        out["dp_check"] = dp_check(m, dp, dev)
     if args.cpu_baseline and rank == 0 and world == 1:
         try:  # the NumPy float32 restatement (oracle/, test infrastructure) on the host
             from oracle import cpu_port
@@ -532,6 +603,10 @@ def fwd_only(model, staged, args, stream):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.model == "rnn":
+            raise SystemExit("--model rnn is a single-GPU row (BASELINE config 4)")
+        sys.exit(spawn_ranks(args))  # before any GPU call: the ranks are children
     if args.model == "rnn":
         return bench_rnn(args)
     if args.model == "multiview":
@@ -543,8 +618,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     local = local % max(1, torch.cuda.device_count()) if args.backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -779,6 +853,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss, acc = model.loss_accuracy()
+    check = dp_check(model, dp, dev) if (dp is not None and args.dp_check) else None
     fwd = fwd_only(model, staged, args, stream) if (args.fwd_only and world == 1 and rehearse == 1
                                                    and feeder is None) else None
 
@@ -888,6 +963,7 @@ def main():
                                       else "split graphs, host-issued collectives" if args.graph else "eager")
         if dp_capture_error:
             out["config"]["dp_capture_error"] = dp_capture_error
+        out["dp_check"] = check
     if (args.fp32_line and rank == 0 and world == 1 and rehearse == 1 and args.dtype == "bf16"
             and feeder is None and args.columns == "zipf"):
         out["fp32_mode"] = fp32_mode_line(args)

@@ -30,7 +30,7 @@ SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_A
 # dssm_plan_set_option ids (include/dssm.h DSSM_OPT_*)
 OPTIONS = {k: i for i, k in enumerate(["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "SCATTER_IN_COS",
                                          "DW_IN_APPLY", "WIRE_GRAD_PASS", "CSC_RANK", "DETERMINISTIC",
-                                         "FUSED_W1_ADAM", "RANK_IN_ADAM"])}
+                                         "FUSED_W1_ADAM", "RANK_IN_ADAM", "MEMCPY_NODES"])}
 
 
 class DssmError(RuntimeError):
@@ -84,6 +84,7 @@ _SIGS = {
     "dssm_plan_set_adam_range": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "dssm_plan_finalize_loss": (C.c_int, [_P, _P]),
     "dssm_plan_graph_probe_read": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    "dssm_plan_graph_topology": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int64)]),
     "dssm_plan_set_fused_w1_adam": (C.c_int, [_P, C.c_int]),
     "dssm_plan_wire_extent": (C.c_int64, [_P]),
     "dssm_plan_dp_wire_size": (C.c_int64, [_P, C.c_int, C.c_int]),

@@ -193,3 +193,24 @@ __device__ __forceinline__ void loss_reduce(const float* __restrict__ part, int 
     }
   }
 }
+
+// ---- zero fill as a kernel node -------------------------------------------------------------------
+// Every device-side clear that can enter a captured graph is a kernel (not a hipMemsetAsync node), so
+// a captured stream is a chain of kernel nodes whose ordering is the stream's.  A
+// template so each translation unit may instantiate it (COMDAT).  4-B words; a byte tail if any.
+template <int kUnused = 0>
+__global__ __launch_bounds__(256) void k_zero_bytes(unsigned char* __restrict__ p, size_t bytes) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool aligned = ((uintptr_t)p % 4) == 0;
+  const size_t words = aligned ? bytes / 4 : 0;
+  for (size_t i = t; i < words; i += stride) reinterpret_cast<unsigned*>(p)[i] = 0u;
+  for (size_t i = words * 4 + t; i < bytes; i += stride) p[i] = 0;
+}
+inline hipError_t zero_bytes_async(void* p, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  const size_t items = (bytes + 3) / 4;
+  const unsigned grid = (unsigned)(items / 256 + 1 < 2048 ? items / 256 + 1 : 2048);
+  hipLaunchKernelGGL(k_zero_bytes<0>, dim3(grid), dim3(256), 0, s, static_cast<unsigned char*>(p), bytes);
+  return hipGetLastError();
+}

@@ -24,6 +24,23 @@ template <> struct RawRow8<u16> {
     acc[7] = __fmaf_rn(v, __uint_as_float(a.w & 0xffff0000u), acc[7]);
   }
 };
+// bf16 rows at a stride that is NOT a multiple of 8 elements (the data-parallel parameter wire:
+// W1 row-major at stride n = 300, read directly by the forward SpMM).  Such rows have no zero pads,
+// so a half group (nvalid == 4: the row's last 4 columns) loads the 16 B that END at the row's end
+// and keeps their upper half: no load reaches into the next row or past the buffer, and the lane's
+// upper 4 columns accumulate zeros.  Needs n >= 8 (launch_spmm_* check).  Loads are 8-B aligned.
+struct u16t {
+  u16 bits;
+};
+template <> struct RawRow8<u16t> {
+  RawRow8<u16> r;
+  __device__ __forceinline__ void load(const u16t* p, int nvalid) {
+    const int back = nvalid >= 8 ? 0 : 4;
+    const uint4 x = *reinterpret_cast<const uint4*>(p - back);
+    r.a = back ? make_uint4(x.z, x.w, 0u, 0u) : x;
+  }
+  __device__ __forceinline__ void fma(float v, float (&acc)[8]) const { r.fma(v, acc); }
+};
 template <> struct RawRow8<float> {
   float4 a, b;
   __device__ __forceinline__ void load(const float* p, int nvalid) {

@@ -186,8 +186,8 @@ int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, 
   if (!src || !map || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols || dst_rows < 0)
     return oerr(DSSM_E_INVALID, "rows_scatter_add: bad argument");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(dst, 0, sizeof(float) * (size_t)dst_rows * ldd, s) != hipSuccess)
-    return oerr(DSSM_E_HIP, "rows_scatter_add: hipMemsetAsync");
+  if (zero_bytes_async(dst, sizeof(float) * (size_t)dst_rows * ldd, s) != hipSuccess)
+    return oerr(DSSM_E_HIP, "rows_scatter_add: zero fill");
   hipLaunchKernelGGL(k_rows_scatter_add, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, s, src, lds, map, n,
                      cols, dst, ldd);
   return hip_status();

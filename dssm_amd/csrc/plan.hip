@@ -219,10 +219,8 @@ struct dssm_plan {
   dssm::WireGeo geo{};
   int dp_rank = 0;
   bool dp_defer_gradpass = false;  // the data-parallel graph builder launches the chunks itself
-  // the data-parallel graph builder's hook around each Adam chunk launch (stream waits / event
-  // records while capturing): (chunk, after)
-  std::function<int(int, bool)> dp_hook;
-  hipStream_t comm_stream = nullptr;  // the data-parallel graphs' collective stream
+  // the data-parallel graph builder's hook after each Adam chunk launch (that chunk's all-gather)
+  std::function<int(int)> dp_hook;
   int64_t wire_end() const { return Lt.fc_off[0] + (int64_t)Lt.in_dim[0] * Lt.n[0]; }
   int64_t sub_elems() const { return (int64_t)geo.ws * geo.n; }
   // rows [r0, r1) of this rank's sub-chunk p (r1 <= r0: none past W1's rows)
@@ -254,6 +252,7 @@ struct dssm_plan {
       0,  // DETERMINISTIC: fixed-order reductions, bit-identical repeated runs
       1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
       1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
+      0,  // MEMCPY_NODES: diagnostics: data-parallel device copies as hipMemcpyAsync nodes
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -262,7 +261,7 @@ struct dssm_plan {
     hipEvent_t ev[DSSM_PROBE_COUNT][2] = {};
     bool probes = false;
     unsigned probe_mask = ~0u;  // while capturing: which probe ids record event nodes
-    std::vector<hipEvent_t> xev;  // fork / join events of a multi-stream capture
+    int64_t topo[8] = {};  // the captured graph's shape (graph_topology)
   };
   std::vector<GraphSlot*> graphs;
   GraphSlot* capturing = nullptr;
@@ -510,10 +509,8 @@ int dssm_plan_destroy(dssm_plan* plan) {
       for (auto& pr : g->ev)
         for (hipEvent_t e : pr)
           if (e) hipEventDestroy(e);
-      for (hipEvent_t e : g->xev) hipEventDestroy(e);
       delete g;
     }
-    if (plan->comm_stream) hipStreamDestroy(plan->comm_stream);
   }
   delete plan;
   return DSSM_OK;
@@ -811,7 +808,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
     // backward() twice without an Adam step in between: re-zero the atomic-target blocks (only
     // the fused path leaves dW1's heavy rows to be cleared by Adam; otherwise dw1-light
     // overwrites every row before the heavy atomics).
-    HIP_TRY(hipMemsetAsync(P->g, 0, sizeof(float) * (size_t)Lt.total, s));
+    HIP_TRY(zero_bytes_async(P->g, sizeof(float) * (size_t)Lt.total, s));
   }
   P->grads_clean = false;
   if (P->fwd_fused) {
@@ -1071,11 +1068,9 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   P->probe_begin(DSSM_PROBE_ADAM, s);
   if (P->pwire) {
     for (int c = 0; c < P->geo.wp; ++c) {
-      if (P->dp_hook)
-        if (int rc = P->dp_hook(c, false)) return rc;
       if (int rc = dp_adam_chunk(P, a, c, s)) return rc;
       if (P->dp_hook)
-        if (int rc = P->dp_hook(c, true)) return rc;
+        if (int rc = P->dp_hook(c)) return rc;
     }
   } else {
     HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
@@ -1229,6 +1224,56 @@ int dssm_plan_get_adam_state(dssm_plan* P, float* beta1_power, float* beta2_powe
   return DSSM_OK;
 }
 
+// The captured graph's shape, kept per graph for dssm_plan_graph_topology: {nodes, edges, roots,
+// kernel nodes, memcpy nodes, memset nodes, other nodes, chain}.  chain = 1 when the graph is ONE
+// path through every node (nodes == edges + 1, in- and out-degree <= 1, one root): then every node,
+// whatever its type, runs after every node captured before it on the stream.
+static void graph_topology(hipGraph_t graph, int64_t* out) {
+  for (int i = 0; i < 8; ++i) out[i] = -1;
+  size_t nn = 0, ne = 0;
+  if (hipGraphGetNodes(graph, nullptr, &nn) != hipSuccess || hipGraphGetEdges(graph, nullptr, nullptr, &ne) != hipSuccess)
+    return;
+  std::vector<hipGraphNode_t> nodes(nn), from(ne), to(ne);
+  if ((nn && hipGraphGetNodes(graph, nodes.data(), &nn) != hipSuccess) ||
+      (ne && hipGraphGetEdges(graph, from.data(), to.data(), &ne) != hipSuccess))
+    return;
+  int64_t kern = 0, cpy = 0, set = 0, other = 0;
+  for (hipGraphNode_t n : nodes) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(n, &t) != hipSuccess) return;
+    if (t == hipGraphNodeTypeKernel) ++kern;
+    else if (t == hipGraphNodeTypeMemcpy) ++cpy;
+    else if (t == hipGraphNodeTypeMemset) ++set;
+    else ++other;
+  }
+  std::vector<int> indeg(nn, 0), outdeg(nn, 0);
+  auto idx = [&](hipGraphNode_t n) {
+    return (int)(std::find(nodes.begin(), nodes.end(), n) - nodes.begin());
+  };
+  for (size_t i = 0; i < ne; ++i) {
+    const int a = idx(from[i]), b = idx(to[i]);
+    if (a >= (int)nn || b >= (int)nn) return;
+    ++outdeg[a];
+    ++indeg[b];
+  }
+  int64_t roots = 0;
+  bool chain = nn == ne + 1;
+  for (size_t i = 0; i < nn; ++i) {
+    roots += indeg[i] == 0;
+    chain = chain && indeg[i] <= 1 && outdeg[i] <= 1;
+  }
+  chain = chain && roots == 1;
+  const int64_t v[8] = {(int64_t)nn, (int64_t)ne, roots, kern, cpy, set, other, chain ? 1 : 0};
+  for (int i = 0; i < 8; ++i) out[i] = v[i];
+}
+
+int dssm_plan_graph_topology(const dssm_plan* P, int graph_id, int64_t* out) {
+  if (!P || !out || graph_id < 0 || graph_id >= (int)P->graphs.size())
+    return fail(DSSM_E_INVALID, "dssm_plan_graph_topology: bad plan / graph id / output");
+  for (int i = 0; i < 8; ++i) out[i] = P->graphs[graph_id]->topo[i];
+  return DSSM_OK;
+}
+
 int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_probes, void* stream,
                           int* graph_id) {
   if (!P || !graph_id) return fail(DSSM_E_INVALID, "null argument");
@@ -1288,6 +1333,7 @@ int dssm_plan_graph_build(dssm_plan* P, int parts, float grad_scale, int with_pr
     delete g;
     return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
   }
+  graph_topology(graph, g->topo);
   e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
   hipGraphDestroy(graph);
   if (e != hipSuccess) {
@@ -1373,6 +1419,7 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     delete g;
     return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
   }
+  graph_topology(graph, g->topo);
   e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
   hipGraphDestroy(graph);
   if (e != hipSuccess) {
@@ -1577,12 +1624,19 @@ int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void
 // all-to-all as the rank's own chunk by a device copy plus one grouped send / recv per peer (all
 // xGMI links busy at once on a fully connected node: one step, not world - 1 ring steps).  (RCCL's
 // ncclAllToAll crashed in hipGraph capture at world 1 on this image; the grouped form captures.)
+// A device copy on the stream: a copy kernel, or (plan option MEMCPY_NODES, diagnostics: the round-3
+// form) a hipMemcpyAsync, which a capture records as a memcpy node.
+static hipError_t device_copy(void* dst, const void* src, size_t bytes, hipStream_t s, bool memcpy_node) {
+  if (memcpy_node) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+  return dssm::launch_copy_bytes(dst, src, bytes, s);
+}
+
 static int all_to_all_impl(const void* send, void* recv, int64_t count, ncclDataType_t t, size_t es,
-                           hipStream_t s) {
+                           hipStream_t s, bool memcpy_node = false) {
   const char* sp = static_cast<const char*>(send);
   char* rp = static_cast<char*>(recv);
   const size_t chunk = (size_t)count * es;
-  HIP_TRY(dssm::launch_copy_bytes(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk, s));
+  HIP_TRY(device_copy(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk, s, memcpy_node));
   if (g_world == 1) return DSSM_OK;
   RCCL_TRY(ncclGroupStart());
   for (int j = 0; j < g_world; ++j) {
@@ -1608,7 +1662,7 @@ int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void
 }
 
 // ---- the data-parallel step graph (include/dssm.h dssm_plan_graph_build_dp_steps) -----------
-// One collective of the exchange on the comm stream cs: the library's RCCL communicator (comm 0),
+// One collective of the exchange on the step's stream cs: the library's RCCL communicator (comm 0),
 // a device copy of the same bytes (comm 1) or a kernel holding cs for the modelled link time (2).
 struct DpComm {
   int mode;
@@ -1629,12 +1683,13 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   uint16_t* gw = P->gwire + chunk * blk;
   uint16_t* st = const_cast<uint16_t*>(P->gstage) + chunk * blk;
   uint16_t* pw = P->pwire + chunk * blk;
+  const bool mc = P->on(DSSM_OPT_MEMCPY_NODES);
   if (k.mode == 1) {  // same bytes through HBM (the tail's copy is skipped: 0.5 MB)
-    if (kind == 0) HIP_TRY(dssm::launch_copy_bytes(st, gw, blk * 2, cs));
-    if (kind == 1) HIP_TRY(dssm::launch_copy_bytes(st, pw, blk * 2, cs));
+    if (kind == 0) HIP_TRY(device_copy(st, gw, blk * 2, cs, mc));
+    if (kind == 1) HIP_TRY(device_copy(st, pw, blk * 2, cs, mc));
     return DSSM_OK;
   }
-  if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs);
+  if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs, mc);
   if (kind == 1) RCCL_TRY(ncclAllGather(pw + (int64_t)P->dp_rank * sub, pw, (size_t)sub, ncclBfloat16, g_comm, cs));
   if (kind == 2) RCCL_TRY(ncclAllReduce(tg, tg, tail, ncclFloat32, ncclSum, g_comm, cs));
   return DSSM_OK;
@@ -1664,25 +1719,10 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     if (!indptrs[i] || (P->Lt.max_nnz && (!indices[i] || !values[i])))
       return fail(DSSM_E_INVALID, "null batch pointer");
   hipStream_t s = (hipStream_t)stream;
-  // overlap: the collectives on a second captured stream (fork / join edges between the two);
-  // otherwise every node on the capture stream, in dependency order
-  if (overlap && !P->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&P->comm_stream, hipStreamNonBlocking));
-  hipStream_t cs = overlap ? P->comm_stream : s;
   const DpComm k{comm, (double)link_gbps, 1e3 * (double)latency_us};
   const int C = P->geo.wp;
   auto* g = new dssm_plan::GraphSlot();
   g->probes = with_probes != 0;
-  // events: per step and chunk gradient-pass / all-to-all / Adam / all-gather, + the tail's
-  const int per_step = 4 * C + 1;
-  g->xev.resize((size_t)per_step * nsteps, nullptr);
-  for (auto& e : g->xev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      e = nullptr;
-      for (hipEvent_t x : g->xev)
-        if (x) hipEventDestroy(x);
-      delete g;
-      return fail(DSSM_E_HIP, "hipEventCreate failed");
-    }
   if (g->probes)
     for (auto& pr : g->ev)
       for (hipEvent_t& e : pr) (void)hipEventCreate(&e);
@@ -1693,7 +1733,6 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   P->grads_clean = true;
   hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {
-    for (hipEvent_t x : g->xev) hipEventDestroy(x);
     delete g;
     return fail(DSSM_E_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
   }
@@ -1701,18 +1740,8 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   P->dp_defer_gradpass = true;
   P->rank_done_for = nullptr;
   int rc = DSSM_OK;
-  auto rec = [&](hipEvent_t e, hipStream_t st) { return cs == s ? hipSuccess : hipEventRecord(e, st); };
-  auto wait = [&](hipStream_t st, hipEvent_t e) { return cs == s ? hipSuccess : hipStreamWaitEvent(st, e, 0); };
-#define DP_TRY(expr)                                                                              \
-  do {                                                                                            \
-    if (!rc) {                                                                                    \
-      hipError_t e_ = (expr);                                                                     \
-      if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    }                                                                                             \
-  } while (0)
+  // every node on the one captured stream, in dependency order (graph_topology checks the chain)
   for (int i = 0; i < nsteps && !rc; ++i) {
-    hipEvent_t* ev = g->xev.data() + (size_t)i * per_step;
-    hipEvent_t *e_gp = ev, *e_a2a = ev + C, *e_adam = ev + 2 * C, *e_ag = ev + 3 * C, e_tail = ev[4 * C];
     g->probes = with_probes != 0 && i == nsteps - 1;
     g->probe_mask = 1u << DSSM_PROBE_ADAM;
     P->indptr = indptrs[i];
@@ -1720,49 +1749,32 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     P->values = values[i];
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
-    // gradient pass chunk by chunk; each chunk's all-to-all on the comm stream as soon as it lands
+    // the gradient pass chunk by chunk, each chunk's all-to-all behind it
     for (int c = 0; c < C && !rc; ++c) {
-      if (!rc) rc = launch_wire_gradient_pass(P, s, C > 1 ? c : -1);
-      DP_TRY(rec(e_gp[c], s));
-      DP_TRY(wait(cs, e_gp[c]));
-      if (!rc) rc = dp_collective(P, k, 0, c, cs);
-      DP_TRY(rec(e_a2a[c], cs));
+      rc = launch_wire_gradient_pass(P, s, C > 1 ? c : -1);
+      if (!rc) rc = dp_collective(P, k, 0, c, s);
     }
-    if (!rc) rc = dp_collective(P, k, 2, 0, cs);  // the fp32 tail (b1's row: the last chunk's pass)
-    DP_TRY(rec(e_tail, cs));
-    // Adam chunk c once its all-to-all is in; each chunk's all-gather as soon as its Adam is done
+    if (!rc) rc = dp_collective(P, k, 2, 0, s);  // the fp32 tail (b1's row: the last chunk's pass)
+    // Adam chunk by chunk, each chunk's all-gather behind its Adam
     if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {
       P->host_rank_indptr = indptrs[i + 1];
       P->host_rank_indices = indices[i + 1];
     }
-    P->dp_hook = [&](int c, bool after) -> int {
-      if (!after) {
-        if (wait(s, e_a2a[c]) != hipSuccess) return fail(DSSM_E_HIP, "hipStreamWaitEvent");
-        if (c == C - 1 && wait(s, e_tail) != hipSuccess) return fail(DSSM_E_HIP, "hipStreamWaitEvent");
-        return DSSM_OK;
-      }
-      if (rec(e_adam[c], s) != hipSuccess || wait(cs, e_adam[c]) != hipSuccess)
-        return fail(DSSM_E_HIP, "hipEventRecord / hipStreamWaitEvent");
-      if (int r = dp_collective(P, k, 1, c, cs)) return r;
-      if (rec(e_ag[c], cs) != hipSuccess) return fail(DSSM_E_HIP, "hipEventRecord");
-      return DSSM_OK;
-    };
+    P->dp_hook = [&](int c) -> int { return dp_collective(P, k, 1, c, s); };
     if (!rc) rc = dssm_plan_adam(P, grad_scale, stream);
     P->dp_hook = nullptr;
-    // W1's shadow rebuilt chunk by chunk as the all-gathers land (the next forward's operand).  With
+    // W1's shadow rebuilt chunk by chunk from the all-gathered wire (the next forward's operand).  With
     // one chunk the wire already holds W1 row-major: the region's next step reads it directly
-    // (w1_wire) and only the last step rebuilds the shadow, which the next region's first step and
-    // the eval forward read.
+    // (w1_wire, tight rows of stride n: RawRow8<u16t>) and only the last step rebuilds the shadow,
+    // which the next region's first step and the eval forward read.
     const bool direct = C == 1 && P->geo.n == P->Lt.n[0] && i + 1 < nsteps;
-    for (int c = 0; c < C && !rc; ++c) {
-      DP_TRY(wait(s, e_ag[c]));
-      if (!direct)
-        DP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s));
+    for (int c = 0; c < C && !rc && !direct; ++c) {
+      hipError_t e_ = dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s);
+      if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string("launch_wire_shadow: ") + hipGetErrorString(e_));
     }
     P->w1_wire = direct ? P->pwire : nullptr;
   }
   P->w1_wire = nullptr;
-#undef DP_TRY
   P->dp_hook = nullptr;
   P->dp_defer_gradpass = false;
   P->host_rank_indptr = P->host_rank_indices = nullptr;
@@ -1780,14 +1792,13 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   P->fwd_train_done = was_fwd;
   if (rc || e != hipSuccess || !graph) {
     if (graph) hipGraphDestroy(graph);
-    for (hipEvent_t x : g->xev) hipEventDestroy(x);
     delete g;
     return fail(rc ? rc : DSSM_E_HIP, rc ? err : std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
   }
+  graph_topology(graph, g->topo);
   e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
   hipGraphDestroy(graph);
   if (e != hipSuccess) {
-    for (hipEvent_t x : g->xev) hipEventDestroy(x);
     delete g;
     return fail(DSSM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
   }

@@ -427,8 +427,8 @@ int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int
       demb_elems < 0)
     return rerr(DSSM_E_INVALID, "rnn_backward: bad argument");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(demb, 0, sizeof(float) * (size_t)demb_elems, s) != hipSuccess)
-    return rerr(DSSM_E_HIP, "rnn_backward: hipMemsetAsync");
+  if (zero_bytes_async(demb, sizeof(float) * (size_t)demb_elems, s) != hipSuccess)
+    return rerr(DSSM_E_HIP, "rnn_backward: zero fill");
   const int K = E + H;
   const size_t plane = (size_t)2 * T * R;
   float* Z = ws;

@@ -900,8 +900,8 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   hipStream_t s = (hipStream_t)stream;
   const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
   // the batch's positions bucketed by token (for the embedding gradient after the BPTT)
-  if (hipMemsetAsync(L.cnt, 0, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
-    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: hipMemsetAsync");
+  if (zero_bytes_async(L.cnt, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
+    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: zero fill");
   const int gpos = std::max(1, std::min((R * T + 255) / 256, 2048));
   hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt);
   hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start,

@@ -989,6 +989,13 @@ int eval_coef_blocks(const EvalCoef& e) {
   return cdiv(items, 256);
 }
 
+// bf16 weight rows: padded to a multiple of 8 elements with zero pads (the shadows), or tight at
+// stride n (the parameter wire), which the u16t instances read without crossing a row's end
+static bool bf16_rows_ok(int ldw, int n) {
+  if (ldw % 8 == 0) return ldw >= n;
+  return ldw == n && n % 4 == 0 && n >= 8;
+}
+
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
                            int ldz, hipStream_t s, const EvalCoef* ec, bool relu) {
@@ -996,7 +1003,11 @@ hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* v
   const int ne = ec ? eval_coef_blocks(*ec) : 0;
   if (ec) e = *ec;
   dim3 grid(ne + cdiv(rows, 4)), block(256);
-  if (w_bf16)
+  if (w_bf16 && !bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
+  if (w_bf16 && ldw % 8)  // the parameter wire's tight rows
+    hipLaunchKernelGGL(k_spmm_fwd<u16t>, grid, block, 0, s, indptr, indices, values, rows,
+                       (const u16t*)W, ldw, n, bias, Z, ldz, e, ne, relu ? 1 : 0);
+  else if (w_bf16)
     hipLaunchKernelGGL(k_spmm_fwd<u16>, grid, block, 0, s, indptr, indices, values, rows,
                        (const u16*)W, ldw, n, bias, Z, ldz, e, ne, relu ? 1 : 0);
   else
@@ -1017,9 +1028,15 @@ hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* 
   int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
   int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const int nscan = cdiv(D + 1, kScanSmallNT * 4);
-  hipLaunchKernelGGL(k_spmm_scan<u16>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
-                     values, rows, (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
-                     heavy_items, nscan);
+  if (!bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
+  if (ldw % 8)  // the parameter wire's tight rows (RawRow8<u16t>)
+    hipLaunchKernelGGL(k_spmm_scan<u16t>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
+                       values, rows, (const u16t*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
+                       heavy_items, nscan);
+  else
+    hipLaunchKernelGGL(k_spmm_scan<u16>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
+                       values, rows, (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
+                       heavy_items, nscan);
   return hipGetLastError();
 }
 
@@ -1117,7 +1134,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                        out_val, csc_col);
   } else {
     if (nzero) {
-      const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(double), s);
+      const hipError_t e = zero_bytes_async(zero, (size_t)nzero * sizeof(double), s);
       if (e != hipSuccess) return e;
     }
     const int cblocks = max(1, min(cdiv(max_nnz, 256), 2048));

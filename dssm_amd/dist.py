@@ -255,6 +255,8 @@ class DataParallel:
         self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
         zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
         fallback taken is listed in .fallbacks and warned about."""
+        if overlap:  # removed in round 3 (DESIGN §6): slower; refused before any side effect
+            raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
@@ -278,8 +280,6 @@ class DataParallel:
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
             self.tx = self._transport(comm, strict_mode)
         self.grad_wire = self.param_wire = self.stage = None
-        if overlap:  # removed in round 3: slower, and its two-stream RCCL graph raced
-            raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
         self.chunks, self.overlap = 1, False
         if self.mode == "zero" and self.wire == "bf16":
             # the W1 rows in `chunks` pieces (include/dssm.h dssm_plan_set_dp_wire): chunk p of each
@@ -392,10 +392,12 @@ class DataParallel:
         return getattr(self.tx, "capturable", False) and self.mode == "zero" and self.wire == "bf16"
 
     def build_region(self, batches, probes: bool = False) -> int:
-        """len(batches) whole data-parallel steps as ONE graph: per step the forward, backward, the
-        gradient pass chunk by chunk with each chunk's all-to-all on a second stream as it lands,
-        Adam chunk by chunk, each chunk's all-gather behind its Adam, the shadow rebuild per
-        gathered chunk; step i+1's CSC rank pass inside step i's Adam.  Replay: model.graph_launch."""
+        """len(batches) whole data-parallel steps as ONE graph, every node on one captured stream:
+        per step the forward, backward, the gradient pass chunk by chunk with each chunk's
+        all-to-all behind it, the fp32 tail all-reduce, Adam chunk by chunk with each chunk's
+        all-gather behind it, the shadow rebuild (with one chunk only after the region's last step:
+        the next step's SpMM reads the parameter wire); step i+1's CSC rank pass inside step i's
+        Adam.  Replay: model.graph_launch."""
         if not self.capturable:
             raise RuntimeError(f"the {self.schedule} exchange cannot be captured (needs zero/bf16 via rccl)")
         return self.model.graph_build_dp_steps(batches, 1.0 / self.world, comm=0, overlap=self.overlap,

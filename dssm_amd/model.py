@@ -349,6 +349,14 @@ class DSSM:
               "graph_probe_read")
         return float(ms.value)
 
+    def graph_topology(self, gid: int) -> Dict[str, int]:
+        """The captured graph's shape (dssm_plan_graph_topology): node / edge / root counts, nodes
+        by type, and chain = 1 when every node is ordered after every node captured before it."""
+        out = (C.c_int64 * 8)()
+        check(self.lib.dssm_plan_graph_topology(self._plan, int(gid), out), "graph_topology")
+        keys = ("nodes", "edges", "roots", "kernel", "memcpy", "memset", "other", "chain")
+        return {k: int(v) for k, v in zip(keys, out)}
+
     def set_option(self, name: str, value: bool):
         """Choose a schedule alternative (dssm_plan_set_option; OPTIONS in _lib): applies to the
         steps enqueued and graphs captured afterwards.  The plan never reads the environment."""

@@ -144,7 +144,10 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *   FUSED_W1_ADAM   see dssm_plan_set_fused_w1_adam
  *   RANK_IN_ADAM    1: in multi-step graphs (dssm_plan_graph_build_steps) step i's Adam launch also
  *                      runs step i+1's CSC rank pass (with MERGED_CSC and FUSED_W1_ADAM), so that
- *                      step's forward skips the rank launch */
+ *                      step's forward skips the rank launch
+ *   MEMCPY_NODES    0; 1 (diagnostics): the data-parallel graph's device copies (the all-to-all's own
+ *                      chunk, the copy rehearsal) as hipMemcpyAsync -- memcpy nodes in a capture --
+ *                      instead of the copy kernel */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -156,6 +159,7 @@ enum {
   DSSM_OPT_DETERMINISTIC,
   DSSM_OPT_FUSED_W1_ADAM,
   DSSM_OPT_RANK_IN_ADAM,
+  DSSM_OPT_MEMCPY_NODES,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);
@@ -263,6 +267,12 @@ int dssm_plan_schedule(const dssm_plan* plan);
  * dssm_plan_backward (no-op otherwise). */
 int dssm_plan_finalize_loss(dssm_plan* plan, void* stream);
 int dssm_plan_graph_probe_read(dssm_plan* plan, int graph_id, int probe_id, float* ms);
+/* The shape of a captured graph as it was before instantiation (hipGraphGetNodes / GetEdges /
+ * NodeGetType): out[8] = {nodes, edges, roots, kernel nodes, memcpy nodes, memset nodes, other
+ * nodes, chain}.  chain = 1 when the graph is one path through every node, i.e. each node runs
+ * after every node captured before it on the stream, whatever its type.  -1 entries: the runtime
+ * could not report. */
+int dssm_plan_graph_topology(const dssm_plan* plan, int graph_id, int64_t* out);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
 /* FC1 (new_dssm.py:124-126): Z[r, :] = sum_k values[k] * W[indices[k], :] + bias.

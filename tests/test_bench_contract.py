@@ -51,3 +51,70 @@ def test_committed_lines_keep_the_contract(name):
     assert abs(r["achieved"] / r["peak"] - r["frac"]) < 1e-3
     assert abs(r["bytes_per_launch"] / (r["avg_ms"] * 1e-3) / 1e9 - r["achieved"]) <= 1e-3 * r["achieved"] + 0.1
     assert "workload" in d["config"]
+
+
+def test_gpus_n_spawns_its_own_ranks(monkeypatch):
+    """`bench.py --gpus N` started as a plain process (the driver's verb) launches its N ranks as a
+    child torch.distributed.run on 127.0.0.1 with the same arguments, before any GPU call."""
+    import subprocess
+    import sys
+    seen = {}
+
+    class FakeChild:
+        def __init__(self, cmd, env=None):
+            seen["cmd"], seen["env"] = cmd, env
+
+        def wait(self):
+            return 7
+
+        def send_signal(self, sig):
+            pass
+    monkeypatch.setattr(subprocess, "Popen", FakeChild)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
+    args = bench.parse()
+    assert args.comm == "rccl"  # strict library RCCL by default: a fallback is never timed
+    assert bench.spawn_ranks(args) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert cmd[-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--backend", "gloo"])
+    assert bench.parse().comm == "torch"
+
+
+def _dp_check_rank(rank, world, port, perturb, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class M:
+        n_params = 1000
+        params = torch.arange(1024, dtype=torch.float32)
+        adam_m = torch.ones(1024)
+        adam_v = torch.full((1024,), 0.5)
+    m = M()
+    if perturb and rank == 1:
+        m.adam_v = m.adam_v.clone()
+        m.adam_v[999] = float.fromhex("0x1.0000020000000p-1")  # one ulp
+    out = bench.dp_check(m, object(), torch.device("cpu"))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_dp_check_compares_every_rank(perturb):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_dp_check_rank, args=(r, 2, port, perturb, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert outs[0] == outs[1] and outs[0]["world"] == 2 and outs[0]["finite"]
+    assert outs[0]["ranks_identical"] is (not perturb)

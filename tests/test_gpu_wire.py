@@ -13,7 +13,8 @@ every collective is one contiguous block.  Checked here:
 * the data-parallel step graph (dssm_plan_graph_build_dp_steps: forward, backward, the chunked
   gradient pass, the collectives, chunked Adam, chunked shadow rebuild, all on one stream) at
   world 1, with the library's RCCL communicator (comm 0) and the device-copy rehearsal (comm 1),
-  against the same steps run eagerly; the modelled-link rehearsal (comm 2) runs.
+  against the same steps run eagerly, bit for bit under DETERMINISTIC, and its captured graph a
+  single chain of nodes; the modelled-link rehearsal (comm 2) runs.
 At world 1 the all-to-all and all-gather are identities; the exchange between ranks is covered by
 tests/test_gpu_dp_bow.py (world 2 over gloo) and tests/test_dist_gloo.py (CPU)."""
 import ctypes as C
@@ -179,39 +180,72 @@ def _staged(seeds):
     return out
 
 
-@pytest.mark.parametrize("comm,chunks", [(0, 3), (1, 3), (0, 1)])
-def test_dp_step_graph_world1_matches_eager(comm, chunks, comm_world1):
-    """Three captured data-parallel steps (comm 0: RCCL at world 1; comm 1: device copies) against
-    the same three steps run eagerly on the same wire (all-to-all = copy, all-gather = identity).
-    With one chunk, steps 2 and 3 of the graph read W1 straight from the parameter wire (no shadow
-    rebuild between the steps)."""
-    steps = 3
+def _first_mismatch(name, got, want, geo, ext):
+    """Where two arenas differ: the W1 wire chunk / the tail, for the assertion message."""
+    d = (got != want).nonzero().flatten()
+    if d.numel() == 0:
+        return ""
+    i = int(d[0])
+    n = geo["sub"] // geo["rows"]
+    where = f"W1 row {i // n} (chunk {(i // n // geo['rows']) % geo['chunks']})" if i < ext else f"tail +{i - ext}"
+    return f"{name}: {d.numel()} of {got.numel()} differ, first at {i} = {where}"
+
+
+@pytest.mark.parametrize("comm,chunks,bs,memcpy", [(0, 3, 96, 0), (1, 3, 96, 0), (0, 1, 96, 0),
+                                                   (0, 1, 128, 0), (0, 3, 96, 1)])
+def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, comm_world1):
+    """The captured data-parallel step graph (comm 0: RCCL at world 1; comm 1: device copies)
+    against the same steps run eagerly on the same wire (all-to-all = copy, all-gather = identity),
+    under DETERMINISTIC (every reduction in a fixed order): params, Adam m / v, beta powers and the
+    wire must be BIT-identical after two replays of a 3-step graph (6 steps).  With one chunk,
+    steps 2 and 3 of the graph read W1 straight from the parameter wire (tight rows of stride 300;
+    bs 128 runs the merged-transpose SpMM launch, bs 96 the plain one), and Z1's pad columns must
+    stay zero.  The captured graph must be one chain of nodes (dssm_plan_graph_topology), with no
+    memcpy / memset nodes -- except in the MEMCPY_NODES diagnostics variant (the round-3 form of
+    the own-chunk copy), which must be ordered the same way."""
+    from dssm_amd import _lib
+    steps, replays = 3, 2
     runs = []
     for mode in ("graph", "eager"):
-        _, _, m = make(D, WIDTHS, BS, NEG, "bf16", fused=False)
+        _, _, m = make(D, WIDTHS, bs, NEG, "bf16", fused=False)
+        m.set_option("DETERMINISTIC", True)
+        m.set_option("MEMCPY_NODES", bool(memcpy))
         gw, st, pw, geo = _wires(m, 1, 0, chunks)
         runs.append((m, gw, st, pw))
-    batches = _staged([300 + i for i in range(steps)])
+    batches = []
+    for i in range(steps):
+        b = synth_batch(D, bs, NEG, seed=300 + i, mean_nnz=32)
+        batches.append(tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)))
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         m, gw, st, pw = runs[0]
         gid = m.graph_build_dp_steps(batches, 1.0, comm=comm)
-        m.graph_launch(gid)
+        for _ in range(replays):
+            m.graph_launch(gid)
         e, egw, est, epw = runs[1]
-        for ip, ix, vv in batches:
-            e.set_batch(indptr=ip, indices=ix, values=vv)
-            e.forward(True)
-            e.backward()
-            est.copy_(egw)  # the all-to-all at world 1
-            e.apply_adam(1.0)
-            e.wire_shadows()
+        for _ in range(replays):
+            for ip, ix, vv in batches:
+                e.set_batch(indptr=ip, indices=ix, values=vv)
+                e.forward(True)
+                e.backward()
+                est.copy_(egw)  # the all-to-all at world 1
+                e.apply_adam(1.0)
+                e.wire_shadows()
     torch.cuda.synchronize()
-    # the two runs differ by float-atomic order (CSC entry order; the graph's rank pass rides in Adam),
-    # which from fresh Adam slots flips the lr * sign(g) update of rounding-level gradients
-    assert m.loss_accuracy()[0] == pytest.approx(e.loss_accuracy()[0], rel=1e-3)
-    _close(m.params[:m.n_params], e.params[:e.n_params])
-    torch.testing.assert_close(m.adam_m, e.adam_m, rtol=1e-2, atol=1e-6)
+    topo = m.graph_topology(gid)
+    assert topo["chain"] == 1 and topo["roots"] == 1 and topo["nodes"] == topo["edges"] + 1, topo
+    assert topo["memset"] == 0, topo
+    assert (topo["memcpy"] > 0) if memcpy else (topo["memcpy"] == 0), topo
+    ext = m.wire_extent()
+    msgs = [_first_mismatch(k, x, y, geo, ext) for k, x, y in
+            (("params", m.params, e.params), ("adam_m", m.adam_m, e.adam_m), ("adam_v", m.adam_v, e.adam_v),
+             ("param_wire", pw, epw))]
+    assert not any(msgs), "; ".join(x for x in msgs if x)
     assert m.beta_powers() == e.beta_powers()
+    assert m.loss_accuracy() == e.loss_accuracy()
+    if chunks == 1:  # the last step's SpMM read the tight wire rows: Z1's pad columns stay zero
+        z1 = m.buffer(_lib.BUF_Z, 0).view(m.rows, -1)
+        assert z1.shape[1] == 304 and float(z1[:, 300:].abs().max()) == 0.0
     # the replayed graph left the shadows rebuilt from its last all-gather: same forward as a refresh
     ip, ix, vv = batches[0]
     m.set_batch(indptr=ip, indices=ix, values=vv)
@@ -221,7 +255,26 @@ def test_dp_step_graph_world1_matches_eager(comm, chunks, comm_world1):
     m.sync_shadows()
     m.forward(False)
     torch.cuda.synchronize()
-    np.testing.assert_allclose(m.fetch("cos_sim_raw"), a, rtol=0, atol=2e-2)
+    np.testing.assert_array_equal(m.fetch("cos_sim_raw"), a)
+
+
+def test_single_gpu_graphs_are_chains():
+    """The single-GPU multi-step graph bench.py times is one chain of kernel nodes (no memcpy /
+    memset node: every device clear is a kernel)."""
+    _, _, m = make(D, WIDTHS, 128, NEG, "bf16")
+    batches = []
+    for i in range(2):
+        b = synth_batch(D, 128, NEG, seed=310 + i, mean_nnz=32)
+        batches.append(tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gid = m.graph_build_steps(batches, probes=False)
+        m.set_batch(indptr=batches[0][0], indices=batches[0][1], values=batches[0][2])
+        gid1 = m.graph_build()
+    torch.cuda.synchronize()
+    for g in (gid, gid1):
+        topo = m.graph_topology(g)
+        assert topo["chain"] == 1 and topo["kernel"] == topo["nodes"], topo
 
 
 def test_dp_step_graph_modelled_links_runs():
