@@ -35,13 +35,13 @@ __device__ __forceinline__ void csc_scatter_role(const CscScatter& s, int b) {
       const int pos = s.col_ptr[c] + s.rank[k];
       s.csc_row[pos] = row;
       s.csc_val[pos] = v;
-      s.csc_col[pos] = c;
+      if (s.csc_col) s.csc_col[pos] = c;  // null on the plan's rank path (nothing reads it)
     }
     if (lane == 0) {
       const int pos = s.col_ptr[s.D] + row;
       s.csc_row[pos] = row;
       s.csc_val[pos] = 1.0f;
-      s.csc_col[pos] = s.D;
+      if (s.csc_col) s.csc_col[pos] = s.D;
     }
   }
 }

@@ -531,13 +531,13 @@ __device__ __forceinline__ void scatter_rows(const int* __restrict__ indptr,
     const int pos = col_ptr[c] + pos_tmp[k];
     csc_row[pos] = row;
     csc_val[pos] = v;
-    csc_col[pos] = c;
+    if (csc_col) csc_col[pos] = c;  // null on the rank path: only k_dw1_heavy's slices read it
   }
   if (lane == 0) {
     const int pos = col_ptr[D] + row;
     csc_row[pos] = row;
     csc_val[pos] = 1.0f;
-    csc_col[pos] = D;
+    if (csc_col) csc_col[pos] = D;
   }
 }
 
@@ -577,21 +577,32 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
                                                    const int* __restrict__ cnt, int D,
                                                    int* __restrict__ col_ptr,
                                                    int* __restrict__ heavy_n,
-                                                   int2* __restrict__ heavy_items, int nscan) {
+                                                   int2* __restrict__ heavy_items, int nscan,
+                                                   LazyMark mark) {
   __shared__ int s_wave[kScanSmallNT / 64];
   __shared__ int s_hbase;
+  // lazy W1 Adam: the next batch's columns marked first in dispatch order (a few us of scattered
+  // 4-B stores into a 120 KB array, beside the scan)
+  if ((int)blockIdx.x < mark.nblocks) {
+    const unsigned tag = reinterpret_cast<const unsigned*>(mark.st)[3] + 1u;
+    const int nnz = mark.indptr[mark.rows];
+    for (int k = (int)blockIdx.x * 256 + (int)threadIdx.x; k < nnz; k += mark.nblocks * 256)
+      mark.flag[mark.indices[k]] = tag;
+    return;
+  }
+  const int bxm = (int)blockIdx.x - mark.nblocks;
 #if DSSM_SCAN_LAST  // the scan workgroups after the row workgroups in dispatch order
-  const int nrow_blocks = (int)gridDim.x - nscan;
-  if ((int)blockIdx.x >= nrow_blocks)
-    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x - nrow_blocks, s_wave,
+  const int nrow_blocks = (int)gridDim.x - mark.nblocks - nscan;
+  if (bxm >= nrow_blocks)
+    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, bxm - nrow_blocks, s_wave,
                              &s_hbase);
   else {
-    const int rb = blockIdx.x;
+    const int rb = bxm;
 #else
-  if ((int)blockIdx.x < nscan)
-    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, blockIdx.x, s_wave, &s_hbase);
+  if (bxm < nscan)
+    scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, bxm, s_wave, &s_hbase);
   else {
-    const int rb = blockIdx.x - nscan;
+    const int rb = bxm - nscan;
 #endif
 #ifdef DSSM_WG_TL
     const int row = rb * 4 + (threadIdx.x >> 6);
@@ -1023,20 +1034,23 @@ bool csc_rank_supported(int D) {
 
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
                             const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
-                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s) {
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s,
+                            const LazyMark* mark) {
   int* cnt = scratch;
+  const LazyMark mk = mark ? *mark : LazyMark{};
   int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
   int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const int nscan = cdiv(D + 1, kScanSmallNT * 4);
   if (!bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
+  const dim3 grid(mk.nblocks + nscan + cdiv(rows, 4));
   if (ldw % 8)  // the parameter wire's tight rows (RawRow8<u16t>)
-    hipLaunchKernelGGL(k_spmm_scan<u16t>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
-                       values, rows, (const u16t*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
-                       heavy_items, nscan);
+    hipLaunchKernelGGL(k_spmm_scan<u16t>, grid, dim3(256), 0, s, indptr, indices, values, rows,
+                       (const u16t*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
+                       nscan, mk);
   else
-    hipLaunchKernelGGL(k_spmm_scan<u16>, dim3(nscan + cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
-                       values, rows, (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n,
-                       heavy_items, nscan);
+    hipLaunchKernelGGL(k_spmm_scan<u16>, grid, dim3(256), 0, s, indptr, indices, values, rows,
+                       (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
+                       nscan, mk);
   return hipGetLastError();
 }
 
