@@ -102,6 +102,8 @@ def parse():
                     help="analysis only: seconds of host sleep between the graph builds and the warm-up")
     ap.add_argument("--busy-before-warmup", type=float, default=0.0,
                     help="analysis only: seconds of dense matmul load between the graph builds and the warm-up")
+    ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=0|1",
+                    help="analysis only: set a schedule option (dssm_plan_set_option, e.g. LAZY_ADAM=0)")
     ap.add_argument("--dp-check", type=int, default=1,
                     help="N>1: after the timed region, gather the sharded optimizer state and compare a "
                          "digest of every rank's parameters / Adam m / v (reported as dp_check)")
@@ -635,6 +637,9 @@ def main():
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
     if args.deterministic:
         model.set_option("DETERMINISTIC", True)
+    for opt in args.plan_option:
+        name, val = opt.split("=")
+        model.set_option(name, bool(int(val)))
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel

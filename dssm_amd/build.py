@@ -10,7 +10,7 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-CSRC = os.path.join(PKG, "csrc")
+CSRC = os.environ.get("DSSM_CSRC_DIR", os.path.join(PKG, "csrc"))  # side builds: a patched copy
 # DSSM_BUILD_TAG: a side build (A/B variants of DSSM_EXTRA_CFLAGS) in _build<tag>/, libdssm<tag>.so
 TAG = os.environ.get("DSSM_BUILD_TAG", "")
 OBJ = os.path.join(PKG, "_build" + TAG)

@@ -154,16 +154,13 @@ __device__ __forceinline__ RowEntries row_entries(const AdamStep& a, int s, int 
 
 template <typename TZ, bool WIRE>
 __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha,
-                                       const RowEntries* pre = nullptr, const LazyCtx* z = nullptr) {
+                                       const RowEntries* pre = nullptr) {
   const int lane = lane_id();
   const int n = a.n;
   const bool heavy = e - s > kLightEntries;
   if (heavy && a.item_blocks) return;  // updated by the heavy-item workgroups
   if (e == s && a.w1_flat) return;  // untouched: the flat roles' pass
   const TZ* dZ = static_cast<const TZ*>(a.dZ);
-  // lazy rows: the steps this row was left behind, replayed before this step's update (c uniform)
-  const int k = (!WIRE && z && z->pold) ? z->pold[c] : 0;
-  if (!WIRE && z && z->pold && lane == 0) z->pnew[c] = 0;
   for (int c0 = 0; c0 < n; c0 += 512) {
     const int cc = c0 + lane * 8;
     const int nvalid = n - cc;
@@ -212,11 +209,6 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
         if (k == 8) *reinterpret_cast<float4*>(a.g + o + 4) = make_float4(G[4], G[5], G[6], G[7]);
       }
     } else if (nvalid > 0) {
-      for (int j = k; j > 0; --j) {  // lazy: the skipped zero-gradient steps, oldest first
-        const float aj = lazy_alpha(*z, j);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) adam1(P[i], M[i], V[i], 0.f, aj, a.b1c, a.b2c, a.eps);
-      }
       const int k = nvalid >= 8 ? 8 : 4;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -248,8 +240,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
 
 // Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
 template <bool WIRE>
-__device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha,
-                                            const LazyCtx* z = nullptr) {
+__device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
   if (WIRE && a.gout) {  // gradient pass
     const int64_t wo = c < a.D ? wire_row_off(a.geo, c) : 0;
     for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
@@ -258,12 +249,9 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
     }
     return;
   }
-  const int k = (!WIRE && z && z->pold) ? z->pold[c] : 0;
-  if (!WIRE && z && z->pold && threadIdx.x == 0) z->pnew[c] = 0;
   for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
     const size_t o = (size_t)c * a.n + j;
     float P = a.p[o], M = a.m[o], V = a.v[o];
-    for (int q = k; q > 0; --q) adam1(P, M, V, 0.f, lazy_alpha(*z, q), a.b1c, a.b2c, a.eps);
     adam1(P, M, V, grow[j] * a.gs, alpha, a.b1c, a.b2c, a.eps);
     a.p[o] = P;
     a.m[o] = M;
@@ -288,8 +276,7 @@ struct HeavyLds {
 };
 
 template <typename TZ, bool WIRE>
-__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb, HeavyLds& L,
-                                            const LazyCtx* z) {
+__device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int hb, HeavyLds& L) {
   float(&part)[4][512] = L.part;
   float(&grow)[512] = L.grow;
   int& s_last = L.last;
@@ -325,7 +312,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
       __syncthreads();
     }
     if (nit == 1) {
-      w1_row_from<WIRE>(a, c, grow, alpha, z);
+      w1_row_from<WIRE>(a, c, grow, alpha);
     } else {
       // Deterministic mode: the slab rows are released before this workgroup's arrival and the
       // last arrival acquires before reading them (common.h).  Atomics mode: every access to the
@@ -362,7 +349,7 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
                                             __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        w1_row_from<WIRE>(a, c, grow, alpha, z);
+        w1_row_from<WIRE>(a, c, grow, alpha);
       }
     }
     __syncthreads();
@@ -383,18 +370,10 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  LazyCtx z{};
-  if (!WIRE && a.pend) {  // lazy W1 rows: this step's view (launch.h)
-    z.L = reinterpret_cast<const unsigned*>(a.st)[3];
-    z.tag = z.L + 1u;
-    const int rows = a.D + 1;
-    z.pold = a.pend + (size_t)(z.L & 1u) * rows;
-    z.pnew = a.pend + (size_t)((z.L + 1u) & 1u) * rows;
-    z.flag = a.lazy_flag;
-    z.ring = a.ring;
-    z.skip = a.lazy;
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.ring[z.L % kLazyRing] = alpha;  // read by later steps only
-  }
+  // lazy W1 rows (launch.h): the lazy-step counter; this step's alpha into the ring (read by later
+  // steps only).  The pending counts are the flat role's (flat.h).
+  if (!WIRE && a.pend && blockIdx.x == 0 && threadIdx.x == 0)
+    a.ring[reinterpret_cast<const unsigned*>(a.st)[3] % kLazyRing] = alpha;
   // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
   // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
   // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
@@ -423,7 +402,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   if (is_rank) {
     csc_rank_role(a.rank, bx - rs, reinterpret_cast<unsigned*>(s_lds));
   } else if (b0 < nh) {
-    heavy_items<TZ, WIRE>(a, alpha, b0, *reinterpret_cast<HeavyLds*>(s_lds), &z);
+    heavy_items<TZ, WIRE>(a, alpha, b0, *reinterpret_cast<HeavyLds*>(s_lds));
   } else if (w1_role) {
     const int b = DSSM_ADAM_ORDER == 0 ? b0 - nh : b0 - nh - nd;
     // the next row's column range is loaded while this row is processed (one dependent load
@@ -454,7 +433,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
           e2 = a.col_ptr[c2 + 1];
         }
         const RowEntries next = row_entries(a, sn, en);
-        w1_row<TZ, false>(a, c, s, e, alpha, &ent, &z);
+        w1_row<TZ, false>(a, c, s, e, alpha, &ent);
         s = sn;
         e = en;
         sn = s2;
@@ -469,7 +448,7 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
           sn = a.col_ptr[cn];
           en = a.col_ptr[cn + 1];
         }
-        w1_row<TZ, false>(a, c, s, e, alpha, nullptr, &z);
+        w1_row<TZ, false>(a, c, s, e, alpha);
         s = sn;
         e = en;
       }
@@ -514,6 +493,16 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       }
     } else if (a.w1_flat) {
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
+      LazyCtx z{};
+      if (!WIRE && a.pend) {
+        z.L = reinterpret_cast<const unsigned*>(a.st)[3];
+        z.tag = z.L + 1u;
+        z.pold = a.pend + (size_t)(z.L & 1u) * (a.D + 1);
+        z.pnew = a.pend + (size_t)((z.L + 1u) & 1u) * (a.D + 1);
+        z.flag = a.lazy_flag;
+        z.ring = a.ring;
+        z.skip = a.lazy;
+      }
       FlatSlice f{a.p, a.m, a.v, a.shadow, a.ldsh, a.n, a.D, a.col_ptr, a.st, a.lr, a.b1c, a.b2c, a.eps,
                   0, (int64_t)(a.D + 1) * a.n / 4, a.dense_blocks, z};
       flat_untouched(f, bi);
@@ -592,7 +581,8 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       if (u == ntop - 1) {
         a.st[0] = b1p * a.beta1;
         a.st[1] = b2p * a.beta2;
-        if (!WIRE && a.pend) reinterpret_cast<unsigned*>(a.st)[3] = z.L + 1u;  // the lazy-step counter
+        if (!WIRE && a.pend)  // the lazy-step counter
+          reinterpret_cast<unsigned*>(a.st)[3] = reinterpret_cast<const unsigned*>(a.st)[3] + 1u;
         if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

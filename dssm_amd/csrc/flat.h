@@ -51,11 +51,17 @@ __device__ __forceinline__ void flat_untouched(const FlatSlice& f, int bi) {
   for (int64_t i = f.i4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < f.i4_end;
        i += (int64_t)f.nblocks * blockDim.x) {
     const int c = (int)((i * 4) / f.n);
-    if (f.col_ptr[c + 1] != f.col_ptr[c]) continue;
+    const bool first = i * 4 == (int64_t)c * f.n;  // the row's first float4 keeps its pending count
+    if (f.col_ptr[c + 1] != f.col_ptr[c]) {
+      // a row with an entry this step (updated by the W1-row / heavy roles) is never behind: the
+      // previous step marked this batch's columns and brought them up to date, or was not lazy and
+      // brought every row up to date
+      if (f.z.pold && first) f.z.pnew[c] = 0;
+      continue;
+    }
     int k = 0;  // lazy: this row's pending steps
     if (f.z.pold) {
       k = f.z.pold[c];
-      const bool first = i * 4 == (int64_t)c * f.n;  // the row's first float4 keeps its count
       if (f.z.skip && k < kLazyCap && f.z.flag[c] != f.z.tag) {  // nothing reads it next step
         if (first) f.z.pnew[c] = k + 1;
         continue;

@@ -862,220 +862,6 @@ __global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, i
 #endif
 }
 
-// ---- row-panel forward NT GEMM (round 4) ---------------------------------------------------------
-// The whole-K 128 x 64 tiles above re-fetch each 128-row A panel (fp32 pre-BN Z, 154 KB, served from
-// the Infinity Cache: the previous launch's output) once per column tile -- 5x at N = 300 -- and
-// spend ~7 us receiving ~193 KB per CU.  Here a workgroup owns a panel of 16 RF rows and a 16 CF-wide
-// column slab covering ldc in ncx = 1-2 slabs, so the A panel is fetched ncx times instead of 5 and
-// the weight slab (W^T rows, L2-resident) takes the rest of the bytes:
-//   N = 300: 48 rows x 160 columns, 6 waves, 128 x 2 = 256 workgroups (57.6 KB of A + 90 KB of W^T);
-//   N = 128: 32 rows x 128 columns, 4 waves, 192 workgroups (38.4 KB of A + 77 KB of W^T).
-// A wave owns 16 rows x 16 CFW columns (CFW accumulator fragments).  Panels may straddle the tower
-// boundary (48 does not divide query_bs): each row takes its own tower's BN coefficients, and a
-// straddling panel publishes its column sums once per tower.  FS = 1 epilogue (bias, per-tower
-// column sums and sums of squares, fp64 atomics), LDS-staged C stores, A written to a_out (bf16,
-// column slab 0).  Not deterministic-mode (the slab rows of DetAcc are per 128-row tile).
-constexpr int kRpMaxK = 320;
-__host__ __device__ constexpr int rp_ldk(int Kp) { return Kp + 8; }
-template <int RF, int CF>
-__host__ __device__ inline size_t rp_smem_bytes(int Kp) {
-  const size_t panels = (size_t)(16 * RF + 16 * CF) * rp_ldk(Kp) * 2 + (size_t)4 * Kp * 4;
-  const size_t epi = (size_t)16 * RF * (16 * CF + 4) * 4;  // the C tile, over the panels
-  return (panels > epi ? panels : epi) + (size_t)RF * 16 * CF * 2 * 8;
-}
-
-template <int RF, int CF, int CFW>
-__global__ __launch_bounds__(64 * RF * (CF / CFW)) void k_gemm_nt_rp(NtParams a, NtFuse f, int ncx,
-                                                                      int ntiles) {
-  constexpr int WC = CF / CFW, NW = RF * WC, NT = 64 * NW, ROWS = 16 * RF, COLS = 16 * CF;
-  constexpr int KG = kRpMaxK / 8;                     // 8-element k groups of a row (max)
-  constexpr int NGA = (ROWS * KG + NT - 1) / NT;      // A groups per thread
-  constexpr int NGB = (COLS * KG + NT - 1) / NT;      // B groups per thread
-  constexpr int NPC = (2 * kWkMaxK + NT - 1) / NT;    // coefficient items per thread
-  extern __shared__ __attribute__((aligned(16))) u16 rp_smem[];
-  if ((int)blockIdx.x >= ntiles) {
-    if (f.in_from_sums) fs_materialize_fwd(f.in);
-    return;
-  }
-  const int tile = xcd_tile(blockIdx.x, ntiles);  // a row panel's column slabs on one XCD
-  const int tx = tile % ncx, ty = tile / ncx;
-  const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc, rs = a.row_split;
-  const int Kp = (K + 31) & ~31, LDK = rp_ldk(Kp), kgs = Kp / 8;
-  u16* sA = rp_smem;                                          // [ROWS][LDK]
-  u16* sB = sA + ROWS * LDK;                                  // [COLS][LDK]
-  float* sCoef = reinterpret_cast<float*>(sB + COLS * LDK);   // [tower][inv|shift][Kp]
-  const size_t panels = (size_t)(ROWS + COLS) * LDK * 2 + (size_t)4 * Kp * 4;
-  const size_t epi = (size_t)ROWS * (COLS + 4) * 4;
-  double* sRed = reinterpret_cast<double*>(reinterpret_cast<char*>(rp_smem) + (panels > epi ? panels : epi));
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int rf = w / WC, cw = w % WC;
-  const int bm = ty * ROWS, bn = tx * COLS;
-  FsCoefStage<NPC> cst;
-  if (f.in_from_sums) cst.load(f.in, t, NT);
-  // ---- every global load of the panel, issued first
-  float4 fa[NGA][2];
-  uint4 ub[NGB];
-#pragma unroll
-  for (int i = 0; i < NGA; ++i) {
-    const int g = t + NT * i, r = g / kgs, kg = (g - r * kgs) * 8;
-    const bool ok = g < ROWS * kgs && bm + r < M && kg < lda;
-    const float* z = (const float*)a.A + (ok ? (size_t)(bm + r) * lda + kg : 0);
-    fa[i][0] = *reinterpret_cast<const float4*>(z);
-    fa[i][1] = *reinterpret_cast<const float4*>(z + 4);
-  }
-#pragma unroll
-  for (int i = 0; i < NGB; ++i) {
-    const int g = t + NT * i, r = g / kgs, kg = (g - r * kgs) * 8;
-    const bool ok = g < COLS * kgs && bn + r < N && kg < ldb;
-    ub[i] = *reinterpret_cast<const uint4*>(a.BT + (ok ? (size_t)(bn + r) * ldb + kg : 0));
-  }
-  float bcol[CFW];
-#pragma unroll
-  for (int j = 0; j < CFW; ++j) {
-    const int n = bn + (cw * CFW + j) * 16 + (lane & 15);
-    bcol[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
-  }
-  // ---- the A operand's BN coefficients, both towers
-  if (f.in_from_sums) {
-    cst.finish(f.in, t, NT, [&](int tw, int k, float, float, float inv, float sh) {
-      if (k < Kp) {
-        sCoef[(tw * 2 + 0) * Kp + k] = inv;
-        sCoef[(tw * 2 + 1) * Kp + k] = sh;
-      }
-    });
-    for (int i = t; i < 2 * (Kp - lda); i += NT) {  // K pad beyond the stored width
-      const int tw = i / (Kp - lda), k = lda + i % (Kp - lda);
-      sCoef[(tw * 2 + 0) * Kp + k] = 0.f;
-      sCoef[(tw * 2 + 1) * Kp + k] = 0.f;
-    }
-  } else {
-    const size_t plane = (size_t)2 * lda;
-    for (int i = t; i < 2 * Kp; i += NT) {
-      const int tw = i / Kp, k = i - tw * Kp;
-      const bool ok = k < lda;
-      sCoef[(tw * 2 + 0) * Kp + k] = ok ? a.coef[2 * plane + (size_t)tw * lda + k] : 0.f;
-      sCoef[(tw * 2 + 1) * Kp + k] = ok ? a.coef[3 * plane + (size_t)tw * lda + k] : 0.f;
-    }
-  }
-  __syncthreads();
-  // ---- LDS images: A = relu(BN(Z)) in bf16 (each row its own tower), B as loaded
-  const bool write_a = a.a_out != nullptr && tx == 0;
-#pragma unroll
-  for (int i = 0; i < NGA; ++i) {
-    const int g = t + NT * i, r = g / kgs, kg = (g - r * kgs) * 8;
-    if (g < ROWS * kgs) {
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      const int m = bm + r;
-      if (m < M && kg < lda) {
-        const float* ci = &sCoef[((m < rs ? 0 : 1) * 2) * Kp + kg];
-        const float* ch = ci + Kp;
-        const float z[8] = {fa[i][0].x, fa[i][0].y, fa[i][0].z, fa[i][0].w,
-                            fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
-        float y[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
-        v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
-        v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
-        if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)m * lda + kg) = v;
-      }
-      *reinterpret_cast<uint4*>(&sA[r * LDK + kg]) = v;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NGB; ++i) {
-    const int g = t + NT * i, r = g / kgs, kg = (g - r * kgs) * 8;
-    if (g < COLS * kgs)
-      *reinterpret_cast<uint4*>(&sB[r * LDK + kg]) =
-          (bn + r < N && kg < ldb) ? ub[i] : make_uint4(0u, 0u, 0u, 0u);
-  }
-  __syncthreads();
-  // ---- MFMA over the whole K: one A fragment, CFW B fragments per k-step (next step read ahead)
-  f32x4 acc[CFW];
-#pragma unroll
-  for (int j = 0; j < CFW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const u16* pa = sA + (rf * 16 + (lane & 15)) * LDK + 8 * (lane >> 4);
-  const u16* pb = sB + (cw * CFW * 16 + (lane & 15)) * LDK + 8 * (lane >> 4);
-  bf16x8 af = *reinterpret_cast<const bf16x8*>(pa), bfr[CFW];
-#pragma unroll
-  for (int j = 0; j < CFW; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(pb + j * 16 * LDK);
-  for (int ks = 0; ks < Kp; ks += 32) {
-    const int kn = ks + 32 < Kp ? ks + 32 : ks;
-    const bf16x8 an = *reinterpret_cast<const bf16x8*>(pa + kn);
-    bf16x8 bnx[CFW];
-#pragma unroll
-    for (int j = 0; j < CFW; ++j) bnx[j] = *reinterpret_cast<const bf16x8*>(pb + j * 16 * LDK + kn);
-#pragma unroll
-    for (int j = 0; j < CFW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[j], 0, 0, 0);
-    af = an;
-#pragma unroll
-    for (int j = 0; j < CFW; ++j) bfr[j] = bnx[j];
-  }
-  // ---- epilogue: C through LDS (the panels' space), per-tower column sums
-  constexpr int kCld = COLS + 4;
-  float* sC = reinterpret_cast<float*>(rp_smem);
-  __syncthreads();
-  float x[CFW][4];
-#pragma unroll
-  for (int j = 0; j < CFW; ++j) {
-    const int c = (cw * CFW + j) * 16 + (lane & 15), n = bn + c;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr = rf * 16 + (lane >> 4) * 4 + r;
-      x[j][r] = (n < N && bm + rr < M) ? acc[j][r] + bcol[j] : 0.f;
-      sC[rr * kCld + c] = x[j][r];
-    }
-  }
-  // towers present in the panel: one pass, two for the panel across the boundary
-  const int t_lo = bm < rs ? 0 : 1, t_hi = bm + ROWS - 1 < rs ? 0 : 1;
-  for (int tw = t_lo; tw <= t_hi; ++tw) {
-    double cs[CFW], cq[CFW];
-#pragma unroll
-    for (int j = 0; j < CFW; ++j) {
-      cs[j] = 0.0;
-      cq[j] = 0.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + rf * 16 + (lane >> 4) * 4 + r;
-        if ((m < rs ? 0 : 1) == tw) {
-          cs[j] += x[j][r];
-          cq[j] += (double)x[j][r] * x[j][r];
-        }
-      }
-      cs[j] += __shfl_xor(cs[j], 16);
-      cs[j] += __shfl_xor(cs[j], 32);
-      cq[j] += __shfl_xor(cq[j], 16);
-      cq[j] += __shfl_xor(cq[j], 32);
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < CFW; ++j) {
-        const int c = (cw * CFW + j) * 16 + lane;
-        sRed[(rf * COLS + c) * 2] = cs[j];
-        sRed[(rf * COLS + c) * 2 + 1] = cq[j];
-      }
-    }
-    __syncthreads();
-    for (int i = t; i < 2 * COLS; i += NT) {
-      const int c = i >> 1, st = i & 1, n = bn + c;
-      if (n < N) {
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < RF; ++q) v += sRed[(q * COLS + c) * 2 + st];
-        atomic_add_f64(f.out_sum + (size_t)(tw * 2 + st) * ldc + n, v);
-      }
-    }
-    __syncthreads();
-  }
-  // C rows out as 16-B segments (the slab's valid width: ldc - bn, a multiple of 8)
-  const int ncols = min(COLS, ldc - bn);
-  for (int i = t; i < ROWS * (COLS / 4); i += NT) {
-    const int r = i / (COLS / 4), q = (i - r * (COLS / 4)) * 4;
-    if (bm + r < M && q < ncols)
-      *reinterpret_cast<float4*>(a.C + (size_t)(bm + r) * ldc + bn + q) =
-          *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
-  }
-}
-
 __global__ __launch_bounds__(256) void k_gemm_tn(TnParams p) {
   __shared__ __attribute__((aligned(16))) u16 sA[2 * kTileElems];  // [k][m]
   __shared__ __attribute__((aligned(16))) u16 sB[2 * kTileElems];  // [k][n]
@@ -1348,22 +1134,6 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
   f.out_sum = out_sum;
   f.lds_epi = 1;  // measured: 14.4 (LDS-staged epilogue) vs 16.2 us per NT launch
   if (det) f.det = *det;
-#ifndef DSSM_NT_RP
-#define DSSM_NT_RP 1
-#endif
-  // row-panel tiles (k_gemm_nt_rp): fused-statistics forward, not deterministic mode
-  if (DSSM_NT_RP && !det && K <= kRpMaxK && (ldc == 304 || ldc == 128) && lda <= kRpMaxK + 8) {
-    const int Kp = (K + 31) & ~31;
-#define DSSM_NTRP(RF, CF, CFW)                                                                    \
-  {                                                                                               \
-    const int ncx = cdiv(ldc, 16 * CF), ntiles = ncx * cdiv(M, 16 * RF);                           \
-    hipLaunchKernelGGL((k_gemm_nt_rp<RF, CF, CFW>), dim3(ntiles + (in_from_sums ? 1 : 0)),          \
-                       dim3(64 * RF * (CF / CFW)), (rp_smem_bytes<RF, CF>(Kp)), s, a, f, ncx, ntiles); \
-  }
-    if (ldc == 304) DSSM_NTRP(3, 10, 5) else DSSM_NTRP(2, 8, 4)
-#undef DSSM_NTRP
-    return hipGetLastError();
-  }
   if (K <= kWkMaxK && (row_split % 64) == 0) {
     const int Kp = (K + 31) & ~31;
     const int nx = cdiv(ldc, 64);

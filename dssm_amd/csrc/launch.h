@@ -57,7 +57,7 @@ hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_i
                            int* row_out, float* val_out, hipStream_t s);
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
-// Lazy W1 Adam (multi-step graphs): the NEXT batch's columns marked in the current step's SpMM
+// Lazy W1 Adam (multi-step graphs): the NEXT batch's columns marked in the current step's BN1-sums
 // launch (flag[c] = the lazy-step counter st[3] + 1), so that step's Adam knows which of the rows it
 // may leave behind (adam.hip).  nblocks == 0: no marking.
 struct LazyMark {
@@ -70,13 +70,13 @@ struct LazyMark {
 };
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
                             const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
-                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s,
-                            const LazyMark* mark = nullptr);
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s);
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s,
-                               CscScatter* scatter_out = nullptr, const DetAcc* det = nullptr);
+                               CscScatter* scatter_out = nullptr, const DetAcc* det = nullptr,
+                               const LazyMark* mark = nullptr);
 // scatter_out: the launch runs the BN1 sums alone and hands the scatter to *scatter_out (a role of
 // a later launch: launch_cosine_loss).
 // dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row

@@ -654,18 +654,10 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   }
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   if (merged) {  // the SpMM rows share their launch with the column scan
-    // lazy W1 Adam: the next batch's columns marked in this launch (multi-step graphs)
-    dssm::LazyMark mark{};
-    P->lazy_marked = false;
-    if (P->lazy_steps && P->lazy_next_indptr && P->lazy_ok()) {
-      mark = dssm::LazyMark{P->lazy_next_indptr, P->lazy_next_indices, Lt.R, P->at<unsigned>(Lt.lazy_flag),
-                            P->at<float>(Lt.adam_state), 64};
-      P->lazy_marked = true;
-    }
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
                                    (const uint16_t*)P->weight(0), P->weight_ld(0), Lt.n[0], P->bias(0),
                                    P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
-                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s, &mark));
+                                   P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
   } else {
     // eval: every layer's BN coefficients from the EMA, in the SpMM launch's extra workgroups
     dssm::EvalCoef ec{};
@@ -703,13 +695,21 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     int* scat_row = det ? P->at<int>(Lt.sort_row) : P->at<int>(Lt.csc_row);
     float* scat_val = det ? P->at<float>(Lt.sort_val) : P->at<float>(Lt.csc_val);
     const dssm::BnSide b0 = P->bn_side(0);
+    // lazy W1 Adam: the next batch's columns marked in the BN1-sums launch (multi-step graphs)
+    dssm::LazyMark mark{};
+    P->lazy_marked = false;
+    if (merged && P->lazy_steps && P->lazy_next_indptr && P->lazy_ok()) {
+      mark = dssm::LazyMark{P->lazy_next_indptr, P->lazy_next_indices, Lt.R, P->at<unsigned>(Lt.lazy_flag),
+                            P->at<float>(Lt.adam_state), 64};
+      P->lazy_marked = true;
+    }
     if (merged)
       HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
                                         P->at<int>(Lt.col_ptr), scat_row, scat_val,
                                         nullptr, s, scat_cos ? &scat : nullptr,  // csc_col: unread on the rank path
-                                        det ? &b0.fdet : nullptr));
+                                        det ? &b0.fdet : nullptr, &mark));
     else
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s, det ? &b0.fdet : nullptr));

@@ -577,22 +577,12 @@ __global__ __launch_bounds__(256) void k_spmm_scan(const int* __restrict__ indpt
                                                    const int* __restrict__ cnt, int D,
                                                    int* __restrict__ col_ptr,
                                                    int* __restrict__ heavy_n,
-                                                   int2* __restrict__ heavy_items, int nscan,
-                                                   LazyMark mark) {
+                                                   int2* __restrict__ heavy_items, int nscan) {
   __shared__ int s_wave[kScanSmallNT / 64];
   __shared__ int s_hbase;
-  // lazy W1 Adam: the next batch's columns marked first in dispatch order (a few us of scattered
-  // 4-B stores into a 120 KB array, beside the scan)
-  if ((int)blockIdx.x < mark.nblocks) {
-    const unsigned tag = reinterpret_cast<const unsigned*>(mark.st)[3] + 1u;
-    const int nnz = mark.indptr[mark.rows];
-    for (int k = (int)blockIdx.x * 256 + (int)threadIdx.x; k < nnz; k += mark.nblocks * 256)
-      mark.flag[mark.indices[k]] = tag;
-    return;
-  }
-  const int bxm = (int)blockIdx.x - mark.nblocks;
+  const int bxm = (int)blockIdx.x;
 #if DSSM_SCAN_LAST  // the scan workgroups after the row workgroups in dispatch order
-  const int nrow_blocks = (int)gridDim.x - mark.nblocks - nscan;
+  const int nrow_blocks = (int)gridDim.x - nscan;
   if (bxm >= nrow_blocks)
     scan_chunk<kScanSmallNT>(cnt, D, rows, col_ptr, heavy_n, heavy_items, bxm - nrow_blocks, s_wave,
                              &s_hbase);
@@ -630,14 +620,24 @@ __global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ 
                                                       int* __restrict__ cnt,
                                                       int* __restrict__ csc_row,
                                                       float* __restrict__ csc_val,
-                                                      int* __restrict__ csc_col, DetAcc det) {
+                                                      int* __restrict__ csc_col, DetAcc det,
+                                                      LazyMark mark) {
   __shared__ double s_red[2][4][64];
   const int b = blockIdx.x;
-  if (b < nsum)
+  const int nscat = (int)gridDim.x - nsum - mark.nblocks;
+  if (b < nsum) {
     bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red, det, nsum / nsum_x);
-  else
+  } else if (b < nsum + nscat) {
     scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val,
-                 csc_col, b - nsum, (int)gridDim.x - nsum);
+                 csc_col, b - nsum, nscat);
+  } else {
+    // lazy W1 Adam: the NEXT batch's columns marked (flag = the lazy-step counter + 1): scattered
+    // 4-B stores into a 120 KB array, on CUs the BN sums leave idle
+    const unsigned tag = reinterpret_cast<const unsigned*>(mark.st)[3] + 1u;
+    const int nnz = mark.indptr[mark.rows];
+    for (int k = (b - nsum - nscat) * 256 + (int)threadIdx.x; k < nnz; k += mark.nblocks * 256)
+      mark.flag[mark.indices[k]] = tag;
+  }
 }
 
 // Fallback fill with per-entry global atomics (one wave per row).
@@ -1034,23 +1034,21 @@ bool csc_rank_supported(int D) {
 
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
                             const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
-                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s,
-                            const LazyMark* mark) {
+                            int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s) {
   int* cnt = scratch;
-  const LazyMark mk = mark ? *mark : LazyMark{};
   int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
   int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const int nscan = cdiv(D + 1, kScanSmallNT * 4);
   if (!bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
-  const dim3 grid(mk.nblocks + nscan + cdiv(rows, 4));
+  const dim3 grid(nscan + cdiv(rows, 4));
   if (ldw % 8)  // the parameter wire's tight rows (RawRow8<u16t>)
     hipLaunchKernelGGL(k_spmm_scan<u16t>, grid, dim3(256), 0, s, indptr, indices, values, rows,
                        (const u16t*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
-                       nscan, mk);
+                       nscan);
   else
     hipLaunchKernelGGL(k_spmm_scan<u16>, grid, dim3(256), 0, s, indptr, indices, values, rows,
                        (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
-                       nscan, mk);
+                       nscan);
   return hipGetLastError();
 }
 
@@ -1058,7 +1056,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out,
-                               const DetAcc* det) {
+                               const DetAcc* det, const LazyMark* mark) {
   (void)max_nnz;
   if (row_split % kSumsRows) return hipErrorInvalidValue;
   int* cnt = scratch;
@@ -1070,9 +1068,10 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
     *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                               csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
   }
-  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n, row_split,
-                     fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
-                     csc_row, csc_val, csc_col, det ? *det : DetAcc{});
+  const LazyMark mk = mark ? *mark : LazyMark{};
+  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4)) + mk.nblocks), dim3(256), 0, s,
+                     Z, ldz, n, row_split, fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr,
+                     pos_tmp, cnt, csc_row, csc_val, csc_col, det ? *det : DetAcc{}, mk);
   return hipGetLastError();
 }
 
