@@ -370,10 +370,6 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  // lazy W1 rows (launch.h): the lazy-step counter; this step's alpha into the ring (read by later
-  // steps only).  The pending counts are the flat role's (flat.h).
-  if (!WIRE && a.pend && blockIdx.x == 0 && threadIdx.x == 0)
-    a.ring[reinterpret_cast<const unsigned*>(a.st)[3] % kLazyRing] = alpha;
   // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
   // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
   // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
@@ -493,18 +489,8 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       }
     } else if (a.w1_flat) {
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
-      LazyCtx z{};
-      if (!WIRE && a.pend) {
-        z.L = reinterpret_cast<const unsigned*>(a.st)[3];
-        z.tag = z.L + 1u;
-        z.pold = a.pend + (size_t)(z.L & 1u) * (a.D + 1);
-        z.pnew = a.pend + (size_t)((z.L + 1u) & 1u) * (a.D + 1);
-        z.flag = a.lazy_flag;
-        z.ring = a.ring;
-        z.skip = a.lazy;
-      }
       FlatSlice f{a.p, a.m, a.v, a.shadow, a.ldsh, a.n, a.D, a.col_ptr, a.st, a.lr, a.b1c, a.b2c, a.eps,
-                  0, (int64_t)(a.D + 1) * a.n / 4, a.dense_blocks, z};
+                  0, (int64_t)(a.D + 1) * a.n / 4, a.dense_blocks};
       flat_untouched(f, bi);
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
@@ -581,8 +567,6 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       if (u == ntop - 1) {
         a.st[0] = b1p * a.beta1;
         a.st[1] = b2p * a.beta2;
-        if (!WIRE && a.pend)  // the lazy-step counter
-          reinterpret_cast<unsigned*>(a.st)[3] = reinterpret_cast<const unsigned*>(a.st)[3] + 1u;
         if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

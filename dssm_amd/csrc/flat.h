@@ -6,7 +6,6 @@
 // Adam launch shrank, 205 -> 211 us/step.)
 #pragma once
 #include "common.h"
-#include "launch.h"
 
 namespace dssm {
 
@@ -16,19 +15,6 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
   v += (g * g - v) * b2c;
   p -= (m * alpha) / (sqrtf(v) + eps);
 }
-
-// Lazy W1 rows (launch.h, kLazyRing / kLazyCap): one launch's view of the pending-step state.
-struct LazyCtx {
-  const int* pold;  // pending zero-gradient steps per row as the previous step left them (null: off)
-  int* pnew;        // ... as this step leaves them
-  const unsigned* flag;  // the next batch's marks (== tag: the next batch reads the row)
-  const float* ring;     // alpha of the previous lazy steps
-  unsigned L, tag;       // this step's lazy-step counter; tag = L + 1
-  int skip;              // 1: rows untouched now and unmarked may stay behind
-};
-// The k skipped steps of one element replayed oldest first, each with its own alpha and g = 0:
-// the arithmetic dense ApplyAdam did for the row at those steps (adam1 with a zero gradient).
-__device__ __forceinline__ float lazy_alpha(const LazyCtx& z, int j) { return z.ring[(z.L - j) % kLazyRing]; }
 
 struct FlatSlice {
   float* p;
@@ -42,7 +28,6 @@ struct FlatSlice {
   float lr, b1c, b2c, eps;
   int64_t i4_begin, i4_end;  // float4 range of the [W1; b1] block
   int nblocks;               // workgroups given to the slice
-  LazyCtx z;                 // lazy rows (z.pold null: every untouched row updated, no bookkeeping)
 };
 
 // Workgroup bi of the slice's nblocks: float4 streaming over the untouched rows of its range.
@@ -51,33 +36,10 @@ __device__ __forceinline__ void flat_untouched(const FlatSlice& f, int bi) {
   for (int64_t i = f.i4_begin + (int64_t)bi * blockDim.x + threadIdx.x; i < f.i4_end;
        i += (int64_t)f.nblocks * blockDim.x) {
     const int c = (int)((i * 4) / f.n);
-    const bool first = i * 4 == (int64_t)c * f.n;  // the row's first float4 keeps its pending count
-    if (f.col_ptr[c + 1] != f.col_ptr[c]) {
-      // a row with an entry this step (updated by the W1-row / heavy roles) is never behind: the
-      // previous step marked this batch's columns and brought them up to date, or was not lazy and
-      // brought every row up to date
-      if (f.z.pold && first) f.z.pnew[c] = 0;
-      continue;
-    }
-    int k = 0;  // lazy: this row's pending steps
-    if (f.z.pold) {
-      k = f.z.pold[c];
-      if (f.z.skip && k < kLazyCap && f.z.flag[c] != f.z.tag) {  // nothing reads it next step
-        if (first) f.z.pnew[c] = k + 1;
-        continue;
-      }
-      if (first) f.z.pnew[c] = 0;
-    }
+    if (f.col_ptr[c + 1] != f.col_ptr[c]) continue;
     float4 pp = ld_stream4(f.p + i * 4);
     float4 mm = ld_stream4(f.m + i * 4);
     float4 vv = ld_stream4(f.v + i * 4);
-    for (int j = k; j > 0; --j) {  // the skipped steps first, oldest first
-      const float aj = lazy_alpha(f.z, j);
-      adam1(pp.x, mm.x, vv.x, 0.f, aj, f.b1c, f.b2c, f.eps);
-      adam1(pp.y, mm.y, vv.y, 0.f, aj, f.b1c, f.b2c, f.eps);
-      adam1(pp.z, mm.z, vv.z, 0.f, aj, f.b1c, f.b2c, f.eps);
-      adam1(pp.w, mm.w, vv.w, 0.f, aj, f.b1c, f.b2c, f.eps);
-    }
     adam1(pp.x, mm.x, vv.x, 0.f, alpha, f.b1c, f.b2c, f.eps);
     adam1(pp.y, mm.y, vv.y, 0.f, alpha, f.b1c, f.b2c, f.eps);
     adam1(pp.z, mm.z, vv.z, 0.f, alpha, f.b1c, f.b2c, f.eps);

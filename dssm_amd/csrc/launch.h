@@ -57,17 +57,6 @@ hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_i
                            int* row_out, float* val_out, hipStream_t s);
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
-// Lazy W1 Adam (multi-step graphs): the NEXT batch's columns marked in the current step's BN1-sums
-// launch (flag[c] = the lazy-step counter st[3] + 1), so that step's Adam knows which of the rows it
-// may leave behind (adam.hip).  nblocks == 0: no marking.
-struct LazyMark {
-  const int* indptr;
-  const int* indices;
-  int rows;
-  unsigned* flag;
-  const float* st;  // the device Adam state (st[3]: the lazy-step counter, as uint bits)
-  int nblocks;
-};
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
                             const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
                             int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s);
@@ -75,8 +64,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s,
-                               CscScatter* scatter_out = nullptr, const DetAcc* det = nullptr,
-                               const LazyMark* mark = nullptr);
+                               CscScatter* scatter_out = nullptr, const DetAcc* det = nullptr);
 // scatter_out: the launch runs the BN1 sums alone and hands the scatter to *scatter_out (a role of
 // a later launch: launch_cosine_loss).
 // dW1 (+ db1 as row D) = [X | 1]^T * dZ1 into G [(D+1) x n] fp32 (ld n).  light=true: every row
@@ -258,16 +246,6 @@ __host__ __device__ inline int wire_chunk_row(const WireGeo& g, int chunk, int v
   return c < D ? c : -1;
 }
 
-// Lazy W1 rows (single GPU, multi-step graphs): TF1.x's dense ApplyAdam
-// moves every row every step, but a row with no entry in the batch has g = 0, so its update is a
-// fixed function of (p, m, v) and the step's alpha.  A step whose next batch is marked (lazy) leaves
-// a row with no entry now AND none in the next batch behind, counting it in pend; the row is caught
-// up -- the skipped steps replayed in order with their own alpha, bit for bit as the dense steps --
-// by the first step that touches it or whose next batch reads it, and by every step whose next batch
-// is not marked (a graph's last step, eager steps), so outside a multi-step graph every row is
-// current.  A row is never more than kLazyCap steps behind.
-constexpr int kLazyRing = 64;  // alpha of the last lazy steps, indexed by the lazy-step counter
-constexpr int kLazyCap = 16;   // a row that many steps behind is updated even if nothing reads it
 struct AdamStep {
   float* p;
   float* g;
@@ -326,14 +304,6 @@ struct AdamStep {
   // items, zero for untouched rows) and write them as bf16 to gout (wire layout below; the bias row
   // as fp32 into g) instead of updating parameters; no dense range, no beta-power advance
   uint16_t* gout;
-  // lazy W1 rows (pend != null): pend [2][D + 1] pending zero-gradient steps per row, the buffer
-  // read / written chosen by the lazy-step counter's parity (st[3]); lazy_flag [D + 1] the next
-  // batch's marks; ring [kLazyRing] this and the previous lazy steps' alpha; lazy = 1: rows untouched
-  // now and unmarked may be left behind (else every row is brought up to date)
-  int* pend;
-  const unsigned* lazy_flag;
-  float* ring;
-  int lazy;
   // chunked wire geometry (WireGeo; ww == 0: the wire is laid out as the arena)
   WireGeo geo;
   int wchunk = -1;     // gradient pass: only the rows of this chunk (-1: every row)

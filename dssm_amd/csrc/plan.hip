@@ -55,7 +55,6 @@ struct Layout {
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
   size_t dw_slab[DSSM_MAX_LAYERS] = {}, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
-  size_t lazy_pend, lazy_flag, lazy_ring;  // lazy W1 Adam state (launch.h kLazyRing)
   size_t sort_row, sort_val, heavy_slab;  // deterministic mode: transpose scratch, heavy partial rows
   // fp64 accumulators of the fused BN statistics (bnfuse.h), one zeroed region
   size_t sums = 0, sums_bytes = 0;
@@ -167,9 +166,6 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.heavy_slab = take(dssm::csc_heavy_cap(Lt.R, Lt.max_nnz) * Lt.n[0] * 4);
   // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
   Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
-  Lt.lazy_pend = take((size_t)2 * (Lt.D + 1) * 4);
-  Lt.lazy_flag = take((size_t)(Lt.D + 1) * 4);
-  Lt.lazy_ring = take((size_t)dssm::kLazyRing * 4);
   if (Lt.bf16) {
     // fp64 [2 towers][2][ld] forward and backward accumulators per layer (fused statistics), one
     // contiguous region zeroed as a whole by the step's first launch
@@ -242,13 +238,6 @@ struct dssm_plan {
   const int32_t* host_rank_indptr = nullptr;
   const int32_t* host_rank_indices = nullptr;
   const int32_t* rank_done_for = nullptr;
-  // Lazy W1 Adam (launch.h): while a multi-step graph is captured, the step's next batch (its columns
-  // marked by this step's SpMM launch); lazy_marked: the forward marked them, so this step's Adam may
-  // leave rows behind.  lazy_steps: the steps being captured keep the pending-step bookkeeping.
-  bool lazy_steps = false;
-  const int32_t* lazy_next_indptr = nullptr;
-  const int32_t* lazy_next_indices = nullptr;
-  bool lazy_marked = false;
   // Schedule options (dssm_plan_set_option; never read from the environment).  Each names a
   // measured-faster default and the alternative it replaced, kept for parity tests and shapes the
   // default does not support.  Graphs captured earlier keep the schedule they were captured with.
@@ -264,7 +253,6 @@ struct dssm_plan {
       1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
       1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
       0,  // MEMCPY_NODES: diagnostics: data-parallel device copies as hipMemcpyAsync nodes
-      1,  // LAZY_ADAM: multi-step graphs: W1 rows nothing reads next step left behind, replayed exactly
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -370,11 +358,6 @@ struct dssm_plan {
     return on(DSSM_OPT_MERGED_CSC) && fused_stats() && csc_rank_path() && (Lt.BS % 128) == 0;
   }
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
-  // lazy W1 rows need the fused single-GPU step with its flat role (heavy items) and the merged
-  // transpose, whose SpMM launch marks the next batch
-  bool lazy_ok() const {
-    return on(DSSM_OPT_LAZY_ADAM) && fused_w1_adam() && heavy_in_adam() && merged_csc() && !gwire;
-  }
   bool fused_stats_ok() const {
     if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -695,21 +678,13 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     int* scat_row = det ? P->at<int>(Lt.sort_row) : P->at<int>(Lt.csc_row);
     float* scat_val = det ? P->at<float>(Lt.sort_val) : P->at<float>(Lt.csc_val);
     const dssm::BnSide b0 = P->bn_side(0);
-    // lazy W1 Adam: the next batch's columns marked in the BN1-sums launch (multi-step graphs)
-    dssm::LazyMark mark{};
-    P->lazy_marked = false;
-    if (merged && P->lazy_steps && P->lazy_next_indptr && P->lazy_ok()) {
-      mark = dssm::LazyMark{P->lazy_next_indptr, P->lazy_next_indices, Lt.R, P->at<unsigned>(Lt.lazy_flag),
-                            P->at<float>(Lt.adam_state), 64};
-      P->lazy_marked = true;
-    }
     if (merged)
       HIP_TRY(dssm::launch_sums_scatter(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], Lt.BS,
                                         P->at<double>(Lt.fsum[0]), P->indptr, P->indices, P->values,
                                         Lt.R, Lt.D, Lt.max_nnz, P->at<int>(Lt.csc_scratch),
                                         P->at<int>(Lt.col_ptr), scat_row, scat_val,
                                         nullptr, s, scat_cos ? &scat : nullptr,  // csc_col: unread on the rank path
-                                        det ? &b0.fdet : nullptr, &mark));
+                                        det ? &b0.fdet : nullptr));
     else
       HIP_TRY(dssm::launch_bn_sums(P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.n[0], tw,
                                    P->at<double>(Lt.fsum[0]), s, det ? &b0.fdet : nullptr));
@@ -1061,15 +1036,6 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   if (P->fused_w1_adam()) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
     fill_w1_roles(P, a);
-    if (P->lazy_steps && P->lazy_ok()) {  // lazy W1 rows (a step whose next batch is unmarked catches up)
-      a.pend = P->at<int>(Lt.lazy_pend);
-      a.lazy_flag = P->at<unsigned>(Lt.lazy_flag);
-      a.ring = P->at<float>(Lt.lazy_ring);
-      a.lazy = P->lazy_marked ? 1 : 0;
-    }
-  }
-  P->lazy_marked = false;
-  if (P->fused_w1_adam()) {
     a.d4_begin = rest / 4;
     if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
@@ -1233,7 +1199,6 @@ int dssm_plan_schedule(const dssm_plan* P) {
   if (fs && P->on(DSSM_OPT_DW_IN_APPLY)) f |= DSSM_SCHED_DW_IN_APPLY;
   if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
   if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;
-  if (P->lazy_ok()) f |= DSSM_SCHED_LAZY_ADAM;
   return f;
 }
 
@@ -1415,7 +1380,6 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     return fail(DSSM_E_HIP, std::string("hipStreamBeginCapture: ") + hipGetErrorString(e));
   }
   P->capturing = g;
-  P->lazy_steps = P->lazy_ok();  // lazy W1 rows inside the graph (its last step catches up)
   int rc = DSSM_OK;
   P->rank_done_for = nullptr;
   for (int i = 0; i < nsteps && !rc; ++i) {
@@ -1429,10 +1393,6 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
     P->indptr = indptrs[i];
     P->indices = indices[i];
     P->values = values[i];
-    // lazy W1 Adam: this step's SpMM marks step i+1's columns; the last step marks none, so its Adam
-    // brings every row up to date and nothing is left behind outside the graph
-    P->lazy_next_indptr = i + 1 < nsteps ? indptrs[i + 1] : nullptr;
-    P->lazy_next_indices = i + 1 < nsteps ? indices[i + 1] : nullptr;
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
     if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {  // step i+1's rank pass rides in this Adam
@@ -1443,9 +1403,6 @@ int dssm_plan_graph_build_steps(dssm_plan* P, const int32_t* const* indptrs,
   }
   P->host_rank_indptr = P->host_rank_indices = nullptr;
   P->rank_done_for = nullptr;
-  P->lazy_steps = false;
-  P->lazy_next_indptr = P->lazy_next_indices = nullptr;
-  P->lazy_marked = false;
   g->probes = with_probes != 0;
   g->probe_mask = ~0u;
   P->capturing = nullptr;

@@ -620,24 +620,14 @@ __global__ __launch_bounds__(256) void k_sums_scatter(const float* __restrict__ 
                                                       int* __restrict__ cnt,
                                                       int* __restrict__ csc_row,
                                                       float* __restrict__ csc_val,
-                                                      int* __restrict__ csc_col, DetAcc det,
-                                                      LazyMark mark) {
+                                                      int* __restrict__ csc_col, DetAcc det) {
   __shared__ double s_red[2][4][64];
   const int b = blockIdx.x;
-  const int nscat = (int)gridDim.x - nsum - mark.nblocks;
-  if (b < nsum) {
+  if (b < nsum)
     bn_sums_block<256>(Z, ldz, ncol, row_split, rows, fsum, b % nsum_x, b / nsum_x, s_red, det, nsum / nsum_x);
-  } else if (b < nsum + nscat) {
+  else
     scatter_rows(indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt, csc_row, csc_val,
-                 csc_col, b - nsum, nscat);
-  } else {
-    // lazy W1 Adam: the NEXT batch's columns marked (flag = the lazy-step counter + 1): scattered
-    // 4-B stores into a 120 KB array, on CUs the BN sums leave idle
-    const unsigned tag = reinterpret_cast<const unsigned*>(mark.st)[3] + 1u;
-    const int nnz = mark.indptr[mark.rows];
-    for (int k = (b - nsum - nscat) * 256 + (int)threadIdx.x; k < nnz; k += mark.nblocks * 256)
-      mark.flag[mark.indices[k]] = tag;
-  }
+                 csc_col, b - nsum, (int)gridDim.x - nsum);
 }
 
 // Fallback fill with per-entry global atomics (one wave per row).
@@ -1056,7 +1046,7 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,
                                float* csc_val, int* csc_col, hipStream_t s, CscScatter* scatter_out,
-                               const DetAcc* det, const LazyMark* mark) {
+                               const DetAcc* det) {
   (void)max_nnz;
   if (row_split % kSumsRows) return hipErrorInvalidValue;
   int* cnt = scratch;
@@ -1068,10 +1058,9 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
     *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                               csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
   }
-  const LazyMark mk = mark ? *mark : LazyMark{};
-  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4)) + mk.nblocks), dim3(256), 0, s,
-                     Z, ldz, n, row_split, fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr,
-                     pos_tmp, cnt, csc_row, csc_val, csc_col, det ? *det : DetAcc{}, mk);
+  hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n,
+                     row_split, fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
+                     csc_row, csc_val, csc_col, det ? *det : DetAcc{});
   return hipGetLastError();
 }
 

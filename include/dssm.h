@@ -147,13 +147,7 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *                      step's forward skips the rank launch
  *   MEMCPY_NODES    0; 1 (diagnostics): the data-parallel graph's device copies (the all-to-all's own
  *                      chunk, the copy rehearsal) as hipMemcpyAsync -- memcpy nodes in a capture --
- *                      instead of the copy kernel
- *   LAZY_ADAM       1: in multi-step graphs (with FUSED_W1_ADAM, HEAVY_IN_ADAM, MERGED_CSC) a W1 row
- *                      with no entry in this step's batch nor the next one is left behind and its
- *                      zero-gradient steps are replayed exactly (same arithmetic, same order) when a
- *                      batch next reads it, after at most 16 steps, and by the graph's last step:
- *                      parameters and Adam slots equal dense ApplyAdam's bit for bit whenever the
- *                      caller can see them */
+ *                      instead of the copy kernel */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -166,7 +160,6 @@ enum {
   DSSM_OPT_FUSED_W1_ADAM,
   DSSM_OPT_RANK_IN_ADAM,
   DSSM_OPT_MEMCPY_NODES,
-  DSSM_OPT_LAZY_ADAM,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);
@@ -266,8 +259,7 @@ enum {
   DSSM_SCHED_WHOLEK = 16,          /* layers >= 2 on the whole-K bf16 NT / backward-pair GEMMs */
   DSSM_SCHED_DW_IN_APPLY = 32,     /* dW_l split-K tiles inside the next BN-backward apply launch */
   DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
-  DSSM_SCHED_DETERMINISTIC = 128,  /* fixed-order reductions: bit-identical repeated runs */
-  DSSM_SCHED_LAZY_ADAM = 256       /* multi-step graphs: untouched W1 rows caught up lazily, exactly */
+  DSSM_SCHED_DETERMINISTIC = 128   /* fixed-order reductions: bit-identical repeated runs */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
 /* The fused-statistics train forward leaves the loss / accuracy reduction to the backward's first
