@@ -409,8 +409,10 @@ def bench_rnn(args):
 def bench_multiview(args):
     """BASELINE.json config 5 (archive/multi_view_dssm_v3.py): user tower + 3 item views (30k-wide
     sparse inputs, FC 300 -> 128, ReLU), in-batch rotated negatives, NEG=4, BS=4096 on one GPU,
-    fp32, synthetic Zipf trigram rows; the active view cycles 1, 2, 3 over the staged batches.
-    One step = forward + backward + Adam (user tower + active view).  Not the headline."""
+    synthetic Zipf trigram rows; the active view cycles 1, 2, 3 over the staged batches.  --dtype
+    bf16 (default: the perf mode, bf16 weight shadows / activations / MFMA, fp32 masters and Adam)
+    or fp32 (the parity mode, also timed as fp32_mode beside a bf16 line).  One step = forward +
+    backward + Adam (user tower + active view).  Not the headline."""
     import torch
     import torch.distributed as dist
     from dssm_amd.data import ZipfColumns, synth_rows
@@ -424,7 +426,7 @@ def bench_multiview(args):
     torch.cuda.set_device(dev)
     if world > 1:  # config 5 on N GPUs: BS users per rank, gradient all-reduce (weak scaling)
         dist.init_process_group(args.backend, device_id=dev if args.backend == "nccl" else None)
-    m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev)
+    m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev, dtype=args.dtype)
     m.init_params(0)
     dp = MultiViewDataParallel(m, comm=args.comm) if world > 1 else None
     cols = ZipfColumns(Dv)
@@ -524,13 +526,15 @@ def bench_multiview(args):
     m.lib.dssm_adam_probe(0)
     adam_ms = avg.value  # per launch
     tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
-    # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower
-    adam_bytes = int(28 * tower_params)
+    # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower; bf16
+    # mode: + 2 B per weight written to its shadow
+    shadow_elems = (Dv * L1 + L1 * L2) if args.dtype == "bf16" else 0
+    adam_bytes = int(28 * tower_params + 2 * shadow_elems)
     achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
     out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
            "value": round(world * B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 4),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
            "data": "synthetic",
            "config": {"workload": "multi_view_dssm_v3: user + 3 views (30k sparse -> 300 -> 128), in-batch "
                                   "rotated negatives, BS=4096 per GPU, NEG=4, fwd+bwd+Adam", "global_batch": B * world,
@@ -538,12 +542,16 @@ def bench_multiview(args):
                       "launch": ("hipgraph: one graph of K steps" if region is not None else "hipgraph") if args.graph else "eager",
                       "dp_exchange": dp.comm if dp is not None else None},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "adam",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel": "k_adam_flat_shadow" if args.dtype == "bf16" else "k_rnn_adam",
                         "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5), "launches": cnt.value},
            "final_loss": round(m.loss(), 3)}
-    t, src = model_profile("traffic", "multiview", "k_rnn_adam")
+    t, src = model_profile("traffic", "multiview" if args.dtype == "fp32" else "multiview_bf16",
+                           out["roofline"]["kernel"])
     if t is not None:
         out["roofline"].update(traffic=t["hbm_bytes"], traffic_source=src)
+    if args.dtype == "bf16" and args.fp32_line and rank == 0 and world == 1:
+        out["fp32_mode"] = child_mode_line(args, ["--model", "multiview", "--dtype", "fp32"])
     if dp is not None and args.dp_check:
         out["dp_check"] = dp_check(m, dp, dev)
     if args.cpu_baseline and rank == 0 and world == 1:

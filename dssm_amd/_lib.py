@@ -37,6 +37,11 @@ class DssmError(RuntimeError):
     pass
 
 
+class dssm_shadow_seg(C.Structure):
+    """include/dssm.h dssm_shadow_seg: a [rows x cols] weight block at p + offset and its bf16 shadow."""
+    _fields_ = [("offset", C.c_int64), ("rows", C.c_int64), ("cols", C.c_int), ("ld", C.c_int), ("ptr", C.c_void_p)]
+
+
 class dssm_config(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int), ("trigram_d", C.c_int), ("n_layers", C.c_int),
@@ -104,6 +109,8 @@ _SIGS = {
                                         C.c_int, C.c_int, _P]),
     "dssm_dense_fwd_act": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
                                      _P, C.c_int, C.c_int, _P]),
+    "dssm_spmm_csr_fwd_ex": (C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int,
+                                       C.c_int, C.c_int, _P]),
     "dssm_bn_ws_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "dssm_bn_relu_fwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float,
                                    C.c_float, C.c_int, C.c_int, _P, C.c_int, _P, _P, _P, _P]),
@@ -154,15 +161,21 @@ _SIGS = {
     "dssm_adam_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "dssm_rows_gather_sum": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_float, _P, C.c_int, _P,
                                        C.c_int, _P]),
+    "dssm_rows_gather_sum_ex": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, C.c_int, C.c_float, _P, C.c_int, _P,
+                                          C.c_int, C.c_int, _P]),
     "dssm_dense_bwd_slab_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int]),
     "dssm_dense_bwd": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
                                  _P, C.c_int, _P, _P, _P]),
     "dssm_dense_bwd_masked": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
                                         C.c_int, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
+    "dssm_dense_bwd_ex": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
+                                    _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P, _P, _P]),
     "dssm_bn_relu_bwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float, C.c_int, _P,
                                    C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,
                                  C.c_float, C.c_int, _P]),
+    "dssm_adam_step_shadow": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float,
+                                        _P, C.c_float, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_scatter_add": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P]),
     "dssm_relu": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P]),

@@ -595,6 +595,53 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
   }
 }
 
+// The functional optimizer step with bf16 shadows (dssm_adam_step_shadow: the multi-view model's bf16
+// mode): ApplyAdam over n4 float4 groups of a flat range, each updated weight also written as bf16 to
+// its block's shadow, so no separate refresh pass re-reads the parameters.  The range is < 2^31
+// elements (launcher), so a group's (row, column) in its block comes from 32-bit division (the
+// 64-bit form of write_shadow4 is a long software sequence per group: 43 -> 51 us measured).
+// One shadow segment's geometry held in registers across the grid-stride loop.
+struct Seg32 {
+  int off, end, cols, ld;
+  u16* ptr;
+};
+__device__ __forceinline__ void put_shadow4(const Seg32& g, int i, float4 v) {
+  const int rel = i - g.off;
+  const int r = rel / g.cols, c = rel - r * g.cols;
+  uint2 p;
+  p.x = pack2bf(v.x, v.y);
+  p.y = pack2bf(v.z, v.w);
+  *reinterpret_cast<uint2*>(g.ptr + (size_t)r * g.ld + c) = p;
+}
+__global__ __launch_bounds__(256) void k_adam_flat_shadow(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v, int64_t n4,
+                                                          const float* __restrict__ st, float lr, float b1c,
+                                                          float b2c, float eps, float gs, ShadowList sh) {
+  const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
+  // at most two segments (a [W1; b1] and a [W2; b2] block), their geometry in registers
+  Seg32 s0{0, 0, 1, 0, nullptr}, s1{0, 0, 1, 0, nullptr};
+  if (sh.count > 0) s0 = Seg32{(int)sh.seg[0].offset, (int)(sh.seg[0].offset + sh.seg[0].rows * sh.seg[0].cols),
+                               sh.seg[0].cols, sh.seg[0].ld, sh.seg[0].ptr};
+  if (sh.count > 1) s1 = Seg32{(int)sh.seg[1].offset, (int)(sh.seg[1].offset + sh.seg[1].rows * sh.seg[1].cols),
+                               sh.seg[1].cols, sh.seg[1].ld, sh.seg[1].ptr};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = ld_stream4(p + i * 4);
+    const float4 gg = *reinterpret_cast<const float4*>(g + i * 4);
+    float4 mm = ld_stream4(m + i * 4);
+    float4 vv = ld_stream4(v + i * 4);
+    adam1(pp.x, mm.x, vv.x, gg.x * gs, alpha, b1c, b2c, eps);
+    adam1(pp.y, mm.y, vv.y, gg.y * gs, alpha, b1c, b2c, eps);
+    adam1(pp.z, mm.z, vv.z, gg.z * gs, alpha, b1c, b2c, eps);
+    adam1(pp.w, mm.w, vv.w, gg.w * gs, alpha, b1c, b2c, eps);
+    st_stream4(p + i * 4, pp);
+    st_stream4(m + i * 4, mm);
+    st_stream4(v + i * 4, vv);
+    const int e = (int)(i * 4);
+    if (e >= s0.off && e < s0.end) put_shadow4(s0, e, pp);
+    else if (e >= s1.off && e < s1.end) put_shadow4(s1, e, pp);
+  }
+}
+
 // the wire's W1 rows from the materialised fp32 gradient (one 4-element group per thread)
 __global__ __launch_bounds__(256) void k_wire_pack(const float* __restrict__ g, u16* __restrict__ w,
                                                    int D, WireGeo geo) {
@@ -719,6 +766,19 @@ hipError_t launch_copy_bytes(void* dst, const void* src, size_t bytes, hipStream
   const size_t items = bytes / width;
   const int grid = (int)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, 2048));
   hipLaunchKernelGGL(k_copy_bytes, dim3(grid), dim3(256), 0, s, dst, src, bytes, width);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, int64_t n, const float* st,
+                                  float lr, float beta1, float beta2, float eps, float gs, ShadowList sh,
+                                  hipStream_t s) {
+  if (n % 4 || n >= (int64_t)1 << 31 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16)
+    return hipErrorInvalidValue;
+  if (sh.count > 2) return hipErrorInvalidValue;
+  for (int i = 0; i < sh.count; ++i)
+    if (sh.seg[i].offset % 4 || sh.seg[i].cols % 4 || sh.seg[i].ld % 4 || sh.seg[i].tptr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_adam_flat_shadow, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, m, v, n / 4, st, lr,
+                     1.0f - beta1, 1.0f - beta2, eps, gs, sh);
   return hipGetLastError();
 }
 

@@ -89,12 +89,19 @@ __device__ __forceinline__ void st8(T* d, const T (&x)[8]) {
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __restrict__ A,
                                               int lda, const T* __restrict__ B, int ldb,
-                                              float* __restrict__ C, int ldc,
+                                              void* __restrict__ Cv, int ldc,
                                               const float* __restrict__ bias, int ones_row,
                                               int k_per_split, int relu,
-                                              const float* __restrict__ mask, int ldmask) {
+                                              const void* __restrict__ maskv, int ldmask, int flags) {
   // relu (FWD): the layer's ReLU in the epilogue; mask (DA): dA zeroed where mask <= 0 (the ReLU
-  // backward through the layer's input activation, ReluGrad)
+  // backward through the layer's input activation, ReluGrad).  flags (FWD / DA): bit 0 = C stored
+  // as bf16 (RNE) instead of fp32, bit 1 = the mask is bf16 (the bf16 activation itself)
+  const bool c_bf16 = MODE != GEMM_DW && (flags & 1);
+  const bool mask_bf16 = (flags & 2) != 0;
+  auto mask_pos = [&](size_t o) {
+    return mask_bf16 ? bf2f(static_cast<const u16*>(maskv)[o]) > 0.f : static_cast<const float*>(maskv)[o] > 0.f;
+  };
+  const bool mask = maskv != nullptr;
   constexpr bool TA = (MODE == GEMM_DW);
   constexpr bool TB = (MODE == GEMM_DA);
   constexpr int BK = Cfg<T>::BK;
@@ -199,7 +206,7 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-              const bool k = m < M && n < N && mask[(size_t)m * ldmask + n] > 0.f;
+              const bool k = m < M && n < N && mask_pos((size_t)m * ldmask + n);
               keep_bits |= (k ? 1u : 0u) << ((i * 2 + j) * 4 + r);
             }
           }
@@ -250,8 +257,13 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
   }
 
   // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
-  float* out = C;
-  if constexpr (MODE == GEMM_DW) out = C + (size_t)tbz * M * ldc;  // this split's slab
+  float* out = static_cast<float*>(Cv);
+  if constexpr (MODE == GEMM_DW) out += (size_t)tbz * M * ldc;  // this split's slab
+  u16* out16 = static_cast<u16*>(Cv);
+  auto put = [&](size_t o, float x) {
+    if (c_bf16) out16[o] = f2bf(x);
+    else out[o] = x;
+  };
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -265,11 +277,11 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const T* __re
         if constexpr (MODE == GEMM_FWD) {
           float x = v + bcol[j];
           if (relu) x = fmaxf(x, 0.f);
-          if (n < ldc) out[(size_t)m * ldc + n] = (n < N) ? x : 0.f;
+          if (n < ldc) put((size_t)m * ldc + n, (n < N) ? x : 0.f);
         } else if constexpr (MODE == GEMM_DA) {
           const bool keep = n < N && (kbeg < kend ? ((keep_bits >> ((i * 2 + j) * 4 + r)) & 1u)
-                                                  : (!mask || mask[(size_t)m * ldmask + n] > 0.f));
-          if (n < ldc) out[(size_t)m * ldc + n] = keep ? v : 0.f;
+                                                  : (!mask || mask_pos((size_t)m * ldmask + n)));
+          if (n < ldc) put((size_t)m * ldc + n, keep ? v : 0.f);
         } else {
           if (n < N) out[(size_t)m * ldc + n] = v;
         }
@@ -1057,15 +1069,15 @@ int dw_splits(int M, int N, int K, int BK) {
 
 template <typename T>
 hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, const T* B, int ldb,
-                    float* C, int ldc, const float* bias, bool ones_row, float* slab,
-                    hipStream_t s, int* deferred_splits, int relu, const float* mask, int ldmask) {
+                    void* C, int ldc, const float* bias, bool ones_row, float* slab,
+                    hipStream_t s, int* deferred_splits, int relu, const void* mask, int ldmask, int flags) {
   dim3 block(256);
   constexpr int BK = Cfg<T>::BK;
   if (mode == GEMM_DW) {
     const int splits = dw_splits(M, N, K, BK);
     const int kps = cdiv(cdiv(K, splits), BK) * BK;
     dim3 grid(cdiv(N, BN), cdiv(M, BM), splits);
-    float* target = splits > 1 ? slab : C;
+    float* target = splits > 1 ? slab : static_cast<float*>(C);
     if constexpr (sizeof(T) == 2) {
       if ((lda % 8) == 0 && (ldb % 8) == 0)
         hipLaunchKernelGGL(k_gemm_tn, grid, block, 0, s,
@@ -1073,26 +1085,26 @@ hipError_t launch_t(GemmMode mode, int M, int N, int K, const T* A, int lda, con
                                     ones_row ? 1 : 0, kps});
       else
         hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb,
-                           target, ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0);
+                           target, ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0, 0);
     } else {
       hipLaunchKernelGGL((k_gemm<T, GEMM_DW>), grid, block, 0, s, M, N, K, A, lda, B, ldb, target,
-                         ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0);
+                         ldc, bias, ones_row ? 1 : 0, kps, 0, nullptr, 0, 0);
     }
     if (deferred_splits) *deferred_splits = splits > 1 ? splits : 0;
     if (splits > 1 && !deferred_splits) {
       const int64_t n = (int64_t)M * ldc;
       const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
-      hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), block, 0, s, slab, splits, n, C);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), block, 0, s, slab, splits, n, static_cast<float*>(C));
     }
   } else {
     dim3 grid(cdiv(ldc, BN), cdiv(M, BM), 1);
     const int kps = cdiv(K, BK) * BK;
     if (mode == GEMM_FWD)
       hipLaunchKernelGGL((k_gemm<T, GEMM_FWD>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C,
-                         ldc, bias, 0, kps, relu, nullptr, 0);
+                         ldc, bias, 0, kps, relu, nullptr, 0, flags);
     else
       hipLaunchKernelGGL((k_gemm<T, GEMM_DA>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C,
-                         ldc, bias, 0, kps, 0, mask, ldmask);
+                         ldc, bias, 0, kps, 0, mask, ldmask, flags);
   }
   return hipGetLastError();
 }
@@ -1251,14 +1263,14 @@ size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
 }
 
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
-                       const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
+                       const void* B, int ldb, void* C, int ldc, const float* bias, bool ones_row,
                        float* slab, hipStream_t s, int* deferred_splits, int relu,
-                       const float* mask, int ldmask) {
+                       const void* mask, int ldmask, int flags) {
   if (bf16)
     return launch_t<u16>(mode, M, N, K, (const u16*)A, lda, (const u16*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s, deferred_splits, relu, mask, ldmask);
+                         ones_row, slab, s, deferred_splits, relu, mask, ldmask, flags);
   return launch_t<float>(mode, M, N, K, (const float*)A, lda, (const float*)B, ldb, C, ldc, bias,
-                         ones_row, slab, s, deferred_splits, relu, mask, ldmask);
+                         ones_row, slab, s, deferred_splits, relu, mask, ldmask, flags);
 }
 
 }  // namespace dssm

@@ -32,7 +32,8 @@ int eval_coef_blocks(const EvalCoef& e);
 // eval_coef_blocks(*ec) extra workgroups write the eval BN coefficients.
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s, const EvalCoef* ec = nullptr, bool relu = false);
+                           int ldz, hipStream_t s, const EvalCoef* ec = nullptr, bool relu = false,
+                           bool z_bf16 = false);
 // CSR -> CSC transpose of X with a virtual all-ones column D appended (its dW row = db1).
 // scratch: csc_scratch_ints() ints, zero on first use (kept zero between calls);
 // col_ptr: int[D+2]; csc_*: capacity max_nnz + rows.
@@ -91,11 +92,13 @@ size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16);
 // DW : C[M x N] = A^T * B, A is [K x M] (ld lda) with a virtual ones row at m == M-1 when
 //      ones_row != 0; B is [K x N]; split-K over the K (rows) dimension into `slab`
 //      (gemm_dw_slab_floats) then a fixed-order reduce into C (ldc must equal N).
+// flags (FWD / DA): kGemmOutBf16 = C stored as bf16, kGemmMaskBf16 = the DA mask is bf16
+constexpr int kGemmOutBf16 = 1, kGemmMaskBf16 = 2;
 hipError_t launch_gemm(GemmMode mode, bool bf16, int M, int N, int K, const void* A, int lda,
-                       const void* B, int ldb, float* C, int ldc, const float* bias, bool ones_row,
+                       const void* B, int ldb, void* C, int ldc, const float* bias, bool ones_row,
                        float* slab, hipStream_t s,
-                       int* deferred_splits = nullptr, int relu = 0, const float* mask = nullptr,
-                       int ldmask = 0);
+                       int* deferred_splits = nullptr, int relu = 0, const void* mask = nullptr,
+                       int ldmask = 0, int flags = 0);
 
 // bf16 "NT" GEMM: C[M x ldc] = A . B + bias, B given k-contiguous as BT [N x ldb]
 // (BT[n][k] = B[k][n]).  bn_a: A = relu(Z*inv + shift) from fp32 Z [M x lda] with BN coefficients
@@ -318,6 +321,11 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 // a timing probe's event (plan.hip): hipEventRecord, or an event-record node while s is capturing
 void record_probe_event(hipStream_t s, hipEvent_t e);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
+// ApplyAdam over a flat range of n elements (n % 4 == 0, 16-B aligned) with each updated weight also
+// written to its bf16 shadow (sh: offsets relative to p; no transposed shadows)
+hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, int64_t n, const float* st,
+                                  float lr, float beta1, float beta2, float eps, float gs, ShadowList sh,
+                                  hipStream_t s);
 // bf16 wire helpers (data parallel): the wire's W1 rows = bf16(g) (rows [0, D) of row length
 // geo.n); the W1 shadow rows from the all-gathered bf16 parameter wire (chunk: that chunk's rows
 // only, -1: all)

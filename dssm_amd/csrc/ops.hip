@@ -130,9 +130,10 @@ __global__ void k_rows_scatter_add(const float* __restrict__ src, int lds, const
 
 // dst[r] = scale * sum of src rows idx[offs[r] .. offs[r+1]) in list order (the scatter-add's
 // inverse: fixed order, no atomics, no clearing pass); with mask, zero where mask[r] <= 0 (ReluGrad)
+template <typename TD>
 __global__ void k_rows_gather_sum(const float* __restrict__ src, int lds, const int* __restrict__ offs,
                                   const int* __restrict__ idx, int n, int cols, float scale,
-                                  const float* __restrict__ mask, int ldm, float* __restrict__ dst, int ldd) {
+                                  const float* __restrict__ mask, int ldm, TD* __restrict__ dst, int ldd) {
   const int64_t total = (int64_t)n * cols;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -141,7 +142,7 @@ __global__ void k_rows_gather_sum(const float* __restrict__ src, int lds, const 
     for (int j = offs[r]; j < offs[r + 1]; ++j) acc += src[(size_t)idx[j] * lds + c];
     acc *= scale;
     if (mask && !(mask[(size_t)r * ldm + c] > 0.f)) acc = 0.f;
-    dst[(size_t)r * ldd + c] = acc;
+    dst[(size_t)r * ldd + c] = from_f<TD>(acc);
   }
 }
 
@@ -193,13 +194,25 @@ int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, 
   return hip_status();
 }
 
+int dssm_rows_gather_sum_ex(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
+                            float scale, const float* mask, int ldm, void* dst, int dst_dtype, int ldd,
+                            void* stream) {
+  if (!src || !offs || !idx || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols || (mask && ldm < cols) ||
+      (dst_dtype != DSSM_F32 && dst_dtype != DSSM_BF16))
+    return oerr(DSSM_E_INVALID, "rows_gather_sum: bad argument");
+  if (dst_dtype == DSSM_BF16)
+    hipLaunchKernelGGL(k_rows_gather_sum<u16>, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, (hipStream_t)stream,
+                       src, lds, offs, idx, n, cols, scale, mask, ldm, static_cast<u16*>(dst), ldd);
+  else
+    hipLaunchKernelGGL(k_rows_gather_sum<float>, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0,
+                       (hipStream_t)stream, src, lds, offs, idx, n, cols, scale, mask, ldm, static_cast<float*>(dst),
+                       ldd);
+  return hip_status();
+}
+
 int dssm_rows_gather_sum(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
                          float scale, const float* mask, int ldm, float* dst, int ldd, void* stream) {
-  if (!src || !offs || !idx || !dst || n < 0 || cols < 0 || lds < cols || ldd < cols || (mask && ldm < cols))
-    return oerr(DSSM_E_INVALID, "rows_gather_sum: bad argument");
-  hipLaunchKernelGGL(k_rows_gather_sum, dim3(ew_grid((int64_t)n * cols)), dim3(256), 0, (hipStream_t)stream, src,
-                     lds, offs, idx, n, cols, scale, mask, ldm, dst, ldd);
-  return hip_status();
+  return dssm_rows_gather_sum_ex(src, lds, offs, idx, n, cols, scale, mask, ldm, dst, DSSM_F32, ldd, stream);
 }
 
 int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, void* stream) {
@@ -268,6 +281,29 @@ int dssm_csc_transpose(const int32_t* indptr, const int32_t* indices, const floa
 
 size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype) {
   return dssm::gemm_dw_slab_floats(K + 1, N, M, dtype == DSSM_BF16);
+}
+
+int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                      const void* dZ, int lddz, void* dA, int da_dtype, int ldda, const void* mask, int mask_dtype,
+                      int ldmask, float* dWb, float* slab, void* stream) {
+  if (!A || !W || !dZ || !dWb || M <= 0 || K <= 0 || N <= 0 || lda < K || ldw < N || lddz < N ||
+      (dA && ldda < K) || (dtype != DSSM_F32 && dtype != DSSM_BF16) || (lda % 4) || (ldw % 4) ||
+      (lddz % 4) || (mask && (!dA || ldmask < K)) || (da_dtype != DSSM_F32 && da_dtype != DSSM_BF16) ||
+      (mask_dtype != DSSM_F32 && mask_dtype != DSSM_BF16))
+    return oerr(DSSM_E_INVALID, "dense_bwd: bad argument");
+  if (dssm_dense_bwd_slab_floats(M, K, N, dtype) && !slab)
+    return oerr(DSSM_E_INVALID, "dense_bwd: this shape needs a split-K slab");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = dtype == DSSM_BF16;
+  const int flags = (da_dtype == DSSM_BF16 ? dssm::kGemmOutBf16 : 0) | (mask_dtype == DSSM_BF16 ? dssm::kGemmMaskBf16 : 0);
+  hipError_t e = hipSuccess;
+  if (dA)
+    e = dssm::launch_gemm(dssm::GEMM_DA, bf, M, K, N, dZ, lddz, W, ldw, dA, ldda, nullptr, false, nullptr,
+                          s, nullptr, 0, mask, ldmask, flags);
+  if (e == hipSuccess)
+    e = dssm::launch_gemm(dssm::GEMM_DW, bf, K + 1, N, M, A, lda, dZ, lddz, dWb, N, nullptr, true, slab, s,
+                          nullptr);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
 int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,

@@ -1467,6 +1467,22 @@ int dssm_spmm_csr_fwd_act(const int32_t* indptr, const int32_t* indices, const f
   return DSSM_OK;
 }
 
+int dssm_spmm_csr_fwd_ex(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                         const void* W, int w_dtype, int ldw, int n, const float* bias, void* Z, int z_dtype,
+                         int ldz, int act, void* stream) {
+  if (z_dtype == DSSM_F32)
+    return dssm_spmm_csr_fwd_act(indptr, indices, values, rows, W, w_dtype, ldw, n, bias, static_cast<float*>(Z),
+                                 ldz, act, stream);
+  if (!indptr || !W || !bias || !Z || rows < 0 || n < 4 || (n % 4) || ldz < n || (ldz % 8) ||
+      z_dtype != DSSM_BF16 || w_dtype != DSSM_BF16 || ldw < ldp8(n) || (ldw % 8) ||
+      (act != DSSM_ACT_NONE && act != DSSM_ACT_RELU))
+    return fail(DSSM_E_INVALID, "dssm_spmm_csr_fwd_ex: a bf16 output needs bf16 W (ldw >= round_up(n, 8), zero "
+                                "pads) and ldz % 8 == 0");
+  HIP_TRY(dssm::launch_spmm_fwd(indptr, indices, values, rows, W, true, ldw, n, bias, static_cast<float*>(Z), ldz,
+                                (hipStream_t)stream, nullptr, act == DSSM_ACT_RELU, true));
+  return DSSM_OK;
+}
+
 int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
                       const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
                       int ldz, void* stream) {

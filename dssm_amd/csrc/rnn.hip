@@ -496,6 +496,30 @@ extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int6
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
+extern "C" int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                                     float beta1, float beta2, float eps, float* state, float grad_scale,
+                                     int advance, const dssm_shadow_seg* segs, int nseg, void* stream) {
+  if (!p || !g || !m || !v || !state || n < 0 || nseg < 0 || nseg > 2 || (nseg && !segs))
+    return rerr(DSSM_E_INVALID, "adam_step_shadow: bad argument");
+  dssm::ShadowList sh{};
+  sh.count = nseg;
+  for (int i = 0; i < nseg; ++i) {
+    const dssm_shadow_seg& q = segs[i];
+    if (!q.ptr || q.offset < 0 || q.rows < 0 || q.cols <= 0 || q.ld < q.cols || q.offset + q.rows * q.cols > n)
+      return rerr(DSSM_E_INVALID, "adam_step_shadow: bad shadow segment");
+    sh.seg[i] = dssm::ShadowSeg{q.offset, q.rows, q.cols, q.ld, q.ptr, nullptr, 0};
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
+  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
+  hipError_t e = dssm::launch_adam_flat_shadow(p, g, m, v, n, state, lr, beta1, beta2, eps, grad_scale, sh, s);
+  if (e != hipSuccess) return rerr(DSSM_E_INVALID, "adam_step_shadow: n % 4, 16-B alignment, segment offsets");
+  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]);
+  if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
+  e = hipGetLastError();
+  return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
 extern "C" int dssm_adam_probe(int n_max) {
   for (hipEvent_t e : g_adam_probe.ev) (void)hipEventDestroy(e);
   g_adam_probe.ev.clear();

@@ -42,12 +42,12 @@ __device__ __forceinline__ void store8n(float* p, const float (&x)[8], int nvali
 
 namespace {
 
-template <typename TW>
+template <typename TW, typename TO = float>
 __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
                                           const int* __restrict__ indices,
                                           const float* __restrict__ values, int rows,
                                           const TW* __restrict__ W, int ldw, int n,
-                                          const float* __restrict__ bias, float* __restrict__ Z,
+                                          const float* __restrict__ bias, TO* __restrict__ Z,
                                           int ldz, int b, bool relu = false) {
   const int row = b * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= rows) return;
@@ -96,20 +96,21 @@ __device__ __forceinline__ void eval_coef_item(const EvalCoef& e, int i) {
   }
 }
 
-// blocks [0, ne): eval coefficients (first in dispatch order); the rest: one wave per CSR row
-template <typename TW>
+// blocks [0, ne): eval coefficients (first in dispatch order); the rest: one wave per CSR row.
+// TO: the output's storage (fp32, or bf16 RNE: the multi-view model's bf16 FC1 activation)
+template <typename TW, typename TO = float>
 __global__ __launch_bounds__(256) void k_spmm_fwd(const int* __restrict__ indptr,
                                                   const int* __restrict__ indices,
                                                   const float* __restrict__ values, int rows,
                                                   const TW* __restrict__ W, int ldw, int n,
                                                   const float* __restrict__ bias,
-                                                  float* __restrict__ Z, int ldz, EvalCoef ec,
+                                                  TO* __restrict__ Z, int ldz, EvalCoef ec,
                                                   int ne, int relu) {
   if ((int)blockIdx.x < ne) {
     eval_coef_item(ec, (int)blockIdx.x * 256 + threadIdx.x);
     return;
   }
-  spmm_rows<TW>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne, relu != 0);
+  spmm_rows<TW, TO>(indptr, indices, values, rows, W, ldw, n, bias, Z, ldz, (int)blockIdx.x - ne, relu != 0);
 }
 
 // ---- CSR -> CSC ------------------------------------------------------------------------------
@@ -999,12 +1000,18 @@ static bool bf16_rows_ok(int ldw, int n) {
 
 hipError_t launch_spmm_fwd(const int* indptr, const int* indices, const float* values, int rows,
                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z,
-                           int ldz, hipStream_t s, const EvalCoef* ec, bool relu) {
+                           int ldz, hipStream_t s, const EvalCoef* ec, bool relu, bool z_bf16) {
   EvalCoef e{};
   const int ne = ec ? eval_coef_blocks(*ec) : 0;
   if (ec) e = *ec;
   dim3 grid(ne + cdiv(rows, 4)), block(256);
   if (w_bf16 && !bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
+  if (z_bf16) {  // bf16 output (functional API: bf16 W, no eval coefficients)
+    if (!w_bf16 || ldw % 8 || ec || ldz % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_spmm_fwd<u16, u16>), grid, block, 0, s, indptr, indices, values, rows, (const u16*)W,
+                       ldw, n, bias, reinterpret_cast<u16*>(Z), ldz, e, ne, relu ? 1 : 0);
+    return hipGetLastError();
+  }
   if (w_bf16 && ldw % 8)  // the parameter wire's tight rows
     hipLaunchKernelGGL(k_spmm_fwd<u16t>, grid, block, 0, s, indptr, indices, values, rows,
                        (const u16t*)W, ldw, n, bias, Z, ldz, e, ne, relu ? 1 : 0);

@@ -12,8 +12,15 @@ dssm_spmm_csr_bwd_w (FC1), dssm_dense_fwd / dssm_dense_bwd (FC2) with the ReLUs 
 (dssm_spmm_csr_fwd_act / dssm_dense_fwd_act, dssm_dense_bwd_masked: FC1's ReLU backward on dA1),
 dssm_rows_gather_sum (the rotation's gradient x BS with FC2's ReLU backward),
 dssm_cosine_softmax_loss_mapped (the cosine kernel shared with the BoW path, reading the rotation's
-merged rows through an index map), dssm_adam_step.  fp32; torch tensors are
-device storage only.
+merged rows through an index map), dssm_adam_step.  Torch tensors are device storage only.
+
+Two modes, as the BoW model:
+* "fp32" (parity mode): fp32 weights, activations and the fp32 MFMA 16x16x4 GEMMs;
+* "bf16" (perf mode): FC1 gathers a bf16 shadow of W1 and stores its ReLU output bf16
+  (dssm_spmm_csr_fwd_ex), FC2 runs on bf16 MFMA 16x16x32 tiles with a bf16 shadow of W2, the
+  backward's dz2 / dz1 are bf16 (dssm_rows_gather_sum_ex, dssm_dense_bwd_ex) so the weight-gradient
+  gathers read half the bytes; master weights, gradients, Adam state, the embeddings, cosine and
+  loss stay fp32, and the optimizer rewrites the shadows as it updates (dssm_adam_step_shadow).
 
 The reference chooses the view with a Python comparison against a placeholder at graph build, so
 it always trains view 3; here the fed active view selects the tower.
@@ -43,8 +50,13 @@ def _ld(n):
 class MultiViewDSSM:
     def __init__(self, user_d: int, view_d: Sequence[int], l1: int, l2: int, bs: int, neg: int = 4,
                  lr: float = 0.05, gamma: float = 20.0, max_nnz_per_row: int = 96, device=None,
-                 rotations: Optional[Sequence[int]] = None, seed: int = 0):
+                 rotations: Optional[Sequence[int]] = None, seed: int = 0, dtype: str = "fp32"):
         self.lib = _lib.load()
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError("dtype: 'fp32' or 'bf16'")
+        self.dtype = dtype
+        self.bf16 = dtype == "bf16"
+        self._dt = _lib.DSSM_BF16 if self.bf16 else _lib.DSSM_F32
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if len(view_d) != 3 or l1 % 4 or l2 % 4:
             raise ValueError("three item views; l1, l2 multiples of 4")
@@ -70,13 +82,20 @@ class MultiViewDSSM:
         self.adam_v = torch.zeros(off, dtype=f32, device=dev)
         self.adam_state = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
         BS, R = self.bs, self.bs * (2 + self.neg)
-        self.a1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
+        act = torch.bfloat16 if self.bf16 else f32  # FC1's activation, dz2, dz1 (the MFMA operands)
+        self.a1 = {k: torch.zeros((BS, self.ld1), dtype=act, device=dev) for k in ("u", "i")}
         self.ysrc = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)   # [user_y; item_y]
-        self.dz2src = torch.zeros((2 * BS, self.ld2), dtype=f32, device=dev)  # FC2's dz, [user; item]
+        self.dz2src = torch.zeros((2 * BS, self.ld2), dtype=act, device=dev)  # FC2's dz, [user; item]
         self.dmerged = torch.zeros((R, self.ld2), dtype=f32, device=dev)
         # per-tower backward scratch: the two towers run concurrently (user tower on the caller's
         # stream, the item tower on self.aux)
-        self.dz1 = {k: torch.zeros((BS, self.ld1), dtype=f32, device=dev) for k in ("u", "i")}
+        self.dz1 = {k: torch.zeros((BS, self.ld1), dtype=act, device=dev) for k in ("u", "i")}
+        # bf16 mode: per tower the weight shadows the forward reads, [rows x ld] with zero pads
+        self.shadow = {}
+        if self.bf16:
+            for t, d in zip(TOWERS, self.dims):
+                self.shadow[f"{t}_1"] = torch.zeros((d, self.ld1), dtype=torch.bfloat16, device=dev)
+                self.shadow[f"{t}_2"] = torch.zeros((self.l1, self.ld2), dtype=torch.bfloat16, device=dev)
         K = self.neg + 1
         self.cos_raw = torch.zeros(K * BS, dtype=f32, device=dev)
         self.cos_sim = torch.zeros(BS * K, dtype=f32, device=dev)
@@ -84,7 +103,7 @@ class MultiViewDSSM:
         self.qnorm = torch.zeros(BS, dtype=f32, device=dev)
         self.loss_buf = torch.zeros(2, dtype=f32, device=dev)
         self.cos_ws = torch.zeros(2 * (-(-BS // 4)) + 64, dtype=f32, device=dev)
-        slab = max(self.lib.dssm_dense_bwd_slab_floats(BS, self.l1, self.l2, _lib.DSSM_F32), 1)
+        slab = max(self.lib.dssm_dense_bwd_slab_floats(BS, self.l1, self.l2, self._dt), 1)
         self.slab = {k: torch.zeros(int(slab), dtype=f32, device=dev) for k in ("u", "i")}
         self.aux = torch.cuda.Stream(device=dev)
         # one CSC-transpose workspace per tower (zero on first use, kept zero by the calls)
@@ -105,6 +124,14 @@ class MultiViewDSSM:
             for l in (1, 2):
                 blk = np.concatenate([p[f"{t}_W{l}"], p[f"{t}_b{l}"][None, :]], 0).astype(np.float32)
                 self._block(self.params, f"{t}_{l}").copy_(torch.from_numpy(blk))
+        self.sync_shadows()
+
+    def sync_shadows(self):
+        """bf16 mode: the weight shadows from the fp32 parameters (RNE, as the optimizer writes
+        them), after loading parameters; a setup step, not the training step."""
+        for name, sh in self.shadow.items():
+            w = self._block(self.params, name)[:-1]
+            sh[:, :w.shape[1]].copy_(w.to(torch.bfloat16))
 
     def named(self, arena: Optional[torch.Tensor] = None) -> Dict[str, np.ndarray]:
         a = self.params if arena is None else arena
@@ -174,11 +201,16 @@ class MultiViewDSSM:
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w1, w2 = self._block(self.params, f"{tower}_1"), self._block(self.params, f"{tower}_2")
-        # FC + ReLU in one launch each (the ReLU in the producers' epilogues)
-        check(self.lib.dssm_spmm_csr_fwd_act(ptr(ip), ptr(ix), ptr(vv), self.bs, ptr(w1), _lib.DSSM_F32, self.l1,
-                                             self.l1, ptr(w1[d]), ptr(self.a1[key]), self.ld1, _lib.DSSM_ACT_RELU, s),
-              "spmm_fwd")
-        check(self.lib.dssm_dense_fwd_act(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32, self.bs,
+        # FC + ReLU in one launch each (the ReLU in the producers' epilogues); bf16 mode: the weight
+        # shadows, FC1's activation stored bf16 for FC2's bf16 MFMA tiles
+        if self.bf16:
+            ws1, ws2, ld_w1, ld_w2 = self.shadow[f"{tower}_1"], self.shadow[f"{tower}_2"], self.ld1, self.ld2
+        else:
+            ws1, ws2, ld_w1, ld_w2 = w1, w2, self.l1, self.l2
+        check(self.lib.dssm_spmm_csr_fwd_ex(ptr(ip), ptr(ix), ptr(vv), self.bs, ptr(ws1), self._dt, ld_w1,
+                                            self.l1, ptr(w1[d]), ptr(self.a1[key]), self._dt, self.ld1,
+                                            _lib.DSSM_ACT_RELU, s), "spmm_fwd")
+        check(self.lib.dssm_dense_fwd_act(ptr(self.a1[key]), self.ld1, ptr(ws2), ld_w2, self._dt, self.bs,
                                           self.l1, self.l2, ptr(w2[self.l1]), ptr(y_rows), self.ld2,
                                           _lib.DSSM_ACT_RELU, s), "dense_fwd")
 
@@ -206,15 +238,17 @@ class MultiViewDSSM:
         ip, ix, vv = self.batch[key]
         d = self.dims[TOWERS.index(tower)]
         w2 = self._block(self.params, f"{tower}_2")
+        ws2, ld_w2 = (self.shadow[f"{tower}_2"], self.ld2) if self.bf16 else (w2, self.l2)
         dz1 = self.dz1[key]
-        # dA1 with FC1's ReLU backward fused (masked by a1 = relu(z1) > 0): dz1 directly
-        check(self.lib.dssm_dense_bwd_masked(ptr(self.a1[key]), self.ld1, ptr(w2), self.l2, _lib.DSSM_F32,
-                                             self.bs, self.l1, self.l2, ptr(dz2), self.ld2, ptr(dz1), self.ld1,
-                                             ptr(self.a1[key]), self.ld1,
-                                             ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
+        # dA1 with FC1's ReLU backward fused (masked by a1 = relu(z1) > 0): dz1 directly (bf16 mode:
+        # stored bf16, the operand of the weight gradient's gathers)
+        check(self.lib.dssm_dense_bwd_ex(ptr(self.a1[key]), self.ld1, ptr(ws2), ld_w2, self._dt,
+                                         self.bs, self.l1, self.l2, ptr(dz2), self.ld2, ptr(dz1), self._dt, self.ld1,
+                                         ptr(self.a1[key]), self._dt, self.ld1,
+                                         ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
               "dense_bwd")
         check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(dz1),
-                                           _lib.DSSM_F32, self.ld1, self.l1,
+                                           self._dt, self.ld1, self.l1,
                                            ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),
                                            s), "spmm_bwd")
 
@@ -225,9 +259,9 @@ class MultiViewDSSM:
         # the cosine kernel's d(mean loss)/dy x BS = d(summed loss)/dy (multi_view_dssm_v3.py:234)
         # Merge_Negative_Doc's gradient, the x BS and FC2's ReLU backward in one launch: dz2 of both
         # towers = BS * (sum of the merged rows each source row feeds) where y > 0
-        check(self.lib.dssm_rows_gather_sum(ptr(self.dmerged), self.ld2, ptr(self.inv_offs), ptr(self.inv_idx),
-                                            2 * BS, self.l2, float(BS), ptr(self.ysrc), self.ld2, ptr(self.dz2src),
-                                            self.ld2, s), "gather_sum")
+        check(self.lib.dssm_rows_gather_sum_ex(ptr(self.dmerged), self.ld2, ptr(self.inv_offs), ptr(self.inv_idx),
+                                               2 * BS, self.l2, float(BS), ptr(self.ysrc), self.ld2, ptr(self.dz2src),
+                                               self._dt, self.ld2, s), "gather_sum")
         self._fork(main)
         self._tower_bwd("u", "user", self.dz2src[:BS], s)
         self._tower_bwd("i", f"view{self.view}", self.dz2src[BS:], stream_ptr(self.aux))
@@ -237,12 +271,26 @@ class MultiViewDSSM:
         """Arena ranges the step updates: the user tower and the active view."""
         return [self.layout[t] for t in ("user", f"view{self.view}")]
 
+    def _shadow_segs(self, tower):
+        """bf16 mode: the tower's two weight blocks (offsets in its range) and their shadows."""
+        start = self.layout[tower][0]
+        segs = (_lib.dssm_shadow_seg * 2)()
+        for i, l in enumerate((1, 2)):
+            off, rows, cols = self.layout[f"{tower}_{l}"]
+            sh = self.shadow[f"{tower}_{l}"]
+            segs[i] = _lib.dssm_shadow_seg(off - start, rows - 1, cols, sh.shape[1], sh.data_ptr())
+        return segs
+
     def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
-        for k, (b, e) in enumerate(self.trained_ranges()):
-            check(self.lib.dssm_adam_step(ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]),
-                                          ptr(self.adam_v[b:e]), e - b, self.lr, 0.9, 0.999, 1e-8,
-                                          ptr(self.adam_state), grad_scale, k == 1, s), "adam")
+        for k, t in enumerate(("user", f"view{self.view}")):
+            b, e = self.layout[t]
+            args = (ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]), ptr(self.adam_v[b:e]), e - b,
+                    self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state), grad_scale, k == 1)
+            if self.bf16:  # the updated weights' bf16 shadows written by the same pass
+                check(self.lib.dssm_adam_step_shadow(*args, self._shadow_segs(t), 2, s), "adam")
+            else:
+                check(self.lib.dssm_adam_step(*args, s), "adam")
         self.global_step += 1
 
     def train_step(self, stream=None):

@@ -286,6 +286,12 @@ enum { DSSM_ACT_NONE = 0, DSSM_ACT_RELU = 1 };
 int dssm_spmm_csr_fwd_act(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
                           const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
                           int ldz, int act, void* stream);
+/* ... with the output's storage chosen: z_dtype DSSM_F32, or DSSM_BF16 (RNE of the fp32 row sums;
+ * needs bf16 W with ldw >= round_up(n, 8) and zero pads): the multi-view model's bf16 FC1
+ * activation, the next layer's bf16 MFMA operand. */
+int dssm_spmm_csr_fwd_ex(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
+                         const void* W, int w_dtype, int ldw, int n, const float* bias, void* Z, int z_dtype,
+                         int ldz, int act, void* stream);
 /* add_layer (archive/dssm_v3.py:44-53) on device: Z[M x ldz] = A[M x lda] . W[K x ldw] + bias,
  * inputs of dtype `dtype`, fp32 accumulate and output. */
 int dssm_dense_fwd(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
@@ -344,6 +350,11 @@ int dssm_dense_bwd(const void* A, int lda, const void* W, int ldw, int dtype, in
 int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                           const void* dZ, int lddz, float* dA, int ldda, const float* mask, int ldmask,
                           float* dWb, float* slab, void* stream);
+/* ... with dA stored as da_dtype (DSSM_F32, or DSSM_BF16: RNE) and the mask read as mask_dtype (the
+ * bf16 activation itself): the multi-view model's bf16 backward. */
+int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
+                      const void* dZ, int lddz, void* dA, int da_dtype, int ldda, const void* mask, int mask_dtype,
+                      int ldmask, float* dWb, float* slab, void* stream);
 /* batch_normalization + ReLU backward with batch statistics (new_dssm.py:62-88, :134-136; ReLU'(0) =
  * 0): from the forward's Z, gamma, beta and batch mean / biased variance (dssm_bn_relu_fwd's
  * batch_mean / batch_var), dout -> dz, dgamma, dbeta.  relu = 0: plain batch norm. */
@@ -356,6 +367,21 @@ int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamm
  * when advance != 0 (an optimizer step spanning several calls advances on its last one). */
 int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                    float beta2, float eps, float* state, float grad_scale, int advance, void* stream);
+/* The same step (float4 groups: n % 4 == 0, 16-B aligned arrays) also writing each updated weight of
+ * the given blocks (at most 2) as bf16 to its shadow: segment i covers elements [offset, offset + rows * cols)
+ * of p (row-major, rows x cols; a [W; b] block's W rows), shadow ptr [rows x ld] (ld >= cols,
+ * offset / cols / ld multiples of 4).  The bf16 weights the next forward reads, without a refresh
+ * pass over the parameters (the multi-view model's bf16 mode). */
+typedef struct dssm_shadow_seg {
+  int64_t offset;
+  int64_t rows;
+  int cols;
+  int ld;
+  uint16_t* ptr;
+} dssm_shadow_seg;
+int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                          float beta2, float eps, float* state, float grad_scale, int advance,
+                          const dssm_shadow_seg* segs, int nseg, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
  * averages the recorded launches (in a captured graph, each launch's latest replay). */
 int dssm_adam_probe(int n_max);
@@ -371,6 +397,10 @@ int dssm_rows_scatter_add(const float* src, int lds, const int32_t* map, int n, 
  * (ld ldm) the result is 0 where mask[r] <= 0 (the ReLU backward of the rows' forward output). */
 int dssm_rows_gather_sum(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
                          float scale, const float* mask, int ldm, float* dst, int ldd, void* stream);
+/* ... with dst stored as dst_dtype (DSSM_F32, or DSSM_BF16: RNE of the fp32 sum). */
+int dssm_rows_gather_sum_ex(const float* src, int lds, const int32_t* offs, const int32_t* idx, int n, int cols,
+                            float scale, const float* mask, int ldm, void* dst, int dst_dtype, int ldd,
+                            void* stream);
 /* tf.nn.relu and its gradient (ReluGrad: dx = y > 0 ? dy : 0); y may alias x. */
 int dssm_relu(const float* x, int ldx, int rows, int cols, float* y, int ldy, void* stream);
 int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, int cols, float* dx,

@@ -11,6 +11,10 @@
   get no gradient, which TF's minimize() skips.
 The reference picks the view with a Python comparison against a placeholder at graph build
 (always view 3); this restatement uses the fed active view, as intended.
+
+emulate="bf16" restates the bf16 perf mode of dssm_amd/multiview.py: the weight operands W1, W2
+(the shadows), FC1's ReLU output and the backward's dz2, dz1 rounded to bfloat16 (RNE) exactly where
+the kernels store them; everything else float64.
 """
 from __future__ import annotations
 
@@ -18,6 +22,8 @@ import dataclasses
 from typing import Dict, List
 
 import numpy as np
+
+from .dssm_oracle import bf16_round
 
 
 @dataclasses.dataclass
@@ -60,16 +66,22 @@ def _dense(csr, d):
     return X
 
 
-def tower(p, t, X):
-    z1 = X @ p[f"{t}_W1"] + p[f"{t}_b1"]
-    a1 = np.maximum(z1, 0)
-    z2 = a1 @ p[f"{t}_W2"] + p[f"{t}_b2"]
+def _rw(a, emulate):
+    return bf16_round(a) if emulate == "bf16" else a
+
+
+def tower(p, t, X, emulate=None):
+    z1 = X @ _rw(p[f"{t}_W1"], emulate) + p[f"{t}_b1"]
+    a1 = _rw(np.maximum(z1, 0), emulate)  # bf16 mode: FC1's activation is stored bf16
+    z2 = a1 @ _rw(p[f"{t}_W2"], emulate) + p[f"{t}_b2"]
     return {"X": X, "z1": z1, "a1": a1, "z2": z2, "y": np.maximum(z2, 0)}
 
 
-def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot, dtype=np.float64, sparse=False):
+def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot, dtype=np.float64, sparse=False,
+            emulate=None):
     """dtype float64 with dense X: the parity oracle.  float32 with sparse (scipy CSR) X: the CPU
-    baseline's restatement (bench.py --model multiview)."""
+    baseline's restatement (bench.py --model multiview).  emulate="bf16": the bf16 mode's rounding
+    points (module doc)."""
     p = {k: v.astype(dtype) for k, v in p.items()}
     dims = [cfg.user_d] + list(cfg.view_d)
     if sparse:
@@ -78,8 +90,8 @@ def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot, dtype=np.float
              for c, d in ((user_csr, dims[0]), (item_csr, dims[view]))]
     else:
         X = [_dense(user_csr, dims[0]), _dense(item_csr, dims[view])]
-    u = tower(p, "user", X[0])
-    it = tower(p, f"view{view}", X[1])
+    u = tower(p, "user", X[0], emulate)
+    it = tower(p, f"view{view}", X[1], emulate)
     BS, K = cfg.bs, cfg.neg + 1
     idx = np.empty((K, BS), np.int64)
     idx[0] = np.arange(BS)
@@ -92,7 +104,7 @@ def forward(cfg: MvConfig, p, user_csr, item_csr, view: int, rot, dtype=np.float
     e = np.exp(s - s.max(1, keepdims=True))
     prob = e / e.sum(1, keepdims=True)
     return {"u": u, "it": it, "idx": idx, "doc": doc, "qn": qn, "dn": dn, "cos": c, "prob": prob,
-            "loss": -np.sum(np.log(prob[:, 0])), "view": view}
+            "loss": -np.sum(np.log(prob[:, 0])), "view": view, "emulate": emulate}
 
 
 def backward(cfg: MvConfig, p, fw) -> Dict[str, np.ndarray]:
@@ -108,10 +120,11 @@ def backward(cfg: MvConfig, p, fw) -> Dict[str, np.ndarray]:
         dd = a * (yq / (qn[:, None] * dn[k][:, None]) - c[:, k][:, None] * doc[k] / dn[k][:, None] ** 2)
         np.add.at(dyi, fw["idx"][k], dd)
     grads = {}
+    em = fw.get("emulate")
     for t, tw, dy in (("user", fw["u"], dyq), (f"view{fw['view']}", fw["it"], dyi)):
-        dz2 = dy * (tw["z2"] > 0)
+        dz2 = _rw(dy * (tw["z2"] > 0), em)  # bf16 mode: the bf16 dz2 the dense backward reads
         grads[f"{t}_W2"], grads[f"{t}_b2"] = tw["a1"].T @ dz2, dz2.sum(0)
-        dz1 = (dz2 @ p[f"{t}_W2"].T) * (tw["z1"] > 0)
+        dz1 = _rw((dz2 @ _rw(p[f"{t}_W2"], em).T) * (tw["z1"] > 0), em)
         grads[f"{t}_W1"], grads[f"{t}_b1"] = np.asarray(tw["X"].T @ dz1), dz1.sum(0)
     return grads
 
