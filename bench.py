@@ -527,9 +527,10 @@ def bench_multiview(args):
     adam_ms = avg.value  # per launch
     tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
     # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower; bf16
-    # mode: + 2 B per weight written to its shadow
+    # mode: + 2 B per weight written to its shadow, and ONE launch updates both trained towers
     shadow_elems = (Dv * L1 + L1 * L2) if args.dtype == "bf16" else 0
-    adam_bytes = int(28 * tower_params + 2 * shadow_elems)
+    towers_per_launch = 2 if args.dtype == "bf16" else 1
+    adam_bytes = int(towers_per_launch * (28 * tower_params + 2 * shadow_elems))
     achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
     out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
            "value": round(world * B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": world,

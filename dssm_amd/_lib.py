@@ -174,7 +174,7 @@ _SIGS = {
                                    C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,
                                  C.c_float, C.c_int, _P]),
-    "dssm_adam_step_shadow": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float,
+    "dssm_adam_step_shadow": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float,
                                         _P, C.c_float, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_scatter_add": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P]),

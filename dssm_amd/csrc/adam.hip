@@ -614,17 +614,20 @@ __device__ __forceinline__ void put_shadow4(const Seg32& g, int i, float4 v) {
   *reinterpret_cast<uint2*>(g.ptr + (size_t)r * g.ld + c) = p;
 }
 __global__ __launch_bounds__(256) void k_adam_flat_shadow(float* __restrict__ p, const float* __restrict__ g,
-                                                          float* __restrict__ m, float* __restrict__ v, int64_t n4,
-                                                          const float* __restrict__ st, float lr, float b1c,
-                                                          float b2c, float eps, float gs, ShadowList sh) {
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          AdamRanges rg, const float* __restrict__ st, float lr,
+                                                          float b1c, float b2c, float eps, float gs, ShadowList sh) {
   const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
-  // at most two segments (a [W1; b1] and a [W2; b2] block), their geometry in registers
-  Seg32 s0{0, 0, 1, 0, nullptr}, s1{0, 0, 1, 0, nullptr};
-  if (sh.count > 0) s0 = Seg32{(int)sh.seg[0].offset, (int)(sh.seg[0].offset + sh.seg[0].rows * sh.seg[0].cols),
-                               sh.seg[0].cols, sh.seg[0].ld, sh.seg[0].ptr};
-  if (sh.count > 1) s1 = Seg32{(int)sh.seg[1].offset, (int)(sh.seg[1].offset + sh.seg[1].rows * sh.seg[1].cols),
-                               sh.seg[1].cols, sh.seg[1].ld, sh.seg[1].ptr};
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+  // at most four segments (a tower's [W1; b1] and [W2; b2] blocks, two towers), geometry in registers
+  Seg32 s4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    s4[k] = k < sh.count ? Seg32{(int)sh.seg[k].offset, (int)(sh.seg[k].offset + sh.seg[k].rows * sh.seg[k].cols),
+                                 sh.seg[k].cols, sh.seg[k].ld, sh.seg[k].ptr}
+                         : Seg32{0, 0, 1, 0, nullptr};
+  const int64_t n0 = rg.n4[0], nt = rg.n4[0] + rg.n4[1];
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nt; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = j < n0 ? rg.b4[0] + j : rg.b4[1] + (j - n0);
     float4 pp = ld_stream4(p + i * 4);
     const float4 gg = *reinterpret_cast<const float4*>(g + i * 4);
     float4 mm = ld_stream4(m + i * 4);
@@ -637,8 +640,12 @@ __global__ __launch_bounds__(256) void k_adam_flat_shadow(float* __restrict__ p,
     st_stream4(m + i * 4, mm);
     st_stream4(v + i * 4, vv);
     const int e = (int)(i * 4);
-    if (e >= s0.off && e < s0.end) put_shadow4(s0, e, pp);
-    else if (e >= s1.off && e < s1.end) put_shadow4(s1, e, pp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e >= s4[k].off && e < s4[k].end) {
+        put_shadow4(s4[k], e, pp);
+        break;
+      }
   }
 }
 
@@ -769,16 +776,20 @@ hipError_t launch_copy_bytes(void* dst, const void* src, size_t bytes, hipStream
   return hipGetLastError();
 }
 
-hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, int64_t n, const float* st,
+hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, AdamRanges rg, const float* st,
                                   float lr, float beta1, float beta2, float eps, float gs, ShadowList sh,
                                   hipStream_t s) {
-  if (n % 4 || n >= (int64_t)1 << 31 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16)
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 || sh.count > 4 || rg.nr < 1 || rg.nr > 2)
     return hipErrorInvalidValue;
-  if (sh.count > 2) return hipErrorInvalidValue;
+  if (rg.nr == 1) rg.n4[1] = 0;
+  for (int k = 0; k < rg.nr; ++k)
+    if (rg.b4[k] < 0 || rg.n4[k] < 0 || (rg.b4[k] + rg.n4[k]) * 4 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
   for (int i = 0; i < sh.count; ++i)
-    if (sh.seg[i].offset % 4 || sh.seg[i].cols % 4 || sh.seg[i].ld % 4 || sh.seg[i].tptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_adam_flat_shadow, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, m, v, n / 4, st, lr,
-                     1.0f - beta1, 1.0f - beta2, eps, gs, sh);
+    if (sh.seg[i].offset % 4 || sh.seg[i].cols % 4 || sh.seg[i].ld % 4 || sh.seg[i].tptr ||
+        sh.seg[i].offset + sh.seg[i].rows * sh.seg[i].cols >= ((int64_t)1 << 31))
+      return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_adam_flat_shadow, dim3(grid_for(rg.n4[0] + rg.n4[1])), dim3(256), 0, s, p, g, m, v, rg, st,
+                     lr, 1.0f - beta1, 1.0f - beta2, eps, gs, sh);
   return hipGetLastError();
 }
 

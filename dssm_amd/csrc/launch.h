@@ -321,9 +321,14 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
 // a timing probe's event (plan.hip): hipEventRecord, or an event-record node while s is capturing
 void record_probe_event(hipStream_t s, hipEvent_t e);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);
-// ApplyAdam over a flat range of n elements (n % 4 == 0, 16-B aligned) with each updated weight also
-// written to its bf16 shadow (sh: offsets relative to p; no transposed shadows)
-hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, int64_t n, const float* st,
+// ApplyAdam over one or two float4 ranges [b4, b4 + n4) of p (16-B aligned; element indices < 2^31)
+// in one launch, each updated weight of a shadow segment (<= 4; offsets in p, no transposed shadows)
+// also written as bf16 to its shadow
+struct AdamRanges {
+  int64_t b4[2], n4[2];
+  int nr;
+};
+hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v, AdamRanges rg, const float* st,
                                   float lr, float beta1, float beta2, float eps, float gs, ShadowList sh,
                                   hipStream_t s);
 // bf16 wire helpers (data parallel): the wire's W1 rows = bf16(g) (rows [0, D) of row length

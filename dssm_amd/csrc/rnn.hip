@@ -496,24 +496,32 @@ extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int6
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
-extern "C" int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr,
-                                     float beta1, float beta2, float eps, float* state, float grad_scale,
+extern "C" int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, const int64_t* ranges, int nr,
+                                     float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
                                      int advance, const dssm_shadow_seg* segs, int nseg, void* stream) {
-  if (!p || !g || !m || !v || !state || n < 0 || nseg < 0 || nseg > 2 || (nseg && !segs))
+  if (!p || !g || !m || !v || !state || !ranges || nr < 1 || nr > 2 || nseg < 0 || nseg > 4 || (nseg && !segs))
     return rerr(DSSM_E_INVALID, "adam_step_shadow: bad argument");
+  dssm::AdamRanges rg{};
+  rg.nr = nr;
+  for (int k = 0; k < nr; ++k) {
+    const int64_t b = ranges[2 * k], e = ranges[2 * k + 1];
+    if (b < 0 || e < b || b % 4 || e % 4) return rerr(DSSM_E_INVALID, "adam_step_shadow: ranges are 4-aligned");
+    rg.b4[k] = b / 4;
+    rg.n4[k] = (e - b) / 4;
+  }
   dssm::ShadowList sh{};
   sh.count = nseg;
   for (int i = 0; i < nseg; ++i) {
     const dssm_shadow_seg& q = segs[i];
-    if (!q.ptr || q.offset < 0 || q.rows < 0 || q.cols <= 0 || q.ld < q.cols || q.offset + q.rows * q.cols > n)
+    if (!q.ptr || q.offset < 0 || q.rows < 0 || q.cols <= 0 || q.ld < q.cols)
       return rerr(DSSM_E_INVALID, "adam_step_shadow: bad shadow segment");
     sh.seg[i] = dssm::ShadowSeg{q.offset, q.rows, q.cols, q.ld, q.ptr, nullptr, 0};
   }
   hipStream_t s = (hipStream_t)stream;
   const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
   if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
-  hipError_t e = dssm::launch_adam_flat_shadow(p, g, m, v, n, state, lr, beta1, beta2, eps, grad_scale, sh, s);
-  if (e != hipSuccess) return rerr(DSSM_E_INVALID, "adam_step_shadow: n % 4, 16-B alignment, segment offsets");
+  hipError_t e = dssm::launch_adam_flat_shadow(p, g, m, v, rg, state, lr, beta1, beta2, eps, grad_scale, sh, s);
+  if (e != hipSuccess) return rerr(DSSM_E_INVALID, "adam_step_shadow: 16-B alignment, segment offsets / widths");
   if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]);
   if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   e = hipGetLastError();

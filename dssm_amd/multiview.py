@@ -271,26 +271,26 @@ class MultiViewDSSM:
         """Arena ranges the step updates: the user tower and the active view."""
         return [self.layout[t] for t in ("user", f"view{self.view}")]
 
-    def _shadow_segs(self, tower):
-        """bf16 mode: the tower's two weight blocks (offsets in its range) and their shadows."""
-        start = self.layout[tower][0]
-        segs = (_lib.dssm_shadow_seg * 2)()
-        for i, l in enumerate((1, 2)):
-            off, rows, cols = self.layout[f"{tower}_{l}"]
-            sh = self.shadow[f"{tower}_{l}"]
-            segs[i] = _lib.dssm_shadow_seg(off - start, rows - 1, cols, sh.shape[1], sh.data_ptr())
-        return segs
-
     def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
-        for k, t in enumerate(("user", f"view{self.view}")):
-            b, e = self.layout[t]
-            args = (ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]), ptr(self.adam_v[b:e]), e - b,
-                    self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state), grad_scale, k == 1)
-            if self.bf16:  # the updated weights' bf16 shadows written by the same pass
-                check(self.lib.dssm_adam_step_shadow(*args, self._shadow_segs(t), 2, s), "adam")
-            else:
-                check(self.lib.dssm_adam_step(*args, s), "adam")
+        towers = ("user", f"view{self.view}")
+        if self.bf16:
+            # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass
+            rng = (C.c_int64 * 4)(*[x for t in towers for x in self.layout[t]])
+            segs = (_lib.dssm_shadow_seg * 4)()
+            for i, (t, l) in enumerate((t, l) for t in towers for l in (1, 2)):
+                off, rows, cols = self.layout[f"{t}_{l}"]
+                sh = self.shadow[f"{t}_{l}"]
+                segs[i] = _lib.dssm_shadow_seg(off, rows - 1, cols, sh.shape[1], sh.data_ptr())
+            check(self.lib.dssm_adam_step_shadow(ptr(self.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
+                                                 rng, 2, self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state), grad_scale,
+                                                 1, segs, 4, s), "adam")
+        else:
+            for k, t in enumerate(towers):
+                b, e = self.layout[t]
+                check(self.lib.dssm_adam_step(ptr(self.params[b:e]), ptr(self.grads[b:e]), ptr(self.adam_m[b:e]),
+                                              ptr(self.adam_v[b:e]), e - b, self.lr, 0.9, 0.999, 1e-8,
+                                              ptr(self.adam_state), grad_scale, k == 1, s), "adam")
         self.global_step += 1
 
     def train_step(self, stream=None):

@@ -367,11 +367,12 @@ int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamm
  * when advance != 0 (an optimizer step spanning several calls advances on its last one). */
 int dssm_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                    float beta2, float eps, float* state, float grad_scale, int advance, void* stream);
-/* The same step (float4 groups: n % 4 == 0, 16-B aligned arrays) also writing each updated weight of
- * the given blocks (at most 2) as bf16 to its shadow: segment i covers elements [offset, offset + rows * cols)
- * of p (row-major, rows x cols; a [W; b] block's W rows), shadow ptr [rows x ld] (ld >= cols,
- * offset / cols / ld multiples of 4).  The bf16 weights the next forward reads, without a refresh
- * pass over the parameters (the multi-view model's bf16 mode). */
+/* The same step over one or two ranges of the arrays in ONE launch (ranges = {begin0, end0[, begin1,
+ * end1]}: element offsets, multiples of 4; 16-B aligned arrays; indices < 2^31), also writing each updated
+ * weight of the given blocks (at most 4) as bf16 to its shadow: segment i covers elements [offset,
+ * offset + rows * cols) of p (row-major, rows x cols: a [W; b] block's W rows), shadow ptr [rows x ld]
+ * (ld >= cols; offset, cols, ld multiples of 4).  The bf16 weights the next forward reads, without a
+ * refresh pass over the parameters (the multi-view model's bf16 mode: both trained towers, one launch). */
 typedef struct dssm_shadow_seg {
   int64_t offset;
   int64_t rows;
@@ -379,8 +380,8 @@ typedef struct dssm_shadow_seg {
   int ld;
   uint16_t* ptr;
 } dssm_shadow_seg;
-int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
-                          float beta2, float eps, float* state, float grad_scale, int advance,
+int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, const int64_t* ranges, int nranges,
+                          float lr, float beta1, float beta2, float eps, float* state, float grad_scale, int advance,
                           const dssm_shadow_seg* segs, int nseg, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
  * averages the recorded launches (in a captured graph, each launch's latest replay). */

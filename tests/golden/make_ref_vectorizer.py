@@ -85,4 +85,8 @@ def main(ref_root: str) -> None:
 
 
 if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from _isolate import in_child, rerun_isolated
+    if not in_child():  # the reference's code runs only in a scrubbed, throwaway child (_isolate.py)
+        sys.exit(rerun_isolated(__file__, sys.argv[1:]))
     main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
