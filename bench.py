@@ -526,11 +526,24 @@ def bench_multiview(args):
     m.lib.dssm_adam_probe(0)
     adam_ms = avg.value  # per launch
     tower_params = sum(m.layout[t][1] - m.layout[t][0] for t in ("user", "view1")) / 2
-    # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower; bf16
-    # mode: + 2 B per weight written to its shadow, and ONE launch updates both trained towers
     shadow_elems = (Dv * L1 + L1 * L2) if args.dtype == "bf16" else 0
-    towers_per_launch = 2 if args.dtype == "bf16" else 1
-    adam_bytes = int(towers_per_launch * (28 * tower_params + 2 * shadow_elems))
+    if m.fused_w1_adam:
+        # one launch per trained tower (dssm_spmm_bwd_w_adam): p, m, v read + written (24 B) per
+        # parameter; [W1; b1]'s gradient gathered from the CSC transpose ((index, value) 8 B + one dz1
+        # row per entry, nnz + BS entries: the ones column), FC2's split-K partials read (4 B x splits);
+        # bf16: + 2 B per weight written to its shadow.  nnz: the staged batches' mean per tower.
+        nnz = float(np.mean([int(f[k][0][-1].item()) for f, _ in feeds for k in ("u", "i")]))
+        w2 = (L1 + 1) * L2
+        splits = max(1, m._splits["u"].value)
+        zb = 2 if args.dtype == "bf16" else 4
+        adam_bytes = int(24 * tower_params + 4 * splits * w2 + (nnz + B) * (8 + zb * L1) + 2 * shadow_elems)
+        adam_kernel = "k_adam_step<unsigned short, false>" if args.dtype == "bf16" else "k_adam_step<float, false>"
+    else:
+        # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower; bf16
+        # mode: + 2 B per weight written to its shadow, and ONE launch updates both trained towers
+        towers_per_launch = 2 if args.dtype == "bf16" else 1
+        adam_bytes = int(towers_per_launch * (28 * tower_params + 2 * shadow_elems))
+        adam_kernel = "k_adam_flat_shadow" if args.dtype == "bf16" else "k_rnn_adam"
     achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
     out = {"metric": "query-doc pairs/sec (fwd+bwd), multi-view DSSM (BASELINE config 5)",
            "value": round(world * B * (NEG + 1) * args.steps / el, 1), "unit": "pairs/s", "n_gpus": world,
@@ -544,7 +557,7 @@ def bench_multiview(args):
                       "dp_exchange": dp.comm if dp is not None else None},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                        "kernel": "k_adam_flat_shadow" if args.dtype == "bf16" else "k_rnn_adam",
+                        "kernel": adam_kernel,
                         "bytes_per_launch": adam_bytes, "avg_ms": round(adam_ms, 5), "launches": cnt.value},
            "final_loss": round(m.loss(), 3)}
     t, src = model_profile("traffic", "multiview" if args.dtype == "fp32" else "multiview_bf16",

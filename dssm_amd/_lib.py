@@ -169,13 +169,18 @@ _SIGS = {
     "dssm_dense_bwd_masked": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P,
                                         C.c_int, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_dense_bwd_ex": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int,
-                                    _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P, _P, _P]),
+                                    _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P, _P, _P, _P]),
     "dssm_bn_relu_bwd": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_float, C.c_int, _P,
                                    C.c_int, _P, C.c_int, _P, _P, _P]),
     "dssm_adam_step": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _P,
                                  C.c_float, C.c_int, _P]),
     "dssm_adam_step_shadow": (C.c_int, [_P, _P, _P, _P, _P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float,
                                         _P, C.c_float, C.c_int, _P, C.c_int, _P]),
+    "dssm_spmm_bwd_w_adam": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
+                                       _P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, C.c_int, _P, C.c_int,
+                                       _P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, _P, C.c_float,
+                                       _P, _P]),
+    "dssm_adam_advance": (C.c_int, [_P, C.c_float, C.c_float, _P]),
     "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_scatter_add": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P]),
     "dssm_relu": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P]),

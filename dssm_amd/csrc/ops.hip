@@ -17,6 +17,8 @@
 
 namespace dssm {
 int report_error(int code, const char* msg);
+bool adam_probe_begin(hipStream_t s);  // rnn.hip
+void adam_probe_end(hipStream_t s);
 }
 
 namespace {
@@ -285,7 +287,7 @@ size_t dssm_dense_bwd_slab_floats(int M, int K, int N, int dtype) {
 
 int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                       const void* dZ, int lddz, void* dA, int da_dtype, int ldda, const void* mask, int mask_dtype,
-                      int ldmask, float* dWb, float* slab, void* stream) {
+                      int ldmask, float* dWb, float* slab, int* deferred_splits, void* stream) {
   if (!A || !W || !dZ || !dWb || M <= 0 || K <= 0 || N <= 0 || lda < K || ldw < N || lddz < N ||
       (dA && ldda < K) || (dtype != DSSM_F32 && dtype != DSSM_BF16) || (lda % 4) || (ldw % 4) ||
       (lddz % 4) || (mask && (!dA || ldmask < K)) || (da_dtype != DSSM_F32 && da_dtype != DSSM_BF16) ||
@@ -302,7 +304,82 @@ int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype,
                           s, nullptr, 0, mask, ldmask, flags);
   if (e == hipSuccess)
     e = dssm::launch_gemm(dssm::GEMM_DW, bf, K + 1, N, M, A, lda, dZ, lddz, dWb, N, nullptr, true, slab, s,
-                          nullptr);
+                          deferred_splits);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                         int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
+                         float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
+                         int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
+                         float lr, float beta1, float beta2, float eps, const float* state, float grad_scale,
+                         void* ws, void* stream) {
+  const int64_t w1_end = (int64_t)(D + 1) * n;
+  if (!indptr || !dZ || !p || !g || !m || !v || !state || !ws || rows <= 0 || D <= 0 || n <= 0 || (n % 4) ||
+      lddz < n || (lddz % 8) || (max_nnz && (!indices || !values)) || (dz_dtype != DSSM_F32 && dz_dtype != DSSM_BF16) ||
+      rest_begin % 4 || rest_end % 4 || rest_begin < w1_end || rest_end < rest_begin || splits < 0 ||
+      (splits && (!slab || slab_count <= 0 || slab_count % 4 || rest_begin + slab_count > rest_end)) ||
+      (w1_shadow && (ld_shadow < n || ld_shadow % 4)) || nseg < 0 || nseg > 4 || (nseg && !segs))
+    return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: bad argument");
+  if (!dssm::csc_rank_supported(D)) return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: D beyond the CSC rank path");
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+       reinterpret_cast<uintptr_t>(v)) % 16)
+    return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: arrays must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const SpmmWs w = spmm_ws(rows, D, max_nnz);
+  char* b = static_cast<char*>(ws);
+  int* scratch = reinterpret_cast<int*>(b + w.scratch);
+  int* col_ptr = reinterpret_cast<int*>(b + w.col_ptr);
+  int* crow = reinterpret_cast<int*>(b + w.row);
+  float* cval = reinterpret_cast<float*>(b + w.val);
+  int* ccol = reinterpret_cast<int*>(b + w.col);
+  hipError_t e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, crow, cval,
+                                        ccol, s, nullptr, 0, true, false);
+  if (e != hipSuccess) return oerr(DSSM_E_HIP, hipGetErrorString(e));
+  dssm::AdamStep a{};
+  a.p = p;
+  a.g = g;
+  a.m = m;
+  a.v = v;
+  a.st = const_cast<float*>(state);  // read only: no_advance
+  a.no_advance = 1;
+  a.lr = lr;
+  a.beta1 = beta1;
+  a.beta2 = beta2;
+  a.eps = eps;
+  a.gs = grad_scale;
+  a.w1_blocks = 1;  // sized by the launcher
+  a.D = D;
+  a.n = n;
+  a.col_ptr = col_ptr;
+  a.csc_row = crow;
+  a.csc_val = cval;
+  a.dZ = dZ;
+  a.lddz = lddz;
+  a.shadow = w1_shadow;
+  a.ldsh = ld_shadow;
+  a.item_blocks = dssm::kAdamItemBlocks;
+  a.heavy_n = dssm::csc_heavy_count(scratch, D, max_nnz);
+  a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
+  a.heavy_ticket = dssm::csc_heavy_tickets(scratch, D, rows, max_nnz);
+  a.d4_begin = rest_begin / 4;
+  a.d4_end = rest_end / 4;
+  a.clear_from = rest_end;  // the rest's gradient is rewritten by the next backward
+  a.sh.count = nseg;
+  for (int i = 0; i < nseg; ++i) {
+    const dssm_shadow_seg& q = segs[i];
+    if (!q.ptr || q.offset < rest_begin || q.rows < 0 || q.cols <= 0 || q.ld < q.cols || q.offset % 4 || q.cols % 4 ||
+        q.ld % 4 || q.offset + q.rows * q.cols > rest_end)
+      return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: bad shadow segment");
+    a.sh.seg[i] = dssm::ShadowSeg{q.offset, q.rows, q.cols, q.ld, q.ptr, nullptr, 0};
+  }
+  if (splits) {
+    a.slabs.count = 1;
+    a.slabs.seg[0] = dssm::SlabSeg{rest_begin, slab_count, splits, slab};
+  }
+  const bool probe = dssm::adam_probe_begin(s);
+  e = dssm::launch_adam_step(a, dz_dtype == DSSM_BF16, s);
+  if (probe) dssm::adam_probe_end(s);
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 

@@ -376,6 +376,17 @@ struct AdamProbe {
 } g_adam_probe;
 }  // namespace
 
+namespace dssm {
+// the optimizer-launch probe (dssm_adam_probe): an event before and after each probed launch on the
+// stream it runs on; adam_probe_begin says whether this launch is probed
+bool adam_probe_begin(hipStream_t s) {
+  const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
+  if (probe) record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
+  return probe;
+}
+void adam_probe_end(hipStream_t s) { record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]); }
+}  // namespace dssm
+
 extern "C" {
 
 size_t dssm_rnn_ws_floats(int R, int T, int E, int H) {
@@ -486,11 +497,10 @@ extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int6
   if (!p || !g || !m || !v || !state || n < 0) return rerr(DSSM_E_INVALID, "adam_step: bad argument");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-  const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
-  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
+  const bool probe = dssm::adam_probe_begin(s);
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, (int64_t)0, n, state, lr,
                      beta1, beta2, eps, grad_scale);
-  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]);
+  if (probe) dssm::adam_probe_end(s);
   if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
@@ -518,13 +528,19 @@ extern "C" int dssm_adam_step_shadow(float* p, const float* g, float* m, float* 
     sh.seg[i] = dssm::ShadowSeg{q.offset, q.rows, q.cols, q.ld, q.ptr, nullptr, 0};
   }
   hipStream_t s = (hipStream_t)stream;
-  const bool probe = g_adam_probe.used < (int)g_adam_probe.ev.size() / 2;
-  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used]);
+  const bool probe = dssm::adam_probe_begin(s);
   hipError_t e = dssm::launch_adam_flat_shadow(p, g, m, v, rg, state, lr, beta1, beta2, eps, grad_scale, sh, s);
   if (e != hipSuccess) return rerr(DSSM_E_INVALID, "adam_step_shadow: 16-B alignment, segment offsets / widths");
-  if (probe) dssm::record_probe_event(s, g_adam_probe.ev[2 * g_adam_probe.used++ + 1]);
+  if (probe) dssm::adam_probe_end(s);
   if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   e = hipGetLastError();
+  return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+extern "C" int dssm_adam_advance(float* state, float beta1, float beta2, void* stream) {
+  if (!state) return rerr(DSSM_E_INVALID, "adam_advance: bad argument");
+  hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, state, beta1, beta2);
+  const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 

@@ -50,7 +50,8 @@ def _ld(n):
 class MultiViewDSSM:
     def __init__(self, user_d: int, view_d: Sequence[int], l1: int, l2: int, bs: int, neg: int = 4,
                  lr: float = 0.05, gamma: float = 20.0, max_nnz_per_row: int = 96, device=None,
-                 rotations: Optional[Sequence[int]] = None, seed: int = 0, dtype: str = "fp32"):
+                 rotations: Optional[Sequence[int]] = None, seed: int = 0, dtype: str = "fp32",
+                 fused_w1_adam: bool = True):
         self.lib = _lib.load()
         if dtype not in ("fp32", "bf16"):
             raise ValueError("dtype: 'fp32' or 'bf16'")
@@ -111,8 +112,28 @@ class MultiViewDSSM:
                                        dtype=torch.uint8, device=dev) for t, d in zip(TOWERS, self.dims)}
         self.batch = {}
         self.view = 3
+        # FC2's split-K weight-gradient partials left for the fused optimizer (per tower key)
+        self._splits = {"u": C.c_int(0), "i": C.c_int(0)}
+        self._fused = False
+        self.fused_w1_adam = fused_w1_adam
         self.set_rotations(rotations if rotations is not None else self.default_rotations(seed))
         self.global_step = 0
+
+    @property
+    def fused_w1_adam(self) -> bool:
+        """One GPU: each trained tower's FC1 weight gradient is never stored -- apply_adam's
+        dssm_spmm_bwd_w_adam gathers it inside the optimizer launch from the batch's CSC transpose
+        and dz1 (the BoW plan's fused W1 Adam), and FC2's split-K partials are summed there too.
+        backward() then leaves the towers' gradients unmaterialised (W1 rows zero).  Off: backward()
+        writes the whole gradient arena (data parallel: the all-reduce needs it)."""
+        return self._fused
+
+    @fused_w1_adam.setter
+    def fused_w1_adam(self, on: bool):
+        on = bool(on)
+        if on and not self._fused:
+            self.grads.zero_()  # the fused launch's heavy W1 rows accumulate into zeroed rows
+        self._fused = on
 
     # ---- parameters ---------------------------------------------------------------------------
     def _block(self, arena, name):
@@ -245,8 +266,11 @@ class MultiViewDSSM:
         check(self.lib.dssm_dense_bwd_ex(ptr(self.a1[key]), self.ld1, ptr(ws2), ld_w2, self._dt,
                                          self.bs, self.l1, self.l2, ptr(dz2), self.ld2, ptr(dz1), self._dt, self.ld1,
                                          ptr(self.a1[key]), self._dt, self.ld1,
-                                         ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]), s),
+                                         ptr(self._block(self.grads, f"{tower}_2")), ptr(self.slab[key]),
+                                         C.byref(self._splits[key]) if self._fused else None, s),
               "dense_bwd")
+        if self._fused:
+            return  # FC1's weight gradient: inside the optimizer launch (apply_adam)
         check(self.lib.dssm_spmm_csr_bwd_w(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(dz1),
                                            self._dt, self.ld1, self.l1,
                                            ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),
@@ -271,10 +295,39 @@ class MultiViewDSSM:
         """Arena ranges the step updates: the user tower and the active view."""
         return [self.layout[t] for t in ("user", f"view{self.view}")]
 
+    def _tower_adam(self, key, tower, s, grad_scale):
+        """Fused mode: one tower's CSC transpose + ONE optimizer launch over its [W1; b1] rows (the
+        gradient gathered inline) and its [W2; b2] block (FC2's split-K partials summed inline)."""
+        ip, ix, vv = self.batch[key]
+        d = self.dims[TOWERS.index(tower)]
+        b, e = self.layout[tower]
+        off2 = self.layout[f"{tower}_2"][0] - b
+        segs, nseg, w1s, ld1 = None, 0, None, 0
+        if self.bf16:
+            sh2 = self.shadow[f"{tower}_2"]
+            segs = (_lib.dssm_shadow_seg * 1)(_lib.dssm_shadow_seg(off2, self.l1, self.l2, sh2.shape[1],
+                                                                  sh2.data_ptr()))
+            nseg, w1s, ld1 = 1, ptr(self.shadow[f"{tower}_1"]), self.ld1
+        splits = self._splits[key].value
+        check(self.lib.dssm_spmm_bwd_w_adam(ptr(ip), ptr(ix), ptr(vv), self.bs, d, self.max_nnz, ptr(self.dz1[key]),
+                                            self._dt, self.ld1, self.l1, ptr(self.params[b:]), ptr(self.grads[b:]),
+                                            ptr(self.adam_m[b:]), ptr(self.adam_v[b:]), off2, e - b,
+                                            ptr(self.slab[key]) if splits else None, (self.l1 + 1) * self.l2, splits,
+                                            w1s, ld1, segs, nseg, self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state),
+                                            grad_scale, ptr(self.spmm_ws[tower]), s), "spmm_bwd_w_adam")
+
     def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
         towers = ("user", f"view{self.view}")
-        if self.bf16:
+        if self._fused:
+            # the two towers' launches run concurrently (the item tower's on self.aux), then the
+            # beta powers advance once both have read them
+            main = self._fork(stream)
+            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale)
+            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale)
+            main.wait_stream(self.aux)
+            check(self.lib.dssm_adam_advance(ptr(self.adam_state), 0.9, 0.999, stream_ptr(main)), "adam_advance")
+        elif self.bf16:
             # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass
             rng = (C.c_int64 * 4)(*[x for t in towers for x in self.layout[t]])
             segs = (_lib.dssm_shadow_seg * 4)()
@@ -316,6 +369,8 @@ class MultiViewDataParallel:
         from .dist import SCHEDULE_OPS, select_transport
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        if self.world > 1:
+            model.fused_w1_adam = False  # the all-reduce sums the materialised gradients
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.tx = None
         self.fallbacks = []

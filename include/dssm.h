@@ -354,7 +354,9 @@ int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dt
  * bf16 activation itself): the multi-view model's bf16 backward. */
 int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                       const void* dZ, int lddz, void* dA, int da_dtype, int ldda, const void* mask, int mask_dtype,
-                      int ldmask, float* dWb, float* slab, void* stream);
+                      int ldmask, float* dWb, float* slab, int* deferred_splits, void* stream);
+/* (deferred_splits != NULL: when the weight gradient is split over K, the partials stay in slab
+ * [splits x (K+1) x N] for dssm_spmm_bwd_w_adam to sum, *deferred_splits = splits; 0: dWb written.) */
 /* batch_normalization + ReLU backward with batch statistics (new_dssm.py:62-88, :134-136; ReLU'(0) =
  * 0): from the forward's Z, gamma, beta and batch mean / biased variance (dssm_bn_relu_fwd's
  * batch_mean / batch_var), dout -> dz, dgamma, dbeta.  relu = 0: plain batch norm. */
@@ -383,6 +385,30 @@ typedef struct dssm_shadow_seg {
 int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, const int64_t* ranges, int nranges,
                           float lr, float beta1, float beta2, float eps, float* state, float grad_scale, int advance,
                           const dssm_shadow_seg* segs, int nseg, void* stream);
+/* One tower's FC1 weight gradient and optimizer step in one pass, the dense [dW1; db1] never stored
+ * (the training-step plan's fused single-GPU Adam as a functional op; replaces dssm_spmm_csr_bwd_w +
+ * that tower's dssm_adam_step_shadow): builds the batch's CSC transpose [X | 1]^T in ws, then ONE
+ * launch applies TF1.x ApplyAdam (new_dssm.py:215-217) to
+ *   - rows [0, D] of the tower's [W1; b1] block at p (row length n, n % 4 == 0): a touched row's
+ *     gradient gathered from the transpose and dZ [rows x lddz] (dz_dtype), the ones column (db1)
+ *     and any column with more than 64 entries as work items of 256 entries; an untouched row
+ *     decays (gradient 0);
+ *   - elements [rest_begin, rest_end) of p (multiples of 4): gradient g, or for
+ *     [rest_begin, rest_begin + slab_count) the sum of splits partials slab[k * slab_count + i]
+ *     (dssm_dense_bwd_ex's deferred split-K; splits == 0: g).
+ * g's rows [0, D] must be zero and are left zero (heavy columns' atomics target); gradient x
+ * grad_scale.  bf16: W1's rows also written to w1_shadow [D x ld_shadow] (NULL: none), the rest range
+ * to the shadow segments (offsets relative to p).  Does not advance the beta powers: call
+ * dssm_adam_advance once every trained block of the step is updated.  Needs the CSC rank path
+ * (D <= 36800). */
+int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                         int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
+                         float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
+                         int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
+                         float lr, float beta1, float beta2, float eps, const float* state, float grad_scale,
+                         void* ws, void* stream);
+/* TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (state on the device). */
+int dssm_adam_advance(float* state, float beta1, float beta2, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
  * averages the recorded launches (in a captured graph, each launch's latest replay). */
 int dssm_adam_probe(int n_max);

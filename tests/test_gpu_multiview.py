@@ -1,7 +1,10 @@
 """Multi-view DSSM (dssm_amd/multiview.py, functional C-ABI) against the float64 oracle on the same
 seeded inputs: loss (rel 1e-5), cosines, every gradient of the user tower and the active view
 (<= 1e-4 * max|g|; the other views get none), teacher-forced Adam (<= 2 lr everywhere, 1e-6 on
-well-conditioned elements), and a short training run."""
+well-conditioned elements), and a short training run.  The fused optimizer (fused_w1_adam: each
+tower's FC1 weight gradient gathered inside its Adam launch, FC2's split-K partials summed there) is
+checked against the oracle's Adam on the materialised gradients of the unfused path, fp32 and bf16,
+at a batch whose ones column and head trigrams span several 256-entry work items."""
 import numpy as np
 import pytest
 import torch
@@ -13,11 +16,12 @@ from oracle import multiview_oracle as M
 pytestmark = pytest.mark.gpu
 
 
-def _setup(view):
-    cfg = M.MvConfig(user_d=3000, view_d=[2000, 2500, 1500], l1=64, l2=32, bs=64, neg=4, lr=0.01)
+def _setup(view, bs=64, fused=False, dtype="fp32"):
+    cfg = M.MvConfig(user_d=3000, view_d=[2000, 2500, 1500], l1=64, l2=32, bs=bs, neg=4, lr=0.01)
     p = M.init_params(cfg, 1)
     rot = M.rotations(cfg, 3)
-    m = MultiViewDSSM(cfg.user_d, cfg.view_d, cfg.l1, cfg.l2, cfg.bs, cfg.neg, lr=cfg.lr, rotations=rot)
+    m = MultiViewDSSM(cfg.user_d, cfg.view_d, cfg.l1, cfg.l2, cfg.bs, cfg.neg, lr=cfg.lr, rotations=rot,
+                      fused_w1_adam=fused, dtype=dtype)
     m.load_params(p)
     rng = np.random.Generator(np.random.PCG64(view))
     u = synth_rows(rng, ZipfColumns(cfg.user_d), cfg.bs, 16.0)
@@ -68,3 +72,44 @@ def test_multiview_adam_and_training():
         m.train_step()
         losses.append(m.loss())
     assert np.isfinite(losses).all() and losses[-1] < losses[0], losses[::5]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_multiview_fused_w1_adam(dtype):
+    """One step with the fused optimizer vs the oracle's ApplyAdam on the unfused path's gradients
+    (same params, batch and dtype): <= 2 lr everywhere, <= 1e-6 on well-conditioned elements,
+    untrained views unchanged, the W1 gradient rows left zero, bf16 shadows = bf16(weights); then a
+    short fused training run."""
+    cfg, p, rot, ref, u, it = _setup(2, bs=512, fused=False, dtype=dtype)
+    _, _, _, m, _, _ = _setup(2, bs=512, fused=True, dtype=dtype)
+    for x in (ref, m):
+        x.forward()
+        x.backward()
+    torch.cuda.synchronize()
+    assert abs(m.loss() - ref.loss()) <= 1e-6 * abs(ref.loss())
+    g = {k: v for k, v in ref.named(ref.grads).items() if k.startswith(("user", "view2"))}
+    pref = {k: v.copy() for k, v in p.items()}
+    M.Adam(cfg, pref).step(pref, g)
+    m.apply_adam()
+    torch.cuda.synchronize()
+    got = m.named()
+    for k in pref:
+        d = np.abs(got[k] - pref[k])
+        assert d.max() <= 2 * cfg.lr, (k, d.max())
+        if k in g:
+            well = np.abs(g[k]) > 1e-3 * np.abs(g[k]).max()
+            assert d[well].max(initial=0.0) <= 1e-6, (k, d[well].max(initial=0.0))
+        else:
+            assert d.max() == 0.0, k
+    for t in TOWERS:  # heavy columns' atomics target: consumed and cleared
+        assert not torch.any(m._block(m.grads, f"{t}_1")), t
+    assert np.allclose(m.adam_state.cpu().numpy(), [0.9 ** 2, 0.999 ** 2], rtol=1e-6)
+    if dtype == "bf16":
+        for name, sh in m.shadow.items():
+            w = m._block(m.params, name)[:-1]
+            assert torch.equal(sh[:, :w.shape[1]], w.to(torch.bfloat16)), name
+    losses = []
+    for _ in range(10):
+        m.train_step()
+        losses.append(m.loss())
+    assert np.isfinite(losses).all() and losses[-1] < losses[0], losses[::3]

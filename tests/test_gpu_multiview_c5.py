@@ -15,7 +15,9 @@ The bf16 perf mode (bf16 W shadows, bf16 FC1 activation, bf16 dz2 / dz1, MFMA 16
 against the bf16-emulating oracle (emulate="bf16": the same rounding points, float64 elsewhere):
 loss rel <= 1e-4 (the north star's bar), cosines <= 1e-3 abs, every gradient ||err|| <= 5e-3 ||g||
 (rounding-boundary flips of bf16 values, RNE ties); the optimizer's shadows equal bf16(weights) bit for
-bit after a step and the untrained views' shadows are untouched."""
+bit after a step and the untrained views' shadows are untouched.  The fused optimizer (the bench's
+default: FC1's weight gradient gathered inside each tower's Adam launch, FC2's split-K partials summed
+there) against the oracle's ApplyAdam on the unfused path's gradients, both dtypes."""
 import numpy as np
 import pytest
 import torch
@@ -29,12 +31,12 @@ pytestmark = pytest.mark.gpu
 CFG = M.MvConfig(user_d=30000, view_d=[30000, 30000, 30000], l1=300, l2=128, bs=4096, neg=4, lr=0.05)
 
 
-def _setup(view, dtype="fp32"):
+def _setup(view, dtype="fp32", fused=False):
     cfg = CFG
     p = M.init_params(cfg, 5)
     rot = M.rotations(cfg, 7)
     m = MultiViewDSSM(cfg.user_d, cfg.view_d, cfg.l1, cfg.l2, cfg.bs, cfg.neg, lr=cfg.lr, rotations=rot,
-                      dtype=dtype)
+                      dtype=dtype, fused_w1_adam=fused)
     m.load_params(p)
     rng = np.random.Generator(np.random.PCG64(40 + view))
     u = synth_rows(rng, ZipfColumns(cfg.user_d), cfg.bs, 32.0)
@@ -135,3 +137,34 @@ def test_multiview_config5_bf16_matches_emulating_oracle(view):
             assert not torch.any(sh[:, w.shape[1]:].float()), name  # zero pads kept
         else:
             assert torch.equal(sh, sh0[name]), name
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_multiview_config5_fused_w1_adam(dtype):
+    cfg, p, rot, ref, u, it = _setup(3, dtype, fused=False)
+    _, _, _, m, _, _ = _setup(3, dtype, fused=True)
+    for x in (ref, m):
+        x.forward()
+        x.backward()
+    torch.cuda.synchronize()
+    assert m._splits["u"].value > 1 and m._splits["i"].value > 1  # FC2's partials summed by the optimizer
+    g = {k: v for k, v in ref.named(ref.grads).items() if k.startswith(("user", "view3"))}
+    pref = {k: v.copy() for k, v in p.items()}
+    M.Adam(cfg, pref).step(pref, g)
+    m.apply_adam()
+    torch.cuda.synchronize()
+    after = m.named()
+    for k in pref:
+        d = np.abs(after[k] - pref[k])
+        assert d.max() <= 2 * cfg.lr, (k, d.max())
+        if k in g:
+            well = np.abs(g[k]) > 1e-3 * np.abs(g[k]).max()
+            assert d[well].max(initial=0.0) <= 1e-6, (k, d[well].max(initial=0.0))
+        else:
+            assert d.max() == 0.0, k
+    for t in ("user", "view1", "view2", "view3"):
+        assert not torch.any(m._block(m.grads, f"{t}_1")), t
+    if dtype == "bf16":
+        for name, sh in m.shadow.items():
+            w = m._block(m.params, name)[:-1]
+            assert torch.equal(sh[:, :w.shape[1]], w.to(torch.bfloat16)), name

@@ -35,7 +35,7 @@ def _batch(cfg, rank):
 def _model(cfg):
     from dssm_amd.multiview import MultiViewDSSM
     m = MultiViewDSSM(cfg["user_d"], cfg["view_d"], cfg["l1"], cfg["l2"], cfg["bs"], cfg["neg"], lr=0.01,
-                      device=torch.device("cuda", 0))
+                      device=torch.device("cuda", 0), fused_w1_adam=False)
     m.init_params(4)
     return m
 
