@@ -179,7 +179,9 @@ _SIGS = {
     "dssm_spmm_bwd_w_adam": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                        _P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, C.c_int, _P, C.c_int,
                                        _P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, _P, C.c_float,
-                                       _P, _P]),
+                                       C.c_int, C.c_int, _P, _P, _P]),
+    "dssm_adam_tickets_bytes": (C.c_size_t, [C.c_int]),
+    "dssm_adam_probe_span": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "dssm_adam_advance": (C.c_int, [_P, C.c_float, C.c_float, _P]),
     "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
     "dssm_rows_scatter_add": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, _P]),

@@ -565,10 +565,21 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       const unsigned u =
           __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (u == ntop - 1) {
-        a.st[0] = b1p * a.beta1;
-        a.st[1] = b2p * a.beta2;
         if (a.heavy_reset) *a.heavy_reset = 0;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a step of group_n launches (possibly concurrent, on other streams): the last launch to
+        // finish advances (each launch's blocks have read the powers before they arrived)
+        bool adv = true;
+        if (a.group_ticket) {
+          const unsigned g =
+              __hip_atomic_fetch_add(a.group_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          adv = g == (unsigned)a.group_n - 1;
+          if (adv) __hip_atomic_store(a.group_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (adv) {
+          a.st[0] = b1p * a.beta1;
+          a.st[1] = b2p * a.beta2;
+        }
       }
     }
   }
@@ -708,6 +719,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (a.w1_blocks > 0) a.w1_blocks = std::min(cdiv(w1_rows, 4), kAdamW1Blocks);
   if (a.gout || a.no_advance) a.ticket = nullptr;  // the gradient pass / a non-final chunk advance nothing
   if (!a.ticket && !a.gout && !a.no_advance) return hipErrorInvalidValue;  // a step advances the beta powers
+  if (a.group_ticket && (!a.ticket || a.group_n < 1)) return hipErrorInvalidValue;
   if (a.wchunk >= 0 && (!a.gout || !a.geo.ww || a.wchunk >= a.geo.wp)) return hipErrorInvalidValue;
   if (a.slab_to_g && (!a.gout || a.d4_end != a.d4_begin)) return hipErrorInvalidValue;  // gradient pass only
   if (a.w1_blocks == 0 || !a.heavy_items) a.item_blocks = 0;

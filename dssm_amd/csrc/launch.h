@@ -312,6 +312,9 @@ struct AdamStep {
   int wchunk = -1;     // gradient pass: only the rows of this chunk (-1: every row)
   int64_t pwire_off4;  // the dense range's parameter-wire float4 index = i + pwire_off4
   int no_advance;      // a chunk of a chunked Adam step other than the last: no beta-power advance
+  // one of group_n launches of the same step (each with its own ticket): the last to finish advances
+  unsigned* group_ticket;
+  int group_n;
   // gradient pass: the dense role sums the deferred split-K slabs (slabs) of [t4_begin, t4_end) into
   // the gradient arena instead of updating parameters (the tail's all-reduce then sends the sums)
   int slab_to_g;

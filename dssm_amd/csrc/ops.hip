@@ -308,18 +308,23 @@ int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype,
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
+size_t dssm_adam_tickets_bytes(int group) {
+  return group <= 0 ? 0 : (64 + (size_t)group * dssm::kAdamTicketUints) * sizeof(unsigned);
+}
+
 int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
                          int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
                          float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
                          int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
-                         float lr, float beta1, float beta2, float eps, const float* state, float grad_scale,
-                         void* ws, void* stream) {
+                         float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
+                         int group, int member, void* tickets, void* ws, void* stream) {
   const int64_t w1_end = (int64_t)(D + 1) * n;
   if (!indptr || !dZ || !p || !g || !m || !v || !state || !ws || rows <= 0 || D <= 0 || n <= 0 || (n % 4) ||
       lddz < n || (lddz % 8) || (max_nnz && (!indices || !values)) || (dz_dtype != DSSM_F32 && dz_dtype != DSSM_BF16) ||
       rest_begin % 4 || rest_end % 4 || rest_begin < w1_end || rest_end < rest_begin || splits < 0 ||
       (splits && (!slab || slab_count <= 0 || slab_count % 4 || rest_begin + slab_count > rest_end)) ||
-      (w1_shadow && (ld_shadow < n || ld_shadow % 4)) || nseg < 0 || nseg > 4 || (nseg && !segs))
+      (w1_shadow && (ld_shadow < n || ld_shadow % 4)) || nseg < 0 || nseg > 4 || (nseg && !segs) || group < 0 ||
+      (group && (!tickets || member < 0 || member >= group)))
     return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: bad argument");
   if (!dssm::csc_rank_supported(D)) return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: D beyond the CSC rank path");
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
@@ -341,8 +346,15 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
   a.g = g;
   a.m = m;
   a.v = v;
-  a.st = const_cast<float*>(state);  // read only: no_advance
-  a.no_advance = 1;
+  a.st = state;
+  if (group) {  // member's own two-level ticket after the group counter (dssm_adam_tickets_bytes)
+    unsigned* t = static_cast<unsigned*>(tickets);
+    a.group_ticket = t;
+    a.group_n = group;
+    a.ticket = t + 64 + (size_t)member * dssm::kAdamTicketUints;
+  } else {
+    a.no_advance = 1;
+  }
   a.lr = lr;
   a.beta1 = beta1;
   a.beta2 = beta2;

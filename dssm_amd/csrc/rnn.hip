@@ -556,6 +556,25 @@ extern "C" int dssm_adam_probe(int n_max) {
   return DSSM_OK;
 }
 
+extern "C" int dssm_adam_probe_span(int first, int n, double* span_ms) {
+  if (!span_ms || first < 0 || n < 1 || first + n > g_adam_probe.used)
+    return rerr(DSSM_E_INVALID, "adam_probe_span: bad argument");
+  // launches first .. first+n-1 (e.g. concurrent ones on several streams): latest end - earliest
+  // start, both relative to the first launch's start event
+  double lo = 0.0, hi = 0.0;
+  for (int i = first; i < first + n; ++i) {
+    float s = 0.f, e = 0.f;
+    if (hipEventSynchronize(g_adam_probe.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&s, g_adam_probe.ev[2 * first], g_adam_probe.ev[2 * i]) != hipSuccess ||
+        hipEventElapsedTime(&e, g_adam_probe.ev[2 * first], g_adam_probe.ev[2 * i + 1]) != hipSuccess)
+      return rerr(DSSM_E_HIP, "adam_probe_span: event");
+    lo = std::min(lo, (double)s);
+    hi = std::max(hi, (double)e);
+  }
+  *span_ms = hi - lo;
+  return DSSM_OK;
+}
+
 extern "C" int dssm_adam_probe_read(double* avg_ms, int* count) {
   if (!avg_ms || !count) return rerr(DSSM_E_INVALID, "adam_probe_read: bad argument");
   double tot = 0.0;

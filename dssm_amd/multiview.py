@@ -115,6 +115,10 @@ class MultiViewDSSM:
         # FC2's split-K weight-gradient partials left for the fused optimizer (per tower key)
         self._splits = {"u": C.c_int(0), "i": C.c_int(0)}
         self._fused = False
+        self._adam_pending = False  # fused: backward left the towers' streams forked for apply_adam
+        # the two tower launches of a fused optimizer step share these tickets: the later one to
+        # finish advances the beta powers (no advance launch, no join in front of it)
+        self.adam_tickets = torch.zeros(int(self.lib.dssm_adam_tickets_bytes(2)), dtype=torch.uint8, device=dev)
         self.fused_w1_adam = fused_w1_adam
         self.set_rotations(rotations if rotations is not None else self.default_rotations(seed))
         self.global_step = 0
@@ -276,7 +280,10 @@ class MultiViewDSSM:
                                            ptr(self._block(self.grads, f"{tower}_1")), ptr(self.spmm_ws[tower]),
                                            s), "spmm_bwd")
 
-    def backward(self, stream=None):
+    def backward(self, stream=None, join: bool = True):
+        """join=False (fused optimizer, apply_adam next on the same streams): the item tower's stream
+        is left forked so each tower's optimizer launch follows its own backward without a join and
+        re-fork in between (apply_adam joins)."""
         main = stream if stream is not None else torch.cuda.current_stream(self.device)
         s = stream_ptr(main)
         BS, R = self.bs, self.bs * (2 + self.neg)
@@ -289,13 +296,16 @@ class MultiViewDSSM:
         self._fork(main)
         self._tower_bwd("u", "user", self.dz2src[:BS], s)
         self._tower_bwd("i", f"view{self.view}", self.dz2src[BS:], stream_ptr(self.aux))
-        main.wait_stream(self.aux)
+        if self._fused and not join:
+            self._adam_pending = True  # each tower's optimizer launch follows on its own stream
+        else:
+            main.wait_stream(self.aux)
 
     def trained_ranges(self):
         """Arena ranges the step updates: the user tower and the active view."""
         return [self.layout[t] for t in ("user", f"view{self.view}")]
 
-    def _tower_adam(self, key, tower, s, grad_scale):
+    def _tower_adam(self, key, tower, s, grad_scale, member):
         """Fused mode: one tower's CSC transpose + ONE optimizer launch over its [W1; b1] rows (the
         gradient gathered inline) and its [W2; b2] block (FC2's split-K partials summed inline)."""
         ip, ix, vv = self.batch[key]
@@ -314,19 +324,24 @@ class MultiViewDSSM:
                                             ptr(self.adam_m[b:]), ptr(self.adam_v[b:]), off2, e - b,
                                             ptr(self.slab[key]) if splits else None, (self.l1 + 1) * self.l2, splits,
                                             w1s, ld1, segs, nseg, self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state),
-                                            grad_scale, ptr(self.spmm_ws[tower]), s), "spmm_bwd_w_adam")
+                                            grad_scale, 2, member, ptr(self.adam_tickets), ptr(self.spmm_ws[tower]),
+                                            s), "spmm_bwd_w_adam")
 
     def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
         towers = ("user", f"view{self.view}")
         if self._fused:
-            # the two towers' launches run concurrently (the item tower's on self.aux), then the
-            # beta powers advance once both have read them
-            main = self._fork(stream)
-            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale)
-            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale)
+            # each tower's launch on its backward's stream (the item tower's on self.aux), running
+            # concurrently; the later one to finish advances the beta powers
+            main = stream if stream is not None else torch.cuda.current_stream(self.device)
+            if not self._adam_pending:
+                self._fork(main)
+            self._adam_pending = False
+            # (both on one stream, each tower's transpose + launch in turn: 0.292 against 0.257 ms/step;
+            # one launch takes 68 us alone, the concurrent pair 128 us)
+            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0)
+            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1)
             main.wait_stream(self.aux)
-            check(self.lib.dssm_adam_advance(ptr(self.adam_state), 0.9, 0.999, stream_ptr(main)), "adam_advance")
         elif self.bf16:
             # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass
             rng = (C.c_int64 * 4)(*[x for t in towers for x in self.layout[t]])
@@ -348,7 +363,7 @@ class MultiViewDSSM:
 
     def train_step(self, stream=None):
         self.forward(stream)
-        self.backward(stream)
+        self.backward(stream, join=False)
         self.apply_adam(stream)
 
     def loss(self) -> float:

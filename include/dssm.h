@@ -398,21 +398,28 @@ int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, const in
  *     (dssm_dense_bwd_ex's deferred split-K; splits == 0: g).
  * g's rows [0, D] must be zero and are left zero (heavy columns' atomics target); gradient x
  * grad_scale.  bf16: W1's rows also written to w1_shadow [D x ld_shadow] (NULL: none), the rest range
- * to the shadow segments (offsets relative to p).  Does not advance the beta powers: call
- * dssm_adam_advance once every trained block of the step is updated.  Needs the CSC rank path
+ * to the shadow segments (offsets relative to p).  The beta powers: group == 0, not advanced (call
+ * dssm_adam_advance once every trained block of the step is updated); group = n > 0, this launch is
+ * member `member` of the step's n launches (any streams, concurrent or not) sharing `tickets`
+ * (dssm_adam_tickets_bytes(n) bytes, zero-filled once, re-armed by the launches), and the last of them
+ * to finish advances the powers -- no separate launch, no join before it.  Needs the CSC rank path
  * (D <= 36800). */
+size_t dssm_adam_tickets_bytes(int group);
 int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
                          int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
                          float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
                          int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
-                         float lr, float beta1, float beta2, float eps, const float* state, float grad_scale,
-                         void* ws, void* stream);
+                         float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
+                         int group, int member, void* tickets, void* ws, void* stream);
 /* TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (state on the device). */
 int dssm_adam_advance(float* state, float beta1, float beta2, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
  * averages the recorded launches (in a captured graph, each launch's latest replay). */
 int dssm_adam_probe(int n_max);
 int dssm_adam_probe_read(double* avg_ms, int* count);
+/* ... and the wall span of n recorded launches from index first (launches that ran concurrently on
+ * several streams): the latest end minus the earliest start. */
+int dssm_adam_probe_span(int first, int n, double* span_ms);
 /* Row gather / scatter-add (Merge_Negative_Doc by index, its backward): dst[r] = src[map[r]];
  * dst[map[r]] += src[r] over r < n after dst (dst_rows x ldd) is cleared.  fp32. */
 int dssm_rows_gather(const float* src, int lds, const int32_t* map, int n, int cols, float* dst, int ldd,
