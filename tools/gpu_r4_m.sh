@@ -1,9 +1,8 @@
 #!/bin/bash
-# round 4 measurement set: multiview check, then tools/gpu_measure.sh (BoW bf16 + fp32: kernel stats,
-# PMC traffic, MFMA, bench lines) and tools/gpu_measure_aux.sh for the multi-view row
+# round 4 measurement set: tools/gpu_measure.sh (BoW bf16 + fp32: kernel stats, PMC traffic, MFMA,
+# bench lines) and tools/gpu_measure_aux.sh for the multi-view row
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_r4_e.sh || exit 1
 DTYPES="bf16 fp32" bash tools/gpu_measure.sh || { echo "measure failed"; exit 1; }
 MODELS=multiview bash tools/gpu_measure_aux.sh || { echo "aux failed"; exit 1; }
 tail -1 gpurun_out/m/bench_bf16.log | cut -c1-300
