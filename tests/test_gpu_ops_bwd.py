@@ -282,3 +282,97 @@ def test_adam_step():
     torch.cuda.synchronize()
     np.testing.assert_allclose(tp.cpu().numpy(), p, rtol=0, atol=1e-6)
     np.testing.assert_allclose(st.cpu().numpy(), [b1p, b2p], rtol=1e-7)
+
+
+def _adam_ref(p, g, m, v, b1p, b2p, lr=0.01):
+    f = np.float32
+    lr_t = f(lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+    m = m + (g - m) * f(1 - 0.9)
+    v = v + (g * g - v) * f(1 - 0.999)
+    return p - (m * lr_t) / (np.sqrt(v) + f(1e-8)), m, v
+
+
+@pytest.mark.parametrize("D,rows,n,dt", [(700, 200, 64, "fp32"), (5000, 768, 300, "bf16"), (30000, 1536, 304, "bf16")])
+def test_spmm_bwd_w_adam(D, rows, n, dt):
+    """dssm_spmm_bwd_w_adam: two towers (separate arenas, batches and workspaces) on two streams, one
+    optimizer step group of 2 sharing the beta powers, 2 steps.  Reference: float32 ApplyAdam on
+    [X | 1]^T dZ (float64, then float32) for [W1; b1] and on the sum of 3 split-K partials for the
+    rest block.  W1's rows where the gradient is well-conditioned (|g| > 1e-3 max|g|) <= 2e-6, every
+    element <= 2 lr; the W1 gradient rows stay zero; bf16 shadows = bf16(p) bit for bit; the beta
+    powers advance once per step.  Batches include an empty row, columns past 64 and 256 entries."""
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(11))
+    bf = dt == "bf16"
+    n2, r2, splits = 32, 20, 3
+    w1 = (D + 1) * n
+    rb = -(-w1 // 64) * 64
+    re = rb + -(-(r2 * n2) // 64) * 64
+    ldz = -(-n // 8) * 8
+    st = torch.tensor([0.9, 0.999], device="cuda")
+    tickets = torch.zeros(int(lib.dssm_adam_tickets_bytes(2)), dtype=torch.uint8, device="cuda")
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    towers = []
+    for k in range(2):
+        ip, ix, vv = synth_rows(rng, ZipfColumns(D), rows, 24.0)
+        ip = np.concatenate([ip[:3], ip[2:]]).astype(np.int32)[:rows + 1]  # row 2 empty
+        ip[-1] = min(ip[-1], len(ix))
+        ix, vv = ix[:ip[-1]], vv[:ip[-1]]
+        import scipy.sparse as sp
+        X = sp.csr_matrix((vv.astype(np.float64), ix, ip), shape=(rows, D + 1)).tolil()
+        X[:, D] = 1.0
+        X = X.tocsr()
+        dZp = np.zeros((rows, ldz), np.float32)
+        dZp[:, :n] = rng.standard_normal((rows, n))
+        tdz = torch.from_numpy(dZp).cuda()
+        if bf:
+            tdz = tdz.to(torch.bfloat16)
+            dZp = tdz.float().cpu().numpy()
+        slab = rng.standard_normal((splits, r2 * n2)).astype(np.float32)
+        g1 = np.asarray(X.T @ dZp[:, :n].astype(np.float64)).astype(np.float32).ravel()
+        g2 = slab[0] + slab[1] + slab[2]  # the optimizer's fixed split order
+        p0 = rng.standard_normal(re).astype(np.float32) * 0.1
+        T = dict(ip=ip, ix=ix, vv=vv, g1=g1, g2=g2, p0=p0,
+                 t=[torch.from_numpy(x).cuda() for x in (ip, ix, vv)], dz=tdz,
+                 slab=torch.from_numpy(slab.ravel()).cuda(), p=torch.from_numpy(p0.copy()).cuda(),
+                 g=torch.zeros(re, device="cuda"), m=torch.zeros(re, device="cuda"), v=torch.zeros(re, device="cuda"),
+                 ws=torch.zeros(int(lib.dssm_spmm_bwd_ws_bytes(rows, D, int(ip[-1]))), dtype=torch.uint8, device="cuda"),
+                 sh1=torch.zeros((D, ldz), dtype=torch.bfloat16, device="cuda"),
+                 sh2=torch.zeros((r2 - 1, n2), dtype=torch.bfloat16, device="cuda"))
+        cnt = np.bincount(ix, minlength=D)
+        assert cnt.max() > (256 if rows >= 768 else 64) and int(ip[3] - ip[2]) == 0
+        towers.append(T)
+    torch.cuda.synchronize()
+    for step in range(2):
+        for k, T in enumerate(towers):
+            streams[k].wait_stream(streams[0])
+            seg = (_lib.dssm_shadow_seg * 1)(_lib.dssm_shadow_seg(rb, r2 - 1, n2, n2, T["sh2"].data_ptr()))
+            check(lib.dssm_spmm_bwd_w_adam(ptr(T["t"][0]), ptr(T["t"][1]), ptr(T["t"][2]), rows, D, int(T["ip"][-1]),
+                                           ptr(T["dz"]), _lib.DSSM_BF16 if bf else _lib.DSSM_F32, ldz, n,
+                                           ptr(T["p"]), ptr(T["g"]), ptr(T["m"]), ptr(T["v"]), rb, re,
+                                           ptr(T["slab"]), r2 * n2, splits,
+                                           ptr(T["sh1"]) if bf else None, ldz, seg if bf else None, 1 if bf else 0,
+                                           0.01, 0.9, 0.999, 1e-8, ptr(st), 1.0, 2, k, ptr(tickets), ptr(T["ws"]),
+                                           streams[k].cuda_stream), "spmm_bwd_w_adam")
+        streams[0].wait_stream(streams[1])
+    torch.cuda.synchronize()
+    f = np.float32
+    np.testing.assert_allclose(st.cpu().numpy(), [f(f(0.9 * 0.9) * 0.9), f(f(0.999 * 0.999) * 0.999)], rtol=1e-7)
+    for T in towers:
+        g = np.zeros(re, np.float32)
+        g[:w1] = T["g1"]
+        g[rb:rb + r2 * n2] = T["g2"]
+        p, m, v = T["p0"].copy(), np.zeros(re, f), np.zeros(re, f)
+        b1p, b2p = f(0.9), f(0.999)
+        for _ in range(2):
+            p, m, v = _adam_ref(p, g, m, v, b1p, b2p)
+            b1p, b2p = f(b1p * f(0.9)), f(b2p * f(0.999))
+        got = T["p"].cpu().numpy()
+        assert np.abs(got - p).max() <= 2 * 2 * 0.01
+        well = np.abs(g) > 1e-3 * np.abs(g).max()
+        assert np.abs(got - p)[well].max() <= 2e-6, np.abs(got - p)[well].max()
+        assert np.array_equal(got[w1:rb], p[w1:rb]) and np.array_equal(got[rb + r2 * n2:], p[rb + r2 * n2:])
+        assert not torch.any(T["g"][:w1])
+        if bf:
+            pw = T["p"][:D * n].view(D, n)
+            assert torch.equal(T["sh1"][:, :n], pw.to(torch.bfloat16))
+            assert torch.equal(T["sh2"], T["p"][rb:rb + (r2 - 1) * n2].view(r2 - 1, n2).to(torch.bfloat16))
