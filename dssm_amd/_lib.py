@@ -149,6 +149,9 @@ _SIGS = {
                                         _P, _P, C.c_int, _P]),
     "dssm_rnn_bf16_backward": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P), _P,
                                          C.c_int, _P, _P, C.POINTER(_P), _P]),
+    "dssm_rnn_bf16_bucket": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P]),
+    "dssm_rnn_bf16_backward_ex": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P),
+                                            _P, C.c_int, _P, _P, C.POINTER(_P), C.c_int, _P]),
     "dssm_rnn_bf16_probe": (C.c_int, [C.c_int]),
     "dssm_rnn_bf16_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "dssm_spmm_bwd_ws_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
@@ -179,7 +182,8 @@ _SIGS = {
     "dssm_spmm_bwd_w_adam": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                        _P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_int64, C.c_int, _P, C.c_int,
                                        _P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, _P, C.c_float,
-                                       C.c_int, C.c_int, _P, _P, _P]),
+                                       C.c_int, C.c_int, _P, C.c_int, _P, _P]),
+    "dssm_spmm_bwd_csc": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "dssm_adam_tickets_bytes": (C.c_size_t, [C.c_int]),
     "dssm_adam_probe_span": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "dssm_adam_advance": (C.c_int, [_P, C.c_float, C.c_float, _P]),

@@ -308,6 +308,20 @@ int dssm_dense_bwd_ex(const void* A, int lda, const void* W, int ldw, int dtype,
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
+int dssm_spmm_bwd_csc(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                      int max_nnz, void* ws, void* stream) {
+  if (!indptr || !ws || rows <= 0 || D <= 0 || max_nnz < 0 || (max_nnz && (!indices || !values)))
+    return oerr(DSSM_E_INVALID, "spmm_bwd_csc: bad argument");
+  if (!dssm::csc_rank_supported(D)) return oerr(DSSM_E_INVALID, "spmm_bwd_csc: D beyond the CSC rank path");
+  const SpmmWs w = spmm_ws(rows, D, max_nnz);
+  char* b = static_cast<char*>(ws);
+  const hipError_t e = dssm::launch_csc_build(
+      indptr, indices, values, rows, D, max_nnz, reinterpret_cast<int*>(b + w.scratch),
+      reinterpret_cast<int*>(b + w.col_ptr), reinterpret_cast<int*>(b + w.row), reinterpret_cast<float*>(b + w.val),
+      reinterpret_cast<int*>(b + w.col), (hipStream_t)stream, nullptr, 0, true, false);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
 size_t dssm_adam_tickets_bytes(int group) {
   return group <= 0 ? 0 : (64 + (size_t)group * dssm::kAdamTicketUints) * sizeof(unsigned);
 }
@@ -317,7 +331,7 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
                          float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
                          int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
                          float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
-                         int group, int member, void* tickets, void* ws, void* stream) {
+                         int group, int member, void* tickets, int build_csc, void* ws, void* stream) {
   const int64_t w1_end = (int64_t)(D + 1) * n;
   if (!indptr || !dZ || !p || !g || !m || !v || !state || !ws || rows <= 0 || D <= 0 || n <= 0 || (n % 4) ||
       lddz < n || (lddz % 8) || (max_nnz && (!indices || !values)) || (dz_dtype != DSSM_F32 && dz_dtype != DSSM_BF16) ||
@@ -338,9 +352,12 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
   int* crow = reinterpret_cast<int*>(b + w.row);
   float* cval = reinterpret_cast<float*>(b + w.val);
   int* ccol = reinterpret_cast<int*>(b + w.col);
-  hipError_t e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, crow, cval,
-                                        ccol, s, nullptr, 0, true, false);
-  if (e != hipSuccess) return oerr(DSSM_E_HIP, hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if (build_csc) {
+    e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, crow, cval, ccol, s,
+                               nullptr, 0, true, false);
+    if (e != hipSuccess) return oerr(DSSM_E_HIP, hipGetErrorString(e));
+  }
   dssm::AdamStep a{};
   a.p = p;
   a.g = g;

@@ -252,7 +252,14 @@ class MultiViewDSSM:
         # the towers are independent until the cosine: the item tower runs beside the user tower
         self._tower_fwd("u", "user", self.ysrc[:BS], s)
         self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], sa)
-        main.wait_stream(self.aux)
+        main.wait_event(self.aux.record_event())
+        self._csc_ev = None
+        if self._fused:
+            # the optimizer's CSC transposes (they depend on the batch only) on the item tower's
+            # stream while the caller's stream runs the loss: off the step's critical path
+            self._csc("u", "user", sa)
+            self._csc_ev = self.aux.record_event()
+            self._csc("i", f"view{self.view}", sa)
         # Make_Negative_Item's merged rows read through the index map by the cosine kernel itself
         check(self.lib.dssm_cosine_softmax_loss_mapped(ptr(self.ysrc), self.ld2, ptr(self.map), self.l2, BS,
                                                        self.neg, self.gamma, ptr(self.cos_raw), ptr(self.cos_sim),
@@ -305,7 +312,12 @@ class MultiViewDSSM:
         """Arena ranges the step updates: the user tower and the active view."""
         return [self.layout[t] for t in ("user", f"view{self.view}")]
 
-    def _tower_adam(self, key, tower, s, grad_scale, member):
+    def _csc(self, key, tower, s):
+        ip, ix, vv = self.batch[key]
+        check(self.lib.dssm_spmm_bwd_csc(ptr(ip), ptr(ix), ptr(vv), self.bs, self.dims[TOWERS.index(tower)],
+                                         self.max_nnz, ptr(self.spmm_ws[tower]), s), "spmm_bwd_csc")
+
+    def _tower_adam(self, key, tower, s, grad_scale, member, build_csc):
         """Fused mode: one tower's CSC transpose + ONE optimizer launch over its [W1; b1] rows (the
         gradient gathered inline) and its [W2; b2] block (FC2's split-K partials summed inline)."""
         ip, ix, vv = self.batch[key]
@@ -324,8 +336,8 @@ class MultiViewDSSM:
                                             ptr(self.adam_m[b:]), ptr(self.adam_v[b:]), off2, e - b,
                                             ptr(self.slab[key]) if splits else None, (self.l1 + 1) * self.l2, splits,
                                             w1s, ld1, segs, nseg, self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state),
-                                            grad_scale, 2, member, ptr(self.adam_tickets), ptr(self.spmm_ws[tower]),
-                                            s), "spmm_bwd_w_adam")
+                                            grad_scale, 2, member, ptr(self.adam_tickets), int(build_csc),
+                                            ptr(self.spmm_ws[tower]), s), "spmm_bwd_w_adam")
 
     def apply_adam(self, stream=None, grad_scale: float = 1.0):
         s = stream_ptr(stream)
@@ -339,8 +351,12 @@ class MultiViewDSSM:
             self._adam_pending = False
             # (both on one stream, each tower's transpose + launch in turn: 0.292 against 0.257 ms/step;
             # one launch takes 68 us alone, the concurrent pair 128 us)
-            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0)
-            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1)
+            built = getattr(self, "_csc_ev", None) is not None  # transposed by forward() on self.aux
+            if built:
+                main.wait_event(self._csc_ev)
+            self._csc_ev = None
+            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0, not built)
+            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1, not built)
             main.wait_stream(self.aux)
         elif self.bf16:
             # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass

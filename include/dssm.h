@@ -405,12 +405,17 @@ int dssm_adam_step_shadow(float* p, const float* g, float* m, float* v, const in
  * to finish advances the powers -- no separate launch, no join before it.  Needs the CSC rank path
  * (D <= 36800). */
 size_t dssm_adam_tickets_bytes(int group);
+/* build_csc = 0: the transpose is already in ws, built for the same batch by dssm_spmm_bwd_csc
+ * earlier in stream order (e.g. on another stream while the loss runs), and only the optimizer
+ * launches. */
+int dssm_spmm_bwd_csc(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                      int max_nnz, void* ws, void* stream);
 int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
                          int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
                          float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
                          int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
                          float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
-                         int group, int member, void* tickets, void* ws, void* stream);
+                         int group, int member, void* tickets, int build_csc, void* ws, void* stream);
 /* TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (state on the device). */
 int dssm_adam_advance(float* state, float beta1, float beta2, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
@@ -534,6 +539,14 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream);
+/* The backward's token bucketing (the batch's positions grouped by token for the embedding gradient:
+ * count, scan, fill into ws) as its own call, so it can run beside the forward on another stream (it
+ * depends on ids / lens only); _ex with bucketed = 1 then skips it (0: as dssm_rnn_bf16_backward). */
+int dssm_rnn_bf16_bucket(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H, void* ws,
+                         void* stream);
+int dssm_rnn_bf16_backward_ex(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
+                              const float* const* w, const float* dy, int lddy, void* ws, float* demb,
+                              float* const* gw, int bucketed, void* stream);
 /* Timing probes (benchmarks): record HIP events around the next n_max BPTT launches (n_max = 0:
  * off); read the average launch duration of the recorded ones (synchronizes on their events). */
 int dssm_rnn_bf16_probe(int n_max);

@@ -351,7 +351,7 @@ def test_spmm_bwd_w_adam(D, rows, n, dt):
                                            ptr(T["p"]), ptr(T["g"]), ptr(T["m"]), ptr(T["v"]), rb, re,
                                            ptr(T["slab"]), r2 * n2, splits,
                                            ptr(T["sh1"]) if bf else None, ldz, seg if bf else None, 1 if bf else 0,
-                                           0.01, 0.9, 0.999, 1e-8, ptr(st), 1.0, 2, k, ptr(tickets), ptr(T["ws"]),
+                                           0.01, 0.9, 0.999, 1e-8, ptr(st), 1.0, 2, k, ptr(tickets), 1, ptr(T["ws"]),
                                            streams[k].cuda_stream), "spmm_bwd_w_adam")
         streams[0].wait_stream(streams[1])
     torch.cuda.synchronize()

@@ -38,7 +38,7 @@ def main(rows=6144, nnz=32.0, D=30000, n=300, reps=50):
     def call():
         check(lib.dssm_spmm_bwd_w_adam(ptr(t[0]), ptr(t[1]), ptr(t[2]), rows, D, int(ip[-1]), ptr(dz), _lib.DSSM_BF16,
                                        ld, n, ptr(p), ptr(g), ptr(m), ptr(v), rb, re, None, 0, 0, ptr(sh1), ld, seg, 1,
-                                       0.01, 0.9, 0.999, 1e-8, ptr(st), 1.0, 1, 0, ptr(tk), ptr(ws),
+                                       0.01, 0.9, 0.999, 1e-8, ptr(st), 1.0, 1, 0, ptr(tk), 1, ptr(ws),
                                        _lib.stream_ptr()), "adam")
     for _ in range(5):
         call()
