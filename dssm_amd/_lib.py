@@ -149,9 +149,6 @@ _SIGS = {
                                         _P, _P, C.c_int, _P]),
     "dssm_rnn_bf16_backward": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P), _P,
                                          C.c_int, _P, _P, C.POINTER(_P), _P]),
-    "dssm_rnn_bf16_bucket": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P]),
-    "dssm_rnn_bf16_backward_ex": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P),
-                                            _P, C.c_int, _P, _P, C.POINTER(_P), C.c_int, _P]),
     "dssm_rnn_bf16_probe": (C.c_int, [C.c_int]),
     "dssm_rnn_bf16_probe_read": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "dssm_spmm_bwd_ws_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),

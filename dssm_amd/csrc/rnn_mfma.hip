@@ -891,36 +891,22 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
   return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
 }
 
-int dssm_rnn_bf16_bucket(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H, void* ws,
-                         void* stream) {
-  if (!ids || !lens || !ws || R <= 0 || T <= 0 || V <= 0 || V > 32768 || !dssm::shape_ok(E, H))
-    return rerr_b(DSSM_E_INVALID, "rnn_bf16_bucket: bad argument or unsupported (E, H)");
-  hipStream_t s = (hipStream_t)stream;
-  const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
-  // the batch's positions bucketed by token (for the embedding gradient after the BPTT)
-  if (zero_bytes_async(L.cnt, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
-    return rerr_b(DSSM_E_HIP, "rnn_bf16_bucket: zero fill");
-  const int gpos = std::max(1, std::min((R * T + 255) / 256, 2048));
-  hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt);
-  hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start,
-                     L.cursor);
-  hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cursor, L.pos);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
-}
-
-int dssm_rnn_bf16_backward_ex(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
-                              const float* const* w, const float* dy, int lddy, void* ws, float* demb,
-                              float* const* gw, int bucketed, void* stream) {
+int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
+                           const float* const* w, const float* dy, int lddy, void* ws, float* demb,
+                           float* const* gw, void* stream) {
   if (!ids || !lens || !w || !dy || !ws || !demb || !gw || R <= 0 || T <= 0 || V <= 0 || V > 32768 ||
       !dssm::shape_ok(E, H) || lddy < 2 * H)
     return rerr_b(DSSM_E_INVALID, "rnn_bf16_backward: bad argument or unsupported (E, H)");
   hipStream_t s = (hipStream_t)stream;
   const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
-  if (!bucketed) {
-    const int rc = dssm_rnn_bf16_bucket(ids, lens, R, T, V, E, H, ws, stream);
-    if (rc != DSSM_OK) return rc;
-  }
+  // the batch's positions bucketed by token (for the embedding gradient after the BPTT)
+  if (zero_bytes_async(L.cnt, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
+    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: zero fill");
+  const int gpos = std::max(1, std::min((R * T + 255) / 256, 2048));
+  hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt);
+  hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start,
+                     L.cursor);
+  hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cursor, L.pos);
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   const bool probe = g_probe.used < (int)g_probe.ev.size() / 2;
@@ -981,12 +967,6 @@ int dssm_rnn_bf16_backward_ex(const int32_t* ids, const int32_t* lens, int R, in
   hipLaunchKernelGGL(dssm::k_rnn_dw_reduce, dim3((n * dssm::kDwSlabRows * 32 + 255) / 256), dim3(256), 0, s, A);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
-}
-
-int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
-                           const float* const* w, const float* dy, int lddy, void* ws, float* demb,
-                           float* const* gw, void* stream) {
-  return dssm_rnn_bf16_backward_ex(ids, lens, R, T, V, E, H, w, dy, lddy, ws, demb, gw, 0, stream);
 }
 
 int dssm_rnn_bf16_probe(int n_max) {

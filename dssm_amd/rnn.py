@@ -90,9 +90,6 @@ class RnnDSSM:
         self.global_step = 0
         self._drop_step = 0
         self._train = False
-        # bf16 train steps: the backward's token bucketing runs on this stream beside the forward
-        self.aux = torch.cuda.Stream(device=dev) if dtype == "bf16" else None
-        self._bucket_ev = None
 
     # ---- parameters (oracle / reference names) ------------------------------------------------
     def _block(self, arena: torch.Tensor, name: str) -> torch.Tensor:
@@ -157,15 +154,6 @@ class RnnDSSM:
     def forward(self, train: bool = True, keep: Optional[float] = None, stream=None):
         s = stream_ptr(stream)
         keep = (self.keep if keep is None else float(keep)) if train else 1.0
-        self._bucket_ev = None
-        if self.dtype == "bf16" and train:
-            # the embedding gradient's token bucketing depends on the batch only: on self.aux while the
-            # recurrence runs (its 4 small launches leave the backward's critical path)
-            main = stream if stream is not None else torch.cuda.current_stream(self.device)
-            self.aux.wait_stream(main)
-            check(self.lib.dssm_rnn_bf16_bucket(ptr(self.ids), ptr(self.lens), self.R, self.T, self.V, self.E,
-                                                self.H, ptr(self.ws), stream_ptr(self.aux)), "rnn_bf16_bucket")
-            self._bucket_ev = self.aux.record_event()
         if self.dtype == "bf16":
             check(self.lib.dssm_rnn_bf16_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
                                                   ptr(self._block(self.params, "emb")), self.V, self.E, self.H,
@@ -197,14 +185,10 @@ class RnnDSSM:
               "dropout_bwd")
         gw = (C.c_void_p * 4)(*[ptr(self._block(self.grads, n)) for n in ("fw_g", "fw_c", "bw_g", "bw_c")])
         if self.dtype == "bf16":
-            bucketed = self._bucket_ev is not None
-            if bucketed:
-                (stream if stream is not None else torch.cuda.current_stream(self.device)).wait_event(self._bucket_ev)
-            self._bucket_ev = None
-            check(self.lib.dssm_rnn_bf16_backward_ex(ptr(self.ids), ptr(self.lens), self.R, self.T, self.V, self.E,
-                                                      self.H, self._w(self.params), ptr(self.dy), 2 * self.H,
-                                                      ptr(self.ws), ptr(self._block(self.grads, "emb")), gw,
-                                                      int(bucketed), s), "rnn_bf16_backward")
+            check(self.lib.dssm_rnn_bf16_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.V, self.E,
+                                                   self.H, self._w(self.params), ptr(self.dy), 2 * self.H,
+                                                   ptr(self.ws), ptr(self._block(self.grads, "emb")), gw, s),
+                  "rnn_bf16_backward")
         else:
             check(self.lib.dssm_rnn_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.E, self.H,
                                               self._w(self.params), ptr(self.dy), 2 * self.H, ptr(self.ws),

@@ -539,14 +539,6 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream);
-/* The backward's token bucketing (the batch's positions grouped by token for the embedding gradient:
- * count, scan, fill into ws) as its own call, so it can run beside the forward on another stream (it
- * depends on ids / lens only); _ex with bucketed = 1 then skips it (0: as dssm_rnn_bf16_backward). */
-int dssm_rnn_bf16_bucket(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H, void* ws,
-                         void* stream);
-int dssm_rnn_bf16_backward_ex(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
-                              const float* const* w, const float* dy, int lddy, void* ws, float* demb,
-                              float* const* gw, int bucketed, void* stream);
 /* Timing probes (benchmarks): record HIP events around the next n_max BPTT launches (n_max = 0:
  * off); read the average launch duration of the recorded ones (synchronizes on their events). */
 int dssm_rnn_bf16_probe(int n_max);
