@@ -736,6 +736,194 @@ __global__ __launch_bounds__(256) void k_rnn_dw_reduce(DwArgs a) {
   }
 }
 
+// E = H = 128 (config 4): every output tile of a direction from ONE read of each cache row.  The
+// 12-tile launch above reads each row's operand panels twice on average (x by three tiles, h, dr, du,
+// dc by two): 1.2 GB through the CUs per step against 0.6 GB of distinct rows.  Here a workgroup of 4
+// waves owns a row split of one direction and accumulates all six 128 x 128 products of it --
+// (x, dr) (x, du) (h, dr) (h, du) (x, dc) (r*h, dc), 98,304 fp32 per workgroup, 384 per lane (the
+// AGPR file) -- from 32-row slabs of the six panels staged through LDS (the swizzled images and
+// transposing fragment reads of k_rnn_dw), double-buffered, the next slab's global loads issued
+// before the current slab's MFMAs.  Wave w owns output rows 32w..32w+31 of every tile.  Partials
+// [dir][split][6 * 128 * 128 + 3 * 128] (the three bias rows: column sums of dr, du, dc); a second
+// launch sums the splits in fixed order into the arena.
+constexpr int kDwAllPanels = 6, kDwAllRows = 32;
+constexpr int kDwAllPart = 6 * 128 * 128 + 3 * 128;
+#ifndef DSSM_RNN_DW_ALL_SPLITS  // row splits per direction (workgroups = 2 x splits, one per CU)
+#define DSSM_RNN_DW_ALL_SPLITS 128
+#endif
+struct DwAllArgs {
+  const u16* HS;   // [dir][TR][128] h_{t-1}
+  const u16* RH;   // [dir][TR][128] r*h_{t-1}
+  const u16* DG;   // [dir][TR][256] [dr | du]
+  const u16* DC;   // [dir][TR][128] dc
+  const int* TOK;  // [dir][TR] token of x_t
+  const u16* emb;  // [V][128] bf16 embedding copy
+  float* part;     // [2][splits][kDwAllPart]
+  int TR, splits, kps;
+};
+
+__global__ __launch_bounds__(256) void k_rnn_dw_all(DwAllArgs a) {
+  // [buf][panel][32 rows x 128 cols] swizzled images (dw_off): x, h, r*h, dr, du, dc
+  __shared__ __attribute__((aligned(16))) u16 sP[2][kDwAllPanels][kDwAllRows * 128];
+  const int dir = blockIdx.y, split = blockIdx.x;
+  const size_t half = (size_t)a.TR * dir;
+  const int kbeg = split * a.kps, kend = min(a.TR, kbeg + a.kps);  // multiples of 32 (launcher)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  // staging by global_load_lds (16 B per lane, LDS destination = wave base + 16 lane): wave w fills
+  // rows rA = 4w + g and rB = rA + 16 of every panel; lane slot li of a row holds global chunk
+  // li ^ dw_sw(row), so the linear LDS write lands in the dw_off image
+  const int rA = 4 * w + g, rB = rA + 16;
+  const int cA = 8 * (li ^ dw_sw(rA)), cB = 8 * (li ^ dw_sw(rB));
+  const u16* HS = a.HS + half * 128;
+  const u16* RH = a.RH + half * 128;
+  const u16* DG = a.DG + half * 256;
+  const u16* DC = a.DC + half * 128;
+  const int* TOK = a.TOK + half;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto glds = [&](const u16* src, u16* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)dst, 16, 0, 0);
+  };
+  // slab k0's tokens of rows rA, rB (the x panel's gather), loaded one slab ahead
+  auto toks = [&](int k0, int& tA, int& tB) {
+    tA = k0 < kend ? TOK[k0 + rA] : 0;
+    tB = k0 < kend ? TOK[k0 + rB] : 0;
+  };
+  auto stage = [&](int buf, int k0, int tA, int tB) {
+    const size_t kA = (size_t)(k0 + rA), kB = (size_t)(k0 + rB);
+    u16* base = &sP[buf][0][0];
+    const int oA = 4 * w * 128, oB = (4 * w + 16) * 128;  // wave-uniform row-group offsets (u16)
+    constexpr int PS = kDwAllRows * 128;
+    glds(a.emb + (size_t)tA * 128 + cA, base + 0 * PS + oA);
+    glds(a.emb + (size_t)tB * 128 + cB, base + 0 * PS + oB);
+    glds(HS + kA * 128 + cA, base + 1 * PS + oA);
+    glds(HS + kB * 128 + cB, base + 1 * PS + oB);
+    glds(RH + kA * 128 + cA, base + 2 * PS + oA);
+    glds(RH + kB * 128 + cB, base + 2 * PS + oB);
+    glds(DG + kA * 256 + cA, base + 3 * PS + oA);
+    glds(DG + kB * 256 + cB, base + 3 * PS + oB);
+    glds(DG + kA * 256 + 128 + cA, base + 4 * PS + oA);
+    glds(DG + kB * 256 + 128 + cB, base + 4 * PS + oB);
+    glds(DC + kA * 128 + cA, base + 5 * PS + oA);
+    glds(DC + kB * 128 + cB, base + 5 * PS + oB);
+  };
+  f32x4 acc[6][2][8];
+#pragma unroll
+  for (int t = 0; t < 6; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  auto compute = [&](int buf) {
+    bf16x8 ax[2], ah[2], arh[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c0 = 32 * w + 16 * i;
+      ax[i] = dw_frag(sP[buf][0], 0, c0, g, q, p);
+      ah[i] = dw_frag(sP[buf][1], 0, c0, g, q, p);
+      arh[i] = dw_frag(sP[buf][2], 0, c0, g, q, p);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8 bdr = dw_frag(sP[buf][3], 0, 16 * j, g, q, p);
+      const bf16x8 bdu = dw_frag(sP[buf][4], 0, 16 * j, g, q, p);
+      const bf16x8 bdc = dw_frag(sP[buf][5], 0, 16 * j, g, q, p);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdr, acc[0][i][j], 0, 0, 0);
+        acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdu, acc[1][i][j], 0, 0, 0);
+        acc[2][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bdr, acc[2][i][j], 0, 0, 0);
+        acc[3][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bdu, acc[3][i][j], 0, 0, 0);
+        acc[4][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdc, acc[4][i][j], 0, 0, 0);
+        acc[5][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(arh[i], bdc, acc[5][i][j], 0, 0, 0);
+      }
+      // bias: wave w sums the columns of n-blocks 2w, 2w + 1 (wave-uniform branch)
+      if ((j >> 1) == w) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          bsum[0][j & 1] += (float)bdr[e];
+          bsum[1][j & 1] += (float)bdu[e];
+          bsum[2][j & 1] += (float)bdc[e];
+        }
+      }
+    }
+  };
+  const int nst = kbeg < kend ? (kend - kbeg) / kDwAllRows : 0;
+  int tA = 0, tB = 0, nA = 0, nB = 0;
+  if (nst > 0) {
+    toks(kbeg, tA, tB);
+    stage(0, kbeg, tA, tB);
+    toks(kbeg + kDwAllRows, nA, nB);
+  }
+  __syncthreads();  // slab 0 landed (the barrier waits for every outstanding load)
+  for (int s = 0; s < nst; ++s) {
+    const int k1 = kbeg + kDwAllRows * (s + 1);
+    if (s + 1 < nst) {
+      stage((s + 1) & 1, k1, nA, nB);  // in flight during this slab's MFMAs
+      toks(k1 + kDwAllRows, nA, nB);   // used after the barrier below
+    }
+    compute(s & 1);
+    __syncthreads();
+  }
+  float* out = a.part + ((size_t)dir * a.splits + split) * kDwAllPart;
+#pragma unroll
+  for (int t = 0; t < 6; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          out[(size_t)t * 16384 + (size_t)(32 * w + 16 * i + 4 * g + e) * 128 + 16 * j + li] = acc[t][i][j][e];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = bsum[b][h];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (g == 0) out[6 * 16384 + b * 128 + 32 * w + 16 * h + li] = v;
+    }
+}
+
+// the splits summed in fixed order into [Wg; bg] ([257 x 256]) and [Wc; bc] ([257 x 128]) per direction
+struct DwAllDest {
+  float* wg[2];
+  float* wc[2];
+};
+__global__ __launch_bounds__(256) void k_rnn_dw_all_reduce(const float* __restrict__ part, int splits,
+                                                           DwAllDest d) {
+  constexpr int q4 = kDwAllPart / 4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 2 * q4; e += gridDim.x * blockDim.x) {
+    const int dir = e / q4, i4 = e - dir * q4, i = 4 * i4;
+    const float* src = part + (size_t)dir * splits * kDwAllPart + i;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * kDwAllPart);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float* wg = dir ? d.wg[1] : d.wg[0];
+    float* wc = dir ? d.wc[1] : d.wc[0];
+    float* dst;
+    if (i < 6 * 16384) {
+      const int t = i >> 14, m = (i >> 7) & 127, n = i & 127;
+      switch (t) {
+        case 0: dst = wg + (size_t)m * 256 + n; break;
+        case 1: dst = wg + (size_t)m * 256 + 128 + n; break;
+        case 2: dst = wg + (size_t)(128 + m) * 256 + n; break;
+        case 3: dst = wg + (size_t)(128 + m) * 256 + 128 + n; break;
+        case 4: dst = wc + (size_t)m * 128 + n; break;
+        default: dst = wc + (size_t)(128 + m) * 128 + n; break;
+      }
+    } else {
+      const int b = (i - 6 * 16384) >> 7, n = (i - 6 * 16384) & 127;
+      dst = b == 0 ? wg + (size_t)256 * 256 + n : (b == 1 ? wg + (size_t)256 * 256 + 128 + n : wc + (size_t)256 * 128 + n);
+    }
+    *reinterpret_cast<float4*>(dst) = s;
+  }
+}
+
 __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int64_t n8) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 a = *reinterpret_cast<const float4*>(x + 8 * i);
@@ -745,6 +933,9 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 }
 
 // ---- workspace and dispatch -------------------------------------------------------------------
+#ifndef DSSM_RNN_DW_ALL  // 1: E = H = 128 takes k_rnn_dw_all (0: the 12-tile k_rnn_dw, A/B builds)
+#define DSSM_RNN_DW_ALL 1
+#endif
 #ifndef DSSM_RNN_DW_WGS  // workgroups of one k_rnn_dw launch (tiles x row splits): 2 per CU
 #define DSSM_RNN_DW_WGS 512
 #endif
@@ -781,7 +972,8 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
   w.start = (int*)take(((size_t)V + 1) * 4);
   w.cursor = (int*)take(((size_t)V + 1) * 4);
   w.pos = (int*)take(TR * 4);
-  w.slab = (float*)take((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128 * 4);
+  w.slab = (float*)take(std::max((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128,
+                                  (size_t)2 * DSSM_RNN_DW_ALL_SPLITS * kDwAllPart) * 4);
   w.bytes = off;
   return w;
 }
@@ -925,10 +1117,22 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
     hipLaunchKernelGGL(dssm::k_emb_grad<64>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
   else
     hipLaunchKernelGGL(dssm::k_emb_grad<32>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
+  const int TR = T * R;
+  if (E == 128 && H == 128 && DSSM_RNN_DW_ALL && TR % dssm::kDwAllRows == 0) {
+    // every tile of a direction per workgroup (k_rnn_dw_all) + the fixed-order split reduce
+    dssm::DwAllArgs B{L.HS, L.RH, L.DG, L.DC, L.TOK, L.emb16, L.slab, TR, DSSM_RNN_DW_ALL_SPLITS, 0};
+    B.kps = ((TR + B.splits - 1) / B.splits + dssm::kDwAllRows - 1) / dssm::kDwAllRows * dssm::kDwAllRows;
+    hipLaunchKernelGGL(dssm::k_rnn_dw_all, dim3(B.splits, 2), dim3(256), 0, s, B);
+    const dssm::DwAllDest D{{gw[0], gw[2]}, {gw[1], gw[3]}};
+    hipLaunchKernelGGL(dssm::k_rnn_dw_all_reduce, dim3((2 * dssm::kDwAllPart / 4 + 255) / 256), dim3(256), 0, s,
+                       L.slab, B.splits, D);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
+  }
   // [W; b] gradients, both directions in one launch (k_rnn_dw) + a fixed-order split reduce:
   //   dWg = [x | h]^T [dr | du] (+ bias = column sums),  dWc rows [0, E) = x^T dc (+ bias),
   //   dWc rows [E, E+H) = (r*h)^T dc
-  const int K = E + H, TR = T * R;
+  const int K = E + H;
   dssm::DwArgs A{};
   int n = 0;
   for (int dir = 0; dir < 2; ++dir) {
