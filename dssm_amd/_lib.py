@@ -143,6 +143,11 @@ _SIGS = {
                                     _P, _P, C.c_int64, C.POINTER(_P), _P]),
     "dssm_rnn_adam": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_float, C.c_float, C.c_float,
                                 C.c_float, _P]),
+    "dssm_rnn_adam_ex": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64, _P, C.c_float, C.c_float, C.c_float,
+                                   C.c_float, _P, _P]),
+    "dssm_rnn_bf16_emb16_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "dssm_rnn_bf16_forward_ex": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.POINTER(_P), _P,
+                                           _P, C.c_int, C.c_int, _P]),
     "dssm_rnn_bf16_supported": (C.c_int, [C.c_int, C.c_int]),
     "dssm_rnn_bf16_ws_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "dssm_rnn_bf16_forward": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.POINTER(_P),

@@ -331,7 +331,8 @@ __global__ void k_dropout(const float* __restrict__ x, float* __restrict__ y, in
 __global__ __launch_bounds__(256) void k_rnn_adam(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ m, float* __restrict__ v,
                                                   int64_t n_sparse, int64_t n, const float* st,
-                                                  float lr, float b1, float b2, float eps, float gs) {
+                                                  float lr, float b1, float b2, float eps, float gs,
+                                                  uint16_t* __restrict__ shadow = nullptr) {
   const float alpha = lr * sqrtf(1.0f - st[1]) / (1.0f - st[0]);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -346,7 +347,10 @@ __global__ __launch_bounds__(256) void k_rnn_adam(float* __restrict__ p, const f
     }
     m[i] = mi;
     v[i] = vi;
-    p[i] -= (mi * alpha) / (sqrtf(vi) + eps);
+    const float pi = p[i] - (mi * alpha) / (sqrtf(vi) + eps);
+    p[i] = pi;
+    // the embedding table's bf16 copy the bf16 recurrences gather (no per-step conversion pass)
+    if (shadow && i < n_sparse) shadow[i] = f2bf(pi);
   }
 }
 
@@ -476,17 +480,22 @@ int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
-int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
-                  float* state, float lr, float beta1, float beta2, float eps, void* stream) {
+int dssm_rnn_adam_ex(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
+                     float* state, float lr, float beta1, float beta2, float eps, uint16_t* shadow, void* stream) {
   if (!p || !g || !m || !v || !state || n_sparse < 0 || n < n_sparse)
     return rerr(DSSM_E_INVALID, "rnn_adam: bad argument");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, n_sparse, n, state, lr,
-                     beta1, beta2, eps, 1.0f);
+                     beta1, beta2, eps, 1.0f, shadow);
   hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DSSM_OK : rerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
+                  float* state, float lr, float beta1, float beta2, float eps, void* stream) {
+  return dssm_rnn_adam_ex(p, g, m, v, n_sparse, n, state, lr, beta1, beta2, eps, nullptr, stream);
 }
 
 }  // extern "C"
@@ -499,7 +508,7 @@ extern "C" int dssm_adam_step(float* p, const float* g, float* m, float* v, int6
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
   const bool probe = dssm::adam_probe_begin(s);
   hipLaunchKernelGGL(dssm::k_rnn_adam, dim3(grid), dim3(256), 0, s, p, g, m, v, (int64_t)0, n, state, lr,
-                     beta1, beta2, eps, grad_scale);
+                     beta1, beta2, eps, grad_scale, nullptr);
   if (probe) dssm::adam_probe_end(s);
   if (advance) hipLaunchKernelGGL(dssm::k_rnn_adam_advance, dim3(1), dim3(64), 0, s, state, beta1, beta2);
   const hipError_t e = hipGetLastError();

@@ -443,24 +443,29 @@ __global__ __launch_bounds__(H / 16 * 64) void k_gru_bwd_mfma(
 // The batch's active (row, position) pairs bucketed by token (count, one-workgroup scan, fill), then
 // one wave per token sums its positions' dx rows of both directions (fw at step s, bw at step
 // len - 1 - s) in fp32 and writes the token's whole gradient row (zero for absent tokens).
+// the batch's active positions bucketed by token: count (each position keeps its rank within its
+// token: the returning atomic's value), exclusive scan (which re-zeroes the counts for the next
+// step), fill pos[start[token] + rank] = position (plain stores)
 __global__ void k_tok_count(const int* __restrict__ ids, const int* __restrict__ lens, int R, int T,
-                            int* __restrict__ cnt) {
+                            int* __restrict__ cnt, int* __restrict__ rank) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * T; i += gridDim.x * blockDim.x) {
     const int r = i / T, p = i - r * T;
-    if (p < lens[r]) atomicAdd(&cnt[ids[i]], 1);
+    if (p < lens[r]) rank[i] = atomicAdd(&cnt[ids[i]], 1);
   }
 }
 
 // exclusive scan of cnt[0, V) (V <= 32768) by one workgroup: the counts are loaded coalesced into
 // LDS (dynamic, V ints), each thread scans its contiguous slice, a shuffle scan per wave and a scan
 // of the 16 wave totals join the slices
-__global__ __launch_bounds__(1024) void k_tok_scan(const int* __restrict__ cnt, int V, int* __restrict__ start,
-                                                   int* __restrict__ cursor) {
+__global__ __launch_bounds__(1024) void k_tok_scan(int* __restrict__ cnt, int V, int* __restrict__ start) {
   extern __shared__ int sc[];
   __shared__ int wsum[16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, per = (V + 1023) / 1024, b = min(V, t * per),
             e = min(V, b + per);
-  for (int i = t; i < V; i += 1024) sc[i] = cnt[i];
+  for (int i = t; i < V; i += 1024) {
+    sc[i] = cnt[i];
+    cnt[i] = 0;  // zero for the next step's count
+  }
   __syncthreads();
   int s = 0;
   for (int i = b; i < e; ++i) s += sc[i];
@@ -483,16 +488,15 @@ __global__ __launch_bounds__(1024) void k_tok_scan(const int* __restrict__ cnt, 
   __syncthreads();
   for (int i = t; i < V; i += 1024) {
     start[i] = sc[i];
-    cursor[i] = sc[i];
   }
   if (t == 1023) start[V] = off + x;
 }
 
 __global__ void k_tok_fill(const int* __restrict__ ids, const int* __restrict__ lens, int R, int T,
-                           int* __restrict__ cursor, int* __restrict__ pos) {
+                           const int* __restrict__ start, const int* __restrict__ rank, int* __restrict__ pos) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * T; i += gridDim.x * blockDim.x) {
     const int r = i / T, p = i - r * T;
-    if (p < lens[r]) pos[atomicAdd(&cursor[ids[i]], 1)] = i;
+    if (p < lens[r]) pos[start[ids[i]] + rank[i]] = i;
   }
 }
 
@@ -943,9 +947,9 @@ constexpr int kDwMaxSplits = 64;
 
 struct WsB {
   u16 *HS, *RH, *GA, *GC, *DG, *DC, *DX, *emb16;
-  int *TOK, *cnt, *start, *cursor, *pos;
+  int *TOK, *cnt, *start, *rank, *pos;
   float* slab;
-  size_t bytes;
+  size_t bytes, emb16_off;
 };
 
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -967,10 +971,11 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
   w.DG = (u16*)take(2 * TR * 2 * H * 2);
   w.DC = (u16*)take(2 * TR * H * 2);
   w.DX = (u16*)take(2 * TR * E * 2);
+  w.emb16_off = off;
   w.emb16 = (u16*)take((size_t)V * E * 2);
   w.cnt = (int*)take(((size_t)V + 1) * 4);
   w.start = (int*)take(((size_t)V + 1) * 4);
-  w.cursor = (int*)take(((size_t)V + 1) * 4);
+  w.rank = (int*)take(TR * 4);
   w.pos = (int*)take(TR * 4);
   w.slab = (float*)take(std::max((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128,
                                   (size_t)2 * DSSM_RNN_DW_ALL_SPLITS * kDwAllPart) * 4);
@@ -1061,16 +1066,23 @@ size_t dssm_rnn_bf16_ws_bytes(int R, int T, int E, int H, int V) {
   return dssm::ws_layout(nullptr, R, T, E, H, V).bytes;
 }
 
-int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
-                          int E, int H, const float* const* w, void* ws, float* y, int ldy, void* stream) {
+size_t dssm_rnn_bf16_emb16_offset(int R, int T, int E, int H, int V) {
+  if (R <= 0 || T <= 0 || V <= 0 || V > 32768 || !dssm::shape_ok(E, H)) return 0;
+  return dssm::ws_layout(nullptr, R, T, E, H, V).emb16_off;
+}
+
+int dssm_rnn_bf16_forward_ex(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
+                             int E, int H, const float* const* w, void* ws, float* y, int ldy, int emb16_current,
+                             void* stream) {
   if (!ids || !lens || !emb || !w || !ws || !y || R <= 0 || T <= 0 || V <= 0 || V > 32768 || !dssm::shape_ok(E, H) ||
       ldy < 2 * H)
     return rerr_b(DSSM_E_INVALID, "rnn_bf16_forward: bad argument or unsupported (E, H)");
   hipStream_t s = (hipStream_t)stream;
   const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
   const int64_t n8 = (int64_t)V * E / 8;
-  hipLaunchKernelGGL(dssm::k_to_bf16, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n8 + 255) / 256, 2048))),
-                     dim3(256), 0, s, emb, L.emb16, n8);
+  if (!emb16_current)
+    hipLaunchKernelGGL(dssm::k_to_bf16, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n8 + 255) / 256, 2048))),
+                       dim3(256), 0, s, emb, L.emb16, n8);
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   if (E == 128)
@@ -1083,6 +1095,11 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
   return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
 }
 
+int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
+                          int E, int H, const float* const* w, void* ws, float* y, int ldy, void* stream) {
+  return dssm_rnn_bf16_forward_ex(ids, lens, R, T, emb, V, E, H, w, ws, y, ldy, 0, stream);
+}
+
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream) {
@@ -1092,13 +1109,11 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   hipStream_t s = (hipStream_t)stream;
   const dssm::WsB L = dssm::ws_layout((char*)ws, R, T, E, H, V);
   // the batch's positions bucketed by token (for the embedding gradient after the BPTT)
-  if (zero_bytes_async(L.cnt, sizeof(int) * ((size_t)V + 1), s) != hipSuccess)
-    return rerr_b(DSSM_E_HIP, "rnn_bf16_backward: zero fill");
+  // (the counts start zero: the workspace is zero-filled once, and each scan re-zeroes them)
   const int gpos = std::max(1, std::min((R * T + 255) / 256, 2048));
-  hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt);
-  hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start,
-                     L.cursor);
-  hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cursor, L.pos);
+  hipLaunchKernelGGL(dssm::k_tok_count, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.cnt, L.rank);
+  hipLaunchKernelGGL(dssm::k_tok_scan, dim3(1), dim3(1024), sizeof(int) * (size_t)V, s, L.cnt, V, L.start);
+  hipLaunchKernelGGL(dssm::k_tok_fill, dim3(gpos), dim3(256), 0, s, ids, lens, R, T, L.start, L.rank, L.pos);
   const dssm::GruDimsB d{R, T};
   const int mt = dssm::pick_mt(R);
   const bool probe = g_probe.used < (int)g_probe.ev.size() / 2;

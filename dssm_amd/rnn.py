@@ -90,6 +90,9 @@ class RnnDSSM:
         self.global_step = 0
         self._drop_step = 0
         self._train = False
+        # bf16 mode: the workspace's bf16 copy of the embedding table is bf16(emb) (written by the last
+        # optimizer step), so the forward skips its conversion pass; reset when parameters are loaded
+        self._emb16_ok = False
 
     # ---- parameters (oracle / reference names) ------------------------------------------------
     def _block(self, arena: torch.Tensor, name: str) -> torch.Tensor:
@@ -97,6 +100,7 @@ class RnnDSSM:
         return arena[off:off + rows * cols].view(rows, cols)
 
     def load_params(self, p: Dict[str, np.ndarray]):
+        self._emb16_ok = False
         self._block(self.params, "emb").copy_(torch.from_numpy(np.asarray(p["emb"], np.float32)))
         for d in ("fw", "bw"):
             g = np.concatenate([p[f"{d}_Wg"], p[f"{d}_bg"][None, :]], 0).astype(np.float32)
@@ -155,10 +159,10 @@ class RnnDSSM:
         s = stream_ptr(stream)
         keep = (self.keep if keep is None else float(keep)) if train else 1.0
         if self.dtype == "bf16":
-            check(self.lib.dssm_rnn_bf16_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
-                                                  ptr(self._block(self.params, "emb")), self.V, self.E, self.H,
-                                                  self._w(self.params), ptr(self.ws), ptr(self.y0), 2 * self.H,
-                                                  s), "rnn_bf16_forward")
+            check(self.lib.dssm_rnn_bf16_forward_ex(ptr(self.ids), ptr(self.lens), self.R, self.T,
+                                                     ptr(self._block(self.params, "emb")), self.V, self.E, self.H,
+                                                     self._w(self.params), ptr(self.ws), ptr(self.y0), 2 * self.H,
+                                                     int(self._emb16_ok), s), "rnn_bf16_forward")
         else:
             check(self.lib.dssm_rnn_forward(ptr(self.ids), ptr(self.lens), self.R, self.T,
                                              ptr(self._block(self.params, "emb")), self.E, self.H,
@@ -196,9 +200,13 @@ class RnnDSSM:
                   "rnn_backward")
 
     def apply_adam(self, stream=None):
-        check(self.lib.dssm_rnn_adam(ptr(self.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
-                                     self.V * self.E, self.n_params, ptr(self.adam_state), self.lr,
-                                     self.beta1, self.beta2, self.eps, stream_ptr(stream)), "rnn_adam")
+        shadow = None
+        if self.dtype == "bf16":  # the optimizer rewrites the recurrences' bf16 embedding copy
+            shadow = ptr(self.ws) + int(self.lib.dssm_rnn_bf16_emb16_offset(self.R, self.T, self.E, self.H, self.V))
+        check(self.lib.dssm_rnn_adam_ex(ptr(self.params), ptr(self.grads), ptr(self.adam_m), ptr(self.adam_v),
+                                        self.V * self.E, self.n_params, ptr(self.adam_state), self.lr,
+                                        self.beta1, self.beta2, self.eps, shadow, stream_ptr(stream)), "rnn_adam")
+        self._emb16_ok = self.dtype == "bf16"
         self.global_step += 1
 
     def train_step(self, stream=None):

@@ -539,6 +539,13 @@ int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T,
 int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T, int V, int E, int H,
                            const float* const* w, const float* dy, int lddy, void* ws, float* demb,
                            float* const* gw, void* stream);
+/* The forward with emb16_current = 1: the workspace's bf16 copy of the embedding table (at byte
+ * dssm_rnn_bf16_emb16_offset() of ws) is already bf16(emb) -- written by the last dssm_rnn_adam_ex
+ * -- so the per-step conversion pass is skipped (0: as dssm_rnn_bf16_forward). */
+size_t dssm_rnn_bf16_emb16_offset(int R, int T, int E, int H, int V);
+int dssm_rnn_bf16_forward_ex(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,
+                             int E, int H, const float* const* w, void* ws, float* y, int ldy, int emb16_current,
+                             void* stream);
 /* Timing probes (benchmarks): record HIP events around the next n_max BPTT launches (n_max = 0:
  * off); read the average launch duration of the recorded ones (synchronizes on their events). */
 int dssm_rnn_bf16_probe(int n_max);
@@ -548,6 +555,10 @@ int dssm_rnn_bf16_probe_read(double* avg_ms, int* count);
  * device {beta1_power, beta2_power}, advanced after the update. */
 int dssm_rnn_adam(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
                   float* state, float lr, float beta1, float beta2, float eps, void* stream);
+/* ... also writing bf16(p) of [0, n_sparse) (the embedding table) to shadow (NULL: none): the bf16
+ * recurrences' embedding copy, kept current by the optimizer. */
+int dssm_rnn_adam_ex(float* p, const float* g, float* m, float* v, int64_t n_sparse, int64_t n,
+                     float* state, float lr, float beta1, float beta2, float eps, uint16_t* shadow, void* stream);
 
 #ifdef __cplusplus
 }
