@@ -59,7 +59,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat,
-    const int* __restrict__ rmap) {
+    const int* __restrict__ rmap, float* __restrict__ loss_out, unsigned* __restrict__ fin_ticket) {
   constexpr int NT = 64 * NW;
   COS_TL(0);
   __shared__ float s_part[2][NW];
@@ -304,8 +304,27 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       a += s_part[0][w];
       b += s_part[1][w];
     }
-    part[2 * blockIdx.x] = a;
-    part[2 * blockIdx.x + 1] = b;
+    if (fin_ticket) {
+      // in-kernel finalize: the partials as device-scope atomic stores (performed at the coherence
+      // point, so no agent-scope release -- which would write back the XCD's L2, the dy rows just
+      // stored -- is needed before the arrival; the last arrival reads them with atomic loads)
+      __hip_atomic_store(part + 2 * blockIdx.x, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(part + 2 * blockIdx.x + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      part[2 * blockIdx.x] = a;
+      part[2 * blockIdx.x + 1] = b;
+    }
+  }
+  if (fin_ticket) {
+    __shared__ int s_lastf;
+    if (threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's partial stores performed
+      const unsigned old = __hip_atomic_fetch_add(fin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_lastf = old == gridDim.x - 1;
+      if (s_lastf) __hip_atomic_store(fin_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    }
+    __syncthreads();
+    if (s_lastf) loss_reduce_coherent(part, gridDim.x, bs, loss_out);
   }
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -327,7 +346,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              const CscScatter* scatter, const int* rmap) {
+                              const CscScatter* scatter, const int* rmap, unsigned* fin_ticket) {
   if (neg + 1 > MAXK || n > kCosMaxN || (rmap && (fused || coef || y_out))) return hipErrorInvalidValue;
   // ws: the per-workgroup loss / accuracy partials (2 floats each)
   const int nw = cosine_waves(n, fused != nullptr);
@@ -339,21 +358,23 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
+  // in-kernel finalize: query workgroups only (the fused launch's extra blocks write no partials)
+  unsigned* const fin = (fin_ticket && !fused && !defer_finalize) ? fin_ticket : nullptr;
   if (fs.bdet.slab && (cdiv(bs, nw) > fs.bdet.cap || ld > 64 * kDetTiles)) return hipErrorInvalidValue;
-  // The loss partials are always summed by a later launch: a second tiny launch here when the
-  // caller does not defer.  (The in-kernel alternative, an agent-scope release + ticket in EVERY
-  // workgroup so that the last one can sum, writes back the XCD's L2 once per workgroup -- the dy
-  // rows the kernel has just written.)
+  // The loss partials are summed by a later launch (deferred: the caller's next one; else a tiny
+  // launch here), or with fin_ticket by the kernel's last workgroup (partials as device-scope atomic
+  // stores: an agent-scope release in every workgroup would write back the XCD's L2 -- the dy rows
+  // just stored -- once per workgroup).
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
-                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr); \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin); \
   else if (rmap)                                                                                \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, true>), grid, block, 0, s, z, ld, n, bs, neg, gamma, \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap);         \
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap, loss_out, fin); \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr)
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -365,7 +386,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #undef DSSM_COS
 #undef DSSM_COS2
 #undef DSSM_COS3
-  if (!defer_finalize)
+  if (!defer_finalize && !fin)
     hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
   return hipGetLastError();
 }

@@ -1535,6 +1535,12 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
   return DSSM_OK;
 }
 
+// the functional cosine's finalize ticket: the word after the per-workgroup partials in the caller's
+// workspace (dssm_cosine_ws_floats: 2 * ceil(BS / 4) + 64 floats, zero-filled before first use)
+static unsigned* cosine_fin_ticket(float* ws, int query_bs) {
+  return reinterpret_cast<unsigned*>(ws + 2 * ((query_bs + 3) / 4));
+}
+
 int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_map, int n, int query_bs, int neg,
                                     float gamma, float* cos_sim_raw, float* cos_sim, float* prob,
                                     float* query_norm, float* loss, float* dy, float* ws, void* stream) {
@@ -1543,7 +1549,7 @@ int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_m
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss_mapped: bad arguments");
   HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
                                    cos_sim, prob, query_norm, ws, loss, dy, (hipStream_t)stream, nullptr,
-                                   false, nullptr, row_map));
+                                   false, nullptr, row_map, cosine_fin_ticket(ws, query_bs)));
   return DSSM_OK;
 }
 
@@ -1554,8 +1560,8 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
       query_bs < 1 || neg < 1 || neg > 15 || n < 1 || n > 512 || ld < n)
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss: bad arguments");
   HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
-                                   cos_sim, prob, query_norm, ws, loss, dy,
-                                   (hipStream_t)stream));
+                                   cos_sim, prob, query_norm, ws, loss, dy, (hipStream_t)stream, nullptr,
+                                   false, nullptr, nullptr, cosine_fin_ticket(ws, query_bs)));
   return DSSM_OK;
 }
 

@@ -766,50 +766,54 @@ struct DwAllArgs {
   int TR, splits, kps;
 };
 
+constexpr int kDwAllBufs = 3, kDwAllMaxRows = 2048;  // slabs in flight; rows per split (tokens in LDS)
+constexpr int kDwAllPS = kDwAllRows * 128;           // u16 per panel image
 __global__ __launch_bounds__(256) void k_rnn_dw_all(DwAllArgs a) {
-  // [buf][panel][32 rows x 128 cols] swizzled images (dw_off): x, h, r*h, dr, du, dc
-  __shared__ __attribute__((aligned(16))) u16 sP[2][kDwAllPanels][kDwAllRows * 128];
+  // ONE LDS array (a second __shared__ object makes the compiler drain the glds before every
+  // ds_read): [buf][panel][32 x 128] swizzled images (x, h, r*h, dr, du, dc), then the split's tokens
+  __shared__ __attribute__((aligned(16))) u16 sm[kDwAllBufs * kDwAllPanels * kDwAllPS + 2 * kDwAllMaxRows];
+  int* const sTok = reinterpret_cast<int*>(sm + kDwAllBufs * kDwAllPanels * kDwAllPS);
   const int dir = blockIdx.y, split = blockIdx.x;
   const size_t half = (size_t)a.TR * dir;
   const int kbeg = split * a.kps, kend = min(a.TR, kbeg + a.kps);  // multiples of 32 (launcher)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  // the split's tokens (the x panel's gather rows) into LDS first, with ordinary loads: no
+  // VGPR-destination global load may be pending beside the glds ring below
+  for (int i = tid; i < kend - kbeg; i += 256) sTok[i] = a.TOK[half + kbeg + i];
+  __syncthreads();
   // staging by global_load_lds (16 B per lane, LDS destination = wave base + 16 lane): wave w fills
   // rows rA = 4w + g and rB = rA + 16 of every panel; lane slot li of a row holds global chunk
-  // li ^ dw_sw(row), so the linear LDS write lands in the dw_off image
+  // li ^ dw_sw(row), so the linear LDS write lands in the dw_off image.  12 per wave per slab.
   const int rA = 4 * w + g, rB = rA + 16;
   const int cA = 8 * (li ^ dw_sw(rA)), cB = 8 * (li ^ dw_sw(rB));
   const u16* HS = a.HS + half * 128;
   const u16* RH = a.RH + half * 128;
   const u16* DG = a.DG + half * 256;
   const u16* DC = a.DC + half * 128;
-  const int* TOK = a.TOK + half;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   auto glds = [&](const u16* src, u16* dst) {
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)dst, 16, 0, 0);
   };
-  // slab k0's tokens of rows rA, rB (the x panel's gather), loaded one slab ahead
-  auto toks = [&](int k0, int& tA, int& tB) {
-    tA = k0 < kend ? TOK[k0 + rA] : 0;
-    tB = k0 < kend ? TOK[k0 + rB] : 0;
-  };
-  auto stage = [&](int buf, int k0, int tA, int tB) {
-    const size_t kA = (size_t)(k0 + rA), kB = (size_t)(k0 + rB);
-    u16* base = &sP[buf][0][0];
+  auto stage = [&](int buf, int k0) {
+    int ra = rA, rb = rB, ca = cA, cb = cB;
+    asm volatile("" : "+v"(ra), "+v"(rb), "+v"(ca), "+v"(cb));  // no hoisted per-panel addresses
+    const int tA = sTok[k0 - kbeg + ra], tB = sTok[k0 - kbeg + rb];
+    const size_t kA = (size_t)(k0 + ra), kB = (size_t)(k0 + rb);
+    u16* base = sm + (size_t)buf * kDwAllPanels * kDwAllPS;
     const int oA = 4 * w * 128, oB = (4 * w + 16) * 128;  // wave-uniform row-group offsets (u16)
-    constexpr int PS = kDwAllRows * 128;
-    glds(a.emb + (size_t)tA * 128 + cA, base + 0 * PS + oA);
-    glds(a.emb + (size_t)tB * 128 + cB, base + 0 * PS + oB);
-    glds(HS + kA * 128 + cA, base + 1 * PS + oA);
-    glds(HS + kB * 128 + cB, base + 1 * PS + oB);
-    glds(RH + kA * 128 + cA, base + 2 * PS + oA);
-    glds(RH + kB * 128 + cB, base + 2 * PS + oB);
-    glds(DG + kA * 256 + cA, base + 3 * PS + oA);
-    glds(DG + kB * 256 + cB, base + 3 * PS + oB);
-    glds(DG + kA * 256 + 128 + cA, base + 4 * PS + oA);
-    glds(DG + kB * 256 + 128 + cB, base + 4 * PS + oB);
-    glds(DC + kA * 128 + cA, base + 5 * PS + oA);
-    glds(DC + kB * 128 + cB, base + 5 * PS + oB);
+    glds(a.emb + (size_t)tA * 128 + ca, base + 0 * kDwAllPS + oA);
+    glds(a.emb + (size_t)tB * 128 + cb, base + 0 * kDwAllPS + oB);
+    glds(HS + kA * 128 + ca, base + 1 * kDwAllPS + oA);
+    glds(HS + kB * 128 + cb, base + 1 * kDwAllPS + oB);
+    glds(RH + kA * 128 + ca, base + 2 * kDwAllPS + oA);
+    glds(RH + kB * 128 + cb, base + 2 * kDwAllPS + oB);
+    glds(DG + kA * 256 + ca, base + 3 * kDwAllPS + oA);
+    glds(DG + kB * 256 + cb, base + 3 * kDwAllPS + oB);
+    glds(DG + kA * 256 + 128 + ca, base + 4 * kDwAllPS + oA);
+    glds(DG + kB * 256 + 128 + cb, base + 4 * kDwAllPS + oB);
+    glds(DC + kA * 128 + ca, base + 5 * kDwAllPS + oA);
+    glds(DC + kB * 128 + cb, base + 5 * kDwAllPS + oB);
   };
   f32x4 acc[6][2][8];
 #pragma unroll
@@ -820,55 +824,58 @@ __global__ __launch_bounds__(256) void k_rnn_dw_all(DwAllArgs a) {
       for (int j = 0; j < 8; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
   auto compute = [&](int buf) {
-    bf16x8 ax[2], ah[2], arh[2];
+    const u16* P = sm + (size_t)buf * kDwAllPanels * kDwAllPS;
+    // the lane's fragment coordinates re-materialised per slab (an opaque copy): hoisted out of the
+    // slab loop, the 50-odd fragment addresses would not fit beside the 384 accumulators
+    int gg = g, qq = q, pp = p;
+    asm volatile("" : "+v"(gg), "+v"(qq), "+v"(pp));
+    // one 16-row strip of the A panels at a time (the B fragments are read once per strip): fewer
+    // live fragment registers beside the 384 accumulators
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c0 = 32 * w + 16 * i;
-      ax[i] = dw_frag(sP[buf][0], 0, c0, g, q, p);
-      ah[i] = dw_frag(sP[buf][1], 0, c0, g, q, p);
-      arh[i] = dw_frag(sP[buf][2], 0, c0, g, q, p);
-    }
+      const bf16x8 ax = dw_frag(P + 0 * kDwAllPS, 0, c0, gg, qq, pp);
+      const bf16x8 ah = dw_frag(P + 1 * kDwAllPS, 0, c0, gg, qq, pp);
+      const bf16x8 arh = dw_frag(P + 2 * kDwAllPS, 0, c0, gg, qq, pp);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bf16x8 bdr = dw_frag(sP[buf][3], 0, 16 * j, g, q, p);
-      const bf16x8 bdu = dw_frag(sP[buf][4], 0, 16 * j, g, q, p);
-      const bf16x8 bdc = dw_frag(sP[buf][5], 0, 16 * j, g, q, p);
+      for (int j = 0; j < 8; ++j) {
+        const bf16x8 bdr = dw_frag(P + 3 * kDwAllPS, 0, 16 * j, gg, qq, pp);
+        const bf16x8 bdu = dw_frag(P + 4 * kDwAllPS, 0, 16 * j, gg, qq, pp);
+        const bf16x8 bdc = dw_frag(P + 5 * kDwAllPS, 0, 16 * j, gg, qq, pp);
+        acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdr, acc[0][i][j], 0, 0, 0);
+        acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdu, acc[1][i][j], 0, 0, 0);
+        acc[2][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bdr, acc[2][i][j], 0, 0, 0);
+        acc[3][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bdu, acc[3][i][j], 0, 0, 0);
+        acc[4][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdc, acc[4][i][j], 0, 0, 0);
+        acc[5][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(arh, bdc, acc[5][i][j], 0, 0, 0);
+        // bias: wave w sums the columns of n-blocks 2w, 2w + 1 (wave-uniform branch), once per slab
+        if (i == 0 && (j >> 1) == w) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdr, acc[0][i][j], 0, 0, 0);
-        acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdu, acc[1][i][j], 0, 0, 0);
-        acc[2][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bdr, acc[2][i][j], 0, 0, 0);
-        acc[3][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bdu, acc[3][i][j], 0, 0, 0);
-        acc[4][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bdc, acc[4][i][j], 0, 0, 0);
-        acc[5][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(arh[i], bdc, acc[5][i][j], 0, 0, 0);
-      }
-      // bias: wave w sums the columns of n-blocks 2w, 2w + 1 (wave-uniform branch)
-      if ((j >> 1) == w) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          bsum[0][j & 1] += (float)bdr[e];
-          bsum[1][j & 1] += (float)bdu[e];
-          bsum[2][j & 1] += (float)bdc[e];
+          for (int e = 0; e < 8; ++e) {
+            bsum[0][j & 1] += (float)bdr[e];
+            bsum[1][j & 1] += (float)bdu[e];
+            bsum[2][j & 1] += (float)bdc[e];
+          }
         }
       }
     }
   };
+  // three LDS buffers, two slabs in flight: slab s + 2 is issued once every wave has passed the
+  // barrier behind its slab-s wait (so the buffer it overwrites, slab s - 1's, is no longer read);
+  // the waits are counted (vmcnt(12): the next slab's 12 loads stay in flight) and the barriers raw
+  // (a __syncthreads would wait for every outstanding load)
   const int nst = kbeg < kend ? (kend - kbeg) / kDwAllRows : 0;
-  int tA = 0, tB = 0, nA = 0, nB = 0;
-  if (nst > 0) {
-    toks(kbeg, tA, tB);
-    stage(0, kbeg, tA, tB);
-    toks(kbeg + kDwAllRows, nA, nB);
-  }
-  __syncthreads();  // slab 0 landed (the barrier waits for every outstanding load)
+  if (nst > 0) stage(0, kbeg);
+  if (nst > 1) stage(1, kbeg + kDwAllRows);
   for (int s = 0; s < nst; ++s) {
-    const int k1 = kbeg + kDwAllRows * (s + 1);
-    if (s + 1 < nst) {
-      stage((s + 1) & 1, k1, nA, nB);  // in flight during this slab's MFMAs
-      toks(k1 + kDwAllRows, nA, nB);   // used after the barrier below
-    }
-    compute(s & 1);
-    __syncthreads();
+    if (s + 1 < nst)
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nst) stage((s + 2) % kDwAllBufs, kbeg + kDwAllRows * (s + 2));
+    compute(s % kDwAllBufs);
   }
   float* out = a.part + ((size_t)dir * a.splits + split) * kDwAllPart;
 #pragma unroll
@@ -903,7 +910,17 @@ __global__ __launch_bounds__(256) void k_rnn_dw_all_reduce(const float* __restri
     const int dir = e / q4, i4 = e - dir * q4, i = 4 * i4;
     const float* src = part + (size_t)dir * splits * kDwAllPart + i;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < splits; ++sp) {
+    int sp = 0;
+    for (; sp + 8 <= splits; sp += 8) {  // eight loads in flight, added in split order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(sp + u) * kDwAllPart);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+      }
+    }
+    for (; sp < splits; ++sp) {
       const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * kDwAllPart);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
@@ -1133,10 +1150,11 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
   else
     hipLaunchKernelGGL(dssm::k_emb_grad<32>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
   const int TR = T * R;
-  if (E == 128 && H == 128 && DSSM_RNN_DW_ALL && TR % dssm::kDwAllRows == 0) {
+  const int all_kps = ((TR + DSSM_RNN_DW_ALL_SPLITS - 1) / DSSM_RNN_DW_ALL_SPLITS + dssm::kDwAllRows - 1) /
+                      dssm::kDwAllRows * dssm::kDwAllRows;
+  if (E == 128 && H == 128 && DSSM_RNN_DW_ALL && TR % dssm::kDwAllRows == 0 && all_kps <= dssm::kDwAllMaxRows) {
     // every tile of a direction per workgroup (k_rnn_dw_all) + the fixed-order split reduce
-    dssm::DwAllArgs B{L.HS, L.RH, L.DG, L.DC, L.TOK, L.emb16, L.slab, TR, DSSM_RNN_DW_ALL_SPLITS, 0};
-    B.kps = ((TR + B.splits - 1) / B.splits + dssm::kDwAllRows - 1) / dssm::kDwAllRows * dssm::kDwAllRows;
+    dssm::DwAllArgs B{L.HS, L.RH, L.DG, L.DC, L.TOK, L.emb16, L.slab, TR, DSSM_RNN_DW_ALL_SPLITS, all_kps};
     hipLaunchKernelGGL(dssm::k_rnn_dw_all, dim3(B.splits, 2), dim3(256), 0, s, B);
     const dssm::DwAllDest D{{gw[0], gw[2]}, {gw[1], gw[3]}};
     hipLaunchKernelGGL(dssm::k_rnn_dw_all_reduce, dim3((2 * dssm::kDwAllPart / 4 + 255) / 256), dim3(256), 0, s,
