@@ -1537,7 +1537,14 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
 
 // the functional cosine's finalize ticket: the word after the per-workgroup partials in the caller's
 // workspace (dssm_cosine_ws_floats: 2 * ceil(BS / 4) + 64 floats, zero-filled before first use)
+// (round 4: the last workgroup summing them in-kernel, behind a ticket in this word, measured slower on
+// the multi-view step -- 0.2554-0.2591 against 0.2424 ms/step -- and neutral on the RNN step; the
+// finalize stays a separate one-wave launch)
+#ifndef DSSM_COS_FIN_TICKET
+#define DSSM_COS_FIN_TICKET 0
+#endif
 static unsigned* cosine_fin_ticket(float* ws, int query_bs) {
+  if (!DSSM_COS_FIN_TICKET) return nullptr;
   return reinterpret_cast<unsigned*>(ws + 2 * ((query_bs + 3) / 4));
 }
 

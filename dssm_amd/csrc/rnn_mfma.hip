@@ -730,218 +730,24 @@ __global__ __launch_bounds__(256) void k_rnn_dw_reduce(DwArgs a) {
     if (c4 >= T.nlen) continue;
     if (row < 128 ? row >= T.mlen : T.bias == nullptr) continue;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < a.splits; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(
-          a.slab + (((size_t)sp * a.ntiles + ti) * kDwSlabRows + row) * 128 + c4);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    float* d = row < 128 ? T.dest + (size_t)(T.drow0 + row) * T.ldd + T.n0 + c4 : T.bias + T.n0 + c4;
-    *reinterpret_cast<float4*>(d) = s;
-  }
-}
-
-// E = H = 128 (config 4): every output tile of a direction from ONE read of each cache row.  The
-// 12-tile launch above reads each row's operand panels twice on average (x by three tiles, h, dr, du,
-// dc by two): 1.2 GB through the CUs per step against 0.6 GB of distinct rows.  Here a workgroup of 4
-// waves owns a row split of one direction and accumulates all six 128 x 128 products of it --
-// (x, dr) (x, du) (h, dr) (h, du) (x, dc) (r*h, dc), 98,304 fp32 per workgroup, 384 per lane (the
-// AGPR file) -- from 32-row slabs of the six panels staged through LDS (the swizzled images and
-// transposing fragment reads of k_rnn_dw), double-buffered, the next slab's global loads issued
-// before the current slab's MFMAs.  Wave w owns output rows 32w..32w+31 of every tile.  Partials
-// [dir][split][6 * 128 * 128 + 3 * 128] (the three bias rows: column sums of dr, du, dc); a second
-// launch sums the splits in fixed order into the arena.
-constexpr int kDwAllPanels = 6, kDwAllRows = 32;
-constexpr int kDwAllPart = 6 * 128 * 128 + 3 * 128;
-#ifndef DSSM_RNN_DW_ALL_SPLITS  // row splits per direction (workgroups = 2 x splits, one per CU)
-#define DSSM_RNN_DW_ALL_SPLITS 128
-#endif
-struct DwAllArgs {
-  const u16* HS;   // [dir][TR][128] h_{t-1}
-  const u16* RH;   // [dir][TR][128] r*h_{t-1}
-  const u16* DG;   // [dir][TR][256] [dr | du]
-  const u16* DC;   // [dir][TR][128] dc
-  const int* TOK;  // [dir][TR] token of x_t
-  const u16* emb;  // [V][128] bf16 embedding copy
-  float* part;     // [2][splits][kDwAllPart]
-  int TR, splits, kps;
-};
-
-constexpr int kDwAllBufs = 3, kDwAllMaxRows = 2048;  // slabs in flight; rows per split (tokens in LDS)
-constexpr int kDwAllPS = kDwAllRows * 128;           // u16 per panel image
-__global__ __launch_bounds__(256) void k_rnn_dw_all(DwAllArgs a) {
-  // ONE LDS array (a second __shared__ object makes the compiler drain the glds before every
-  // ds_read): [buf][panel][32 x 128] swizzled images (x, h, r*h, dr, du, dc), then the split's tokens
-  __shared__ __attribute__((aligned(16))) u16 sm[kDwAllBufs * kDwAllPanels * kDwAllPS + 2 * kDwAllMaxRows];
-  int* const sTok = reinterpret_cast<int*>(sm + kDwAllBufs * kDwAllPanels * kDwAllPS);
-  const int dir = blockIdx.y, split = blockIdx.x;
-  const size_t half = (size_t)a.TR * dir;
-  const int kbeg = split * a.kps, kend = min(a.TR, kbeg + a.kps);  // multiples of 32 (launcher)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  // the split's tokens (the x panel's gather rows) into LDS first, with ordinary loads: no
-  // VGPR-destination global load may be pending beside the glds ring below
-  for (int i = tid; i < kend - kbeg; i += 256) sTok[i] = a.TOK[half + kbeg + i];
-  __syncthreads();
-  // staging by global_load_lds (16 B per lane, LDS destination = wave base + 16 lane): wave w fills
-  // rows rA = 4w + g and rB = rA + 16 of every panel; lane slot li of a row holds global chunk
-  // li ^ dw_sw(row), so the linear LDS write lands in the dw_off image.  12 per wave per slab.
-  const int rA = 4 * w + g, rB = rA + 16;
-  const int cA = 8 * (li ^ dw_sw(rA)), cB = 8 * (li ^ dw_sw(rB));
-  const u16* HS = a.HS + half * 128;
-  const u16* RH = a.RH + half * 128;
-  const u16* DG = a.DG + half * 256;
-  const u16* DC = a.DC + half * 128;
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  auto glds = [&](const u16* src, u16* dst) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)dst, 16, 0, 0);
-  };
-  auto stage = [&](int buf, int k0) {
-    int ra = rA, rb = rB, ca = cA, cb = cB;
-    asm volatile("" : "+v"(ra), "+v"(rb), "+v"(ca), "+v"(cb));  // no hoisted per-panel addresses
-    const int tA = sTok[k0 - kbeg + ra], tB = sTok[k0 - kbeg + rb];
-    const size_t kA = (size_t)(k0 + ra), kB = (size_t)(k0 + rb);
-    u16* base = sm + (size_t)buf * kDwAllPanels * kDwAllPS;
-    const int oA = 4 * w * 128, oB = (4 * w + 16) * 128;  // wave-uniform row-group offsets (u16)
-    glds(a.emb + (size_t)tA * 128 + ca, base + 0 * kDwAllPS + oA);
-    glds(a.emb + (size_t)tB * 128 + cb, base + 0 * kDwAllPS + oB);
-    glds(HS + kA * 128 + ca, base + 1 * kDwAllPS + oA);
-    glds(HS + kB * 128 + cb, base + 1 * kDwAllPS + oB);
-    glds(RH + kA * 128 + ca, base + 2 * kDwAllPS + oA);
-    glds(RH + kB * 128 + cb, base + 2 * kDwAllPS + oB);
-    glds(DG + kA * 256 + ca, base + 3 * kDwAllPS + oA);
-    glds(DG + kB * 256 + cb, base + 3 * kDwAllPS + oB);
-    glds(DG + kA * 256 + 128 + ca, base + 4 * kDwAllPS + oA);
-    glds(DG + kB * 256 + 128 + cb, base + 4 * kDwAllPS + oB);
-    glds(DC + kA * 128 + ca, base + 5 * kDwAllPS + oA);
-    glds(DC + kB * 128 + cb, base + 5 * kDwAllPS + oB);
-  };
-  f32x4 acc[6][2][8];
-#pragma unroll
-  for (int t = 0; t < 6; ++t)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-  auto compute = [&](int buf) {
-    const u16* P = sm + (size_t)buf * kDwAllPanels * kDwAllPS;
-    // the lane's fragment coordinates re-materialised per slab (an opaque copy): hoisted out of the
-    // slab loop, the 50-odd fragment addresses would not fit beside the 384 accumulators
-    int gg = g, qq = q, pp = p;
-    asm volatile("" : "+v"(gg), "+v"(qq), "+v"(pp));
-    // one 16-row strip of the A panels at a time (the B fragments are read once per strip): fewer
-    // live fragment registers beside the 384 accumulators
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c0 = 32 * w + 16 * i;
-      const bf16x8 ax = dw_frag(P + 0 * kDwAllPS, 0, c0, gg, qq, pp);
-      const bf16x8 ah = dw_frag(P + 1 * kDwAllPS, 0, c0, gg, qq, pp);
-      const bf16x8 arh = dw_frag(P + 2 * kDwAllPS, 0, c0, gg, qq, pp);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bf16x8 bdr = dw_frag(P + 3 * kDwAllPS, 0, 16 * j, gg, qq, pp);
-        const bf16x8 bdu = dw_frag(P + 4 * kDwAllPS, 0, 16 * j, gg, qq, pp);
-        const bf16x8 bdc = dw_frag(P + 5 * kDwAllPS, 0, 16 * j, gg, qq, pp);
-        acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdr, acc[0][i][j], 0, 0, 0);
-        acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdu, acc[1][i][j], 0, 0, 0);
-        acc[2][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bdr, acc[2][i][j], 0, 0, 0);
-        acc[3][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bdu, acc[3][i][j], 0, 0, 0);
-        acc[4][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bdc, acc[4][i][j], 0, 0, 0);
-        acc[5][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(arh, bdc, acc[5][i][j], 0, 0, 0);
-        // bias: wave w sums the columns of n-blocks 2w, 2w + 1 (wave-uniform branch), once per slab
-        if (i == 0 && (j >> 1) == w) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            bsum[0][j & 1] += (float)bdr[e];
-            bsum[1][j & 1] += (float)bdu[e];
-            bsum[2][j & 1] += (float)bdc[e];
-          }
-        }
-      }
-    }
-  };
-  // three LDS buffers, two slabs in flight: slab s + 2 is issued once every wave has passed the
-  // barrier behind its slab-s wait (so the buffer it overwrites, slab s - 1's, is no longer read);
-  // the waits are counted (vmcnt(12): the next slab's 12 loads stay in flight) and the barriers raw
-  // (a __syncthreads would wait for every outstanding load)
-  const int nst = kbeg < kend ? (kend - kbeg) / kDwAllRows : 0;
-  if (nst > 0) stage(0, kbeg);
-  if (nst > 1) stage(1, kbeg + kDwAllRows);
-  for (int s = 0; s < nst; ++s) {
-    if (s + 1 < nst)
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 2 < nst) stage((s + 2) % kDwAllBufs, kbeg + kDwAllRows * (s + 2));
-    compute(s % kDwAllBufs);
-  }
-  float* out = a.part + ((size_t)dir * a.splits + split) * kDwAllPart;
-#pragma unroll
-  for (int t = 0; t < 6; ++t)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          out[(size_t)t * 16384 + (size_t)(32 * w + 16 * i + 4 * g + e) * 128 + 16 * j + li] = acc[t][i][j][e];
-#pragma unroll
-  for (int b = 0; b < 3; ++b)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v = bsum[b][h];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (g == 0) out[6 * 16384 + b * 128 + 32 * w + 16 * h + li] = v;
-    }
-}
-
-// the splits summed in fixed order into [Wg; bg] ([257 x 256]) and [Wc; bc] ([257 x 128]) per direction
-struct DwAllDest {
-  float* wg[2];
-  float* wc[2];
-};
-__global__ __launch_bounds__(256) void k_rnn_dw_all_reduce(const float* __restrict__ part, int splits,
-                                                           DwAllDest d) {
-  constexpr int q4 = kDwAllPart / 4;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 2 * q4; e += gridDim.x * blockDim.x) {
-    const int dir = e / q4, i4 = e - dir * q4, i = 4 * i4;
-    const float* src = part + (size_t)dir * splits * kDwAllPart + i;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = a.slab + ((size_t)ti * kDwSlabRows + row) * 128 + c4;
+    const size_t stride = (size_t)a.ntiles * kDwSlabRows * 128;  // one split
     int sp = 0;
-    for (; sp + 8 <= splits; sp += 8) {  // eight loads in flight, added in split order
+    for (; sp + 8 <= a.splits; sp += 8) {  // eight loads in flight, added in split order
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(sp + u) * kDwAllPart);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(sp + u) * stride);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
       }
     }
-    for (; sp < splits; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * kDwAllPart);
+    for (; sp < a.splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * stride);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    float* wg = dir ? d.wg[1] : d.wg[0];
-    float* wc = dir ? d.wc[1] : d.wc[0];
-    float* dst;
-    if (i < 6 * 16384) {
-      const int t = i >> 14, m = (i >> 7) & 127, n = i & 127;
-      switch (t) {
-        case 0: dst = wg + (size_t)m * 256 + n; break;
-        case 1: dst = wg + (size_t)m * 256 + 128 + n; break;
-        case 2: dst = wg + (size_t)(128 + m) * 256 + n; break;
-        case 3: dst = wg + (size_t)(128 + m) * 256 + 128 + n; break;
-        case 4: dst = wc + (size_t)m * 128 + n; break;
-        default: dst = wc + (size_t)(128 + m) * 128 + n; break;
-      }
-    } else {
-      const int b = (i - 6 * 16384) >> 7, n = (i - 6 * 16384) & 127;
-      dst = b == 0 ? wg + (size_t)256 * 256 + n : (b == 1 ? wg + (size_t)256 * 256 + 128 + n : wc + (size_t)256 * 128 + n);
-    }
-    *reinterpret_cast<float4*>(dst) = s;
+    float* d = row < 128 ? T.dest + (size_t)(T.drow0 + row) * T.ldd + T.n0 + c4 : T.bias + T.n0 + c4;
+    *reinterpret_cast<float4*>(d) = s;
   }
 }
 
@@ -954,9 +760,6 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 }
 
 // ---- workspace and dispatch -------------------------------------------------------------------
-#ifndef DSSM_RNN_DW_ALL  // 1: E = H = 128 takes k_rnn_dw_all (0: the 12-tile k_rnn_dw, A/B builds)
-#define DSSM_RNN_DW_ALL 1
-#endif
 #ifndef DSSM_RNN_DW_WGS  // workgroups of one k_rnn_dw launch (tiles x row splits): 2 per CU
 #define DSSM_RNN_DW_WGS 512
 #endif
@@ -994,8 +797,7 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
   w.start = (int*)take(((size_t)V + 1) * 4);
   w.rank = (int*)take(TR * 4);
   w.pos = (int*)take(TR * 4);
-  w.slab = (float*)take(std::max((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128,
-                                  (size_t)2 * DSSM_RNN_DW_ALL_SPLITS * kDwAllPart) * 4);
+  w.slab = (float*)take((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128 * 4);
   w.bytes = off;
   return w;
 }
@@ -1149,23 +951,10 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
     hipLaunchKernelGGL(dssm::k_emb_grad<64>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
   else
     hipLaunchKernelGGL(dssm::k_emb_grad<32>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
-  const int TR = T * R;
-  const int all_kps = ((TR + DSSM_RNN_DW_ALL_SPLITS - 1) / DSSM_RNN_DW_ALL_SPLITS + dssm::kDwAllRows - 1) /
-                      dssm::kDwAllRows * dssm::kDwAllRows;
-  if (E == 128 && H == 128 && DSSM_RNN_DW_ALL && TR % dssm::kDwAllRows == 0 && all_kps <= dssm::kDwAllMaxRows) {
-    // every tile of a direction per workgroup (k_rnn_dw_all) + the fixed-order split reduce
-    dssm::DwAllArgs B{L.HS, L.RH, L.DG, L.DC, L.TOK, L.emb16, L.slab, TR, DSSM_RNN_DW_ALL_SPLITS, all_kps};
-    hipLaunchKernelGGL(dssm::k_rnn_dw_all, dim3(B.splits, 2), dim3(256), 0, s, B);
-    const dssm::DwAllDest D{{gw[0], gw[2]}, {gw[1], gw[3]}};
-    hipLaunchKernelGGL(dssm::k_rnn_dw_all_reduce, dim3((2 * dssm::kDwAllPart / 4 + 255) / 256), dim3(256), 0, s,
-                       L.slab, B.splits, D);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
-  }
   // [W; b] gradients, both directions in one launch (k_rnn_dw) + a fixed-order split reduce:
   //   dWg = [x | h]^T [dr | du] (+ bias = column sums),  dWc rows [0, E) = x^T dc (+ bias),
   //   dWc rows [E, E+H) = (r*h)^T dc
-  const int K = E + H;
+  const int K = E + H, TR = T * R;
   dssm::DwArgs A{};
   int n = 0;
   for (int dir = 0; dir < 2; ++dir) {
