@@ -356,8 +356,15 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
   }
 }
 
-// The whole optimizer step in one launch: blocks [0, w1_blocks) run the fused W1 rows (grid-
-// stride over rows, one wave per row), the others stream the dense float4 range.  Every block
+// one LDS block shared by the two roles that use LDS (the hosted rank role's hash table, the heavy
+// items' rows): 16.4 instead of 26.6 KB per workgroup, so LDS no longer caps the launch at 6
+// workgroups per CU
+constexpr size_t kAdamLdsBytes = sizeof(unsigned) * kRankHash > sizeof(HeavyLds) ? sizeof(unsigned) * kRankHash
+                                                                                 : sizeof(HeavyLds);
+
+// The whole optimizer step in one launch (k_adam_step's body, run as workgroup blk of nblk):
+// blocks [0, w1_blocks) run the fused W1 rows (grid-stride over rows, one wave per row), the
+// others stream the dense float4 range.  Every block
 // reads the beta powers at its start; the last block to finish (relaxed agent-scope tickets: it
 // only needs every other block to have READ them, which precedes their arrival) advances them
 // (TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2, fp32) and re-arms
@@ -366,30 +373,25 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
 // range); the single-GPU step compiles without them (their row remapping and per-element wire tests
 // in the W1 and streaming loops cost the fused step 16 us: 57.5 -> 75 us measured)
 template <typename TZ, bool WIRE>
-__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
+__device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk, const unsigned nblk,
+                                               unsigned char* s_lds) {
   ADAM_TL(0);
   const float b1p = a.st[0], b2p = a.st[1];
   const float alpha = a.lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   // Block roles in dispatch order: the heavy-item blocks (the longest dependent chains) first,
   // then the W1-row gather blocks, then the flat/dense streaming blocks.  (Interleaving the
   // gathers with the streaming was measured slower: the heavy chains start late, 61 -> 86 us.)
-  // one LDS block shared by the two roles that use LDS (the hosted rank role's hash table, the
-  // heavy items' rows): 16.4 instead of 26.6 KB per workgroup, so LDS no longer caps the launch at
-  // 6 workgroups per CU
-  constexpr size_t kLdsBytes = sizeof(unsigned) * kRankHash > sizeof(HeavyLds) ? sizeof(unsigned) * kRankHash
-                                                                                : sizeof(HeavyLds);
-  __shared__ __align__(16) unsigned char s_lds[kLdsBytes];
   const int nr = a.rank.nblocks;
   // where the hosted rank workgroups sit in dispatch order (build knob DSSM_RANK_POS): 1 (default)
   // last, after the streaming blocks; 0 first; 2 right after the heavy items
 #if DSSM_RANK_POS == 0
   const int rs = 0;
 #elif DSSM_RANK_POS == 1
-  const int rs = (int)gridDim.x - nr;
+  const int rs = (int)nblk - nr;
 #else
   const int rs = a.item_blocks;
 #endif
-  const int bx = blockIdx.x;
+  const int bx = blk;
   const bool is_rank = bx >= rs && bx < rs + nr;
   const int b0 = bx < rs ? bx : bx - nr;
   const int nh = a.item_blocks, nw = a.w1_blocks, nd = a.dense_blocks;
@@ -555,13 +557,13 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
     // Two-level ticket: same-address atomics serialise (~6 ns each; one counter for ~8k blocks
     // measured +45 us), so blocks arrive on kAdamSubTickets counters 256 B apart and only the
     // last arrival of each moves the top counter.
-    const unsigned k = blockIdx.x % kAdamSubTickets;
-    const unsigned nk = gridDim.x / kAdamSubTickets + (k < gridDim.x % kAdamSubTickets ? 1u : 0u);
+    const unsigned k = (unsigned)blk % kAdamSubTickets;
+    const unsigned nk = nblk / kAdamSubTickets + (k < nblk % kAdamSubTickets ? 1u : 0u);
     unsigned* sub = a.ticket + 64 * (k + 1);
     const unsigned t = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == nk - 1) {
       __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned ntop = min(gridDim.x, (unsigned)kAdamSubTickets);
+      const unsigned ntop = min(nblk, (unsigned)kAdamSubTickets);
       const unsigned u =
           __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (u == ntop - 1) {
@@ -583,6 +585,24 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
       }
     }
   }
+}
+
+template <typename TZ, bool WIRE>
+__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
+  __shared__ __align__(16) unsigned char s_lds[kAdamLdsBytes];
+  adam_step_body<TZ, WIRE>(a, blockIdx.x, gridDim.x, s_lds);
+}
+
+// Two optimizer steps in one launch (the multi-view model's two trained towers): workgroups [0, na)
+// run a's roles, the rest b's, each part with its own tickets; a group ticket lets the later part
+// advance the beta powers.
+template <typename TZ>
+__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step2(AdamStep a, AdamStep b, int na) {
+  __shared__ __align__(16) unsigned char s_lds[kAdamLdsBytes];
+  if ((int)blockIdx.x < na)
+    adam_step_body<TZ, false>(a, blockIdx.x, (unsigned)na, s_lds);
+  else
+    adam_step_body<TZ, false>(b, (int)blockIdx.x - na, gridDim.x - (unsigned)na, s_lds);
 }
 
 __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p, ShadowSeg g) {
@@ -710,7 +730,8 @@ int grid_for(int64_t n4) {
 
 }  // namespace
 
-hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
+// the launch geometry of one step (block counts by role), checked
+static hipError_t prepare_adam_step(AdamStep& a) {
   if ((a.d4_begin < 0) || (a.d4_end < a.d4_begin)) return hipErrorInvalidValue;
   a.b1c = 1.0f - a.beta1;
   a.b2c = 1.0f - a.beta2;
@@ -731,6 +752,12 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + (a.w1_flat ? flat_rows * a.n / 4 : 0);
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
+  return hipSuccess;
+}
+
+hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
+  const hipError_t pe = prepare_adam_step(a);
+  if (pe != hipSuccess) return pe;
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g;
 #define DSSM_ADAM_LAUNCH(TZ)                                                         \
@@ -742,6 +769,22 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     DSSM_ADAM_LAUNCH(float);
   }
 #undef DSSM_ADAM_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_adam_step2(AdamStep a, AdamStep b, bool dz_bf16, hipStream_t s) {
+  hipError_t e = prepare_adam_step(a);
+  if (e == hipSuccess) e = prepare_adam_step(b);
+  if (e != hipSuccess) return e;
+  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g ||
+                    b.gout || b.wchunk >= 0 || b.wire4 > 0 || b.gstage || b.gwire || b.pwire || b.slab_to_g;
+  if (wire) return hipErrorInvalidValue;  // single-GPU parts only
+  const int na = a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks;
+  const int nb = b.rank.nblocks + b.item_blocks + b.w1_blocks + b.dense_blocks;
+  if (dz_bf16)
+    hipLaunchKernelGGL((k_adam_step2<u16>), dim3(na + nb), dim3(256), 0, s, a, b, na);
+  else
+    hipLaunchKernelGGL((k_adam_step2<float>), dim3(na + nb), dim3(256), 0, s, a, b, na);
   return hipGetLastError();
 }
 

@@ -326,49 +326,49 @@ size_t dssm_adam_tickets_bytes(int group) {
   return group <= 0 ? 0 : (64 + (size_t)group * dssm::kAdamTicketUints) * sizeof(unsigned);
 }
 
-int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
-                         int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
-                         float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
-                         int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
-                         float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
-                         int group, int member, void* tickets, int build_csc, void* ws, void* stream) {
-  const int64_t w1_end = (int64_t)(D + 1) * n;
-  if (!indptr || !dZ || !p || !g || !m || !v || !state || !ws || rows <= 0 || D <= 0 || n <= 0 || (n % 4) ||
-      lddz < n || (lddz % 8) || (max_nnz && (!indices || !values)) || (dz_dtype != DSSM_F32 && dz_dtype != DSSM_BF16) ||
-      rest_begin % 4 || rest_end % 4 || rest_begin < w1_end || rest_end < rest_begin || splits < 0 ||
-      (splits && (!slab || slab_count <= 0 || slab_count % 4 || rest_begin + slab_count > rest_end)) ||
-      (w1_shadow && (ld_shadow < n || ld_shadow % 4)) || nseg < 0 || nseg > 4 || (nseg && !segs) || group < 0 ||
-      (group && (!tickets || member < 0 || member >= group)))
+}  // extern "C"
+
+namespace {
+// One tower's optimizer step (validated; its CSC transpose built first when asked) as an AdamStep.
+int tower_step(const dssm_tower_adam& t, float lr, float beta1, float beta2, float eps, float* state,
+               float grad_scale, int group, int member, void* tickets, hipStream_t s, dssm::AdamStep& a) {
+  const int D = t.D, n = t.n, rows = t.rows, max_nnz = t.max_nnz;
+  const int64_t w1_end = (int64_t)(D + 1) * n, rest_begin = t.rest_begin, rest_end = t.rest_end;
+  if (!t.indptr || !t.dZ || !t.p || !t.g || !t.m || !t.v || !state || !t.ws || rows <= 0 || D <= 0 || n <= 0 ||
+      (n % 4) || t.lddz < n || (t.lddz % 8) || (max_nnz && (!t.indices || !t.values)) ||
+      (t.dz_dtype != DSSM_F32 && t.dz_dtype != DSSM_BF16) || rest_begin % 4 || rest_end % 4 || rest_begin < w1_end ||
+      rest_end < rest_begin || t.splits < 0 ||
+      (t.splits && (!t.slab || t.slab_count <= 0 || t.slab_count % 4 || rest_begin + t.slab_count > rest_end)) ||
+      (t.w1_shadow && (t.ld_shadow < n || t.ld_shadow % 4)) || t.nseg < 0 || t.nseg > 4 || (t.nseg && !t.segs) ||
+      group < 0 || (group && (!tickets || member < 0 || member >= group)))
     return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: bad argument");
   if (!dssm::csc_rank_supported(D)) return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: D beyond the CSC rank path");
-  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
-       reinterpret_cast<uintptr_t>(v)) % 16)
+  if ((reinterpret_cast<uintptr_t>(t.p) | reinterpret_cast<uintptr_t>(t.g) | reinterpret_cast<uintptr_t>(t.m) |
+       reinterpret_cast<uintptr_t>(t.v)) % 16)
     return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: arrays must be 16-B aligned");
-  hipStream_t s = (hipStream_t)stream;
   const SpmmWs w = spmm_ws(rows, D, max_nnz);
-  char* b = static_cast<char*>(ws);
+  char* b = static_cast<char*>(t.ws);
   int* scratch = reinterpret_cast<int*>(b + w.scratch);
   int* col_ptr = reinterpret_cast<int*>(b + w.col_ptr);
   int* crow = reinterpret_cast<int*>(b + w.row);
   float* cval = reinterpret_cast<float*>(b + w.val);
   int* ccol = reinterpret_cast<int*>(b + w.col);
-  hipError_t e = hipSuccess;
-  if (build_csc) {
-    e = dssm::launch_csc_build(indptr, indices, values, rows, D, max_nnz, scratch, col_ptr, crow, cval, ccol, s,
-                               nullptr, 0, true, false);
+  if (t.build_csc) {
+    const hipError_t e = dssm::launch_csc_build(t.indptr, t.indices, t.values, rows, D, max_nnz, scratch, col_ptr,
+                                                crow, cval, ccol, s, nullptr, 0, true, false);
     if (e != hipSuccess) return oerr(DSSM_E_HIP, hipGetErrorString(e));
   }
-  dssm::AdamStep a{};
-  a.p = p;
-  a.g = g;
-  a.m = m;
-  a.v = v;
+  a = dssm::AdamStep{};
+  a.p = t.p;
+  a.g = t.g;
+  a.m = t.m;
+  a.v = t.v;
   a.st = state;
   if (group) {  // member's own two-level ticket after the group counter (dssm_adam_tickets_bytes)
-    unsigned* t = static_cast<unsigned*>(tickets);
-    a.group_ticket = t;
+    unsigned* tk = static_cast<unsigned*>(tickets);
+    a.group_ticket = tk;
     a.group_n = group;
-    a.ticket = t + 64 + (size_t)member * dssm::kAdamTicketUints;
+    a.ticket = tk + 64 + (size_t)member * dssm::kAdamTicketUints;
   } else {
     a.no_advance = 1;
   }
@@ -383,10 +383,10 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
   a.col_ptr = col_ptr;
   a.csc_row = crow;
   a.csc_val = cval;
-  a.dZ = dZ;
-  a.lddz = lddz;
-  a.shadow = w1_shadow;
-  a.ldsh = ld_shadow;
+  a.dZ = t.dZ;
+  a.lddz = t.lddz;
+  a.shadow = t.w1_shadow;
+  a.ldsh = t.ld_shadow;
   a.item_blocks = dssm::kAdamItemBlocks;
   a.heavy_n = dssm::csc_heavy_count(scratch, D, max_nnz);
   a.heavy_items = reinterpret_cast<const int2*>(a.heavy_n + 64);
@@ -394,20 +394,56 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
   a.d4_begin = rest_begin / 4;
   a.d4_end = rest_end / 4;
   a.clear_from = rest_end;  // the rest's gradient is rewritten by the next backward
-  a.sh.count = nseg;
-  for (int i = 0; i < nseg; ++i) {
-    const dssm_shadow_seg& q = segs[i];
+  a.sh.count = t.nseg;
+  for (int i = 0; i < t.nseg; ++i) {
+    const dssm_shadow_seg& q = t.segs[i];
     if (!q.ptr || q.offset < rest_begin || q.rows < 0 || q.cols <= 0 || q.ld < q.cols || q.offset % 4 || q.cols % 4 ||
         q.ld % 4 || q.offset + q.rows * q.cols > rest_end)
       return oerr(DSSM_E_INVALID, "spmm_bwd_w_adam: bad shadow segment");
     a.sh.seg[i] = dssm::ShadowSeg{q.offset, q.rows, q.cols, q.ld, q.ptr, nullptr, 0};
   }
-  if (splits) {
+  if (t.splits) {
     a.slabs.count = 1;
-    a.slabs.seg[0] = dssm::SlabSeg{rest_begin, slab_count, splits, slab};
+    a.slabs.seg[0] = dssm::SlabSeg{rest_begin, t.slab_count, t.splits, t.slab};
   }
+  return DSSM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const float* values, int rows, int D,
+                         int max_nnz, const void* dZ, int dz_dtype, int lddz, int n, float* p, float* g, float* m,
+                         float* v, int64_t rest_begin, int64_t rest_end, const float* slab, int64_t slab_count,
+                         int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
+                         float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
+                         int group, int member, void* tickets, int build_csc, void* ws, void* stream) {
+  const dssm_tower_adam t{indptr, indices, values, rows, D, max_nnz, dZ, dz_dtype, lddz, n, p, g, m, v,
+                          rest_begin, rest_end, slab, slab_count, splits, w1_shadow, ld_shadow, segs, nseg,
+                          build_csc, ws};
+  hipStream_t s = (hipStream_t)stream;
+  dssm::AdamStep a;
+  const int rc = tower_step(t, lr, beta1, beta2, eps, state, grad_scale, group, member, tickets, s, a);
+  if (rc != DSSM_OK) return rc;
   const bool probe = dssm::adam_probe_begin(s);
-  e = dssm::launch_adam_step(a, dz_dtype == DSSM_BF16, s);
+  const hipError_t e = dssm::launch_adam_step(a, dz_dtype == DSSM_BF16, s);
+  if (probe) dssm::adam_probe_end(s);
+  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
+}
+
+int dssm_towers_adam(const dssm_tower_adam* towers, int ntowers, float lr, float beta1, float beta2, float eps,
+                     float* state, float grad_scale, void* tickets, void* stream) {
+  if (!towers || ntowers < 1 || ntowers > 2 || !tickets || (ntowers == 2 && towers[0].dz_dtype != towers[1].dz_dtype))
+    return oerr(DSSM_E_INVALID, "towers_adam: 1 or 2 towers of one dZ dtype, tickets");
+  hipStream_t s = (hipStream_t)stream;
+  dssm::AdamStep a[2];
+  for (int k = 0; k < ntowers; ++k) {
+    const int rc = tower_step(towers[k], lr, beta1, beta2, eps, state, grad_scale, ntowers, k, tickets, s, a[k]);
+    if (rc != DSSM_OK) return rc;
+  }
+  const bool bf = towers[0].dz_dtype == DSSM_BF16;
+  const bool probe = dssm::adam_probe_begin(s);
+  const hipError_t e = ntowers == 1 ? dssm::launch_adam_step(a[0], bf, s) : dssm::launch_adam_step2(a[0], a[1], bf, s);
   if (probe) dssm::adam_probe_end(s);
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
