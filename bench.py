@@ -528,8 +528,7 @@ def bench_multiview(args):
     check(m.lib.dssm_adam_probe_read(C.byref(avg), C.byref(cnt)), "adam_probe_read")
     adam_ms = avg.value  # per launch
     span_ms = None
-    pair = m.fused_w1_adam and getattr(m, "adam_pair", False)
-    if m.fused_w1_adam and not pair and cnt.value >= 2:
+    if m.fused_w1_adam and cnt.value >= 2:
         # the two towers' launches run concurrently (two streams): the roofline is over the pair's
         # wall span (latest end - earliest start), each step's pair of recorded launches
         spans = []
@@ -552,9 +551,6 @@ def bench_multiview(args):
         zb = 2 if args.dtype == "bf16" else 4
         adam_bytes = int(24 * tower_params + 4 * splits * w2 + (nnz + B) * (8 + zb * L1) + 2 * shadow_elems)
         adam_kernel = "k_adam_step<unsigned short, false>" if args.dtype == "bf16" else "k_adam_step<float, false>"
-        if pair:  # both towers in one launch (dssm_towers_adam): the launch moves both towers' bytes
-            adam_bytes *= 2
-            adam_kernel = "k_adam_step2<unsigned short>" if args.dtype == "bf16" else "k_adam_step2<float>"
     else:
         # p, m, v read + written (24 B) and the fp32 gradient read (4 B) per parameter of the tower; bf16
         # mode: + 2 B per weight written to its shadow, and ONE launch updates both trained towers

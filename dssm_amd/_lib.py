@@ -42,16 +42,6 @@ class dssm_shadow_seg(C.Structure):
     _fields_ = [("offset", C.c_int64), ("rows", C.c_int64), ("cols", C.c_int), ("ld", C.c_int), ("ptr", C.c_void_p)]
 
 
-class dssm_tower_adam(C.Structure):
-    """include/dssm.h dssm_tower_adam: one tower's arguments of dssm_towers_adam."""
-    _fields_ = [("indptr", C.c_void_p), ("indices", C.c_void_p), ("values", C.c_void_p), ("rows", C.c_int),
-                ("D", C.c_int), ("max_nnz", C.c_int), ("dZ", C.c_void_p), ("dz_dtype", C.c_int), ("lddz", C.c_int),
-                ("n", C.c_int), ("p", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p),
-                ("rest_begin", C.c_int64), ("rest_end", C.c_int64), ("slab", C.c_void_p), ("slab_count", C.c_int64),
-                ("splits", C.c_int), ("w1_shadow", C.c_void_p), ("ld_shadow", C.c_int), ("segs", C.c_void_p),
-                ("nseg", C.c_int), ("build_csc", C.c_int), ("ws", C.c_void_p)]
-
-
 class dssm_config(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int), ("trigram_d", C.c_int), ("n_layers", C.c_int),
@@ -197,7 +187,6 @@ _SIGS = {
                                        C.c_int, C.c_int, _P, C.c_int, _P, _P]),
     "dssm_spmm_bwd_csc": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "dssm_adam_tickets_bytes": (C.c_size_t, [C.c_int]),
-    "dssm_towers_adam": (C.c_int, [_P, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, _P, C.c_float, _P, _P]),
     "dssm_adam_probe_span": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "dssm_adam_advance": (C.c_int, [_P, C.c_float, C.c_float, _P]),
     "dssm_rows_gather": (C.c_int, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P]),

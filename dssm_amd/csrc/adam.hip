@@ -593,18 +593,6 @@ __global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step(AdamStep a) {
   adam_step_body<TZ, WIRE>(a, blockIdx.x, gridDim.x, s_lds);
 }
 
-// Two optimizer steps in one launch (the multi-view model's two trained towers): workgroups [0, na)
-// run a's roles, the rest b's, each part with its own tickets; a group ticket lets the later part
-// advance the beta powers.
-template <typename TZ>
-__global__ __launch_bounds__(256) DSSM_ADAM_ATTR void k_adam_step2(AdamStep a, AdamStep b, int na) {
-  __shared__ __align__(16) unsigned char s_lds[kAdamLdsBytes];
-  if ((int)blockIdx.x < na)
-    adam_step_body<TZ, false>(a, blockIdx.x, (unsigned)na, s_lds);
-  else
-    adam_step_body<TZ, false>(b, (int)blockIdx.x - na, gridDim.x - (unsigned)na, s_lds);
-}
-
 __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p, ShadowSeg g) {
   const int64_t n4 = g.rows * g.cols / 4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
@@ -769,22 +757,6 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
     DSSM_ADAM_LAUNCH(float);
   }
 #undef DSSM_ADAM_LAUNCH
-  return hipGetLastError();
-}
-
-hipError_t launch_adam_step2(AdamStep a, AdamStep b, bool dz_bf16, hipStream_t s) {
-  hipError_t e = prepare_adam_step(a);
-  if (e == hipSuccess) e = prepare_adam_step(b);
-  if (e != hipSuccess) return e;
-  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g ||
-                    b.gout || b.wchunk >= 0 || b.wire4 > 0 || b.gstage || b.gwire || b.pwire || b.slab_to_g;
-  if (wire) return hipErrorInvalidValue;  // single-GPU parts only
-  const int na = a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks;
-  const int nb = b.rank.nblocks + b.item_blocks + b.w1_blocks + b.dense_blocks;
-  if (dz_bf16)
-    hipLaunchKernelGGL((k_adam_step2<u16>), dim3(na + nb), dim3(256), 0, s, a, b, na);
-  else
-    hipLaunchKernelGGL((k_adam_step2<float>), dim3(na + nb), dim3(256), 0, s, a, b, na);
   return hipGetLastError();
 }
 

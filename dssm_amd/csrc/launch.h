@@ -321,9 +321,6 @@ struct AdamStep {
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
-// two single-GPU steps (e.g. two towers, each with its own ticket and a shared group ticket) in ONE
-// launch: a's workgroups, then b's
-hipError_t launch_adam_step2(AdamStep a, AdamStep b, bool dz_bf16, hipStream_t s);
 // a timing probe's event (plan.hip): hipEventRecord, or an event-record node while s is capturing
 void record_probe_event(hipStream_t s, hipEvent_t e);
 hipError_t launch_shadow_sync(const float* p, ShadowList sh, hipStream_t s);

@@ -431,23 +431,6 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
   return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
 }
 
-int dssm_towers_adam(const dssm_tower_adam* towers, int ntowers, float lr, float beta1, float beta2, float eps,
-                     float* state, float grad_scale, void* tickets, void* stream) {
-  if (!towers || ntowers < 1 || ntowers > 2 || !tickets || (ntowers == 2 && towers[0].dz_dtype != towers[1].dz_dtype))
-    return oerr(DSSM_E_INVALID, "towers_adam: 1 or 2 towers of one dZ dtype, tickets");
-  hipStream_t s = (hipStream_t)stream;
-  dssm::AdamStep a[2];
-  for (int k = 0; k < ntowers; ++k) {
-    const int rc = tower_step(towers[k], lr, beta1, beta2, eps, state, grad_scale, ntowers, k, tickets, s, a[k]);
-    if (rc != DSSM_OK) return rc;
-  }
-  const bool bf = towers[0].dz_dtype == DSSM_BF16;
-  const bool probe = dssm::adam_probe_begin(s);
-  const hipError_t e = ntowers == 1 ? dssm::launch_adam_step(a[0], bf, s) : dssm::launch_adam_step2(a[0], a[1], bf, s);
-  if (probe) dssm::adam_probe_end(s);
-  return e == hipSuccess ? DSSM_OK : oerr(DSSM_E_HIP, hipGetErrorString(e));
-}
-
 int dssm_dense_bwd_masked(const void* A, int lda, const void* W, int ldw, int dtype, int M, int K, int N,
                           const void* dZ, int lddz, float* dA, int ldda, const float* mask, int ldmask,
                           float* dWb, float* slab, void* stream) {

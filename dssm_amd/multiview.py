@@ -28,7 +28,6 @@ it always trains view 3; here the fed active view selects 
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -121,9 +120,6 @@ class MultiViewDSSM:
         # finish advances the beta powers (no advance launch, no join in front of it)
         self.adam_tickets = torch.zeros(int(self.lib.dssm_adam_tickets_bytes(2)), dtype=torch.uint8, device=dev)
         self.fused_w1_adam = fused_w1_adam
-        # fused: both towers' optimizer steps in one launch after the backward (True) or one launch per
-        # tower on its backward's stream (False)
-        self.adam_pair = os.environ.get("DSSM_MV_ADAM_PAIR", "1") == "1"
         self.set_rotations(rotations if rotations is not None else self.default_rotations(seed))
         self.global_step = 0
 
@@ -321,30 +317,6 @@ class MultiViewDSSM:
         check(self.lib.dssm_spmm_bwd_csc(ptr(ip), ptr(ix), ptr(vv), self.bs, self.dims[TOWERS.index(tower)],
                                          self.max_nnz, ptr(self.spmm_ws[tower]), s), "spmm_bwd_csc")
 
-    def _tower_args(self, key, tower, build_csc):
-        """dssm_tower_adam of one trained tower (the optimizer's view of its blocks)."""
-        ip, ix, vv = self.batch[key]
-        d = self.dims[TOWERS.index(tower)]
-        b, e = self.layout[tower]
-        off2 = self.layout[f"{tower}_2"][0] - b
-        t = _lib.dssm_tower_adam()
-        t.indptr, t.indices, t.values = ptr(ip), ptr(ix), ptr(vv)
-        t.rows, t.D, t.max_nnz = self.bs, d, self.max_nnz
-        t.dZ, t.dz_dtype, t.lddz, t.n = ptr(self.dz1[key]), self._dt, self.ld1, self.l1
-        t.p, t.g = ptr(self.params[b:]), ptr(self.grads[b:])
-        t.m, t.v = ptr(self.adam_m[b:]), ptr(self.adam_v[b:])
-        t.rest_begin, t.rest_end = off2, e - b
-        splits = self._splits[key].value
-        t.slab, t.slab_count, t.splits = (ptr(self.slab[key]) if splits else None), (self.l1 + 1) * self.l2, splits
-        segs = None
-        if self.bf16:
-            sh2 = self.shadow[f"{tower}_2"]
-            segs = (_lib.dssm_shadow_seg * 1)(_lib.dssm_shadow_seg(off2, self.l1, self.l2, sh2.shape[1], sh2.data_ptr()))
-            t.w1_shadow, t.ld_shadow = ptr(self.shadow[f"{tower}_1"]), self.ld1
-            t.segs, t.nseg = C.cast(segs, C.c_void_p), 1
-        t.build_csc, t.ws = int(build_csc), ptr(self.spmm_ws[tower])
-        return t, segs  # (segs: kept alive by the caller until the call)
-
     def _tower_adam(self, key, tower, s, grad_scale, member, build_csc):
         """Fused mode: one tower's CSC transpose + ONE optimizer launch over its [W1; b1] rows (the
         gradient gathered inline) and its [W2; b2] block (FC2's split-K partials summed inline)."""
@@ -378,23 +350,13 @@ class MultiViewDSSM:
                 self._fork(main)
             self._adam_pending = False
             # (both on one stream, each tower's transpose + launch in turn: 0.292 against 0.257 ms/step;
-            # one launch takes 68 us alone, the concurrent pair 128 us)
+            # both towers in ONE launch after a join, commit history: 0.251-0.254 against 0.240-0.242)
             built = getattr(self, "_csc_ev", None) is not None  # transposed by forward() on self.aux
-            if self.adam_pair:
-                # both towers in ONE launch (dssm_towers_adam) once both backwards are done
-                main.wait_stream(self.aux)
-                tu, su = self._tower_args("u", towers[0], not built)
-                ti, si = self._tower_args("i", towers[1], not built)
-                arr = (_lib.dssm_tower_adam * 2)(tu, ti)
-                check(self.lib.dssm_towers_adam(arr, 2, self.lr, 0.9, 0.999, 1e-8, ptr(self.adam_state), grad_scale,
-                                                ptr(self.adam_tickets), stream_ptr(main)), "towers_adam")
-                del su, si
-            else:
-                if built:
-                    main.wait_event(self._csc_ev)
-                self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0, not built)
-                self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1, not built)
-                main.wait_stream(self.aux)
+            if built:
+                main.wait_event(self._csc_ev)
+            self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0, not built)
+            self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1, not built)
+            main.wait_stream(self.aux)
             self._csc_ev = None
         elif self.bf16:
             # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass

@@ -416,10 +416,7 @@ int dssm_spmm_bwd_w_adam(const int32_t* indptr, const int32_t* indices, const fl
                          int splits, uint16_t* w1_shadow, int ld_shadow, const dssm_shadow_seg* segs, int nseg,
                          float lr, float beta1, float beta2, float eps, float* state, float grad_scale,
                          int group, int member, void* tickets, int build_csc, void* ws, void* stream);
-/* The same for one or two towers in ONE launch (the multi-view model's trained towers: the second
- * tower's workgroups follow the first's; each tower's arguments as dssm_spmm_bwd_w_adam's), the beta
- * powers advanced once by the later tower: tickets = dssm_adam_tickets_bytes(ntowers) bytes,
- * zero-filled once.  Both towers' dZ of one dtype. */
+/* (dssm_tower_adam: the per-tower arguments above as one record, the form the C++ side validates) */
 typedef struct dssm_tower_adam {
   const int32_t* indptr;
   const int32_t* indices;
@@ -439,8 +436,6 @@ typedef struct dssm_tower_adam {
   int build_csc;
   void* ws;
 } dssm_tower_adam;
-int dssm_towers_adam(const dssm_tower_adam* towers, int ntowers, float lr, float beta1, float beta2, float eps,
-                     float* state, float grad_scale, void* tickets, void* stream);
 /* TF1.x AdamOptimizer._finish: beta1_power *= beta1, beta2_power *= beta2 (state on the device). */
 int dssm_adam_advance(float* state, float beta1, float beta2, void* stream);
 /* Measurement: HIP events around the next n_max dssm_adam_step optimizer launches (0: off); read
