@@ -721,185 +721,6 @@ __global__ __launch_bounds__(512) void k_rnn_dw(DwArgs a) {
   }
 }
 
-// E = H = 128 (config 4): the six tiles of a direction as three PAIRS sharing a panel -- (x, dr) +
-// (x, du), (h, dr) + (h, du), (x, dc) + (r*h, dc) -- so a workgroup reads 3 panels for 2 tiles (9 panel
-// reads per row and direction instead of the 12-tile launch's 12).  8 waves: waves 0-3 the first tile,
-// 4-7 the second, each 64 x 64 (acc 4 x 4).  Same swizzled 64-row slabs and transposing fragment reads
-// as k_rnn_dw; 96 KB of LDS (one workgroup per CU), one round of 6 x splits workgroups.
-struct DwPanel {
-  const u16* base;  // row k at base + k * ld (+ col0)
-  int ld, col0, gather;  // gather: rows of the bf16 embedding by token (the x panel)
-};
-struct DwPair {
-  DwPanel p[3];
-  int shared_b;  // 0: tiles (p0, p1), (p0, p2); 1: tiles (p0, p2), (p1, p2)
-};
-struct DwPairArgs {
-  DwPair q[6];  // [dir * 3 + pair]
-  const int* tok;
-  int TR, splits, kps;
-  float* slab;  // [split][6][2 * 16384 + 2 * 128]
-};
-constexpr int kDwPairPart = 2 * 16384 + 2 * 128;
-#ifndef DSSM_RNN_DW_PAIR
-#define DSSM_RNN_DW_PAIR 1
-#endif
-
-__global__ __launch_bounds__(512) void k_rnn_dw_pair(DwPairArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 sP[2][3][64 * 128];
-  const int W = a.splits * 6;
-  const int L = (W % 8 == 0) ? (int)(blockIdx.x % 8) * (W / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const int qi = L % 6, split = L / 6, dir = qi / 3;
-  const DwPair& Q = ((const DwPairArgs*)__builtin_amdgcn_kernarg_segment_ptr())->q[qi];
-  const int* tok = a.tok + (size_t)dir * a.TR;
-  const int kbeg = split * a.kps, kend = min(a.TR, kbeg + a.kps);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int tt = w >> 2, wm = (w >> 1) & 1, wn = w & 1;
-  const int pa = Q.shared_b ? tt : 0, pb = Q.shared_b ? 2 : 1 + tt;  // this wave's A / B panel
-  const bool dobias = wm == 0 && (!Q.shared_b || tt == 0);             // wave-uniform
-  struct Set {
-    uint4 v[3][2];
-  };
-  const int ch = tid & 15, row0 = tid >> 4;  // chunk ch of rows row0, row0 + 32
-  auto tok1 = [&](int k) { return k < kend ? tok[k] : 0; };
-  int tk0 = tok1(kbeg + row0), tk1 = tok1(kbeg + row0 + 32);
-  auto load = [&](int k0) {
-    Set r;
-#pragma unroll
-    for (int pn = 0; pn < 3; ++pn) {
-      const DwPanel& P = Q.p[pn];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = k0 + row0 + 32 * h;
-        const int rowsel = P.gather ? (h ? tk1 : tk0) : k;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < kend) v = *reinterpret_cast<const uint4*>(P.base + (size_t)rowsel * P.ld + P.col0 + ch * 8);
-        r.v[pn][h] = v;
-      }
-    }
-    tk0 = tok1(k0 + 64 + row0);
-    tk1 = tok1(k0 + 64 + row0 + 32);
-    return r;
-  };
-  const int o0 = dw_off(row0, ch), o1 = dw_off(row0 + 32, ch);
-  auto store = [&](int buf, const Set& r) {
-#pragma unroll
-    for (int pn = 0; pn < 3; ++pn) {
-      *reinterpret_cast<uint4*>(&sP[buf][pn][o0]) = r.v[pn][0];
-      *reinterpret_cast<uint4*>(&sP[buf][pn][o1]) = r.v[pn][1];
-    }
-  };
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
-    const u16* SA = sP[buf][pa];
-    const u16* SB = sP[buf][pb];
-#pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = dw_frag(SA, 32 * kc, wm * 64 + 16 * i, g, q, p);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = dw_frag(SB, 32 * kc, wn * 64 + 16 * j, g, q, p);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      if (dobias) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bsum[j] += (float)bfr[j][e];
-      }
-    }
-  };
-  const int nst = kbeg < kend ? (kend - kbeg + 63) / 64 : 0;
-  Set r0{}, r1{};
-  if (nst > 0) r0 = load(kbeg);
-  if (nst > 1) r1 = load(kbeg + 64);
-  if (nst > 0) store(0, r0);
-  __syncthreads();
-  for (int s = 0; s < nst; s += 2) {
-    if (s + 2 < nst) r0 = load(kbeg + 64 * (s + 2));
-    compute(0);
-    if (s + 1 < nst) store(1, r1);
-    __syncthreads();
-    if (s + 1 >= nst) break;
-    if (s + 3 < nst) r1 = load(kbeg + 64 * (s + 3));
-    compute(1);
-    if (s + 2 < nst) store(0, r0);
-    __syncthreads();
-  }
-  float* out = a.slab + ((size_t)split * 6 + qi) * kDwPairPart;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out[(size_t)tt * 16384 + (size_t)(wm * 64 + 16 * i + 4 * g + r) * 128 + wn * 64 + 16 * j + li] = acc[i][j][r];
-  if (dobias) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = bsum[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (g == 0) out[2 * 16384 + tt * 128 + wn * 64 + 16 * j + li] = v;
-    }
-  }
-}
-
-// the splits summed in fixed order into [Wg; bg] ([257 x 256]) and [Wc; bc] ([257 x 128]) per direction
-struct DwPairDest {
-  float* wg[2];
-  float* wc[2];
-};
-__global__ __launch_bounds__(256) void k_rnn_dw_pair_reduce(const float* __restrict__ slab, int splits, DwPairDest d) {
-  constexpr int q4 = kDwPairPart / 4;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 6 * q4; e += gridDim.x * blockDim.x) {
-    const int qi = e / q4, i = 4 * (e - qi * q4), dir = qi / 3, pr = qi % 3;
-    if (pr == 2 && i >= 2 * 16384 + 128) continue;  // the (x, dc) + (r*h, dc) pair has one bias row
-    const float* src = slab + (size_t)qi * kDwPairPart + i;
-    const size_t stride = (size_t)6 * kDwPairPart;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    int sp = 0;
-    for (; sp + 8 <= splits; sp += 8) {  // eight loads in flight, added in split order
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(sp + u) * stride);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
-      }
-    }
-    for (; sp < splits; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * stride);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    float* wg = dir ? d.wg[1] : d.wg[0];
-    float* wc = dir ? d.wc[1] : d.wc[0];
-    float* dst;
-    if (i < 2 * 16384) {
-      const int t = i >> 14, m = (i >> 7) & 127, n = i & 127;
-      if (pr == 0) dst = wg + (size_t)m * 256 + 128 * t + n;               // x: dr | du
-      else if (pr == 1) dst = wg + (size_t)(128 + m) * 256 + 128 * t + n;  // h: dr | du
-      else dst = wc + (size_t)(128 * t + m) * 128 + n;                     // x, r*h: dc
-    } else {
-      const int t = (i - 2 * 16384) >> 7, n = (i - 2 * 16384) & 127;
-      if (pr == 0) dst = wg + (size_t)256 * 256 + 128 * t + n;  // bias of dr | du
-      else if (pr == 1) continue;                               // (the same sums as pair 0)
-      else dst = wc + (size_t)256 * 128 + n;                    // bias of dc
-    }
-    *reinterpret_cast<float4*>(dst) = s;
-  }
-}
-
 // sum the splits in fixed order into the destinations (rows < mlen, columns < nlen; row 128 = bias)
 __global__ __launch_bounds__(256) void k_rnn_dw_reduce(DwArgs a) {
   const int per_tile = kDwSlabRows * 32;  // float4 groups
@@ -939,9 +760,6 @@ __global__ void k_to_bf16(const float* __restrict__ x, u16* __restrict__ y, int6
 }
 
 // ---- workspace and dispatch -------------------------------------------------------------------
-#ifndef DSSM_RNN_DW_PAIR_WGS  // workgroups of one k_rnn_dw_pair launch (pairs x row splits): 1 per CU
-#define DSSM_RNN_DW_PAIR_WGS 256
-#endif
 #ifndef DSSM_RNN_DW_WGS  // workgroups of one k_rnn_dw launch (tiles x row splits): 2 per CU
 #define DSSM_RNN_DW_WGS 512
 #endif
@@ -951,7 +769,7 @@ struct WsB {
   u16 *HS, *RH, *GA, *GC, *DG, *DC, *DX, *emb16;
   int *TOK, *cnt, *start, *rank, *pos;
   float* slab;
-  size_t slab_bytes, bytes, emb16_off;
+  size_t bytes, emb16_off;
 };
 
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -979,8 +797,7 @@ WsB ws_layout(char* base, int R, int T, int E, int H, int V) {
   w.start = (int*)take(((size_t)V + 1) * 4);
   w.rank = (int*)take(TR * 4);
   w.pos = (int*)take(TR * 4);
-  w.slab_bytes = (size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128 * 4;
-  w.slab = (float*)take(w.slab_bytes);
+  w.slab = (float*)take((size_t)kDwMaxSplits * kDwMaxTiles * kDwSlabRows * 128 * 4);
   w.bytes = off;
   return w;
 }
@@ -1134,37 +951,10 @@ int dssm_rnn_bf16_backward(const int32_t* ids, const int32_t* lens, int R, int T
     hipLaunchKernelGGL(dssm::k_emb_grad<64>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
   else
     hipLaunchKernelGGL(dssm::k_emb_grad<32>, gemb, dim3(256), 0, s, L.start, L.pos, lens, R, T, V, L.DX, demb);
-  const int TR = T * R;
-  if (E == 128 && H == 128 && DSSM_RNN_DW_PAIR) {
-    // the six tiles per direction as three panel-sharing pairs (k_rnn_dw_pair) + the split reduce
-    dssm::DwPairArgs B{};
-    for (int dir = 0; dir < 2; ++dir) {
-      const size_t hf = (size_t)TR * dir;
-      const dssm::DwPanel x{L.emb16, 128, 0, 1}, hh{L.HS + hf * 128, 128, 0, 0}, rh{L.RH + hf * 128, 128, 0, 0},
-          dr{L.DG + hf * 256, 256, 0, 0}, du{L.DG + hf * 256, 256, 128, 0}, dc{L.DC + hf * 128, 128, 0, 0};
-      B.q[dir * 3 + 0] = dssm::DwPair{{x, dr, du}, 0};
-      B.q[dir * 3 + 1] = dssm::DwPair{{hh, dr, du}, 0};
-      B.q[dir * 3 + 2] = dssm::DwPair{{x, rh, dc}, 1};
-    }
-    B.tok = L.TOK;
-    B.TR = TR;
-    B.splits = std::max(2, std::min(DSSM_RNN_DW_PAIR_WGS / 6, (int)((L.slab_bytes / 4) / (6 * (size_t)dssm::kDwPairPart))));
-    B.splits -= B.splits & 1;  // 6 * splits % 8 == 0 for the XCD grouping needs splits % 4 == 0
-    B.splits -= B.splits % 4;
-    B.splits = std::max(B.splits, 4);
-    B.kps = ((TR + B.splits - 1) / B.splits + 63) / 64 * 64;
-    B.slab = L.slab;
-    hipLaunchKernelGGL(dssm::k_rnn_dw_pair, dim3(B.splits * 6), dim3(512), 0, s, B);
-    const dssm::DwPairDest Dd{{gw[0], gw[2]}, {gw[1], gw[3]}};
-    hipLaunchKernelGGL(dssm::k_rnn_dw_pair_reduce, dim3((6 * dssm::kDwPairPart / 4 + 255) / 256), dim3(256), 0, s,
-                       L.slab, B.splits, Dd);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? DSSM_OK : rerr_b(DSSM_E_HIP, hipGetErrorString(e));
-  }
   // [W; b] gradients, both directions in one launch (k_rnn_dw) + a fixed-order split reduce:
   //   dWg = [x | h]^T [dr | du] (+ bias = column sums),  dWc rows [0, E) = x^T dc (+ bias),
   //   dWc rows [E, E+H) = (r*h)^T dc
-  const int K = E + H;
+  const int K = E + H, TR = T * R;
   dssm::DwArgs A{};
   int n = 0;
   for (int dir = 0; dir < 2; ++dir) {
