@@ -25,19 +25,26 @@ template <> struct RawRow8<u16> {
   }
 };
 // bf16 rows at a stride that is NOT a multiple of 8 elements (the data-parallel parameter wire:
-// W1 row-major at stride n = 300, read directly by the forward SpMM).  Such rows have no zero pads,
-// so a half group (nvalid == 4: the row's last 4 columns) loads the 16 B that END at the row's end
-// and keeps their upper half: no load reaches into the next row or past the buffer, and the lane's
-// upper 4 columns accumulate zeros.  Needs n >= 8 (launch_spmm_* check).  Loads are 8-B aligned.
+// W1 row-major at stride n = 300, read directly by the forward SpMM).  Such rows have no zero pads:
+// a half group (nvalid == 4: the row's last 4 columns) still loads 16 B -- its upper 8 B are the
+// next row's first columns, or for the buffer's last row the 8-element slack dssm_plan_dp_wire_size
+// includes -- and masks the upper half to zeros, so the lane's upper 4 columns accumulate zeros.
+// (Loading the 16 B that END at the row's end instead let the compiler narrow every gather to two
+// 8-B loads: the SpMM 19.8 -> 27.2 us.)  Loads are 8-B aligned.
 struct u16t {
   u16 bits;
 };
 template <> struct RawRow8<u16t> {
   RawRow8<u16> r;
   __device__ __forceinline__ void load(const u16t* p, int nvalid) {
-    const int back = nvalid >= 8 ? 0 : 4;
-    const uint4 x = *reinterpret_cast<const uint4*>(p - back);
-    r.a = back ? make_uint4(x.z, x.w, 0u, 0u) : x;
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+#ifdef DSSM_U16T_PLAIN  // diagnostics: the unmasked load (the upper half then reads the next row)
+    (void)nvalid;
+    r.a = x;
+#else
+    const unsigned keep = nvalid >= 8 ? 0xffffffffu : 0u;  // a value mask: the load stays one 16-B load
+    r.a = make_uint4(x.x, x.y, x.z & keep, x.w & keep);
+#endif
   }
   __device__ __forceinline__ void fma(float v, float (&acc)[8]) const { r.fma(v, acc); }
 };

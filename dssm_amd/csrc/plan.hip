@@ -1105,7 +1105,9 @@ static dssm::WireGeo dp_geo(const dssm_plan* P, int world, int chunks) {
 int64_t dssm_plan_dp_wire_size(const dssm_plan* P, int world, int chunks) {
   if (!P || world < 1 || chunks < 1) return -1;
   const dssm::WireGeo g = dp_geo(P, world, chunks);
-  return (int64_t)g.ww * g.wp * g.ws * g.n;
+  // + 8 elements of slack: the SpMM's tight-row reads of the parameter wire load up to 8 B past the
+  // last row (RawRow8<u16t>, masked)
+  return (int64_t)g.ww * g.wp * g.ws * g.n + 8;
 }
 
 int dssm_plan_set_dp_wire(dssm_plan* P, int world, int rank, int chunks, uint16_t* grad_wire,
