@@ -26,26 +26,19 @@ template <> struct RawRow8<u16> {
 };
 // bf16 rows at a stride that is NOT a multiple of 8 elements (the data-parallel parameter wire:
 // W1 row-major at stride n = 300, read directly by the forward SpMM).  Such rows have no zero pads:
-// a half group (nvalid == 4: the row's last 4 columns) still loads 16 B -- its upper 8 B are the
-// next row's first columns, or for the buffer's last row the 8-element slack dssm_plan_dp_wire_size
-// includes -- and masks the upper half to zeros, so the lane's upper 4 columns accumulate zeros.
-// (Loading the 16 B that END at the row's end instead let the compiler narrow every gather to two
-// 8-B loads: the SpMM 19.8 -> 27.2 us.)  Loads are 8-B aligned.
+// a half group (nvalid == 4: the row's last 4 columns) loads the full 16 B, whose upper 8 B are the
+// next row's first columns (for the buffer's last row: the 8-element slack dssm_plan_dp_wire_size
+// includes, and that dssm_spmm_csr_fwd documents for tight bf16 rows).  The lane's upper 4 sums are
+// garbage and spmm_rows zeroes them once per row after the gather.  Measured alternatives, both
+// slower because they add work to every gathered row: loading the 16 B that END at the row's end
+// (the compiler narrowed every gather to two 8-B loads: SpMM 19.8 -> 27.2 us) and masking the
+// upper half per load (25.9 us; the plain load: 20.2 us).  Loads are 8-B aligned.
 struct u16t {
   u16 bits;
 };
 template <> struct RawRow8<u16t> {
   RawRow8<u16> r;
-  __device__ __forceinline__ void load(const u16t* p, int nvalid) {
-    const uint4 x = *reinterpret_cast<const uint4*>(p);
-#ifdef DSSM_U16T_PLAIN  // diagnostics: the unmasked load (the upper half then reads the next row)
-    (void)nvalid;
-    r.a = x;
-#else
-    const unsigned keep = nvalid >= 8 ? 0xffffffffu : 0u;  // a value mask: the load stays one 16-B load
-    r.a = make_uint4(x.x, x.y, x.z & keep, x.w & keep);
-#endif
-  }
+  __device__ __forceinline__ void load(const u16t* p, int) { r.a = *reinterpret_cast<const uint4*>(p); }
   __device__ __forceinline__ void fma(float v, float (&acc)[8]) const { r.fma(v, acc); }
 };
 template <> struct RawRow8<float> {

@@ -19,6 +19,7 @@
 // W1 Adam kernel (adam.hip), which then never writes or re-reads a dense dW1.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "bnfuse.h"
 #include "common.h"
@@ -60,6 +61,10 @@ __device__ __forceinline__ void spmm_rows(const int* __restrict__ indptr,
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = (c + i < n) ? bias[c + i] : 0.f;
     gather_accumulate<TW, 1, DSSM_SPMM_U>(indices, values, s, e, W, ldw, c, nvalid, acc);
+    if constexpr (std::is_same<TW, u16t>::value) {  // tight rows: the half group's upper sums
+#pragma unroll
+      for (int i = 4; i < 8; ++i) acc[i] = (c + i < n) ? acc[i] : 0.f;  // read the next row (gather.h)
+    }
     if (relu) {  // the layer's ReLU fused (functional API: FC1 + tf.nn.relu)
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = fmaxf(acc[i], 0.f);
@@ -992,7 +997,7 @@ int eval_coef_blocks(const EvalCoef& e) {
 }
 
 // bf16 weight rows: padded to a multiple of 8 elements with zero pads (the shadows), or tight at
-// stride n (the parameter wire), which the u16t instances read without crossing a row's end
+// stride n (the parameter wire), whose last row the u16t instances read 8 B past (gather.h)
 static bool bf16_rows_ok(int ldw, int n) {
   if (ldw % 8 == 0) return ldw >= n;
   return ldw == n && n % 4 == 0 && n >= 8;

@@ -276,7 +276,9 @@ int dssm_plan_graph_topology(const dssm_plan* plan, int graph_id, int64_t* out);
 
 /* ---- fine-grained kernels (the functional API: add_layer / batch_normalization / cosine) -- */
 /* FC1 (new_dssm.py:124-126): Z[r, :] = sum_k values[k] * W[indices[k], :] + bias.
- * W: [d x ldw] of w_dtype (ldw >= n, multiple of 4); Z: [rows x ldz] fp32, ldz = ldp(n). */
+ * W: [d x ldw] of w_dtype (ldw >= n, multiple of 4); Z: [rows x ldz] fp32, ldz = ldp(n).  bf16 W
+ * with tight rows (ldw == n, not a multiple of 8: the parameter wire) needs 8 readable elements
+ * after its last row (dssm_plan_dp_wire_size includes them). */
 int dssm_spmm_csr_fwd(const int32_t* indptr, const int32_t* indices, const float* values, int rows,
                       const void* W, int w_dtype, int ldw, int n, const float* bias, float* Z,
                       int ldz, void* stream);
