@@ -493,7 +493,9 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
       FlatSlice f{a.p, a.m, a.v, a.shadow, a.ldsh, a.n, a.D, a.col_ptr, a.st, a.lr, a.b1c, a.b2c, a.eps,
                   0, (int64_t)(a.D + 1) * a.n / 4, a.dense_blocks};
+#ifndef DSSM_ADAM_SKIP_UNTOUCHED  // diagnostics build: the untouched rows' cost (wrong results)
       flat_untouched(f, bi);
+#endif
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
     if (WIRE && a.slab_to_g) {  // gradient pass: g = the deferred split-K slabs' sums (fixed order)
@@ -737,7 +739,11 @@ static hipError_t prepare_adam_step(AdamStep& a) {
   a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && (a.n % 4) == 0) ? 1 : 0;
   if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
   const int64_t flat_rows = a.wchunk < 0 ? (int64_t)a.D + 1 : (int64_t)a.geo.ww * a.geo.ws;
+#ifdef DSSM_ADAM_SKIP_UNTOUCHED
+  const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + 0 * flat_rows;
+#else
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + (a.w1_flat ? flat_rows * a.n / 4 : 0);
+#endif
   a.dense_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n4, 256), kAdamDenseBlocks));
   if (a.rank.nblocks && !a.ticket) return hipErrorInvalidValue;  // the hosted rank needs a whole step
   return hipSuccess;
