@@ -91,6 +91,12 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
         d[k][e] = (k < K && c < n) ? z[(size_t)src[1 + k] * ld + c] : 0.f;
       }
   }
+  if constexpr (!FSC) {
+    if ((int)blockIdx.x >= nrow_blocks) {  // fp32 parity mode: the CSC transpose's scatter (csc.h)
+      csc_scatter_role(scat, (int)blockIdx.x - nrow_blocks);
+      return;
+    }
+  }
   if constexpr (FSC) {
     if ((int)blockIdx.x >= nrow_blocks) {  // the extra block: BN_L's coefficients, moments, EMA
       const int xb = (int)blockIdx.x - nrow_blocks - 1;
@@ -351,9 +357,9 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   // ws: the per-workgroup loss / accuracy partials (2 floats each)
   const int nw = cosine_waves(n, fused != nullptr);
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
-  CscScatter sc = (scatter && fused) ? *scatter : CscScatter{};
+  CscScatter sc = scatter ? *scatter : CscScatter{};
   if (sc.nblocks) sc.nblocks = std::max(1, sc.nblocks * 4 / nw);  // sized in 4-wave workgroups
-  if (scatter && !fused) return hipErrorInvalidValue;  // the role rides on the fused kernel only
+  if (scatter && (rmap || fin_ticket)) return hipErrorInvalidValue;  // the mapped / self-finalizing forms
   // fused: + materialising and scatter blocks
   dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);

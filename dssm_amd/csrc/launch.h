@@ -59,8 +59,11 @@ hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_i
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
-                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z, int ldz,
                             int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s);
+// The scatter as a role of a later launch (launch_cosine_loss), on the rank transpose's scratch.
+CscScatter csc_scatter_args(const int* indptr, const int* indices, const float* values, int rows, int D,
+                            int* scratch, const int* col_ptr, int* csc_row, float* csc_val, int* csc_col);
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
                                const int* indptr, const int* indices, const float* values, int rows,
                                int D, int max_nnz, int* scratch, const int* col_ptr, int* csc_row,

@@ -354,8 +354,13 @@ struct dssm_plan {
   // fp64 atomics), every CSC column in row order, heavy dW1 rows through per-item slabs
   bool deterministic() const { return on(DSSM_OPT_DETERMINISTIC); }
   bool fused_stats() const { return on(DSSM_OPT_FUSED_STATS) && fused_stats_ok(); }
+  // the rank transpose's launches merged into the step's: the scan beside the SpMM rows, the scatter
+  // beside the cosine (or BN1 sums), the rank in the previous Adam.  fp32 parity mode (no fused
+  // statistics): the scatter always rides in the cosine launch, and not in deterministic mode
   bool merged_csc() const {
-    return on(DSSM_OPT_MERGED_CSC) && fused_stats() && csc_rank_path() && (Lt.BS % 128) == 0;
+    if (!on(DSSM_OPT_MERGED_CSC) || !csc_rank_path() || (Lt.BS % 128)) return false;
+    if (fused_stats()) return true;
+    return !Lt.bf16 && on(DSSM_OPT_SCATTER_IN_COS) && !deterministic();
   }
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
   bool fused_stats_ok() const {
@@ -638,7 +643,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   if (merged) {  // the SpMM rows share their launch with the column scan
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
-                                   (const uint16_t*)P->weight(0), P->weight_ld(0), Lt.n[0], P->bias(0),
+                                   P->weight(0), Lt.bf16, P->weight_ld(0), Lt.n[0], P->bias(0),
                                    P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
   } else {
@@ -747,6 +752,11 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   }
   const int lL = Lt.L - 1;
   const bool fused_last = Lt.bf16;  // fp32 parity mode keeps the separately applied embeddings
+  dssm::CscScatter scat{};  // merged (fp32 parity mode): the transpose's scatter rides in the cosine launch
+  if (merged)
+    scat = dssm::csc_scatter_args(P->indptr, P->indices, P->values, Lt.R, Lt.D, P->at<int>(Lt.csc_scratch),
+                                  P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
+                                  nullptr);  // csc_col: unread on the rank path
   HIP_TRY(dssm::launch_cosine_loss(
       P->at<float>(fused_last ? Lt.Z[lL] : Lt.A[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG,
       c.gamma, fused_last ? P->at<float>(Lt.coef[lL]) : nullptr,
@@ -754,7 +764,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
       P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
       P->at<float>(Lt.loss_j), P->at<float>(Lt.loss),
       train ? P->at<float>(Lt.dA[lL]) : nullptr,  // eval: no gradient
-      s));
+      s, nullptr, false, merged ? &scat : nullptr));
   P->fwd_train_done = train != 0;
   return DSSM_OK;
 }

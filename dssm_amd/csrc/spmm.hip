@@ -1035,15 +1035,19 @@ bool csc_rank_supported(int D) {
 }
 
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,
-                            const uint16_t* W, int ldw, int n, const float* bias, float* Z, int ldz,
+                            const void* W, bool w_bf16, int ldw, int n, const float* bias, float* Z, int ldz,
                             int D, int max_nnz, int* scratch, int* col_ptr, hipStream_t s) {
   int* cnt = scratch;
   int* heavy_n = csc_heavy_count(scratch, D, max_nnz);
   int2* heavy_items = reinterpret_cast<int2*>(heavy_n + 64);
   const int nscan = cdiv(D + 1, kScanSmallNT * 4);
-  if (!bf16_rows_ok(ldw, n)) return hipErrorInvalidValue;
+  if (w_bf16 ? !bf16_rows_ok(ldw, n) : (ldw < n || ldw % 4)) return hipErrorInvalidValue;
   const dim3 grid(nscan + cdiv(rows, 4));
-  if (ldw % 8)  // the parameter wire's tight rows (RawRow8<u16t>)
+  if (!w_bf16)  // fp32 parity mode
+    hipLaunchKernelGGL(k_spmm_scan<float>, grid, dim3(256), 0, s, indptr, indices, values, rows,
+                       (const float*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
+                       nscan);
+  else if (ldw % 8)  // the parameter wire's tight rows (RawRow8<u16t>)
     hipLaunchKernelGGL(k_spmm_scan<u16t>, grid, dim3(256), 0, s, indptr, indices, values, rows,
                        (const u16t*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
                        nscan);
@@ -1052,6 +1056,14 @@ hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* 
                        (const u16*)W, ldw, n, bias, Z, ldz, cnt, D, col_ptr, heavy_n, heavy_items,
                        nscan);
   return hipGetLastError();
+}
+
+CscScatter csc_scatter_args(const int* indptr, const int* indices, const float* values, int rows, int D,
+                            int* scratch, const int* col_ptr, int* csc_row, float* csc_val, int* csc_col) {
+  constexpr int nb = 384;  // scatter workgroups beside the cosine launch
+  // cnt and the per-entry ranks where launch_csc_build keeps them
+  return CscScatter{indptr, indices, values, rows, D, col_ptr, scratch + 2 * (D + 1 + 64), scratch,
+                    csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
 }
 
 hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, double* fsum,
@@ -1065,11 +1077,8 @@ hipError_t launch_sums_scatter(const float* Z, int ldz, int n, int row_split, do
   int* pos_tmp = scratch + 2 * (D + 1 + 64);
   const int nsum_x = cdiv(ldz, 64), nsum = nsum_x * cdiv(rows, kSumsRows);
   if (det && det->slab && (cdiv(rows, kSumsRows) > det->cap || nsum_x > kDetTiles)) return hipErrorInvalidValue;
-  if (scatter_out) {
-    constexpr int nb = 384;  // scatter workgroups beside the cosine launch
-    *scatter_out = CscScatter{indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
-                              csc_row, csc_val, csc_col, std::min(nb, cdiv(rows, 4))};
-  }
+  if (scatter_out)
+    *scatter_out = csc_scatter_args(indptr, indices, values, rows, D, scratch, col_ptr, csc_row, csc_val, csc_col);
   hipLaunchKernelGGL(k_sums_scatter, dim3(nsum + (scatter_out ? 0 : cdiv(rows, 4))), dim3(256), 0, s, Z, ldz, n,
                      row_split, fsum, nsum_x, nsum, indptr, indices, values, rows, D, col_ptr, pos_tmp, cnt,
                      csc_row, csc_val, csc_col, det ? *det : DetAcc{});
