@@ -313,9 +313,15 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_stats(const float* __restrict__
                                                       const float* __restrict__ coef, BnGrads G,
                                                       float* __restrict__ part,
                                                       unsigned* __restrict__ tickets,
-                                                      float* __restrict__ bcoef) {
+                                                      float* __restrict__ bcoef,
+                                                      const float* __restrict__ loss_part, int loss_nblk,
+                                                      float* __restrict__ loss_out) {
   __shared__ float s_a[NG][64], s_b[NG][64];
   __shared__ int s_flag;
+  if (loss_part && (int)blockIdx.x == (int)gridDim.x - 1) {  // the forward's deferred loss
+    if (blockIdx.y == 0) loss_reduce(loss_part, loss_nblk, tw.row_split, loss_out);
+    return;
+  }
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int rb = blockIdx.y;
@@ -592,13 +598,15 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, hipStream_t s) {
+                         void* dZ, bool dz_bf16, hipStream_t s, const float* loss_part, int loss_nblk,
+                         float* loss_out) {
   RowBlocks b(t);
   BnGrads G;
   G.dgamma[0] = dgamma_q; G.dgamma[1] = dgamma_d;
   G.dbeta[0] = dbeta_q; G.dbeta[1] = dbeta_d;
-  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64), b.total()), dim3(1024), 0, s, Z, dA, ldz,
-                     n, t, coef, G, partial, tickets, bcoef);
+  if (loss_part && (!loss_out || loss_nblk < 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(ldz, 64) + (loss_part ? 1 : 0), b.total()), dim3(1024), 0, s, Z,
+                     dA, ldz, n, t, coef, G, partial, tickets, bcoef, loss_part, loss_nblk, loss_out);
   const int grid = ew_grid((size_t)t.rows * (ldz / 4));
   if (dz_bf16)
     hipLaunchKernelGGL(k_bn_bwd_apply<u16>, dim3(grid), dim3(256), 0, s, Z, dA, ldz, t, coef,

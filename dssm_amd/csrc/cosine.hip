@@ -397,9 +397,9 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   return hipGetLastError();
 }
 
-hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s) {
-  // only after a fused-statistics forward (the deferred loss)
-  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, cosine_blocks(bs, n, true), bs, loss_out);
+hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s, bool fused) {
+  // only after a forward that deferred its loss (the partials of a fused / unfused cosine launch)
+  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, cosine_blocks(bs, n, fused), bs, loss_out);
   return hipGetLastError();
 }
 

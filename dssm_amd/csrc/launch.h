@@ -166,7 +166,10 @@ hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const flo
 hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowers t,
                          const float* coef, float* dgamma_q, float* dbeta_q, float* dgamma_d,
                          float* dbeta_d, float* partial, unsigned* tickets, float* bcoef,
-                         void* dZ, bool dz_bf16, hipStream_t s);
+                         void* dZ, bool dz_bf16, hipStream_t s, const float* loss_part = nullptr,
+                         int loss_nblk = 0, float* loss_out = nullptr);
+// loss_part: the forward's deferred loss partials (loss_nblk cosine workgroups), reduced into
+// loss_out by one extra workgroup of the statistics launch
 
 // ---- cosine / loss (cosine.hip) ----
 // z: last-layer activations [R x ld] fp32: pre-BN when coef != null (BN+ReLU applied on the
@@ -189,7 +192,7 @@ inline int cosine_blocks(int bs, int n = 0, bool fused = false) {
   const int w = cosine_waves(n, fused);
   return (bs + w - 1) / w;
 }
-hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s);
+hipError_t launch_loss_finalize(const float* ws, int bs, int n, float* loss_out, hipStream_t s, bool fused = true);
 
 // ---- optimizer (adam.hip) ----
 struct ShadowSeg {

@@ -730,7 +730,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           c.bn_eps, c.ema_decay, true, P->at<float>(Lt.bmean[l]), P->at<float>(Lt.bvar[l]),
           P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]), s));
     const bool last = l == Lt.L - 1;
-    if (last && Lt.bf16) break;  // the cosine kernel applies the last BN+ReLU itself
+    if (last) break;  // the cosine kernel applies the last BN+ReLU itself (and writes the embeddings)
     if (!last && P->wholek(l + 1)) {
       // BN+ReLU of layer l applied while staging the next GEMM's A operand; the bf16 activation
       // is written once (for the dW GEMM) by the first column tile.
@@ -751,20 +751,21 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
                                 nullptr, s));
   }
   const int lL = Lt.L - 1;
-  const bool fused_last = Lt.bf16;  // fp32 parity mode keeps the separately applied embeddings
   dssm::CscScatter scat{};  // merged (fp32 parity mode): the transpose's scatter rides in the cosine launch
   if (merged)
     scat = dssm::csc_scatter_args(P->indptr, P->indices, P->values, Lt.R, Lt.D, P->at<int>(Lt.csc_scratch),
                                   P->at<int>(Lt.col_ptr), P->at<int>(Lt.csc_row), P->at<float>(Lt.csc_val),
                                   nullptr);  // csc_col: unread on the rank path
   HIP_TRY(dssm::launch_cosine_loss(
-      P->at<float>(fused_last ? Lt.Z[lL] : Lt.A[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG,
-      c.gamma, fused_last ? P->at<float>(Lt.coef[lL]) : nullptr,
-      fused_last ? P->at<float>(Lt.A[lL]) : nullptr, P->at<float>(Lt.cos_raw),
+      P->at<float>(Lt.Z[lL]), Lt.ldp[lL], Lt.n[lL], Lt.BS, Lt.NEG,
+      c.gamma, P->at<float>(Lt.coef[lL]),
+      P->at<float>(Lt.A[lL]), P->at<float>(Lt.cos_raw),
       P->at<float>(Lt.cos_sim), P->at<float>(Lt.prob), P->at<float>(Lt.qnorm),
       P->at<float>(Lt.loss_j), P->at<float>(Lt.loss),
       train ? P->at<float>(Lt.dA[lL]) : nullptr,  // eval: no gradient
-      s, nullptr, false, merged ? &scat : nullptr));
+      s, nullptr, /*defer_finalize=*/train != 0, merged ? &scat : nullptr));
+  // train: the loss partials are reduced by the backward's first launch (or finalize_loss)
+  P->loss_pending = train != 0;
   P->fwd_train_done = train != 0;
   return DSSM_OK;
 }
@@ -864,12 +865,15 @@ static int backward_impl(dssm_plan* P, void* stream) {
   }
   for (int l = Lt.L - 1; l >= 0; --l) {
     const int n = Lt.n[l];
+    const bool fin = l == Lt.L - 1 && P->loss_pending;  // the forward's loss, deferred to this launch
     HIP_TRY(dssm::launch_bn_bwd(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), Lt.ldp[l], n, tw,
                                 P->at<float>(Lt.coef[l]), P->g + Lt.bn_off[l][0],
                                 P->g + Lt.bn_off[l][1], P->g + Lt.bn_off[l][2],
                                 P->g + Lt.bn_off[l][3], P->at<float>(Lt.partial),
                                 P->at<unsigned>(Lt.tickets[l][1]), P->at<float>(Lt.bcoef[l]),
-                                P->ws + Lt.dZ[l], Lt.bf16, s));
+                                P->ws + Lt.dZ[l], Lt.bf16, s, fin ? P->at<float>(Lt.loss_j) : nullptr,
+                                dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], false), P->at<float>(Lt.loss)));
+    if (fin) P->loss_pending = false;
     if (l > 0) {
       const int kin = Lt.in_dim[l];
       float* gw = P->g + Lt.fc_off[l];
@@ -1191,7 +1195,7 @@ int dssm_plan_finalize_loss(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (P->loss_pending) {
     HIP_TRY(dssm::launch_loss_finalize(P->at<float>(P->Lt.loss_j), P->Lt.BS, P->Lt.n[P->Lt.L - 1],
-                                       P->at<float>(P->Lt.loss), (hipStream_t)stream));
+                                       P->at<float>(P->Lt.loss), (hipStream_t)stream, P->fwd_fused));
     P->loss_pending = false;
   }
   return DSSM_OK;

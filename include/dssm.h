@@ -262,7 +262,7 @@ enum {
   DSSM_SCHED_DETERMINISTIC = 128   /* fixed-order reductions: bit-identical repeated runs */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
-/* The fused-statistics train forward leaves the loss / accuracy reduction to the backward's first
+/* A train forward (either precision) leaves the loss / accuracy reduction to the backward's first
  * launch; call this before reading DSSM_BUF_LOSS after a train forward that was not followed by
  * dssm_plan_backward (no-op otherwise). */
 int dssm_plan_finalize_loss(dssm_plan* plan, void* stream);
