@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 measurement set: tools/gpu_measure.sh (BoW bf16 + fp32: kernel stats, PMC traffic, MFMA,
+# a round's measurement set: tools/gpu_measure.sh (BoW bf16 + fp32: kernel stats, PMC traffic, MFMA,
 # bench lines) and tools/gpu_measure_aux.sh for the multi-view row
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
