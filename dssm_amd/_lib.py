@@ -116,6 +116,9 @@ _SIGS = {
                                    C.c_float, C.c_int, C.c_int, _P, C.c_int, _P, _P, _P, _P]),
     "dssm_cosine_softmax_loss": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, _P,
                                            _P, _P, _P, _P, _P, _P, _P]),
+    "dssm_cosine_softmax_loss_dropout": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                                   C.c_uint32, C.c_uint32, C.c_float, _P, _P, _P, _P, _P, _P,
+                                                   _P, _P, _P]),
     "dssm_text_clean": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dssm_vocab_create": (C.c_int, [C.POINTER(_P)]),
     "dssm_vocab_destroy": (C.c_int, [_P]),

@@ -156,6 +156,18 @@ __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // Loss / accuracy of the step from the cosine kernel's per-workgroup partials: wave 0 of the
 // calling workgroup, fixed order (lane-strided partial sums, then a shuffle tree).
+// Inverted-dropout mask of element i (row-major index r * cols + c): kept when the hash < thr,
+// thr = keep * 2^32 (oracle/rnn_oracle.py dropout_mask); shared by k_dropout and the fused cosine.
+__device__ __forceinline__ unsigned dropout_hash(unsigned i, unsigned seed, unsigned step) {
+  unsigned x = i * 0x9E3779B1u + seed * 0x85EBCA77u + step * 0xC2B2AE3Du;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ void loss_reduce(const float* __restrict__ part, int nblk, int bs,
                                             float* __restrict__ loss_out) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

@@ -53,13 +53,19 @@ __device__ unsigned long long g_cos_tl[1024][8];  // 0 start 1 end, 2..6 phases 
 #endif
 // MAP: the merged row r of [q; pos; neg] is read from z row rmap[r] (the multi-view model's in-batch
 // rotation as an index map instead of a gathered copy); dy stays in the merged layout.
-template <int EPL, int KM, bool FSC, int NW, bool MAP = false>
+__device__ __forceinline__ bool drop_kept(const CosDrop& d, int r, int c) {
+  return d.all || dropout_hash((unsigned)(r * d.cols + c), d.seed, d.step) < d.thr;
+}
+
+// DROP: inverted dropout on the rows (CosDrop), fused (the unfused, unmapped form only).
+template <int EPL, int KM, bool FSC, int NW, bool MAP = false, bool DROP = false>
 __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ z, int ld, int n, int bs, int neg, float gamma,
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat,
-    const int* __restrict__ rmap, float* __restrict__ loss_out, unsigned* __restrict__ fin_ticket) {
+    const int* __restrict__ rmap, float* __restrict__ loss_out, unsigned* __restrict__ fin_ticket,
+    CosDrop drop) {
   constexpr int NT = 64 * NW;
   COS_TL(0);
   __shared__ float s_part[2][NW];
@@ -134,6 +140,18 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
         zq[e] = q[e];
 #pragma unroll
         for (int k = 0; k < KM; ++k) zd[k][e] = d[k][e];
+      }
+    }
+    if constexpr (DROP) {  // x * m / keep (k_dropout's arithmetic)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const int c = lane + 64 * e;
+        if (c < n) {
+          q[e] = drop_kept(drop, j, c) ? q[e] * drop.fwd : 0.f;
+#pragma unroll
+          for (int k = 0; k < KM; ++k)
+            if (k < K) d[k][e] = drop_kept(drop, doc_row(j, k, bs, neg), c) ? d[k][e] * drop.fwd : 0.f;
+        }
       }
     }
     if (coef || FSC) {  // last layer's BN + ReLU (query tower for q, doc tower for the docs)
@@ -242,9 +260,15 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
           const int c = lane + 64 * e;
-          dq[e] += a * d[k][e] - bq * q[e];
-          const float gd = (c < n) ? a * q[e] - bd * d[k][e] : 0.f;
-          if (c < ld) dy[row + c] = gd;
+          // explicit FMAs: one rounding sequence in every instantiation (the contraction the
+          // compiler picks otherwise differs between them)
+          dq[e] += __fmaf_rn(a, d[k][e], -(bq * q[e]));
+          const float gd = (c < n) ? __fmaf_rn(a, q[e], -(bd * d[k][e])) : 0.f;
+          if constexpr (DROP) {  // d loss / d x through the same mask
+            if (c < ld) dy[row + c] = (c < n && drop_kept(drop, doc_row(j, k, bs, neg), c)) ? gd * drop.bwd : 0.f;
+          } else {
+            if (c < ld) dy[row + c] = gd;
+          }
           if constexpr (FSC) {
             if (c < n) {
               const float m = d[k][e] > 0.f ? gd : 0.f;  // ReluGrad on the doc row
@@ -258,7 +282,11 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const int c = lane + 64 * e;
-      if (c < ld) dy[(size_t)j * ld + c] = (c < n) ? dq[e] : 0.f;
+      if constexpr (DROP) {
+        if (c < ld) dy[(size_t)j * ld + c] = (c < n && drop_kept(drop, j, c)) ? dq[e] * drop.bwd : 0.f;
+      } else {
+        if (c < ld) dy[(size_t)j * ld + c] = (c < n) ? dq[e] : 0.f;
+      }
       if constexpr (FSC) {
         if (c < n) {
           const float m = q[e] > 0.f ? dq[e] : 0.f;
@@ -352,8 +380,11 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              const CscScatter* scatter, const int* rmap, unsigned* fin_ticket) {
+                              const CscScatter* scatter, const int* rmap, unsigned* fin_ticket,
+                              const CosDrop* drop) {
   if (neg + 1 > MAXK || n > kCosMaxN || (rmap && (fused || coef || y_out))) return hipErrorInvalidValue;
+  const CosDrop dr = drop ? *drop : CosDrop{};
+  if (dr.on && (fused || rmap || coef || scatter)) return hipErrorInvalidValue;  // the plain form only
   // ws: the per-workgroup loss / accuracy partials (2 floats each)
   const int nw = cosine_waves(n, fused != nullptr);
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
@@ -374,13 +405,18 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
-                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin); \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin, \
+                       dr);                                                                     \
   else if (rmap)                                                                                \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, true>), grid, block, 0, s, z, ld, n, bs, neg, gamma, \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap, loss_out, fin); \
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap, loss_out, fin, dr); \
+  else if (dr.on)                                                                               \
+    hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, false, true>), grid, block, 0, s, z, ld, n, bs, neg, \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, \
+                       fin, dr);                                                                \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin)
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin, dr)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \

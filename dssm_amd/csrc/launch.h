@@ -176,12 +176,21 @@ hipError_t launch_bn_bwd(const float* Z, const float* dA, int ldz, int n, BnTowe
 // fly, embeddings written to y_out if non-null), else the embeddings themselves.
 // ws: cosine_ws_floats(bs) floats, zero-filled before first use (holds a re-armed ticket).
 size_t cosine_ws_floats(int bs);
+// Inverted dropout on the cosine's input rows (the RNN tower: dropout(keep) on the final states,
+// dssm_rnn.py), fused: rows read as x * m / keep, dy stored as dy * m * bwd (bwd = scale / keep).
+struct CosDrop {
+  int on;
+  unsigned thr, seed, step;  // mask: dropout_hash(r * cols + c, seed, step) < thr (all kept: thr unused)
+  int all, cols;
+  float fwd, bwd;
+};
 hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, float gamma,
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused = nullptr,
                               bool defer_finalize = false, const CscScatter* scatter = nullptr,
-                              const int* rmap = nullptr, unsigned* fin_ticket = nullptr);
+                              const int* rmap = nullptr, unsigned* fin_ticket = nullptr,
+                              const CosDrop* drop = nullptr);
 // rmap (unfused, no coef / y_out): merged row r read from z row rmap[r]
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 // (queries per workgroup: kCosFusedWaves for the fused-statistics kernel at widths <= 128,

@@ -1588,6 +1588,31 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
   return DSSM_OK;
 }
 
+int dssm_cosine_softmax_loss_dropout(const float* x, int ld, int n, int query_bs, int neg, float gamma, float keep,
+                                     uint32_t seed, uint32_t step, float bwd_scale, float* y, float* cos_sim_raw,
+                                     float* cos_sim, float* prob, float* query_norm, float* loss, float* dy,
+                                     float* ws, void* stream) {
+  if (!x || !cos_sim_raw || !cos_sim || !prob || !query_norm || !loss || !dy || !ws || query_bs < 1 || neg < 1 ||
+      neg > 15 || n < 1 || n > 512 || ld < n || !(keep > 0.f) || (int64_t)query_bs * (2 + neg) * n >= (1ll << 31))
+    return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss_dropout: bad arguments");
+  // dssm_rnn_dropout's mask and arithmetic: thr = keep * 2^32, x * (1 / keep), dy * (scale / keep)
+  const double t = (double)keep * 4294967296.0;
+  dssm::CosDrop d{};
+  d.on = 1;
+  d.all = keep >= 1.f ? 1 : 0;
+  d.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (unsigned)t;
+  d.seed = seed;
+  d.step = step;
+  d.cols = n;
+  const float kd = keep >= 1.f ? 1.f : keep;
+  d.fwd = 1.0f / kd;
+  d.bwd = bwd_scale / kd;
+  HIP_TRY(dssm::launch_cosine_loss(x, ld, n, query_bs, neg, gamma, nullptr, y, cos_sim_raw, cos_sim, prob,
+                                   query_norm, ws, loss, dy, (hipStream_t)stream, nullptr, false, nullptr, nullptr,
+                                   cosine_fin_ticket(ws, query_bs), &d));
+  return DSSM_OK;
+}
+
 // ---- RCCL ---------------------------------------------------------------------------------
 // The library's own communicator (one per process: one process per GPU).  Collectives are
 // enqueued on the caller's stream, between the step's graphs.

@@ -306,22 +306,13 @@ __global__ void k_transpose(const float* __restrict__ src, int rows, int cols, f
 
 // inverted dropout with the counter-based mask (oracle/rnn_oracle.py dropout_mask): y = x * m *
 // scale / keep; the backward uses the same call on dy (scale folds the summed loss's BS).
-__device__ __forceinline__ unsigned drop_hash(unsigned i, unsigned seed, unsigned step) {
-  unsigned x = i * 0x9E3779B1u + seed * 0x85EBCA77u + step * 0xC2B2AE3Du;
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
-}
 
 __global__ void k_dropout(const float* __restrict__ x, float* __restrict__ y, int rows, int cols,
                           int ld, float keep, unsigned thr, unsigned seed, unsigned step, float scale) {
   const int n = rows * cols;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int r = i / cols, c = i - r * cols;
-    const bool kept = keep >= 1.f || drop_hash((unsigned)i, seed, step) < thr;
+    const bool kept = keep >= 1.f || dropout_hash((unsigned)i, seed, step) < thr;
     y[(size_t)r * ld + c] = kept ? x[(size_t)r * ld + c] * (scale / (keep >= 1.f ? 1.f : keep)) : 0.f;
   }
 }

@@ -171,22 +171,21 @@ class RnnDSSM:
         if train:
             self._drop_step += 1
         self._keep_used = keep
-        check(self.lib.dssm_rnn_dropout(ptr(self.y0), ptr(self.y), self.R, 2 * self.H, 2 * self.H, keep,
-                                        self.seed, self._drop_step, 1.0, s), "dropout")
-        check(self.lib.dssm_cosine_softmax_loss(ptr(self.y), 2 * self.H, 2 * self.H, self.BS, self.NEG,
-                                                self.gamma, ptr(self.cos_raw), ptr(self.cos_sim),
-                                                ptr(self.prob), ptr(self.qnorm), ptr(self.loss_buf),
-                                                ptr(self.dy), ptr(self.cos_ws), s), "cosine")
+        # dropout(keep) on the final states fused into the cosine launch: y = y0 * m / keep, and dy
+        # leaves it as d(summed loss)/dy0 (the cosine's d(mean loss)/dy x BS through the same mask)
+        check(self.lib.dssm_cosine_softmax_loss_dropout(ptr(self.y0), 2 * self.H, 2 * self.H, self.BS, self.NEG,
+                                                        self.gamma, keep, self.seed, self._drop_step,
+                                                        float(self.BS), ptr(self.y), ptr(self.cos_raw),
+                                                        ptr(self.cos_sim), ptr(self.prob), ptr(self.qnorm),
+                                                        ptr(self.loss_buf), ptr(self.dy), ptr(self.cos_ws), s),
+              "cosine_dropout")
         self._train = train
 
     def backward(self, stream=None):
         if not self._train:
             raise RuntimeError("backward needs a train-mode forward")
         s = stream_ptr(stream)
-        # d(sum loss)/dy0: the cosine kernel's d(mean loss)/dy x BS through the same dropout mask
-        check(self.lib.dssm_rnn_dropout(ptr(self.dy), ptr(self.dy), self.R, 2 * self.H, 2 * self.H,
-                                        self._keep_used, self.seed, self._drop_step, float(self.BS), s),
-              "dropout_bwd")
+        # dy = d(sum loss)/dy0 already (the forward's fused dropout)
         gw = (C.c_void_p * 4)(*[ptr(self._block(self.grads, n)) for n in ("fw_g", "fw_c", "bw_g", "bw_c")])
         if self.dtype == "bf16":
             check(self.lib.dssm_rnn_bf16_backward(ptr(self.ids), ptr(self.lens), self.R, self.T, self.V, self.E,

@@ -313,6 +313,14 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
  * [q; pos; neg] [R x ld] fp32 -> cos_sim_raw, cos_sim, prob, query_norm, loss[2] (loss, acc),
  * dy [R x ld] (d loss / d y).  ws: >= 2*ceil(BS/4) + 64 floats, zero-filled before its first
  * use (it holds a completion ticket the kernel re-arms). */
+/* ... with the RNN tower's inverted dropout (dssm_rnn.py:139,146,153: tf.nn.dropout on the final states)
+ * fused: rows read as x * m / keep with dssm_rnn_dropout's counter-based mask m (seed, step; mask index
+ * r * n + c), the dropped rows written to y (NULL: not stored), and dy stored as d loss / d x =
+ * (d loss / d y) * m * bwd_scale / keep -- the two dssm_rnn_dropout launches of the unfused form. */
+int dssm_cosine_softmax_loss_dropout(const float* x, int ld, int n, int query_bs, int neg, float gamma, float keep,
+                                     uint32_t seed, uint32_t step, float bwd_scale, float* y, float* cos_sim_raw,
+                                     float* cos_sim, float* prob, float* query_norm, float* loss, float* dy,
+                                     float* ws, void* stream);
 int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int neg, float gamma,
                              float* cos_sim_raw, float* cos_sim, float* prob, float* query_norm,
                              float* loss, float* dy, float* ws, void* stream);
