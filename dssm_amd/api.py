@@ -25,7 +25,9 @@ at import of the model (dssm_amd._lib.load).
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
+from types import SimpleNamespace
 from typing import Any, Dict, Iterable, Optional
 
 import numpy as np
@@ -135,6 +137,17 @@ class DSSMGraph:
                 self._by_name[comp.name] = comp
         for key, name in _FETCHES.items():
             self._by_name[name] = getattr(self, key)
+        global _DEFAULT_GRAPH
+        _DEFAULT_GRAPH = self
+
+    def meta(self) -> Dict[str, Any]:
+        """What import_meta_graph needs to rebuild this graph (written beside a checkpoint as
+        <prefix>.meta by Saver.save)."""
+        c = self.conf
+        return {"format": META_FORMAT, "trigram_d": self.trigram_d, "query_BS": self.query_BS, "NEG": self.NEG,
+                "L1_N": c.L1_N, "L2_N": c.L2_N, "L3_N": c.L3_N, "learning_rate": c.learning_rate,
+                "compute_dtype": c.compute_dtype, "max_nnz_per_row": c.max_nnz_per_row, "seed": c.seed,
+                "tensors": sorted(self._by_name)}
 
     def get_tensor_by_name(self, name: str):
         """graph.get_tensor_by_name (load_model_and_save_vector.py:30-46); ':0' suffix optional."""
@@ -148,8 +161,9 @@ class Session:
     """sess.run over a DSSMGraph: one device forward per run (train- or eval-mode BN per the
     on_train feed), + backward + Adam when train_step is fetched."""
 
-    def __init__(self, graph: DSSMGraph, stream=None):
-        self.graph = graph
+    def __init__(self, graph: Optional[DSSMGraph] = None, stream=None):
+        """graph: None = the default graph (the last one built or imported), as tf.Session()."""
+        self.graph = graph if graph is not None else get_default_graph()
         self.stream = stream
 
     def __enter__(self):
@@ -248,12 +262,15 @@ class Saver:
             raise ValueError("format must be 'tf' or 'npz'")
         self.format = format
 
-    def save(self, sess: Session, save_path: str) -> str:
+    def save(self, sess: Session, save_path: str, write_meta_graph: bool = True) -> str:
         if self.format == "npz" or save_path.endswith(".npz"):
             path = save_path if save_path.endswith(".npz") else save_path + ".npz"
             sess.graph.model.save(path)
             return path
-        return tfckpt.save_model(sess.graph.model, save_path)
+        prefix = tfckpt.save_model(sess.graph.model, save_path)
+        if write_meta_graph:
+            write_meta(sess.graph, prefix + ".meta")
+        return prefix
 
     def restore(self, sess: Session, save_path: str):
         if os.path.exists(save_path + ".index"):
@@ -261,6 +278,54 @@ class Saver:
             return
         path = save_path if save_path.endswith(".npz") else save_path + ".npz"
         sess.graph.model.restore(path)
+
+
+# ---- the export script's graph handling (load_model_and_save_vector.py:8-11,25) --------------
+# tf.train.Saver.save also writes <prefix>.meta, the MetaGraphDef that import_meta_graph rebuilds the
+# graph from.  Here the graph is this module's DSSMGraph, so <prefix>.meta is a JSON description of it
+# (the Config fields that shape it and its tensor names), not a protobuf: a TF reader cannot load it,
+# and this module's import_meta_graph cannot load a TF one.
+META_FORMAT = "dssm_amd.meta/1"
+_DEFAULT_GRAPH: Optional[DSSMGraph] = None
+
+
+def write_meta(graph: DSSMGraph, path: str) -> str:
+    with open(path, "w") as f:
+        json.dump(graph.meta(), f, indent=1, sort_keys=True)
+    return path
+
+
+def read_meta(path: str) -> Dict[str, Any]:
+    with open(path) as f:
+        meta = json.load(f)
+    if not isinstance(meta, dict) or meta.get("format") != META_FORMAT:
+        raise ValueError(f"{path}: not a {META_FORMAT} graph description (a TF MetaGraphDef cannot be "
+                         "imported here)")
+    return meta
+
+
+def get_default_graph() -> DSSMGraph:
+    """tf.get_default_graph(): the last DSSMGraph built or imported."""
+    if _DEFAULT_GRAPH is None:
+        raise RuntimeError("no DSSM graph has been built or imported")
+    return _DEFAULT_GRAPH
+
+
+def import_meta_graph(meta_path: str, device=None) -> Saver:
+    """tf.train.import_meta_graph (load_model_and_save_vector.py:10): rebuild the graph a
+    checkpoint was saved from (it becomes the default graph) and return a Saver for its variables."""
+    from .config import Config
+    m = read_meta(meta_path)
+    conf = Config(query_BS=m["query_BS"], NEG=m["NEG"], L1_N=m["L1_N"], L2_N=m["L2_N"], L3_N=m["L3_N"],
+                  learning_rate=m["learning_rate"], compute_dtype=m["compute_dtype"],
+                  max_nnz_per_row=m["max_nnz_per_row"], seed=m["seed"])
+    DSSMGraph(conf, m["trigram_d"], device=device)
+    return Saver()
+
+
+latest_checkpoint = tfckpt.latest_checkpoint
+# the reference reaches these through tf.train
+train = SimpleNamespace(Saver=Saver, import_meta_graph=import_meta_graph, latest_checkpoint=latest_checkpoint)
 
 
 # ---- functional forward ops (inference / export) -----------------------------------------

@@ -11,9 +11,10 @@ A V2 checkpoint ``<prefix>`` is three files:
   {dtype, shape, offset, size, crc32c = masked CRC-32C of its bytes};
 * ``checkpoint`` in the same directory: the text proto naming the latest prefix.
 
-``Saver.save`` also writes a ``.meta`` graph (MetaGraphDef); it is not written here, since a
-checkpoint is restored into a graph built by the same code (``Saver.restore`` reads only the index
-and data files).  The protobuf messages are encoded by hand (a handful of fields).
+``tf.train.Saver.save`` also writes a ``.meta`` graph (MetaGraphDef); ``api.Saver.save`` writes its
+own ``.meta`` instead (a JSON description of the api's DSSMGraph that ``api.import_meta_graph``
+rebuilds the graph from), since the graph here is not a TF graph.  The protobuf messages of the
+bundle are encoded by hand (a handful of fields).
 
 Variable names follow TF1.x's naming of the reference graph (new_dssm.py:117-217, with
 ``batch_normalization`` :62-88): ``tf.Variable`` takes the enclosing name scope, a second

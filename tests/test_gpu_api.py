@@ -251,3 +251,36 @@ def test_export_mid_vectors_eval(tmp_path):
         lines = open(path, encoding="utf8").read().splitlines()
         assert lines == [mid_vector_line(t, r) for t, r in zip(tx, rows)]
         assert out[path] == len(tx)
+
+
+def test_export_script_sequence_with_meta_graph(tmp_path):
+    """load_model_and_save_vector.py:8-46 as written against `tf`, with `tf` = dssm_amd.api:
+    Session(), train.import_meta_graph(<prefix>.meta), restore(sess, train.latest_checkpoint(dir)),
+    get_default_graph().get_tensor_by_name(...) -- the embeddings equal the saving graph's."""
+    conf, g, cfg = _graph()
+    q, d, n = _matrices(1)
+    sess = api.Session(g)
+    feed = pull_batch(True, q, d, n, 0, BS, g.query_batch, g.doc_positive_batch, g.doc_negative_batch,
+                      g.on_train, conf)
+    sess.run(g.train_step, feed_dict=feed)
+    prefix = api.Saver().save(sess, str(tmp_path / "model_1.ckpt"))
+    assert (tmp_path / "model_1.ckpt.meta").exists()
+    want = sess.run(g.embedding_query_y, feed_dict={**feed, g.on_train: False})
+    # the export script, in a fresh graph
+    tf = api
+    saver = tf.train.import_meta_graph(str(tmp_path / "model_1.ckpt.meta"))
+    sess2 = tf.Session()
+    saver.restore(sess2, tf.train.latest_checkpoint(str(tmp_path)))
+    graph = tf.get_default_graph()
+    assert graph is not g and sess2.graph is graph
+    get = graph.get_tensor_by_name
+    from dssm_amd.data import convert_sparse_matrix_to_sparse_tensor
+    f2 = {get("input/on_train:0"): False}
+    for ph, X in (("query_batch", q), ("doc_positive_batch", d), ("doc_negative_batch", n)):
+        sv = convert_sparse_matrix_to_sparse_tensor(X)
+        f2[get(f"input/{ph}/indices:0")] = sv[0]
+        f2[get(f"input/{ph}/values:0")] = sv[1]
+        f2[get(f"input/{ph}/shape:0")] = sv[2]
+    y = sess2.run(get("BN2/embedding_query_y:0"), feed_dict=f2)
+    np.testing.assert_array_equal(y, want)
+    assert prefix == tf.train.latest_checkpoint(str(tmp_path))
