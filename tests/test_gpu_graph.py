@@ -126,14 +126,20 @@ def test_graph_rejects_partial_fused_and_default_stream():
 
 
 @pytest.mark.parametrize("case", CASES[:2])
-def test_multi_step_graph_matches_eager(case):
+@pytest.mark.parametrize("det", [False, True])
+def test_multi_step_graph_matches_eager(case, det):
     """graph_build_steps: k whole steps captured back to back in one graph (bench's cycle graph)
-    equal k eager steps on the same batches (free-running over 3 steps: the atomics' rounding
-    noise stays within the per-step bar widened by the step count)."""
+    equal k eager steps on the same batches.  DETERMINISTIC: bit-identical.  Default schedule:
+    free-running over 3 steps the atomics' order differs run to run (eager vs eager too), and Adam
+    turns a rounding-noise gradient into a full step of either sign, which the next forward
+    propagates (measured 93-100% of the parameters within 1e-4 across runs, tools/graph_noise.py):
+    the bars are the loss, the 2 lr per step envelope and >= 80% within 1e-4."""
     D, widths, BS, NEG, dtype, fused = case
     lr, k = 0.01, 3
     _, _, ea = make(D, widths, BS, NEG, dtype, fused=fused)
     _, _, gr = make(D, widths, BS, NEG, dtype, fused=fused)
+    for m in (ea, gr):
+        m.set_option("DETERMINISTIC", det)
     batches = _batches(D, BS, NEG, k)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
@@ -150,9 +156,12 @@ def test_multi_step_graph_matches_eager(case):
     assert ea.beta_powers() == gr.beta_powers()
     la, lg = ea.loss_accuracy()[0], gr.loss_accuracy()[0]
     assert abs(la - lg) <= 1e-3 * abs(la) + 1e-6, (la, lg)
+    if det:
+        assert torch.equal(ea.params, gr.params)
+        return
     d = (ea.params - gr.params).abs()
     assert float(d.max()) <= 2 * k * lr, float(d.max())
-    assert float((d <= 1e-4).float().mean()) >= 0.99, float((d <= 1e-4).float().mean())
+    assert float((d <= 1e-4).float().mean()) >= 0.8, float((d <= 1e-4).float().mean())
 
 
 TIMED = ("FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "FUSED_W1_ADAM", "WHOLEK", "DW_IN_APPLY",
