@@ -104,6 +104,10 @@ def parse():
                     help="analysis only: seconds of dense matmul load between the graph builds and the warm-up")
     ap.add_argument("--plan-option", action="append", default=[], metavar="NAME=0|1",
                     help="analysis only: set a schedule option (dssm_plan_set_option, e.g. LAZY_ADAM=0)")
+    ap.add_argument("--dp-alt", type=int, default=1,
+                    help="N>1 started as a plain process: after the headline ranks exit, run a second N-rank "
+                         "child with --dp-mode allreduce --wire fp32 (one fp32 gradient all-reduce + replicated "
+                         "Adam) and report its line as dp_alt, so one run measures both exchanges")
     ap.add_argument("--dp-check", type=int, default=1,
                     help="N>1: after the timed region, gather the sharded optimizer state and compare a "
                          "digest of every rank's parameters / Adam m / v (reported as dp_check)")
@@ -120,25 +124,66 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def _run_ranks(args, argv, capture: bool):
+    """One child `torch.distributed.run` of args.gpus ranks (127.0.0.1) running this script with
+    argv; its non-JSON output is passed through as it arrives (a long run keeps printing progress),
+    the JSON line(s) rank 0 prints are returned instead of printed when capture is set."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the only kind the host driver has)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    child = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if capture else None, text=True)
+
+    def forward(sig, _frame):  # the driver's timeout reaches the ranks too
+        child.send_signal(sig)
+    for sg in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sg, forward)
+    lines = []
+    if capture:
+        for line in child.stdout:
+            if line.startswith("{"):
+                lines.append(line.strip())
+            else:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+    return child.wait(), lines
+
+
 def spawn_ranks(args) -> int:
     """`bench.py --gpus N` (N > 1) started as a plain process: launch the N ranks as a child
     `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1) with the same
     arguments and return its exit code.  Runs before anything touches the GPU (no HIP call, no
-    torch.cuda query), so the parent never holds a device context; rank 0 prints the line."""
-    import signal
-    import subprocess
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the only kind the host driver has)
-    env.setdefault("OMP_NUM_THREADS", "1")
-    child = subprocess.Popen(cmd, env=env)
-
-    def forward(sig, _frame):  # the driver's timeout reaches the ranks too
-        child.send_signal(sig)
-    for s in (signal.SIGTERM, signal.SIGINT):
-        signal.signal(s, forward)
-    return child.wait()
+    torch.cuda query), so the parent never holds a device context.  With --dp-alt (default), after
+    the headline ranks exit a second child runs the one-all-reduce exchange (--dp-mode allreduce
+    --wire fp32) on the same N GPUs, and the parent prints ONE line: the headline's, with the
+    alternative's summary under dp_alt."""
+    argv = sys.argv[1:]
+    alt = args.dp_alt and args.model == "bow" and args.dp_mode != "allreduce"
+    rc, lines = _run_ranks(args, argv, capture=alt)
+    if not alt:
+        return rc
+    if rc != 0 or not lines:
+        for ln in lines:
+            print(ln, flush=True)
+        return rc or 1
+    out = json.loads(lines[-1])
+    arc, alines = _run_ranks(args, argv + ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0"],
+                             capture=True)
+    if arc != 0 or not alines:
+        out["dp_alt"] = {"error": f"exit {arc}, no line"}
+    else:
+        a = json.loads(alines[-1])
+        out["dp_alt"] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")}
+        out["dp_alt"].update({k: a["config"].get(k) for k in ("dp_exchange", "dp_launch", "comm")
+                              if k in a.get("config", {})})
+        for k in ("dp_kernels_ms", "dp_check"):
+            if k in a:
+                out["dp_alt"][k] = a[k]
+    print(json.dumps(out), flush=True)
+    return 0
 
 
 def dp_check(model, dp, dev) -> dict:
@@ -277,7 +322,7 @@ def cpu_baseline(seconds: float):
     """Time the CPU port of the step (oracle/, test infrastructure) on a bounded sample, and the
     NumPy float32 oracle on a shorter one as the secondary number."""
     from oracle import cpu_port
-    out = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds)
+    out = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=seconds, scaling=(1, 2, 4, 8, 16))
     if "C/OpenMP" in out.get("sample", ""):
         sec = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=min(5.0, seconds / 3), use_c=False)
         out["numpy_oracle"] = {k: sec[k] for k in ("value", "unit", "cores", "sample")}
@@ -713,6 +758,7 @@ def main():
     # cycle of len(staged) steps plus a partial one.  A capture the runtime refuses falls back to
     # split graphs with host-issued collectives, recorded in the line.
     region_graphs, dp_capture_error = None, None
+    dp_events = []  # split-graph data parallel: (phase, start, end) events of the last timed step
     if args.graph and args.feed == "device" and (rehearse > 1 or (dp is not None and dp.capturable)):
         MAX_REGION_STEPS = 256
         comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2}[args.rehearse_comm]
@@ -793,7 +839,9 @@ def main():
 
         def run_steps(i0, n):
             for i in range(i0, i0 + n):
-                dp.graph_step(i)
+                # the timed region's last step: its phases bracketed by events on the stream
+                last = bool(args.probes) and i0 == args.warmup and i == i0 + n - 1
+                dp.graph_step(i, events=dp_events if last else None)
     elif args.graph:
         # One captured step per staged batch (the batch pointers are baked into the graph).  Timing
         # probes are event nodes inside the graphs (their last replay is read after the timed region).
@@ -900,6 +948,18 @@ def main():
     fwd = fwd_only(model, staged, args, stream) if (args.fwd_only and world == 1 and rehearse == 1
                                                    and feeder is None) else None
 
+    dp_kernels = None
+    if (world > 1 or rehearse > 1) and args.probes and args.graph and region_graphs is not None:
+        # the captured region's last step: its phases' event-record nodes (DSSM_PROBE_DP_*)
+        g = region[args.steps] if args.steps in region else (
+            cycle if args.steps % len(staged) == 0 else partial[args.steps % len(staged)])
+        dp_kernels = {k: round(model.graph_probe_read(g, pid), 5) for k, pid in _lib.DP_PROBES.items()}
+        dp_kernels["adam"] = round(model.graph_probe_read(g, _lib.PROBE_ADAM), 5)
+        dp_kernels["source"] = "event-record nodes in the captured region's last step"
+    elif world > 1 and args.probes and args.graph and dp is not None and dp_events:
+        torch.cuda.synchronize()
+        dp_kernels = {name: round(a.elapsed_time(b), 5) for name, a, b in dp_events}
+        dp_kernels["source"] = "torch.cuda events around the timed region's last step (host-issued exchange)"
     probes = {}
     if args.graph and probe_graph is not None:
         model.graph_launch(probe_graph)  # untimed: the secondary probes' replay
@@ -994,6 +1054,8 @@ def main():
         out["mfma"] = mf
     if fwd is not None:
         out["fwd_only"] = fwd
+    if rehearse > 1 and dp_kernels is not None:
+        out["dp_kernels_ms"] = dp_kernels
     if rehearse > 1:
         out["rehearsal"] = {"world": rehearse, "chunks": args.dp_chunks,
                             "collectives": ({"model": f"modelled: {args.link_latency_us} us + bytes sent / "
@@ -1002,6 +1064,12 @@ def main():
                             "note": "rank 0 of an N-rank bf16-wire step on one GPU; not a headline number"}
     if dp is not None:
         out["config"]["dp_chunks"] = dp.chunks
+        try:
+            out["config"]["comm"] = dp.tx.info()
+        except Exception as e:  # informational only
+            out["config"]["comm"] = {"error": repr(e)}
+        if dp_kernels is not None:
+            out["dp_kernels_ms"] = dp_kernels
         out["config"]["dp_launch"] = ("one graph per region, collectives captured" if region_graphs is not None
                                       else "split graphs, host-issued collectives" if args.graph else "eager")
         if dp_capture_error:

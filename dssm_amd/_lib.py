@@ -23,6 +23,9 @@ DSSM_ACT_NONE, DSSM_ACT_RELU = 0, 1
  BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
 BUF_A, BUF_DA = 11, 12
 PROBE_SPMM_FWD, PROBE_DW1, PROBE_ADAM, PROBE_CSC = range(4)
+# the phases of a data-parallel step graph's last step (include/dssm.h DSSM_PROBE_DP_*)
+DP_PROBES = {"fwd_bwd": 4, "grad_pass": 5, "all_to_all": 6, "tail_allreduce": 7, "all_gather": 8,
+             "shadow_rebuild": 9}
 GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS, GRAPH_WIRE_SHADOWS = 1, 2, 4, 8
 # dssm_plan_schedule bits (include/dssm.h DSSM_SCHED_*)
 SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_ADAM": 8,
@@ -200,6 +203,7 @@ _SIGS = {
     "dssm_comm_init": (C.c_int, [C.c_int, C.c_int, _P]),
     "dssm_allreduce_sum_f32": (C.c_int, [_P, C.c_int64, _P]),
     "dssm_comm_world": (C.c_int, []),
+    "dssm_comm_info": (C.c_int, [_P, _P, _P]),
     "dssm_allreduce_sum": (C.c_int, [_P, C.c_int64, C.c_int, _P]),
     "dssm_reduce_scatter_sum": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_all_gather": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),

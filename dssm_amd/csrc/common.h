@@ -205,44 +205,6 @@ __device__ __forceinline__ void loss_reduce(const float* __restrict__ part, int 
     }
   }
 }
-// loss_reduce over partials written by device-scope atomic stores (read at the coherence point)
-__device__ __forceinline__ void loss_reduce_coherent(const float* __restrict__ part, int nblk, int bs,
-                                            float* __restrict__ loss_out) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (wv == 0) {
-    float a = 0.f, b = 0.f;
-    int i = lane;
-    // eight partials' loads in flight per lane before the (in-order) adds: the launch is one
-    // wave, so its time is the load latency chain
-    for (; i + 7 * 64 < nblk; i += 8 * 64) {
-      float pa[8], pb[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        pa[k] = __hip_atomic_load(part + 2 * (i + 64 * k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pb[k] = __hip_atomic_load(part + 2 * (i + 64 * k) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        a += pa[k];
-        b += pb[k];
-      }
-    }
-    for (; i < nblk; i += 64) {
-      a += __hip_atomic_load(part + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      b += __hip_atomic_load(part + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // fixed-order tree over the 64 lane partials
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      a += __shfl_down(a, o);
-      b += __shfl_down(b, o);
-    }
-    if (lane == 0) {
-      loss_out[0] = a / (float)bs;
-      loss_out[1] = b / (float)bs;
-    }
-  }
-}
 
 // ---- zero fill as a kernel node -------------------------------------------------------------------
 // Every device-side clear that can enter a captured graph is a kernel (not a hipMemsetAsync node), so

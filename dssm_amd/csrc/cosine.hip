@@ -64,8 +64,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     const float* __restrict__ coef, float* __restrict__ y_out, float* __restrict__ cos_raw,
     float* __restrict__ cos_sim, float* __restrict__ prob, float* __restrict__ qnorm,
     float* __restrict__ part, float* __restrict__ dy, BnSide fs, CscScatter scat,
-    const int* __restrict__ rmap, float* __restrict__ loss_out, unsigned* __restrict__ fin_ticket,
-    CosDrop drop) {
+    const int* __restrict__ rmap, float* __restrict__ loss_out, CosDrop drop) {
   constexpr int NT = 64 * NW;
   COS_TL(0);
   __shared__ float s_part[2][NW];
@@ -338,27 +337,10 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       a += s_part[0][w];
       b += s_part[1][w];
     }
-    if (fin_ticket) {
-      // in-kernel finalize: the partials as device-scope atomic stores (performed at the coherence
-      // point, so no agent-scope release -- which would write back the XCD's L2, the dy rows just
-      // stored -- is needed before the arrival; the last arrival reads them with atomic loads)
-      __hip_atomic_store(part + 2 * blockIdx.x, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(part + 2 * blockIdx.x + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      part[2 * blockIdx.x] = a;
-      part[2 * blockIdx.x + 1] = b;
-    }
-  }
-  if (fin_ticket) {
-    __shared__ int s_lastf;
-    if (threadIdx.x == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's partial stores performed
-      const unsigned old = __hip_atomic_fetch_add(fin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_lastf = old == gridDim.x - 1;
-      if (s_lastf) __hip_atomic_store(fin_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
-    }
-    __syncthreads();
-    if (s_lastf) loss_reduce_coherent(part, gridDim.x, bs, loss_out);
+    // (an in-kernel finalize by the last workgroup behind a ticket measured slower on the multi-view
+    // and RNN steps in round 4 and was removed; the partials are summed by a later launch)
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
   }
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -380,8 +362,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               const float* coef, float* y_out, float* cos_raw, float* cos_sim,
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused, bool defer_finalize,
-                              const CscScatter* scatter, const int* rmap, unsigned* fin_ticket,
-                              const CosDrop* drop) {
+                              const CscScatter* scatter, const int* rmap, const CosDrop* drop) {
   if (neg + 1 > MAXK || n > kCosMaxN || (rmap && (fused || coef || y_out))) return hipErrorInvalidValue;
   const CosDrop dr = drop ? *drop : CosDrop{};
   if (dr.on && (fused || rmap || coef || scatter)) return hipErrorInvalidValue;  // the plain form only
@@ -390,33 +371,28 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
   const int blocks = cosine_blocks(bs, n, fused != nullptr);
   CscScatter sc = scatter ? *scatter : CscScatter{};
   if (sc.nblocks) sc.nblocks = std::max(1, sc.nblocks * 4 / nw);  // sized in 4-wave workgroups
-  if (scatter && (rmap || fin_ticket)) return hipErrorInvalidValue;  // the mapped / self-finalizing forms
+  if (scatter && rmap) return hipErrorInvalidValue;  // the mapped form
   // fused: + materialising and scatter blocks
   dim3 grid(blocks + (fused ? 1 : 0) + sc.nblocks), block(64 * nw);
   const int epl = cdiv(n, 64);
   const BnSide fs = fused ? *fused : BnSide{};
-  // in-kernel finalize: query workgroups only (the fused launch's extra blocks write no partials)
-  unsigned* const fin = (fin_ticket && !fused && !defer_finalize) ? fin_ticket : nullptr;
   if (fs.bdet.slab && (cdiv(bs, nw) > fs.bdet.cap || ld > 64 * kDetTiles)) return hipErrorInvalidValue;
   // The loss partials are summed by a later launch (deferred: the caller's next one; else a tiny
-  // launch here), or with fin_ticket by the kernel's last workgroup (partials as device-scope atomic
-  // stores: an agent-scope release in every workgroup would write back the XCD's L2 -- the dy rows
-  // just stored -- once per workgroup).
+  // launch here).
 #define DSSM_COS3(E, KM, F)                                                                     \
   if (nw == kCosFusedWaves)                                                                     \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, kCosFusedWaves>), grid, block, 0, s, z, ld, n, bs, neg, \
-                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin, \
-                       dr);                                                                     \
+                       gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, dr); \
   else if (rmap)                                                                                \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, true>), grid, block, 0, s, z, ld, n, bs, neg, gamma, \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap, loss_out, fin, dr); \
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, rmap, loss_out, dr); \
   else if (dr.on)                                                                               \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, false, 4, false, true>), grid, block, 0, s, z, ld, n, bs, neg, \
                        gamma, coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, \
-                       fin, dr);                                                                \
+                       dr);                                                                \
   else                                                                                          \
     hipLaunchKernelGGL((k_cosine_loss<E, KM, F, 4>), grid, block, 0, s, z, ld, n, bs, neg, gamma,    \
-                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, fin, dr)
+                       coef, y_out, cos_raw, cos_sim, prob, qnorm, ws, dy, fs, sc, nullptr, loss_out, dr)
 #define DSSM_COS2(E, KM) \
   if (fused) DSSM_COS3(E, KM, true); else DSSM_COS3(E, KM, false)
 #define DSSM_COS(E) \
@@ -428,7 +404,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 #undef DSSM_COS
 #undef DSSM_COS2
 #undef DSSM_COS3
-  if (!defer_finalize && !fin)
+  if (!defer_finalize)
     hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(64), 0, s, ws, blocks, bs, loss_out);
   return hipGetLastError();
 }

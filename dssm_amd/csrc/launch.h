@@ -189,8 +189,7 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
                               float* prob, float* qnorm, float* ws, float* loss_out, float* dy,
                               hipStream_t s, const BnSide* fused = nullptr,
                               bool defer_finalize = false, const CscScatter* scatter = nullptr,
-                              const int* rmap = nullptr, unsigned* fin_ticket = nullptr,
-                              const CosDrop* drop = nullptr);
+                              const int* rmap = nullptr, const CosDrop* drop = nullptr);
 // rmap (unfused, no coef / y_out): merged row r read from z row rmap[r]
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 // (queries per workgroup: kCosFusedWaves for the fused-statistics kernel at widths <= 128,

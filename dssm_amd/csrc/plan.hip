@@ -1081,15 +1081,22 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
   a.sh = sh;
   P->probe_begin(DSSM_PROBE_ADAM, s);
   if (P->pwire) {
+    // the Adam probe ends with the last chunk's Adam launch; the all-gather behind it (the data-
+    // parallel graph's hook) has its own probe
     for (int c = 0; c < P->geo.wp; ++c) {
+      const bool last = c == P->geo.wp - 1;
       if (int rc = dp_adam_chunk(P, a, c, s)) return rc;
-      if (P->dp_hook)
+      if (last) P->probe_end(DSSM_PROBE_ADAM, s);
+      if (P->dp_hook) {
+        if (last) P->probe_begin(DSSM_PROBE_DP_ALL_GATHER, s);
         if (int rc = P->dp_hook(c)) return rc;
+        if (last) P->probe_end(DSSM_PROBE_DP_ALL_GATHER, s);
+      }
     }
   } else {
     HIP_TRY(dssm::launch_adam_step(a, Lt.bf16, s));
+    P->probe_end(DSSM_PROBE_ADAM, s);
   }
-  P->probe_end(DSSM_PROBE_ADAM, s);
   P->grads_clean = true;
   return DSSM_OK;
 }
@@ -1551,19 +1558,9 @@ int dssm_bn_relu_fwd(const float* Z, int ldz, int rows, int n, const float* gamm
   return DSSM_OK;
 }
 
-// the functional cosine's finalize ticket: the word after the per-workgroup partials in the caller's
-// workspace (dssm_cosine_ws_floats: 2 * ceil(BS / 4) + 64 floats, zero-filled before first use)
-// (round 4: the last workgroup summing them in-kernel, behind a ticket in this word, measured slower on
-// the multi-view step -- 0.2554-0.2591 against 0.2424 ms/step -- and neutral on the RNN step; the
-// finalize stays a separate one-wave launch)
-#ifndef DSSM_COS_FIN_TICKET
-#define DSSM_COS_FIN_TICKET 0
-#endif
-static unsigned* cosine_fin_ticket(float* ws, int query_bs) {
-  if (!DSSM_COS_FIN_TICKET) return nullptr;
-  return reinterpret_cast<unsigned*>(ws + 2 * ((query_bs + 3) / 4));
-}
-
+// (round 4: the last workgroup summing the functional cosine's loss partials in-kernel, behind a
+// ticket, measured slower on the multi-view step -- 0.2554-0.2591 against 0.2424 ms/step -- and
+// neutral on the RNN step; removed: the finalize is a separate one-wave launch)
 int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_map, int n, int query_bs, int neg,
                                     float gamma, float* cos_sim_raw, float* cos_sim, float* prob,
                                     float* query_norm, float* loss, float* dy, float* ws, void* stream) {
@@ -1572,7 +1569,7 @@ int dssm_cosine_softmax_loss_mapped(const float* y, int ld, const int32_t* row_m
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss_mapped: bad arguments");
   HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
                                    cos_sim, prob, query_norm, ws, loss, dy, (hipStream_t)stream, nullptr,
-                                   false, nullptr, row_map, cosine_fin_ticket(ws, query_bs)));
+                                   false, nullptr, row_map));
   return DSSM_OK;
 }
 
@@ -1584,7 +1581,7 @@ int dssm_cosine_softmax_loss(const float* y, int ld, int n, int query_bs, int ne
     return fail(DSSM_E_INVALID, "dssm_cosine_softmax_loss: bad arguments");
   HIP_TRY(dssm::launch_cosine_loss(y, ld, n, query_bs, neg, gamma, nullptr, nullptr, cos_sim_raw,
                                    cos_sim, prob, query_norm, ws, loss, dy, (hipStream_t)stream, nullptr,
-                                   false, nullptr, nullptr, cosine_fin_ticket(ws, query_bs)));
+                                   false, nullptr, nullptr));
   return DSSM_OK;
 }
 
@@ -1609,7 +1606,7 @@ int dssm_cosine_softmax_loss_dropout(const float* x, int ld, int n, int query_bs
   d.bwd = bwd_scale / kd;
   HIP_TRY(dssm::launch_cosine_loss(x, ld, n, query_bs, neg, gamma, nullptr, y, cos_sim_raw, cos_sim, prob,
                                    query_norm, ws, loss, dy, (hipStream_t)stream, nullptr, false, nullptr, nullptr,
-                                   cosine_fin_ticket(ws, query_bs), &d));
+                                   &d));
   return DSSM_OK;
 }
 
@@ -1657,6 +1654,17 @@ int dssm_comm_init(int rank, int world, const void* unique_id128) {
 }
 
 int dssm_comm_world(void) { return g_comm ? g_world : 0; }
+
+int dssm_comm_info(int* rccl_world, int* rccl_rank, int* rccl_version) {
+  if (!rccl_world || !rccl_rank || !rccl_version) return fail(DSSM_E_INVALID, "null argument");
+  *rccl_world = *rccl_rank = -1;
+  RCCL_TRY(ncclGetVersion(rccl_version));
+  if (g_comm) {
+    RCCL_TRY(ncclCommCount(g_comm, rccl_world));
+    RCCL_TRY(ncclCommUserRank(g_comm, rccl_rank));
+  }
+  return DSSM_OK;
+}
 
 int dssm_allreduce_sum(void* buf, int64_t count, int dtype, void* stream) {
   if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
@@ -1811,20 +1819,31 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   P->rank_done_for = nullptr;
   int rc = DSSM_OK;
   // every node on the one captured stream, in dependency order (graph_topology checks the chain)
+  // probes (event-record nodes, the last step only): its phases (DSSM_PROBE_DP_*) and Adam shard
+  unsigned dp_mask = 1u << DSSM_PROBE_ADAM;
+  for (int id = DSSM_PROBE_DP_FWD_BWD; id <= DSSM_PROBE_DP_SHADOW; ++id) dp_mask |= 1u << id;
   for (int i = 0; i < nsteps && !rc; ++i) {
     g->probes = with_probes != 0 && i == nsteps - 1;
-    g->probe_mask = 1u << DSSM_PROBE_ADAM;
+    g->probe_mask = dp_mask;
     P->indptr = indptrs[i];
     P->indices = indices[i];
     P->values = values[i];
+    P->probe_begin(DSSM_PROBE_DP_FWD_BWD, s);
     rc = dssm_plan_forward(P, 1, stream);
     if (!rc) rc = dssm_plan_backward(P, stream);
-    // the gradient pass chunk by chunk, each chunk's all-to-all behind it
+    P->probe_end(DSSM_PROBE_DP_FWD_BWD, s);
+    // the gradient pass chunk by chunk, each chunk's all-to-all behind it (probes: chunk 0's)
     for (int c = 0; c < C && !rc; ++c) {
+      if (c == 0) P->probe_begin(DSSM_PROBE_DP_GRAD_PASS, s);
       rc = launch_wire_gradient_pass(P, s, C > 1 ? c : -1);
+      if (c == 0) P->probe_end(DSSM_PROBE_DP_GRAD_PASS, s);
+      if (c == 0) P->probe_begin(DSSM_PROBE_DP_ALL_TO_ALL, s);
       if (!rc) rc = dp_collective(P, k, 0, c, s);
+      if (c == 0) P->probe_end(DSSM_PROBE_DP_ALL_TO_ALL, s);
     }
+    P->probe_begin(DSSM_PROBE_DP_TAIL, s);
     if (!rc) rc = dp_collective(P, k, 2, 0, s);  // the fp32 tail (b1's row: the last chunk's pass)
+    P->probe_end(DSSM_PROBE_DP_TAIL, s);
     // Adam chunk by chunk, each chunk's all-gather behind its Adam
     if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {
       P->host_rank_indptr = indptrs[i + 1];
@@ -1838,10 +1857,12 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     // (w1_wire, tight rows of stride n: RawRow8<u16t>) and only the last step rebuilds the shadow,
     // which the next region's first step and the eval forward read.
     const bool direct = C == 1 && P->geo.n == P->Lt.n[0] && i + 1 < nsteps;
+    P->probe_begin(DSSM_PROBE_DP_SHADOW, s);
     for (int c = 0; c < C && !rc && !direct; ++c) {
       hipError_t e_ = dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s);
       if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string("launch_wire_shadow: ") + hipGetErrorString(e_));
     }
+    P->probe_end(DSSM_PROBE_DP_SHADOW, s);
     P->w1_wire = direct ? P->pwire : nullptr;
   }
   P->w1_wire = nullptr;

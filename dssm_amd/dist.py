@@ -103,6 +103,17 @@ class TorchTransport:
     def all_to_all(self, send, recv):
         self._host(lambda s, r: dist.all_to_all_single(r, s), send, recv)
 
+    def info(self) -> dict:
+        ver = None
+        if self.nccl:
+            try:
+                v = torch.cuda.nccl.version()
+                ver = v[0] * 10000 + v[1] * 100 + v[2] if isinstance(v, tuple) else int(v)
+            except Exception:  # noqa: BLE001 - informational only
+                ver = None
+        return {"transport": f"torch.distributed {dist.get_backend()}", "comm_world": dist.get_world_size(),
+                "comm_rank": dist.get_rank(), "rccl_version": ver}
+
     def destroy(self):
         pass
 
@@ -149,6 +160,13 @@ class LibTransport:
         assert send.numel() == recv.numel() and send.numel() % self.world == 0
         check(self.lib.dssm_all_to_all(ptr(send), ptr(recv), send.numel() // self.world, _dtype_id(send),
                                        stream_ptr()), "all_to_all")
+
+    def info(self) -> dict:
+        """The communicator as RCCL reports it (dssm_comm_info): its rank count, this rank, version."""
+        w, r, v = C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.dssm_comm_info(C.byref(w), C.byref(r), C.byref(v)), "comm_info")
+        return {"transport": "libdssm rccl", "comm_world": w.value, "comm_rank": r.value,
+                "rccl_version": v.value}
 
     def destroy(self):
         self.lib.dssm_comm_destroy()
@@ -425,15 +443,26 @@ class DataParallel:
         self._g_shadow = m.graph_build(shadow) if shadow else None
         self._shadows_pending = False
 
-    def graph_step(self, i: int):
-        """One step on staged batch i (mod the staged count) from the captured graphs."""
+    def graph_step(self, i: int, events=None):
+        """One step on staged batch i (mod the staged count) from the captured graphs.  events: a
+        list to which (phase, start, end) torch.cuda.Event pairs recorded on the current stream are
+        appended (bench.py's dp_kernels_ms for the host-issued exchange)."""
         m = self.model
         n = len(self._g_plain)
-        m.graph_launch((self._g_merged if self._shadows_pending else self._g_plain)[i % n])
-        self.exchange_before_adam()
-        m.graph_launch(self._g_adam)
+
+        def timed(name, fn):
+            if events is None:
+                return fn()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            events.append((name, a, b))
+        timed("fwd_bwd", lambda: m.graph_launch((self._g_merged if self._shadows_pending else self._g_plain)[i % n]))
+        timed("exchange_before_adam", self.exchange_before_adam)
+        timed("adam", lambda: m.graph_launch(self._g_adam))
         if self.mode == "zero":
-            self.exchange_after_adam()
+            timed("exchange_after_adam", self.exchange_after_adam)
             self._shadows_pending = self._g_shadow is not None
 
     def settle(self):

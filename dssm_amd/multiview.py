@@ -256,7 +256,13 @@ class MultiViewDSSM:
         self._csc_ev = None
         if self._fused:
             # the optimizer's CSC transposes (they depend on the batch only) on the item tower's
-            # stream while the caller's stream runs the loss: off the step's critical path
+            # stream while the caller's stream runs the loss: off the step's critical path.  They
+            # read the batch after the join above, so the batch tensors are marked in use on aux:
+            # a set_batch before apply_adam (eval loops) frees them, and the caching allocator
+            # must not hand their memory out again until aux's transposes have read it
+            for key in ("u", "i"):
+                for t in self.batch[key]:
+                    t.record_stream(self.aux)
             self._csc("u", "user", sa)
             self._csc_ev = self.aux.record_event()
             self._csc("i", f"view{self.view}", sa)

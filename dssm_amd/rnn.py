@@ -99,8 +99,13 @@ class RnnDSSM:
         off, rows, cols = self.layout[name]
         return arena[off:off + rows * cols].view(rows, cols)
 
-    def load_params(self, p: Dict[str, np.ndarray]):
+    def mark_params_changed(self):
+        """Call after writing self.params directly (arena copy, external restore, broadcast): the
+        workspace's bf16 embedding copy is stale, so the next bf16 forward re-converts it."""
         self._emb16_ok = False
+
+    def load_params(self, p: Dict[str, np.ndarray]):
+        self.mark_params_changed()
         self._block(self.params, "emb").copy_(torch.from_numpy(np.asarray(p["emb"], np.float32)))
         for d in ("fw", "bw"):
             g = np.concatenate([p[f"{d}_Wg"], p[f"{d}_bg"][None, :]], 0).astype(np.float32)

@@ -241,8 +241,18 @@ int dssm_plan_graph_build_steps(dssm_plan* plan, const int32_t* const* indptrs,
                                 int nsteps, int with_probes, void* stream, int* graph_id);
 
 /* Kernel timing probes (bench/roofline): HIP events recorded on the launch stream around one
- * kernel family for up to max_samples launches (0 disables); read back the summed duration. */
-enum { DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC, DSSM_PROBE_COUNT };
+ * kernel family for up to max_samples launches (0 disables); read back the summed duration.
+ * The DP_* probes time the phases of the LAST step of a data-parallel step graph
+ * (dssm_plan_graph_build_dp_steps with probes): forward + backward (gradient pass excluded), the
+ * wire gradient pass, the gradient all-to-all, the fp32 tail all-reduce, the parameter all-gather
+ * and the W1 shadow rebuild; DSSM_PROBE_ADAM there is the Adam shard alone (its all-gather
+ * excluded).  With wire chunks > 1 the gradient-pass / all-to-all / all-gather probes time chunk 0's
+ * launch (the first gradient pass / all-to-all, the last all-gather). */
+enum {
+  DSSM_PROBE_SPMM_FWD = 0, DSSM_PROBE_DW1, DSSM_PROBE_ADAM, DSSM_PROBE_CSC,
+  DSSM_PROBE_DP_FWD_BWD, DSSM_PROBE_DP_GRAD_PASS, DSSM_PROBE_DP_ALL_TO_ALL, DSSM_PROBE_DP_TAIL,
+  DSSM_PROBE_DP_ALL_GATHER, DSSM_PROBE_DP_SHADOW, DSSM_PROBE_COUNT
+};
 int dssm_plan_probe_enable(dssm_plan* plan, int probe_id, int max_samples);
 int dssm_plan_probe_read(dssm_plan* plan, int probe_id, float* total_ms, int* count);
 /* 1 when the plan's bf16 train steps run with the batch-norm statistics fused into the producing /
@@ -488,6 +498,9 @@ int dssm_relu_bwd(const float* y, int ldy, const float* dy, int lddy, int rows, 
 int dssm_comm_unique_id(void* out128);
 int dssm_comm_init(int rank, int world, const void* unique_id128);
 int dssm_comm_world(void);  /* world size, 0 before dssm_comm_init */
+/* The communicator as RCCL sees it (ncclCommCount / ncclCommUserRank; -1 before dssm_comm_init) and
+ * the linked RCCL's version (ncclGetVersion, e.g. 22703 for 2.27.3): for the N > 1 bench line. */
+int dssm_comm_info(int* rccl_world, int* rccl_rank, int* rccl_version);
 int dssm_allreduce_sum(void* buf, int64_t count, int dtype, void* stream);
 int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
 int dssm_reduce_scatter_sum(const void* send, void* recv, int64_t count, int dtype, void* stream);
@@ -561,7 +574,11 @@ int dssm_rnn_backward(const int32_t* ids, const int32_t* lens, int R, int T, int
  * with each direction's weights resident in VGPRs (bf16 copies of the fp32 w[4] made by the
  * kernels), fp32 states / accumulation / gradients, bf16 step caches in ws.  Same arguments and
  * outputs as the fp32 calls plus V (the embedding table's rows, for its bf16 copy in ws).
- * Shapes: (E, H) in {(128, 128), (64, 128), (32, 32)} (dssm_rnn_bf16_supported), V <= 32768. */
+ * Shapes: (E, H) in {(128, 128), (64, 128), (32, 32)} (dssm_rnn_bf16_supported), V <= 32768.
+ * Workspace contract: ws (dssm_rnn_bf16_ws_bytes) must be ZERO-FILLED before its first use and
+ * kept for this model alone: the backward's token-bucketing counts live in it, are assumed zero on
+ * entry and are re-zeroed by the backward itself (no clear launch per step).  A ws allocated with
+ * a plain hipMalloc and not cleared gives garbage start offsets (out-of-bounds position writes). */
 int dssm_rnn_bf16_supported(int E, int H);
 size_t dssm_rnn_bf16_ws_bytes(int R, int T, int E, int H, int V);
 int dssm_rnn_bf16_forward(const int32_t* ids, const int32_t* lens, int R, int T, const float* emb, int V,

@@ -86,6 +86,8 @@ def _load():
         _lib.dssm_cpu_adam.restype = None
         _lib.dssm_cpu_adam.argtypes = [C.POINTER(_Cfg), C.POINTER(_Params), C.POINTER(_Params),
                                        C.POINTER(_Params), C.POINTER(_Params), P, C.c_float]
+        _lib.dssm_cpu_set_threads.restype = C.c_int
+        _lib.dssm_cpu_set_threads.argtypes = [C.c_int]
         _lib.dssm_cpu_accuracy.restype = C.c_float
         _lib.dssm_cpu_accuracy.argtypes = [P]
         _lib.rnn_cpu_ws_create.restype = P
@@ -228,26 +230,46 @@ def _threads() -> int:
         return os.cpu_count() or 1
 
 
-def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 200):
-    """Timed full C2 training steps of the C/OpenMP restatement on synthetic batches."""
+def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 200, scaling=None,
+               scaling_budget_s: float = 2.5):
+    """Timed full C2 training steps of the C/OpenMP restatement on synthetic batches, on the
+    process's OpenMP team (OMP_NUM_THREADS: the box's CPU share).  scaling: thread counts (each at
+    most that team) whose rates are also timed, scaling_budget_s each (at least 2 steps), reported
+    as "scaling" {threads: pairs/s} -- how the port's rate grows with cores, for reading the
+    GPU / CPU ratio against a whole host."""
     from dssm_amd.data import ZipfColumns, synth_batch
     from .. import dssm_oracle as O
     cfg = O.OracleConfig(trigram_d=D, widths=list(widths), query_bs=BS, neg=NEG)
     m = CpuDSSM(D, widths, BS, NEG, O.init_params(cfg, seed=0))
     cols = ZipfColumns(D)
     batches = [synth_batch(D, BS, NEG, seed=1000 + b, cols=cols).as_dict() for b in range(4)]
+    team = m.lib.dssm_cpu_set_threads(0)
+
+    def rate(budget, cap, min_steps=1):
+        steps, t0 = 0, time.perf_counter()
+        while steps < cap:
+            m.train_step(batches[steps % len(batches)])
+            steps += 1
+            if steps >= min_steps and time.perf_counter() - t0 >= budget:
+                break
+        return steps, time.perf_counter() - t0
     m.train_step(batches[0])  # untimed warm-up
-    steps, t0 = 0, time.perf_counter()
-    while steps < max_steps:
-        m.train_step(batches[steps % len(batches)])
-        steps += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    el = time.perf_counter() - t0
-    return {"value": round(steps * BS * (NEG + 1) / el, 1), "unit": "pairs/s", "cores": _threads(),
-            "kind": "port",
-            "sample": f"{steps} full C2 training steps (fwd+bwd+dense Adam, BS={BS}, NEG={NEG}) of the "
-                      f"C/OpenMP fp32 restatement (oracle/cpu_c) in {el:.1f}s on {_threads()} threads"}
+    steps, el = rate(budget_s, max_steps)
+    out = {"value": round(steps * BS * (NEG + 1) / el, 1), "unit": "pairs/s", "cores": team,
+           "kind": "port",
+           "sample": f"{steps} full C2 training steps (fwd+bwd+dense Adam, BS={BS}, NEG={NEG}) of the "
+                     f"C/OpenMP fp32 restatement (oracle/cpu_c) in {el:.1f}s on {team} threads"}
+    if scaling:
+        sc = {}
+        for n in sorted({int(x) for x in scaling if 0 < int(x) <= team}):
+            m.lib.dssm_cpu_set_threads(n)
+            m.train_step(batches[1])  # untimed: the new team's first step
+            k, t = rate(scaling_budget_s, max_steps, min_steps=2)
+            sc[str(n)] = round(k * BS * (NEG + 1) / t, 1)
+        m.lib.dssm_cpu_set_threads(team)
+        out["scaling"] = {"threads_to_pairs_per_s": sc,
+                          "sample": f"full C2 steps, >= {scaling_budget_s}s (>= 2 steps) per thread count"}
+    return out
 
 
 class CpuRnnDSSM:

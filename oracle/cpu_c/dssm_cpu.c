@@ -396,3 +396,11 @@ float dssm_cpu_forward_backward(const cpu_cfg* c, cpu_params* P, cpu_params* G, 
 }
 
 float dssm_cpu_accuracy(void* ws) { return ((cpu_ws*)ws)->acc; }
+
+/* OpenMP team size of the following steps (bench.py's cpu_baseline.scaling: 1..16 threads inside the
+ * box's CPU share); n <= 0 leaves it as OMP_NUM_THREADS set it.  Returns the team size now in effect. */
+#include <omp.h>
+int dssm_cpu_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+}

@@ -37,15 +37,17 @@ def host_cpus() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000, use_c: bool = True):
+def time_steps(D, widths, BS, NEG, budget_s: float = 15.0, max_steps: int = 100000, use_c: bool = True,
+               scaling=None):
     """use_c=False times the NumPy float32 oracle even when the C port is built (SURVEY §8(d)'s
-    secondary CPU number)."""
+    secondary CPU number).  scaling: thread counts for the C port's rate-vs-threads record."""
     from dssm_amd.data import ZipfColumns, synth_batch  # synthetic batches only (host numpy)
     if use_c:
         try:
             from . import cpu_c
             if cpu_c.available():
-                out = cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps)
+                out = cpu_c.time_steps(D, widths, BS, NEG, budget_s=budget_s, max_steps=max_steps,
+                                       scaling=scaling)
                 out["host"] = host_cpus()
                 return out
         except ImportError:

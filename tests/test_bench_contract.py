@@ -53,33 +53,55 @@ def test_committed_lines_keep_the_contract(name):
     assert "workload" in d["config"]
 
 
-def test_gpus_n_spawns_its_own_ranks(monkeypatch):
+def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     """`bench.py --gpus N` started as a plain process (the driver's verb) launches its N ranks as a
-    child torch.distributed.run on 127.0.0.1 with the same arguments, before any GPU call."""
+    child torch.distributed.run on 127.0.0.1 with the same arguments, before any GPU call; by default
+    a second child then runs the one-all-reduce exchange, and the parent prints ONE line carrying
+    the second run's summary as dp_alt."""
+    import io
+    import json
     import subprocess
     import sys
-    seen = {}
+    seen = []
 
     class FakeChild:
-        def __init__(self, cmd, env=None):
-            seen["cmd"], seen["env"] = cmd, env
+        def __init__(self, cmd, env=None, stdout=None, text=None):
+            seen.append((cmd, env))
+            head = {"value": 1.0, "ms_per_step": 2.0, "steps": 20, "warmup": 5, "unit": "pairs/s",
+                    "config": {"dp_exchange": "zero/bf16 via rccl" if len(seen) == 1 else "allreduce via rccl"},
+                    "dp_kernels_ms": {"adam": 0.05}}
+            self.stdout = io.StringIO("progress\n" + json.dumps(head) + "\n") if stdout is not None else None
+            self.rc = 7 if stdout is None else 0
 
         def wait(self):
-            return 7
+            return self.rc
 
         def send_signal(self, sig):
             pass
     monkeypatch.setattr(subprocess, "Popen", FakeChild)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
-    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5", "--dp-alt", "0"])
     args = bench.parse()
     assert args.comm == "rccl"  # strict library RCCL by default: a fallback is never timed
     assert bench.spawn_ranks(args) == 7
-    cmd = seen["cmd"]
+    cmd, env = seen[0]
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
-    assert cmd[-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
-    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert cmd[-8:] == ["--gpus", "8", "--steps", "20", "--warmup", "5", "--dp-alt", "0"]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # default: the headline child, then the allreduce / fp32-wire child; one merged line
+    seen.clear()
+    capsys.readouterr()
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
+    assert bench.spawn_ranks(bench.parse()) == 0
+    assert len(seen) == 2
+    assert seen[0][0][-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    assert seen[1][0][-6:] == ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0"]
+    lines = [x for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["config"]["dp_exchange"] == "zero/bf16 via rccl"
+    assert d["dp_alt"]["dp_exchange"] == "allreduce via rccl" and d["dp_alt"]["dp_kernels_ms"] == {"adam": 0.05}
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--backend", "gloo"])
     assert bench.parse().comm == "torch"
 

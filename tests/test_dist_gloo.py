@@ -1,4 +1,4 @@
-"""Data-parallel path on CPU: world_size 2 and 4 over gloo.
+"""Data-parallel path on CPU: world_size 2, 4 and 8 over gloo (8 = the driver's node).
 
 Each rank runs `dssm_amd.dist.DataParallel` (the product's DP step: forward, backward, the
 gradient exchange of its schedule, Adam with grad_scale = 1/world) with the torch.distributed
@@ -144,7 +144,7 @@ def _free_port():
 
 
 def _worker(rank, port, out_dir, mode, wire, world, chunks):
-    os.environ["OMP_NUM_THREADS"] = "2"
+    os.environ["OMP_NUM_THREADS"] = "1" if world >= 8 else "2"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         cfg = O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS, neg=NEG)
@@ -165,7 +165,7 @@ def _worker(rank, port, out_dir, mode, wire, world, chunks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("mode,wire,chunks", [("allreduce", "fp32", 1), ("zero", "fp32", 1), ("zero", "bf16", 1),
                                               ("zero", "bf16", 3)])
 def test_data_parallel_gloo(mode, wire, chunks, world):

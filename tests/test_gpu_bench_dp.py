@@ -37,6 +37,18 @@ def test_bench_gpus2_spawns_ranks_and_checks_them():
     chk = d["dp_check"]
     assert chk["world"] == 2 and chk["ranks_identical"] is True and chk["finite"] is True
     assert d["value"] > 0 and d["value"] == pytest.approx(2 * 1024 * 5 * 4 / (d["ms_per_step"] * 4e-3), rel=1e-3)
+    # self-explaining N > 1 line: the exchange's phases of the last timed step, the communicator
+    comm = d["config"]["comm"]
+    assert comm["comm_world"] == 2 and comm["comm_rank"] == 0 and "gloo" in comm["transport"]
+    ph = d["dp_kernels_ms"]
+    for k in ("fwd_bwd", "exchange_before_adam", "adam", "exchange_after_adam"):
+        assert ph[k] > 0, (k, ph)
+    # the second child: the one-all-reduce exchange on the same two ranks
+    alt = d["dp_alt"]
+    assert "error" not in alt, alt
+    assert alt["dp_exchange"] == "allreduce via torch" and alt["value"] > 0
+    assert alt["dp_check"]["ranks_identical"] is True and alt["dp_check"]["world"] == 2
+    assert alt["dp_kernels_ms"]["exchange_before_adam"] > 0
 
 
 @pytest.mark.gpu
@@ -46,3 +58,25 @@ def test_bench_multiview_gpus2_spawns_ranks_and_checks_them():
     assert d["config"]["dp_exchange"] == "torch"
     chk = d["dp_check"]
     assert chk["world"] == 2 and chk["ranks_identical"] is True and chk["finite"] is True
+
+
+@pytest.mark.gpu
+def test_bench_rehearsal_reports_dp_phases():
+    """The captured data-parallel step graph (the one the RCCL ranks time) rehearsed on one GPU with
+    its collectives as device copies: the last step's phase probes are all recorded."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse-world", "8", "--rehearse-comm", "copy",
+           "--steps", "4", "--warmup", "2", "--cpu-baseline", "0", "--fp32-line", "0", "--det-line", "0",
+           "--fwd-only", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    ph = d["dp_kernels_ms"]
+    for k in ("fwd_bwd", "grad_pass", "all_to_all", "tail_allreduce", "adam", "all_gather", "shadow_rebuild"):
+        assert k in ph, (k, ph)
+    for k in ("fwd_bwd", "grad_pass", "all_to_all", "adam", "all_gather", "shadow_rebuild"):
+        assert ph[k] > 0, (k, ph)
+    # the step's phases fit inside its measured time
+    assert sum(v for k, v in ph.items() if k != "source") <= 1.2 * d["ms_per_step"], (ph, d["ms_per_step"])

@@ -115,6 +115,35 @@ def test_multiview_fused_w1_adam(dtype):
     assert np.isfinite(losses).all() and losses[-1] < losses[0], losses[::3]
 
 
+def test_multiview_fused_forward_only_set_batch_loop():
+    """Eval-style loop in fused mode (set_batch, forward, loss; no backward / Adam): forward()
+    leaves the optimizer's CSC transposes running on self.aux after its only join, and set_batch
+    frees the previous batch tensors.  The batch tensors are marked in use on aux (record_stream), so
+    their memory is not handed out again while the transposes read them: every loss equals the
+    unfused model's on the same batch, and a train step after the loop still matches."""
+    cfg, p, rot, ref, _, _ = _setup(2, bs=512, fused=False)
+    _, _, _, m, _, _ = _setup(2, bs=512, fused=True)
+    rng = np.random.Generator(np.random.PCG64(5))
+    for i in range(8):
+        view = 1 + i % 3
+        uu = synth_rows(rng, ZipfColumns(cfg.user_d), cfg.bs, 16.0)
+        ii = synth_rows(rng, ZipfColumns(cfg.view_d[view - 1]), cfg.bs, 16.0)
+        for x in (ref, m):
+            x.set_batch(uu, ii, view)
+            x.forward()
+        # allocations on the caller's stream while aux may still read the freed batch
+        junk = [torch.full((4096,), -1, dtype=torch.int32, device=m.device) for _ in range(8)]
+        assert abs(m.loss() - ref.loss()) <= 1e-6 * abs(ref.loss()), (i, m.loss(), ref.loss())
+        del junk
+    for x in (ref, m):
+        x.backward()
+        x.apply_adam()
+    torch.cuda.synchronize()
+    pa, pb = ref.params.cpu().numpy(), m.params.cpu().numpy()
+    d = np.abs(pa - pb)
+    assert d.max() <= 2 * cfg.lr and (d <= 1e-5).mean() >= 0.999, (d.max(), (d > 1e-5).sum())
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_multiview_fused_graph_matches_eager(dtype):
     """The fused step's stream structure (item tower and transposes on self.aux, the optimizer launches
