@@ -22,6 +22,7 @@
 #include "common.h"
 #include "launch.h"
 #include "tn.h"
+#include "g32.h"
 
 namespace dssm {
 namespace {
@@ -448,16 +449,42 @@ constexpr int kApplyMaxLd = 512;
 // LDS of the launch: the coefficient cache of the element blocks, or the double-buffered operand
 // tiles of the dW blocks (tn.h)
 static_assert(kTnTile * 2 >= 128 * kTnLd, "a 128-row sub-chunk per operand");
-constexpr int kApplySmemFloats = 2 * 6 * kApplyMaxLd > kTnTile * 2 ? 2 * 6 * kApplyMaxLd : kTnTile * 2;
+// TO = u16 (bf16 dZ; hosted dW tiles: tn.h) or float (fp32 parity mode; hosted tiles: g32.h)
+template <typename TO>
+struct ApplyDw;
+template <>
+struct ApplyDw<u16> {
+  using P = TnParams;
+  static constexpr int kFloats = kTnTile * 2;
+  __device__ static void run(const P& dw, int r, int dw_x, int dw_y, float* smem) {
+    u16* sA = reinterpret_cast<u16*>(smem);
+    tn_chunk_body<3>(dw, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y), sA, sA + 2 * kTnTile);
+  }
+};
+template <>
+struct ApplyDw<float> {
+  using P = G32Params;
+  static constexpr int kFloats = (int)(sizeof(G32Lds) / 4);
+  __device__ static void run(const P& dw, int r, int dw_x, int dw_y, float* smem) {
+    g32_body<G32_DW, 0, kG32DwSplit / kG32KC>(dw, G32Fuse{}, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y),
+                                              *reinterpret_cast<G32Lds*>(smem));
+  }
+};
+template <typename TO>
+constexpr int apply_smem_floats() {
+  return 2 * 6 * kApplyMaxLd > ApplyDw<TO>::kFloats ? 2 * 6 * kApplyMaxLd : ApplyDw<TO>::kFloats;
+}
+
+template <typename TO>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
-                                                         u16* __restrict__ dZ,
+                                                         TO* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
                                                          int loss_blocks,
                                                          float* __restrict__ loss_out,
-                                                         int nwork, TnParams dw,
+                                                         int nwork, typename ApplyDw<TO>::P dw,
                                                          int dw_x, int dw_y, int dw_blocks) {
-  __shared__ __attribute__((aligned(16))) float smem[kApplySmemFloats];
+  __shared__ __attribute__((aligned(16))) float smem[apply_smem_floats<TO>()];
   // blocks [0, dw_blocks): the previous backward pair's dW split-K tiles (the longest chains,
   // first in dispatch order); they read dZ of the layer above and the forward's activations, so
   // they are independent of this launch's own work
@@ -467,8 +494,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
 #define DSSM_XCD_DW_APPLY 1
 #endif
     const int r = DSSM_XCD_DW_APPLY ? xcd_tile(blockIdx.x, dw_blocks) : (int)blockIdx.x;
-    u16* sA = reinterpret_cast<u16*>(smem);
-    tn_chunk_body<3>(dw, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y), sA, sA + 2 * kTnTile);
+    ApplyDw<TO>::run(dw, r, dw_x, dw_y, smem);
     return;
   }
   const int bid = (int)blockIdx.x - dw_blocks;
@@ -541,10 +567,14 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
       bwd_terms(zz[k], dd[k], sc[t][0][c + k], sc[t][1][c + k], sc[t][2][c + k], sc[t][3][c + k], dy, xh);
       out[k] = sc[t][2][c + k] * (dy - sc[t][4][c + k] - xh * sc[t][5][c + k]);
     }
-    uint2 p;
-    p.x = pack2bf(out[0], out[1]);
-    p.y = pack2bf(out[2], out[3]);
-    *reinterpret_cast<uint2*>(dZ + (size_t)r * ld + c) = p;
+    if constexpr (sizeof(TO) == 2) {
+      uint2 p;
+      p.x = pack2bf(out[0], out[1]);
+      p.y = pack2bf(out[2], out[3]);
+      *reinterpret_cast<uint2*>(dZ + (size_t)r * ld + c) = p;
+    } else {
+      *reinterpret_cast<float4*>(dZ + (size_t)r * ld + c) = make_float4(out[0], out[1], out[2], out[3]);
+    }
   }
 }
 
@@ -626,22 +656,35 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
   return hipGetLastError();
 }
 
-hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
-                                     hipStream_t s, const float* loss_part, int loss_blocks,
-                                     float* loss_out, const TnParams* dw) {
+template <typename TO>
+static hipError_t apply_fused(const float* Z, const float* dA, const BnSide& b, TO* dZ, hipStream_t s,
+                              const float* loss_part, int loss_blocks, float* loss_out,
+                              const typename ApplyDw<TO>::P* dw, int max_kps) {
   if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
   // element workgroups: fewer beside hosted dW tiles, which share the CUs
 #ifndef DSSM_APPLY_GRID_DW
 #define DSSM_APPLY_GRID_DW 512
 #endif
   const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? DSSM_APPLY_GRID_DW : 1024);
-  if (dw && dw->k_per_split > 3 * 128) return hipErrorInvalidValue;  // tn_chunk_body<3>
-  const TnParams p = dw ? *dw : TnParams{};
+  if (dw && dw->k_per_split > max_kps) return hipErrorInvalidValue;
+  const typename ApplyDw<TO>::P p = dw ? *dw : typename ApplyDw<TO>::P{};
   const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
   const int dw_blocks = dw ? dw_x * dw_y * cdiv(p.K, p.k_per_split) : 0;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, dA, b,
-                     (u16*)dZ, loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks);
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs<TO>, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, dA, b, dZ,
+                     loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks);
   return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
+                                     hipStream_t s, const float* loss_part, int loss_blocks,
+                                     float* loss_out, const TnParams* dw) {
+  return apply_fused<u16>(Z, dA, b, (u16*)dZ, s, loss_part, loss_blocks, loss_out, dw, 3 * 128);  // tn_chunk_body<3>
+}
+
+hipError_t launch_bn_bwd_apply_fused32(const float* Z, const float* dA, const BnSide& b, float* dZ,
+                                       hipStream_t s, const float* loss_part, int loss_blocks,
+                                       float* loss_out, const G32Params* dw) {
+  return apply_fused<float>(Z, dA, b, dZ, s, loss_part, loss_blocks, loss_out, dw, kG32DwSplit);
 }
 
 }  // namespace dssm

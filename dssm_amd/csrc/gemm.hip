@@ -1259,6 +1259,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 size_t gemm_dw_slab_floats(int M, int N, int K, bool bf16) {
   int splits = dw_splits(M, N, K, bf16 ? Cfg<u16>::BK : Cfg<float>::BK);
   if (bf16) splits = std::max(splits, cdiv(K, kTwKc));  // the whole-K pair's chunk count
+  else splits = std::max(splits, g32_dw_splits(K));      // the fp32 pair's (gemm32.hip)
   return splits > 1 ? (size_t)splits * M * N : 0;
 }
 

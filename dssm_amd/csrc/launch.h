@@ -11,6 +11,7 @@ namespace dssm {
 struct BnSide;    // bnfuse.h
 struct DetAcc;    // bnfuse.h
 struct TnParams;  // tn.h
+struct G32Params;  // g32.h
 
 // Eval-mode (on_train=False) BN coefficients of every layer from the EMA shadows
 // (new_dssm.py:85-86): they depend on the parameters only, not on the batch, so the forward
@@ -132,6 +133,27 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 // caller then sums the slabs into gw with launch_splitk_reduce.
 hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float* dst, hipStream_t s);
 
+// ---- fp32 parity mode's fused dense layers (gemm32.hip, g32.h: f32-input MFMA 16x16x4) ----
+// Forward of layer l: C = relu(BN_{l-1}(Z)) . W + bias with W [K x ldw] row-major (the arena's
+// block), the activation written to a_out (fp32, ld lda), BN coefficients from in_from_sums (then
+// materialised by one extra workgroup) or coef; Z_l's per-tower column sums into out_sum.
+// K <= 320, widths multiples of 4, row_split % 64 == 0.
+hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const float* coef,
+                          const BnSide* in_from_sums, int row_split, const float* W, int ldw, float* C,
+                          int ldc, const float* bias, float* a_out, double* out_sum, hipStream_t s,
+                          const DetAcc* det = nullptr);
+// Backward of layer l: dA_{l-1} = dZ_l . W_l^T (BN_{l-1}'s backward sums from z_prev / coef_prev
+// into bsum_prev); dW_l = [A_{l-1}; 1]^T . dZ_l in kG32DwSplit-row split-K slabs, handed to
+// *dw_out for the next BN-backward apply launch or launched here (then reduced into gw unless
+// defer: *deferred_splits = count for the Adam step).
+hipError_t launch_g32_pair(int M, int kin, int n, const float* dZ, int lddz, const float* W, int ldw,
+                           float* dA, int ldda, const float* z_prev, const float* coef_prev, double* bsum_prev,
+                           int row_split, const float* A_prev, int lda_prev, float* slab, float* gw, bool defer,
+                           hipStream_t s, int* deferred_splits, G32Params* dw_out = nullptr,
+                           const DetAcc* det = nullptr);
+hipError_t launch_g32_dw(const G32Params& dw, hipStream_t s);
+int g32_dw_splits(int rows);
+
 // ---- batch norm (bn.hip) ----
 struct BnTowers {
   int row_split;   // rows [0,row_split) tower 0 (query), [row_split, rows) tower 1 (doc)
@@ -158,6 +180,11 @@ hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSi
                                      hipStream_t s, const float* loss_part = nullptr,
                                      int loss_blocks = 0, float* loss_out = nullptr,
                                      const TnParams* dw = nullptr);
+// fp32 parity mode: dZ stored fp32; the hosted dW tiles are the fp32 ones (g32.h)
+hipError_t launch_bn_bwd_apply_fused32(const float* Z, const float* dA, const BnSide& b, float* dZ,
+                                       hipStream_t s, const float* loss_part = nullptr,
+                                       int loss_blocks = 0, float* loss_out = nullptr,
+                                       const G32Params* dw = nullptr);
 // out = relu?(Z*inv + shift) in out dtype; pads zero.
 hipError_t launch_bn_apply(const float* Z, int ldz, int n, BnTowers t, const float* coef,
                            bool relu, void* out, bool out_bf16, hipStream_t s);

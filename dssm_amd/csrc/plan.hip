@@ -17,6 +17,7 @@
 #include "bnfuse.h"
 #include "launch.h"
 #include "tn.h"
+#include "g32.h"
 #include "csc.h"
 
 namespace {
@@ -166,9 +167,9 @@ void make_layout(const dssm_config* c, Layout& Lt) {
   Lt.heavy_slab = take(dssm::csc_heavy_cap(Lt.R, Lt.max_nnz) * Lt.n[0] * 4);
   // {beta1_power, beta2_power} (device-side Adam step state), then the Adam kernel's tickets
   Lt.adam_state = take(4 * (64 + dssm::kAdamTicketUints));
-  if (Lt.bf16) {
-    // fp64 [2 towers][2][ld] forward and backward accumulators per layer (fused statistics), one
-    // contiguous region zeroed as a whole by the step's first launch
+  {
+    // fp64 [2 towers][2][ld] forward and backward accumulators per layer (fused statistics, both
+    // dtypes), one contiguous region zeroed as a whole by the step's first launch
     size_t sums = 0;
     for (int l = 0; l < Lt.L; ++l) sums += 2 * (size_t)4 * Lt.ldp[l] * 8;
     Lt.sums = take(sums);
@@ -318,6 +319,8 @@ struct dssm_plan {
   }
   // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
   bool wholek(int l) const { return Lt.bf16 && l > 0 && Lt.ldp[l - 1] <= 512; }
+  // fp32 parity mode: layer l (>= 1) on the fused fp32 MFMA tiles (g32.h: K <= 320 both ways)
+  bool nt32(int l) const { return !Lt.bf16 && l > 0 && Lt.in_dim[l] <= 320 && Lt.n[l] <= 320; }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
   dssm::BnSide bn_side(int l) const {
     dssm::BnSide b{};
@@ -364,11 +367,11 @@ struct dssm_plan {
   }
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
   bool fused_stats_ok() const {
-    if (!Lt.bf16 || Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
+    if (Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
       if (Lt.ldp[l] > 512) return false;
     for (int l = 1; l < Lt.L; ++l)
-      if (!wholek(l)) return false;
+      if (!(Lt.bf16 ? wholek(l) : nt32(l))) return false;
     return true;
   }
   dssm::ShadowList shadows() {
@@ -696,6 +699,13 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       const dssm::BnSide out = P->bn_side(l);
+      if (!Lt.bf16) {  // fp32 parity mode: W_l straight from the arena ([in x n] row-major)
+        HIP_TRY(dssm::launch_g32_fwd(Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
+                                     P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->p + Lt.fc_off[l], Lt.n[l],
+                                     P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<float>(Lt.A[l - 1]),
+                                     P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr));
+        continue;
+      }
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
           Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
           P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->at<uint16_t>(Lt.shadowT[l]), Lt.ldp[l - 1],
@@ -827,7 +837,8 @@ static int backward_impl(dssm_plan* P, void* stream) {
     // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply.
     // DW_IN_APPLY: the pair launches run their dA tiles only (one round) and each dW_l's tiles
     // ride in the following apply launch (BN_{l-1}'s), whose element blocks leave CUs idle
-    dssm::TnParams dw{};
+    dssm::TnParams dw{};      // bf16: dW_l's split-K tiles handed from the pair to the next apply
+    dssm::G32Params dw32{};   // fp32: the same for the g32.h tiles
     bool dw_pending = false;
     float* dw_reduce_to = nullptr;
     // dW_l's split-K slabs summed later: by the fused Adam step, or by the wire gradient pass
@@ -835,14 +846,22 @@ static int backward_impl(dssm_plan* P, void* stream) {
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
-      HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
-                                              P->at<uint16_t>(Lt.dZ[l]), s,
-                                              fin ? P->at<float>(Lt.loss_j) : nullptr,
-                                              dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true),
-                                              P->at<float>(Lt.loss), dw_pending ? &dw : nullptr));
+      const float* lp = fin ? P->at<float>(Lt.loss_j) : nullptr;
+      const int lb = dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true);
+      if (Lt.bf16)
+        HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
+                                                P->at<uint16_t>(Lt.dZ[l]), s, lp, lb, P->at<float>(Lt.loss),
+                                                dw_pending ? &dw : nullptr));
+      else
+        HIP_TRY(dssm::launch_bn_bwd_apply_fused32(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
+                                                  P->at<float>(Lt.dZ[l]), s, lp, lb, P->at<float>(Lt.loss),
+                                                  dw_pending ? &dw32 : nullptr));
       if (dw_pending && dw_reduce_to) {  // not deferred to Adam: the slabs summed right after
-        const int nsplit = (dw.K + dw.k_per_split - 1) / dw.k_per_split;
-        HIP_TRY(dssm::launch_splitk_reduce(dw.C, nsplit, (int64_t)dw.M * dw.N, dw_reduce_to, s));
+        const float* slab = Lt.bf16 ? dw.C : dw32.C;
+        const int nsplit = Lt.bf16 ? (dw.K + dw.k_per_split - 1) / dw.k_per_split
+                                   : (dw32.K + dw32.k_per_split - 1) / dw32.k_per_split;
+        const int64_t cnt = Lt.bf16 ? (int64_t)dw.M * dw.N : (int64_t)dw32.M * dw32.N;
+        HIP_TRY(dssm::launch_splitk_reduce(slab, nsplit, cnt, dw_reduce_to, s));
       }
       dw_pending = false;
       dw_reduce_to = nullptr;
@@ -851,15 +870,26 @@ static int backward_impl(dssm_plan* P, void* stream) {
       const bool host_dw = P->on(DSSM_OPT_DW_IN_APPLY);
       const dssm::BnSide bprev = P->bn_side(l - 1);
       dw = dssm::TnParams{};  // filled by the pair launch when it hands its dW tiles over
-      HIP_TRY(dssm::launch_bwd_pair(
-          Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
-          P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
-          P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
-          Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
-          P->g + Lt.fc_off[l], defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
-          P->deterministic() ? &bprev.bdet : nullptr));
-      dw_pending = host_dw && dw.C != nullptr;
-      if (dw_pending && !defer_slabs && dw.C != P->g + Lt.fc_off[l]) dw_reduce_to = P->g + Lt.fc_off[l];
+      dw32 = dssm::G32Params{};
+      float* gw = P->g + Lt.fc_off[l];
+      if (Lt.bf16)
+        HIP_TRY(dssm::launch_bwd_pair(
+            Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
+            P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
+            P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]), P->at<double>(Lt.bsum[l - 1]),
+            Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.dw_slab[l]),
+            gw, defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw : nullptr,
+            P->deterministic() ? &bprev.bdet : nullptr));
+      else  // fp32: W_l [in x n] from the arena is dA's B^T as it lies
+        HIP_TRY(dssm::launch_g32_pair(
+            Lt.R, Lt.in_dim[l], Lt.n[l], P->at<float>(Lt.dZ[l]), Lt.ldp[l], P->p + Lt.fc_off[l], Lt.n[l],
+            P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]),
+            P->at<double>(Lt.bsum[l - 1]), Lt.BS, P->at<float>(Lt.A[l - 1]), Lt.ldp[l - 1],
+            P->at<float>(Lt.dw_slab[l]), gw, defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw32 : nullptr,
+            P->deterministic() ? &bprev.bdet : nullptr));
+      const float* handed = Lt.bf16 ? dw.C : dw32.C;
+      dw_pending = host_dw && handed != nullptr;
+      if (dw_pending && !defer_slabs && handed != gw) dw_reduce_to = gw;
     }
     return dw1_backward(P, s);
   }
@@ -1216,9 +1246,13 @@ int dssm_plan_schedule(const dssm_plan* P) {
   if (P->merged_csc()) f |= DSSM_SCHED_MERGED_CSC;
   if (P->heavy_in_adam()) f |= DSSM_SCHED_HEAVY_IN_ADAM;
   if (P->fused_w1_adam()) f |= DSSM_SCHED_FUSED_W1_ADAM;
-  bool wk = P->Lt.L > 1;
-  for (int l = 1; l < P->Lt.L; ++l) wk = wk && P->wholek(l);
+  bool wk = P->Lt.L > 1, w32 = P->Lt.L > 1;
+  for (int l = 1; l < P->Lt.L; ++l) {
+    wk = wk && P->wholek(l);
+    w32 = w32 && P->nt32(l);
+  }
   if (wk) f |= DSSM_SCHED_WHOLEK;
+  if (fs && w32) f |= DSSM_SCHED_NT32;
   if (fs && P->on(DSSM_OPT_DW_IN_APPLY)) f |= DSSM_SCHED_DW_IN_APPLY;
   if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
   if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;

@@ -269,7 +269,8 @@ enum {
   DSSM_SCHED_WHOLEK = 16,          /* layers >= 2 on the whole-K bf16 NT / backward-pair GEMMs */
   DSSM_SCHED_DW_IN_APPLY = 32,     /* dW_l split-K tiles inside the next BN-backward apply launch */
   DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
-  DSSM_SCHED_DETERMINISTIC = 128   /* fixed-order reductions: bit-identical repeated runs */
+  DSSM_SCHED_DETERMINISTIC = 128,  /* fixed-order reductions: bit-identical repeated runs */
+  DSSM_SCHED_NT32 = 256            /* fp32: layers >= 2 on the fused fp32 MFMA tiles (g32.h) */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
 /* A train forward (either precision) leaves the loss / accuracy reduction to the backward's first
