@@ -466,7 +466,9 @@ struct ApplyDw<float> {
   using P = G32Params;
   static constexpr int kFloats = (int)(sizeof(G32Lds) / 4);
   __device__ static void run(const P& dw, int r, int dw_x, int dw_y, float* smem) {
-    g32_body<G32_DW, 0, kG32DwSplit / kG32KC>(dw, G32Fuse{}, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y),
+    G32Fuse f{};
+    f.tl_slot = -1;
+    g32_body<G32_DW, 0, kG32DwSplit / kG32KC>(dw, f, r % dw_x, (r / dw_x) % dw_y, r / (dw_x * dw_y),
                                               *reinterpret_cast<G32Lds*>(smem));
   }
 };

@@ -8,11 +8,13 @@
 // One 256-thread workgroup computes a 64 x 64 tile (4 waves of 32 x 32 = 2 x 2 MFMA 16 x 16 blocks).
 // K runs in 32-deep chunks: every chunk's global loads go to registers D chunks ahead (a ring of
 // D + 1 register sets, the chunk loop fully unrolled so every index is compile-time), the current
-// chunk is written to one of two LDS images and read back one fp32 per lane per MFMA operand
-// (64 FLOP/clk/SIMD at 32 cycles per MFMA leaves the LDS idle).  Images are stored as the operand
-// lies in memory:
-//   RK ([row][k], 36-float rows): 16 rows x 4 consecutive k per read -> 64 distinct banks
-//   KR ([k][row], 80-float rows): 4 k rows x 16 consecutive columns -> 64 distinct banks
+// chunk is written to one of two LDS images and read back in 8-deep k steps: two MFMAs per step,
+// MFMA q taking k = kk + 2 g + q from lane group g = lane >> 4 (the same permutation for A and B, so
+// each lane holds two consecutive k of its row / column).  Images are stored as the operand lies in
+// memory (MI355X_MICROARCH.md LDS banking):
+//   RK ([row][k], 36-float rows): one ds_read_b64 per lane, 16 rows x 2 groups -> 64 distinct banks
+//   KR ([k][row], 72-float rows): one ds_read2_b32 (rows kk + 2g, + 1) per lane; each of its reads
+//       covers 16 columns x 2 groups on 32 distinct banks
 // FWD: A = Z_{l-1} [M x lda] (RK, BN + ReLU applied while staging), B = W_l [K x ldb] (KR)
 // DA : A = dZ_l  [M x lda] (RK), B^T = W_l [N x ldb], i.e. W's rows (RK)
 // DW : A^T of A_{l-1} [K x lda] (KR, a virtual ones column at m == M - 1 gives db), B = dZ_l (KR)
@@ -24,12 +26,15 @@ namespace dssm {
 
 constexpr int kG32KC = 32;                    // k per chunk
 constexpr int kG32LdRK = kG32KC + 4;          // 36
-constexpr int kG32LdKR = 64 + 16;             // 80
+constexpr int kG32LdKR = 64 + 8;              // 72
 constexpr int kG32Img = 64 * kG32LdRK > kG32KC * kG32LdKR ? 64 * kG32LdRK : kG32KC * kG32LdKR;
 constexpr int kG32SmemFloats = 2 * 2 * kG32Img;  // two chunk buffers of (A, B) images: 40 KB
 constexpr int kG32MaxK = 320;                 // FWD / DA: the whole K in NCH = 10 chunks
 constexpr int kG32DwSplit = 384;              // DW: batch rows per split-K slab (12 chunks)
-constexpr int kG32Depth = 3;                  // chunks in flight ahead of the one being written
+#ifndef DSSM_G32_DEPTH
+#define DSSM_G32_DEPTH 4
+#endif
+constexpr int kG32Depth = DSSM_G32_DEPTH;     // chunks in flight ahead of the one being computed
 
 enum { G32_FWD = 0, G32_DA = 1, G32_DW = 2 };
 
@@ -56,7 +61,24 @@ struct G32Fuse {
   const float* coefb;  // DA: its coefficients [4][2][ldc]
   DetAcc det;          // deterministic mode: per-row-tile slab rows + fixed-order sums
   int det_rows;
+  int tl_slot;         // diagnostics build (G32_TL): the launch's timeline slot, -1 none
 };
+
+// Diagnostics build only (-DDSSM_G32_TL, gemm32.hip's forward / dA launches): per-workgroup
+// s_memrealtime stamps (100 MHz) of wave 0: [0] start, [1] prologue done, [2 + 2c] chunk c staged
+// (after its barrier), [3 + 2c] chunk c's MFMAs issued, [30] epilogue done; read back by
+// dssm_debug_g32_timeline (tools/g32_timeline.py).
+#if defined(DSSM_G32_TL) && defined(DSSM_G32_TL_HOST)
+#define G32_TL(slot, idx)                                                                        \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (slot) >= 0)                                                         \
+      g_g32_tl[slot][blockIdx.x & 2047][idx] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
+#else
+#define G32_TL(slot, idx) \
+  do {                    \
+  } while (0)
+#endif
 
 namespace {
 
@@ -68,54 +90,76 @@ struct G32Lds {
   double red[2 * 64 * 2];
 };
 
-// NCH: FWD / DA ceil(K / kG32KC) exactly (the launchers dispatch on it); DW kG32DwSplit / kG32KC
-template <int MODE, int FS, int NCH>
+// NCH: FWD / DA ceil(K / kG32KC) exactly (the launchers dispatch on it); DW kG32DwSplit / kG32KC.
+// WN: waves along the tile's 64 columns (2: 4 waves of 32 x 32; 4: 8 waves of 32 x 16, two per
+// SIMD, for launches that give a CU one tile: a lone wave per SIMD waits out every LDS and barrier
+// latency with the matrix core idle, two interleave).  Threads: 128 WN.
+template <int MODE, int FS, int NCH, int WN = 2>
 __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, int tx, int ty, int tz,
                                          G32Lds& L) {
   constexpr bool A_RK = MODE != G32_DW;
   constexpr bool B_RK = MODE == G32_DA;
   constexpr bool BN_A = MODE == G32_FWD;
   constexpr int D = kG32Depth, S = kG32Depth + 1;
+  constexpr int NT = 128 * WN;    // threads
+  constexpr int JN = 4 / WN;      // 16-column MFMA blocks per wave
+  constexpr int WC = 64 / WN;     // columns per wave
+  constexpr int G = 512 / NT;     // staged float4 per thread, operand and chunk
   const int M = p.M, N = p.N;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
   const int bm = ty * 64, bn = tx * 64;
   const int kbeg = MODE == G32_DW ? tz * p.k_per_split : 0;
   const int kend = MODE == G32_DW ? min(p.K, kbeg + p.k_per_split) : p.K;
   const int tower = bm < p.row_split ? 0 : 1;
   const int Mload = p.ones_row ? M - 1 : M;  // DW: rows of A^T stored in memory
+  G32_TL(f.tl_slot, 0);
+#if defined(DSSM_G32_TL) && defined(DSSM_G32_TL_HOST)
+  if (threadIdx.x == 0 && f.tl_slot >= 0) g_g32_tl[f.tl_slot][blockIdx.x & 2047][28] = __builtin_amdgcn_s_memtime();
+#endif
   // the A operand's coefficient inputs first (they return ahead of the bulk loads)
-  constexpr int NPC = (2 * kG32MaxK + 255) / 256;
+  constexpr int NPC = (2 * kG32MaxK + NT - 1) / NT;
   FsCoefStage<NPC> cst;
   const bool from_sums = BN_A && f.in_from_sums;
-  if (from_sums) cst.load(f.in, t, 256);
-  // ---- thread -> staged groups (two float4 of one row / k-row per operand and chunk)
-  //   RK: row t >> 2, k (t & 3) * 8 .. + 8;  KR: k-row t >> 3, columns (t & 7) * 8 .. + 8
-  const int rk_r = t >> 2, rk_k = (t & 3) * 8;
-  const int kr_k = t >> 3, kr_c = (t & 7) * 8;
-  float4 ra[S][2], rb[S][2];
+  if (from_sums) cst.load(f.in, t, NT);
+  // ---- thread -> staged groups: G float4 per operand and chunk, each wave instruction reading
+  // whole 128-B lines (RK: 8 lanes per 32-float row, rows rk_r + (NT / 8) h; KR: 16 lanes per
+  // 64-float k-row, k-rows kr_k + (NT / 16) h)
+  const int rk_r = t >> 3, rk_k = (t & 7) * 4;
+  const int kr_k = t >> 4, kr_c = (t & 15) * 4;
+  constexpr int RKH = NT / 8, KRH = NT / 16;
+  float4 ra[S][G], rb[S][G];
   // Every load is unconditional, from its own address when in range and from the operand's base
   // otherwise (a select, no branch: a masked load in a branch makes the compiler drain vmcnt at
   // the merge); stage() zeroes the out-of-range groups.  Widths are multiples of 4, so a float4
   // is all in range or all out.
+  // Chunk c of the pipeline is K chunk (c + rot) % NCH: tiles that share an operand walk K from
+  // different chunks (a row block's column tiles share A, a column tile's row blocks share B).  Each
+  // tile's k order is fixed by its position: results are deterministic fp32 FMA chains.
+  const int rot = (tx + ty + tz) % NCH;
+  auto kofs = [&](int c) { return kbeg + ((c + rot) % NCH) * kG32KC; };
   auto a_ok = [&](int c, int h) {
-    const int k0 = kbeg + c * kG32KC;
-    if constexpr (A_RK) return bm + rk_r < M && k0 + rk_k + 4 * h < kend;
-    else return k0 + kr_k < kend && bm + kr_c + 4 * h < Mload;
+    const int k0 = kofs(c);
+    if constexpr (A_RK) return bm + rk_r + RKH * h < M && k0 + rk_k < kend;
+    else return k0 + kr_k + KRH * h < kend && bm + kr_c < Mload;
   };
   auto b_ok = [&](int c, int h) {
-    const int k0 = kbeg + c * kG32KC;
-    if constexpr (B_RK) return bn + rk_r < N && k0 + rk_k + 4 * h < kend;
-    else return k0 + kr_k < kend && bn + kr_c + 4 * h < N;
+    const int k0 = kofs(c);
+    if constexpr (B_RK) return bn + rk_r + RKH * h < N && k0 + rk_k < kend;
+    else return k0 + kr_k + KRH * h < kend && bn + kr_c < N;
   };
-  auto load = [&](int c, float4 (&xa)[2], float4 (&xb)[2]) {
-    const int k0 = kbeg + c * kG32KC;
+  auto load = [&](int c, float4 (&xa)[G], float4 (&xb)[G]) {
+#ifdef DSSM_G32_SAMECHUNK  // diagnostics (wrong results): every chunk's loads from chunk 0's lines
+    const int k0 = kofs(0);
+#else
+    const int k0 = kofs(c);
+#endif
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const size_t oa = A_RK ? (size_t)(bm + rk_r) * p.lda + k0 + rk_k + 4 * h   // A [M x lda]
-                             : (size_t)(k0 + kr_k) * p.lda + bm + kr_c + 4 * h;  // A^T from A [K x lda]
-      const size_t ob = B_RK ? (size_t)(bn + rk_r) * p.ldb + k0 + rk_k + 4 * h   // B^T [N x ldb]
-                             : (size_t)(k0 + kr_k) * p.ldb + bn + kr_c + 4 * h;  // B [K x ldb]
+    for (int h = 0; h < G; ++h) {
+      const size_t oa = A_RK ? (size_t)(bm + rk_r + RKH * h) * p.lda + k0 + rk_k   // A [M x lda]
+                             : (size_t)(k0 + kr_k + KRH * h) * p.lda + bm + kr_c;  // A^T from A [K x lda]
+      const size_t ob = B_RK ? (size_t)(bn + rk_r + RKH * h) * p.ldb + k0 + rk_k   // B^T [N x ldb]
+                             : (size_t)(k0 + kr_k + KRH * h) * p.ldb + bn + kr_c;  // B [K x ldb]
       xa[h] = *reinterpret_cast<const float4*>(p.A + (a_ok(c, h) ? oa : 0));
       xb[h] = *reinterpret_cast<const float4*>(p.B + (b_ok(c, h) ? ob : 0));
     }
@@ -124,21 +168,20 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
 #pragma unroll
   for (int c = 0; c < D; ++c)
     if (c < NCH) load(c, ra[c], rb[c]);
+  const int fr = lane & 15, fk = lane >> 4;  // fragment row / column, k group of the lane
   // the epilogue's bias columns (FWD) and pre-BN values / coefficients (DA), loaded with the operands
-  float bcol[2] = {0.f, 0.f};
-  if constexpr (MODE == G32_FWD) {
+  float bcol[JN];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = bn + wn * 32 + j * 16 + (lane & 15);
-      bcol[j] = (p.bias && n < N) ? p.bias[n] : 0.f;
-    }
+  for (int j = 0; j < JN; ++j) {
+    const int n = bn + wn * WC + j * 16 + fr;
+    bcol[j] = (MODE == G32_FWD && p.bias && n < N) ? p.bias[n] : 0.f;
   }
-  float zb[2][2][4], cb[2][4];
+  float zb[2][JN][4], cb[JN][4];
   if constexpr (FS == 2) {
     const size_t plane = (size_t)2 * p.ldc;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = bn + wn * 32 + j * 16 + (lane & 15);
+    for (int j = 0; j < JN; ++j) {
+      const int n = bn + wn * WC + j * 16 + fr;
       const size_t o = (size_t)tower * p.ldc + (n < N ? n : 0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) cb[j][q] = f.coefb[q * plane + o];
@@ -146,7 +189,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+          const int m = bm + wm * 32 + i * 16 + fk * 4 + r;
           zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * p.ldc + (n < N ? n : 0)];
         }
     }
@@ -155,20 +198,20 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   const int Kc = NCH * kG32KC;  // staged k extent (<= kG32MaxK for FWD)
   if constexpr (BN_A) {
     if (from_sums) {
-      cst.finish(f.in, t, 256, [&](int tw, int k, float, float, float inv, float sh) {
+      cst.finish(f.in, t, NT, [&](int tw, int k, float, float, float inv, float sh) {
         if (k < Kc) {
           L.coef[(tw * 2 + 0) * kG32MaxK + k] = inv;
           L.coef[(tw * 2 + 1) * kG32MaxK + k] = sh;
         }
       });
-      for (int i = t; i < 2 * (Kc - p.lda); i += 256) {
+      for (int i = t; i < 2 * (Kc - p.lda); i += NT) {
         const int tw = i / (Kc - p.lda), k = p.lda + i % (Kc - p.lda);
         L.coef[(tw * 2 + 0) * kG32MaxK + k] = 0.f;
         L.coef[(tw * 2 + 1) * kG32MaxK + k] = 0.f;
       }
     } else {
       const size_t plane = (size_t)2 * p.lda;
-      for (int i = t; i < 2 * Kc; i += 256) {
+      for (int i = t; i < 2 * Kc; i += NT) {
         const int tw = i / Kc, k = i - tw * Kc;
         const bool ok = k < p.lda;
         L.coef[(tw * 2 + 0) * kG32MaxK + k] = ok ? p.coef[2 * plane + (size_t)tw * p.lda + k] : 0.f;
@@ -179,129 +222,150 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   }
   const bool write_a = BN_A && p.a_out != nullptr && tx == 0;
   // chunk c's registers -> LDS image buf (BN + ReLU on A for FWD; the ones column for DW)
-  auto stage = [&](int c, float4 (&xa)[2], float4 (&xb)[2], int buf) {
+  auto stage = [&](int c, float4 (&xa)[G], float4 (&xb)[G], int buf) {
     float* sa = L.img + buf * 2 * kG32Img;
     float* sb = sa + kG32Img;
-    const int k0 = kbeg + c * kG32KC;
+    const int k0 = kofs(c);
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < G; ++h) {
       if (!a_ok(c, h)) xa[h] = z4;
       if (!b_ok(c, h)) xb[h] = z4;
     }
     if constexpr (BN_A) {
-      const int r = bm + rk_r;
       const float* ci = &L.coef[(tower * 2) * kG32MaxK + k0 + rk_k];
-      const float* ch = ci + kG32MaxK;
+      const float4 inv = *reinterpret_cast<const float4*>(ci);
+      const float4 sh = *reinterpret_cast<const float4*>(ci + kG32MaxK);
+      const int k = k0 + rk_k;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < G; ++h) {
         float4& v = xa[h];
-        v.x = fmaxf(bn_affine(v.x, ci[4 * h + 0], ch[4 * h + 0]), 0.f);
-        v.y = fmaxf(bn_affine(v.y, ci[4 * h + 1], ch[4 * h + 1]), 0.f);
-        v.z = fmaxf(bn_affine(v.z, ci[4 * h + 2], ch[4 * h + 2]), 0.f);
-        v.w = fmaxf(bn_affine(v.w, ci[4 * h + 3], ch[4 * h + 3]), 0.f);
-        const int k = k0 + rk_k + 4 * h;
+        v.x = fmaxf(bn_affine(v.x, inv.x, sh.x), 0.f);
+        v.y = fmaxf(bn_affine(v.y, inv.y, sh.y), 0.f);
+        v.z = fmaxf(bn_affine(v.z, inv.z, sh.z), 0.f);
+        v.w = fmaxf(bn_affine(v.w, inv.w, sh.w), 0.f);
+        const int r = bm + rk_r + RKH * h;
         if (write_a && r < M && k < p.lda) *reinterpret_cast<float4*>(p.a_out + (size_t)r * p.lda + k) = v;
       }
     }
     if constexpr (MODE == G32_DW) {
-      if (p.ones_row) {
-        const int k = k0 + kr_k;
+      if (p.ones_row && bm + kr_c == Mload) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          if (bm + kr_c + 4 * h == Mload && k < kend) xa[h].x = 1.0f;
+        for (int h = 0; h < G; ++h)
+          if (k0 + kr_k + KRH * h < kend) xa[h].x = 1.0f;
       }
     }
-    if constexpr (A_RK) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) *reinterpret_cast<float4*>(&sa[rk_r * kG32LdRK + rk_k + 4 * h]) = xa[h];
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) *reinterpret_cast<float4*>(&sa[kr_k * kG32LdKR + kr_c + 4 * h]) = xa[h];
-    }
-    if constexpr (B_RK) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) *reinterpret_cast<float4*>(&sb[rk_r * kG32LdRK + rk_k + 4 * h]) = xb[h];
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) *reinterpret_cast<float4*>(&sb[kr_k * kG32LdKR + kr_c + 4 * h]) = xb[h];
+    for (int h = 0; h < G; ++h) {
+      if constexpr (A_RK) *reinterpret_cast<float4*>(&sa[(rk_r + RKH * h) * kG32LdRK + rk_k]) = xa[h];
+      else *reinterpret_cast<float4*>(&sa[(kr_k + KRH * h) * kG32LdKR + kr_c]) = xa[h];
+      if constexpr (B_RK) *reinterpret_cast<float4*>(&sb[(rk_r + RKH * h) * kG32LdRK + rk_k]) = xb[h];
+      else *reinterpret_cast<float4*>(&sb[(kr_k + KRH * h) * kG32LdKR + kr_c]) = xb[h];
     }
   };
-  f32x4 acc[2][2];
+  f32x4 acc[2][JN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fk = lane >> 4;  // fragment row / column and k within the 4-deep step
-  // ---- the chunk pipeline: load c + D, stage c, barrier, MFMA c (one barrier per chunk: the image
-  // staged at c was last read at c - 2, before every wave passed barrier c - 1).  NCH is the
-  // chunk count (FWD / DA: exactly ceil(K / 32); DW: the split's, chunks past its rows staged as
-  // zeros), so the unrolled pipeline is straight-line code and the compiler's vmcnt waits are exact
-  // (a runtime chunk bound around the loads made it drain every load at each branch merge).
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  G32_TL(f.tl_slot, 1);
+  // ---- the chunk pipeline.  Iteration c: load chunk c + D, stage chunk c + 1 into the other LDS
+  // image, the MFMAs of chunk c, one barrier.  Staging (the wait for c + 1's loads, BN + ReLU, the
+  // LDS writes) and the MFMAs share a basic block, so the compiler interleaves them.  The image
+  // staged at c + 1 was last read by the MFMAs of c - 1, which every wave finished before the barrier
+  // ending iteration c - 1; the register set chunk c + D loads into held chunk c - 1 (ring of D + 1),
+  // staged at iteration c - 2.  NCH is the chunk count (FWD / DA: exactly ceil(K / 32); DW: the
+  // split's, chunks past its rows staged as zeros), so the unrolled pipeline is straight-line code
+  // and the compiler's vmcnt waits are exact (a runtime chunk bound around the loads made it drain
+  // every load at each branch merge).
+  stage(0, ra[0], rb[0], 0);
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    {
-      if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
-      const int buf = c & 1;
-      stage(c, ra[c % S], rb[c % S], buf);
-      __syncthreads();
-      const float* sa = L.img + buf * 2 * kG32Img;
-      const float* sb = sa + kG32Img;
-      const int kv = kend - (kbeg + c * kG32KC);  // valid k of this chunk (the rest are zeros)
+#ifndef DSSM_G32_NOSTAGE  // diagnostics (wrong results): the loop without its loads and staging
+    if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
+    if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
+#endif
+    G32_TL(f.tl_slot, 2 + 2 * c);
+    const float* sa = L.img + (c & 1) * 2 * kG32Img;
+    const float* sb = sa + kG32Img;
+    // the whole chunk (k past the operand's end staged as zeros: exact no-ops on the sums); 8-deep
+    // steps, MFMA q of a step taking k = kk + 2 fk + q; step kk + 8's fragments read ahead of step
+    // kk's MFMAs, so the LDS latency overlaps them
+    auto frag = [&](int kk, float2 (&av)[2], float2 (&bv)[JN]) {
+      const int k2 = kk + 2 * fk;
+#ifdef DSSM_G32_NOFRAG  // diagnostics (wrong results): MFMA operands from registers only
+      for (int i = 0; i < 2; ++i) av[i] = make_float2((float)k2, (float)i);
+      for (int j = 0; j < JN; ++j) bv[j] = make_float2((float)j, (float)k2);
+      return;
+#endif
 #pragma unroll
-      for (int kk = 0; kk < kG32KC; kk += 4) {
-        if (kk < kv) {
-          float av[2], bv[2];
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 32 + i * 16 + fr;
+        if constexpr (A_RK) av[i] = *reinterpret_cast<const float2*>(&sa[r * kG32LdRK + k2]);
+        else av[i] = make_float2(sa[k2 * kG32LdKR + r], sa[(k2 + 1) * kG32LdKR + r]);
+      }
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
-            av[i] = A_RK ? sa[(wm * 32 + i * 16 + fr) * kG32LdRK + kk + fk]
-                         : sa[(kk + fk) * kG32LdKR + wm * 32 + i * 16 + fr];
+      for (int j = 0; j < JN; ++j) {
+        const int r = wn * WC + j * 16 + fr;
+        if constexpr (B_RK) bv[j] = *reinterpret_cast<const float2*>(&sb[r * kG32LdRK + k2]);
+        else bv[j] = make_float2(sb[k2 * kG32LdKR + r], sb[(k2 + 1) * kG32LdKR + r]);
+      }
+    };
+    float2 av[2], bv[JN];
+    frag(0, av, bv);
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            bv[j] = B_RK ? sb[(wn * 32 + j * 16 + fr) * kG32LdRK + kk + fk]
-                         : sb[(kk + fk) * kG32LdKR + wn * 32 + j * 16 + fr];
+    for (int kk = 0; kk < kG32KC; kk += 8) {
+      float2 an[2], bnx[JN];
+      if (kk + 8 < kG32KC) frag(kk + 8, an, bnx);
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+      if (kk + 8 < kG32KC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = an[i];
+#pragma unroll
+        for (int j = 0; j < JN; ++j) bv[j] = bnx[j];
       }
     }
+#ifndef DSSM_G32_NOBAR  // diagnostics (wrong results): no barrier per chunk
+    __syncthreads();
+#endif
+    G32_TL(f.tl_slot, 3 + 2 * c);
   }
-  // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
-  if constexpr (MODE == G32_DW) {
-    float* out = p.C + (size_t)tz * M * p.ldc;
+  // ---- epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.  The tile goes to LDS (the
+  // chunk images are free after the loop's last barrier) and leaves as float4 row segments: whole
+  // 256-B rows per 16 lanes instead of the accumulator layout's scattered 4-B stores.
+  constexpr int kCld = 68;
+  float* sC = L.img;  // [64][kCld]
+  double cs[JN], cq[JN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = bn + wn * 32 + j * 16 + fr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = bm + wm * 32 + i * 16 + fk * 4 + r;
-          if (m < M && n < N) out[(size_t)m * p.ldc + n] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};
+  for (int j = 0; j < JN; ++j) cs[j] = cq[j] = 0.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = bn + wn * 32 + j * 16 + fr;
+    for (int j = 0; j < JN; ++j) {
+      const int cl = wn * WC + j * 16 + fr, n = bn + cl;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * 32 + i * 16 + fk * 4 + r;
-        if (m < M && n < p.ldc) {
-          const float v = acc[i][j][r];
-          const float x = (n < N) ? v + bcol[j] : 0.f;
-          p.C[(size_t)m * p.ldc + n] = x;
-          if constexpr (FS == 1) {
+        const int rl = wm * 32 + i * 16 + fk * 4 + r, m = bm + rl;
+        const float v = acc[i][j][r];
+        const float x = (n < N) ? v + bcol[j] : 0.f;  // DW / DA: no bias (bcol zero)
+        sC[rl * kCld + cl] = x;
+        if constexpr (FS == 1) {
+          if (m < M) {
             cs[j] += x;
             cq[j] += (double)x * x;
-          } else if constexpr (FS == 2) {
+          }
+        } else if constexpr (FS == 2) {
+          if (m < M) {
             const float z = zb[i][j][r];
             // the forward's ReLU mask (bn.hip bwd_terms): dy = dA where BN(z) > 0
             const float dy = (n < N && bn_affine(z, cb[j][2], cb[j][3]) > 0.f) ? x : 0.f;
@@ -313,10 +377,23 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
       }
     }
   }
+  __syncthreads();
+  {
+    float* out = MODE == G32_DW ? p.C + (size_t)tz * M * p.ldc : p.C;
+    const int ncols = MODE == G32_DW ? min(64, N - bn) : min(64, p.ldc - bn);  // multiples of 4
+#pragma unroll
+    for (int k = 0; k < 1024 / NT; ++k) {
+      const int idx = t + NT * k, r = idx >> 4, q = (idx & 15) * 4;
+      if (bm + r < M && q < ncols)
+        *reinterpret_cast<float4*>(out + (size_t)(bm + r) * p.ldc + bn + q) =
+            *reinterpret_cast<const float4*>(&sC[r * kCld + q]);
+    }
+  }
+  if constexpr (MODE == G32_DW) return;
   if constexpr (FS != 0) {
     // the wave's 4 row groups by shuffles, the two wm halves through LDS, one atomic per statistic
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < JN; ++j) {
       cs[j] += __shfl_xor(cs[j], 16);
       cs[j] += __shfl_xor(cs[j], 32);
       cq[j] += __shfl_xor(cq[j], 16);
@@ -324,16 +401,16 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     }
     if (wm == 1 && lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        L.red[(wn * 32 + j * 16 + lane) * 2] = cs[j];
-        L.red[(wn * 32 + j * 16 + lane) * 2 + 1] = cq[j];
+      for (int j = 0; j < JN; ++j) {
+        L.red[(wn * WC + j * 16 + lane) * 2] = cs[j];
+        L.red[(wn * WC + j * 16 + lane) * 2 + 1] = cq[j];
       }
     }
     __syncthreads();
     if (wm == 0 && lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = wn * 32 + j * 16 + lane, n = bn + c;
+      for (int j = 0; j < JN; ++j) {
+        const int c = wn * WC + j * 16 + lane, n = bn + c;
         if (n < N) {
           const double s1 = cs[j] + L.red[c * 2], s2 = cq[j] + L.red[c * 2 + 1];
           if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
@@ -354,6 +431,11 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
       det_publish(f.det, tx, ty, f.det_rows, p.ldc, bn, min(bn + 64, N), f.out_sum, &s_det);
     }
   }
+#if defined(DSSM_G32_TL) && defined(DSSM_G32_TL_HOST)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  G32_TL(f.tl_slot, 30);
+  if (threadIdx.x == 0 && f.tl_slot >= 0) g_g32_tl[f.tl_slot][blockIdx.x & 2047][29] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 }  // namespace

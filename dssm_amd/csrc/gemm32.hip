@@ -4,28 +4,39 @@
 //               per-tower column sums (fused statistics); + 1 workgroup materialising BN_{l-1}
 //   k_g32_da  : dA_{l-1} = dZ_l . W_l^T with BN_{l-1}'s backward sums in the epilogue
 //   k_g32_dw  : dW_l split-K slabs (when they do not ride in the BN-backward apply launch, bn.hip)
+#define DSSM_G32_TL_HOST 1
+#ifdef DSSM_G32_TL
+namespace dssm {
+__device__ unsigned long long g_g32_tl[4][2048][32];
+}
+#endif
 #include "g32.h"
 #include "launch.h"
 
 namespace dssm {
 namespace {
 
+#ifndef DSSM_G32_WN
+#define DSSM_G32_WN 4  // forward / dA tiles: 8 waves of 32 x 16 (2: 4 waves of 32 x 32)
+#endif
+constexpr int kWN = DSSM_G32_WN;
+
 template <int NCH>
-__global__ __launch_bounds__(256) void k_g32_fwd(G32Params p, G32Fuse f, int nx, int ntiles) {
+__global__ __launch_bounds__(128 * kWN) void k_g32_fwd(G32Params p, G32Fuse f, int nx, int ntiles) {
   __shared__ G32Lds L;
   if ((int)blockIdx.x >= ntiles) {  // the extra workgroup: BN_{l-1}'s coef, batch moments, EMA
     if (f.in_from_sums) fs_materialize_fwd(f.in);
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);  // a row block's column tiles on one XCD
-  g32_body<G32_FWD, 1, NCH>(p, f, tile % nx, tile / nx, 0, L);
+  g32_body<G32_FWD, 1, NCH, kWN>(p, f, tile % nx, tile / nx, 0, L);
 }
 
 template <int NCH>
-__global__ __launch_bounds__(256) void k_g32_da(G32Params p, G32Fuse f, int nx, int ntiles) {
+__global__ __launch_bounds__(128 * kWN) void k_g32_da(G32Params p, G32Fuse f, int nx, int ntiles) {
   __shared__ G32Lds L;
   const int tile = xcd_tile(blockIdx.x, ntiles);
-  g32_body<G32_DA, 2, NCH>(p, f, tile % nx, tile / nx, 0, L);
+  g32_body<G32_DA, 2, NCH, kWN>(p, f, tile % nx, tile / nx, 0, L);
 }
 
 // the kernel instance for K: NCH = ceil(K / 32) chunks (K <= kG32MaxK)
@@ -33,7 +44,7 @@ template <template <int> class KS>
 void g32_by_chunks(int K, dim3 grid, hipStream_t s, const G32Params& p, const G32Fuse& f, int nx, int nt) {
   switch ((K + kG32KC - 1) / kG32KC) {
 #define DSSM_G32_NCH(n) \
-    case n: hipLaunchKernelGGL(KS<n>::fn, grid, dim3(256), 0, s, p, f, nx, nt); break;
+    case n: hipLaunchKernelGGL(KS<n>::fn, grid, dim3(128 * kWN), 0, s, p, f, nx, nt); break;
     DSSM_G32_NCH(1) DSSM_G32_NCH(2) DSSM_G32_NCH(3) DSSM_G32_NCH(4) DSSM_G32_NCH(5)
     DSSM_G32_NCH(6) DSSM_G32_NCH(7) DSSM_G32_NCH(8) DSSM_G32_NCH(9) DSSM_G32_NCH(10)
 #undef DSSM_G32_NCH
@@ -46,7 +57,9 @@ template <int n> struct DaK { static constexpr auto fn = k_g32_da<n>; };
 __global__ __launch_bounds__(256) void k_g32_dw(G32Params p, int nx, int ny, int nblocks) {
   __shared__ G32Lds L;
   const int r = xcd_tile(blockIdx.x, nblocks);  // one batch-row chunk's tiles on one XCD
-  g32_body<G32_DW, 0, kG32DwSplit / kG32KC>(p, G32Fuse{}, r % nx, (r / nx) % ny, r / (nx * ny), L);
+  G32Fuse f{};
+  f.tl_slot = -1;
+  g32_body<G32_DW, 0, kG32DwSplit / kG32KC>(p, f, r % nx, (r / nx) % ny, r / (nx * ny), L);
 }
 
 bool g32_det_fits(const G32Fuse& f, int ld) {
@@ -73,6 +86,7 @@ hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const fl
   f.out_sum = out_sum;
   if (det) f.det = *det;
   f.det_rows = cdiv(M, 64);
+  f.tl_slot = N > 128 ? 0 : 1;
   if (!g32_det_fits(f, ldc)) return hipErrorInvalidValue;
   const int nx = cdiv(ldc, 64), ntiles = nx * cdiv(M, 64);
   g32_by_chunks<FwdK>(K, dim3(ntiles + (in_from_sums ? 1 : 0)), s, p, f, nx, ntiles);
@@ -101,6 +115,7 @@ hipError_t launch_g32_pair(int M, int kin, int n, const float* dZ, int lddz, con
   f.coefb = coef_prev;
   if (det) f.det = *det;
   f.det_rows = cdiv(M, 64);
+  f.tl_slot = n > 128 ? 3 : 2;
   if (!g32_det_fits(f, ldda)) return hipErrorInvalidValue;
   const int nx = cdiv(ldda, 64), ntiles = nx * cdiv(M, 64);
   g32_by_chunks<DaK>(n, dim3(ntiles), s, a, f, nx, ntiles);
@@ -120,3 +135,11 @@ hipError_t launch_g32_pair(int M, int kin, int n, const float* dZ, int lddz, con
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_G32_TL
+extern "C" int dssm_debug_g32_timeline(int slot, unsigned long long* out, int n) {
+  if (slot < 0 || slot >= 4 || n > 2048) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_g32_tl), sizeof(unsigned long long) * 32 * n,
+                             sizeof(unsigned long long) * 32 * 2048 * slot) == hipSuccess ? 0 : -2;
+}
+#endif

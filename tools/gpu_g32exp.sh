@@ -1,0 +1,11 @@
+#!/bin/bash
+# fp32 tile experiments (diagnostics builds with timelines, wrong results): e1 no loads / staging in the
+# chunk loop, e2 also no barrier, e3 also no LDS fragment reads (MFMA alone)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/g32exp
+for v in g32tl e1 e2 e3; do
+  echo "== $v"
+  DSSM_LIB_PATH=$GRAFT_REPO_ROOT/dssm_amd/libdssm_$v.so timeout -k 10 120 python tools/g32_timeline.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/g32exp/$v.txt || exit 1
+done
+cd /tmp && timeout -k 10 120 rocprofv3 --list-avail > $GRAFT_REPO_ROOT/gpurun_out/pmc_list.txt 2>&1 || true
