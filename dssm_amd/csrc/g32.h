@@ -35,6 +35,9 @@ constexpr int kG32DwSplit = 384;              // DW: batch rows per split-K slab
 #define DSSM_G32_DEPTH 4
 #endif
 constexpr int kG32Depth = DSSM_G32_DEPTH;     // chunks in flight ahead of the one being computed
+#ifndef DSSM_G32_FRAGALL
+#define DSSM_G32_FRAGALL 0  // 1: a chunk's fragments all read before its staging / MFMAs (A/B option)
+#endif
 
 enum { G32_FWD = 0, G32_DA = 1, G32_DW = 2 };
 
@@ -282,11 +285,6 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-#ifndef DSSM_G32_NOSTAGE  // diagnostics (wrong results): the loop without its loads and staging
-    if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
-    if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
-#endif
-    G32_TL(f.tl_slot, 2 + 2 * c);
     const float* sa = L.img + (c & 1) * 2 * kG32Img;
     const float* sb = sa + kG32Img;
     // the whole chunk (k past the operand's end staged as zeros: exact no-ops on the sums); 8-deep
@@ -312,6 +310,33 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         else bv[j] = make_float2(sb[k2 * kG32LdKR + r], sb[(k2 + 1) * kG32LdKR + r]);
       }
     };
+#if DSSM_G32_FRAGALL
+    // every fragment of the chunk read first (4 steps x (2 + JN) float2), behind them the next
+    // chunk's loads and staging, then the MFMAs back to back
+    float2 av[kG32KC / 8][2], bv[kG32KC / 8][JN];
+#pragma unroll
+    for (int st = 0; st < kG32KC / 8; ++st) frag(8 * st, av[st], bv[st]);
+#endif
+#ifndef DSSM_G32_NOSTAGE  // diagnostics (wrong results): the loop without its loads and staging
+    if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
+    if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
+#endif
+    G32_TL(f.tl_slot, 2 + 2 * c);
+#if DSSM_G32_FRAGALL
+#pragma unroll
+    for (int st = 0; st < kG32KC / 8; ++st) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st][i].x, bv[st][j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st][i].y, bv[st][j].y, acc[i][j], 0, 0, 0);
+    }
+#else
     float2 av[2], bv[JN];
     frag(0, av, bv);
 #pragma unroll
@@ -335,6 +360,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         for (int j = 0; j < JN; ++j) bv[j] = bnx[j];
       }
     }
+#endif
 #ifndef DSSM_G32_NOBAR  // diagnostics (wrong results): no barrier per chunk
     __syncthreads();
 #endif
