@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--model", default="bow", choices=["bow", "rnn", "multiview"],
                     help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4); "
                          "multiview: multi_view_dssm_v3 (config 5)")
+    ap.add_argument("--mv-csc-stream", type=int, default=0,
+                    help="multiview, fused optimizer: the CSC transposes on a third stream forked from the step's "
+                         "stream (MultiViewDSSM(csc_stream=True)) instead of the item tower's stream")
     ap.add_argument("--feed", default="device", choices=["device", "host"],
                     help="device: batches staged in HBM before the timed region (the headline); host: "
                          "batches streamed from host CSR matrices by the native pinned async feeder "
@@ -474,7 +477,8 @@ def bench_multiview(args):
     torch.cuda.set_device(dev)
     if world > 1:  # config 5 on N GPUs: BS users per rank, gradient all-reduce (weak scaling)
         dist.init_process_group(args.backend, device_id=dev if args.backend == "nccl" else None)
-    m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev, dtype=args.dtype)
+    m = MultiViewDSSM(Dv, [Dv, Dv, Dv], L1, L2, B, NEG, lr=0.05, device=dev, dtype=args.dtype,
+                      csc_stream=bool(args.mv_csc_stream))
     m.init_params(0)
     dp = MultiViewDataParallel(m, comm=args.comm) if world > 1 else None
     cols = ZipfColumns(Dv)
@@ -612,7 +616,8 @@ def bench_multiview(args):
                                   "rotated negatives, BS=4096 per GPU, NEG=4, fwd+bwd+Adam", "global_batch": B * world,
                       "neg": NEG, "parallelism": f"dp{world}",
                       "launch": ("hipgraph: one graph of K steps" if region is not None else "hipgraph") if args.graph else "eager",
-                      "dp_exchange": dp.comm if dp is not None else None},
+                      "dp_exchange": dp.comm if dp is not None else None,
+                      "csc_stream": bool(m.csc_stream and m.fused_w1_adam)},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                         "kernel": adam_kernel,

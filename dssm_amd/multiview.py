@@ -51,7 +51,7 @@ class MultiViewDSSM:
     def __init__(self, user_d: int, view_d: Sequence[int], l1: int, l2: int, bs: int, neg: int = 4,
                  lr: float = 0.05, gamma: float = 20.0, max_nnz_per_row: int = 96, device=None,
                  rotations: Optional[Sequence[int]] = None, seed: int = 0, dtype: str = "fp32",
-                 fused_w1_adam: bool = True):
+                 fused_w1_adam: bool = True, csc_stream: bool = False):
         self.lib = _lib.load()
         if dtype not in ("fp32", "bf16"):
             raise ValueError("dtype: 'fp32' or 'bf16'")
@@ -107,6 +107,14 @@ class MultiViewDSSM:
         slab = max(self.lib.dssm_dense_bwd_slab_floats(BS, self.l1, self.l2, self._dt), 1)
         self.slab = {k: torch.zeros(int(slab), dtype=f32, device=dev) for k in ("u", "i")}
         self.aux = torch.cuda.Stream(device=dev)
+        # fused mode, csc_stream: the optimizer's CSC transposes on a third stream forked from the
+        # caller's stream at the top of forward(), so the item tower's forward and backward on aux do
+        # not queue behind them.  It must fork from the caller's (in a captured step: the capture's
+        # origin) stream: a stream forked from aux, itself forked by an event wait, makes ROCm 7.0's
+        # hipStreamEndCapture segfault with every stream joined (profiles/r05_mv_capture_probe.txt)
+        self.csc_stream = bool(csc_stream)
+        self.aux2 = torch.cuda.Stream(device=dev) if self.csc_stream else None
+        self._csc_ev_i = None
         # one CSC-transpose workspace per tower (zero on first use, kept zero by the calls)
         self.spmm_ws = {t: torch.zeros(int(self.lib.dssm_spmm_bwd_ws_bytes(BS, d, self.max_nnz)),
                                        dtype=torch.uint8, device=dev) for t, d in zip(TOWERS, self.dims)}
@@ -249,12 +257,22 @@ class MultiViewDSSM:
         main = self._fork(stream)
         s, sa = stream_ptr(main), stream_ptr(self.aux)
         BS = self.bs
+        self._csc_ev = self._csc_ev_i = None
+        if self._fused and self.csc_stream:
+            self.aux2.wait_stream(main)  # forked from the caller's stream, never from aux
+            for key in ("u", "i"):
+                for t in self.batch[key]:
+                    t.record_stream(self.aux2)
+            s2 = stream_ptr(self.aux2)
+            self._csc("u", "user", s2)
+            self._csc_ev = self.aux2.record_event()
+            self._csc("i", f"view{self.view}", s2)
+            self._csc_ev_i = self.aux2.record_event()
         # the towers are independent until the cosine: the item tower runs beside the user tower
         self._tower_fwd("u", "user", self.ysrc[:BS], s)
         self._tower_fwd("i", f"view{self.view}", self.ysrc[BS:], sa)
         main.wait_event(self.aux.record_event())
-        self._csc_ev = None
-        if self._fused:
+        if self._fused and not self.csc_stream:
             # the optimizer's CSC transposes (they depend on the batch only) on the item tower's
             # stream while the caller's stream runs the loss: off the step's critical path.  They
             # read the batch after the join above, so the batch tensors are marked in use on aux:
@@ -360,10 +378,12 @@ class MultiViewDSSM:
             built = getattr(self, "_csc_ev", None) is not None  # transposed by forward() on self.aux
             if built:
                 main.wait_event(self._csc_ev)
+            if self._csc_ev_i is not None:  # csc_stream: the item transpose on aux2
+                self.aux.wait_event(self._csc_ev_i)
             self._tower_adam("u", towers[0], stream_ptr(main), grad_scale, 0, not built)
             self._tower_adam("i", towers[1], stream_ptr(self.aux), grad_scale, 1, not built)
             main.wait_stream(self.aux)
-            self._csc_ev = None
+            self._csc_ev = self._csc_ev_i = None
         elif self.bf16:
             # both trained towers in one launch, the updated weights' bf16 shadows written by the same pass
             rng = (C.c_int64 * 4)(*[x for t in towers for x in self.layout[t]])

@@ -16,12 +16,12 @@ from oracle import multiview_oracle as M
 pytestmark = pytest.mark.gpu
 
 
-def _setup(view, bs=64, fused=False, dtype="fp32"):
+def _setup(view, bs=64, fused=False, dtype="fp32", csc_stream=False):
     cfg = M.MvConfig(user_d=3000, view_d=[2000, 2500, 1500], l1=64, l2=32, bs=bs, neg=4, lr=0.01)
     p = M.init_params(cfg, 1)
     rot = M.rotations(cfg, 3)
     m = MultiViewDSSM(cfg.user_d, cfg.view_d, cfg.l1, cfg.l2, cfg.bs, cfg.neg, lr=cfg.lr, rotations=rot,
-                      fused_w1_adam=fused, dtype=dtype)
+                      fused_w1_adam=fused, dtype=dtype, csc_stream=csc_stream)
     m.load_params(p)
     rng = np.random.Generator(np.random.PCG64(view))
     u = synth_rows(rng, ZipfColumns(cfg.user_d), cfg.bs, 16.0)
@@ -144,15 +144,17 @@ def test_multiview_fused_forward_only_set_batch_loop():
     assert d.max() <= 2 * cfg.lr and (d <= 1e-5).mean() >= 0.999, (d.max(), (d > 1e-5).sum())
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_multiview_fused_graph_matches_eager(dtype):
+@pytest.mark.parametrize("dtype,csc_stream", [("fp32", False), ("bf16", False), ("bf16", True)])
+def test_multiview_fused_graph_matches_eager(dtype, csc_stream):
     """The fused step's stream structure (item tower and transposes on self.aux, the optimizer launches
     chained on the backward streams, the beta powers advanced by the later launch) captured as ONE
     graph of 4 steps over 2 alternating feeds (views 1 and 3), as bench.py times it, against the same
     4 steps run eagerly: losses rel <= 1e-5, beta powers exact, parameters within 1e-5 on 99.99% of the
-    elements and 2 lr everywhere (the heavy W1 columns' fp32 atomics may add in another order)."""
-    cfg, p, rot, a, u, it = _setup(1, bs=512, fused=True, dtype=dtype)
-    _, _, _, b, _, _ = _setup(1, bs=512, fused=True, dtype=dtype)
+    elements and 2 lr everywhere (the heavy W1 columns' fp32 atomics may add in another order).
+    csc_stream: the transposes on a third stream forked from the capture's origin stream (a fork
+    from self.aux segfaulted capture_end, profiles/r05_mv_capture_probe.txt)."""
+    cfg, p, rot, a, u, it = _setup(1, bs=512, fused=True, dtype=dtype, csc_stream=csc_stream)
+    _, _, _, b, _, _ = _setup(1, bs=512, fused=True, dtype=dtype, csc_stream=csc_stream)
     rng = np.random.Generator(np.random.PCG64(77))
     feeds = []
     for view in (1, 3):

@@ -258,6 +258,53 @@ def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, comm_world
     np.testing.assert_array_equal(m.fetch("cos_sim_raw"), a)
 
 
+@pytest.mark.parametrize("comm,chunks,bs,replays,bar5,bar4", [(0, 3, 96, 1, 0.999, 1.0), (0, 3, 96, 2, None, 0.98),
+                                                               (1, 3, 96, 2, None, 0.98), (0, 1, 128, 2, None, 0.98)])
+def test_dp_step_graph_default_schedule_matches_eager(comm, chunks, bs, replays, bar5, bar4, comm_world1):
+    """The DEFAULT schedule (no DETERMINISTIC: fp32 column-sum atomics, the schedule the 8-GPU run
+    times) of the captured data-parallel step graph against the same steps run eagerly.  One launch
+    of the 3-step graph is the round-3 test's shape and keeps its bar (>= 99.9% of the parameters
+    within 1e-5; measured 100%, max 7e-7, profiles/r05_dp_graph_noise.txt).  After 6 steps the
+    atomics' order has been amplified through Adam: graph-vs-eager equals eager-vs-eager there
+    (90% within 1e-5, 99.1-99.6% within 1e-4, same max), so the bar is the eager runs' own spread:
+    >= 98% within 1e-4, every element within 2 lr x steps, losses rel 1e-3."""
+    steps = 3
+    runs = []
+    for mode in ("graph", "eager"):
+        _, _, m = make(D, WIDTHS, bs, NEG, "bf16", fused=False)
+        gw, st, pw, geo = _wires(m, 1, 0, chunks)
+        runs.append((m, gw, st, pw))
+    batches = []
+    for i in range(steps):
+        b = synth_batch(D, bs, NEG, seed=300 + i, mean_nnz=32)
+        batches.append(tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        m, gw, st, pw = runs[0]
+        gid = m.graph_build_dp_steps(batches, 1.0, comm=comm)
+        for _ in range(replays):
+            m.graph_launch(gid)
+        e, egw, est, epw = runs[1]
+        for _ in range(replays):
+            for ip, ix, vv in batches:
+                e.set_batch(indptr=ip, indices=ix, values=vv)
+                e.forward(True)
+                e.backward()
+                est.copy_(egw)  # the all-to-all at world 1
+                e.apply_adam(1.0)
+                e.wire_shadows()
+    torch.cuda.synchronize()
+    assert m.beta_powers() == e.beta_powers()
+    d = (m.params - e.params).abs()
+    frac5, frac4 = float((d <= 1e-5).float().mean()), float((d <= 1e-4).float().mean())
+    if bar5 is not None:
+        assert frac5 >= bar5, (frac5, float(d.max()))
+    assert frac4 >= bar4, (frac4, float(d.max()))
+    assert float(d.max()) <= 2 * m.lr * steps * replays, float(d.max())
+    lg, le = m.loss_accuracy()[0], e.loss_accuracy()[0]
+    assert abs(lg - le) <= 1e-3 * abs(le), (lg, le)
+
+
 def test_single_gpu_graphs_are_chains():
     """The single-GPU multi-step graph bench.py times is one chain of kernel nodes (no memcpy /
     memset node: every device clear is a kernel)."""
