@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--model", default="bow", choices=["bow", "rnn", "multiview"],
                     help="bow: the headline BoW DSSM (BASELINE config 2); rnn: the dssm_rnn tower (config 4); "
                          "multiview: multi_view_dssm_v3 (config 5)")
-    ap.add_argument("--mv-csc-stream", type=int, default=0,
+    ap.add_argument("--mv-csc-stream", type=int, default=1,
                     help="multiview, fused optimizer: the CSC transposes on a third stream forked from the step's "
                          "stream (MultiViewDSSM(csc_stream=True)) instead of the item tower's stream")
     ap.add_argument("--feed", default="device", choices=["device", "host"],

@@ -51,7 +51,7 @@ class MultiViewDSSM:
     def __init__(self, user_d: int, view_d: Sequence[int], l1: int, l2: int, bs: int, neg: int = 4,
                  lr: float = 0.05, gamma: float = 20.0, max_nnz_per_row: int = 96, device=None,
                  rotations: Optional[Sequence[int]] = None, seed: int = 0, dtype: str = "fp32",
-                 fused_w1_adam: bool = True, csc_stream: bool = False):
+                 fused_w1_adam: bool = True, csc_stream: bool = True):
         self.lib = _lib.load()
         if dtype not in ("fp32", "bf16"):
             raise ValueError("dtype: 'fp32' or 'bf16'")
@@ -111,7 +111,8 @@ class MultiViewDSSM:
         # caller's stream at the top of forward(), so the item tower's forward and backward on aux do
         # not queue behind them.  It must fork from the caller's (in a captured step: the capture's
         # origin) stream: a stream forked from aux, itself forked by an event wait, makes ROCm 7.0's
-        # hipStreamEndCapture segfault with every stream joined (profiles/r05_mv_capture_probe.txt)
+        # hipStreamEndCapture segfault with every stream joined (profiles/r05_mv_capture_probe.txt).
+        # Measured at C5 bf16: 0.2400 against 0.2467 ms/step on two streams (profiles/r05_mv_streams.txt)
         self.csc_stream = bool(csc_stream)
         self.aux2 = torch.cuda.Stream(device=dev) if self.csc_stream else None
         self._csc_ev_i = None

@@ -47,9 +47,9 @@ def _run(case, dtype, fused, steps, csc_rank=True, graph=False):
     m.set_option("DETERMINISTIC", True)
     m.set_option("CSC_RANK", csc_rank)
     sch = m.schedule()
-    # bf16 at C2 keeps the timed schedule (fused statistics, merged transpose); fp32 has neither
-    timed = dtype == "bf16" and csc_rank and case[2] % 128 == 0
-    assert sch["DETERMINISTIC"] and sch["FUSED_STATS"] == (dtype == "bf16") and sch["MERGED_CSC"] == timed, sch
+    # both dtypes keep the timed schedule (fused statistics; the merged transpose at batch % 128)
+    timed = csc_rank and case[2] % 128 == 0
+    assert sch["DETERMINISTIC"] and sch["FUSED_STATS"] and sch["MERGED_CSC"] == timed, sch
     batches = [synth_batch(D, BS, NEG, seed=4000 + i, mean_nnz=32) for i in range(steps)]
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):

@@ -133,8 +133,10 @@ def test_fused_stats_unsupported_batch_falls_back():
     assert not m.fused_stats
     m2 = DSSM(1000, (64, 32), 64, 4, dtype="bf16")
     assert m2.fused_stats
-    m3 = DSSM(1000, (64, 32), 64, 4, dtype="fp32")
-    assert not m3.fused_stats
+    m3 = DSSM(1000, (64, 32), 64, 4, dtype="fp32")  # fp32 parity mode: fused too (g32.h tiles)
+    assert m3.fused_stats
+    m4 = DSSM(1000, (64, 32), 48, 4, dtype="fp32")
+    assert not m4.fused_stats
 
 
 def test_train_forward_without_backward_reports_its_loss():
