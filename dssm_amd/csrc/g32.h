@@ -18,9 +18,25 @@
 // FWD: A = Z_{l-1} [M x lda] (RK, BN + ReLU applied while staging), B = W_l [K x ldb] (KR)
 // DA : A = dZ_l  [M x lda] (RK), B^T = W_l [N x ldb], i.e. W's rows (RK)
 // DW : A^T of A_{l-1} [K x lda] (KR, a virtual ones column at m == M - 1 gives db), B = dZ_l (KR)
+//
+// DSSM_G32_SPLIT (default 1): the products on the bf16 matrix cores instead, each fp32 operand
+// split EXACTLY into three bf16 planes while staging (x = h + m + l: h = bf16(x), m = bf16(x - h),
+// l = x - h - m, each step exact in fp32 for normal x), and per 32-deep chunk the six partial
+// products down to 2^-16 relative (hh; hm, mh; hl, lh, mm) on v_mfma_f32_16x16x32_bf16, fp32
+// accumulate, the hh chain and the small-term chain in separate accumulators summed in the
+// epilogue.  The dropped ml, lm, ll terms are below 2^-24 |a b|: every product is accurate to about
+// one fp32 rounding, and 6 bf16 MFMAs cost 6/16 of the 8 fp32 MFMAs they replace (the fp32 matrix
+// rate is 1/16 of bf16's, MI355X_MICROARCH.md).  LDS images hold the three planes as bf16: RK
+// [row][k] rows of 40 (ds_read_b128 fragments), KR [k][col] rows of 72 (ds_read_b64_tr_b16
+// fragments, tn.h).  DSSM_G32_SPLIT=0 builds the exact fp32 FMA-chain tiles described above.
 #pragma once
 #include "bnfuse.h"
 #include "common.h"
+#include "tn.h"
+
+#ifndef DSSM_G32_SPLIT
+#define DSSM_G32_SPLIT 1
+#endif
 
 namespace dssm {
 
@@ -28,7 +44,13 @@ constexpr int kG32KC = 32;                    // k per chunk
 constexpr int kG32LdRK = kG32KC + 4;          // 36
 constexpr int kG32LdKR = 64 + 8;              // 72
 constexpr int kG32Img = 64 * kG32LdRK > kG32KC * kG32LdKR ? 64 * kG32LdRK : kG32KC * kG32LdKR;
-constexpr int kG32SmemFloats = 2 * 2 * kG32Img;  // two chunk buffers of (A, B) images: 40 KB
+constexpr bool kG32Split = DSSM_G32_SPLIT != 0;
+constexpr int kS3LdRK = kG32KC + 8;           // split planes, RK: 40 bf16 (80-B rows)
+constexpr int kS3LdKR = kTnLd;                // split planes, KR: 72 bf16 (tn.h's stride)
+constexpr int kS3Plane = 64 * kS3LdRK > kG32KC * kS3LdKR ? 64 * kS3LdRK : kG32KC * kS3LdKR;  // u16
+constexpr int kS3Img = 3 * kS3Plane;          // one operand's three planes (u16)
+// two chunk buffers of (A, B) images: exact 36 KB; split 60 KB
+constexpr int kG32SmemFloats = kG32Split ? 2 * 2 * kS3Img / 2 : 2 * 2 * kG32Img;
 constexpr int kG32MaxK = 320;                 // FWD / DA: the whole K in NCH = 10 chunks
 constexpr int kG32DwSplit = 384;              // DW: batch rows per split-K slab (12 chunks)
 #ifndef DSSM_G32_DEPTH
@@ -92,6 +114,24 @@ struct G32Lds {
   float coef[4 * kG32MaxK];
   double red[2 * 64 * 2];
 };
+
+// 4 fp32 values -> their three bf16 planes, 4 bf16 each (x = h + m + l exactly for normal x)
+__device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  float r[4], q[4];
+  u16 a[4], b[4], c[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = f2bf(x[e]);
+    r[e] = x[e] - bf2f(a[e]);
+    b[e] = f2bf(r[e]);
+    q[e] = r[e] - bf2f(b[e]);
+    c[e] = f2bf(q[e]);
+  }
+  h = make_uint2(a[0] | ((unsigned)a[1] << 16), a[2] | ((unsigned)a[3] << 16));
+  m = make_uint2(b[0] | ((unsigned)b[1] << 16), b[2] | ((unsigned)b[3] << 16));
+  l = make_uint2(c[0] | ((unsigned)c[1] << 16), c[2] | ((unsigned)c[3] << 16));
+}
 
 // NCH: FWD / DA ceil(K / kG32KC) exactly (the launchers dispatch on it); DW kG32DwSplit / kG32KC.
 // WN: waves along the tile's 64 columns (2: 4 waves of 32 x 32; 4: 8 waves of 32 x 16, two per
@@ -258,6 +298,25 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
           if (k0 + kr_k + KRH * h < kend) xa[h].x = 1.0f;
       }
     }
+    if constexpr (kG32Split) {
+      u16* pa = reinterpret_cast<u16*>(L.img) + buf * 2 * kS3Img;
+      u16* pb = pa + kS3Img;
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const int oa = A_RK ? (rk_r + RKH * h) * kS3LdRK + rk_k : (kr_k + KRH * h) * kS3LdKR + kr_c;
+        const int ob = B_RK ? (rk_r + RKH * h) * kS3LdRK + rk_k : (kr_k + KRH * h) * kS3LdKR + kr_c;
+        uint2 x0, x1, x2;
+        split3(xa[h], x0, x1, x2);
+        *reinterpret_cast<uint2*>(pa + oa) = x0;
+        *reinterpret_cast<uint2*>(pa + kS3Plane + oa) = x1;
+        *reinterpret_cast<uint2*>(pa + 2 * kS3Plane + oa) = x2;
+        split3(xb[h], x0, x1, x2);
+        *reinterpret_cast<uint2*>(pb + ob) = x0;
+        *reinterpret_cast<uint2*>(pb + kS3Plane + ob) = x1;
+        *reinterpret_cast<uint2*>(pb + 2 * kS3Plane + ob) = x2;
+      }
+      return;
+    }
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       if constexpr (A_RK) *reinterpret_cast<float4*>(&sa[(rk_r + RKH * h) * kG32LdRK + rk_k]) = xa[h];
@@ -266,11 +325,11 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
       else *reinterpret_cast<float4*>(&sb[(kr_k + KRH * h) * kG32LdKR + kr_c]) = xb[h];
     }
   };
-  f32x4 acc[2][JN];
+  f32x4 acc[2][JN], acc2[2][JN];  // split: hh; the five small terms
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   G32_TL(f.tl_slot, 1);
   // ---- the chunk pipeline.  Iteration c: load chunk c + D, stage chunk c + 1 into the other LDS
   // image, the MFMAs of chunk c, one barrier.  Staging (the wait for c + 1's loads, BN + ReLU, the
@@ -317,6 +376,54 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
 #pragma unroll
     for (int st = 0; st < kG32KC / 8; ++st) frag(8 * st, av[st], bv[st]);
 #endif
+    if constexpr (kG32Split) {
+      // the chunk's fragments: per operand block its three planes (RK: one ds_read_b128 of 8
+      // consecutive k; KR: tn.h's transposing pair of ds_read_b64_tr_b16), read before the next
+      // chunk's loads and staging, then the 6 x 2 x JN MFMAs term by term (independent chains
+      // back to back)
+      const u16* pa = reinterpret_cast<const u16*>(L.img) + (c & 1) * 2 * kS3Img;
+      const u16* pb = pa + kS3Img;
+      bf16x8 af[2][3], bf[JN][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = wm * 32 + i * 16;
+          if constexpr (A_RK)
+            af[i][q] = *reinterpret_cast<const bf16x8*>(pa + q * kS3Plane + (r + fr) * kS3LdRK + 8 * fk);
+          else
+            af[i][q] = tn_frag(pa + q * kS3Plane, 0, r, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int r = wn * WC + j * 16;
+          if constexpr (B_RK)
+            bf[j][q] = *reinterpret_cast<const bf16x8*>(pb + q * kS3Plane + (r + fr) * kS3LdRK + 8 * fk);
+          else
+            bf[j][q] = tn_frag(pb + q * kS3Plane, 0, r, lane);
+        }
+      }
+#ifndef DSSM_G32_NOSTAGE
+      if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
+      if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
+#endif
+      G32_TL(f.tl_slot, 2 + 2 * c);
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {  // (a plane, b plane): hh, hm, mh, hl, lh, mm
+        const int qa = u == 2 || u == 5 ? 1 : (u == 4 ? 2 : 0);
+        const int qb = u == 1 || u == 5 ? 1 : (u == 3 ? 2 : 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < JN; ++j) {
+            if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[j][0], acc[i][j], 0, 0, 0);
+            else acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][qa], bf[j][qb], acc2[i][j], 0, 0, 0);
+          }
+      }
+      __syncthreads();
+      G32_TL(f.tl_slot, 3 + 2 * c);
+      continue;
+    }
 #ifndef DSSM_G32_NOSTAGE  // diagnostics (wrong results): the loop without its loads and staging
     if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
     if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
@@ -382,7 +489,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * 32 + i * 16 + fk * 4 + r, m = bm + rl;
-        const float v = acc[i][j][r];
+        const float v = kG32Split ? acc2[i][j][r] + acc[i][j][r] : acc[i][j][r];
         const float x = (n < N) ? v + bcol[j] : 0.f;  // DW / DA: no bias (bcol zero)
         sC[rl * kCld + cl] = x;
         if constexpr (FS == 1) {

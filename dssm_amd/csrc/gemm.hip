@@ -329,6 +329,15 @@ struct NtFuse {
   int lds_epi;             // whole-K tiles: C staged through LDS, stored as 16-B row segments
   DetAcc det;              // deterministic mode: out_sum by slab rows + fixed-order last-arrival sum
   int det_rows;            // the launch's row tiles (arrivals per column tile)
+  // BN-backward A (dA pair of the last layer): A = dZ_l formed while staging from dA_l (a.A, fp32),
+  // the layer's pre-BN Z_l (zA), coefficients and backward sums (inb); dZ_l also written (bf16) by
+  // the column-tile-0 workgroups to a.a_out for dW_l.  One extra workgroup: the forward's deferred
+  // loss (loss_part) and BN_l's dgamma / dbeta.
+  BnSide inb;
+  const float* zA;
+  const float* loss_part;
+  int loss_blocks;
+  float* loss_out;
 };
 
 template <bool BN_A, int FS>
@@ -569,16 +578,17 @@ constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: (32 WM)
 __host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
 // LDS: A / B panels, BN coefficients, then the column-sum reduction.  The LDS epilogue stages a
 // [32 WM][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
-__host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi, int WM = 4) {
-  const size_t panels = (size_t)(32 * WM + 64) * wk_ldk(Kp) * 2 + (size_t)4 * Kp * 4;
+constexpr int kBnbMaxK = 128;          // BN-backward A: K (the last layer's width) it stages
+__host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi, int WM = 4, int coef_rows = 4) {
+  const size_t panels = (size_t)(32 * WM + 64) * wk_ldk(Kp) * 2 + (size_t)coef_rows * Kp * 4;
   const size_t epi = (size_t)32 * WM * 68 * 4;
   return (lds_epi && panels < epi) ? epi : panels;
 }
-__host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM = 4) {
-  return wk_red_offset(Kp, lds_epi, WM) + (size_t)WM * 64 * 2 * 8;
+__host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM = 4, int coef_rows = 4) {
+  return wk_red_offset(Kp, lds_epi, WM, coef_rows) + (size_t)WM * 64 * 2 * 8;
 }
 
-template <bool BN_A, int FS, int WM = 4>
+template <bool BN_A, int FS, int WM = 4, bool BNB = false>
 __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
                                            u16* wk_smem) {
   constexpr int NT = 128 * WM, ROWS = 32 * WM, BT = NT / 64;  // threads, tile rows, B threads / row
@@ -586,9 +596,10 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const int Kp = (K + 31) & ~31, LDK = wk_ldk(Kp);
   u16* sA = wk_smem;                                     // [ROWS][LDK]
   u16* sB = sA + ROWS * LDK;                             // [64][LDK]
-  float* sCoef = reinterpret_cast<float*>(sB + 64 * LDK);  // [tower][inv|shift][Kp]
+  // [tower][inv|shift][Kp]; BNB: [tower][mu|rstd|inv|shift|m1|m2][Kp]
+  float* sCoef = reinterpret_cast<float*>(sB + 64 * LDK);
   double* sRed = reinterpret_cast<double*>(reinterpret_cast<char*>(wk_smem) +
-                                           wk_red_offset(Kp, f.lds_epi, WM));  // [WM][64][2]
+                                           wk_red_offset(Kp, f.lds_epi, WM, BNB ? 12 : 4));  // [WM][64][2]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int bm = ty * ROWS, bn = tx * 64;
@@ -605,8 +616,10 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   // rotation of the K groups' issue order.)
   const int arow = t >> 2, ag0 = t & 3;
   const int brow = t / BT, bg0 = t % BT;
-  constexpr int NGA = kWkMaxG, NGB = (4 * kWkMaxG + BT - 1) / BT;  // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
-  float4 fa[NGA][2];  // fp32 A groups (BN_A)
+  // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
+  constexpr int NGA = BNB ? kBnbMaxK / 32 : kWkMaxG, NGB = (4 * NGA + BT - 1) / BT;
+  float4 fa[NGA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
+  float4 fz[BNB ? NGA : 1][2];  // BNB: the A layer's Z
   uint4 ua[NGA];      // bf16 A groups
   uint4 ub[NGB];
   {
@@ -616,9 +629,13 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     for (int i = 0; i < NGA; ++i) {
       const int kg = (ag0 + 4 * i) * 8;
       const size_t off = (rok && kg < lda) ? rbase + kg : 0;
-      if constexpr (BN_A) {
+      if constexpr (BN_A || BNB) {
         fa[i][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
         fa[i][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
+        if constexpr (BNB) {
+          fz[i][0] = *reinterpret_cast<const float4*>(f.zA + off);
+          fz[i][1] = *reinterpret_cast<const float4*>(f.zA + off + 4);
+        }
       } else {
         ua[i] = *reinterpret_cast<const uint4*>((const u16*)a.A + off);
       }
@@ -687,8 +704,27 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     }
     __syncthreads();
   }
+  if constexpr (BNB) {  // the A layer's forward coefficients and backward means (pad columns zero)
+    const BnSide& b = f.inb;
+    const size_t plane = (size_t)2 * b.ld;
+    for (int i = t; i < 2 * Kp; i += NT) {
+      const int tw = i / Kp, k = i - tw * Kp;
+      const bool ok = k < b.n;
+      const size_t o = (size_t)tw * b.ld + (ok ? k : 0);
+      float v[6];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ok ? b.coef[q * plane + o] : 0.f;
+      float m1 = 0.f, m2 = 0.f;
+      if (ok) fs_dcoef(b, tw, k, m1, m2);
+      v[4] = m1;
+      v[5] = m2;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) sCoef[(tw * 6 + q) * Kp + k] = v[q];
+    }
+    __syncthreads();
+  }
   // ---- LDS images (bf16); out-of-range groups zeroed here, after every load was issued
-  const bool write_a = BN_A && a.a_out != nullptr && tx == 0;
+  const bool write_a = (BN_A || BNB) && a.a_out != nullptr && tx == 0;
   {
     const bool rok = bm + arow < M;
 #pragma unroll
@@ -706,6 +742,25 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
             float y[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
+            v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
+            v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
+            if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + arow) * lda + kg) = v;
+          }
+        } else if constexpr (BNB) {
+          if (ok) {  // bn.hip's k_bn_bwd_apply_fs arithmetic: dZ = inv * (dy - m1 - xhat * m2)
+            const float* cm = &sCoef[(tower * 6) * Kp + kg];
+            const float z[8] = {fz[i][0].x, fz[i][0].y, fz[i][0].z, fz[i][0].w,
+                                fz[i][1].x, fz[i][1].y, fz[i][1].z, fz[i][1].w};
+            const float d[8] = {fa[i][0].x, fa[i][0].y, fa[i][0].z, fa[i][0].w,
+                                fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
+            float y[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const float mu = cm[q], rstd = cm[Kp + q], inv = cm[2 * Kp + q], sh = cm[3 * Kp + q];
+              const float dy = (bn_affine(z[q], inv, sh) > 0.f) ? d[q] : 0.f;  // ReluGrad
+              const float xh = (z[q] - mu) * rstd;
+              y[q] = inv * (dy - cm[4 * Kp + q] - xh * cm[5 * Kp + q]);
+            }
             v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
             v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
             if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + arow) * lda + kg) = v;
@@ -985,12 +1040,21 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
 }
 
 // Whole-K backward pair, dA tiles only (the dW_l tiles ride in the next BN-backward apply launch).
-template <int WM>
+// BNB: the A operand dZ_l formed from dA_l while staging (NtFuse::inb); block nt_blocks: the loss
+// and BN_l's dgamma / dbeta.
+template <int WM, bool BNB = false>
 __global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks) {
   extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
   WG_TL(a.K == 300 ? 3 : 2, 0);
+  if constexpr (BNB) {
+    if ((int)blockIdx.x >= nt_blocks) {
+      if (f.loss_part) loss_reduce(f.loss_part, f.loss_blocks, f.inb.rows_q, f.loss_out);
+      fs_materialize_bwd(f.inb);
+      return;
+    }
+  }
   const int tile = xcd_tile(blockIdx.x, nt_blocks);
-  nt_wk_body<false, 2, WM>(a, f, tile % nt_x, tile / nt_x, pw_smem);
+  nt_wk_body<false, 2, WM, BNB>(a, f, tile % nt_x, tile / nt_x, pw_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1170,6 +1234,44 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
 hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float* dst, hipStream_t s) {
   const int rg = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
   hipLaunchKernelGGL(k_splitk_reduce, dim3(rg), dim3(256), 0, s, slab, splits, n, dst);
+  return hipGetLastError();
+}
+
+// The last layer's pair with its BN backward folded into the dA tiles' A staging (no apply launch
+// for BN_l): dZ_l = BN_l backward of (dA_l, Z_l) formed per element while staging, written bf16 to
+// dZ_out by the column-tile-0 tiles for dW_l, whose split-K tiles are handed over (dw_out) to the next
+// apply launch; one extra workgroup writes BN_l's dgamma / dbeta and the deferred loss.
+hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const float* Z_l, const BnSide& b,
+                               uint16_t* dZ_out, int lddz, const uint16_t* W, int ldw, float* dA, int ldda,
+                               const float* z_prev, const float* coef_prev, double* bsum_prev, int row_split,
+                               const uint16_t* A_prev, int lda_prev, float* slab, float* gw, bool defer,
+                               hipStream_t s, int* deferred_splits, TnParams* dw_out, const DetAcc* det,
+                               const float* loss_part, int loss_blocks, float* loss_out) {
+  if ((lddz % 8) || (ldw % 8) || (lda_prev % 8) || n > lddz || n > ldw || n > kBnbMaxK || (row_split % 128) ||
+      lda_prev < kin || b.ld != lddz || b.n != n || !dw_out || kWkRows != 128)
+    return hipErrorInvalidValue;
+  const NtParams a{M, kin, n, dA_l, lddz, nullptr, row_split, W, ldw, dA, ldda, nullptr, dZ_out};
+  NtFuse f{};
+  f.out_sum = bsum_prev;
+  f.zb = z_prev;
+  f.coefb = coef_prev;
+  f.lds_epi = 0;
+  if (det) f.det = *det;
+  f.inb = b;
+  f.zA = Z_l;
+  f.loss_part = loss_part;
+  f.loss_blocks = loss_blocks;
+  f.loss_out = loss_out;
+  const int Kp = (n + 31) & ~31;
+  const int nt_x = cdiv(ldda, 64), nt_blocks = nt_x * cdiv(M, 128);
+  const int Mw = kin + 1;
+  const int nsplit = cdiv(M, kTwKc);
+  *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ_out, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
+  f.det_rows = cdiv(M, 128);
+  if (!det_fits(f, ldda)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_pair_da_wk<4, true>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s, a,
+                     f, nt_x, nt_blocks);
+  *deferred_splits = (defer && nsplit > 1) ? nsplit : 0;
   return hipGetLastError();
 }
 

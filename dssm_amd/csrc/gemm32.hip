@@ -17,7 +17,7 @@ namespace dssm {
 namespace {
 
 #ifndef DSSM_G32_WN
-#define DSSM_G32_WN 4  // forward / dA tiles: 8 waves of 32 x 16 (2: 4 waves of 32 x 32)
+#define DSSM_G32_WN (DSSM_G32_SPLIT ? 2 : 4)  // forward / dA tiles: 2 = 4 waves of 32 x 32, 4 = 8 of 32 x 16
 #endif
 constexpr int kWN = DSSM_G32_WN;
 

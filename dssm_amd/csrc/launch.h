@@ -131,6 +131,15 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
 // caller then sums the slabs into gw with launch_splitk_reduce.
+// The same for the last layer (n <= 128) with BN_l's backward folded into the A staging: dZ_l
+// formed from dA_l / Z_l / b's coefficients and backward sums, written bf16 to dZ_out (stride lddz
+// = b.ld); one extra workgroup writes dgamma / dbeta and reduces the deferred loss (loss_part).
+hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const float* Z_l, const BnSide& b,
+                               uint16_t* dZ_out, int lddz, const uint16_t* W, int ldw, float* dA, int ldda,
+                               const float* z_prev, const float* coef_prev, double* bsum_prev, int row_split,
+                               const uint16_t* A_prev, int lda_prev, float* slab, float* gw, bool defer,
+                               hipStream_t s, int* deferred_splits, TnParams* dw_out, const DetAcc* det,
+                               const float* loss_part, int loss_blocks, float* loss_out);
 hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float* dst, hipStream_t s);
 
 // ---- fp32 parity mode's fused dense layers (gemm32.hip, g32.h: f32-input MFMA 16x16x4) ----

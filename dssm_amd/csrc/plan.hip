@@ -254,6 +254,7 @@ struct dssm_plan {
       1,  // FUSED_W1_ADAM: dW1 light rows and the dW_l slabs consumed inside Adam
       1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
       0,  // MEMCPY_NODES: diagnostics: data-parallel device copies as hipMemcpyAsync nodes
+      1,  // BNB_IN_PAIR: the last layer's BN backward formed in the dA pair's A staging
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -366,6 +367,13 @@ struct dssm_plan {
     return !Lt.bf16 && on(DSSM_OPT_SCATTER_IN_COS) && !deterministic();
   }
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
+  // bf16 fused schedule: the last layer's BN backward inside its dA pair launch (gemm.hip
+  // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 128, the dW tiles handed to the next apply)
+  bool bnb_in_pair() const {
+    const int l = Lt.L - 1;
+    return on(DSSM_OPT_BNB_IN_PAIR) && on(DSSM_OPT_DW_IN_APPLY) && Lt.bf16 && Lt.L >= 2 && fused_stats() &&
+           wholek(l) && Lt.n[l] <= 128 && (Lt.BS % 128) == 0 && ((Lt.R - Lt.BS) % 128) == 0;
+  }
   bool fused_stats_ok() const {
     if (Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -843,12 +851,16 @@ static int backward_impl(dssm_plan* P, void* stream) {
     float* dw_reduce_to = nullptr;
     // dW_l's split-K slabs summed later: by the fused Adam step, or by the wire gradient pass
     const bool defer_slabs = P->fused_w1_adam() || wire_gradient_pass(P);
+    const bool bnb = P->bnb_in_pair();
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
       const float* lp = fin ? P->at<float>(Lt.loss_j) : nullptr;
       const int lb = dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true);
-      if (Lt.bf16)
+      const bool folded = bnb && l == Lt.L - 1;  // BN_l's backward rides in the pair launch below
+      if (folded)
+        ;
+      else if (Lt.bf16)
         HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                                 P->at<uint16_t>(Lt.dZ[l]), s, lp, lb, P->at<float>(Lt.loss),
                                                 dw_pending ? &dw : nullptr));
@@ -872,7 +884,15 @@ static int backward_impl(dssm_plan* P, void* stream) {
       dw = dssm::TnParams{};  // filled by the pair launch when it hands its dW tiles over
       dw32 = dssm::G32Params{};
       float* gw = P->g + Lt.fc_off[l];
-      if (Lt.bf16)
+      if (folded)
+        HIP_TRY(dssm::launch_bwd_pair_bnb(
+            Lt.R, Lt.in_dim[l], Lt.n[l], P->at<float>(Lt.dA[l]), P->at<float>(Lt.Z[l]), b,
+            P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l], P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l],
+            P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]),
+            P->at<double>(Lt.bsum[l - 1]), Lt.BS, P->at<uint16_t>(Lt.A[l - 1]), Lt.ldp[l - 1],
+            P->at<float>(Lt.dw_slab[l]), gw, defer_slabs, s, &P->dw_deferred[l], &dw,
+            P->deterministic() ? &bprev.bdet : nullptr, lp, lb, P->at<float>(Lt.loss)));
+      else if (Lt.bf16)
         HIP_TRY(dssm::launch_bwd_pair(
             Lt.R, Lt.in_dim[l], Lt.n[l], P->at<uint16_t>(Lt.dZ[l]), Lt.ldp[l],
             P->at<uint16_t>(Lt.shadow[l]), Lt.ldp[l], P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1],
@@ -1256,6 +1276,7 @@ int dssm_plan_schedule(const dssm_plan* P) {
   if (fs && P->on(DSSM_OPT_DW_IN_APPLY)) f |= DSSM_SCHED_DW_IN_APPLY;
   if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
   if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;
+  if (P->bnb_in_pair()) f |= DSSM_SCHED_BNB_IN_PAIR;
   return f;
 }
 

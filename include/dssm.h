@@ -147,7 +147,10 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *                      step's forward skips the rank launch
  *   MEMCPY_NODES    0; 1 (diagnostics): the data-parallel graph's device copies (the all-to-all's own
  *                      chunk, the copy rehearsal) as hipMemcpyAsync -- memcpy nodes in a capture --
- *                      instead of the copy kernel */
+ *                      instead of the copy kernel
+ *   BNB_IN_PAIR     1: bf16 fused schedule, last layer <= 128 wide: its BN backward is formed while the
+ *                      dA pair launch stages its A operand (no BN-backward apply launch for it); 0: the
+ *                      apply launch */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -160,6 +163,7 @@ enum {
   DSSM_OPT_FUSED_W1_ADAM,
   DSSM_OPT_RANK_IN_ADAM,
   DSSM_OPT_MEMCPY_NODES,
+  DSSM_OPT_BNB_IN_PAIR,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);
@@ -270,7 +274,8 @@ enum {
   DSSM_SCHED_DW_IN_APPLY = 32,     /* dW_l split-K tiles inside the next BN-backward apply launch */
   DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
   DSSM_SCHED_DETERMINISTIC = 128,  /* fixed-order reductions: bit-identical repeated runs */
-  DSSM_SCHED_NT32 = 256            /* fp32: layers >= 2 on the fused fp32 MFMA tiles (g32.h) */
+  DSSM_SCHED_NT32 = 256,           /* fp32: layers >= 2 on the fused fp32 MFMA tiles (g32.h) */
+  DSSM_SCHED_BNB_IN_PAIR = 512     /* the last layer's BN backward inside the dA pair's A staging */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
 /* A train forward (either precision) leaves the loss / accuracy reduction to the backward's first

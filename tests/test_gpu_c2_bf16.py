@@ -83,7 +83,7 @@ def _expect_timed_schedule(m, case):
     if case != C2:
         return
     f = m.schedule()
-    want = ["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "WHOLEK", "DW_IN_APPLY", "SCATTER_IN_COS"]
+    want = ["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "WHOLEK", "DW_IN_APPLY", "SCATTER_IN_COS", "BNB_IN_PAIR"]
     missing = [w for w in want if not f.get(w)]
     assert not missing, (case, missing, f)
 

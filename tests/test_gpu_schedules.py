@@ -5,7 +5,10 @@ Two placements of work are plan options (dssm_plan_set_option):
 * DW_IN_APPLY: dW_l's split-K tiles run in the BN_{l-1} backward-apply launch (default,
   tn.h tn_chunk_body, 64 x 64 tiles) or in the backward pair launch (0, 128 x 64 tiles);
 * SCATTER_IN_COS: the CSC transpose's scatter runs as a role of the cosine launch
-  (default, csc.h) or beside the BN1 sums (0).
+  (default, csc.h) or beside the BN1 sums (0);
+* BNB_IN_PAIR: the last layer's BN backward is formed while its dA pair launch stages the A
+  operand (default, gemm.hip launch_bwd_pair_bnb, which also writes dZ_L for dW_L, dgamma / dbeta
+  and the loss) or by its own BN-backward apply launch (0).
 
 Both tile shapes sum every split in the same k order, and the scatter writes every entry to
 the slot its rank reserved, so the schedules compute the same step.  The check is teacher-forced
@@ -29,7 +32,7 @@ from tests.test_gpu_parity import make
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{"DW_IN_APPLY": False}, {"SCATTER_IN_COS": False},
-            {"DW_IN_APPLY": False, "SCATTER_IN_COS": False}]
+            {"DW_IN_APPLY": False, "SCATTER_IN_COS": False}, {"BNB_IN_PAIR": False}]
 CASES = [
     # (D, widths, BS, NEG, fused); BS a multiple of 128: the whole-K backward pair path
     (5000, (300, 300, 128), 128, 4, True),
@@ -54,6 +57,7 @@ def test_schedule_matches_default(case, variant):
     _, _, var = make(D, widths, BS, NEG, "bf16", fused=fused)
     for k, x in variant.items():
         var.set_option(k, x)
+    assert ref.schedule()["BNB_IN_PAIR"] and not (var.schedule()["BNB_IN_PAIR"] and "BNB_IN_PAIR" in variant)
     batches = [synth_batch(D, BS, NEG, seed=3000 + i, mean_nnz=32) for i in range(steps)]
     for i, hb in enumerate(batches):
         _copy_state(var, ref)
