@@ -427,9 +427,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
     float out[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float dy, xh;
-      bwd_terms(zz[k], dd[k], mm[k], rr[k], ii[k], ss[k], dy, xh);
-      out[k] = ii[k] * (dy - a1[k] - xh * a2[k]);
+      out[k] = bn_bwd_dz(zz[k], dd[k], mm[k], rr[k], ii[k], ss[k], a1[k], a2[k]);
     }
     if constexpr (sizeof(TO) == 4) {
       *reinterpret_cast<float4*>((float*)dZ + (size_t)r * ldz + c) = make_float4(out[0], out[1], out[2], out[3]);
@@ -565,9 +563,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
     float out[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float dy, xh;
-      bwd_terms(zz[k], dd[k], sc[t][0][c + k], sc[t][1][c + k], sc[t][2][c + k], sc[t][3][c + k], dy, xh);
-      out[k] = sc[t][2][c + k] * (dy - sc[t][4][c + k] - xh * sc[t][5][c + k]);
+      out[k] = bn_bwd_dz(zz[k], dd[k], sc[t][0][c + k], sc[t][1][c + k], sc[t][2][c + k], sc[t][3][c + k],
+                         sc[t][4][c + k], sc[t][5][c + k]);
     }
     if constexpr (sizeof(TO) == 2) {
       uint2 p;

@@ -323,6 +323,18 @@ __device__ __forceinline__ void fs_dcoef(const BnSide& b, int t, int c, float& m
   m2 = (float)(s2 / N);
 }
 
+// BN + ReLU backward of one element: dZ = inv * (dy - m1 - xhat * m2), dy = da where BN(z) > 0
+// (ReluGrad), xhat = (z - mu) * rstd, m1 / m2 the column's mean(dy) / mean(dy * xhat).  Every
+// operation rounded on its own (no FMA contraction), so each kernel that forms dZ -- bn.hip's apply
+// launches, gemm.hip's pair with the BN backward folded into its staging -- gets the same fp32 value.
+__device__ __forceinline__ float bn_bwd_dz(float z, float da, float mu, float rstd, float inv, float sh,
+                                           float m1, float m2) {
+#pragma clang fp contract(off)  // (HIP's __fmul_rn / __fsub_rn are plain operators: contractible)
+  const float dy = (bn_affine(z, inv, sh) > 0.f) ? da : 0.f;
+  const float xh = (z - mu) * rstd;
+  return inv * ((dy - m1) - xh * m2);
+}
+
 // dbeta = sum dy, dgamma = sum dy*xhat per tower (one workgroup).
 __device__ __forceinline__ void fs_materialize_bwd(const BnSide& b) {
   for (int i = threadIdx.x; i < 2 * b.n; i += blockDim.x) {

@@ -755,12 +755,9 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
                                 fa[i][1].x, fa[i][1].y, fa[i][1].z, fa[i][1].w};
             float y[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const float mu = cm[q], rstd = cm[Kp + q], inv = cm[2 * Kp + q], sh = cm[3 * Kp + q];
-              const float dy = (bn_affine(z[q], inv, sh) > 0.f) ? d[q] : 0.f;  // ReluGrad
-              const float xh = (z[q] - mu) * rstd;
-              y[q] = inv * (dy - cm[4 * Kp + q] - xh * cm[5 * Kp + q]);
-            }
+            for (int q = 0; q < 8; ++q)
+              y[q] = bn_bwd_dz(z[q], d[q], cm[q], cm[Kp + q], cm[2 * Kp + q], cm[3 * Kp + q], cm[4 * Kp + q],
+                               cm[5 * Kp + q]);
             v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
             v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
             if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + arow) * lda + kg) = v;
