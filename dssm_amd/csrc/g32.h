@@ -172,24 +172,48 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   const int kr_k = t >> 4, kr_c = (t & 15) * 4;
   constexpr int RKH = NT / 8, KRH = NT / 16;
   float4 ra[S][G], rb[S][G];
-  // Every load is unconditional, from its own address when in range and from the operand's base
-  // otherwise (a select, no branch: a masked load in a branch makes the compiler drain vmcnt at
-  // the merge); stage() zeroes the out-of-range groups.  Widths are multiples of 4, so a float4
-  // is all in range or all out.
-  // Chunk c of the pipeline is K chunk (c + rot) % NCH: tiles that share an operand walk K from
-  // different chunks (a row block's column tiles share A, a column tile's row blocks share B).  Each
-  // tile's k order is fixed by its position: results are deterministic fp32 FMA chains.
-  const int rot = (tx + ty + tz) % NCH;
-  auto kofs = [&](int c) { return kbeg + ((c + rot) % NCH) * kG32KC; };
+  // Each staged group's row / column part of its address is computed once; a chunk adds its k
+  // offset (RK: along the row, a compile-time offset for FWD / DA; KR: k rows of stride ld).  Loads
+  // are unconditional (a masked load in a branch makes the compiler drain vmcnt at the merge):
+  // out-of-range rows / columns read row / column 0, and in a chunk that reaches past kend the k
+  // index is clamped to the operand's stored extent.  stage() zeroes the groups outside, under
+  // uniform conditions (edge tiles, the tail chunk) that interior tiles and full chunks skip.
+  // Every tile walks K in order: each result is a fixed sequence of fp32 accumulations.
+  const int kdim = MODE == G32_DW ? p.K : kend;  // k extent in memory (DW: every batch row)
+  size_t a_off[G], b_off[G];
+  bool a_in[G], b_in[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    if constexpr (A_RK) {
+      const int r = bm + rk_r + RKH * h;
+      a_in[h] = r < M;
+      a_off[h] = (size_t)(a_in[h] ? r : 0) * p.lda + rk_k;
+    } else {
+      const int c = bm + kr_c;
+      a_in[h] = c < Mload;
+      a_off[h] = (size_t)(kr_k + KRH * h) * p.lda + (a_in[h] ? c : 0);
+    }
+    if constexpr (B_RK) {
+      const int r = bn + rk_r + RKH * h;
+      b_in[h] = r < N;
+      b_off[h] = (size_t)(b_in[h] ? r : 0) * p.ldb + rk_k;
+    } else {
+      const int c = bn + kr_c;
+      b_in[h] = c < N;
+      b_off[h] = (size_t)(kr_k + KRH * h) * p.ldb + (b_in[h] ? c : 0);
+    }
+  }
+  const bool edge = bm + 64 > (A_RK ? M : Mload) || bn + 64 > N;  // uniform
+  auto kofs = [&](int c) { return kbeg + c * kG32KC; };
   auto a_ok = [&](int c, int h) {
     const int k0 = kofs(c);
-    if constexpr (A_RK) return bm + rk_r + RKH * h < M && k0 + rk_k < kend;
-    else return k0 + kr_k + KRH * h < kend && bm + kr_c < Mload;
+    if constexpr (A_RK) return a_in[h] && k0 + rk_k < kend;
+    else return a_in[h] && k0 + kr_k + KRH * h < kend;
   };
   auto b_ok = [&](int c, int h) {
     const int k0 = kofs(c);
-    if constexpr (B_RK) return bn + rk_r + RKH * h < N && k0 + rk_k < kend;
-    else return k0 + kr_k + KRH * h < kend && bn + kr_c < N;
+    if constexpr (B_RK) return b_in[h] && k0 + rk_k < kend;
+    else return b_in[h] && k0 + kr_k + KRH * h < kend;
   };
   auto load = [&](int c, float4 (&xa)[G], float4 (&xb)[G]) {
 #ifdef DSSM_G32_SAMECHUNK  // diagnostics (wrong results): every chunk's loads from chunk 0's lines
@@ -197,14 +221,21 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
 #else
     const int k0 = kofs(c);
 #endif
+    // uniform; FWD / DA: only the last chunk (compile-time) can reach past K
+    const bool tail = (MODE == G32_DW || c == NCH - 1) && k0 + kG32KC > kend;
+    const float* pa = p.A + (A_RK ? (size_t)k0 : (size_t)k0 * p.lda);
+    const float* pb = p.B + (B_RK ? (size_t)k0 : (size_t)k0 * p.ldb);
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-      const size_t oa = A_RK ? (size_t)(bm + rk_r + RKH * h) * p.lda + k0 + rk_k   // A [M x lda]
-                             : (size_t)(k0 + kr_k + KRH * h) * p.lda + bm + kr_c;  // A^T from A [K x lda]
-      const size_t ob = B_RK ? (size_t)(bn + rk_r + RKH * h) * p.ldb + k0 + rk_k   // B^T [N x ldb]
-                             : (size_t)(k0 + kr_k + KRH * h) * p.ldb + bn + kr_c;  // B [K x ldb]
-      xa[h] = *reinterpret_cast<const float4*>(p.A + (a_ok(c, h) ? oa : 0));
-      xb[h] = *reinterpret_cast<const float4*>(p.B + (b_ok(c, h) ? ob : 0));
+      size_t oa = a_off[h], ob = b_off[h];
+      if (tail) {  // clamp k into the stored extent (rows past kend are zeroed by stage())
+        if constexpr (A_RK) oa -= (size_t)max(0, k0 + rk_k - (kdim - 4));
+        else oa -= (size_t)max(0, k0 + kr_k + KRH * h - (kdim - 1)) * p.lda;
+        if constexpr (B_RK) ob -= (size_t)max(0, k0 + rk_k - (kdim - 4));
+        else ob -= (size_t)max(0, k0 + kr_k + KRH * h - (kdim - 1)) * p.ldb;
+      }
+      xa[h] = *reinterpret_cast<const float4*>(pa + oa);
+      xb[h] = *reinterpret_cast<const float4*>(pb + ob);
     }
   };
   // the first D chunks' loads in flight before anything waits
@@ -270,10 +301,12 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     float* sb = sa + kG32Img;
     const int k0 = kofs(c);
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (edge || ((MODE == G32_DW || c == NCH - 1) && k0 + kG32KC > kend)) {  // uniform: edge tiles, tail chunk
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-      if (!a_ok(c, h)) xa[h] = z4;
-      if (!b_ok(c, h)) xb[h] = z4;
+      for (int h = 0; h < G; ++h) {
+        if (!a_ok(c, h)) xa[h] = z4;
+        if (!b_ok(c, h)) xb[h] = z4;
+      }
     }
     if constexpr (BN_A) {
       const float* ci = &L.coef[(tower * 2) * kG32MaxK + k0 + rk_k];
