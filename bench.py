@@ -111,6 +111,13 @@ def parse():
                     help="N>1 started as a plain process: after the headline ranks exit, run a second N-rank "
                          "child with --dp-mode allreduce --wire fp32 (one fp32 gradient all-reduce + replicated "
                          "Adam) and report its line as dp_alt, so one run measures both exchanges")
+    ap.add_argument("--dp-sparse", type=int, default=0,
+                    help="N>1 zero/bf16 schedule: the touched-row sparse gradient all-to-all (DataParallel"
+                         "(sparse=True): packed touched W1 rows, counts first, the tail all-reduce in the same "
+                         "RCCL group; between captured graphs)")
+    ap.add_argument("--dp-alt-sparse", type=int, default=1,
+                    help="N>1 started as a plain process: also run the --dp-sparse 1 exchange as a third child "
+                         "and report it as dp_alt_sparse")
     ap.add_argument("--dp-check", type=int, default=1,
                     help="N>1: after the timed region, gather the sharded optimizer state and compare a "
                          "digest of every rank's parameters / Adam m / v (reported as dp_check)")
@@ -165,6 +172,7 @@ def spawn_ranks(args) -> int:
     alternative's summary under dp_alt."""
     argv = sys.argv[1:]
     alt = args.dp_alt and args.model == "bow" and args.dp_mode != "allreduce"
+    alt_sparse = alt and args.dp_alt_sparse and not args.dp_sparse
     rc, lines = _run_ranks(args, argv, capture=alt)
     if not alt:
         return rc
@@ -173,18 +181,21 @@ def spawn_ranks(args) -> int:
             print(ln, flush=True)
         return rc or 1
     out = json.loads(lines[-1])
-    arc, alines = _run_ranks(args, argv + ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0"],
-                             capture=True)
-    if arc != 0 or not alines:
-        out["dp_alt"] = {"error": f"exit {arc}, no line"}
-    else:
+    legs = [("dp_alt", ["--dp-mode", "allreduce", "--wire", "fp32"])]
+    if alt_sparse:
+        legs.append(("dp_alt_sparse", ["--dp-sparse", "1"]))
+    for key, extra in legs:
+        arc, alines = _run_ranks(args, argv + extra + ["--dp-alt", "0", "--dp-alt-sparse", "0"], capture=True)
+        if arc != 0 or not alines:
+            out[key] = {"error": f"exit {arc}, no line"}
+            continue
         a = json.loads(alines[-1])
-        out["dp_alt"] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")}
-        out["dp_alt"].update({k: a["config"].get(k) for k in ("dp_exchange", "dp_launch", "comm")
-                              if k in a.get("config", {})})
+        out[key] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")}
+        out[key].update({k: a["config"].get(k) for k in ("dp_exchange", "dp_launch", "comm", "dp_sparse")
+                         if k in a.get("config", {})})
         for k in ("dp_kernels_ms", "dp_check"):
             if k in a:
-                out["dp_alt"][k] = a[k]
+                out[key][k] = a[k]
     print(json.dumps(out), flush=True)
     return 0
 
@@ -731,7 +742,8 @@ def main():
     dp = None
     if world > 1:
         from dssm_amd.dist import DataParallel
-        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks)
+        dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks,
+                          sparse=bool(args.dp_sparse))
     rehearse = args.rehearse_world if world == 1 else 1
     if rehearse > 1:
         # rank 0's kernels of a W-rank bf16-wire step in the data-parallel step graph, each
@@ -1043,6 +1055,10 @@ def main():
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",
                    "dp_exchange": dp.schedule if dp is not None else None,
                    "dp_fallbacks": dp.fallbacks if dp is not None else None,
+                   **({"dp_sparse": {"steps": dp.sparse_stats["steps"],
+                                     "rows_sent_frac": round(dp.sparse_stats["rows_sent"]
+                                                             / max(1, dp.sparse_stats["rows_dense"]), 4)}}
+                      if dp is not None and dp.sparse else {}),
                    "feed": "host CSR -> pinned async H2D (native feeder), PCIe inside the timed region"
                            if feeder is not None else "device-resident staged batches"},
         "roofline": dict(rl[dominant], kernel=dominant),

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("DSSM_LIB_PATH", LIB_PATH)
 
 DSSM_ABI_VERSION = 2
 DSSM_MAX_LAYERS = 8
-DSSM_F32, DSSM_BF16 = 0, 1
+DSSM_F32, DSSM_BF16, DSSM_I32 = 0, 1, 2
 DSSM_ACT_NONE, DSSM_ACT_RELU = 0, 1
 (BUF_LOSS, BUF_COS_SIM_RAW, BUF_COS_SIM, BUF_PROB, BUF_QUERY_NORM, BUF_EMBED, BUF_Z,
  BUF_BATCH_MEAN, BUF_BATCH_VAR, BUF_DZ) = range(10)
@@ -209,6 +209,9 @@ _SIGS = {
     "dssm_reduce_scatter_sum": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_all_gather": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_all_to_all": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
+    "dssm_all_to_allv": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, C.c_int64, C.c_int, _P]),
+    "dssm_rows_pack_u16": (C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P]),
+    "dssm_rows_unpack_u16": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _P, _P]),
     "dssm_comm_destroy": (C.c_int, []),
 }
 

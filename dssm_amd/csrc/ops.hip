@@ -476,3 +476,64 @@ int dssm_bn_relu_bwd(const float* Z, int ldz, int rows, int n, const float* gamm
 }
 
 }  // extern "C"
+
+// ---- touched-row sparse gradient exchange (dssm_amd/dist.py DataParallel(sparse=True)) --------
+// A packed row: [row id (int32, 2 u16)][2 u16 pad][n u16 of the row], stride n + 4 (8-B aligned).
+namespace {
+__global__ __launch_bounds__(256) void k_rows_pack_u16(const uint16_t* __restrict__ src, int64_t n,
+                                                       const int32_t* __restrict__ rows, int64_t count,
+                                                       uint16_t* __restrict__ out) {
+  const int64_t q = n / 4, stride = n + 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count * (q + 1);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / (q + 1), g = i - k * (q + 1);
+    const int32_t r = rows[k];
+    uint2 v;
+    if (g == 0) {
+      v.x = (uint32_t)r;
+      v.y = 0u;
+    } else {
+      v = *reinterpret_cast<const uint2*>(src + (int64_t)r * n + 4 * (g - 1));
+    }
+    *reinterpret_cast<uint2*>(out + k * stride + 4 * g) = v;
+  }
+}
+__global__ __launch_bounds__(256) void k_rows_unpack_u16(const uint16_t* __restrict__ in, int64_t n,
+                                                         int64_t count, int64_t row_base, int64_t nrows,
+                                                         uint16_t* __restrict__ dst) {
+  const int64_t q = n / 4, stride = n + 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count * q;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / q, g = i - k * q;
+    const int64_t r = (int64_t)*reinterpret_cast<const int32_t*>(in + k * stride) - row_base;
+    if (r < 0 || r >= nrows) continue;  // not this rank's row: never sent here
+    *reinterpret_cast<uint2*>(dst + r * n + 4 * g) = *reinterpret_cast<const uint2*>(in + k * stride + 4 + 4 * g);
+  }
+}
+int rows_grid(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 4096)); }
+}  // namespace
+
+extern "C" {
+
+int dssm_rows_pack_u16(const uint16_t* src, int64_t n, const int32_t* rows, int64_t count, uint16_t* out,
+                       void* stream) {
+  if (count < 0 || n <= 0 || (n % 4) || (count && (!src || !rows || !out)))
+    return oerr(DSSM_E_INVALID, "rows_pack_u16: bad argument (n a multiple of 4)");
+  if (count)
+    hipLaunchKernelGGL(k_rows_pack_u16, dim3(rows_grid(count * (n / 4 + 1))), dim3(256), 0, (hipStream_t)stream,
+                       src, n, rows, count, out);
+  return hip_status();
+}
+
+int dssm_rows_unpack_u16(const uint16_t* in, int64_t n, int64_t count, int64_t row_base, int64_t nrows,
+                         uint16_t* dst, void* stream) {
+  if (count < 0 || n <= 0 || (n % 4) || nrows < 0 || (count && (!in || !dst)))
+    return oerr(DSSM_E_INVALID, "rows_unpack_u16: bad argument (n a multiple of 4)");
+  if (count)
+    hipLaunchKernelGGL(k_rows_unpack_u16, dim3(rows_grid(count * (n / 4))), dim3(256), 0, (hipStream_t)stream,
+                       in, n, count, row_base, nrows, dst);
+  return hip_status();
+}
+
+}  // extern "C"
+

@@ -1674,6 +1674,7 @@ static int g_rank = 0, g_world = 0;
 static bool nccl_type(int dtype, ncclDataType_t* t, size_t* es) {
   if (dtype == DSSM_F32) { *t = ncclFloat32; *es = 4; return true; }
   if (dtype == DSSM_BF16) { *t = ncclBfloat16; *es = 2; return true; }
+  if (dtype == DSSM_I32) { *t = ncclInt32; *es = 4; return true; }
   return false;
 }
 
@@ -1792,6 +1793,54 @@ int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void
   if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es) || send == recv)
     return fail(DSSM_E_INVALID, "dssm_all_to_all: bad arguments (distinct send / recv)");
   return all_to_all_impl(send, recv, count, t, es, (hipStream_t)stream);
+}
+
+// Variable-count all-to-all of the touched-row sparse exchange, with the replicated tail's sum in the
+// same RCCL group (one launch of the group for both).  The rank's own part is a device copy.
+int dssm_all_to_allv(const void* send, const int64_t* send_counts, void* recv, const int64_t* recv_counts,
+                     int dtype, void* tail, int64_t tail_count, int tail_dtype, void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t, tt = ncclFloat32;
+  size_t es, tes = 4;
+  if (!send_counts || !recv_counts || !nccl_type(dtype, &t, &es) || send == recv ||
+      (tail && (tail_count < 0 || !nccl_type(tail_dtype, &tt, &tes))))
+    return fail(DSSM_E_INVALID, "dssm_all_to_allv: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const char* sp = static_cast<const char*>(send);
+  char* rp = static_cast<char*>(recv);
+  int64_t so = 0, ro = 0;
+  std::vector<int64_t> soff(g_world), roff(g_world);
+  for (int j = 0; j < g_world; ++j) {
+    if (send_counts[j] < 0 || recv_counts[j] < 0) return fail(DSSM_E_INVALID, "dssm_all_to_allv: negative count");
+    soff[j] = so;
+    roff[j] = ro;
+    so += send_counts[j];
+    ro += recv_counts[j];
+  }
+  if (send_counts[g_rank] != recv_counts[g_rank]) return fail(DSSM_E_INVALID, "dssm_all_to_allv: own counts differ");
+  if (send_counts[g_rank])
+    HIP_TRY(device_copy(rp + (size_t)roff[g_rank] * es, sp + (size_t)soff[g_rank] * es,
+                        (size_t)send_counts[g_rank] * es, s, false));
+  RCCL_TRY(ncclGroupStart());
+  for (int j = 0; j < g_world; ++j) {
+    if (j == g_rank) continue;
+    ncclResult_t r = ncclSuccess;
+    if (send_counts[j]) r = ncclSend(sp + (size_t)soff[j] * es, (size_t)send_counts[j], t, j, g_comm, s);
+    if (r == ncclSuccess && recv_counts[j]) r = ncclRecv(rp + (size_t)roff[j] * es, (size_t)recv_counts[j], t, j, g_comm, s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return fail(DSSM_E_RCCL, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    }
+  }
+  if (tail && tail_count) {
+    ncclResult_t r = ncclAllReduce(tail, tail, (size_t)tail_count, tt, ncclSum, g_comm, s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return fail(DSSM_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
+  }
+  RCCL_TRY(ncclGroupEnd());
+  return DSSM_OK;
 }
 
 // ---- the data-parallel step graph (include/dssm.h dssm_plan_graph_build_dp_steps) -----------

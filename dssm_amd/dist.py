@@ -52,7 +52,9 @@ def _dtype_id(t: torch.Tensor) -> int:
         return _lib.DSSM_F32
     if t.dtype == torch.bfloat16:
         return _lib.DSSM_BF16
-    raise TypeError(f"collectives move fp32 / bf16 tensors, not {t.dtype}")
+    if t.dtype == torch.int32:
+        return _lib.DSSM_I32
+    raise TypeError(f"collectives move fp32 / bf16 / int32 tensors, not {t.dtype}")
 
 
 class TorchTransport:
@@ -102,6 +104,13 @@ class TorchTransport:
 
     def all_to_all(self, send, recv):
         self._host(lambda s, r: dist.all_to_all_single(r, s), send, recv)
+
+    def all_to_allv(self, send, send_counts, recv, recv_counts, tail=None):
+        """send_counts[j] elements of send to rank j, recv_counts[j] from rank j; tail all-reduced."""
+        self._host(lambda s, r: dist.all_to_all_single(r, s, output_split_sizes=list(recv_counts),
+                                                       input_split_sizes=list(send_counts)), send, recv)
+        if tail is not None:
+            self.all_reduce(tail)
 
     def info(self) -> dict:
         ver = None
@@ -160,6 +169,15 @@ class LibTransport:
         assert send.numel() == recv.numel() and send.numel() % self.world == 0
         check(self.lib.dssm_all_to_all(ptr(send), ptr(recv), send.numel() // self.world, _dtype_id(send),
                                        stream_ptr()), "all_to_all")
+
+    def all_to_allv(self, send, send_counts, recv, recv_counts, tail=None):
+        """dssm_all_to_allv: grouped sends / receives of per-peer counts, the tail's all-reduce in the
+        same RCCL group."""
+        W = self.world
+        sc, rc = (C.c_int64 * W)(*send_counts), (C.c_int64 * W)(*recv_counts)
+        tp, tn, td = (ptr(tail), tail.numel(), _dtype_id(tail)) if tail is not None else (None, 0, 0)
+        check(self.lib.dssm_all_to_allv(ptr(send), sc, ptr(recv), rc, _dtype_id(send), tp, tn, td, stream_ptr()),
+              "all_to_allv")
 
     def info(self) -> dict:
         """The communicator as RCCL reports it (dssm_comm_info): its rank count, this rank, version."""
@@ -268,11 +286,17 @@ class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
     def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto", chunks: int = 1,
-                 overlap: bool = False):
+                 overlap: bool = False, sparse: bool = False):
         """comm: "auto" (the library's RCCL communicator on GPUs, torch.distributed as the
         self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
         zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
-        fallback taken is listed in .fallbacks and warned about."""
+        fallback taken is listed in .fallbacks and warned about.
+        sparse (zero / bf16 wire, one chunk): the touched-row gradient exchange -- each rank sends
+        to rank j only the W1 gradient rows of j's shard its batch touched (packed with their row
+        ids; the counts exchanged first), the fp32 tail's all-reduce in the same RCCL group; the
+        receiver scatters them into the zeroed stage, so Adam sums exactly the dense exchange's
+        values.  The counts are known only on the host after the batch is read, so this exchange runs
+        between captured graphs (never inside one)."""
         if overlap:  # removed in round 3 (DESIGN §6): slower; refused before any side effect
             raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
         self.model = model
@@ -313,9 +337,17 @@ class DataParallel:
             self.extent, self.sub = geo["extent"], geo["sub"]
             self.begin, self.end = geo["shard_begin"], geo["shard_end"]
             self.shard = self.chunks * self.sub  # W1 elements per rank (the last rank's padded)
+            self.rows = geo["rows"]              # W1 rows per rank and chunk
+            self.width = self.sub // self.rows   # W1 row length on the wire
         elif self.mode == "zero":
             self.begin, self.end, self.shard = shard_bounds(npad, model.n_params, self.rank, self.world)
             model.set_adam_range(self.begin, max(self.begin, self.end))
+        self.sparse = bool(sparse)
+        if self.sparse and not (self.mode == "zero" and self.wire == "bf16" and self.chunks == 1):
+            raise ValueError("sparse exchange: the zero schedule with the bf16 wire in one chunk")
+        self._staged_indices = None
+        self._cur = None
+        self.sparse_stats = {"steps": 0, "rows_sent": 0, "rows_dense": 0}
 
     @property
     def comm(self) -> str:
@@ -325,6 +357,8 @@ class DataParallel:
     def schedule(self) -> str:
         """What the exchange runs, e.g. "zero/bf16 via rccl" (bench.py's config.dp_exchange)."""
         s = f"{self.mode}/{self.wire}" if self.mode == "zero" else self.mode
+        if getattr(self, "sparse", False):
+            s += " sparse"
         return f"{s} via {self.comm}"
 
     def _transport(self, comm: str, strict_mode: bool):
@@ -346,10 +380,46 @@ class DataParallel:
         return tx
 
     # ---- collectives ----------------------------------------------------------------------
+    def _sparse_exchange(self):
+        """The touched-row gradient all-to-all (see __init__): this rank's batch's W1 rows (the
+        columns its CSR holds, torch.unique) split by owner rank, packed with their ids
+        (dssm_rows_pack_u16), the counts all-to-all'd, the packed rows exchanged with the tail's
+        all-reduce in one group, and scattered into the zeroed stage (dssm_rows_unpack_u16)."""
+        m, W = self.model, self.world
+        ids = m.touched_rows(*(self._cur or ()))  # ascending W1 rows the batch touched (int32)
+        S, n, dev = self.rows, self.width, ids.device
+        cut = torch.searchsorted(ids, torch.arange(1, W, device=dev, dtype=torch.int32) * S)
+        bounds = torch.cat([torch.zeros(1, dtype=cut.dtype, device=dev), cut,
+                            torch.full((1,), ids.numel(), dtype=cut.dtype, device=dev)])
+        send_rows = (bounds[1:] - bounds[:-1]).to(torch.int32)
+        recv_rows = torch.empty_like(send_rows)
+        self.tx.all_to_all(send_rows, recv_rows)
+        sc, rc = send_rows.tolist(), recv_rows.tolist()  # the sizes, on the host (sync)
+        stride = n + 4
+        sbuf = torch.empty(max(1, ids.numel()) * stride, dtype=torch.bfloat16, device=dev)
+        m.rows_pack(self.grad_wire, n, ids, sbuf)
+        rbuf = torch.empty(max(1, sum(rc)) * stride, dtype=torch.bfloat16, device=dev)
+        g = m.grads
+        self.tx.all_to_allv(sbuf, [c * stride for c in sc], rbuf, [c * stride for c in rc],
+                            tail=g[self.extent:m.n_params])
+        self.stage.zero_()
+        off = 0
+        for i in range(W):  # stage block i: rank i's gradient rows of this rank's shard
+            dst = self.stage[i * self.sub:(i + 1) * self.sub]
+            m.rows_unpack(rbuf[off * stride:(off + rc[i]) * stride], n, rc[i], self.rank * S, S, dst)
+            off += rc[i]
+        st = self.sparse_stats
+        st["steps"] += 1
+        st["rows_sent"] += ids.numel()
+        st["rows_dense"] += W * S
+
     def exchange_before_adam(self):
         if self.world == 1:
             return
         g = self.model.grads
+        if self.sparse:
+            self._sparse_exchange()
+            return
         if self.mode != "zero":
             self.tx.all_reduce(g)
         elif self.wire == "bf16":
@@ -407,7 +477,8 @@ class DataParallel:
     def capturable(self) -> bool:
         """Whole steps, collectives included, can be captured into one graph: the library's RCCL
         transport with the zero / bf16-wire schedule (dssm_plan_graph_build_dp_steps)."""
-        return getattr(self.tx, "capturable", False) and self.mode == "zero" and self.wire == "bf16"
+        return (getattr(self.tx, "capturable", False) and self.mode == "zero" and self.wire == "bf16"
+                and not self.sparse)
 
     def build_region(self, batches, probes: bool = False) -> int:
         """len(batches) whole data-parallel steps as ONE graph, every node on one captured stream:
@@ -442,6 +513,8 @@ class DataParallel:
         self._g_adam = m.graph_build(_lib.GRAPH_ADAM, 1.0 / self.world, probes=probe_batch is not None)
         self._g_shadow = m.graph_build(shadow) if shadow else None
         self._shadows_pending = False
+        # the sparse exchange reads the replayed step's batch: its indices and nnz, known once here
+        self._staged_indices = [(ix, int(ip[-1].item())) for ip, ix, _ in staged] if self.sparse else None
 
     def graph_step(self, i: int, events=None):
         """One step on staged batch i (mod the staged count) from the captured graphs.  events: a
@@ -459,7 +532,10 @@ class DataParallel:
             b.record()
             events.append((name, a, b))
         timed("fwd_bwd", lambda: m.graph_launch((self._g_merged if self._shadows_pending else self._g_plain)[i % n]))
+        if self._staged_indices is not None:
+            self._cur = self._staged_indices[i % n]
         timed("exchange_before_adam", self.exchange_before_adam)
+        self._cur = None
         timed("adam", lambda: m.graph_launch(self._g_adam))
         if self.mode == "zero":
             timed("exchange_after_adam", self.exchange_after_adam)

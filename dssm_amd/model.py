@@ -267,6 +267,25 @@ class DSSM:
                                              ptr(stage), ptr(param_wire), n), "set_dp_wire")
         self._wires = (grad_wire, stage, param_wire)
 
+    # ---- the touched-row sparse exchange (dssm_amd/dist.py DataParallel(sparse=True)) ----------
+    def touched_rows(self, indices=None, nnz=None) -> torch.Tensor:
+        """Ascending W1 rows (trigram columns) the current batch -- or (indices, nnz) -- touches: the
+        rows whose gradient can be non-zero (int32, on the device)."""
+        if indices is None:
+            ip, indices, _ = self._batch_refs
+            nnz = int(ip[-1].item())
+        return torch.unique(indices[:nnz]).to(torch.int32)
+
+    def rows_pack(self, src, n: int, rows, out, stream=None):
+        """dssm_rows_pack_u16: packed bf16 rows (stride n + 4, the row id in front) of src rows."""
+        check(self.lib.dssm_rows_pack_u16(ptr(src), n, ptr(rows), rows.numel(), ptr(out), stream_ptr(stream)),
+              "rows_pack")
+
+    def rows_unpack(self, packed, n: int, count: int, row_base: int, nrows: int, dst, stream=None):
+        """dssm_rows_unpack_u16: packed rows back into dst rows (id - row_base)."""
+        check(self.lib.dssm_rows_unpack_u16(ptr(packed), n, count, row_base, nrows, ptr(dst),
+                                            stream_ptr(stream)), "rows_unpack")
+
     def dp_geometry(self) -> Dict[str, int]:
         """The wire layout (dssm_plan_dp_geometry): world, chunks, rows per sub-chunk, elements per
         rank and chunk ('sub'), this rank's W1 shard [shard_begin, shard_end) in the arena, the wire

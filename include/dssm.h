@@ -33,7 +33,7 @@ extern "C" {
 #define DSSM_MAX_LAYERS 8
 
 enum { DSSM_OK = 0, DSSM_E_INVALID = -1, DSSM_E_HIP = -2, DSSM_E_RCCL = -3, DSSM_E_UNSUPPORTED = -4 };
-enum { DSSM_F32 = 0, DSSM_BF16 = 1 };
+enum { DSSM_F32 = 0, DSSM_BF16 = 1, DSSM_I32 = 2 /* collectives only */ };
 
 /* Model/step configuration (semantic_matching/dssm/config.py:19-28 + new_dssm.py constants). */
 typedef struct dssm_config {
@@ -512,7 +512,22 @@ int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
 int dssm_reduce_scatter_sum(const void* send, void* recv, int64_t count, int dtype, void* stream);
 int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void* stream);
 int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream);
+/* Variable-count all-to-all (the touched-row sparse gradient exchange, dssm_amd/dist.py
+ * DataParallel(sparse=True)): send_counts[j] elements of send (consecutive, in rank order) go to
+ * rank j, recv_counts[j] elements of recv come from rank j (host arrays of world entries; the own
+ * entries equal).  tail != NULL: tail_count elements of tail summed over the ranks in place
+ * (all-reduce) in the same RCCL group.  Replaces the dense all-to-all + tail all-reduce of the
+ * zero schedule (new_dssm.py:215-217's gradient application, sharded). */
+int dssm_all_to_allv(const void* send, const int64_t* send_counts, void* recv, const int64_t* recv_counts,
+                     int dtype, void* tail, int64_t tail_count, int tail_dtype, void* stream);
 int dssm_comm_destroy(void);
+/* Packed rows of the sparse exchange, stride n + 4 u16: [row id int32][pad][n u16 of src row id].
+ * pack: packed row k from src row rows[k] (n % 4 == 0); unpack: dst row (id - row_base) = packed row
+ * k's data for ids in [row_base, row_base + nrows) (others skipped). */
+int dssm_rows_pack_u16(const uint16_t* src, int64_t n, const int32_t* rows, int64_t count, uint16_t* out,
+                       void* stream);
+int dssm_rows_unpack_u16(const uint16_t* in, int64_t n, int64_t count, int64_t row_base, int64_t nrows,
+                         uint16_t* dst, void* stream);
 
 /* ---- host data path (utils/utils.py:20-24, 45-61, 368-437; new_dssm.py:26-49) ---------------
  * Host memory only (no device pointers) except the feeder's outputs. */

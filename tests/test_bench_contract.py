@@ -67,9 +67,9 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     class FakeChild:
         def __init__(self, cmd, env=None, stdout=None, text=None):
             seen.append((cmd, env))
+            exch = {1: "zero/bf16 via rccl", 2: "allreduce via rccl"}.get(len(seen), "zero/bf16 sparse via rccl")
             head = {"value": 1.0, "ms_per_step": 2.0, "steps": 20, "warmup": 5, "unit": "pairs/s",
-                    "config": {"dp_exchange": "zero/bf16 via rccl" if len(seen) == 1 else "allreduce via rccl"},
-                    "dp_kernels_ms": {"adam": 0.05}}
+                    "config": {"dp_exchange": exch}, "dp_kernels_ms": {"adam": 0.05}}
             self.stdout = io.StringIO("progress\n" + json.dumps(head) + "\n") if stdout is not None else None
             self.rc = 7 if stdout is None else 0
 
@@ -89,19 +89,22 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
     assert cmd[-8:] == ["--gpus", "8", "--steps", "20", "--warmup", "5", "--dp-alt", "0"]
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
-    # default: the headline child, then the allreduce / fp32-wire child; one merged line
+    # default: the headline child, then the allreduce / fp32-wire child and the sparse-exchange
+    # child; one merged line
     seen.clear()
     capsys.readouterr()
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
     assert bench.spawn_ranks(bench.parse()) == 0
-    assert len(seen) == 2
+    assert len(seen) == 3
     assert seen[0][0][-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
-    assert seen[1][0][-6:] == ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0"]
+    assert seen[1][0][-8:] == ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0", "--dp-alt-sparse", "0"]
+    assert seen[2][0][-6:] == ["--dp-sparse", "1", "--dp-alt", "0", "--dp-alt-sparse", "0"]
     lines = [x for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["config"]["dp_exchange"] == "zero/bf16 via rccl"
     assert d["dp_alt"]["dp_exchange"] == "allreduce via rccl" and d["dp_alt"]["dp_kernels_ms"] == {"adam": 0.05}
+    assert d["dp_alt_sparse"]["dp_exchange"] == "zero/bf16 sparse via rccl"
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--backend", "gloo"])
     assert bench.parse().comm == "torch"
 

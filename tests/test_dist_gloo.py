@@ -96,6 +96,23 @@ class CpuEngine:
     def set_batch(self, batch):
         self.batch = batch.as_dict()
 
+    # the touched-row sparse exchange's model hooks (dssm_amd/model.py DSSM.touched_rows / rows_pack /
+    # rows_unpack; packed rows of stride n + 4 with the int32 row id in front)
+    def touched_rows(self, indices=None, nnz=None):
+        ix = self.batch["indices"] if indices is None else indices[:nnz]
+        return torch.from_numpy(np.unique(np.asarray(ix)).astype(np.int32))
+
+    def rows_pack(self, src, n, rows, out):
+        k = rows.numel()
+        o = out[:k * (n + 4)].view(k, n + 4)
+        o[:, 4:] = src.view(-1, n)[rows.long()]
+        o.view(torch.int32)[:, 0] = rows
+
+    def rows_unpack(self, packed, n, count, row_base, nrows, dst):
+        pk = packed[:count * (n + 4)].view(count, n + 4)
+        ids = pk.view(torch.int32)[:, 0].long() - row_base
+        dst.view(-1, n)[ids] = pk[:, 4:]
+
     def forward(self, train=True):
         self._train = bool(train)
 
@@ -143,7 +160,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, port, out_dir, mode, wire, world, chunks):
+def _worker(rank, port, out_dir, mode, wire, world, chunks, sparse=False):
     os.environ["OMP_NUM_THREADS"] = "1" if world >= 8 else "2"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -151,7 +168,7 @@ def _worker(rank, port, out_dir, mode, wire, world, chunks):
         p0 = O.init_params(cfg, seed=9)
         glob = synth_batch(D, BS, NEG, seed=1234, mean_nnz=16)
         eng = CpuEngine(p0, world)
-        dp = DataParallel(eng, comm="auto", mode=mode, wire=wire, chunks=chunks)
+        dp = DataParallel(eng, comm="auto", mode=mode, wire=wire, chunks=chunks, sparse=sparse)
         assert dp.world == world and dp.rank == rank and dp.mode == mode and dp.comm == "torch"
         assert dp.wire == (wire if mode == "zero" else "fp32")
         eng.set_batch(shard_batch(glob, BS, NEG, rank, world))
@@ -165,17 +182,31 @@ def _worker(rank, port, out_dir, mode, wire, world, chunks):
         dist.destroy_process_group()
 
 
+def test_sparse_exchange_equals_dense():
+    """The touched-row sparse exchange (DataParallel(sparse=True)) delivers exactly the dense
+    all-to-all's stage: world 4, parameters and Adam slots bit-identical to the dense bf16 wire."""
+    out = {}
+    for sparse in (False, True):
+        with tempfile.TemporaryDirectory() as d:
+            mp.spawn(_worker, args=(_free_port(), d, "zero", "bf16", 4, 1, sparse), nprocs=4, join=True)
+            out[sparse] = [np.load(os.path.join(d, f"{x}0.npy")) for x in ("p", "m")]
+    for a, b in zip(out[False], out[True]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("mode,wire,chunks", [("allreduce", "fp32", 1), ("zero", "fp32", 1), ("zero", "bf16", 1),
-                                              ("zero", "bf16", 3)])
+                                              ("zero", "bf16", 3), ("zero", "bf16-sparse", 1)])
 def test_data_parallel_gloo(mode, wire, chunks, world):
     """allreduce: all-reduce + replicated Adam; zero: Adam on the rank's shard + all-gather of the
     parameters, W1's rows on an fp32 (reduce-scatter) or a bf16 all-to-all wire. All must give
     the same step (the bf16 wire within Adam's insensitivity to gradient rounding: a first step
     moves each element by lr * sign(g) wherever |g| >> eps)."""
     WORLD = world
+    sparse = wire == "bf16-sparse"
+    wire = "bf16" if sparse else wire
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d, mode, wire, world, chunks), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, mode, wire, world, chunks, sparse), nprocs=WORLD, join=True)
         p = [np.load(os.path.join(d, f"p{r}.npy")) for r in range(WORLD)]
         m_ = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(WORLD)]
         ema = [np.load(os.path.join(d, f"ema{r}.npy")) for r in range(WORLD)]

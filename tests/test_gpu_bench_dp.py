@@ -49,6 +49,12 @@ def test_bench_gpus2_spawns_ranks_and_checks_them():
     assert alt["dp_exchange"] == "allreduce via torch" and alt["value"] > 0
     assert alt["dp_check"]["ranks_identical"] is True and alt["dp_check"]["world"] == 2
     assert alt["dp_kernels_ms"]["exchange_before_adam"] > 0
+    # the third child: the touched-row sparse gradient all-to-all (DataParallel(sparse=True))
+    sp = d["dp_alt_sparse"]
+    assert "error" not in sp, sp
+    assert sp["dp_exchange"] == "zero/bf16 sparse via torch" and sp["value"] > 0
+    assert sp["dp_check"]["ranks_identical"] is True and sp["dp_check"]["world"] == 2
+    assert 0 < sp["dp_sparse"]["rows_sent_frac"] < 1 and sp["dp_sparse"]["steps"] >= 4
 
 
 @pytest.mark.gpu

@@ -41,7 +41,7 @@ pytestmark = pytest.mark.gpu
 
 D, WIDTHS, BS, NEG, WORLD = 30000, [300, 300, 128], 1024, 4, 2
 LR = 0.01
-SCHEDULES = [("zero", "bf16"), ("zero", "fp32"), ("allreduce", "fp32")]
+SCHEDULES = [("zero", "bf16"), ("zero", "bf16-sparse"), ("zero", "fp32"), ("allreduce", "fp32")]
 
 
 def _global_batch(step):
@@ -75,7 +75,9 @@ def _worker(rank, port, out_dir, mode, wire):
         m = _model()
         with np.load(os.path.join(out_dir, "state0.npz")) as z:
             _load(m, {k: z[k] for k in z.files})
-        dp = DataParallel(m, comm="auto", mode=mode, wire=wire)
+        sparse = wire == "bf16-sparse"  # the touched-row sparse gradient all-to-all
+        wire = "bf16" if sparse else wire
+        dp = DataParallel(m, comm="auto", mode=mode, wire=wire, sparse=sparse)
         assert (dp.world, dp.rank, dp.mode, dp.wire, dp.comm) == (WORLD, rank, mode, wire, "torch"), dp.schedule
         assert not dp.fallbacks, dp.fallbacks
         # step 1: eager
@@ -141,10 +143,11 @@ def _bf16(x):
 
 
 def _exchanged(gs, mode, wire, ext):
-    """The gradient the rank's Adam sees (before its 1/world scale): the exchange emulated."""
+    """The gradient the rank's Adam sees (before its 1/world scale): the exchange emulated (the
+    sparse exchange delivers the dense one's values: untouched rows are zero)."""
     g = np.zeros_like(gs[0])
     for gr in gs:  # fp32 sums in rank order
-        if mode == "zero" and wire == "bf16":
+        if mode == "zero" and wire in ("bf16", "bf16-sparse"):
             g[:ext] += _bf16(gr[:ext])
             g[ext:] += gr[ext:]
         else:

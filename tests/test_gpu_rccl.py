@@ -100,6 +100,55 @@ def test_collectives_captured_in_graph(tx):
         assert torch.equal(a, ra) and torch.equal(b, rb) and torch.equal(out, rc)
 
 
+def test_sparse_exchange_pieces_world1(tx):
+    """The touched-row sparse exchange's library pieces at world 1: dssm_rows_pack_u16 /
+    dssm_rows_unpack_u16 against torch indexing (bit-exact bf16 rows, the int32 id in front), and
+    dssm_all_to_allv (the own part's device copy, int32 counts, the tail's all-reduce in the same
+    RCCL group), eager and captured in a hipGraph."""
+    from dssm_amd import _lib
+    from dssm_amd.model import DSSM
+    m = DSSM(500, (300, 64), 8, 4, dtype="bf16")
+    n, rows_all = 300, 400
+    g = torch.Generator(device="cuda").manual_seed(5)
+    src = torch.randn(rows_all * n, device="cuda", generator=g).to(torch.bfloat16)
+    ids = torch.unique(torch.randint(0, rows_all, (150,), device="cuda", generator=g)).to(torch.int32)
+    k = ids.numel()
+    packed = torch.zeros(k * (n + 4), dtype=torch.bfloat16, device="cuda")
+    m.rows_pack(src, n, ids, packed)
+    pk = packed.view(k, n + 4)
+    assert torch.equal(pk.view(torch.int32)[:, 0], ids)
+    assert torch.equal(pk[:, 4:], src.view(-1, n)[ids.long()])
+    # unpack the ids in [100, 300) into a 200-row block (others skipped)
+    dst = torch.zeros(200 * n, dtype=torch.bfloat16, device="cuda")
+    m.rows_unpack(packed, n, k, 100, 200, dst)
+    want = torch.zeros(200, n, dtype=torch.bfloat16, device="cuda")
+    sel = ids[(ids >= 100) & (ids < 300)].long()
+    want[sel - 100] = src.view(-1, n)[sel]
+    assert torch.equal(dst.view(200, n), want)
+    # all_to_allv at world 1: the own part copied, the tail summed over one rank (unchanged)
+    recv = torch.zeros_like(packed)
+    tail = torch.randn(1000, device="cuda", generator=g)
+    tail0 = tail.clone()
+    cnt = torch.tensor([7], dtype=torch.int32, device="cuda")
+    cnt_r = torch.zeros_like(cnt)
+    tx.all_to_all(cnt, cnt_r)
+    assert int(cnt_r.item()) == 7
+    tx.all_to_allv(packed, [packed.numel()], recv, [packed.numel()], tail=tail)
+    torch.cuda.synchronize()
+    assert torch.equal(recv, packed) and torch.equal(tail, tail0)
+    s = torch.cuda.Stream()
+    recv.zero_()
+    s.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=s):
+        tx.all_to_allv(packed, [packed.numel()], recv, [packed.numel()], tail=tail)
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(recv, packed) and torch.equal(tail, tail0)
+    bad = (_lib.load().dssm_rows_pack_u16(0, 6, 0, 1, 0, 0))
+    assert bad != 0  # n not a multiple of 4: refused
+
+
 def test_strict_rccl_without_nccl_backend_raises():
     """comm="rccl" is strict: under a backend other than nccl (here: the module's gloo group, if
     still initialised, else a fresh one) the library transport is not a candidate and the
