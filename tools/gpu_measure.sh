@@ -16,7 +16,8 @@ for dt in ${DTYPES:-bf16 fp32}; do
       -- $B --dtype $dt --steps 16 --warmup 3 --graph 0 --probes 0 --fwd-only 0 > gpurun_out/m/pmc_${dt}_$c.log 2>&1
     echo "pmc $dt $c ok"
   done
-  M=SQ_INSTS_VALU_MFMA_MOPS_BF16; [ $dt = fp32 ] && M=SQ_INSTS_VALU_MFMA_MOPS_F32
+  # fp32: the split tiles run bf16 MFMAs (csrc/g32.h), the exact build f32 ones: count both
+  M=SQ_INSTS_VALU_MFMA_MOPS_BF16; [ $dt = fp32 ] && M="SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16"
   timeout -k 10 300 rocprofv3 --pmc $M SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d gpurun_out/m/mfma_$dt -o run \
     -- $B --dtype $dt --steps 16 --warmup 3 --graph 0 --probes 0 --fwd-only 0 > gpurun_out/m/mfma_$dt.log 2>&1

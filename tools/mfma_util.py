@@ -46,6 +46,11 @@ def main(root, stats_csv, out, dtype="bf16", model=None):
         res["_workload"]["model"] = model
     for k, c in vals.items():
         mops = c.get(mops_name, [])
+        split = False
+        if dtype == "fp32" and (not mops or sum(mops) == 0) and sum(c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", [])) > 0:
+            # fp32 parity mode's split tiles (csrc/g32.h DSSM_G32_SPLIT): six bf16 partial products per
+            # fp32 product on the bf16 matrix cores
+            mops, split = c["SQ_INSTS_VALU_MFMA_MOPS_BF16"], True
         if not mops or sum(mops) == 0:
             continue
         n = len(mops)
@@ -56,9 +61,14 @@ def main(root, stats_csv, out, dtype="bf16", model=None):
              "grbm_gui_active": int(gui)}
         if k in dur:
             tf = flops / (dur[k] * 1e-9) / 1e12
-            e.update({"avg_us": round(dur[k] / 1e3, 2), "tflops": round(tf, 2),
-                      "peak_tflops": PEAK_TFLOPS[dtype], "frac_of_peak": round(tf / PEAK_TFLOPS[dtype], 5),
-                      "mfma_busy": round(busy / (SIMDS * CLOCK_HZ * dur[k] * 1e-9), 4)})
+            e.update({"avg_us": round(dur[k] / 1e3, 2), "mfma_busy": round(busy / (SIMDS * CLOCK_HZ * dur[k] * 1e-9), 4)})
+            if split:  # executed bf16 rate against the bf16 peak; the fp32 products (1 per 6) against fp32's
+                e.update({"split_bf16x6": True, "bf16_tflops_executed": round(tf, 2), "bf16_peak_tflops": PEAK_TFLOPS["bf16"],
+                          "bf16_frac_of_peak": round(tf / PEAK_TFLOPS["bf16"], 5), "tflops": round(tf / 6, 2),
+                          "peak_tflops": PEAK_TFLOPS["fp32"], "frac_of_peak": round(tf / 6 / PEAK_TFLOPS["fp32"], 5)})
+            else:
+                e.update({"tflops": round(tf, 2), "peak_tflops": PEAK_TFLOPS[dtype],
+                          "frac_of_peak": round(tf / PEAK_TFLOPS[dtype], 5)})
         res[k] = e
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, v in sorted(res.items()):
