@@ -483,21 +483,30 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
                                                          int loss_blocks,
                                                          float* __restrict__ loss_out,
                                                          int nwork, typename ApplyDw<TO>::P dw,
-                                                         int dw_x, int dw_y, int dw_blocks) {
+                                                         int dw_x, int dw_y, int dw_blocks,
+                                                         typename ApplyDw<TO>::P dw2, int dw2_x, int dw2_y,
+                                                         int dw2_blocks) {
   __shared__ __attribute__((aligned(16))) float smem[apply_smem_floats<TO>()];
   // blocks [0, dw_blocks): the previous backward pair's dW split-K tiles (the longest chains,
-  // first in dispatch order); they read dZ of the layer above and the forward's activations, so
-  // they are independent of this launch's own work
-  if ((int)blockIdx.x < dw_blocks) {
+  // first in dispatch order), then [dw_blocks, + dw2_blocks) a second pair's (the one before it,
+  // when that pair's BN-backward apply was folded into the next pair: BNB_IN_PAIR); they read dZ of
+  // the layers above and the forward's activations, so they are independent of this launch's work
+  if ((int)blockIdx.x < dw_blocks + dw2_blocks) {
     // XCD-grouped: the tiles of one batch-row chunk share its A / dZ sub-panels through one L2
 #ifndef DSSM_XCD_DW_APPLY
 #define DSSM_XCD_DW_APPLY 1
 #endif
-    const int r = DSSM_XCD_DW_APPLY ? xcd_tile(blockIdx.x, dw_blocks) : (int)blockIdx.x;
-    ApplyDw<TO>::run(dw, r, dw_x, dw_y, smem);
+    if ((int)blockIdx.x < dw_blocks) {
+      const int r = DSSM_XCD_DW_APPLY ? xcd_tile(blockIdx.x, dw_blocks) : (int)blockIdx.x;
+      ApplyDw<TO>::run(dw, r, dw_x, dw_y, smem);
+    } else {
+      const int b2 = (int)blockIdx.x - dw_blocks;
+      const int r = DSSM_XCD_DW_APPLY ? xcd_tile(b2, dw2_blocks) : b2;
+      ApplyDw<TO>::run(dw2, r, dw2_x, dw2_y, smem);
+    }
     return;
   }
-  const int bid = (int)blockIdx.x - dw_blocks;
+  const int bid = (int)blockIdx.x - dw_blocks - dw2_blocks;
   // one extra block past the element blocks: the step's loss / accuracy from the cosine kernel's
   // partials (deferred finalize: no cross-workgroup ticket in the cosine launch) and dgamma /
   // dbeta, off the element blocks' critical path
@@ -658,26 +667,31 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 template <typename TO>
 static hipError_t apply_fused(const float* Z, const float* dA, const BnSide& b, TO* dZ, hipStream_t s,
                               const float* loss_part, int loss_blocks, float* loss_out,
-                              const typename ApplyDw<TO>::P* dw, int max_kps) {
-  if (b.ld > kApplyMaxLd || (b.ld % 4)) return hipErrorInvalidValue;
+                              const typename ApplyDw<TO>::P* dw, int max_kps,
+                              const typename ApplyDw<TO>::P* dw2 = nullptr) {
+  if (b.ld > kApplyMaxLd || (b.ld % 4) || (dw2 && !dw)) return hipErrorInvalidValue;
   // element workgroups: fewer beside hosted dW tiles, which share the CUs
 #ifndef DSSM_APPLY_GRID_DW
 #define DSSM_APPLY_GRID_DW 512
 #endif
   const int grid = std::min(ew_grid((size_t)(b.rows_q + b.rows_d) * (b.ld / 4)), dw ? DSSM_APPLY_GRID_DW : 1024);
-  if (dw && dw->k_per_split > max_kps) return hipErrorInvalidValue;
+  if ((dw && dw->k_per_split > max_kps) || (dw2 && dw2->k_per_split > max_kps)) return hipErrorInvalidValue;
   const typename ApplyDw<TO>::P p = dw ? *dw : typename ApplyDw<TO>::P{};
+  const typename ApplyDw<TO>::P p2 = dw2 ? *dw2 : typename ApplyDw<TO>::P{};
   const int dw_x = dw ? cdiv(p.N, 64) : 1, dw_y = dw ? cdiv(p.M, 64) : 1;
   const int dw_blocks = dw ? dw_x * dw_y * cdiv(p.K, p.k_per_split) : 0;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fs<TO>, dim3(dw_blocks + grid + 1), dim3(256), 0, s, Z, dA, b, dZ,
-                     loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks);
+  const int dw2_x = dw2 ? cdiv(p2.N, 64) : 1, dw2_y = dw2 ? cdiv(p2.M, 64) : 1;
+  const int dw2_blocks = dw2 ? dw2_x * dw2_y * cdiv(p2.K, p2.k_per_split) : 0;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fs<TO>, dim3(dw_blocks + dw2_blocks + grid + 1), dim3(256), 0, s, Z, dA, b,
+                     dZ, loss_part, loss_blocks, loss_out, grid, p, dw_x, dw_y, dw_blocks, p2, dw2_x, dw2_y,
+                     dw2_blocks);
   return hipGetLastError();
 }
 
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part, int loss_blocks,
-                                     float* loss_out, const TnParams* dw) {
-  return apply_fused<u16>(Z, dA, b, (u16*)dZ, s, loss_part, loss_blocks, loss_out, dw, 3 * 128);  // tn_chunk_body<3>
+                                     float* loss_out, const TnParams* dw, const TnParams* dw2) {
+  return apply_fused<u16>(Z, dA, b, (u16*)dZ, s, loss_part, loss_blocks, loss_out, dw, 3 * 128, dw2);  // tn_chunk_body<3>
 }
 
 hipError_t launch_bn_bwd_apply_fused32(const float* Z, const float* dA, const BnSide& b, float* dZ,

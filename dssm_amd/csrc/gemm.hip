@@ -578,7 +578,7 @@ constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: (32 WM)
 __host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
 // LDS: A / B panels, BN coefficients, then the column-sum reduction.  The LDS epilogue stages a
 // [32 WM][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
-constexpr int kBnbMaxK = 128;          // BN-backward A: K (the last layer's width) it stages
+constexpr int kBnbMaxK = 320;          // BN-backward A: the widest K it stages (instances: 128, 320)
 __host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi, int WM = 4, int coef_rows = 4) {
   const size_t panels = (size_t)(32 * WM + 64) * wk_ldk(Kp) * 2 + (size_t)coef_rows * Kp * 4;
   const size_t epi = (size_t)32 * WM * 68 * 4;
@@ -588,9 +588,11 @@ __host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM 
   return wk_red_offset(Kp, lds_epi, WM, coef_rows) + (size_t)WM * 64 * 2 * 8;
 }
 
-template <bool BN_A, int FS, int WM = 4, bool BNB = false>
+// BNBK > 0: the BN-backward A operand, K <= BNBK (its fp32 dA / Z groups sized for BNBK)
+template <bool BN_A, int FS, int WM = 4, int BNBK = 0>
 __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
                                            u16* wk_smem) {
+  constexpr bool BNB = BNBK > 0;
   constexpr int NT = 128 * WM, ROWS = 32 * WM, BT = NT / 64;  // threads, tile rows, B threads / row
   const int M = a.M, N = a.N, K = a.K, lda = a.lda, ldb = a.ldb, ldc = a.ldc;
   const int Kp = (K + 31) & ~31, LDK = wk_ldk(Kp);
@@ -617,7 +619,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const int arow = t >> 2, ag0 = t & 3;
   const int brow = t / BT, bg0 = t % BT;
   // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
-  constexpr int NGA = BNB ? kBnbMaxK / 32 : kWkMaxG, NGB = (4 * NGA + BT - 1) / BT;
+  constexpr int NGA = BNB ? BNBK / 32 : kWkMaxG, NGB = (4 * NGA + BT - 1) / BT;
   float4 fa[NGA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
   float4 fz[BNB ? NGA : 1][2];  // BNB: the A layer's Z
   uint4 ua[NGA];      // bf16 A groups
@@ -657,7 +659,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
     bcol[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
   }
   float zb[2][2][4], cb[2][4];  // FS == 2: the epilogue's pre-BN values and coefficients
-  if constexpr (FS == 2) {
+  auto load_epi = [&]() {
     const size_t plane = (size_t)2 * ldc;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -673,7 +675,10 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
           zb[i][j][r] = f.zb[(size_t)(m < M ? m : 0) * ldc + (n < N ? n : 0)];
         }
     }
-  }
+  };
+  // with the operands (their latency hidden by the staging); BNB's fp32 panels leave no registers
+  // for them there, so it loads them after the staging (hidden by the MFMA loop)
+  if constexpr (FS == 2 && !BNB) load_epi();
 #ifdef DSSM_WG_TL
   const int tl_slot = FS == 1 ? (a.N == 300 ? 0 : 1) : (a.K == 300 ? 3 : 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -777,6 +782,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
             (bok && kg < ldb) ? ub[i] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
+  if constexpr (FS == 2 && BNB) load_epi();
   __syncthreads();
 #ifdef DSSM_WG_TL
   WG_TL(tl_slot, 3);
@@ -1039,11 +1045,11 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
 // Whole-K backward pair, dA tiles only (the dW_l tiles ride in the next BN-backward apply launch).
 // BNB: the A operand dZ_l formed from dA_l while staging (NtFuse::inb); block nt_blocks: the loss
 // and BN_l's dgamma / dbeta.
-template <int WM, bool BNB = false>
+template <int WM, int BNBK = 0>
 __global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks) {
   extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
   WG_TL(a.K == 300 ? 3 : 2, 0);
-  if constexpr (BNB) {
+  if constexpr (BNBK > 0) {
     if ((int)blockIdx.x >= nt_blocks) {
       if (f.loss_part) loss_reduce(f.loss_part, f.loss_blocks, f.inb.rows_q, f.loss_out);
       fs_materialize_bwd(f.inb);
@@ -1051,7 +1057,7 @@ __global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, i
     }
   }
   const int tile = xcd_tile(blockIdx.x, nt_blocks);
-  nt_wk_body<false, 2, WM, BNB>(a, f, tile % nt_x, tile / nt_x, pw_smem);
+  nt_wk_body<false, 2, WM, BNBK>(a, f, tile % nt_x, tile / nt_x, pw_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1266,8 +1272,12 @@ hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const f
   *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ_out, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
   f.det_rows = cdiv(M, 128);
   if (!det_fits(f, ldda)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_pair_da_wk<4, true>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s, a,
-                     f, nt_x, nt_blocks);
+  if (Kp <= 128)
+    hipLaunchKernelGGL((k_pair_da_wk<4, 128>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s, a,
+                       f, nt_x, nt_blocks);
+  else
+    hipLaunchKernelGGL((k_pair_da_wk<4, kBnbMaxK>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s,
+                       a, f, nt_x, nt_blocks);
   *deferred_splits = (defer && nsplit > 1) ? nsplit : 0;
   return hipGetLastError();
 }

@@ -131,7 +131,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
 // caller then sums the slabs into gw with launch_splitk_reduce.
-// The same for the last layer (n <= 128) with BN_l's backward folded into the A staging: dZ_l
+// The same for layer l (n <= 320) with BN_l's backward folded into the A staging: dZ_l
 // formed from dA_l / Z_l / b's coefficients and backward sums, written bf16 to dZ_out (stride lddz
 // = b.ld); one extra workgroup writes dgamma / dbeta and reduces the deferred loss (loss_part).
 hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const float* Z_l, const BnSide& b,
@@ -188,7 +188,7 @@ hipError_t launch_bn_sums(const float* Z, int ldz, int n, BnTowers t, double* fs
 hipError_t launch_bn_bwd_apply_fused(const float* Z, const float* dA, const BnSide& b, uint16_t* dZ,
                                      hipStream_t s, const float* loss_part = nullptr,
                                      int loss_blocks = 0, float* loss_out = nullptr,
-                                     const TnParams* dw = nullptr);
+                                     const TnParams* dw = nullptr, const TnParams* dw2 = nullptr);
 // fp32 parity mode: dZ stored fp32; the hosted dW tiles are the fp32 ones (g32.h)
 hipError_t launch_bn_bwd_apply_fused32(const float* Z, const float* dA, const BnSide& b, float* dZ,
                                        hipStream_t s, const float* loss_part = nullptr,

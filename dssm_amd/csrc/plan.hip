@@ -369,11 +369,13 @@ struct dssm_plan {
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
   // bf16 fused schedule: the last layer's BN backward inside its dA pair launch (gemm.hip
   // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 128, the dW tiles handed to the next apply)
-  bool bnb_in_pair() const {
-    const int l = Lt.L - 1;
-    return on(DSSM_OPT_BNB_IN_PAIR) && on(DSSM_OPT_DW_IN_APPLY) && Lt.bf16 && Lt.L >= 2 && fused_stats() &&
-           wholek(l) && Lt.n[l] <= 128 && (Lt.BS % 128) == 0 && ((Lt.R - Lt.BS) % 128) == 0;
+  // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 320, the dW tiles handed to the next apply.
+  // The last two layers (>= 1) fold, so the apply launch after them hosts at most two dW tile sets.
+  bool bnb_fold(int l) const {
+    return on(DSSM_OPT_BNB_IN_PAIR) && on(DSSM_OPT_DW_IN_APPLY) && Lt.bf16 && l >= 1 && l >= Lt.L - 2 &&
+           fused_stats() && wholek(l) && Lt.n[l] <= 320 && (Lt.BS % 128) == 0 && ((Lt.R - Lt.BS) % 128) == 0;
   }
+  bool bnb_in_pair() const { return Lt.L >= 2 && bnb_fold(Lt.L - 1); }
   bool fused_stats_ok() const {
     if (Lt.L < 2 || (Lt.BS % 64) || !Lt.sums_bytes) return false;
     for (int l = 0; l < Lt.L; ++l)
@@ -845,35 +847,42 @@ static int backward_impl(dssm_plan* P, void* stream) {
     // BN_{l-1}'s backward sums) + dW_l, and BN_{l-1}'s apply.
     // DW_IN_APPLY: the pair launches run their dA tiles only (one round) and each dW_l's tiles
     // ride in the following apply launch (BN_{l-1}'s), whose element blocks leave CUs idle
-    dssm::TnParams dw{};      // bf16: dW_l's split-K tiles handed from the pair to the next apply
-    dssm::G32Params dw32{};   // fp32: the same for the g32.h tiles
+    // bf16: the dW split-K tile sets handed from the pairs to the next apply (two when the pair in
+    // between folded its BN backward, BNB_IN_PAIR), each with the gradient its slabs are summed into
+    // when not deferred
+    dssm::TnParams dwq[2] = {};
+    float* dwq_reduce[2] = {nullptr, nullptr};
+    int nq = 0;
+    dssm::TnParams dw{};
+    dssm::G32Params dw32{};   // fp32: the same for the g32.h tiles (one set)
     bool dw_pending = false;
     float* dw_reduce_to = nullptr;
     // dW_l's split-K slabs summed later: by the fused Adam step, or by the wire gradient pass
     const bool defer_slabs = P->fused_w1_adam() || wire_gradient_pass(P);
-    const bool bnb = P->bnb_in_pair();
     for (int l = Lt.L - 1; l >= 0; --l) {
       const dssm::BnSide b = P->bn_side(l);
       const bool fin = l == Lt.L - 1;  // the forward's loss, deferred to this launch
       const float* lp = fin ? P->at<float>(Lt.loss_j) : nullptr;
       const int lb = dssm::cosine_blocks(Lt.BS, Lt.n[Lt.L - 1], true);
-      const bool folded = bnb && l == Lt.L - 1;  // BN_l's backward rides in the pair launch below
-      if (folded)
-        ;
-      else if (Lt.bf16)
+      const bool folded = P->bnb_fold(l);  // BN_l's backward rides in the pair launch below
+      if (folded) {
+        // nothing here: the pending dW tile sets wait for the next apply
+      } else if (Lt.bf16) {
         HIP_TRY(dssm::launch_bn_bwd_apply_fused(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                                 P->at<uint16_t>(Lt.dZ[l]), s, lp, lb, P->at<float>(Lt.loss),
-                                                dw_pending ? &dw : nullptr));
-      else
+                                                nq > 0 ? &dwq[0] : nullptr, nq > 1 ? &dwq[1] : nullptr));
+        for (int q = 0; q < nq; ++q)
+          if (dwq_reduce[q])  // not deferred to Adam: the slabs summed right after
+            HIP_TRY(dssm::launch_splitk_reduce(dwq[q].C, (dwq[q].K + dwq[q].k_per_split - 1) / dwq[q].k_per_split,
+                                               (int64_t)dwq[q].M * dwq[q].N, dwq_reduce[q], s));
+        nq = 0;
+      } else {
         HIP_TRY(dssm::launch_bn_bwd_apply_fused32(P->at<float>(Lt.Z[l]), P->at<float>(Lt.dA[l]), b,
                                                   P->at<float>(Lt.dZ[l]), s, lp, lb, P->at<float>(Lt.loss),
                                                   dw_pending ? &dw32 : nullptr));
-      if (dw_pending && dw_reduce_to) {  // not deferred to Adam: the slabs summed right after
-        const float* slab = Lt.bf16 ? dw.C : dw32.C;
-        const int nsplit = Lt.bf16 ? (dw.K + dw.k_per_split - 1) / dw.k_per_split
-                                   : (dw32.K + dw32.k_per_split - 1) / dw32.k_per_split;
-        const int64_t cnt = Lt.bf16 ? (int64_t)dw.M * dw.N : (int64_t)dw32.M * dw32.N;
-        HIP_TRY(dssm::launch_splitk_reduce(slab, nsplit, cnt, dw_reduce_to, s));
+        if (dw_pending && dw_reduce_to)  // not deferred to Adam: the slabs summed right after
+          HIP_TRY(dssm::launch_splitk_reduce(dw32.C, (dw32.K + dw32.k_per_split - 1) / dw32.k_per_split,
+                                             (int64_t)dw32.M * dw32.N, dw_reduce_to, s));
       }
       dw_pending = false;
       dw_reduce_to = nullptr;
@@ -910,6 +919,11 @@ static int backward_impl(dssm_plan* P, void* stream) {
       const float* handed = Lt.bf16 ? dw.C : dw32.C;
       dw_pending = host_dw && handed != nullptr;
       if (dw_pending && !defer_slabs && handed != gw) dw_reduce_to = gw;
+      if (Lt.bf16 && dw_pending) {  // queued for the next apply
+        if (nq == 2) return fail(DSSM_E_INVALID, "internal: more than two pending dW tile sets");
+        dwq[nq] = dw;
+        dwq_reduce[nq++] = dw_reduce_to;
+      }
     }
     return dw1_backward(P, s);
   }
