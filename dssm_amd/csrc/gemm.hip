@@ -578,7 +578,10 @@ constexpr int kWkMaxG = kWkMaxK / 32;  // 8-element A groups per thread: (32 WM)
 __host__ __device__ constexpr int wk_ldk(int Kp) { return Kp + 8; }
 // LDS: A / B panels, BN coefficients, then the column-sum reduction.  The LDS epilogue stages a
 // [32 WM][68] fp32 tile over the panels, so for small K the reduction moves past that tile.
-constexpr int kBnbMaxK = 320;          // BN-backward A: the widest K it stages (instances: 128, 320)
+// BN-backward A: the widest K it stages.  A K <= 320 instance (both hidden layers of C2 folded)
+// measured slower: 18.1 us against 10.3 + 10.15 for the pair and apply it replaced, with 256 VGPRs
+// and spills for the fp32 dA / Z panels, and +3.3 us in the apply that then hosts both dW sets.
+constexpr int kBnbMaxK = 128;
 __host__ __device__ inline size_t wk_red_offset(int Kp, int lds_epi, int WM = 4, int coef_rows = 4) {
   const size_t panels = (size_t)(32 * WM + 64) * wk_ldk(Kp) * 2 + (size_t)coef_rows * Kp * 4;
   const size_t epi = (size_t)32 * WM * 68 * 4;
@@ -1272,12 +1275,8 @@ hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const f
   *dw_out = TnParams{Mw, n, M, A_prev, lda_prev, dZ_out, lddz, nsplit > 1 ? slab : gw, n, 1, kTwKc};
   f.det_rows = cdiv(M, 128);
   if (!det_fits(f, ldda)) return hipErrorInvalidValue;
-  if (Kp <= 128)
-    hipLaunchKernelGGL((k_pair_da_wk<4, 128>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s, a,
-                       f, nt_x, nt_blocks);
-  else
-    hipLaunchKernelGGL((k_pair_da_wk<4, kBnbMaxK>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s,
-                       a, f, nt_x, nt_blocks);
+  hipLaunchKernelGGL((k_pair_da_wk<4, kBnbMaxK>), dim3(nt_blocks + 1), dim3(512), wk_smem_bytes(Kp, 0, 4, 12), s, a,
+                     f, nt_x, nt_blocks);
   *deferred_splits = (defer && nsplit > 1) ? nsplit : 0;
   return hipGetLastError();
 }

@@ -131,7 +131,7 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
 // dw_out (whole-K path): the launch runs the dA tiles only and hands dW_l's split-K tiles (64 x 64,
 // 384-row splits, same slabs) to *dw_out for the next BN-backward apply launch; without defer the
 // caller then sums the slabs into gw with launch_splitk_reduce.
-// The same for layer l (n <= 320) with BN_l's backward folded into the A staging: dZ_l
+// The same for layer l (n <= 128) with BN_l's backward folded into the A staging: dZ_l
 // formed from dA_l / Z_l / b's coefficients and backward sums, written bf16 to dZ_out (stride lddz
 // = b.ld); one extra workgroup writes dgamma / dbeta and reduces the deferred loss (loss_part).
 hipError_t launch_bwd_pair_bnb(int M, int kin, int n, const float* dA_l, const float* Z_l, const BnSide& b,

@@ -369,11 +369,12 @@ struct dssm_plan {
   bool heavy_in_adam() const { return on(DSSM_OPT_HEAVY_IN_ADAM) && csc_rank_path(); }
   // bf16 fused schedule: the last layer's BN backward inside its dA pair launch (gemm.hip
   // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 128, the dW tiles handed to the next apply)
-  // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 320, the dW tiles handed to the next apply.
-  // The last two layers (>= 1) fold, so the apply launch after them hosts at most two dW tile sets.
+  // launch_bwd_pair_bnb: whole-K 128-row tiles, K <= 128, the dW tiles handed to the next apply.
+  // Of the last two layers (>= 1) those <= 128 wide fold, so the apply launch after them hosts at
+  // most two dW tile sets (C2: the last layer; the 300-wide fold measured slower, gemm.hip kBnbMaxK).
   bool bnb_fold(int l) const {
     return on(DSSM_OPT_BNB_IN_PAIR) && on(DSSM_OPT_DW_IN_APPLY) && Lt.bf16 && l >= 1 && l >= Lt.L - 2 &&
-           fused_stats() && wholek(l) && Lt.n[l] <= 320 && (Lt.BS % 128) == 0 && ((Lt.R - Lt.BS) % 128) == 0;
+           fused_stats() && wholek(l) && Lt.n[l] <= 128 && (Lt.BS % 128) == 0 && ((Lt.R - Lt.BS) % 128) == 0;
   }
   bool bnb_in_pair() const { return Lt.L >= 2 && bnb_fold(Lt.L - 1); }
   bool fused_stats_ok() const {
