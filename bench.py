@@ -134,23 +134,38 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run_ranks(args, argv, capture: bool):
+def _run_ranks(args, argv, capture: bool, limit: float = None):
     """One child `torch.distributed.run` of args.gpus ranks (127.0.0.1) running this script with
     argv; its non-JSON output is passed through as it arrives (a long run keeps printing progress),
-    the JSON line(s) rank 0 prints are returned instead of printed when capture is set."""
+    the JSON line(s) rank 0 prints are returned instead of printed when capture is set.  limit
+    (seconds; the alternative-exchange legs): past it the child's own process group (its launcher
+    and ranks) is killed and the leg reported as timed out, so a stuck alternative never holds back
+    the headline line."""
     import signal
     import subprocess
+    import threading
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the only kind the host driver has)
     env.setdefault("OMP_NUM_THREADS", "1")
-    child = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if capture else None, text=True)
+    kw = {"start_new_session": True} if limit else {}
+    child = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if capture else None, text=True, **kw)
 
     def forward(sig, _frame):  # the driver's timeout reaches the ranks too
         child.send_signal(sig)
     for sg in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sg, forward)
+    timer = None
+    if limit:
+        def expire():
+            try:
+                os.killpg(child.pid, signal.SIGKILL)  # the group this Popen started, nothing else
+            except (ProcessLookupError, PermissionError):
+                pass
+        timer = threading.Timer(limit, expire)
+        timer.daemon = True
+        timer.start()
     lines = []
     if capture:
         for line in child.stdout:
@@ -159,7 +174,10 @@ def _run_ranks(args, argv, capture: bool):
             else:
                 sys.stdout.write(line)
                 sys.stdout.flush()
-    return child.wait(), lines
+    rc = child.wait()
+    if timer is not None:
+        timer.cancel()
+    return rc, lines
 
 
 def spawn_ranks(args) -> int:
@@ -173,6 +191,7 @@ def spawn_ranks(args) -> int:
     argv = sys.argv[1:]
     alt = args.dp_alt and args.model == "bow" and args.dp_mode != "allreduce"
     alt_sparse = alt and args.dp_alt_sparse and not args.dp_sparse
+    t_head = time.perf_counter()
     rc, lines = _run_ranks(args, argv, capture=alt)
     if not alt:
         return rc
@@ -184,10 +203,15 @@ def spawn_ranks(args) -> int:
     legs = [("dp_alt", ["--dp-mode", "allreduce", "--wire", "fp32"])]
     if alt_sparse:
         legs.append(("dp_alt_sparse", ["--dp-sparse", "1"]))
+    # each alternative leg gets a wall-clock limit from the headline child's own time
+    limit = max(180.0, 3.0 * (time.perf_counter() - t_head))
     for key, extra in legs:
-        arc, alines = _run_ranks(args, argv + extra + ["--dp-alt", "0", "--dp-alt-sparse", "0"], capture=True)
+        t0 = time.perf_counter()
+        arc, alines = _run_ranks(args, argv + extra + ["--dp-alt", "0", "--dp-alt-sparse", "0"], capture=True,
+                                 limit=limit)
         if arc != 0 or not alines:
-            out[key] = {"error": f"exit {arc}, no line"}
+            late = time.perf_counter() - t0 >= limit
+            out[key] = {"error": f"timed out after {limit:.0f} s" if late else f"exit {arc}, no line"}
             continue
         a = json.loads(alines[-1])
         out[key] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")}

@@ -65,7 +65,7 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     seen = []
 
     class FakeChild:
-        def __init__(self, cmd, env=None, stdout=None, text=None):
+        def __init__(self, cmd, env=None, stdout=None, text=None, **kw):
             seen.append((cmd, env))
             exch = {1: "zero/bf16 via rccl", 2: "allreduce via rccl"}.get(len(seen), "zero/bf16 sparse via rccl")
             head = {"value": 1.0, "ms_per_step": 2.0, "steps": 20, "warmup": 5, "unit": "pairs/s",
@@ -107,6 +107,24 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     assert d["dp_alt_sparse"]["dp_exchange"] == "zero/bf16 sparse via rccl"
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--backend", "gloo"])
     assert bench.parse().comm == "torch"
+
+
+def test_alternative_leg_time_limit(monkeypatch):
+    """An alternative-exchange leg past its wall-clock limit is killed (its own process group) and
+    reported, so a stuck alternative never holds back the headline line."""
+    import subprocess
+    import sys
+    import time
+    real = subprocess.Popen
+
+    def sleeper(cmd, **kw):  # the rank launcher replaced by a child that never finishes
+        return real([sys.executable, "-c", "import time; print('progress', flush=True); time.sleep(120)"], **kw)
+    monkeypatch.setattr(subprocess, "Popen", sleeper)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    args = bench.parse()
+    t0 = time.perf_counter()
+    rc, lines = bench._run_ranks(args, [], capture=True, limit=2.0)
+    assert time.perf_counter() - t0 < 30 and rc != 0 and lines == []
 
 
 def _dp_check_rank(rank, world, port, perturb, q):
