@@ -70,7 +70,11 @@ __device__ __forceinline__ P pick2(P const (&a)[2], int t) {
 }
 
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
+#ifdef DSSM_DIAG_NO_STAT_ATOMICS  // diagnostics (wrong results): plain stores, to time the chains
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // Every storing thread's slab stores drained, then one lane's release + arrival on ticket[tile]:
