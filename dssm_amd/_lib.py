@@ -34,7 +34,8 @@ SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_A
 # dssm_plan_set_option ids (include/dssm.h DSSM_OPT_*)
 OPTIONS = {k: i for i, k in enumerate(["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "SCATTER_IN_COS",
                                          "DW_IN_APPLY", "WIRE_GRAD_PASS", "CSC_RANK", "DETERMINISTIC",
-                                         "FUSED_W1_ADAM", "RANK_IN_ADAM", "MEMCPY_NODES", "BNB_IN_PAIR"])}
+                                         "FUSED_W1_ADAM", "RANK_IN_ADAM", "MEMCPY_NODES", "BNB_IN_PAIR",
+                                         "TAIL_IN_A2A"])}
 
 
 class DssmError(RuntimeError):

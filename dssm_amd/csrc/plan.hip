@@ -255,6 +255,7 @@ struct dssm_plan {
       1,  // RANK_IN_ADAM: multi-step graphs: the next step's CSC rank pass inside this Adam launch
       0,  // MEMCPY_NODES: diagnostics: data-parallel device copies as hipMemcpyAsync nodes
       1,  // BNB_IN_PAIR: the last layer's BN backward formed in the dA pair's A staging
+      0,  // TAIL_IN_A2A: data-parallel graph: the tail's all-reduce in the last all-to-all's RCCL group
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -1781,12 +1782,12 @@ static hipError_t device_copy(void* dst, const void* src, size_t bytes, hipStrea
 }
 
 static int all_to_all_impl(const void* send, void* recv, int64_t count, ncclDataType_t t, size_t es,
-                           hipStream_t s, bool memcpy_node = false) {
+                           hipStream_t s, bool memcpy_node = false, float* tail = nullptr, size_t tail_n = 0) {
   const char* sp = static_cast<const char*>(send);
   char* rp = static_cast<char*>(recv);
   const size_t chunk = (size_t)count * es;
   HIP_TRY(device_copy(rp + (size_t)g_rank * chunk, sp + (size_t)g_rank * chunk, chunk, s, memcpy_node));
-  if (g_world == 1) return DSSM_OK;
+  if (g_world == 1 && !tail) return DSSM_OK;
   RCCL_TRY(ncclGroupStart());
   for (int j = 0; j < g_world; ++j) {
     if (j == g_rank) continue;
@@ -1795,6 +1796,13 @@ static int all_to_all_impl(const void* send, void* recv, int64_t count, ncclData
     if (r != ncclSuccess) {
       ncclGroupEnd();
       return fail(DSSM_E_RCCL, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    }
+  }
+  if (tail && tail_n) {  // the fp32 tail's sum in the same group (plan option TAIL_IN_A2A)
+    ncclResult_t r = ncclAllReduce(tail, tail, tail_n, ncclFloat32, ncclSum, g_comm, s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return fail(DSSM_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
   }
   RCCL_TRY(ncclGroupEnd());
@@ -1871,9 +1879,12 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   const int64_t blk = (int64_t)W * sub;  // chunk's elements in each wire
   const size_t tail = (size_t)(P->Lt.total - P->wire_end());
   float* tg = P->g + P->wire_end();
+  // TAIL_IN_A2A: the last chunk's all-to-all carries the tail's all-reduce in its RCCL group
+  const bool with_tail = kind == 0 && chunk == P->geo.wp - 1 && P->on(DSSM_OPT_TAIL_IN_A2A);
   // bytes this rank sends: all-to-all / all-gather (W-1) * sub bf16; all-reduce (ring) 2(W-1)/W fp32
-  const double bytes = kind == 2 ? 2.0 * (W - 1) / W * tail * 4 : (double)(W - 1) * sub * 2;
-  if (k.mode == 2) {
+  const double tail_bytes = 2.0 * (W - 1) / W * tail * 4;
+  const double bytes = kind == 2 ? tail_bytes : (double)(W - 1) * sub * 2 + (with_tail ? tail_bytes : 0.0);
+  if (k.mode == 2) {  // one fixed cost per launched group
     HIP_TRY(dssm::launch_spin(k.latency_ns + bytes / k.gbps, cs));
     return DSSM_OK;
   }
@@ -1886,7 +1897,7 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
     if (kind == 1) HIP_TRY(device_copy(st, pw, blk * 2, cs, mc));
     return DSSM_OK;
   }
-  if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs, mc);
+  if (kind == 0) return all_to_all_impl(gw, st, sub, ncclBfloat16, 2, cs, mc, with_tail ? tg : nullptr, tail);
   if (kind == 1) RCCL_TRY(ncclAllGather(pw + (int64_t)P->dp_rank * sub, pw, (size_t)sub, ncclBfloat16, g_comm, cs));
   if (kind == 2) RCCL_TRY(ncclAllReduce(tg, tg, tail, ncclFloat32, ncclSum, g_comm, cs));
   return DSSM_OK;
@@ -1961,7 +1972,8 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
       if (c == 0) P->probe_end(DSSM_PROBE_DP_ALL_TO_ALL, s);
     }
     P->probe_begin(DSSM_PROBE_DP_TAIL, s);
-    if (!rc) rc = dp_collective(P, k, 2, 0, s);  // the fp32 tail (b1's row: the last chunk's pass)
+    if (!rc && !P->on(DSSM_OPT_TAIL_IN_A2A))  // the fp32 tail (b1's row: the last chunk's pass)
+      rc = dp_collective(P, k, 2, 0, s);
     P->probe_end(DSSM_PROBE_DP_TAIL, s);
     // Adam chunk by chunk, each chunk's all-gather behind its Adam
     if (!rc && i + 1 < nsteps && P->opt[DSSM_OPT_RANK_IN_ADAM]) {

@@ -150,7 +150,10 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *                      instead of the copy kernel
  *   BNB_IN_PAIR     1: bf16 fused schedule, last layer <= 128 wide: its BN backward is formed while the
  *                      dA pair launch stages its A operand (no BN-backward apply launch for it); 0: the
- *                      apply launch */
+ *                      apply launch
+ *   TAIL_IN_A2A     0; 1: dssm_plan_graph_build_dp_steps puts the fp32 tail's all-reduce into the last
+ *                      chunk's all-to-all RCCL group (one collective launch fewer per step; a mixed
+ *                      p2p / collective group, exercised at world 1 only on one-GPU boxes) */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -164,6 +167,7 @@ enum {
   DSSM_OPT_RANK_IN_ADAM,
   DSSM_OPT_MEMCPY_NODES,
   DSSM_OPT_BNB_IN_PAIR,
+  DSSM_OPT_TAIL_IN_A2A,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);

@@ -191,9 +191,10 @@ def _first_mismatch(name, got, want, geo, ext):
     return f"{name}: {d.numel()} of {got.numel()} differ, first at {i} = {where}"
 
 
-@pytest.mark.parametrize("comm,chunks,bs,memcpy", [(0, 3, 96, 0), (1, 3, 96, 0), (0, 1, 96, 0),
-                                                   (0, 1, 128, 0), (0, 3, 96, 1)])
-def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, comm_world1):
+@pytest.mark.parametrize("comm,chunks,bs,memcpy,tail", [(0, 3, 96, 0, 0), (1, 3, 96, 0, 0), (0, 1, 96, 0, 0),
+                                                        (0, 1, 128, 0, 0), (0, 3, 96, 1, 0), (0, 3, 96, 0, 1),
+                                                        (0, 1, 128, 0, 1)])
+def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, tail, comm_world1):
     """The captured data-parallel step graph (comm 0: RCCL at world 1; comm 1: device copies)
     against the same steps run eagerly on the same wire (all-to-all = copy, all-gather = identity),
     under DETERMINISTIC (every reduction in a fixed order): params, Adam m / v, beta powers and the
@@ -210,6 +211,7 @@ def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, comm_world
         _, _, m = make(D, WIDTHS, bs, NEG, "bf16", fused=False)
         m.set_option("DETERMINISTIC", True)
         m.set_option("MEMCPY_NODES", bool(memcpy))
+        m.set_option("TAIL_IN_A2A", bool(tail))  # the tail's all-reduce inside the last all-to-all's group
         gw, st, pw, geo = _wires(m, 1, 0, chunks)
         runs.append((m, gw, st, pw))
     batches = []
