@@ -591,8 +591,9 @@ __host__ __device__ inline size_t wk_smem_bytes(int Kp, int lds_epi = 0, int WM 
   return wk_red_offset(Kp, lds_epi, WM, coef_rows) + (size_t)WM * 64 * 2 * 8;
 }
 
-// BNBK > 0: the BN-backward A operand, K <= BNBK (its fp32 dA / Z groups sized for BNBK)
-template <bool BN_A, int FS, int WM = 4, int BNBK = 0>
+// BNBK > 0: the BN-backward A operand, K <= BNBK (its fp32 dA / Z groups sized for BNBK).
+// KGA > 0: the A groups per thread for K <= 32 KGA (default: kWkMaxK's), so no load is issued past Kp.
+template <bool BN_A, int FS, int WM = 4, int BNBK = 0, int KGA = 0>
 __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, int tx, int ty,
                                            u16* wk_smem) {
   constexpr bool BNB = BNBK > 0;
@@ -622,7 +623,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const int arow = t >> 2, ag0 = t & 3;
   const int brow = t / BT, bg0 = t % BT;
   // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
-  constexpr int NGA = BNB ? BNBK / 32 : kWkMaxG, NGB = (4 * NGA + BT - 1) / BT;
+  constexpr int NGA = BNB ? BNBK / 32 : (KGA ? KGA : kWkMaxG), NGB = (4 * NGA + BT - 1) / BT;
   float4 fa[NGA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
   float4 fz[BNB ? NGA : 1][2];  // BNB: the A layer's Z
   uint4 ua[NGA];      // bf16 A groups
@@ -918,7 +919,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
 // Whole-K forward NT GEMM: blocks [0, ntiles) compute tiles (XCD-grouped row blocks); with the
 // A coefficients derived from the sums, one extra block materialises them (coef, batch moments,
 // EMA update) off the tiles' critical path.
-template <bool BN_A, int FS, int WM>
+template <bool BN_A, int FS, int WM, int KGA = 0>
 __global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, int nx, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) u16 wk_smem[];
   WG_TL(a.N == 300 ? 0 : 1, 0);
@@ -927,7 +928,7 @@ __global__ __launch_bounds__(128 * WM) void k_gemm_nt_wk(NtParams a, NtFuse f, i
     return;
   }
   const int tile = xcd_tile(blockIdx.x, ntiles);
-  nt_wk_body<BN_A, FS, WM>(a, f, tile % nx, tile / nx, wk_smem);
+  nt_wk_body<BN_A, FS, WM, 0, KGA>(a, f, tile % nx, tile / nx, wk_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1048,7 +1049,7 @@ __device__ __forceinline__ void tn_wk_body(const TnParams& p, int tx, int ty, in
 // Whole-K backward pair, dA tiles only (the dW_l tiles ride in the next BN-backward apply launch).
 // BNB: the A operand dZ_l formed from dA_l while staging (NtFuse::inb); block nt_blocks: the loss
 // and BN_l's dgamma / dbeta.
-template <int WM, int BNBK = 0>
+template <int WM, int BNBK = 0, int KGA = 0>
 __global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, int nt_x, int nt_blocks) {
   extern __shared__ __attribute__((aligned(16))) u16 pw_smem[];
   WG_TL(a.K == 300 ? 3 : 2, 0);
@@ -1060,7 +1061,7 @@ __global__ __launch_bounds__(128 * WM) void k_pair_da_wk(NtParams a, NtFuse f, i
     }
   }
   const int tile = xcd_tile(blockIdx.x, nt_blocks);
-  nt_wk_body<false, 2, WM, BNBK>(a, f, tile % nt_x, tile / nt_x, pw_smem);
+  nt_wk_body<false, 2, WM, BNBK, KGA>(a, f, tile % nt_x, tile / nt_x, pw_smem);
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1224,6 +1225,10 @@ hipError_t launch_gemm_nt_fwd_fused(int M, int N, int K, const float* Z, int lda
     f.det_rows = cdiv(M, 32 * WM);                                                            \
     if (!det_fits(f, ldc)) return hipErrorInvalidValue;                                       \
     const int ntiles = nx * cdiv(M, 32 * WM);                                                 \
+    if (Kp == 320)                                                                            \
+      hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM, 10>), dim3(ntiles + (in_from_sums ? 1 : 0)), \
+                         dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
+    else                                                                                      \
     hipLaunchKernelGGL((k_gemm_nt_wk<true, 1, WM>), dim3(ntiles + (in_from_sums ? 1 : 0)),    \
                        dim3(128 * WM), wk_smem_bytes(Kp, f.lds_epi, WM), s, a, f, nx, ntiles); \
   }
@@ -1313,6 +1318,12 @@ hipError_t launch_bwd_pair(int M, int kin, int n, const uint16_t* dZ, int lddz, 
       if (kWkRows == 64)
         hipLaunchKernelGGL(k_pair_da_wk<2>, dim3(nt_blocks64), dim3(256), wk_smem_bytes(Kp, f.lds_epi, 2),
                            s, a, f, nt_x, nt_blocks64);
+      else if (Kp == 320)  // every A load inside K (10 groups per thread)
+        hipLaunchKernelGGL((k_pair_da_wk<4, 0, 10>), dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi, 4),
+                           s, a, f, nt_x, nt_blocks);
+      else if (Kp == 128)
+        hipLaunchKernelGGL((k_pair_da_wk<4, 0, 4>), dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi, 4),
+                           s, a, f, nt_x, nt_blocks);
       else
         hipLaunchKernelGGL(k_pair_da_wk<4>, dim3(nt_blocks), dim3(512), wk_smem_bytes(Kp, f.lds_epi, 4),
                            s, a, f, nt_x, nt_blocks);
