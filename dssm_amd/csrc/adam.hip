@@ -75,8 +75,8 @@ __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, f
       const int64_t r = rel / g.cols;
       const int c = (int)(rel - r * g.cols);
       uint2 p;
-      p.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
-      p.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+      p.x = pack2bf(v.x, v.y);
+      p.y = pack2bf(v.z, v.w);
       *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) = p;
       if (g.tptr) {
         g.tptr[(int64_t)(c + 0) * g.tld + r] = f2bf(v.x);
@@ -604,8 +604,8 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
     const int c = (int)(rel - r * g.cols);
     const float4 v = *reinterpret_cast<const float4*>(p + g.offset + rel);
     uint2 q;
-    q.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
-    q.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+    q.x = pack2bf(v.x, v.y);
+    q.y = pack2bf(v.z, v.w);
     *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) = q;
     if (g.tptr) {
       g.tptr[(int64_t)(c + 0) * g.tld + r] = f2bf(v.x);

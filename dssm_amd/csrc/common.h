@@ -91,8 +91,12 @@ __device__ __forceinline__ void store8(float* p, const float (&x)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
 }
+// One v_cvt_pk_bf16_f32 (RNE, as f2bf): the two-scalar form compiles to a pair of packed converts
+// and four shift / mask / or instructions to re-pair their halves.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack2bf(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{a, b}), bf16x2));
 }
 __device__ __forceinline__ void store8(u16* p, const float (&x)[8]) {
   uint4 a;

@@ -52,9 +52,7 @@ __device__ __forceinline__ float ftanh(float x) {
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
 }
 
-__device__ __forceinline__ unsigned pk2(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
-}
+__device__ __forceinline__ unsigned pk2(float a, float b) { return pack2bf(a, b); }
 __device__ __forceinline__ float lo16(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float hi16(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
 
