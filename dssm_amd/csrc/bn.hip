@@ -475,6 +475,21 @@ constexpr int apply_smem_floats() {
   return 2 * 6 * kApplyMaxLd > ApplyDw<TO>::kFloats ? 2 * 6 * kApplyMaxLd : ApplyDw<TO>::kFloats;
 }
 
+#ifdef DSSM_WG_TL
+// Diagnostics build only: per-workgroup stamps of the bf16 apply launches, slot 0 = the one hosting
+// an N = 128 dW (layer 3's), 1 = the other; [0] start [1] end [2] role (0 dW, 1 second dW set,
+// 2 element block, 3 extra block) [3] element blocks: coefficient prologue done
+__device__ unsigned long long g_apply_tl[2][2048][4];
+#define APPLY_TL(idx, v)                                                                             \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_apply_tl[tl_slot][blockIdx.x][idx] = (v);           \
+  } while (0)
+#else
+#define APPLY_TL(idx, v) \
+  do {                   \
+  } while (0)
+#endif
+
 template <typename TO>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
@@ -487,6 +502,19 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
                                                          typename ApplyDw<TO>::P dw2, int dw2_x, int dw2_y,
                                                          int dw2_blocks) {
   __shared__ __attribute__((aligned(16))) float smem[apply_smem_floats<TO>()];
+#ifdef DSSM_WG_TL
+  const int tl_slot = (sizeof(TO) == 2 && dw_blocks && dw.N == 128) ? 0 : 1;
+  const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+  auto tl_end = [&](int role) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    APPLY_TL(0, tl0);
+    APPLY_TL(1, __builtin_amdgcn_s_memrealtime());
+    APPLY_TL(2, (unsigned long long)role);
+  };
+#else
+  auto tl_end = [](int) {};
+#endif
   // blocks [0, dw_blocks): the previous backward pair's dW split-K tiles (the longest chains,
   // first in dispatch order), then [dw_blocks, + dw2_blocks) a second pair's (the one before it,
   // when that pair's BN-backward apply was folded into the next pair: BNB_IN_PAIR); they read dZ of
@@ -504,6 +532,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
       const int r = DSSM_XCD_DW_APPLY ? xcd_tile(b2, dw2_blocks) : b2;
       ApplyDw<TO>::run(dw2, r, dw2_x, dw2_y, smem);
     }
+    tl_end((int)blockIdx.x < dw_blocks ? 0 : 1);
     return;
   }
   const int bid = (int)blockIdx.x - dw_blocks - dw2_blocks;
@@ -513,6 +542,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   if (bid >= nwork) {
     if (loss_part) loss_reduce(loss_part, loss_blocks, b.rows_q, loss_out);
     fs_materialize_bwd(b);
+    tl_end(3);
     return;
   }
   float (*sc)[6][kApplyMaxLd] = reinterpret_cast<float (*)[6][kApplyMaxLd]>(smem);  // mu rstd inv shift m1 m2
@@ -559,6 +589,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
     }
   }
   __syncthreads();
+  APPLY_TL(3, __builtin_amdgcn_s_memrealtime());
   for (size_t i = i0; i < total; i += (size_t)nwork * 256) {
     const int r = (int)(i / q);
     const int c = (int)(i - (size_t)r * q) * 4;
@@ -584,6 +615,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
       *reinterpret_cast<float4*>(dZ + (size_t)r * ld + c) = make_float4(out[0], out[1], out[2], out[3]);
     }
   }
+  tl_end(2);
 }
 
 int ew_grid(size_t total) {
@@ -701,3 +733,11 @@ hipError_t launch_bn_bwd_apply_fused32(const float* Z, const float* dA, const Bn
 }
 
 }  // namespace dssm
+
+#ifdef DSSM_WG_TL
+extern "C" int dssm_debug_apply_timeline(int slot, unsigned long long* out, int n) {
+  if (slot < 0 || slot >= 2 || n > 2048) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dssm::g_apply_tl), sizeof(unsigned long long) * 4 * n,
+                             sizeof(unsigned long long) * 4 * 2048 * slot) == hipSuccess ? 0 : -2;
+}
+#endif

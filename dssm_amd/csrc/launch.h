@@ -230,7 +230,10 @@ hipError_t launch_cosine_loss(const float* z, int ld, int n, int bs, int neg, fl
 // the cosine workspace's per-workgroup loss partials (finalized by a later launch when deferred)
 // (queries per workgroup: kCosFusedWaves for the fused-statistics kernel at widths <= 128,
 // whose per-wave LDS slots then stay small; otherwise 4)
-constexpr int kCosFusedWaves = 16;
+#ifndef DSSM_COS_FUSED_WAVES
+#define DSSM_COS_FUSED_WAVES 16
+#endif
+constexpr int kCosFusedWaves = DSSM_COS_FUSED_WAVES;
 inline int cosine_waves(int n, bool fused) { return (fused && n <= 128) ? kCosFusedWaves : 4; }
 inline int cosine_blocks(int bs, int n = 0, bool fused = false) {
   const int w = cosine_waves(n, fused);

@@ -141,3 +141,31 @@ for name, sel in (("query blocks", slice(0, nq)), ("materialise", slice(nq, nq +
     if d.size:
         print(f"cosine {name}: {d.size} blocks, start {st[sel].min():.1f}..{st[sel].max():.1f}, end "
               f"{en[sel].min():.1f}..{en[sel].max():.1f} us, duration median {np.median(d):.2f} max {d.max():.2f}")
+
+# the two bf16 BN-backward apply launches (bn.hip, g_apply_tl): dW tile blocks vs element blocks
+fa = getattr(lib, "dssm_debug_apply_timeline", None)
+if fa is not None:
+    fa.restype = C.c_int
+    fa.argtypes = [C.c_int, C.c_void_p, C.c_int]
+    for slot, name in enumerate(("apply hosting dW3 (N=128)", "apply (other)")):
+        buf = np.zeros((2048, 4), np.uint64)
+        assert fa(slot, buf.ctypes.data, 2048) == 0
+        ok = buf[:, 0] > 0
+        if not ok.any():
+            print(f"{name}: no stamps")
+            continue
+        t = buf[ok].astype(np.int64)
+        t0 = t[:, 0].min()
+        st, en = (t[:, 0] - t0) * 0.01, (t[:, 1] - t0) * 0.01
+        print(f"{name}: {int(ok.sum())} WGs, span {en.max():.2f} us")
+        for role, rn in enumerate(("dW tiles", "second dW set", "element blocks", "extra block")):
+            m = t[:, 2] == role
+            if not m.any():
+                continue
+            d = en[m] - st[m]
+            line = (f"   {rn}: {int(m.sum())} WGs, start {st[m].min():.2f}..{st[m].max():.2f}, end "
+                    f"{np.median(en[m]):.2f} median / {en[m].max():.2f} max, duration median {np.median(d):.2f} max {d.max():.2f}")
+            if role == 2:
+                pro = (t[m][:, 3] - t[m][:, 0]) * 0.01
+                line += f"; prologue median {np.median(pro):.2f} max {pro.max():.2f}"
+            print(line)
