@@ -475,6 +475,13 @@ constexpr int apply_smem_floats() {
   return 2 * 6 * kApplyMaxLd > ApplyDw<TO>::kFloats ? 2 * 6 * kApplyMaxLd : ApplyDw<TO>::kFloats;
 }
 
+#ifndef DSSM_APPLY_PF  // grid-stride iterations of an element block whose loads are issued up front
+#define DSSM_APPLY_PF 1
+#endif
+constexpr int kApplyPf = DSSM_APPLY_PF;
+#ifndef DSSM_APPLY_WAVES  // waves per SIMD the apply launch is compiled for (its VGPR budget)
+#define DSSM_APPLY_WAVES 1
+#endif
 #ifdef DSSM_WG_TL
 // Diagnostics build only: per-workgroup stamps of the bf16 apply launches, slot 0 = the one hosting
 // an N = 128 dW (layer 3's), 1 = the other; [0] start [1] end [2] role (0 dW, 1 second dW set,
@@ -491,7 +498,7 @@ __device__ unsigned long long g_apply_tl[2][2048][4];
 #endif
 
 template <typename TO>
-__global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
+__global__ __launch_bounds__(256, DSSM_APPLY_WAVES) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
                                                          TO* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
@@ -551,14 +558,21 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   const int q = ld >> 2;
   const int rows = b.rows_q + b.rows_d;
   const size_t total = (size_t)rows * q;
-  // the first grid-stride element's loads go out before the coefficient prologue
-  const size_t i0 = (size_t)bid * 256 + threadIdx.x;
-  float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), da0 = z0;
-  if (i0 < total) {
-    const int r = (int)(i0 / q);
-    const int c = (int)(i0 - (size_t)r * q) * 4;
-    z0 = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
-    da0 = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+  // the first kApplyPf grid-stride elements' loads go out before the coefficient prologue (a
+  // dependent load per iteration would put one memory latency per iteration on the block)
+  const size_t i0 = (size_t)bid * 256 + threadIdx.x, stride = (size_t)nwork * 256;
+  float4 zp[kApplyPf], dp[kApplyPf];
+#pragma unroll
+  for (int u = 0; u < kApplyPf; ++u) {
+    const size_t i = i0 + u * stride;
+    zp[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    dp[u] = zp[u];
+    if (i < total) {
+      const int r = (int)(i / q);
+      const int c = (int)(i - (size_t)r * q) * 4;
+      zp[u] = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
+      dp[u] = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
+    }
   }
   {  // coefficients of all 2*ld (tower, column) items: every load in flight at once
     constexpr int NPER = 2 * kApplyMaxLd / 256;
@@ -590,15 +604,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
   }
   __syncthreads();
   APPLY_TL(3, __builtin_amdgcn_s_memrealtime());
-  for (size_t i = i0; i < total; i += (size_t)nwork * 256) {
+  auto element = [&](size_t i, float4 z, float4 da) {
     const int r = (int)(i / q);
     const int c = (int)(i - (size_t)r * q) * 4;
     const int t = r < b.rows_q ? 0 : 1;
-    float4 z = z0, da = da0;
-    if (i != i0) {
-      z = *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c);
-      da = *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c);
-    }
     const float zz[4] = {z.x, z.y, z.z, z.w}, dd[4] = {da.x, da.y, da.z, da.w};
     float out[4];
 #pragma unroll
@@ -614,6 +623,15 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_fs(const float* __restrict
     } else {
       *reinterpret_cast<float4*>(dZ + (size_t)r * ld + c) = make_float4(out[0], out[1], out[2], out[3]);
     }
+  };
+#pragma unroll
+  for (int u = 0; u < kApplyPf; ++u)
+    if (i0 + u * stride < total) element(i0 + u * stride, zp[u], dp[u]);
+  for (size_t i = i0 + kApplyPf * stride; i < total; i += stride) {
+    const int r = (int)(i / q);
+    const int c = (int)(i - (size_t)r * q) * 4;
+    element(i, *reinterpret_cast<const float4*>(Z + (size_t)r * ld + c),
+            *reinterpret_cast<const float4*>(dA + (size_t)r * ld + c));
   }
   tl_end(2);
 }

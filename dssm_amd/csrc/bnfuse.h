@@ -214,7 +214,10 @@ __device__ __forceinline__ void fs_coef_stage(const BnSide& b, int tid, int nthr
 
 // Per-tower column sums of z and z^2 of one kSumsRows x 64 block (NT threads: NT/64 row groups),
 // fp64 atomics into fsum [2 towers][2][ldz]; blocks never straddle the tower boundary.
-constexpr int kSumsRows = 128;  // 256-row blocks measured +0.4 us/step (round 3)
+#ifndef DSSM_SUMS_ROWS
+#define DSSM_SUMS_ROWS 128
+#endif
+constexpr int kSumsRows = DSSM_SUMS_ROWS;  // 256-row blocks measured +0.4 us/step (round 3)
 template <int NT>
 __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int ldz, int ncol,
                                               int row_split, int rows, double* __restrict__ fsum,

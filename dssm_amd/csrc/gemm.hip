@@ -570,6 +570,9 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NtParams a, NtFuse f) {
 // epilogue chains.  FS epilogues as nt_body's (tiles never straddle the tower boundary:
 // row_split % (32 WM) == 0).
 constexpr int kWkMaxK = 352;
+#ifndef DSSM_NT_COLMAP
+#define DSSM_NT_COLMAP 1
+#endif
 #ifndef DSSM_WK_ROWS
 #define DSSM_WK_ROWS 128
 #endif
@@ -624,11 +627,29 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const int brow = t / BT, bg0 = t % BT;
   // >= ceil(Kp/8 / 4), ceil(Kp/8 / BT)
   constexpr int NGA = BNB ? BNBK / 32 : (KGA ? KGA : kWkMaxG), NGB = (4 * NGA + BT - 1) / BT;
-  float4 fa[NGA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
+  // CM (BN_A, exact-K instances): the fp32 A panel by fixed column group -- thread t stages group
+  // t % CG of rows t / CG + CP j -- so each thread reads its group's BN coefficients from LDS once
+  // instead of once per group (4 ds_read_b128 per 8 elements, ~1 KiB of LDS reads per wave-group)
+  constexpr bool CM = BN_A && !BNB && KGA > 0 && DSSM_NT_COLMAP;
+  constexpr int CG = 4 * (KGA ? KGA : 1), CP = NT / CG, CR = (ROWS + CP - 1) / CP;
+  constexpr int NFA = CM ? CR : NGA;
+  float4 fa[NFA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
   float4 fz[BNB ? NGA : 1][2];  // BNB: the A layer's Z
   uint4 ua[NGA];      // bf16 A groups
   uint4 ub[NGB];
-  {
+  const int cg = t % CG, cr0 = t / CG;  // CM: this thread's column group and first row
+  if constexpr (CM) {
+    const int kg = cg * 8;
+#pragma unroll
+    for (int j = 0; j < CR; ++j) {
+      const int row = cr0 + CP * j;
+      const bool ok = row < ROWS && bm + row < M && kg < lda;
+      const size_t off = ok ? (size_t)(bm + row) * lda + kg : 0;
+      fa[j][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
+      fa[j][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
+    }
+  }
+  if constexpr (!CM) {
     const bool rok = bm + arow < M;
     const size_t rbase = (size_t)(rok ? bm + arow : 0) * lda;
 #pragma unroll
@@ -646,6 +667,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         ua[i] = *reinterpret_cast<const uint4*>((const u16*)a.A + off);
       }
     }
+  }
+  {
     const bool bok = bn + brow < N;
     const size_t bbase = (size_t)(bok ? bn + brow : 0) * ldb;
 #pragma unroll
@@ -734,7 +757,37 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   }
   // ---- LDS images (bf16); out-of-range groups zeroed here, after every load was issued
   const bool write_a = (BN_A || BNB) && a.a_out != nullptr && tx == 0;
-  {
+  if constexpr (CM) {
+    const int kg = cg * 8;
+    if (cr0 < CP) {  // threads past CP * CG stage nothing
+      float ci[8], ch[8];
+      const float* cp = &sCoef[(tower * 2) * Kp + kg];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        ci[q] = cp[q];
+        ch[q] = cp[Kp + q];
+      }
+#pragma unroll
+      for (int j = 0; j < CR; ++j) {
+        const int row = cr0 + CP * j;
+        if (row < ROWS) {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (bm + row < M && kg < lda) {
+            const float z[8] = {fa[j][0].x, fa[j][0].y, fa[j][0].z, fa[j][0].w,
+                                fa[j][1].x, fa[j][1].y, fa[j][1].z, fa[j][1].w};
+            float y[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
+            v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
+            v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
+            if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + row) * lda + kg) = v;
+          }
+          *reinterpret_cast<uint4*>(&sA[row * LDK + kg]) = v;
+        }
+      }
+    }
+  }
+  if constexpr (!CM) {
     const bool rok = bm + arow < M;
 #pragma unroll
     for (int i = 0; i < NGA; ++i) {
@@ -777,6 +830,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         *reinterpret_cast<uint4*>(&sA[arow * LDK + kg]) = v;
       }
     }
+  }
+  {
     const bool bok = bn + brow < N;
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
