@@ -630,11 +630,12 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   // CM (BN_A, exact-K instances): the fp32 A panel by fixed column group -- thread t stages group
   // t % CG of rows t / CG + CP j -- so each thread reads its group's BN coefficients from LDS once
   // instead of once per group (4 ds_read_b128 per 8 elements, ~1 KiB of LDS reads per wave-group)
-  constexpr bool CM = BN_A && !BNB && KGA > 0 && DSSM_NT_COLMAP;
-  constexpr int CG = 4 * (KGA ? KGA : 1), CP = NT / CG, CR = (ROWS + CP - 1) / CP;
+  // (BNB: six coefficient planes per group)
+  constexpr bool CM = ((BN_A && KGA > 0) || BNB) && DSSM_NT_COLMAP;
+  constexpr int CG = 4 * (BNB ? BNBK / 32 : (KGA ? KGA : 1)), CP = NT / CG, CR = (ROWS + CP - 1) / CP;
   constexpr int NFA = CM ? CR : NGA;
   float4 fa[NFA][2];  // fp32 A groups (BN_A: Z; BNB: dA)
-  float4 fz[BNB ? NGA : 1][2];  // BNB: the A layer's Z
+  float4 fz[BNB ? NFA : 1][2];  // BNB: the A layer's Z
   uint4 ua[NGA];      // bf16 A groups
   uint4 ub[NGB];
   const int cg = t % CG, cr0 = t / CG;  // CM: this thread's column group and first row
@@ -647,6 +648,10 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       const size_t off = ok ? (size_t)(bm + row) * lda + kg : 0;
       fa[j][0] = *reinterpret_cast<const float4*>((const float*)a.A + off);
       fa[j][1] = *reinterpret_cast<const float4*>((const float*)a.A + off + 4);
+      if constexpr (BNB) {
+        fz[j][0] = *reinterpret_cast<const float4*>(f.zA + off);
+        fz[j][1] = *reinterpret_cast<const float4*>(f.zA + off + 4);
+      }
     }
   }
   if constexpr (!CM) {
@@ -759,14 +764,14 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   const bool write_a = (BN_A || BNB) && a.a_out != nullptr && tx == 0;
   if constexpr (CM) {
     const int kg = cg * 8;
-    if (cr0 < CP) {  // threads past CP * CG stage nothing
-      float ci[8], ch[8];
-      const float* cp = &sCoef[(tower * 2) * Kp + kg];
+    if (cr0 < CP && kg < Kp) {  // threads past CP * CG, and groups past Kp (BNB: K < BNBK), stage nothing
+      constexpr int NC = BNB ? 6 : 2;  // BN_A: inv, shift; BNB: mu, rstd, inv, shift, m1, m2
+      float cf[NC][8];
+      const float* cp = &sCoef[(tower * NC) * Kp + kg];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        ci[q] = cp[q];
-        ch[q] = cp[Kp + q];
-      }
+      for (int u = 0; u < NC; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cf[u][q] = cp[u * Kp + q];
 #pragma unroll
       for (int j = 0; j < CR; ++j) {
         const int row = cr0 + CP * j;
@@ -776,8 +781,16 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
             const float z[8] = {fa[j][0].x, fa[j][0].y, fa[j][0].z, fa[j][0].w,
                                 fa[j][1].x, fa[j][1].y, fa[j][1].z, fa[j][1].w};
             float y[8];
+            if constexpr (BNB) {  // bn.hip's k_bn_bwd_apply_fs arithmetic: dZ = inv * (dy - m1 - xhat * m2)
+              const float zz[8] = {fz[j][0].x, fz[j][0].y, fz[j][0].z, fz[j][0].w,
+                                   fz[j][1].x, fz[j][1].y, fz[j][1].z, fz[j][1].w};
 #pragma unroll
-            for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], ci[q], ch[q]), 0.f);
+              for (int q = 0; q < 8; ++q)
+                y[q] = bn_bwd_dz(zz[q], z[q], cf[0][q], cf[1][q], cf[2][q], cf[3][q], cf[4][q], cf[5][q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) y[q] = fmaxf(bn_affine(z[q], cf[0][q], cf[1][q]), 0.f);
+            }
             v.x = pack2bf(y[0], y[1]); v.y = pack2bf(y[2], y[3]);
             v.z = pack2bf(y[4], y[5]); v.w = pack2bf(y[6], y[7]);
             if (write_a) *reinterpret_cast<uint4*>(a.a_out + (size_t)(bm + row) * lda + kg) = v;
