@@ -20,6 +20,34 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Butterfly all-sum stages on the VALU (no LDS-pipe ds_bpermute): stage S of wave_allsum_step
+// adds the partner value of the lane's 2^S-block neighbour.  Stages run in order 0..5; stages 2
+// and 3 use the row half-mirror / mirror permutations, which pair each lane with a lane of the
+// other half-block -- the same partner value as lane ^ 4 / lane ^ 8, because after the earlier
+// stages every lane of a half-block holds the same partial sum -- and stages 4 / 5 the gfx950
+// row / half-wave swaps.  Every lane ends with the same bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int S>
+__device__ __forceinline__ float wave_allsum_step(float v) {
+  if constexpr (S == 0) return v + dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  if constexpr (S == 1) return v + dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (S == 2) return v + dpp_mov<0x141>(v);  // row_half_mirror
+  if constexpr (S == 3) return v + dpp_mov<0x140>(v);  // row_mirror
+  if constexpr (S == 4) {  // rows 0 <-> 1, 2 <-> 3: both results hold one row each
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                    false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+  }
+  if constexpr (S == 5) {  // half-waves
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                    false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+  }
+}
+
 // Broadcast lane j's value (j wave-uniform) -> scalar register.
 __device__ __forceinline__ int bcast_i(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
 __device__ __forceinline__ float bcast_f(float v, int j) {

@@ -11,8 +11,10 @@
 // atomics).  The per-block loss/accuracy partials are summed in fixed order by a later launch
 // (the backward's first, or k_loss_finalize).
 #include <algorithm>
+#include <type_traits>
 
 #include "bnfuse.h"
+
 #include "common.h"
 #include "launch.h"
 #include "csc.h"
@@ -35,6 +37,9 @@ __device__ __forceinline__ void loss_finalize(const float* part, int nblk, int b
 // moments and the EMA update) and the workgroup adds its rows' backward sums (sum dy,
 // sum dy*xhat per tower, ReLU mask applied) to fs.bsum.
 constexpr int kCosMaxN = 512;
+#ifndef DSSM_COS_DPP  // the rows' norm / dot butterflies on DPP and row swaps (0: ds_bpermute shuffles)
+#define DSSM_COS_DPP 1
+#endif
 // NW: waves (queries) per workgroup.  The fused kernel uses 16: each workgroup adds its backward
 // sums with one fp64 atomic per (statistic, column), and the 64-deep same-address chains (instead
 // of 256-deep at 4 waves) no longer trail the launch.
@@ -198,10 +203,23 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       red[1 + 2 * k] = dd;
       red[2 + 2 * k] = qd;
     }
+#if DSSM_COS_DPP
+    auto stage = [&](auto st) {
+#pragma unroll
+      for (int i = 0; i < 1 + 2 * KM; ++i) red[i] = wave_allsum_step<decltype(st)::value>(red[i]);
+    };
+    stage(std::integral_constant<int, 0>{});
+    stage(std::integral_constant<int, 1>{});
+    stage(std::integral_constant<int, 2>{});
+    stage(std::integral_constant<int, 3>{});
+    stage(std::integral_constant<int, 4>{});
+    stage(std::integral_constant<int, 5>{});
+#else
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
       for (int i = 0; i < 1 + 2 * KM; ++i) red[i] += __shfl_xor(red[i], o);
+#endif
     const float qn = sqrtf(red[0]);
     float cs[KM], dn[KM];
 #pragma unroll
