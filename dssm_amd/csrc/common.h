@@ -30,22 +30,45 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+// v + v[lane ^ 16] / v + v[lane ^ 32] in every lane (the same bits as a __shfl_xor butterfly stage:
+// each lane adds the even-row / low-half value and the odd-row / high-half value), on the VALU
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ double sum_xor16(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double d0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[0] | ((unsigned long long)(unsigned)b[0] << 32));
+  const double d1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[1] | ((unsigned long long)(unsigned)b[1] << 32));
+  return d0 + d1;
+}
+__device__ __forceinline__ double sum_xor32(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const double d0 = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[0] | ((unsigned long long)(unsigned)b[0] << 32));
+  const double d1 = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[1] | ((unsigned long long)(unsigned)b[1] << 32));
+  return d0 + d1;
+}
+
 template <int S>
 __device__ __forceinline__ float wave_allsum_step(float v) {
   if constexpr (S == 0) return v + dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
   if constexpr (S == 1) return v + dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
   if constexpr (S == 2) return v + dpp_mov<0x141>(v);  // row_half_mirror
   if constexpr (S == 3) return v + dpp_mov<0x140>(v);  // row_mirror
-  if constexpr (S == 4) {  // rows 0 <-> 1, 2 <-> 3: both results hold one row each
-    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
-                                                    false, false);
-    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-  }
-  if constexpr (S == 5) {  // half-waves
-    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
-                                                    false, false);
-    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-  }
+  if constexpr (S == 4) return sum_xor16(v);  // rows 0 <-> 1, 2 <-> 3
+  if constexpr (S == 5) return sum_xor32(v);  // half-waves
 }
 
 // Broadcast lane j's value (j wave-uniform) -> scalar register.

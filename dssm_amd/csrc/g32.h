@@ -560,10 +560,8 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     // the wave's 4 row groups by shuffles, the two wm halves through LDS, one atomic per statistic
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16);
-      cs[j] += __shfl_xor(cs[j], 32);
-      cq[j] += __shfl_xor(cq[j], 16);
-      cq[j] += __shfl_xor(cq[j], 32);
+      cs[j] = sum_xor32(sum_xor16(cs[j]));
+      cq[j] = sum_xor32(sum_xor16(cq[j]));
     }
     if (wm == 1 && lane < 16) {
 #pragma unroll

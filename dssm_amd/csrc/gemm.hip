@@ -512,10 +512,8 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
     // reduce the 4 row groups of the wave, then the two wm halves through LDS
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16);
-      cs[j] += __shfl_xor(cs[j], 32);
-      cq[j] += __shfl_xor(cq[j], 16);
-      cq[j] += __shfl_xor(cq[j], 32);
+      cs[j] = sum_xor32(sum_xor16(cs[j]));
+      cq[j] = sum_xor32(sum_xor16(cq[j]));
     }
     if (wm == 1 && lane < 16) {
 #pragma unroll
@@ -933,10 +931,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   if constexpr (FS != 0) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16);
-      cs[j] += __shfl_xor(cs[j], 32);
-      cq[j] += __shfl_xor(cq[j], 16);
-      cq[j] += __shfl_xor(cq[j], 32);
+      cs[j] = sum_xor32(sum_xor16(cs[j]));
+      cq[j] = sum_xor32(sum_xor16(cq[j]));
     }
     if (lane < 16) {
 #pragma unroll

@@ -712,8 +712,7 @@ __global__ __launch_bounds__(512) void k_rnn_dw(DwArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       float v = bsum[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
+      v = sum_xor32(sum_xor16(v));
       if (g == 0) out[(size_t)128 * 128 + wn * 32 + 16 * j + li] = v;
     }
   }
