@@ -172,27 +172,32 @@ __device__ __forceinline__ void tn_chunk_body(const TnParams& p, int tx, int ty,
       ra[s][g] = *reinterpret_cast<const uint4*>(p.A + (size_t)gk * p.lda + gmc);
       rb[s][g] = *reinterpret_cast<const uint4*>(p.B + (size_t)gk * p.ldb + gnc);
     }
-  if (!(bm + 64 <= Mload && bn + 64 <= p.N && kbeg + 128 * NSUB <= kend)) {  // edge tile
-    auto fix = [](uint4 v, int g0, int lim, bool ones, bool rowok) {
-      unsigned e[4] = {v.x, v.y, v.z, v.w};
+  // Edge tiles: this thread's 8 columns get a keep mask (column < lim) and the ones-row pattern
+  // (column == lim), formed once; each operand vector is written to LDS as (v & keep) | ones, or zero
+  // for a row past the split.  (A per-element extract / select / insert right after the loads cost
+  // ~50 VALU instructions per vector and made the edge tiles the apply launch's longest.)
+  const bool edge = !(bm + 64 <= Mload && bn + 64 <= p.N && kbeg + 128 * NSUB <= kend);
+  uint4 ka = make_uint4(~0u, ~0u, ~0u, ~0u), oa = make_uint4(0u, 0u, 0u, 0u), kb = ka, ob = oa;
+  if (edge) {
+    auto masks = [](int g0, int lim, bool ones, uint4& keep, uint4& one) {
+      unsigned kk[4], oo[4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int m = g0 + q;
-        const unsigned h = (e[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-        const unsigned k = !rowok ? 0u : (m < lim ? h : ((ones && m == lim) ? 0x3f80u : 0u));
-        e[q >> 1] = (e[q >> 1] & ~(0xffffu << (16 * (q & 1)))) | (k << (16 * (q & 1)));
+      for (int q = 0; q < 4; ++q) {
+        const int lo = g0 + 2 * q, hi = lo + 1;
+        kk[q] = (lo < lim ? 0xffffu : 0u) | (hi < lim ? 0xffff0000u : 0u);
+        oo[q] = ((ones && lo == lim) ? 0x3f80u : 0u) | ((ones && hi == lim) ? 0x3f800000u : 0u);
       }
-      return make_uint4(e[0], e[1], e[2], e[3]);
+      keep = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+      one = make_uint4(oo[0], oo[1], oo[2], oo[3]);
     };
-#pragma unroll
-    for (int s = 0; s < NSUB; ++s)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const bool rowok = kbeg + 128 * s + (t >> 3) + 32 * g < kend;
-        ra[s][g] = fix(ra[s][g], gm, Mload, p.ones_row != 0, rowok);
-        rb[s][g] = fix(rb[s][g], gn, p.N, false, rowok);
-      }
+    masks(gm, Mload, p.ones_row != 0, ka, oa);
+    masks(gn, p.N, false, kb, ob);
   }
+  auto fix = [](uint4 v, uint4 keep, uint4 one, bool rowok) {
+    return rowok ? make_uint4((v.x & keep.x) | one.x, (v.y & keep.y) | one.y, (v.z & keep.z) | one.z,
+                              (v.w & keep.w) | one.w)
+                 : make_uint4(0u, 0u, 0u, 0u);
+  };
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -205,8 +210,14 @@ __device__ __forceinline__ void tn_chunk_body(const TnParams& p, int tx, int ty,
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int r = (t >> 3) + 32 * g;
-      *reinterpret_cast<uint4*>(&sA[r * kTnLd + sc]) = ra[s][g];
-      *reinterpret_cast<uint4*>(&sB[r * kTnLd + sc]) = rb[s][g];
+      uint4 va = ra[s][g], vb = rb[s][g];
+      if (edge) {
+        const bool rowok = kbeg + 128 * s + r < kend;
+        va = fix(va, ka, oa, rowok);
+        vb = fix(vb, kb, ob, rowok);
+      }
+      *reinterpret_cast<uint4*>(&sA[r * kTnLd + sc]) = va;
+      *reinterpret_cast<uint4*>(&sB[r * kTnLd + sc]) = vb;
     }
     __syncthreads();
     const int kc = min(128, ((kend - kbeg - 128 * s) + 31) & ~31);
