@@ -37,6 +37,9 @@ __device__ __forceinline__ void loss_finalize(const float* part, int nblk, int b
 // moments and the EMA update) and the workgroup adds its rows' backward sums (sum dy,
 // sum dy*xhat per tower, ReLU mask applied) to fs.bsum.
 constexpr int kCosMaxN = 512;
+#ifndef DSSM_COS_LANEPAR  // the per-doc scalar math one doc per lane (0: every lane computes every doc's)
+#define DSSM_COS_LANEPAR 1
+#endif
 #ifndef DSSM_COS_DPP  // the rows' norm / dot butterflies on DPP and row swaps (0: ds_bpermute shuffles)
 #define DSSM_COS_DPP 1
 #endif
@@ -221,7 +224,52 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       for (int i = 0; i < 1 + 2 * KM; ++i) red[i] += __shfl_xor(red[i], o);
 #endif
     const float qn = sqrtf(red[0]);
-    float cs[KM], dn[KM];
+    float cs[KM], dn[KM], p[KM];
+    int amax = 0;
+    float pbest = -1.f;
+#if DSSM_COS_LANEPAR
+    // The per-doc scalars (norms, cosines, softmax, gradient coefficients) are wave-uniform: lane k
+    // computes doc k's, each an IEEE sqrt / exp / division of the same operands as the serial form,
+    // and v_readlane hands them to the wave (one division sequence per stage instead of one per doc)
+    auto bcast = [](float v, int k) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k)); };
+    float my_dn = 1.f, my_cs = 0.f;
+    {
+      float dd = 0.f, qd = 0.f;
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+        if (lane == k) {
+          dd = red[1 + 2 * k];
+          qd = red[2 + 2 * k];
+        }
+      if (lane < K) {
+        my_dn = sqrtf(dd);
+        my_cs = qd / (qn * my_dn);  // truediv(prod, query_norm*doc_norm); NaN on a zero row, as TF
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      cs[k] = k < K ? bcast(my_cs, k) : 0.f;
+      dn[k] = k < K ? bcast(my_dn, k) : 1.f;
+    }
+    // softmax over the K scaled scores (tf.nn.softmax: exp(x - max) / sum)
+    float mx = gamma * cs[0];
+#pragma unroll
+    for (int k = 1; k < KM; ++k)
+      if (k < K) mx = fmaxf(mx, gamma * cs[k]);
+    const float my_ex = lane < K ? expf(gamma * my_cs - mx) : 0.f;
+    float ex[KM], sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      ex[k] = k < K ? bcast(my_ex, k) : 0.f;
+      sum += ex[k];
+    }
+    const float my_p = my_ex / sum;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      p[k] = bcast(my_p, k);
+      if (k < K && p[k] > pbest) { pbest = p[k]; amax = k; }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       cs[k] = 0.f;
@@ -242,14 +290,12 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
       ex[k] = (k < K) ? expf(gamma * cs[k] - mx) : 0.f;
       sum += ex[k];
     }
-    float p[KM];
-    int amax = 0;
-    float pbest = -1.f;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       p[k] = ex[k] / sum;
       if (k < K && p[k] > pbest) { pbest = p[k]; amax = k; }
     }
+#endif
 #pragma unroll
     for (int k = 0; k < KM; ++k)
       if (k < K && k == lane) {
@@ -266,13 +312,26 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
     float dq[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) dq[e] = 0.f;
+#if DSSM_COS_LANEPAR
+    float my_a = 0.f, my_bq = 0.f, my_bd = 0.f;
+    if (lane < K) {
+      const float g = gamma * (my_p - (lane == 0 ? 1.f : 0.f)) / (float)bs;
+      my_a = g / (qn * my_dn);
+      my_bq = g * my_cs / (qn * qn);
+      my_bd = g * my_cs / (my_dn * my_dn);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       if (k < K) {
+#if DSSM_COS_LANEPAR
+        const float a = bcast(my_a, k), bq = bcast(my_bq, k), bd = bcast(my_bd, k);
+#else
         const float g = gamma * (p[k] - (k == 0 ? 1.f : 0.f)) / (float)bs;
         const float a = g / (qn * dn[k]);
         const float bq = g * cs[k] / (qn * qn);
         const float bd = g * cs[k] / (dn[k] * dn[k]);
+#endif
         const size_t row = (size_t)doc_row(j, k, bs, neg) * ld;
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
