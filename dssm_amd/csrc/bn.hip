@@ -475,12 +475,17 @@ constexpr int apply_smem_floats() {
   return 2 * 6 * kApplyMaxLd > ApplyDw<TO>::kFloats ? 2 * 6 * kApplyMaxLd : ApplyDw<TO>::kFloats;
 }
 
+// The element blocks of the bf16 launch are the critical path once the dW tiles' edge handling is
+// cheap (per-workgroup timeline): their loads for kApplyPf grid-stride iterations go out up front,
+// and the launch is compiled for 4 waves per SIMD (128 VGPRs, no spill) so all of its workgroups
+// (400 dW tiles + 512 element blocks at C2) are resident at once instead of the last ~145 element
+// blocks starting ~6 us late.  154.6 vs 155.7 us/step, four alternations.
 #ifndef DSSM_APPLY_PF  // grid-stride iterations of an element block whose loads are issued up front
-#define DSSM_APPLY_PF 1
+#define DSSM_APPLY_PF 4
 #endif
 constexpr int kApplyPf = DSSM_APPLY_PF;
-#ifndef DSSM_APPLY_WAVES  // waves per SIMD the apply launch is compiled for (its VGPR budget)
-#define DSSM_APPLY_WAVES 1
+#ifndef DSSM_APPLY_WAVES  // waves per SIMD the bf16 apply launch is compiled for (its VGPR budget)
+#define DSSM_APPLY_WAVES 4
 #endif
 #ifdef DSSM_WG_TL
 // Diagnostics build only: per-workgroup stamps of the bf16 apply launches, slot 0 = the one hosting
@@ -498,7 +503,7 @@ __device__ unsigned long long g_apply_tl[2][2048][4];
 #endif
 
 template <typename TO>
-__global__ __launch_bounds__(256, DSSM_APPLY_WAVES) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
+__global__ __launch_bounds__(256, sizeof(TO) == 2 ? DSSM_APPLY_WAVES : 1) void k_bn_bwd_apply_fs(const float* __restrict__ Z,
                                                          const float* __restrict__ dA, BnSide b,
                                                          TO* __restrict__ dZ,
                                                          const float* __restrict__ loss_part,
