@@ -14,6 +14,7 @@
 // zero-init).  The bias gradient rides along: the A^T operand gets a virtual all-ones row at
 // m = K_in, so row K_in of the [K_in+1 x N] output (the arena's [W; b] block) is colsum(dZ).
 #include <cstdlib>
+#include <type_traits>
 
 #include "bnfuse.h"
 #include "common.h"
@@ -899,33 +900,52 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
   constexpr int kCld = 68;
   if (lds_epi) __syncthreads();
   double cs[2] = {0.0, 0.0}, cq[2] = {0.0, 0.0};
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  // The store target (LDS or global) and the tile's row bound are workgroup-uniform: one loop
+  // instance per case, so the unrolled loop carries no per-element branch (the per-element form
+  // compiled to 16 exec-mask regions and uniform branches); per j, the column bound per lane.
+  // Each column's sums add its values in the same (i, r) order as before.
+  auto epi = [&](auto lds_c, auto rows_c) {
+    constexpr bool LDS = decltype(lds_c)::value, RF = decltype(rows_c)::value;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = bn + wn * 32 + j * 16 + (lane & 15);
+      if (n < ldc) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < ldc) {
-          const float v = acc[i][j][r];
-          const float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
-          if (lds_epi)
-            sC[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * kCld + wn * 32 + j * 16 + (lane & 15)] = x;
-          else
-            a.C[(size_t)m * ldc + n] = x;
-          if constexpr (FS == 1) {
-            cs[j] += x;
-            cq[j] += (double)x * x;
-          } else if constexpr (FS == 2) {
-            const float z = zb[i][j][r];
-            const float dy = (n < N && bn_affine(z, cb[j][2], cb[j][3]) > 0.f) ? x : 0.f;
-            const float xh = (z - cb[j][0]) * cb[j][1];
-            cs[j] += dy;
-            cq[j] += (double)dy * xh;
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = bm + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+            if (RF || m < M) {
+              const float v = acc[i][j][r];
+              const float x = (n < N) ? (a.bias ? v + bcol[j] : v) : 0.f;
+              if constexpr (LDS)
+                sC[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * kCld + wn * 32 + j * 16 + (lane & 15)] = x;
+              else
+                a.C[(size_t)m * ldc + n] = x;
+              if constexpr (FS == 1) {
+                cs[j] += x;
+                cq[j] += (double)x * x;
+              } else if constexpr (FS == 2) {
+                const float z = zb[i][j][r];
+                const float dy = (n < N && bn_affine(z, cb[j][2], cb[j][3]) > 0.f) ? x : 0.f;
+                const float xh = (z - cb[j][0]) * cb[j][1];
+                cs[j] += dy;
+                cq[j] += (double)dy * xh;
+              }
+            }
           }
         }
       }
+    }
+  };
+  {
+    using T = std::true_type;
+    using F = std::false_type;
+    const bool rows_full = bm + ROWS <= M;
+    if (lds_epi) {
+      if (rows_full) epi(T{}, T{}); else epi(T{}, F{});
+    } else {
+      if (rows_full) epi(F{}, T{}); else epi(F{}, F{});
     }
   }
   if constexpr (FS != 0) {
