@@ -261,7 +261,7 @@ def test_dp_step_graph_world1_matches_eager(comm, chunks, bs, memcpy, tail, comm
 
 
 @pytest.mark.parametrize("comm,chunks,bs,replays,bar5,bar4", [(0, 3, 96, 1, 0.999, 1.0), (0, 3, 96, 2, None, 0.93),
-                                                               (1, 3, 96, 2, None, 0.93), (0, 1, 128, 2, None, 0.93)])
+                                                               (1, 3, 96, 2, None, 0.93), (0, 1, 128, 2, None, 0.85)])
 def test_dp_step_graph_default_schedule_matches_eager(comm, chunks, bs, replays, bar5, bar4, comm_world1):
     """The DEFAULT schedule (no DETERMINISTIC: fp32 column-sum atomics, the schedule the 8-GPU run
     times) of the captured data-parallel step graph against the same steps run eagerly.  One launch
@@ -269,8 +269,10 @@ def test_dp_step_graph_default_schedule_matches_eager(comm, chunks, bs, replays,
     within 1e-5; measured 100%, max 7e-7, profiles/r05_dp_graph_noise.txt).  After 6 steps the
     atomics' order has been amplified through Adam: graph-vs-eager equals eager-vs-eager there
     (90% within 1e-5, 99.1-99.6% within 1e-4, same max), so the bar is the eager runs' own spread:
-    >= 93% within 1e-4 (measured 96.4-99.6% over runs; graph vs graph 98.4% at BS 128), every element
-    within 2 lr x steps, losses
+    >= 93% within 1e-4 (measured 96.4-99.6% over runs; graph vs graph 98.4% at BS 128); at BS 128 with
+    one chunk two EAGER runs themselves land at 89.3-89.4% in three of four repetitions (and 100% in the
+    fourth; graph-vs-eager the same, profiles/r05_dp_graph_spread.txt, tools/dp_graph_spread.py), so that
+    case's bar is 85%; every element within 2 lr x steps, losses
     rel 5e-3 (measured 1.2e-3 at a loss of 0.039)."""
     steps = 3
     runs = []
