@@ -1,7 +1,7 @@
 """Diagnostics: the spread behind tests/test_gpu_wire.py::test_dp_step_graph_default_schedule_matches_eager
 (default schedule, fp32 column-sum atomics): for its (comm 0, 1 chunk, BS 128, 2 replays) case, the
 fraction of parameters within 1e-4 for graph-vs-eager and for eager-vs-eager, several repetitions.
-    python3 tools/dp_graph_spread.py"""
+    python3 tools/dp_graph_spread.py [BS CHUNKS]   (default 128 1)"""
 import os
 import sys
 
@@ -13,8 +13,11 @@ from tests.test_gpu_parity import make
 from tests.test_gpu_wire import D, NEG, WIDTHS, _wires
 
 
+BS_, CHUNKS = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (128, 1)
+
+
 def run(mode, batches, chunks, replays, comm=0):
-    _, _, m = make(D, WIDTHS, 128, NEG, "bf16", fused=False)
+    _, _, m = make(D, WIDTHS, BS_, NEG, "bf16", fused=False)
     gw, st, pw, geo = _wires(m, 1, 0, chunks)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
@@ -46,10 +49,10 @@ if lib.dssm_comm_world() == 0:  # libdssm.so's RCCL communicator at world 1 (as 
     _lib.check(lib.dssm_comm_init(0, 1, buf), "comm_init")
 batches = []
 for i in range(3):
-    b = synth_batch(D, 128, NEG, seed=300 + i, mean_nnz=32)
+    b = synth_batch(D, BS_, NEG, seed=300 + i, mean_nnz=32)
     batches.append(tuple(torch.from_numpy(x).cuda() for x in (b.indptr, b.indices, b.values)))
 for rep in range(4):
-    g, e1, e2 = run("graph", batches, 1, 2), run("eager", batches, 1, 2), run("eager", batches, 1, 2)
+    g, e1, e2 = run("graph", batches, CHUNKS, 2), run("eager", batches, CHUNKS, 2), run("eager", batches, CHUNKS, 2)
     f = lambda a, b: float(((a - b).abs() <= 1e-4).float().mean())
     print(f"rep {rep}: graph-vs-eager {f(g, e1):.4f}  eager-vs-eager {f(e1, e2):.4f}  graph-vs-eager2 {f(g, e2):.4f}", flush=True)
 lib.dssm_comm_destroy()
