@@ -264,17 +264,19 @@ def adam_alg_bytes(n_params: int, bf16: bool, fused: bool, w1_elems: int, nnz: i
 
     Every updated element streams p, m, v in and out (24 B).  Its gradient is read as fp32 (4 B),
     except (a) fused single-GPU step: the [W1; b1] rows' gradient is never stored -- the launch
-    gathers it from the CSC transpose instead, (index, value) 8 B + one bf16 dZ1 row (2 n1 B) per
-    entry, over nnz + rows entries (the ones column gives db1) -- the SpMM-backward bytes of
-    SURVEY §8(d) minus its dense dW1 write; (b) data-parallel bf16 wire: the rank's W1 shard
-    reads wire_parts bf16 partial gradients (2 B each: one per rank after the all-to-all) and
-    writes a bf16 parameter copy (2 B).  bf16 mode adds 2 B per
-    weight element written to its shadows (W_l for l >= 2 also transposed: 4 B)."""
+    gathers it from the CSC transpose instead, (index, value) 8 B + one dZ1 row per entry, over
+    nnz + rows entries (the ones column gives db1) -- the SpMM-backward bytes of SURVEY §8(d)
+    minus its dense dW1 write.  The dZ1 row is stored at the step's dZ element size
+    (DSSM_BUF_DZ, csrc/plan.hip:602): bf16 (2 n1 B) in bf16 mode, fp32 (4 n1 B) in fp32 mode;
+    (b) data-parallel bf16 wire: the rank's W1 shard reads wire_parts bf16 partial gradients
+    (2 B each: one per rank after the all-to-all) and writes a bf16 parameter copy (2 B).  bf16
+    mode adds 2 B per weight element written to its shadows (W_l for l >= 2 also transposed: 4 B)."""
     if range_elems is None:
         range_elems = n_params
     b = 24 * range_elems
     if fused:
-        b += 4 * (n_params - w1_elems) + (nnz + rows) * (8 + 2 * n1)
+        dz_bytes = 2 if bf16 else 4
+        b += 4 * (n_params - w1_elems) + (nnz + rows) * (8 + dz_bytes * n1)
     else:
         b += 4 * (range_elems - wire_elems) + (2 * wire_parts + 2) * wire_elems
     if bf16:
@@ -1073,7 +1075,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
         "config": {"workload": "dssm C2: TRIGRAM_D=30000, widths 300/300/128, NEG=4, "
-                               "Zipf(1.1) trigram batches ~32 nnz/row, fwd+bwd+dense Adam",
+                               + ("Zipf(1.1)" if args.columns == "zipf" else "uniform-column")
+                               + " trigram batches ~32 nnz/row, fwd+bwd+dense Adam",
                    "global_batch": BS * world, "per_gpu_query_bs": BS, "neg": NEG,
                    "trigram_d": D, "widths": list(WIDTHS), "parallelism": f"dp{world}",
                    "avg_nnz_per_step": nnz_avg, "launch": "hipgraph" if args.graph else "eager",

@@ -1,6 +1,8 @@
-// fp32 parity mode's dense-layer tiles on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: each
-// result is the k-ordered fp32 fmaf chain, no reduced-precision path), shared by gemm32.hip (the
-// forward / dA launches) and bn.hip (the dW split-K tiles that ride in the BN-backward apply launch).
+// fp32 parity mode's dense-layer tiles, shared by gemm32.hip (the forward / dA launches) and bn.hip
+// (the dW split-K tiles that ride in the BN-backward apply launch).  The DEFAULT build
+// (DSSM_G32_SPLIT=1, below) forms the products on the bf16 matrix cores from an exact three-way
+// split of each fp32 operand; -DDSSM_G32_SPLIT=0 builds the k-ordered fp32 fmaf chains on
+// v_mfma_f32_16x16x4_f32 (no reduced-precision path) that the rest of this paragraph describes.
 // Same fusion as the bf16 path (bnfuse.h): the forward tile applies the previous layer's BN + ReLU
 // while staging its A operand and adds its output's per-tower column sums; the dA tile adds the
 // previous layer's backward sums (sum dy, sum dy * xhat).
@@ -29,6 +31,13 @@
 // rate is 1/16 of bf16's, MI355X_MICROARCH.md).  LDS images hold the three planes as bf16: RK
 // [row][k] rows of 40 (ds_read_b128 fragments), KR [k][col] rows of 72 (ds_read_b64_tr_b16
 // fragments, tn.h).  DSSM_G32_SPLIT=0 builds the exact fp32 FMA-chain tiles described above.
+// Range: the split is exact for normal and zero x below bf16's largest finite value.  A non-finite
+// operand makes the product NaN, not Inf: its residual x - h is NaN, and even with the residual
+// forced to zero the partial product h_a * m_b (m_b = 0 for a bf16-exact b) is Inf * 0 = NaN
+// (tests/test_split3_numerics.py restates this).  Either way the step's loss turns non-finite, as
+// the reference's would; DSSM_G32_SPLIT=0 keeps IEEE Inf.  Subnormal x: bf16 shares fp32's exponent
+// range, so h / m / l of a subnormal are subnormal bf16 and the matrix core may flush them (the
+// product then loses < 2^-126 in absolute terms, far below every tolerance here).
 #pragma once
 #include "bnfuse.h"
 #include "common.h"

@@ -36,8 +36,15 @@ def test_algorithmic_bytes():
     assert bench.spmm_alg_bytes(196608, 6144, 300, 2) == 4 * 6145 + 196608 * 8 + 196608 * 600 + 6144 * 1200
     # fused single-GPU Adam: 24 B per parameter + the gathered [W1; b1] gradient rows + the shadows
     n_params, w1 = 9132040, 30001 * 300
-    b = bench.adam_alg_bytes(n_params, True, True, w1, 197742, 6144, 300, n_params, 0, 1)
+    nnz, R = 197742, 6144
+    b = bench.adam_alg_bytes(n_params, True, True, w1, nnz, R, 300, n_params, 0, 1)
     assert 3.5e8 < b < 3.7e8
+    shadows = 2 * ((w1 - 300) + 2 * (300 * 300 + 300 * 128))
+    assert b == 24 * n_params + 4 * (n_params - w1) + (nnz + R) * (8 + 2 * 300) + shadows
+    # fp32 parity mode: dZ1 is stored (and gathered) fp32 (DSSM_BUF_DZ, csrc/plan.hip:602), no shadows
+    b32 = bench.adam_alg_bytes(n_params, False, True, w1, nnz, R, 300, n_params, 0, 1)
+    assert b32 == 24 * n_params + 4 * (n_params - w1) + (nnz + R) * (8 + 4 * 300)
+    assert 4.5e8 < b32 < 4.8e8
 
 
 @pytest.mark.parametrize("name", ["r02_bench_bf16", "r02_bench_fp32", "r02_bench_rnn", "r02_bench_multiview"])

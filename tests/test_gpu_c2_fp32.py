@@ -4,7 +4,11 @@ fp32 mode is the reference's own precision (new_dssm.py:111-114: tf.float32 plac
 variables).  At BASELINE config 2 (D=30000, widths 300/300/128, BS=1024, NEG=4) it runs the same
 launch structure as the bf16 perf mode -- fused BN statistics (fp64 column sums in the producers,
 coefficients derived by the consumers), the merged CSC transpose, dW1 inside Adam -- with the dense
-layers on the fp32 MFMA tiles of csrc/g32.h (v_mfma_f32_16x16x4_f32, exact fp32 FMA chains):
+layers on the fp32 tiles of csrc/g32.h.  The default build forms their products on the bf16 matrix
+cores from an exact three-way split of each fp32 operand (x = h + m + l, six partial products
+hh, hm, mh, hl, lh, mm on v_mfma_f32_16x16x32_bf16 with fp32 accumulation: the dropped terms are
+< 2^-22 |ab|, about one fp32 rounding per product); -DDSSM_G32_SPLIT=0 builds the exact
+v_mfma_f32_16x16x4_f32 FMA chains instead.  Both are held to the bars below:
 
 1. **Kernel chain, teacher-forced** (``test_fp32_kernel_chain``): every product of one step
    recomputed by the oracle's per-op functions in float64 from the GPU's own inputs to that op

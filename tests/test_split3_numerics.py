@@ -21,7 +21,8 @@ def bf16(x: np.ndarray) -> np.ndarray:
 def split3(x: np.ndarray):
     x = np.asarray(x, np.float32)
     h = bf16(x)
-    r = (x - h).astype(np.float32)
+    with np.errstate(invalid="ignore"):
+        r = (x - h).astype(np.float32)
     m = bf16(r)
     q = (r - m).astype(np.float32)
     l = bf16(q)
@@ -71,3 +72,17 @@ def test_split_dot_product_within_fp32_accumulation():
     err = np.abs(got - ref) / scale
     # fp32 sequential accumulation of K terms: ~sqrt(K) * 2^-24 relative to the terms' norm
     assert err.max() < 4 * np.sqrt(K) * 2.0 ** -24, err.max()
+
+
+def test_non_finite_operand_gives_nan():
+    """g32.h's documented range: an Inf operand makes the split product NaN (not Inf).  Its
+    residual x - h is NaN; and even a residual forced to zero would leave h_a * m_b = Inf * 0 = NaN
+    for a bf16-exact b, whose m and l planes are zero."""
+    a = np.array([np.inf, -np.inf, 1.5], np.float32)
+    b = np.array([2.0, 2.0, 2.0], np.float32)
+    (ah, am, al), (bh, bm, bl) = split3(a), split3(b)
+    assert not np.any(bm) and not np.any(bl)
+    with np.errstate(invalid="ignore"):
+        six = ah * bh + ah * bm + am * bh + ah * bl + al * bh + am * bm
+        forced = ah * bh + ah * bm  # m_a = l_a = 0
+    assert np.isnan(six[:2]).all() and np.isnan(forced[:2]).all() and six[2] == 3.0
