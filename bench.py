@@ -46,6 +46,9 @@ def parse():
                          "graph-launch gap and the cycle's one separate rank launch: 183.9 -> 180.6 us/step vs 8)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--parity", type=int, default=1,
+                    help="N=1, with --cpu-baseline: one fwd+bwd step per mode (bf16, fp32) on batch 0 against "
+                         "the float64 oracle, reported as cpu_baseline.parity_vs_oracle")
     ap.add_argument("--comm", default=None, choices=["auto", "rccl", "torch"],
                     help="N>1 transport: rccl = libdssm.so's own RCCL communicator (the default under the "
                          "nccl backend, strict: a failure raises instead of timing a fallback), torch = "
@@ -366,6 +369,60 @@ def cpu_baseline(seconds: float):
     if "C/OpenMP" in out.get("sample", ""):
         sec = cpu_port.time_steps(D, list(WIDTHS), BS, NEG, budget_s=min(5.0, seconds / 3), use_c=False)
         out["numpy_oracle"] = {k: sec[k] for k in ("value", "unit", "cores", "sample")}
+    return out
+
+
+def parity_vs_oracle(dev, batch, trained: dict) -> dict:
+    """Each mode's measured error against the reference's precision (north star:
+    <= 1e-4 relative on the loss and cosine scores).  Part of the cpu_baseline leg -- the one place
+    bench.py may call the checker: a fresh plan per mode (bf16 perf mode, fp32 parity mode) runs
+    ONE training forward + backward on the bench's first staged C2 batch, and the float64 NumPy
+    oracle (oracle/dssm_oracle.py, new_dssm.py:117-213) runs the same step on the same parameters.
+    Two states: the Glorot init (seed 0, new_dssm.py:118-120) and the bench model's own parameters
+    after its timed steps (`trained`).  Reported, not asserted (the tests hold the bars)."""
+    import torch
+    from oracle import dssm_oracle as O
+    from dssm_amd.model import DSSM
+    cfg = O.OracleConfig(trigram_d=D, widths=list(WIDTHS), query_bs=BS, neg=NEG)
+    states = {"init": O.init_params(cfg, seed=0), "trained": trained}
+    out = {"what": "one fwd+bwd step on bench batch 0 vs the float64 oracle: loss |rel|, cos_sim_raw / prob "
+                   "max |abs| (cos also / max|cos|), per weight gradient max|err| / max|g| (biases excluded: "
+                   "d loss / d b is 0 under batch-stat BN)",
+           "batch": {"rows": int(batch.rows), "nnz": int(batch.nnz)}}
+    ora = {}
+    for sname, p in states.items():
+        cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
+        ora[sname] = (cache, O.backward(cfg, p, cache, np.float64))
+    for dtype in ("bf16", "fp32"):
+        m = DSSM(D, WIDTHS, BS, NEG, dtype=dtype, init=False, device=dev)
+        m.set_fused_w1_adam(False)  # materialise dW1 to read it
+        res = {}
+        for sname, p in states.items():
+            cache, grads = ora[sname]
+            m.load_params(p)
+            m.set_batch(batch)
+            m.forward(True)
+            m.backward()
+            torch.cuda.synchronize(dev)
+            loss, _ = m.loss_accuracy()
+            cos = m.fetch("cos_sim_raw").ravel().astype(np.float64)
+            prob = m.fetch("prob").astype(np.float64)
+            gg = {k: v.cpu().numpy().astype(np.float64) for k, v in m.named_grads().items()}
+            cerr = float(np.abs(cos - cache["cos_sim_raw"]).max())
+            res[sname] = {
+                "loss": round(float(loss), 7), "loss_oracle": round(float(cache["loss"]), 7),
+                "loss_rel_err": float(f"{abs(loss - cache['loss']) / abs(cache['loss']):.3e}"),
+                "cos_abs_err": float(f"{cerr:.3e}"),
+                "cos_err_over_max": float(f"{cerr / np.abs(cache['cos_sim_raw']).max():.3e}"),
+                "prob_abs_err": float(f"{np.abs(prob - cache['prob']).max():.3e}"),
+                "grad_err_over_max": {k: float(f"{np.abs(gg[k] - g).max() / max(np.abs(g).max(), 1e-30):.3e}")
+                                      for k, g in grads.items() if k.startswith("W")},
+            }
+        res["meets_1e-4"] = all(r["loss_rel_err"] <= 1e-4 and r["cos_abs_err"] <= 1e-4
+                                for k, r in res.items() if k in states)
+        out[dtype] = res
+        del m
+        torch.cuda.empty_cache()
     return out
 
 
@@ -1135,6 +1192,13 @@ def main():
             out["cpu_baseline"]["cpu_model"] = cpu_model()
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": repr(e)}
+        if args.parity and rehearse == 1 and feeder is None and args.columns == "zipf":
+            try:  # the checker leg: each mode's error against the float64 oracle on batch 0
+                trained = {k: v.detach().cpu().numpy().copy() for k, v in model.named_params().items()}
+                b0 = synth_batch(D, BS, NEG, seed=1000 + rank * 100003, cols=cols)
+                out["cpu_baseline"]["parity_vs_oracle"] = parity_vs_oracle(dev, b0, trained)
+            except Exception as e:
+                out["cpu_baseline"]["parity_vs_oracle"] = {"error": repr(e)}
     if feeder is not None:
         feeder.close()
     if rank == 0:
