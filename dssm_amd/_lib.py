@@ -211,6 +211,7 @@ _SIGS = {
     "dssm_all_gather": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_all_to_all": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P]),
     "dssm_all_to_allv": (C.c_int, [_P, _P, _P, _P, C.c_int, _P, C.c_int64, C.c_int, _P]),
+    "dssm_all_to_all_tail": (C.c_int, [_P, _P, C.c_int64, C.c_int, _P, C.c_int64, _P]),
     "dssm_rows_pack_u16": (C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P]),
     "dssm_rows_unpack_u16": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _P, _P]),
     "dssm_comm_destroy": (C.c_int, []),

@@ -1818,6 +1818,16 @@ int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void
   return all_to_all_impl(send, recv, count, t, es, (hipStream_t)stream);
 }
 
+int dssm_all_to_all_tail(const void* send, void* recv, int64_t count, int dtype, float* tail, int64_t tail_count,
+                         void* stream) {
+  if (!g_comm) return fail(DSSM_E_INVALID, "communicator not initialised");
+  ncclDataType_t t;
+  size_t es;
+  if (!send || !recv || count < 0 || !nccl_type(dtype, &t, &es) || send == recv || !tail || tail_count <= 0)
+    return fail(DSSM_E_INVALID, "dssm_all_to_all_tail: bad arguments (distinct send / recv, a tail)");
+  return all_to_all_impl(send, recv, count, t, es, (hipStream_t)stream, false, tail, (size_t)tail_count);
+}
+
 // Variable-count all-to-all of the touched-row sparse exchange, with the replicated tail's sum in the
 // same RCCL group (one launch of the group for both).  The rank's own part is a device copy.
 int dssm_all_to_allv(const void* send, const int64_t* send_counts, void* recv, const int64_t* recv_counts,

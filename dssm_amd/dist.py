@@ -105,6 +105,11 @@ class TorchTransport:
     def all_to_all(self, send, recv):
         self._host(lambda s, r: dist.all_to_all_single(r, s), send, recv)
 
+    def all_to_all_tail(self, send, recv, tail):
+        """The all-to-all and the tail's all-reduce (two calls: torch.distributed has no group)."""
+        self.all_to_all(send, recv)
+        self.all_reduce(tail)
+
     def all_to_allv(self, send, send_counts, recv, recv_counts, tail=None):
         """send_counts[j] elements of send to rank j, recv_counts[j] from rank j; tail all-reduced."""
         self._host(lambda s, r: dist.all_to_all_single(r, s, output_split_sizes=list(recv_counts),
@@ -170,9 +175,16 @@ class LibTransport:
         check(self.lib.dssm_all_to_all(ptr(send), ptr(recv), send.numel() // self.world, _dtype_id(send),
                                        stream_ptr()), "all_to_all")
 
+    def all_to_all_tail(self, send, recv, tail):
+        """dssm_all_to_all_tail: the all-to-all with the fp32 tail's all-reduce in the same RCCL group
+        (the call the step graph captures under TAIL_IN_A2A)."""
+        assert send.numel() == recv.numel() and send.numel() % self.world == 0 and tail.dtype == torch.float32
+        check(self.lib.dssm_all_to_all_tail(ptr(send), ptr(recv), send.numel() // self.world, _dtype_id(send),
+                                            ptr(tail), tail.numel(), stream_ptr()), "all_to_all_tail")
+
     def all_to_allv(self, send, send_counts, recv, recv_counts, tail=None):
         """dssm_all_to_allv: grouped sends / receives of per-peer counts, the tail's all-reduce in the
-        same RCCL group."""
+        same RCCL group (tail=None: the sends / receives alone)."""
         W = self.world
         sc, rc = (C.c_int64 * W)(*send_counts), (C.c_int64 * W)(*recv_counts)
         tp, tn, td = (ptr(tail), tail.numel(), _dtype_id(tail)) if tail is not None else (None, 0, 0)
@@ -226,6 +238,29 @@ def selftest(tx, ops, device, rank: int, world: int) -> bool:
                 z = torch.full((k,), float(r + 1), dtype=dt, device=device)
                 tx.all_reduce(z)
                 ok = ok and bool(torch.equal(z, torch.full((k,), float(w * (w + 1) // 2), dtype=dt, device=device)))
+            elif op in ("all_to_all_tail", "all_to_all_tail_captured"):
+                # the mixed point-to-point / collective RCCL group of TAIL_IN_A2A; "captured": recorded
+                # into a graph and replayed twice (each replay re-sums the tail: r + 1, then w(w+1)/2 * w)
+                s = (torch.arange(w, device=device) + 8 * r).to(dt).repeat_interleave(k)
+                d = torch.zeros_like(s)
+                tail = torch.full((k + 3,), float(r + 1), dtype=torch.float32, device=device)
+                want = (torch.arange(w, device=device) * 8 + r).to(dt).repeat_interleave(k)
+                tot = float(w * (w + 1) // 2)
+                if op == "all_to_all_tail":
+                    tx.all_to_all_tail(s, d, tail)
+                    wt = tot
+                else:
+                    side = torch.cuda.Stream(device)
+                    side.wait_stream(torch.cuda.current_stream(device))
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                        tx.all_to_all_tail(s, d, tail)
+                    torch.cuda.current_stream(device).wait_stream(side)
+                    for _ in range(2):
+                        g.replay()
+                    wt = tot * w
+                ok = ok and bool(torch.equal(d, want))
+                ok = ok and bool(torch.equal(tail, torch.full_like(tail, wt)))
             else:
                 raise ValueError(op)
         if device.type == "cuda":
@@ -286,7 +321,7 @@ class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
     def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto", chunks: int = 1,
-                 overlap: bool = False, sparse: bool = False):
+                 overlap: bool = False, sparse: bool = False, tail_in_a2a="auto", verify_sparse: bool = True):
         """comm: "auto" (the library's RCCL communicator on GPUs, torch.distributed as the
         self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
         zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
@@ -296,7 +331,15 @@ class DataParallel:
         ids; the counts exchanged first), the fp32 tail's all-reduce in the same RCCL group; the
         receiver scatters them into the zeroed stage, so Adam sums exactly the dense exchange's
         values.  The counts are known only on the host after the batch is read, so this exchange runs
-        between captured graphs (never inside one)."""
+        between captured graphs (never inside one).
+        tail_in_a2a (zero / bf16 wire): the fp32 tail's all-reduce inside the last all-to-all's RCCL
+        group (plan option TAIL_IN_A2A: one collective launch fewer per step).  "auto" (default):
+        on when that mixed group passes its start-up self-test on every rank, eagerly and captured in
+        a graph (library transport), otherwise the tail is all-reduced separately and the demotion
+        is recorded in .fallbacks; True: strict (a failing self-test raises); False: off.
+        verify_sparse: before the first step, one exchange of a synthetic gradient through the
+        sparse path and the dense all-to-all; the stages must be bit-identical on every rank, or the
+        sparse path is turned off (recorded in .fallbacks)."""
         if overlap:  # removed in round 3 (DESIGN §6): slower; refused before any side effect
             raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
         self.model = model
@@ -348,7 +391,29 @@ class DataParallel:
         self._staged_indices = None
         self._cur = None
         self.sparse_stats = {"steps": 0, "rows_sent": 0, "rows_dense": 0}
+        self.tail_group = False
+        if self.world > 1 and self.mode == "zero" and self.wire == "bf16" and tail_in_a2a is not False:
+            self._select_tail_group(strict=tail_in_a2a is True)
+        if self.sparse and verify_sparse and self.world > 1:
+            self._verify_sparse()
 
+    def _select_tail_group(self, strict: bool):
+        """TAIL_IN_A2A on iff the mixed group passes its self-test on every rank (see __init__)."""
+        dev = self.model.params.device
+        ops = [("all_to_all_tail", torch.bfloat16)]
+        if getattr(self.tx, "capturable", False) and dev.type == "cuda":
+            ops.append(("all_to_all_tail_captured", torch.bfloat16))
+        ok = agree(selftest(self.tx, ops, dev, self.rank, self.world), dev)
+        if ok:
+            self.tail_group = True
+            if hasattr(self.model, "set_option"):  # the plan's captured step (CPU engines: eager only)
+                self.model.set_option("TAIL_IN_A2A", True)
+            return
+        if strict:
+            raise RuntimeError("tail_in_a2a=True but the mixed all-to-all + all-reduce group failed its self-test")
+        note = "mixed all-to-all + tail all-reduce group failed its self-test: tail all-reduced separately"
+        self.fallbacks.append(note)
+        warnings.warn(f"DataParallel: {note}", RuntimeWarning, stacklevel=3)
     @property
     def comm(self) -> str:
         return self.tx.name if self.tx is not None else "none"
@@ -359,6 +424,8 @@ class DataParallel:
         s = f"{self.mode}/{self.wire}" if self.mode == "zero" else self.mode
         if getattr(self, "sparse", False):
             s += " sparse"
+        if getattr(self, "tail_group", False):
+            s += " tail-in-a2a"
         return f"{s} via {self.comm}"
 
     def _transport(self, comm: str, strict_mode: bool):
@@ -380,13 +447,15 @@ class DataParallel:
         return tx
 
     # ---- collectives ----------------------------------------------------------------------
-    def _sparse_exchange(self):
+    def _sparse_exchange(self, ids=None, stats: bool = True):
         """The touched-row gradient all-to-all (see __init__): this rank's batch's W1 rows (the
         columns its CSR holds, torch.unique) split by owner rank, packed with their ids
-        (dssm_rows_pack_u16), the counts all-to-all'd, the packed rows exchanged with the tail's
-        all-reduce in one group, and scattered into the zeroed stage (dssm_rows_unpack_u16)."""
+        (dssm_rows_pack_u16), the counts all-to-all'd, the packed rows exchanged (with the tail's
+        all-reduce in the same group when that group passed its self-test, tail_group; otherwise
+        the tail's all-reduce follows), and scattered into the zeroed stage (dssm_rows_unpack_u16)."""
         m, W = self.model, self.world
-        ids = m.touched_rows(*(self._cur or ()))  # ascending W1 rows the batch touched (int32)
+        if ids is None:
+            ids = m.touched_rows(*(self._cur or ()))  # ascending W1 rows the batch touched (int32)
         S, n, dev = self.rows, self.width, ids.device
         cut = torch.searchsorted(ids, torch.arange(1, W, device=dev, dtype=torch.int32) * S)
         bounds = torch.cat([torch.zeros(1, dtype=cut.dtype, device=dev), cut,
@@ -399,19 +468,59 @@ class DataParallel:
         sbuf = torch.empty(max(1, ids.numel()) * stride, dtype=torch.bfloat16, device=dev)
         m.rows_pack(self.grad_wire, n, ids, sbuf)
         rbuf = torch.empty(max(1, sum(rc)) * stride, dtype=torch.bfloat16, device=dev)
-        g = m.grads
+        tail = m.grads[self.extent:m.n_params]
         self.tx.all_to_allv(sbuf, [c * stride for c in sc], rbuf, [c * stride for c in rc],
-                            tail=g[self.extent:m.n_params])
+                            tail=tail if self.tail_group else None)
+        if not self.tail_group:
+            self.tx.all_reduce(tail)
         self.stage.zero_()
         off = 0
         for i in range(W):  # stage block i: rank i's gradient rows of this rank's shard
             dst = self.stage[i * self.sub:(i + 1) * self.sub]
             m.rows_unpack(rbuf[off * stride:(off + rc[i]) * stride], n, rc[i], self.rank * S, S, dst)
             off += rc[i]
+        if not stats:
+            return
         st = self.sparse_stats
         st["steps"] += 1
         st["rows_sent"] += ids.numel()
         st["rows_dense"] += W * S
+
+    def _verify_sparse(self):
+        """The sparse exchange against the dense all-to-all at the real world size and transport (see
+        __init__): a synthetic bf16 gradient (exact small integers) on a seeded subset of W1 rows,
+        zero elsewhere, exchanged both ways; the two stages must be bit-identical on every rank.
+        The wires, the stage and the gradient tail are cleared afterwards."""
+        m, dev = self.model, self.model.params.device
+        g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
+        nrows = self.world * self.rows
+        touched = torch.randperm(nrows, generator=g)[:max(1, nrows // 3)].sort().values
+        touched = touched[touched * self.width < self.extent].to(torch.int32)
+        n = self.width
+        gw = self.grad_wire[:self.world * self.sub].view(-1, n)
+        gw.zero_()
+        vals = ((torch.arange(n, device=dev) % 7) + 1 + 8 * self.rank).to(torch.bfloat16)
+        gw[touched.to(dev).long()] = vals
+        tail = m.grads[self.extent:m.n_params]
+        tail.fill_(float(self.rank + 1))
+        dense = torch.zeros_like(self.stage)
+        self.tx.all_to_all(self.grad_wire, dense)
+        self.tx.all_reduce(tail)
+        tail_dense = tail.clone()
+        tail.fill_(float(self.rank + 1))
+        self._sparse_exchange(ids=touched.to(dev), stats=False)
+        ok = bool(torch.equal(self.stage, dense)) and bool(torch.equal(tail, tail_dense))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        ok = agree(ok, dev)
+        self.grad_wire.zero_()
+        self.stage.zero_()
+        tail.zero_()
+        if not ok:
+            self.sparse = False
+            note = "sparse exchange differed from the dense all-to-all in its start-up check: dense exchange"
+            self.fallbacks.append(note)
+            warnings.warn(f"DataParallel: {note}", RuntimeWarning, stacklevel=3)
 
     def exchange_before_adam(self):
         if self.world == 1:
@@ -424,9 +533,15 @@ class DataParallel:
             self.tx.all_reduce(g)
         elif self.wire == "bf16":
             blk = self.world * self.sub
+            tail = g[self.extent:self.model.n_params]  # the fp32 tail, replicated
             for p in range(self.chunks):  # chunk p: every rank's bf16 slice of MY shard's sub-chunk p
-                self.tx.all_to_all(self.grad_wire[p * blk:(p + 1) * blk], self.stage[p * blk:(p + 1) * blk])
-            self.tx.all_reduce(g[self.extent:self.model.n_params])  # the fp32 tail, replicated
+                send, recv = self.grad_wire[p * blk:(p + 1) * blk], self.stage[p * blk:(p + 1) * blk]
+                if self.tail_group and p == self.chunks - 1:  # as the captured step (TAIL_IN_A2A)
+                    self.tx.all_to_all_tail(send, recv, tail)
+                else:
+                    self.tx.all_to_all(send, recv)
+            if not self.tail_group:
+                self.tx.all_reduce(tail)
         else:
             self.tx.reduce_scatter_(g, self.shard)
 

@@ -516,6 +516,13 @@ int dssm_allreduce_sum_f32(float* buf, int64_t count, void* stream);
 int dssm_reduce_scatter_sum(const void* send, void* recv, int64_t count, int dtype, void* stream);
 int dssm_all_gather(const void* send, void* recv, int64_t count, int dtype, void* stream);
 int dssm_all_to_all(const void* send, void* recv, int64_t count, int dtype, void* stream);
+/* The same all-to-all with an fp32 all-reduce of tail[0, tail_count) in place inside its RCCL group
+ * (ncclGroupStart; per peer ncclSend / ncclRecv; ncclAllReduce; ncclGroupEnd): exactly the call the
+ * data-parallel step graph captures under plan option TAIL_IN_A2A, exported so the start-up
+ * self-test (dssm_amd/dist.py) runs that mixed point-to-point / collective group at the real world
+ * size, eagerly and captured, before the option is turned on. */
+int dssm_all_to_all_tail(const void* send, void* recv, int64_t count, int dtype, float* tail,
+                         int64_t tail_count, void* stream);
 /* Variable-count all-to-all (the touched-row sparse gradient exchange, dssm_amd/dist.py
  * DataParallel(sparse=True)): send_counts[j] elements of send (consecutive, in rank order) go to
  * rank j, recv_counts[j] elements of recv come from rank j (host arrays of world entries; the own

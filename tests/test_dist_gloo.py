@@ -171,6 +171,11 @@ def _worker(rank, port, out_dir, mode, wire, world, chunks, sparse=False):
         dp = DataParallel(eng, comm="auto", mode=mode, wire=wire, chunks=chunks, sparse=sparse)
         assert dp.world == world and dp.rank == rank and dp.mode == mode and dp.comm == "torch"
         assert dp.wire == (wire if mode == "zero" else "fp32")
+        # the tail's all-reduce rides in the last all-to-all's group when that group passes its
+        # self-test (here: the torch transport's two calls); the sparse path passed its start-up
+        # comparison with the dense all-to-all
+        assert dp.tail_group == (mode == "zero" and wire == "bf16") and dp.sparse == sparse, dp.fallbacks
+        assert not dp.fallbacks and ("tail-in-a2a" in dp.schedule) == dp.tail_group
         eng.set_batch(shard_batch(glob, BS, NEG, rank, world))
         dp.train_step()
         dp.gather_state()
@@ -180,6 +185,38 @@ def _worker(rank, port, out_dir, mode, wire, world, chunks, sparse=False):
         np.save(os.path.join(out_dir, f"loss{rank}.npy"), np.array([eng.loss]))
     finally:
         dist.destroy_process_group()
+
+
+def _broken_sparse_worker(rank, port, world, q):
+    """A sparse exchange that loses rows (rows_unpack drops each packet's last row) must fail the
+    start-up comparison with the dense all-to-all: DataParallel turns sparse off and records it."""
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cfg = O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS, neg=NEG)
+        eng = CpuEngine(O.init_params(cfg, seed=9), world)
+        good = eng.rows_unpack
+        eng.rows_unpack = lambda packed, n, count, row_base, nrows, dst: good(packed, n, max(0, count - 1),
+                                                                              row_base, nrows, dst)
+        dp = DataParallel(eng, comm="auto", mode="zero", wire="bf16", chunks=1, sparse=True)
+        q.put((rank, dp.sparse, list(dp.fallbacks), float(eng.grads.abs().max()),
+               float(dp.stage.float().abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sparse_exchange_self_check_demotes_a_broken_path():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_broken_sparse_worker, args=(r, port, 2, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(60)
+    for rank, sparse, notes, gmax, smax in outs:
+        assert sparse is False and any("sparse exchange differed" in n for n in notes), (rank, notes)
+        assert gmax == 0.0 and smax == 0.0  # the check leaves the gradient tail and the stage cleared
 
 
 def test_sparse_exchange_equals_dense():

@@ -73,6 +73,22 @@ def test_schedule_selftests_world1(tx, sched):
     assert selftest(tx, SCHEDULE_OPS[sched], torch.device("cuda", 0), 0, 1)
 
 
+def test_mixed_group_selftest_world1(tx):
+    """The TAIL_IN_A2A group (dssm_all_to_all_tail: grouped sends / receives + the fp32 tail's
+    all-reduce) through DataParallel's start-up self-test, eager and captured in a graph (the form the
+    step graph replays), and a wrong answer detected."""
+    from dssm_amd.dist import selftest
+    dev = torch.device("cuda", 0)
+    assert selftest(tx, [("all_to_all_tail", torch.bfloat16), ("all_to_all_tail_captured", torch.bfloat16)],
+                    dev, 0, 1)
+
+    class Broken:  # the tail summed twice: the self-test must say no
+        def all_to_all_tail(self, s, d, t):
+            tx.all_to_all_tail(s, d, t)
+            t.mul_(2)
+    assert not selftest(Broken(), [("all_to_all_tail", torch.bfloat16)], dev, 0, 1)
+
+
 def test_collectives_captured_in_graph(tx):
     """The four collectives captured into one hipGraph on a side stream and replayed twice: each
     replay re-runs them on the buffers' current contents."""
