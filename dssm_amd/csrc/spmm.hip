@@ -668,19 +668,25 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
 // fill place a column's entries in an order set by atomics (per-block slot reservations, LDS
 // histogram arrival), which changes the fp32 summation order of dW1 from run to run; this pass
 // rewrites each column [col_ptr[c], col_ptr[c+1]) of (row_in, val_in) sorted by row into
-// (row_out, val_out).  Workgroup b takes columns b + k * grid, k < kSortWaves (one workgroup per column
-// left the launch dominated by 30k workgroup dispatches: most columns hold a handful of entries):
-// * up to kSortWaveMax entries: one WAVE per column.  Its rows are set in the wave's LDS bitmap (a
-//   window of kSortWin rows at a time; a row appears at most once per column), a wave prefix count
-//   of the bitmap words gives every entry its slot, and each lane writes its own entries there;
-// * longer (the Zipf-hot columns): afterwards the whole workgroup per column, the same scheme over
-//   all the waves' bitmap words (a kSortWinWg-row window); the virtual ones column is already in
-//   row order (slot col_ptr[D] + row) and is copied.
-// A column holding a row twice (a CSR row with a repeated column: never from CountVectorizer, but
-// legal input) shows as fewer bits than entries in a window; it is then ranked by (row, value bits,
-// input slot) in O(n^2) work instead -- equal keys are identical entries, so the output is still a
-// function of the batch alone.
-constexpr int kSortWaves = 8;
+// (row_out, val_out).  Every entry's slot is its rank by the key (row, value bits, input slot): a
+// column holding a row once (always, from CountVectorizer) is thus in row order, and a column
+// repeating a row (legal input) still gets an order that is a function of the batch alone (equal
+// keys are identical entries).  Workgroup b (kSortWaves waves) takes columns b + k * grid; wave k
+// handles column b + k * grid by its length n (21k of the C2 batch's 30k columns hold <= 1 entry, all
+// but ~350 hold <= 64):
+// * n <= 1: a copy.  The virtual ones column (already in row order: slot col_ptr[D] + row): a copy;
+// * n <= 64: lane i holds entry i and counts the lanes with a smaller key (n v_readlane steps):
+//   no LDS, no barrier, so a wave with a short column finishes in a few hundred cycles;
+// * n <= kSortWaveMax: the wave's own LDS bitmap of the column's rows (a window of kSortWin rows at a
+//   time), a wave prefix count of the bitmap words gives every entry its slot; wave-synchronous
+//   (fences, no workgroup barrier).  A window with fewer bits than entries (a repeated row) falls
+//   back to the key rank, O(n^2);
+// * longer (the Zipf-hot columns): afterwards the whole workgroup per column, the same bitmap scheme
+//   over all the waves' words (a kSortWinWg-row window) with barriers; only workgroups that hold
+//   such a column run that part (a workgroup-uniform test).
+// Round 6: the previous form ran the bitmap windows (four workgroup barriers each) for every column,
+// empty ones included, in 3751 workgroups of 512 threads: 27.6 us at C2.
+constexpr int kSortWaves = 4;
 constexpr int kSortNT = 64 * kSortWaves;
 constexpr int kSortWords = 4;                        // bitmap words per lane
 constexpr int kSortWin = 64 * 32 * kSortWords;       // rows per window of a wave
@@ -699,6 +705,14 @@ __device__ __forceinline__ int sort_rank_slow(const int* __restrict__ row_in, co
   return p;
 }
 
+// LDS written by some lanes of this wave and read by others: the wave's LDS operations execute in
+// order, so a compiler fence is all the ordering needed
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict__ col_ptr, int D, int rows,
                                                            const int* __restrict__ row_in,
                                                            const float* __restrict__ val_in,
@@ -707,26 +721,45 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
   __shared__ unsigned bits[kSortWaves * 64 * kSortWords];
   __shared__ int wpre[kSortWaves * 64 * kSortWords];
   __shared__ int s_wave[kSortWaves];
-  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  __shared__ int s_long;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   unsigned* wbits = bits + wv * 64 * kSortWords;
   int* wp = wpre + wv * 64 * kSortWords;
+  if (t == 0) s_long = 0;
+  __syncthreads();
   {
     const int c = blockIdx.x + wv * gridDim.x;  // strided: hot columns of nearby ids spread out
-    const int s = c <= D ? col_ptr[c] : 0, e = c <= D ? col_ptr[c + 1] : 0;
-    if (e - s == 1 && lane == 0) {  // in order
-      row_out[s] = row_in[s];
-      val_out[s] = val_in[s];
-    }
-    // the window loop's bounds stay workgroup-uniform (barriers); other waves idle through it
-    const bool sort = e - s > 1 && e - s <= kSortWaveMax;
-    bool dup = false;  // wave-uniform
-    int base = s;
-    for (int w0 = 0; w0 < rows; w0 += kSortWin) {
+    const int s = __builtin_amdgcn_readfirstlane(c <= D ? col_ptr[c] : 0);
+    const int e = __builtin_amdgcn_readfirstlane(c <= D ? col_ptr[c + 1] : 0);
+    const int n = e - s;
+    if (c == D || n == 1) {  // in order already
+      for (int i = s + lane; i < e; i += 64) {
+        row_out[i] = row_in[i];
+        val_out[i] = val_in[i];
+      }
+    } else if (n > 1 && n <= 64) {
+      const bool own = lane < n;
+      const int ri = own ? row_in[s + lane] : 0;
+      const unsigned bi = own ? __float_as_uint(val_in[s + lane]) : 0u;
+      int p = 0;
+      for (int j = 0; j < n; ++j) {
+        const int rj = __builtin_amdgcn_readlane(ri, j);
+        const unsigned bj = (unsigned)__builtin_amdgcn_readlane((int)bi, j);
+        p += rj < ri || (rj == ri && (bj < bi || (bj == bi && j < lane)));
+      }
+      if (own) {
+        row_out[s + p] = ri;
+        val_out[s + p] = __uint_as_float(bi);
+      }
+    } else if (n > 64 && n <= kSortWaveMax) {
+      bool dup = false;  // wave-uniform
+      int base = s;
+      for (int w0 = 0; w0 < rows && !dup; w0 += kSortWin) {
 #pragma unroll
-      for (int j = 0; j < kSortWords; ++j) wbits[lane * kSortWords + j] = 0u;
-      __syncthreads();
-      int nin = 0;  // the column's entries in this window (duplicates: more than its bits)
-      if (sort)
+        for (int j = 0; j < kSortWords; ++j) wbits[lane * kSortWords + j] = 0u;
+        wave_lds_sync();
+        int nin = 0;  // the column's entries in this window (a repeated row: more than its bits)
         for (int i = s + lane; i < e; i += 64) {
           const int r = row_in[i] - w0;
           if (r >= 0 && r < kSortWin) {
@@ -734,66 +767,64 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
             ++nin;
           }
         }
-      __syncthreads();
-      unsigned m[kSortWords];
-      int own = 0;
+        wave_lds_sync();
+        unsigned m[kSortWords];
+        int cnt = 0;
 #pragma unroll
-      for (int j = 0; j < kSortWords; ++j) {
-        m[j] = wbits[lane * kSortWords + j];
-        own += __popc(m[j]);
-      }
-      int inc = own;  // wave inclusive scan of the lanes' counts
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += y;
-      }
-      int run = inc - own;
-#pragma unroll
-      for (int j = 0; j < kSortWords; ++j) {
-        wp[lane * kSortWords + j] = run;
-        run += __popc(m[j]);
-      }
-      const int total = __shfl(inc, 63, 64);
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) nin += __shfl_xor(nin, d, 64);
-      dup = dup || nin != total;
-      __syncthreads();
-      if (sort && !dup)
-        for (int i = s + lane; i < e; i += 64) {
-          const int rr = row_in[i], r = rr - w0;
-          if (r >= 0 && r < kSortWin) {
-            const int wd = r >> 5;
-            const int p = base + wp[wd] + __popc(wbits[wd] & ((1u << (r & 31)) - 1u));
-            row_out[p] = rr;
-            val_out[p] = val_in[i];
-          }
+        for (int j = 0; j < kSortWords; ++j) {
+          m[j] = wbits[lane * kSortWords + j];
+          cnt += __popc(m[j]);
         }
-      base += total;
-      __syncthreads();
-    }
-    if (sort && dup)
-      for (int i = s + lane; i < e; i += 64) {
-        const int ri = row_in[i];
-        const float vi = val_in[i];
-        const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
-        row_out[p] = ri;
-        val_out[p] = vi;
+        int inc = cnt;  // wave inclusive scan of the lanes' counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int y = __shfl_up(inc, d, 64);
+          if (lane >= d) inc += y;
+        }
+        int run = inc - cnt;
+#pragma unroll
+        for (int j = 0; j < kSortWords; ++j) {
+          wp[lane * kSortWords + j] = run;
+          run += __popc(m[j]);
+        }
+        const int total = __shfl(inc, 63, 64);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) nin += __shfl_xor(nin, d, 64);
+        dup = nin != total;
+        wave_lds_sync();
+        if (!dup)
+          for (int i = s + lane; i < e; i += 64) {
+            const int rr = row_in[i], r = rr - w0;
+            if (r >= 0 && r < kSortWin) {
+              const int wd = r >> 5;
+              const int p = base + wp[wd] + __popc(wbits[wd] & ((1u << (r & 31)) - 1u));
+              row_out[p] = rr;
+              val_out[p] = val_in[i];
+            }
+          }
+        base += total;
+        wave_lds_sync();
       }
+      if (dup)  // every entry ranked by its key (earlier windows' slots are rewritten the same way)
+        for (int i = s + lane; i < e; i += 64) {
+          const int ri = row_in[i];
+          const float vi = val_in[i];
+          const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
+          row_out[p] = ri;
+          val_out[p] = vi;
+        }
+    } else if (n > kSortWaveMax && lane == 0) {
+      s_long = 1;
+    }
   }
+  __syncthreads();
+  if (!s_long) return;  // workgroup-uniform
   // the long columns of this workgroup, one at a time with every wave
   for (int k = 0; k < kSortWaves; ++k) {
     const int c = blockIdx.x + k * gridDim.x;
-    if (c > D) break;  // uniform
+    if (c >= D) break;  // uniform (the ones column was copied above)
     const int s = col_ptr[c], e = col_ptr[c + 1];
     if (e - s <= kSortWaveMax) continue;
-    if (c == D) {  // the ones column: slot col_ptr[D] + row already
-      for (int i = s + t; i < e; i += kSortNT) {
-        row_out[i] = row_in[i];
-        val_out[i] = val_in[i];
-      }
-      continue;
-    }
     bool dup = false;
     int base = s;
     for (int w0 = 0; w0 < rows; w0 += kSortWinWg) {
