@@ -266,7 +266,7 @@ __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const floa
 // gradient arena with fp32 atomics and arrive on the column's ticket: the last arrival takes
 // the row with atomic exchanges (read and clear at the coherence point), updates it and
 // re-arms the ticket.  Deterministic mode (heavy_slab): the items store their rows into the slab
-// instead (released before the ticket, acquired by the last arrival) and the last arrival sums
+// instead (write-through stores drained before the ticket, sc1 loads by the last arrival) and the last arrival sums
 // them in item order, so the fp32 sum no longer depends on arrival order.
 // LDS of one heavy-item workgroup: the 4 waves' partial rows, the summed row, the last-arrival flag
 struct HeavyLds {
@@ -314,14 +314,14 @@ __device__ __forceinline__ void heavy_items(const AdamStep& a, float alpha, int 
     if (nit == 1) {
       w1_row_from<WIRE>(a, c, grow, alpha);
     } else {
-      // Deterministic mode: the slab rows are released before this workgroup's arrival and the
-      // last arrival acquires before reading them (common.h).  Atomics mode: every access to the
+      // Deterministic mode: the slab rows are write-through stores drained before this workgroup's
+      // arrival and the last arrival reads them with sc1 loads (common.h last_block_arrival_wt).  Atomics mode: every access to the
       // column's row is a device-scope atomic performed at the coherence point, so the drained adds
       // need no L2 write-back (an agent-scope release here writes back the XCD's L2 per item:
       // measured +20 us on the Adam launch).
       bool last;
       if (a.heavy_slab) {
-        last = last_block_arrival(a.heavy_ticket + c, (unsigned)nit, &s_last);
+        last = last_block_arrival_wt(a.heavy_ticket + c, (unsigned)nit, &s_last);
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed
         __syncthreads();

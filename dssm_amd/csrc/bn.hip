@@ -248,8 +248,8 @@ __global__ __launch_bounds__(1024) void k_bn_sums(const float* __restrict__ Z, i
     for (int k = 0; k < NG; ++k) a += g == 0 ? s_a[k][lane] : s_b[k][lane];
     if (det.slab) {  // deterministic: this row block's slab row, the other tower zero
       double* row = det.slab + (size_t)blockIdx.y * 4 * ldz;
-      row[(size_t)(tower * 2 + g) * ldz + c] = a;
-      row[(size_t)((1 - tower) * 2 + g) * ldz + c] = 0.0;
+      det_st(row + (size_t)(tower * 2 + g) * ldz + c, a);
+      det_st(row + (size_t)((1 - tower) * 2 + g) * ldz + c, 0.0);
     } else {
       __hip_atomic_fetch_add(fsum + (size_t)(tower * 2 + g) * ldz + c, a, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);

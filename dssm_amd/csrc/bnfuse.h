@@ -77,22 +77,30 @@ __device__ __forceinline__ void atomic_add_f64(double* p, double v) {
 #endif
 }
 
-// Every storing thread's slab stores drained, then one lane's release + arrival on ticket[tile]:
-// true (block-uniform) in the workgroup that arrived last of `expected`; it has acquired the other
-// rows (MI355X_MICROARCH.md, inter-workgroup visibility: producer drain + release, consumer acquire).
+// The slab rows are handed from workgroup to workgroup inside one launch WITHOUT agent-scope
+// fences: every slab store is write-through (sc1: an agent-scope relaxed atomic store, the line
+// leaves the XCD's L2) and drained by its wave before the arrival, and every read of a slab row is
+// an sc1 load (an agent-scope relaxed atomic load).  That is MI355X_MICROARCH.md's measured
+// fence-free hand-off form (inter-workgroup visibility, "Valid forms": sc1 stores drained before
+// one lane's agent-scope ticket add, the last adder's sc1 loads).  Round 6: the release fence it
+// replaces wrote back the XCD L2's dirty lines -- the producer's whole output tile -- in every
+// producer workgroup (+6.5 us per statistics launch in deterministic mode).
+__device__ __forceinline__ void det_st(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double det_ld(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every storing thread's write-through slab stores drained, then one lane's arrival on
+// ticket[tile]: true (block-uniform) in the workgroup that arrived last of `expected`.
 __device__ __forceinline__ bool det_arrive(unsigned* ticket, unsigned expected, int* s_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = old == expected - 1;
-    if (last) {
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
     *s_flag = last ? 1 : 0;
   }
   __syncthreads();
@@ -101,8 +109,10 @@ __device__ __forceinline__ bool det_arrive(unsigned* ticket, unsigned expected, 
 
 // Fixed-order sum of nr consecutive slab rows from row r0: dst[k * ld + c] = sum over rows (in
 // order) of src[((r0 + r) * 4 + k) * ld + c], k < 4, c in [c0, c1); 16 loads in flight per thread.
+// A level-2 destination is itself handed off (handoff = true: write-through stores); the final
+// accumulator is read by the next launch (plain stores).
 __device__ __forceinline__ void det_sum_rows(const double* src, int r0, int nr, int ld, int c0, int c1,
-                                             double* dst) {
+                                             double* dst, bool handoff) {
   const int w = c1 - c0;
   for (int i = threadIdx.x; i < 4 * w; i += blockDim.x) {
     const int k = i / w, c = c0 + i - k * w;
@@ -111,11 +121,12 @@ __device__ __forceinline__ void det_sum_rows(const double* src, int r0, int nr, 
     for (int r = 0; r < nr; r += 16) {
       double v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = r + u < nr ? p[(size_t)(r + u) * 4 * ld] : 0.0;
+      for (int u = 0; u < 16; ++u) v[u] = r + u < nr ? det_ld(p + (size_t)(r + u) * 4 * ld) : 0.0;
 #pragma unroll
       for (int u = 0; u < 16; ++u) a += v[u];
     }
-    dst[(size_t)k * ld + c] = a;
+    if (handoff) det_st(dst + (size_t)k * ld + c, a);
+    else dst[(size_t)k * ld + c] = a;
   }
 }
 
@@ -126,14 +137,14 @@ __device__ __forceinline__ void det_publish(const DetAcc& d, int tile, int row, 
   unsigned* tk = d.ticket + tile * kDetTickets;
   const int G = det_group(nrows), ng = (nrows + G - 1) / G;
   if (ng == 1) {
-    if (det_arrive(tk, (unsigned)nrows, s_flag)) det_sum_rows(d.slab, 0, nrows, ld, c0, c1, out);
+    if (det_arrive(tk, (unsigned)nrows, s_flag)) det_sum_rows(d.slab, 0, nrows, ld, c0, c1, out, false);
     return;
   }
   const int g = row / G, gn = min(G, nrows - g * G);
   if (!det_arrive(tk + 1 + g, (unsigned)gn, s_flag)) return;
   double* lvl2 = d.slab + (size_t)nrows * 4 * ld;
-  det_sum_rows(d.slab, g * G, gn, ld, c0, c1, lvl2 + (size_t)g * 4 * ld);
-  if (det_arrive(tk, (unsigned)ng, s_flag)) det_sum_rows(lvl2, 0, ng, ld, c0, c1, out);
+  det_sum_rows(d.slab, g * G, gn, ld, c0, c1, lvl2 + (size_t)g * 4 * ld, true);
+  if (det_arrive(tk, (unsigned)ng, s_flag)) det_sum_rows(lvl2, 0, ng, ld, c0, c1, out, false);
 }
 
 // Forward coefficients of column c (< n), tower t, from the step's sums s = sum z, q = sum z^2
@@ -250,8 +261,8 @@ __device__ __forceinline__ void bn_sums_block(const float* __restrict__ Z, int l
     for (int k = 0; k < NG; ++k) a += s_red[g][k][lane];
     if (det.slab) {  // this row block's partials, the other tower's zero (deterministic mode)
       double* row = det.slab + (size_t)by * 4 * ldz;
-      row[(size_t)(tower * 2 + g) * ldz + c] = a;
-      row[(size_t)((1 - tower) * 2 + g) * ldz + c] = 0.0;
+      det_st(row + (size_t)(tower * 2 + g) * ldz + c, a);
+      det_st(row + (size_t)((1 - tower) * 2 + g) * ldz + c, 0.0);
     } else {
       atomic_add_f64(fsum + (size_t)(tower * 2 + g) * ldz + c, a);
     }

@@ -193,6 +193,25 @@ __device__ __forceinline__ bool last_block_arrival(unsigned* cnt, unsigned arriv
   return *s_flag != 0;
 }
 
+// The same arrival WITHOUT agent-scope fences, for hand-offs whose every store was write-through
+// (sc1: an agent-scope relaxed atomic store) and every read of which is an sc1 load (agent-scope
+// relaxed atomic load): each wave drains its stores, then one lane's agent-scope ticket add; the
+// last adder's workgroup reads after the barrier (MI355X_MICROARCH.md, inter-workgroup visibility,
+// the measured fence-free form).  The release fence of last_block_arrival writes back the whole
+// XCD L2's dirty lines, which is what made the deterministic heavy-column slab cost ~20 us.
+__device__ __forceinline__ bool last_block_arrival_wt(unsigned* cnt, unsigned arrivals, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == arrivals - 1);
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Block b -> tile: tiles [x n/8, (x+1) n/8) go to the blocks b = x (mod 8), which the observed
 // round-robin dispatch places on one XCD (speed only, never correctness: any placement computes
 // the same tiles).  Consecutive tiles share their A rows (a row block's column tiles) or their

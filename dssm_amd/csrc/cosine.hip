@@ -391,7 +391,7 @@ __global__ __launch_bounds__(64 * NW) void k_cosine_loss(
 #pragma unroll
       for (int w = 0; w < NW; ++w) acc += s_bs[(w * 4 + st) * EPL * 64 + c];
       if (fs.bdet.slab)  // deterministic: this workgroup's slab row (both towers: [tower * 2 + stat])
-        fs.bdet.slab[((size_t)blockIdx.x * 4 + st) * ld + c] = acc;
+        det_st(fs.bdet.slab + ((size_t)blockIdx.x * 4 + st) * ld + c, acc);
       else
         atomic_add_f64(fs.bsum + (size_t)st * ld + c, acc);
     }

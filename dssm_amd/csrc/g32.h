@@ -588,10 +588,10 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
           const double s1 = cs[j] + L.red[c * 2], s2 = cq[j] + L.red[c * 2 + 1];
           if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
             double* row = f.det.slab + (size_t)ty * 4 * p.ldc;
-            row[(size_t)(tower * 2) * p.ldc + n] = s1;
-            row[(size_t)(tower * 2 + 1) * p.ldc + n] = s2;
-            row[(size_t)((1 - tower) * 2) * p.ldc + n] = 0.0;
-            row[(size_t)((1 - tower) * 2 + 1) * p.ldc + n] = 0.0;
+            det_st(row + (size_t)(tower * 2) * p.ldc + n, s1);
+            det_st(row + (size_t)(tower * 2 + 1) * p.ldc + n, s2);
+            det_st(row + (size_t)((1 - tower) * 2) * p.ldc + n, 0.0);
+            det_st(row + (size_t)((1 - tower) * 2 + 1) * p.ldc + n, 0.0);
           } else {
             atomic_add_f64(f.out_sum + (size_t)(tower * 2) * p.ldc + n, s1);
             atomic_add_f64(f.out_sum + (size_t)(tower * 2 + 1) * p.ldc + n, s2);

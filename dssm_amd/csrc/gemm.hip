@@ -531,10 +531,10 @@ __device__ __forceinline__ void nt_body(const NtParams& a, const NtFuse& f, int 
         if (n < N) {
           if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
             double* row = f.det.slab + (size_t)ty * 4 * ldc;
-            row[(size_t)(tower * 2) * ldc + n] = cs[j] + sRed[c * 2];
-            row[(size_t)(tower * 2 + 1) * ldc + n] = cq[j] + sRed[c * 2 + 1];
-            row[(size_t)((1 - tower) * 2) * ldc + n] = 0.0;
-            row[(size_t)((1 - tower) * 2 + 1) * ldc + n] = 0.0;
+            det_st(row + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
+            det_st(row + (size_t)(tower * 2 + 1) * ldc + n, cq[j] + sRed[c * 2 + 1]);
+            det_st(row + (size_t)((1 - tower) * 2) * ldc + n, 0.0);
+            det_st(row + (size_t)((1 - tower) * 2 + 1) * ldc + n, 0.0);
           } else {
             double* os = f.out_sum;
             atomic_add_f64(os + (size_t)(tower * 2) * ldc + n, cs[j] + sRed[c * 2]);
@@ -971,8 +971,8 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
         for (int q = 0; q < WM; ++q) v += sRed[(q * 64 + c) * 2 + st];
         if (f.det.slab) {  // deterministic: this row tile's slab row, the other tower zero
           double* row = f.det.slab + (size_t)ty * 4 * ldc;
-          row[(size_t)(tower * 2 + st) * ldc + n] = v;
-          row[(size_t)((1 - tower) * 2 + st) * ldc + n] = 0.0;
+          det_st(row + (size_t)(tower * 2 + st) * ldc + n, v);
+          det_st(row + (size_t)((1 - tower) * 2 + st) * ldc + n, 0.0);
         } else {
           atomic_add_f64(f.out_sum + (size_t)(tower * 2 + st) * ldc + n, v);
         }

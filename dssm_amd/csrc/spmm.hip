@@ -674,7 +674,8 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
 // keys are identical entries).  Workgroup b (kSortWaves waves) takes columns b + k * grid; wave k
 // handles column b + k * grid by its length n (21k of the C2 batch's 30k columns hold <= 1 entry, all
 // but ~350 hold <= 64):
-// * n <= 1: a copy.  The virtual ones column (already in row order: slot col_ptr[D] + row): a copy;
+// * n <= 1: a copy.  The virtual ones column (already in row order: slot col_ptr[D] + row) is copied
+//   by the whole grid first;
 // * n <= 64: lane i holds entry i and counts the lanes with a smaller key (n v_readlane steps):
 //   no LDS, no barrier, so a wave with a short column finishes in a few hundred cycles;
 // * n <= kSortWaveMax: the wave's own LDS bitmap of the column's rows (a window of kSortWin rows at a
@@ -692,6 +693,7 @@ constexpr int kSortWords = 4;                        // bitmap words per lane
 constexpr int kSortWin = 64 * 32 * kSortWords;       // rows per window of a wave
 constexpr int kSortWinWg = kSortWaves * kSortWin;    // rows per window of the workgroup
 constexpr int kSortWaveMax = 512;
+constexpr int kSortU = 8;                            // long columns: entries in flight per thread
 
 // rank of entry i among [s, e) by (row, value bits, slot): the duplicate-row fallback
 __device__ __forceinline__ int sort_rank_slow(const int* __restrict__ row_in, const float* __restrict__ val_in,
@@ -727,16 +729,23 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
   unsigned* wbits = bits + wv * 64 * kSortWords;
   int* wp = wpre + wv * 64 * kSortWords;
   if (t == 0) s_long = 0;
+  {  // the virtual ones column (in row order already), copied by the whole grid
+    const int o0 = col_ptr[D], on = col_ptr[D + 1] - o0;
+    for (int i = blockIdx.x * kSortNT + t; i < on; i += gridDim.x * kSortNT) {
+      row_out[o0 + i] = row_in[o0 + i];
+      val_out[o0 + i] = val_in[o0 + i];
+    }
+  }
   __syncthreads();
   {
     const int c = blockIdx.x + wv * gridDim.x;  // strided: hot columns of nearby ids spread out
-    const int s = __builtin_amdgcn_readfirstlane(c <= D ? col_ptr[c] : 0);
-    const int e = __builtin_amdgcn_readfirstlane(c <= D ? col_ptr[c + 1] : 0);
+    const int s = __builtin_amdgcn_readfirstlane(c < D ? col_ptr[c] : 0);
+    const int e = __builtin_amdgcn_readfirstlane(c < D ? col_ptr[c + 1] : 0);
     const int n = e - s;
-    if (c == D || n == 1) {  // in order already
-      for (int i = s + lane; i < e; i += 64) {
-        row_out[i] = row_in[i];
-        val_out[i] = val_in[i];
+    if (n == 1) {  // in order already
+      if (lane == 0) {
+        row_out[s] = row_in[s];
+        val_out[s] = val_in[s];
       }
     } else if (n > 1 && n <= 64) {
       const bool own = lane < n;
@@ -760,13 +769,18 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
         for (int j = 0; j < kSortWords; ++j) wbits[lane * kSortWords + j] = 0u;
         wave_lds_sync();
         int nin = 0;  // the column's entries in this window (a repeated row: more than its bits)
-        for (int i = s + lane; i < e; i += 64) {
-          const int r = row_in[i] - w0;
-          if (r >= 0 && r < kSortWin) {
-            atomicOr(&wbits[r >> 5], 1u << (r & 31));
+        int rr[kSortWaveMax / 64];  // a lane's entries, every load in flight first
+#pragma unroll
+        for (int u = 0; u < kSortWaveMax / 64; ++u) {
+          const int i = s + lane + 64 * u;
+          rr[u] = i < e ? row_in[i] - w0 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kSortWaveMax / 64; ++u)
+          if (rr[u] >= 0 && rr[u] < kSortWin) {
+            atomicOr(&wbits[rr[u] >> 5], 1u << (rr[u] & 31));
             ++nin;
           }
-        }
         wave_lds_sync();
         unsigned m[kSortWords];
         int cnt = 0;
@@ -792,16 +806,24 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
         for (int d = 32; d >= 1; d >>= 1) nin += __shfl_xor(nin, d, 64);
         dup = nin != total;
         wave_lds_sync();
-        if (!dup)
-          for (int i = s + lane; i < e; i += 64) {
-            const int rr = row_in[i], r = rr - w0;
+        if (!dup) {
+          float vv[kSortWaveMax / 64];
+#pragma unroll
+          for (int u = 0; u < kSortWaveMax / 64; ++u) {
+            const int i = s + lane + 64 * u;
+            vv[u] = i < e ? val_in[i] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < kSortWaveMax / 64; ++u) {
+            const int r = rr[u];
             if (r >= 0 && r < kSortWin) {
               const int wd = r >> 5;
               const int p = base + wp[wd] + __popc(wbits[wd] & ((1u << (r & 31)) - 1u));
-              row_out[p] = rr;
-              val_out[p] = val_in[i];
+              row_out[p] = r + w0;
+              val_out[p] = vv[u];
             }
           }
+        }
         base += total;
         wave_lds_sync();
       }
@@ -822,7 +844,7 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
   // the long columns of this workgroup, one at a time with every wave
   for (int k = 0; k < kSortWaves; ++k) {
     const int c = blockIdx.x + k * gridDim.x;
-    if (c >= D) break;  // uniform (the ones column was copied above)
+    if (c >= D) break;  // uniform (the ones column was copied first)
     const int s = col_ptr[c], e = col_ptr[c + 1];
     if (e - s <= kSortWaveMax) continue;
     bool dup = false;
@@ -832,12 +854,19 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
       for (int j = 0; j < kSortWords; ++j) bits[t * kSortWords + j] = 0u;
       __syncthreads();
       int nin = 0;
-      for (int i = s + t; i < e; i += kSortNT) {
-        const int r = row_in[i] - w0;
-        if (r >= 0 && r < kSortWinWg) {
-          atomicOr(&bits[r >> 5], 1u << (r & 31));
-          ++nin;
+      for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {  // kSortU loads in flight per thread
+        int rr[kSortU];
+#pragma unroll
+        for (int u = 0; u < kSortU; ++u) {
+          const int i = i0 + kSortNT * u;
+          rr[u] = i < e ? row_in[i] - w0 : -1;
         }
+#pragma unroll
+        for (int u = 0; u < kSortU; ++u)
+          if (rr[u] >= 0 && rr[u] < kSortWinWg) {
+            atomicOr(&bits[rr[u] >> 5], 1u << (rr[u] & 31));
+            ++nin;
+          }
       }
       __syncthreads();
       unsigned m[kSortWords];
@@ -858,13 +887,24 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
       dup = dup || nin_total != total;
       __syncthreads();
       if (!dup)
-        for (int i = s + t; i < e; i += kSortNT) {
-          const int rr = row_in[i], r = rr - w0;
-          if (r >= 0 && r < kSortWinWg) {
-            const int wd = r >> 5;
-            const int p = base + wpre[wd] + __popc(bits[wd] & ((1u << (r & 31)) - 1u));
-            row_out[p] = rr;
-            val_out[p] = val_in[i];
+        for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {
+          int rr[kSortU];
+          float vv[kSortU];
+#pragma unroll
+          for (int u = 0; u < kSortU; ++u) {
+            const int i = i0 + kSortNT * u;
+            rr[u] = i < e ? row_in[i] - w0 : -1;
+            vv[u] = i < e ? val_in[i] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < kSortU; ++u) {
+            const int r = rr[u];
+            if (r >= 0 && r < kSortWinWg) {
+              const int wd = r >> 5;
+              const int p = base + wpre[wd] + __popc(bits[wd] & ((1u << (r & 31)) - 1u));
+              row_out[p] = r + w0;
+              val_out[p] = vv[u];
+            }
           }
         }
       base += total;
