@@ -672,6 +672,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       }
     }
   }
+#ifndef DSSM_DIAG_NT_NOB  // diagnostics build (wrong results): the B panel neither loaded nor staged
   {
     const bool bok = bn + brow < N;
     const size_t bbase = (size_t)(bok ? bn + brow : 0) * ldb;
@@ -681,6 +682,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       ub[i] = *reinterpret_cast<const uint4*>(a.BT + ((bok && kg < ldb) ? bbase + kg : 0));
     }
   }
+#endif
   // the epilogue's bias columns, loaded with the operands (a load issued after the MFMA loop would
   // put its latency into the epilogue)
   float bcol[2];
@@ -843,6 +845,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
       }
     }
   }
+#ifndef DSSM_DIAG_NT_NOB
   {
     const bool bok = bn + brow < N;
 #pragma unroll
@@ -853,6 +856,7 @@ __device__ __forceinline__ void nt_wk_body(const NtParams& a, const NtFuse& f, i
             (bok && kg < ldb) ? ub[i] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
+#endif
   if constexpr (FS == 2 && BNB) load_epi();
   __syncthreads();
 #ifdef DSSM_WG_TL

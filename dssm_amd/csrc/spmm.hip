@@ -671,29 +671,37 @@ __global__ __launch_bounds__(256) void k_csc_fill_global(const int* __restrict__
 // (row_out, val_out).  Every entry's slot is its rank by the key (row, value bits, input slot): a
 // column holding a row once (always, from CountVectorizer) is thus in row order, and a column
 // repeating a row (legal input) still gets an order that is a function of the batch alone (equal
-// keys are identical entries).  Workgroup b (kSortWaves waves) takes columns b + k * grid; wave k
-// handles column b + k * grid by its length n (21k of the C2 batch's 30k columns hold <= 1 entry, all
-// but ~350 hold <= 64):
-// * n <= 1: a copy.  The virtual ones column (already in row order: slot col_ptr[D] + row) is copied
-//   by the whole grid first;
-// * n <= 64: lane i holds entry i and counts the lanes with a smaller key (n v_readlane steps):
-//   no LDS, no barrier, so a wave with a short column finishes in a few hundred cycles;
+// keys are identical entries).  Wave g of the grid's G waves takes the kSortCols columns g + k G
+// (lane k loads column k's bounds; interleaved so the Zipf-hot columns spread out) and handles each
+// by its length n (at C2: 8k of the 30k columns hold 1 entry, 10k 2..8, all but ~350 <= 64):
+// * n <= kSortSmall: all the wave's such columns at once, one 8-lane group per column: lane r of
+//   group k holds entry r and counts the group's entries with a smaller key (8 shuffles);
+// * n <= 64, one column at a time: lane i holds entry i and counts the lanes with a smaller key (n
+//   v_readlane steps); no LDS, no barrier;
 // * n <= kSortWaveMax: the wave's own LDS bitmap of the column's rows (a window of kSortWin rows at a
 //   time), a wave prefix count of the bitmap words gives every entry its slot; wave-synchronous
 //   (fences, no workgroup barrier).  A window with fewer bits than entries (a repeated row) falls
 //   back to the key rank, O(n^2);
-// * longer (the Zipf-hot columns): afterwards the whole workgroup per column, the same bitmap scheme
-//   over all the waves' words (a kSortWinWg-row window) with barriers; only workgroups that hold
-//   such a column run that part (a workgroup-uniform test).
-// Round 6: the previous form ran the bitmap windows (four workgroup barriers each) for every column,
-// empty ones included, in 3751 workgroups of 512 threads: 27.6 us at C2.
+// * longer (the Zipf-hot columns): listed, then the whole workgroup per listed column, the same
+//   bitmap scheme over all the waves' words (a kSortWinWg-row window) with barriers.
+// The virtual ones column (already in row order: slot col_ptr[D] + row) is copied by the whole grid.
+// Round 6: the previous form gave every column a wave of 512-thread workgroups and ran the bitmap
+// windows (four workgroup barriers each) for every column, empty ones included: 27.6 us at C2.
 constexpr int kSortWaves = 4;
 constexpr int kSortNT = 64 * kSortWaves;
+constexpr int kSortCols = 8;                         // columns per wave
+constexpr int kSortSmall = 8;                        // longest column of the 8-lane group path
 constexpr int kSortWords = 4;                        // bitmap words per lane
 constexpr int kSortWin = 64 * 32 * kSortWords;       // rows per window of a wave
 constexpr int kSortWinWg = kSortWaves * kSortWin;    // rows per window of the workgroup
 constexpr int kSortWaveMax = 512;
 constexpr int kSortU = 8;                            // long columns: entries in flight per thread
+static_assert(kSortCols * kSortSmall == 64, "one 8-lane group per column");
+#ifndef DSSM_SORT_DIAG  // diagnostics builds (wrong results), bits: 1 skip the group path, 2 the <= 64
+#define DSSM_SORT_DIAG 0  // path, 4 the wave-bitmap path, 8 the workgroup path (tools/sort_bench.py)
+#endif
+
+__host__ __device__ inline int csc_sort_grid(int D) { return (D + kSortWaves * kSortCols - 1) / (kSortWaves * kSortCols); }
 
 // rank of entry i among [s, e) by (row, value bits, slot): the duplicate-row fallback
 __device__ __forceinline__ int sort_rank_slow(const int* __restrict__ row_in, const float* __restrict__ val_in,
@@ -723,12 +731,13 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
   __shared__ unsigned bits[kSortWaves * 64 * kSortWords];
   __shared__ int wpre[kSortWaves * 64 * kSortWords];
   __shared__ int s_wave[kSortWaves];
-  __shared__ int s_long;
+  __shared__ int s_long[kSortWaves * kSortCols];
+  __shared__ int s_nlong;
   const int t = threadIdx.x, lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   unsigned* wbits = bits + wv * 64 * kSortWords;
   int* wp = wpre + wv * 64 * kSortWords;
-  if (t == 0) s_long = 0;
+  if (t == 0) s_nlong = 0;
   {  // the virtual ones column (in row order already), copied by the whole grid
     const int o0 = col_ptr[D], on = col_ptr[D + 1] - o0;
     for (int i = blockIdx.x * kSortNT + t; i < on; i += gridDim.x * kSortNT) {
@@ -736,18 +745,41 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
       val_out[o0 + i] = val_in[o0 + i];
     }
   }
-  __syncthreads();
-  {
-    const int c = blockIdx.x + wv * gridDim.x;  // strided: hot columns of nearby ids spread out
-    const int s = __builtin_amdgcn_readfirstlane(c < D ? col_ptr[c] : 0);
-    const int e = __builtin_amdgcn_readfirstlane(c < D ? col_ptr[c + 1] : 0);
-    const int n = e - s;
-    if (n == 1) {  // in order already
-      if (lane == 0) {
-        row_out[s] = row_in[s];
-        val_out[s] = val_in[s];
-      }
-    } else if (n > 1 && n <= 64) {
+  const int G = gridDim.x * kSortWaves, gw = blockIdx.x * kSortWaves + wv;
+  int cs = 0, cn = 0;  // lane k < kSortCols: column gw + k G
+  if (lane < kSortCols) {
+    const int c = gw + lane * G;
+    if (c < D) {
+      cs = col_ptr[c];
+      cn = col_ptr[c + 1] - cs;
+    }
+  }
+  {  // the short columns, one 8-lane group each (every lane runs the shuffles: no inactive sources)
+    const int q = lane >> 3, r = lane & 7;
+    const int s = __shfl(cs, q, 64), n = __shfl(cn, q, 64);
+    const bool own = n <= kSortSmall && r < n;
+    const int ri = own ? row_in[s + r] : 0;
+    const unsigned bi = own ? __float_as_uint(val_in[s + r]) : 0u;
+    int p = 0;
+#pragma unroll
+    for (int j = 0; j < kSortSmall; ++j) {
+      const int rj = __shfl(ri, (q << 3) + j, 64);
+      const unsigned bj = (unsigned)__shfl((int)bi, (q << 3) + j, 64);
+      p += j < n && (rj < ri || (rj == ri && (bj < bi || (bj == bi && j < r))));
+    }
+    if (own && !(DSSM_SORT_DIAG & 1)) {
+      row_out[s + p] = ri;
+      val_out[s + p] = __uint_as_float(bi);
+    }
+  }
+  for (int k = 0; k < kSortCols; ++k) {  // the longer ones, one at a time (wave-uniform bounds)
+    const int s = __builtin_amdgcn_readlane(cs, k), n = __builtin_amdgcn_readlane(cn, k);
+    const int e = s + n;
+    if (n <= kSortSmall) continue;
+    if ((DSSM_SORT_DIAG & 2) && n <= 64) continue;
+    if ((DSSM_SORT_DIAG & 4) && n > 64 && n <= kSortWaveMax) continue;
+    if ((DSSM_SORT_DIAG & 8) && n > kSortWaveMax) continue;
+    if (n <= 64) {
       const bool own = lane < n;
       const int ri = own ? row_in[s + lane] : 0;
       const unsigned bi = own ? __float_as_uint(val_in[s + lane]) : 0u;
@@ -761,7 +793,7 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
         row_out[s + p] = ri;
         val_out[s + p] = __uint_as_float(bi);
       }
-    } else if (n > 64 && n <= kSortWaveMax) {
+    } else if (n <= kSortWaveMax) {
       bool dup = false;  // wave-uniform
       int base = s;
       for (int w0 = 0; w0 < rows && !dup; w0 += kSortWin) {
@@ -835,18 +867,15 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
           row_out[p] = ri;
           val_out[p] = vi;
         }
-    } else if (n > kSortWaveMax && lane == 0) {
-      s_long = 1;
+    } else if (lane == 0) {
+      s_long[atomicAdd(&s_nlong, 1)] = gw + k * G;  // the workgroup's pass below (order irrelevant)
     }
   }
   __syncthreads();
-  if (!s_long) return;  // workgroup-uniform
-  // the long columns of this workgroup, one at a time with every wave
-  for (int k = 0; k < kSortWaves; ++k) {
-    const int c = blockIdx.x + k * gridDim.x;
-    if (c >= D) break;  // uniform (the ones column was copied first)
+  const int nlong = s_nlong;  // workgroup-uniform
+  for (int k = 0; k < nlong; ++k) {  // the long columns, one at a time with every wave
+    const int c = s_long[k];
     const int s = col_ptr[c], e = col_ptr[c + 1];
-    if (e - s <= kSortWaveMax) continue;
     bool dup = false;
     int base = s;
     for (int w0 = 0; w0 < rows; w0 += kSortWinWg) {
@@ -1183,7 +1212,7 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 
 hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
                            int* row_out, float* val_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_csc_sort_rows, dim3(cdiv(D + 1, kSortWaves)), dim3(kSortNT), 0, s, col_ptr, D,
+  hipLaunchKernelGGL(k_csc_sort_rows, dim3(csc_sort_grid(D)), dim3(kSortNT), 0, s, col_ptr, D,
                      rows, row_in, val_in, row_out, val_out);
   return hipGetLastError();
 }
@@ -1239,7 +1268,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
                        values, rows, D, cursor, col_ptr, out_row, out_val, csc_col);
   }
   if (sort_row)
-    hipLaunchKernelGGL(k_csc_sort_rows, dim3(cdiv(D + 1, kSortWaves)), dim3(kSortNT), 0, s, col_ptr,
+    hipLaunchKernelGGL(k_csc_sort_rows, dim3(csc_sort_grid(D)), dim3(kSortNT), 0, s, col_ptr,
                        D, rows, sort_row, sort_val, csc_row, csc_val);
   return hipGetLastError();
 }
