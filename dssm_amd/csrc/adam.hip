@@ -74,15 +74,6 @@ __device__ __forceinline__ void write_shadow4(const ShadowList& sh, int64_t i, f
     if (rel >= 0 && rel < g.rows * g.cols) {
       const int64_t r = rel / g.cols;
       const int c = (int)(rel - r * g.cols);
-      if (g.plane) {  // fp32 parity mode: the weight's three split planes (g32.h reads them as B)
-        uint2 h, m, l;
-        split3(v, h, m, l);
-        u16* q = g.ptr + r * g.ld + c;
-        *reinterpret_cast<uint2*>(q) = h;
-        *reinterpret_cast<uint2*>(q + g.plane) = m;
-        *reinterpret_cast<uint2*>(q + 2 * g.plane) = l;
-        return;
-      }
       uint2 p;
       p.x = pack2bf(v.x, v.y);
       p.y = pack2bf(v.z, v.w);
@@ -612,15 +603,6 @@ __global__ __launch_bounds__(256) void k_shadow_sync(const float* __restrict__ p
     const int64_t r = rel / g.cols;
     const int c = (int)(rel - r * g.cols);
     const float4 v = *reinterpret_cast<const float4*>(p + g.offset + rel);
-    if (g.plane) {  // fp32 parity mode: the three split planes
-      uint2 h, m, l;
-      split3(v, h, m, l);
-      u16* q = g.ptr + r * g.ld + c;
-      *reinterpret_cast<uint2*>(q) = h;
-      *reinterpret_cast<uint2*>(q + g.plane) = m;
-      *reinterpret_cast<uint2*>(q + 2 * g.plane) = l;
-      continue;
-    }
     uint2 q;
     q.x = pack2bf(v.x, v.y);
     q.y = pack2bf(v.z, v.w);

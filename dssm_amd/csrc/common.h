@@ -156,25 +156,6 @@ __device__ __forceinline__ void store8(u16* p, const float (&x)[8]) {
   *reinterpret_cast<uint4*>(p) = a;
 }
 
-// 4 fp32 values -> their three bf16 planes (x = h + m + l exactly for normal x; the fp32 parity
-// mode's split products, g32.h): each plane pair by one v_cvt_pk_bf16_f32 (RNE, bit-identical to
-// per-element f2bf, without the per-element convert + shift / or re-pairing the scalar form costs)
-// and the residuals from the packed halves (lo << 16, hi & 0xffff0000)
-__device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2& l) {
-  h.x = pack2bf(v.x, v.y);
-  h.y = pack2bf(v.z, v.w);
-  float r0 = v.x - __uint_as_float(h.x << 16), r1 = v.y - __uint_as_float(h.x & 0xffff0000u);
-  float r2 = v.z - __uint_as_float(h.y << 16), r3 = v.w - __uint_as_float(h.y & 0xffff0000u);
-  m.x = pack2bf(r0, r1);
-  m.y = pack2bf(r2, r3);
-  r0 -= __uint_as_float(m.x << 16);
-  r1 -= __uint_as_float(m.x & 0xffff0000u);
-  r2 -= __uint_as_float(m.y << 16);
-  r3 -= __uint_as_float(m.y & 0xffff0000u);
-  l.x = pack2bf(r0, r1);
-  l.y = pack2bf(r2, r3);
-}
-
 template <typename T> __device__ __forceinline__ float to_f(T v);
 template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ float to_f<u16>(u16 v) { return bf2f(v); }

@@ -85,11 +85,6 @@ struct G32Params {
   const float* coef;  // FWD without sums: the A layer's materialised coefficients [4][2][lda]
   int row_split;      // tower boundary (multiple of 64)
   int ones_row, k_per_split;  // DW
-  // FWD / DA in split builds: B's three bf16 planes (h, m, l of common.h split3), each laid out as B
-  // ([K x ldb] / [N x ldb]), bplane elements apart, kept by the optimizer beside W_l: B is staged
-  // without splitting it (round 6; the tile is VALU-issue bound and the split is most of its VALU)
-  const u16* bs;
-  int64_t bplane;
 };
 
 struct G32Fuse {
@@ -129,6 +124,24 @@ struct G32Lds {
   double red[2 * 64 * 2];
 };
 
+// 4 fp32 values -> their three bf16 planes, 4 bf16 each (x = h + m + l exactly for normal x)
+__device__ __forceinline__ void split3(const float4 v, uint2& h, uint2& m, uint2& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  float r[4], q[4];
+  u16 a[4], b[4], c[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = f2bf(x[e]);
+    r[e] = x[e] - bf2f(a[e]);
+    b[e] = f2bf(r[e]);
+    q[e] = r[e] - bf2f(b[e]);
+    c[e] = f2bf(q[e]);
+  }
+  h = make_uint2(a[0] | ((unsigned)a[1] << 16), a[2] | ((unsigned)a[3] << 16));
+  m = make_uint2(b[0] | ((unsigned)b[1] << 16), b[2] | ((unsigned)b[3] << 16));
+  l = make_uint2(c[0] | ((unsigned)c[1] << 16), c[2] | ((unsigned)c[3] << 16));
+}
+
 // NCH: FWD / DA ceil(K / kG32KC) exactly (the launchers dispatch on it); DW kG32DwSplit / kG32KC.
 // WN: waves along the tile's 64 columns (2: 4 waves of 32 x 32; 4: 8 waves of 32 x 16, two per
 // SIMD, for launches that give a CU one tile: a lone wave per SIMD waits out every LDS and barrier
@@ -138,7 +151,6 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
                                          G32Lds& L) {
   constexpr bool A_RK = MODE != G32_DW;
   constexpr bool B_RK = MODE == G32_DA;
-  constexpr bool BPL = kG32Split && MODE != G32_DW;  // B from its pre-split planes (p.bs)
   constexpr bool BN_A = MODE == G32_FWD;
   constexpr int D = kG32Depth, S = kG32Depth + 1;
   constexpr int NT = 128 * WN;    // threads
@@ -169,7 +181,6 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   const int kr_k = t >> 4, kr_c = (t & 15) * 4;
   constexpr int RKH = NT / 8, KRH = NT / 16;
   float4 ra[S][G], rb[S][G];
-  uint2 rbl[BPL ? S : 1][G];  // BPL: B's h plane in rb[].xy, m in rb[].zw, l here
   // Each staged group's row / column part of its address is computed once; a chunk adds its k
   // offset (RK: along the row, a compile-time offset for FWD / DA; KR: k rows of stride ld).  Loads
   // are unconditional (a masked load in a branch makes the compiler drain vmcnt at the merge):
@@ -213,7 +224,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     if constexpr (B_RK) return b_in[h] && k0 + rk_k < kend;
     else return b_in[h] && k0 + kr_k + KRH * h < kend;
   };
-  auto load = [&](int c, float4 (&xa)[G], float4 (&xb)[G], uint2 (&xl)[G]) {
+  auto load = [&](int c, float4 (&xa)[G], float4 (&xb)[G]) {
 #ifdef DSSM_G32_SAMECHUNK  // diagnostics (wrong results): every chunk's loads from chunk 0's lines
     const int k0 = kofs(0);
 #else
@@ -223,7 +234,6 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     const bool tail = (MODE == G32_DW || c == NCH - 1) && k0 + kG32KC > kend;
     const float* pa = p.A + (A_RK ? (size_t)k0 : (size_t)k0 * p.lda);
     const float* pb = p.B + (B_RK ? (size_t)k0 : (size_t)k0 * p.ldb);
-    const u16* qb = BPL ? p.bs + (B_RK ? (size_t)k0 : (size_t)k0 * p.ldb) : nullptr;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       size_t oa = a_off[h], ob = b_off[h];
@@ -234,21 +244,13 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         else ob -= (size_t)max(0, k0 + kr_k + KRH * h - (kdim - 1)) * p.ldb;
       }
       xa[h] = *reinterpret_cast<const float4*>(pa + oa);
-      if constexpr (BPL) {
-        const uint2 bh = *reinterpret_cast<const uint2*>(qb + ob);
-        const uint2 bm = *reinterpret_cast<const uint2*>(qb + p.bplane + ob);
-        xl[h] = *reinterpret_cast<const uint2*>(qb + 2 * p.bplane + ob);
-        xb[h] = make_float4(__uint_as_float(bh.x), __uint_as_float(bh.y), __uint_as_float(bm.x),
-                            __uint_as_float(bm.y));
-      } else {
-        xb[h] = *reinterpret_cast<const float4*>(pb + ob);
-      }
+      xb[h] = *reinterpret_cast<const float4*>(pb + ob);
     }
   };
   // the first D chunks' loads in flight before anything waits
 #pragma unroll
   for (int c = 0; c < D; ++c)
-    if (c < NCH) load(c, ra[c], rb[c], rbl[BPL ? c : 0]);
+    if (c < NCH) load(c, ra[c], rb[c]);
   const int fr = lane & 15, fk = lane >> 4;  // fragment row / column, k group of the lane
   // the epilogue's bias columns (FWD) and pre-BN values / coefficients (DA), loaded with the operands
   float bcol[JN];
@@ -303,7 +305,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   }
   const bool write_a = BN_A && p.a_out != nullptr && tx == 0;
   // chunk c's registers -> LDS image buf (BN + ReLU on A for FWD; the ones column for DW)
-  auto stage = [&](int c, float4 (&xa)[G], float4 (&xb)[G], uint2 (&xl)[G], int buf) {
+  auto stage = [&](int c, float4 (&xa)[G], float4 (&xb)[G], int buf) {
     float* sa = L.img + buf * 2 * kG32Img;
     float* sb = sa + kG32Img;
     const int k0 = kofs(c);
@@ -312,10 +314,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         if (!a_ok(c, h)) xa[h] = z4;
-        if (!b_ok(c, h)) {
-          xb[h] = z4;
-          if constexpr (BPL) xl[h] = make_uint2(0u, 0u);
-        }
+        if (!b_ok(c, h)) xb[h] = z4;
       }
     }
     if constexpr (BN_A) {
@@ -353,13 +352,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         *reinterpret_cast<uint2*>(pa + oa) = x0;
         *reinterpret_cast<uint2*>(pa + kS3Plane + oa) = x1;
         *reinterpret_cast<uint2*>(pa + 2 * kS3Plane + oa) = x2;
-        if constexpr (BPL) {  // B's planes as loaded
-          x0 = make_uint2(__float_as_uint(xb[h].x), __float_as_uint(xb[h].y));
-          x1 = make_uint2(__float_as_uint(xb[h].z), __float_as_uint(xb[h].w));
-          x2 = xl[h];
-        } else {
-          split3(xb[h], x0, x1, x2);
-        }
+        split3(xb[h], x0, x1, x2);
         *reinterpret_cast<uint2*>(pb + ob) = x0;
         *reinterpret_cast<uint2*>(pb + kS3Plane + ob) = x1;
         *reinterpret_cast<uint2*>(pb + 2 * kS3Plane + ob) = x2;
@@ -389,7 +382,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
   // split's, chunks past its rows staged as zeros), so the unrolled pipeline is straight-line code
   // and the compiler's vmcnt waits are exact (a runtime chunk bound around the loads made it drain
   // every load at each branch merge).
-  stage(0, ra[0], rb[0], rbl[0], 0);
+  stage(0, ra[0], rb[0], 0);
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -453,8 +446,8 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         }
       }
 #ifndef DSSM_G32_NOSTAGE
-      if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S], rbl[BPL ? (c + D) % S : 0]);
-      if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], rbl[BPL ? (c + 1) % S : 0], (c + 1) & 1);
+      if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
+      if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
 #endif
       G32_TL(f.tl_slot, 2 + 2 * c);
 #pragma unroll
@@ -474,8 +467,8 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
       continue;
     }
 #ifndef DSSM_G32_NOSTAGE  // diagnostics (wrong results): the loop without its loads and staging
-    if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S], rbl[BPL ? (c + D) % S : 0]);
-    if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], rbl[BPL ? (c + 1) % S : 0], (c + 1) & 1);
+    if (c + D < NCH) load(c + D, ra[(c + D) % S], rb[(c + D) % S]);
+    if (c + 1 < NCH) stage(c + 1, ra[(c + 1) % S], rb[(c + 1) % S], (c + 1) & 1);
 #endif
     G32_TL(f.tl_slot, 2 + 2 * c);
 #if DSSM_G32_FRAGALL

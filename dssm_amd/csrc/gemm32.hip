@@ -69,18 +69,15 @@ bool g32_det_fits(const G32Fuse& f, int ld) {
 }  // namespace
 
 int g32_dw_splits(int rows) { return cdiv(rows, kG32DwSplit); }
-bool g32_split_build() { return kG32Split; }
 
 hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const float* coef,
                           const BnSide* in_from_sums, int row_split, const float* W, int ldw, float* C,
                           int ldc, const float* bias, float* a_out, double* out_sum, hipStream_t s,
-                          const DetAcc* det, const uint16_t* wsplit) {
+                          const DetAcc* det) {
   if (K < 1 || K > kG32MaxK || K > lda || (lda % 4) || (ldw % 4) || (ldc % 4) || (K % 4) || (N % 4) || ldw < N ||
-      (row_split % 64) || (!in_from_sums && !coef) || (kG32Split && !wsplit))
+      (row_split % 64) || (!in_from_sums && !coef))
     return hipErrorInvalidValue;
   G32Params p{M, N, K, Z, lda, W, ldw, C, ldc, bias, a_out, coef, row_split, 0, 0};
-  p.bs = wsplit;
-  p.bplane = (int64_t)K * ldw;
   G32Fuse f{};
   if (in_from_sums) {
     f.in_from_sums = 1;
@@ -106,16 +103,12 @@ hipError_t launch_g32_dw(const G32Params& dw, hipStream_t s) {
 hipError_t launch_g32_pair(int M, int kin, int n, const float* dZ, int lddz, const float* W, int ldw,
                            float* dA, int ldda, const float* z_prev, const float* coef_prev, double* bsum_prev,
                            int row_split, const float* A_prev, int lda_prev, float* slab, float* gw, bool defer,
-                           hipStream_t s, int* deferred_splits, G32Params* dw_out, const DetAcc* det,
-                           const uint16_t* wsplit) {
+                           hipStream_t s, int* deferred_splits, G32Params* dw_out, const DetAcc* det) {
   if (n < 1 || n > kG32MaxK || n > lddz || (lddz % 4) || (ldw % 4) || ldw < n || (ldda % 4) || (lda_prev % 4) ||
-      (n % 4) || (kin % 4) || lda_prev < kin || (row_split % 64) || (kG32Split && !wsplit))
+      (n % 4) || (kin % 4) || lda_prev < kin || (row_split % 64))
     return hipErrorInvalidValue;
-  // dA_{l-1} = dZ_l . W_l^T: W_l [kin x n] row-major is B^T, its rows k-contiguous (its split
-  // planes the same)
-  G32Params a{M, kin, n, dZ, lddz, W, ldw, dA, ldda, nullptr, nullptr, nullptr, row_split, 0, 0};
-  a.bs = wsplit;
-  a.bplane = (int64_t)kin * ldw;
+  // dA_{l-1} = dZ_l . W_l^T: W_l [kin x n] row-major is B^T, its rows k-contiguous
+  const G32Params a{M, kin, n, dZ, lddz, W, ldw, dA, ldda, nullptr, nullptr, nullptr, row_split, 0, 0};
   G32Fuse f{};
   f.out_sum = bsum_prev;
   f.zb = z_prev;

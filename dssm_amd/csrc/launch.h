@@ -150,7 +150,7 @@ hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float*
 hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const float* coef,
                           const BnSide* in_from_sums, int row_split, const float* W, int ldw, float* C,
                           int ldc, const float* bias, float* a_out, double* out_sum, hipStream_t s,
-                          const DetAcc* det = nullptr, const uint16_t* wsplit = nullptr);
+                          const DetAcc* det = nullptr);
 // Backward of layer l: dA_{l-1} = dZ_l . W_l^T (BN_{l-1}'s backward sums from z_prev / coef_prev
 // into bsum_prev); dW_l = [A_{l-1}; 1]^T . dZ_l in kG32DwSplit-row split-K slabs, handed to
 // *dw_out for the next BN-backward apply launch or launched here (then reduced into gw unless
@@ -159,11 +159,7 @@ hipError_t launch_g32_pair(int M, int kin, int n, const float* dZ, int lddz, con
                            float* dA, int ldda, const float* z_prev, const float* coef_prev, double* bsum_prev,
                            int row_split, const float* A_prev, int lda_prev, float* slab, float* gw, bool defer,
                            hipStream_t s, int* deferred_splits, G32Params* dw_out = nullptr,
-                           const DetAcc* det = nullptr, const uint16_t* wsplit = nullptr);
-// The g32.h tiles' build: true when their products run on the bf16 matrix cores from split planes
-// (DSSM_G32_SPLIT, the default); the forward / dA launchers then read W_l's three planes (wsplit,
-// [K x ldw] each, K * ldw elements apart), which the optimizer keeps beside W_l (ShadowSeg.plane).
-bool g32_split_build();
+                           const DetAcc* det = nullptr);
 hipError_t launch_g32_dw(const G32Params& dw, hipStream_t s);
 int g32_dw_splits(int rows);
 
@@ -254,8 +250,6 @@ struct ShadowSeg {
   uint16_t* ptr;   // bf16 shadow [rows x ld]
   uint16_t* tptr;  // optional transposed bf16 shadow [cols x tld] (null: none)
   int tld;
-  int64_t plane;   // > 0: ptr holds the fp32 parity mode's three bf16 split planes (h, m, l: x = h + m + l,
-                   // common.h split3) of the weight, each [rows x ld], plane elements apart; no tptr
 };
 struct ShadowList {
   int count;

@@ -54,8 +54,6 @@ struct Layout {
   size_t tickets[DSSM_MAX_LAYERS][2];
   size_t coef[DSSM_MAX_LAYERS], bcoef[DSSM_MAX_LAYERS], bmean[DSSM_MAX_LAYERS],
       bvar[DSSM_MAX_LAYERS], shadow[DSSM_MAX_LAYERS], shadowT[DSSM_MAX_LAYERS];
-  // fp32 parity mode, split tile build (g32.h): W_l's three bf16 split planes [3][in x n], l >= 1
-  size_t wsplit[DSSM_MAX_LAYERS] = {};
   size_t dw_slab[DSSM_MAX_LAYERS] = {}, partial, cos_raw, cos_sim, prob, qnorm, loss_j, loss;
   size_t csc_scratch, col_ptr, csc_row, csc_val, csc_col, adam_state;
   size_t sort_row, sort_val, heavy_slab;  // deterministic mode: transpose scratch, heavy partial rows
@@ -144,7 +142,6 @@ void make_layout(const dssm_config* c, Layout& Lt) {
     Lt.shadow[l] = Lt.bf16 ? take((size_t)Lt.in_dim[l] * ld * 2) : 0;
     // transposed bf16 weights [n_l x ldp(in)] for the whole-K forward GEMM (layers >= 2)
     Lt.shadowT[l] = (Lt.bf16 && l > 0) ? take((size_t)Lt.n[l] * Lt.ldp[l - 1] * 2) : 0;
-    Lt.wsplit[l] = (!Lt.bf16 && l > 0 && dssm::g32_split_build()) ? take((size_t)3 * Lt.in_dim[l] * Lt.n[l] * 2) : 0;
     max_part = std::max(max_part, dssm::bn_partial_floats(Lt.R, Lt.ldp[l], Lt.BS));
   }
   Lt.partial = take(max_part * 4);
@@ -389,27 +386,10 @@ struct dssm_plan {
       if (!(Lt.bf16 ? wholek(l) : nt32(l))) return false;
     return true;
   }
-  // The weight copies the optimizer keeps beside the fp32 masters: bf16 mode, every layer's bf16
-  // shadow (seg[0] = W1's, which the data-parallel wire rebuilds); fp32 parity mode with the split
-  // tile build, the three split planes of W_l, l >= 1 (g32.h's B operand; W1 is gathered fp32).
   dssm::ShadowList shadows() {
     dssm::ShadowList s;
     s.count = 0;
-    if (!Lt.bf16) {
-      for (int l = 1; l < Lt.L; ++l) {
-        if (!Lt.wsplit[l]) continue;
-        dssm::ShadowSeg& g = s.seg[s.count++];
-        g.offset = Lt.fc_off[l];
-        g.rows = Lt.in_dim[l];
-        g.cols = Lt.n[l];
-        g.ld = Lt.n[l];
-        g.ptr = at<uint16_t>(Lt.wsplit[l]);
-        g.tptr = nullptr;
-        g.tld = 0;
-        g.plane = (int64_t)Lt.in_dim[l] * Lt.n[l];
-      }
-      return s;
-    }
+    if (!Lt.bf16) return s;
     for (int l = 0; l < Lt.L; ++l) {
       dssm::ShadowSeg& g = s.seg[s.count++];
       g.offset = Lt.fc_off[l];
@@ -419,11 +399,9 @@ struct dssm_plan {
       g.ptr = at<uint16_t>(Lt.shadow[l]);
       g.tptr = l > 0 ? at<uint16_t>(Lt.shadowT[l]) : nullptr;
       g.tld = Lt.ldp[l - (l > 0 ? 1 : 0)];
-      g.plane = 0;
     }
     return s;
   }
-  const uint16_t* wsplit(int l) const { return Lt.wsplit[l] ? at<uint16_t>(Lt.wsplit[l]) : nullptr; }
 };
 
 #ifndef DSSM_GRAPH_UPLOAD
@@ -646,7 +624,7 @@ int dssm_plan_set_batch(dssm_plan* P, const int32_t* indptr, const int32_t* indi
 
 int dssm_plan_sync_shadows(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
-  // bf16 mode: the bf16 shadows; fp32 mode (split tile build): W_l's split planes; else nothing
+  if (!P->Lt.bf16) return DSSM_OK;
   HIP_TRY(dssm::launch_shadow_sync(P->p, P->shadows(), (hipStream_t)stream));
   return DSSM_OK;
 }
@@ -737,7 +715,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         HIP_TRY(dssm::launch_g32_fwd(Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
                                      P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->p + Lt.fc_off[l], Lt.n[l],
                                      P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<float>(Lt.A[l - 1]),
-                                     P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr, P->wsplit(l)));
+                                     P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr));
         continue;
       }
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
@@ -939,7 +917,7 @@ static int backward_impl(dssm_plan* P, void* stream) {
             P->at<float>(Lt.dA[l - 1]), Lt.ldp[l - 1], P->at<float>(Lt.Z[l - 1]), P->at<float>(Lt.coef[l - 1]),
             P->at<double>(Lt.bsum[l - 1]), Lt.BS, P->at<float>(Lt.A[l - 1]), Lt.ldp[l - 1],
             P->at<float>(Lt.dw_slab[l]), gw, defer_slabs, s, &P->dw_deferred[l], host_dw ? &dw32 : nullptr,
-            P->deterministic() ? &bprev.bdet : nullptr, P->wsplit(l)));
+            P->deterministic() ? &bprev.bdet : nullptr));
       const float* handed = Lt.bf16 ? dw.C : dw32.C;
       dw_pending = host_dw && handed != nullptr;
       if (dw_pending && !defer_slabs && handed != gw) dw_reduce_to = gw;
@@ -1132,16 +1110,14 @@ int dssm_plan_adam(dssm_plan* P, float grad_scale, void* stream) {
     a.gstride = P->sub_elems();
     // the tail's gradient is consumed here; clear it (b1's row is the gradient pass's atomic target)
     if (wire_gradient_pass(P)) a.clear_from = we;
-    if (sh.count && sh.seg[0].offset == Lt.fc_off[0]) {  // W1's shadow: from the wire
-      for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
-      sh.count -= 1;
-    }
+    for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];  // W1's shadow: from the wire
+    if (sh.count) sh.count -= 1;
   }
   if (P->fused_w1_adam()) {
     if (P->grads_clean) return fail(DSSM_E_INVALID, "fused W1 Adam needs backward() of this step first");
     fill_w1_roles(P, a);
     a.d4_begin = rest / 4;
-    if (sh.count && sh.seg[0].offset == Lt.fc_off[0]) {  // W1's bf16 shadow is written by the fused rows
+    if (sh.count) {  // W1's shadow is written by the fused rows
       for (int i = 1; i < sh.count; ++i) sh.seg[i - 1] = sh.seg[i];
       sh.count -= 1;
     }
