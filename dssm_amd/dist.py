@@ -503,13 +503,14 @@ class DataParallel:
         gw[touched.to(dev).long()] = vals
         tail = m.grads[self.extent:m.n_params]
         tail.fill_(float(self.rank + 1))
-        dense = torch.zeros_like(self.stage)
-        self.tx.all_to_all(self.grad_wire, dense)
+        blk = self.world * self.sub  # the exchanged block (the wire may carry a few slack elements)
+        dense = torch.zeros_like(self.stage[:blk])
+        self.tx.all_to_all(self.grad_wire[:blk], dense)
         self.tx.all_reduce(tail)
         tail_dense = tail.clone()
         tail.fill_(float(self.rank + 1))
         self._sparse_exchange(ids=touched.to(dev), stats=False)
-        ok = bool(torch.equal(self.stage, dense)) and bool(torch.equal(tail, tail_dense))
+        ok = bool(torch.equal(self.stage[:blk], dense)) and bool(torch.equal(tail, tail_dense))
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         ok = agree(ok, dev)

@@ -61,7 +61,7 @@ class CpuEngine:
 
     def dp_wire_size(self, world, chunks):
         w, p, rows, n = self._geo(world, chunks)
-        return w * p * rows * n
+        return w * p * rows * n + 8  # the device wire's 8-element slack after the last row (dssm_plan_dp_wire_size)
 
     def set_dp_wire(self, world, rank, chunks, gw, st, pw):
         self.gwire, self.stage, self.pwire = gw, st, pw
@@ -105,13 +105,13 @@ class CpuEngine:
     def rows_pack(self, src, n, rows, out):
         k = rows.numel()
         o = out[:k * (n + 4)].view(k, n + 4)
-        o[:, 4:] = src.view(-1, n)[rows.long()]
+        o[:, 4:] = src[:src.numel() // n * n].view(-1, n)[rows.long()]
         o.view(torch.int32)[:, 0] = rows
 
     def rows_unpack(self, packed, n, count, row_base, nrows, dst):
         pk = packed[:count * (n + 4)].view(count, n + 4)
         ids = pk.view(torch.int32)[:, 0].long() - row_base
-        dst.view(-1, n)[ids] = pk[:, 4:]
+        dst[:dst.numel() // n * n].view(-1, n)[ids] = pk[:, 4:]
 
     def forward(self, train=True):
         self._train = bool(train)

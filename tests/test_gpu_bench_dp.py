@@ -32,7 +32,8 @@ def test_bench_gpus2_spawns_ranks_and_checks_them():
     d = _run([])
     assert d["n_gpus"] == 2 and d["steps"] == 4 and d["warmup"] == 1
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 2048
-    assert d["config"]["dp_exchange"] == "zero/bf16 via torch"
+    # the tail's all-reduce rides in the last all-to-all's group once that group passed its self-test
+    assert d["config"]["dp_exchange"] == "zero/bf16 tail-in-a2a via torch"
     assert not d["config"]["dp_fallbacks"]
     chk = d["dp_check"]
     assert chk["world"] == 2 and chk["ranks_identical"] is True and chk["finite"] is True
@@ -52,7 +53,7 @@ def test_bench_gpus2_spawns_ranks_and_checks_them():
     # the third child: the touched-row sparse gradient all-to-all (DataParallel(sparse=True))
     sp = d["dp_alt_sparse"]
     assert "error" not in sp, sp
-    assert sp["dp_exchange"] == "zero/bf16 sparse via torch" and sp["value"] > 0
+    assert sp["dp_exchange"] == "zero/bf16 sparse tail-in-a2a via torch" and sp["value"] > 0
     assert sp["dp_check"]["ranks_identical"] is True and sp["dp_check"]["world"] == 2
     assert 0 < sp["dp_sparse"]["rows_sent_frac"] < 1 and sp["dp_sparse"]["steps"] >= 4
 
