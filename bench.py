@@ -99,6 +99,11 @@ def parse():
                          "the line's fp32_mode key")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="plan option DETERMINISTIC: run-to-run bit-identical steps (not the headline)")
+    ap.add_argument("--fwd32", type=int, default=0,
+                    help="bf16 plan option FWD32: the forward at the reference's fp32 precision (fp32 W1 "
+                         "gathers, the fp32-parity tiles for layers >= 2), the bf16 backward and optimizer")
+    ap.add_argument("--fwd32-line", type=int, default=1,
+                    help="N=1 bf16 headline: also time the FWD32 mode (child process) and report it as fwd32_mode")
     ap.add_argument("--det-line", type=int, default=1,
                     help="also time the deterministic mode (child process) and report it beside the line")
     ap.add_argument("--fwd-only", type=int, default=1,
@@ -375,7 +380,8 @@ def cpu_baseline(seconds: float):
 def parity_vs_oracle(dev, batch, trained: dict) -> dict:
     """Each mode's measured error against the reference's precision (north star:
     <= 1e-4 relative on the loss and cosine scores).  Part of the cpu_baseline leg -- the one place
-    bench.py may call the checker: a fresh plan per mode (bf16 perf mode, fp32 parity mode) runs
+    bench.py may call the checker: a fresh plan per mode (bf16 perf mode, bf16 with the fp32-accurate
+    forward of plan option FWD32, fp32 parity mode) runs
     ONE training forward + backward on the bench's first staged C2 batch, and the float64 NumPy
     oracle (oracle/dssm_oracle.py, new_dssm.py:117-213) runs the same step on the same parameters.
     Two states: the Glorot init (seed 0, new_dssm.py:118-120) and the bench model's own parameters
@@ -393,9 +399,12 @@ def parity_vs_oracle(dev, batch, trained: dict) -> dict:
     for sname, p in states.items():
         cache, _ = O.forward(cfg, p, O.make_ema(cfg), batch.as_dict(), True, np.float64)
         ora[sname] = (cache, O.backward(cfg, p, cache, np.float64))
-    for dtype in ("bf16", "fp32"):
+    for mode in ("bf16", "bf16_fwd32", "fp32"):
+        dtype = "fp32" if mode == "fp32" else "bf16"
         m = DSSM(D, WIDTHS, BS, NEG, dtype=dtype, init=False, device=dev)
         m.set_fused_w1_adam(False)  # materialise dW1 to read it
+        if mode == "bf16_fwd32":
+            m.set_option("FWD32", True)
         res = {}
         for sname, p in states.items():
             cache, grads = ora[sname]
@@ -420,7 +429,7 @@ def parity_vs_oracle(dev, batch, trained: dict) -> dict:
             }
         res["meets_1e-4"] = all(r["loss_rel_err"] <= 1e-4 and r["cos_abs_err"] <= 1e-4
                                 for k, r in res.items() if k in states)
-        out[dtype] = res
+        out[mode] = res
         del m
         torch.cuda.empty_cache()
     return out
@@ -444,7 +453,8 @@ def child_mode_line(args, extra) -> dict:
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--batches", str(args.batches), "--cpu-baseline", "0",
-           "--fwd-only", "0", "--fp32-line", "0", "--det-line", "0", "--probes", str(args.probes)] + extra
+           "--fwd-only", "0", "--fp32-line", "0", "--det-line", "0", "--fwd32-line", "0",
+           "--probes", str(args.probes)] + extra
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -819,6 +829,8 @@ def main():
     model = DSSM(D, WIDTHS, BS, NEG, dtype=args.dtype, seed=0, device=dev)
     if args.deterministic:
         model.set_option("DETERMINISTIC", True)
+    if args.fwd32:
+        model.set_option("FWD32", True)
     for opt in args.plan_option:
         name, val = opt.split("=")
         model.set_option(name, bool(int(val)))
@@ -1186,6 +1198,10 @@ def main():
     if (args.det_line and not args.deterministic and rank == 0 and world == 1 and rehearse == 1
             and args.dtype == "bf16" and feeder is None and args.columns == "zipf"):
         out["deterministic_mode"] = deterministic_mode_line(args)
+    if (args.fwd32_line and not args.fwd32 and rank == 0 and world == 1 and rehearse == 1
+            and args.dtype == "bf16" and feeder is None and args.columns == "zipf"):
+        # the bf16 plan with the forward at the reference's precision (plan option FWD32)
+        out["fwd32_mode"] = child_mode_line(args, ["--fwd32", "1"])
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -30,12 +30,12 @@ GRAPH_FWD_BWD, GRAPH_ADAM, GRAPH_SHADOWS, GRAPH_WIRE_SHADOWS = 1, 2, 4, 8
 # dssm_plan_schedule bits (include/dssm.h DSSM_SCHED_*)
 SCHED_BITS = {"FUSED_STATS": 1, "MERGED_CSC": 2, "HEAVY_IN_ADAM": 4, "FUSED_W1_ADAM": 8,
               "WHOLEK": 16, "DW_IN_APPLY": 32, "SCATTER_IN_COS": 64, "DETERMINISTIC": 128, "NT32": 256,
-              "BNB_IN_PAIR": 512}
+              "BNB_IN_PAIR": 512, "FWD32": 1024}
 # dssm_plan_set_option ids (include/dssm.h DSSM_OPT_*)
 OPTIONS = {k: i for i, k in enumerate(["FUSED_STATS", "MERGED_CSC", "HEAVY_IN_ADAM", "SCATTER_IN_COS",
                                          "DW_IN_APPLY", "WIRE_GRAD_PASS", "CSC_RANK", "DETERMINISTIC",
                                          "FUSED_W1_ADAM", "RANK_IN_ADAM", "MEMCPY_NODES", "BNB_IN_PAIR",
-                                         "TAIL_IN_A2A"])}
+                                         "TAIL_IN_A2A", "FWD32"])}
 
 
 class DssmError(RuntimeError):

@@ -85,6 +85,7 @@ struct G32Params {
   const float* coef;  // FWD without sums: the A layer's materialised coefficients [4][2][lda]
   int row_split;      // tower boundary (multiple of 64)
   int ones_row, k_per_split;  // DW
+  u16* a_out16;       // FWD (bf16 plan, DSSM_OPT_FWD32): relu(BN(A)) written bf16 instead of a_out
 };
 
 struct G32Fuse {
@@ -304,6 +305,7 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
     __syncthreads();
   }
   const bool write_a = BN_A && p.a_out != nullptr && tx == 0;
+  const bool write_a16 = BN_A && p.a_out16 != nullptr && tx == 0;
   // chunk c's registers -> LDS image buf (BN + ReLU on A for FWD; the ones column for DW)
   auto stage = [&](int c, float4 (&xa)[G], float4 (&xb)[G], int buf) {
     float* sa = L.img + buf * 2 * kG32Img;
@@ -331,6 +333,8 @@ __device__ __forceinline__ void g32_body(const G32Params& p, const G32Fuse& f, i
         v.w = fmaxf(bn_affine(v.w, inv.w, sh.w), 0.f);
         const int r = bm + rk_r + RKH * h;
         if (write_a && r < M && k < p.lda) *reinterpret_cast<float4*>(p.a_out + (size_t)r * p.lda + k) = v;
+        if (write_a16 && r < M && k < p.lda)  // the bf16 NT tile's rounding of the same activation
+          *reinterpret_cast<uint2*>(p.a_out16 + (size_t)r * p.lda + k) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
       }
     }
     if constexpr (MODE == G32_DW) {

@@ -73,11 +73,12 @@ int g32_dw_splits(int rows) { return cdiv(rows, kG32DwSplit); }
 hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const float* coef,
                           const BnSide* in_from_sums, int row_split, const float* W, int ldw, float* C,
                           int ldc, const float* bias, float* a_out, double* out_sum, hipStream_t s,
-                          const DetAcc* det) {
+                          const DetAcc* det, uint16_t* a_out16) {
   if (K < 1 || K > kG32MaxK || K > lda || (lda % 4) || (ldw % 4) || (ldc % 4) || (K % 4) || (N % 4) || ldw < N ||
       (row_split % 64) || (!in_from_sums && !coef))
     return hipErrorInvalidValue;
   G32Params p{M, N, K, Z, lda, W, ldw, C, ldc, bias, a_out, coef, row_split, 0, 0};
+  p.a_out16 = a_out16;
   G32Fuse f{};
   if (in_from_sums) {
     f.in_from_sums = 1;

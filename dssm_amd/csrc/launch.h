@@ -150,7 +150,7 @@ hipError_t launch_splitk_reduce(const float* slab, int splits, int64_t n, float*
 hipError_t launch_g32_fwd(int M, int N, int K, const float* Z, int lda, const float* coef,
                           const BnSide* in_from_sums, int row_split, const float* W, int ldw, float* C,
                           int ldc, const float* bias, float* a_out, double* out_sum, hipStream_t s,
-                          const DetAcc* det = nullptr);
+                          const DetAcc* det = nullptr, uint16_t* a_out16 = nullptr);
 // Backward of layer l: dA_{l-1} = dZ_l . W_l^T (BN_{l-1}'s backward sums from z_prev / coef_prev
 // into bsum_prev); dW_l = [A_{l-1}; 1]^T . dZ_l in kG32DwSplit-row split-K slabs, handed to
 // *dw_out for the next BN-backward apply launch or launched here (then reduced into gw unless

@@ -256,6 +256,7 @@ struct dssm_plan {
       0,  // MEMCPY_NODES: diagnostics: data-parallel device copies as hipMemcpyAsync nodes
       1,  // BNB_IN_PAIR: the last layer's BN backward formed in the dA pair's A staging
       0,  // TAIL_IN_A2A: data-parallel graph: the tail's all-reduce in the last all-to-all's RCCL group
+      0,  // FWD32: bf16 plan: the forward on fp32 weights / tiles (fp32-accurate loss, cosine), bf16 backward
   };
   bool on(int o) const { return opt[o] != 0; }
   // Captured train steps (hipGraph) and, while capturing, the slot whose probe events to record.
@@ -322,7 +323,15 @@ struct dssm_plan {
   // Layer l (>= 1) runs its forward/dA GEMMs on the bf16 NT kernel (fused BN staging).
   bool wholek(int l) const { return Lt.bf16 && l > 0 && Lt.ldp[l - 1] <= 512; }
   // fp32 parity mode: layer l (>= 1) on the fused fp32 MFMA tiles (g32.h: K <= 320 both ways)
-  bool nt32(int l) const { return !Lt.bf16 && l > 0 && Lt.in_dim[l] <= 320 && Lt.n[l] <= 320; }
+  bool g32_fits(int l) const { return l > 0 && Lt.in_dim[l] <= 320 && Lt.n[l] <= 320; }
+  bool nt32(int l) const { return !Lt.bf16 && g32_fits(l); }
+  // bf16 plan with the fp32-accurate forward (DSSM_OPT_FWD32): the SpMM on the fp32 W1 masters, the
+  // layers >= 2 forward on the g32 tiles and fp32 W_l; not with the data-parallel bf16 wire (W1's fp32
+  // rows outside a rank's shard are stale there)
+  bool fwd32() const { return Lt.bf16 && on(DSSM_OPT_FWD32) && !pwire; }
+  const void* fwd_weight0() const { return fwd32() ? (const void*)(p + Lt.fc_off[0]) : weight(0); }
+  bool fwd_weight0_bf16() const { return fwd32() ? false : Lt.bf16; }
+  int fwd_weight0_ld() const { return fwd32() ? Lt.n[0] : weight_ld(0); }
   const float* bias(int l) const { return p + Lt.fc_off[l] + (int64_t)Lt.in_dim[l] * Lt.n[l]; }
   dssm::BnSide bn_side(int l) const {
     dssm::BnSide b{};
@@ -383,7 +392,7 @@ struct dssm_plan {
     for (int l = 0; l < Lt.L; ++l)
       if (Lt.ldp[l] > 512) return false;
     for (int l = 1; l < Lt.L; ++l)
-      if (!(Lt.bf16 ? wholek(l) : nt32(l))) return false;
+      if (!(Lt.bf16 ? wholek(l) && (!fwd32() || g32_fits(l)) : nt32(l))) return false;
     return true;
   }
   dssm::ShadowList shadows() {
@@ -638,6 +647,8 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   const dssm::BnTowers tw{Lt.BS, Lt.R};
   const bool fused = train && P->fused_stats();
   const bool merged = train && P->merged_csc();
+  if (train && P->fwd32() && !fused)
+    return fail(DSSM_E_UNSUPPORTED, "FWD32 trains on the fused-statistics schedule only");
   if (train) {
     // The CSC transpose of the batch (dW1's operand).  Fused-statistics steps: its first launch
     // also clears the step's BN sums; merged: its scan / scatter ride in later launches.
@@ -658,7 +669,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
   P->probe_begin(DSSM_PROBE_SPMM_FWD, s);
   if (merged) {  // the SpMM rows share their launch with the column scan
     HIP_TRY(dssm::launch_spmm_scan(P->indptr, P->indices, P->values, Lt.R,
-                                   P->weight(0), Lt.bf16, P->weight_ld(0), Lt.n[0], P->bias(0),
+                                   P->fwd_weight0(), P->fwd_weight0_bf16(), P->fwd_weight0_ld(), Lt.n[0], P->bias(0),
                                    P->at<float>(Lt.Z[0]), Lt.ldp[0], Lt.D, Lt.max_nnz,
                                    P->at<int>(Lt.csc_scratch), P->at<int>(Lt.col_ptr), s));
   } else {
@@ -681,9 +692,9 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
         }
       }
     }
-    HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->weight(0), Lt.bf16,
-                                P->weight_ld(0), Lt.n[0], P->bias(0), P->at<float>(Lt.Z[0]),
-                                Lt.ldp[0], s, train ? nullptr : &ec));
+    HIP_TRY(dssm::launch_spmm_fwd(P->indptr, P->indices, P->values, Lt.R, P->fwd_weight0(),
+                                P->fwd_weight0_bf16(), P->fwd_weight0_ld(), Lt.n[0], P->bias(0),
+                                P->at<float>(Lt.Z[0]), Lt.ldp[0], s, train ? nullptr : &ec));
   }
   P->probe_end(DSSM_PROBE_SPMM_FWD, s);
   if (fused) {
@@ -711,11 +722,14 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     for (int l = 1; l < Lt.L; ++l) {
       const dssm::BnSide in = P->bn_side(l - 1);
       const dssm::BnSide out = P->bn_side(l);
-      if (!Lt.bf16) {  // fp32 parity mode: W_l straight from the arena ([in x n] row-major)
+      if (!Lt.bf16 || P->fwd32()) {  // fp32 parity mode / FWD32: W_l straight from the arena ([in x n])
+        // FWD32: the activation the bf16 backward reads is written bf16 (the bf16 mode's rounding)
         HIP_TRY(dssm::launch_g32_fwd(Lt.R, Lt.n[l], Lt.n[l - 1], P->at<float>(Lt.Z[l - 1]), Lt.ldp[l - 1],
                                      P->at<float>(Lt.coef[l - 1]), &in, Lt.BS, P->p + Lt.fc_off[l], Lt.n[l],
-                                     P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l), P->at<float>(Lt.A[l - 1]),
-                                     P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr));
+                                     P->at<float>(Lt.Z[l]), Lt.ldp[l], P->bias(l),
+                                     Lt.bf16 ? nullptr : P->at<float>(Lt.A[l - 1]),
+                                     P->at<double>(Lt.fsum[l]), s, det ? &out.fdet : nullptr,
+                                     Lt.bf16 ? P->at<uint16_t>(Lt.A[l - 1]) : nullptr));
         continue;
       }
       HIP_TRY(dssm::launch_gemm_nt_fwd_fused(
@@ -753,6 +767,16 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
           P->at<float>(Lt.partial), P->at<unsigned>(Lt.tickets[l][0]), P->at<float>(Lt.coef[l]), s));
     const bool last = l == Lt.L - 1;
     if (last) break;  // the cosine kernel applies the last BN+ReLU itself (and writes the embeddings)
+    if (P->fwd32()) {
+      // FWD32 eval: the fp32 parity mode's path -- BN + ReLU into an fp32 scratch (dA_l: free in a
+      // forward; the backward rewrites it before reading) and the fp32 GEMM on the fp32 W_{l+1}
+      HIP_TRY(dssm::launch_bn_apply(P->at<float>(Lt.Z[l]), Lt.ldp[l], n, tw, P->at<float>(Lt.coef[l]), true,
+                                    P->ws + Lt.dA[l], false, s));
+      HIP_TRY(dssm::launch_gemm(dssm::GEMM_FWD, false, Lt.R, Lt.n[l + 1], n, P->ws + Lt.dA[l], Lt.ldp[l],
+                                P->p + Lt.fc_off[l + 1], Lt.n[l + 1], P->at<float>(Lt.Z[l + 1]), Lt.ldp[l + 1],
+                                P->bias(l + 1), false, nullptr, s));
+      continue;
+    }
     if (!last && P->wholek(l + 1)) {
       // BN+ReLU of layer l applied while staging the next GEMM's A operand; the bf16 activation
       // is written once (for the dW GEMM) by the first column tile.
@@ -1293,6 +1317,7 @@ int dssm_plan_schedule(const dssm_plan* P) {
   if (P->merged_csc() && P->on(DSSM_OPT_SCATTER_IN_COS)) f |= DSSM_SCHED_SCATTER_IN_COS;
   if (P->deterministic()) f |= DSSM_SCHED_DETERMINISTIC;
   if (P->bnb_in_pair()) f |= DSSM_SCHED_BNB_IN_PAIR;
+  if (P->fwd32()) f |= DSSM_SCHED_FWD32;
   return f;
 }
 

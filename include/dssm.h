@@ -152,8 +152,14 @@ int dssm_plan_set_fused_w1_adam(dssm_plan* plan, int on);
  *                      dA pair launch stages its A operand (no BN-backward apply launch for it); 0: the
  *                      apply launch
  *   TAIL_IN_A2A     0; 1: dssm_plan_graph_build_dp_steps puts the fp32 tail's all-reduce into the last
- *                      chunk's all-to-all RCCL group (one collective launch fewer per step; a mixed
- *                      p2p / collective group, exercised at world 1 only on one-GPU boxes) */
+ *                      chunk's all-to-all RCCL group (one collective launch fewer per step; dssm_amd/dist.py
+ *                      turns it on after a start-up self-test of that mixed group at the real world size)
+ *   FWD32           0; 1 (bf16 plans, fused-statistics schedule, no data-parallel wire): the forward
+ *                      at the reference's precision -- the SpMM gathers the fp32 W1 masters and the
+ *                      layers >= 2 run the fp32-parity g32 tiles on the fp32 W_l, writing the bf16
+ *                      activations the bf16 backward reads -- so loss, cosine scores and embeddings
+ *                      match new_dssm.py:117-213 at fp32 accuracy while the backward and the optimizer
+ *                      stay the bf16 perf mode's (their gradients carry bf16 rounding) */
 enum {
   DSSM_OPT_FUSED_STATS = 0,
   DSSM_OPT_MERGED_CSC,
@@ -168,6 +174,7 @@ enum {
   DSSM_OPT_MEMCPY_NODES,
   DSSM_OPT_BNB_IN_PAIR,
   DSSM_OPT_TAIL_IN_A2A,
+  DSSM_OPT_FWD32,
   DSSM_OPT_COUNT
 };
 int dssm_plan_set_option(dssm_plan* plan, int option, int value);
@@ -279,7 +286,8 @@ enum {
   DSSM_SCHED_SCATTER_IN_COS = 64,  /* CSC scatter as workgroups of the cosine launch */
   DSSM_SCHED_DETERMINISTIC = 128,  /* fixed-order reductions: bit-identical repeated runs */
   DSSM_SCHED_NT32 = 256,           /* fp32: layers >= 2 on the fused fp32 MFMA tiles (g32.h) */
-  DSSM_SCHED_BNB_IN_PAIR = 512     /* the last layer's BN backward inside the dA pair's A staging */
+  DSSM_SCHED_BNB_IN_PAIR = 512,    /* the last layer's BN backward inside the dA pair's A staging */
+  DSSM_SCHED_FWD32 = 1024          /* bf16 plan: the forward at fp32 accuracy (DSSM_OPT_FWD32) */
 };
 int dssm_plan_schedule(const dssm_plan* plan);
 /* A train forward (either precision) leaves the loss / accuracy reduction to the backward's first
