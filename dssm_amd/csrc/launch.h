@@ -55,8 +55,10 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
 // scratch for the scatter, whose output every column then gets in row order.
 // Every column [col_ptr[c], col_ptr[c+1]) of (row_in, val_in) into (row_out, val_out) in row order
 // (deterministic mode of the merged transpose, after its scatter).
+// scratch / max_nnz (optional): the rank transpose's scratch, whose heavy-column list sends the long
+// columns to their own workgroups.
 hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
-                           int* row_out, float* val_out, hipStream_t s);
+                           int* row_out, float* val_out, hipStream_t s, int* scratch = nullptr, int max_nnz = 0);
 // The rank transpose split across the fused-statistics forward (rank_only above first):
 // FC1 SpMM rows + the column scan in one launch; BN1 sums + the scatter in one launch.
 hipError_t launch_spmm_scan(const int* indptr, const int* indices, const float* values, int rows,

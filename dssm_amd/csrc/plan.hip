@@ -749,7 +749,7 @@ int dssm_plan_forward(dssm_plan* P, int train, void* stream) {
     if (merged && det)
       HIP_TRY(dssm::launch_csc_sort(P->at<int>(Lt.col_ptr), Lt.R, Lt.D, P->at<int>(Lt.sort_row),
                                     P->at<float>(Lt.sort_val), P->at<int>(Lt.csc_row),
-                                    P->at<float>(Lt.csc_val), s));
+                                    P->at<float>(Lt.csc_val), s, P->at<int>(Lt.csc_scratch), Lt.max_nnz));
     P->fwd_train_done = true;
     P->fwd_fused = true;
     P->loss_pending = true;

@@ -723,29 +723,145 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The workgroup path for one long column c (every wave of the workgroup; block-uniform call).
+__device__ __forceinline__ void sort_long_column(const int* __restrict__ col_ptr, int c, int rows,
+                                                 const int* __restrict__ row_in, const float* __restrict__ val_in,
+                                                 int* __restrict__ row_out, float* __restrict__ val_out,
+                                                 unsigned* bits, int* wpre, int* s_wave) {
+  const int t = threadIdx.x;
+  const int s = col_ptr[c], e = col_ptr[c + 1];
+  bool dup = false;
+  int base = s;
+  for (int w0 = 0; w0 < rows; w0 += kSortWinWg) {
+#pragma unroll
+    for (int j = 0; j < kSortWords; ++j) bits[t * kSortWords + j] = 0u;
+    __syncthreads();
+    int nin = 0;
+    for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {  // kSortU loads in flight per thread
+      int rr[kSortU];
+#pragma unroll
+      for (int u = 0; u < kSortU; ++u) {
+        const int i = i0 + kSortNT * u;
+        rr[u] = i < e ? row_in[i] - w0 : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kSortU; ++u)
+        if (rr[u] >= 0 && rr[u] < kSortWinWg) {
+          atomicOr(&bits[rr[u] >> 5], 1u << (rr[u] & 31));
+          ++nin;
+        }
+    }
+    __syncthreads();
+    unsigned m[kSortWords];
+    int own = 0;
+#pragma unroll
+    for (int j = 0; j < kSortWords; ++j) {
+      m[j] = bits[t * kSortWords + j];
+      own += __popc(m[j]);
+    }
+    int total, nin_total;
+    int run = block_excl_scan<kSortNT>(own, s_wave, total);
+    (void)block_excl_scan<kSortNT>(nin, s_wave, nin_total);
+#pragma unroll
+    for (int j = 0; j < kSortWords; ++j) {
+      wpre[t * kSortWords + j] = run;
+      run += __popc(m[j]);
+    }
+    dup = dup || nin_total != total;
+    __syncthreads();
+    if (!dup)
+      for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {
+        int rr[kSortU];
+        float vv[kSortU];
+#pragma unroll
+        for (int u = 0; u < kSortU; ++u) {
+          const int i = i0 + kSortNT * u;
+          rr[u] = i < e ? row_in[i] - w0 : -1;
+          vv[u] = i < e ? val_in[i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kSortU; ++u) {
+          const int r = rr[u];
+          if (r >= 0 && r < kSortWinWg) {
+            const int wd = r >> 5;
+            const int p = base + wpre[wd] + __popc(bits[wd] & ((1u << (r & 31)) - 1u));
+            row_out[p] = r + w0;
+            val_out[p] = vv[u];
+          }
+        }
+      }
+    base += total;
+    __syncthreads();
+  }
+  if (dup)
+    for (int i = s + t; i < e; i += kSortNT) {
+      const int ri = row_in[i];
+      const float vi = val_in[i];
+      const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
+      row_out[p] = ri;
+      val_out[p] = vi;
+    }
+  __syncthreads();  // the LDS bitmap is reused by the next long column
+}
+
+// heavy_n / heavy_items (the rank transpose's heavy-column work list, csc_heavy_count): when given,
+// the long columns (> kSortWaveMax entries) are sorted by kSortLongWgs extra workgroups that find
+// them in the list (item 0 of each), so the column waves never wait for them; without the list a
+// column wave hands its long columns to its own workgroup after its other columns.
+constexpr int kSortLongWgs = 64;
 __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict__ col_ptr, int D, int rows,
                                                            const int* __restrict__ row_in,
                                                            const float* __restrict__ val_in,
                                                            int* __restrict__ row_out,
-                                                           float* __restrict__ val_out) {
+                                                           float* __restrict__ val_out,
+                                                           const int* __restrict__ heavy_n,
+                                                           const int2* __restrict__ heavy_items,
+                                                           int ncol_blocks) {
   __shared__ unsigned bits[kSortWaves * 64 * kSortWords];
   __shared__ int wpre[kSortWaves * 64 * kSortWords];
   __shared__ int s_wave[kSortWaves];
   __shared__ int s_long[kSortWaves * kSortCols];
   __shared__ int s_nlong;
   const int t = threadIdx.x, lane = t & 63;
+  if ((int)blockIdx.x >= ncol_blocks) {  // the long-column role (workgroup-uniform)
+    // Every role workgroup walks the whole list (kSortNT items per pass, all loads in flight) and
+    // numbers the long columns in list order -- item 0 of a column longer than kSortWaveMax, not the
+    // ones column -- with a workgroup prefix count; workgroup j sorts those numbered j mod the role's
+    // size, one at a time, so the Zipf-hot columns (often adjacent in the list) spread over the role
+    const int nh = *heavy_n, nlw = (int)gridDim.x - ncol_blocks, j = (int)blockIdx.x - ncol_blocks;
+    int seen = 0;  // long columns numbered in earlier passes (uniform)
+    for (int b0 = 0; b0 < nh; b0 += kSortNT) {
+      if (t == 0) s_nlong = 0;
+      const int it = b0 + t;
+      int c = -1;
+      if (it < nh) {
+        const int2 item = heavy_items[it];
+        if (item.y == 0 && item.x < D && col_ptr[item.x + 1] - col_ptr[item.x] > kSortWaveMax) c = item.x;
+      }
+      int total;
+      const int idx = seen + block_excl_scan<kSortNT>(c >= 0 ? 1 : 0, s_wave, total);
+      if (c >= 0 && idx % nlw == j) s_long[min(atomicAdd(&s_nlong, 1), kSortWaves * kSortCols - 1)] = c;
+      __syncthreads();
+      const int nl = min(s_nlong, kSortWaves * kSortCols);  // <= ceil(kSortNT / nlw) = 4 at 64 workgroups
+      for (int k = 0; k < nl; ++k)
+        sort_long_column(col_ptr, s_long[k], rows, row_in, val_in, row_out, val_out, bits, wpre, s_wave);
+      seen += total;
+      __syncthreads();
+    }
+    return;
+  }
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   unsigned* wbits = bits + wv * 64 * kSortWords;
   int* wp = wpre + wv * 64 * kSortWords;
   if (t == 0) s_nlong = 0;
-  {  // the virtual ones column (in row order already), copied by the whole grid
+  {  // the virtual ones column (in row order already), copied by the column workgroups
     const int o0 = col_ptr[D], on = col_ptr[D + 1] - o0;
-    for (int i = blockIdx.x * kSortNT + t; i < on; i += gridDim.x * kSortNT) {
+    for (int i = blockIdx.x * kSortNT + t; i < on; i += ncol_blocks * kSortNT) {
       row_out[o0 + i] = row_in[o0 + i];
       val_out[o0 + i] = val_in[o0 + i];
     }
   }
-  const int G = gridDim.x * kSortWaves, gw = blockIdx.x * kSortWaves + wv;
+  const int G = ncol_blocks * kSortWaves, gw = blockIdx.x * kSortWaves + wv;
   int cs = 0, cn = 0;  // lane k < kSortCols: column gw + k G
   if (lane < kSortCols) {
     const int c = gw + lane * G;
@@ -867,87 +983,14 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
           row_out[p] = ri;
           val_out[p] = vi;
         }
-    } else if (lane == 0) {
+    } else if (!heavy_n && lane == 0) {  // with the heavy list the long-column role takes it
       s_long[atomicAdd(&s_nlong, 1)] = gw + k * G;  // the workgroup's pass below (order irrelevant)
     }
   }
   __syncthreads();
   const int nlong = s_nlong;  // workgroup-uniform
-  for (int k = 0; k < nlong; ++k) {  // the long columns, one at a time with every wave
-    const int c = s_long[k];
-    const int s = col_ptr[c], e = col_ptr[c + 1];
-    bool dup = false;
-    int base = s;
-    for (int w0 = 0; w0 < rows; w0 += kSortWinWg) {
-#pragma unroll
-      for (int j = 0; j < kSortWords; ++j) bits[t * kSortWords + j] = 0u;
-      __syncthreads();
-      int nin = 0;
-      for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {  // kSortU loads in flight per thread
-        int rr[kSortU];
-#pragma unroll
-        for (int u = 0; u < kSortU; ++u) {
-          const int i = i0 + kSortNT * u;
-          rr[u] = i < e ? row_in[i] - w0 : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < kSortU; ++u)
-          if (rr[u] >= 0 && rr[u] < kSortWinWg) {
-            atomicOr(&bits[rr[u] >> 5], 1u << (rr[u] & 31));
-            ++nin;
-          }
-      }
-      __syncthreads();
-      unsigned m[kSortWords];
-      int own = 0;
-#pragma unroll
-      for (int j = 0; j < kSortWords; ++j) {
-        m[j] = bits[t * kSortWords + j];
-        own += __popc(m[j]);
-      }
-      int total, nin_total;
-      int run = block_excl_scan<kSortNT>(own, s_wave, total);
-      (void)block_excl_scan<kSortNT>(nin, s_wave, nin_total);
-#pragma unroll
-      for (int j = 0; j < kSortWords; ++j) {
-        wpre[t * kSortWords + j] = run;
-        run += __popc(m[j]);
-      }
-      dup = dup || nin_total != total;
-      __syncthreads();
-      if (!dup)
-        for (int i0 = s + t; i0 < e; i0 += kSortNT * kSortU) {
-          int rr[kSortU];
-          float vv[kSortU];
-#pragma unroll
-          for (int u = 0; u < kSortU; ++u) {
-            const int i = i0 + kSortNT * u;
-            rr[u] = i < e ? row_in[i] - w0 : -1;
-            vv[u] = i < e ? val_in[i] : 0.f;
-          }
-#pragma unroll
-          for (int u = 0; u < kSortU; ++u) {
-            const int r = rr[u];
-            if (r >= 0 && r < kSortWinWg) {
-              const int wd = r >> 5;
-              const int p = base + wpre[wd] + __popc(bits[wd] & ((1u << (r & 31)) - 1u));
-              row_out[p] = r + w0;
-              val_out[p] = vv[u];
-            }
-          }
-        }
-      base += total;
-      __syncthreads();
-    }
-    if (dup)
-      for (int i = s + t; i < e; i += kSortNT) {
-        const int ri = row_in[i];
-        const float vi = val_in[i];
-        const int p = sort_rank_slow(row_in, val_in, s, e, i, ri, __float_as_uint(vi));
-        row_out[p] = ri;
-        val_out[p] = vi;
-      }
-  }
+  for (int k = 0; k < nlong; ++k)  // the long columns, one at a time with every wave
+    sort_long_column(col_ptr, s_long[k], rows, row_in, val_in, row_out, val_out, bits, wpre, s_wave);
 }
 
 // ---- dW1 ---------------------------------------------------------------------------------------
@@ -1211,9 +1254,13 @@ int* csc_heavy_count(int* scratch, int D, int max_nnz) {
 }
 
 hipError_t launch_csc_sort(const int* col_ptr, int rows, int D, const int* row_in, const float* val_in,
-                           int* row_out, float* val_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_csc_sort_rows, dim3(csc_sort_grid(D)), dim3(kSortNT), 0, s, col_ptr, D,
-                     rows, row_in, val_in, row_out, val_out);
+                           int* row_out, float* val_out, hipStream_t s, int* scratch, int max_nnz) {
+  // scratch (the rank transpose's): its heavy-column list routes the long columns to their own role
+  const int* hn = scratch ? csc_heavy_count(scratch, D, max_nnz) : nullptr;
+  const int2* hi = hn ? reinterpret_cast<const int2*>(hn + 64) : nullptr;
+  const int nb = csc_sort_grid(D);
+  hipLaunchKernelGGL(k_csc_sort_rows, dim3(nb + (hn ? kSortLongWgs : 0)), dim3(kSortNT), 0, s, col_ptr, D,
+                     rows, row_in, val_in, row_out, val_out, hn, hi, nb);
   return hipGetLastError();
 }
 
@@ -1269,7 +1316,7 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
   }
   if (sort_row)
     hipLaunchKernelGGL(k_csc_sort_rows, dim3(csc_sort_grid(D)), dim3(kSortNT), 0, s, col_ptr,
-                       D, rows, sort_row, sort_val, csc_row, csc_val);
+                       D, rows, sort_row, sort_val, csc_row, csc_val, nullptr, nullptr, csc_sort_grid(D));
   return hipGetLastError();
 }
 
