@@ -183,3 +183,42 @@ def test_strict_rccl_without_nccl_backend_raises():
     finally:
         if made:
             dist.destroy_process_group()
+
+
+def _rccl_world2_worker(rank, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=2, device_id=torch.device("cuda", rank))
+    try:
+        from dssm_amd.dist import DataParallel
+        from dssm_amd.model import DSSM
+        m = DSSM(5000, (300, 300, 128), 128, 4, dtype="bf16", seed=0, device=torch.device("cuda", rank))
+        dp = DataParallel(m, comm="rccl", sparse=True)
+        q.put((rank, dp.schedule, dp.sparse, dp.tail_group, list(dp.fallbacks)))
+        dp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL refuses two ranks on one device)")
+def test_sparse_exchange_and_mixed_group_rccl_world2():
+    """the library transport's variable-count all-to-all across real peers.  At world 2 on
+    two GPUs DataParallel's start-up checks run on RCCL: the mixed all-to-all + all-reduce group's
+    self-test (eager and captured) and the sparse exchange against the dense all-to-all, bit for bit;
+    both must pass on both ranks.  Skipped on one-GPU boxes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ps = [ctx.Process(target=_rccl_world2_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(60)
+    for rank, sched, sparse, tail, notes in outs:
+        assert sparse and tail and not notes, (rank, sched, notes)
+        assert sched == "zero/bf16 sparse tail-in-a2a via rccl"
