@@ -809,6 +809,8 @@ __device__ __forceinline__ void sort_long_column(const int* __restrict__ col_ptr
 // them in the list (item 0 of each), so the column waves never wait for them; without the list a
 // column wave hands its long columns to its own workgroup after its other columns.
 constexpr int kSortLongWgs = 64;
+// one pass of the long-column role lists at most ceil(kSortNT / kSortLongWgs) columns per workgroup
+static_assert((kSortNT + kSortLongWgs - 1) / kSortLongWgs <= kSortWaves * kSortCols, "s_long holds a pass");
 __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict__ col_ptr, int D, int rows,
                                                            const int* __restrict__ row_in,
                                                            const float* __restrict__ val_in,
