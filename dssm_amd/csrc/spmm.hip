@@ -697,8 +697,10 @@ constexpr int kSortWinWg = kSortWaves * kSortWin;    // rows per window of the w
 constexpr int kSortWaveMax = 512;
 constexpr int kSortU = 8;                            // long columns: entries in flight per thread
 static_assert(kSortCols * kSortSmall == 64, "one 8-lane group per column");
-#ifndef DSSM_SORT_DIAG  // diagnostics builds (wrong results), bits: 1 skip the group path, 2 the <= 64
-#define DSSM_SORT_DIAG 0  // path, 4 the wave-bitmap path, 8 the workgroup path (tools/sort_bench.py)
+// diagnostics builds (wrong results), bits: 1 skip the group path, 2 the <= 64 path, 4 the
+// wave-bitmap path, 8 the in-workgroup long path, 16 the long-column role (tools/sort_bench.py)
+#ifndef DSSM_SORT_DIAG
+#define DSSM_SORT_DIAG 0
 #endif
 
 __host__ __device__ inline int csc_sort_grid(int D) { return (D + kSortWaves * kSortCols - 1) / (kSortWaves * kSortCols); }
@@ -826,6 +828,7 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
   __shared__ int s_nlong;
   const int t = threadIdx.x, lane = t & 63;
   if ((int)blockIdx.x >= ncol_blocks) {  // the long-column role (workgroup-uniform)
+    if (DSSM_SORT_DIAG & 16) return;
     // Every role workgroup walks the whole list (kSortNT items per pass, all loads in flight) and
     // numbers the long columns in list order -- item 0 of a column longer than kSortWaveMax, not the
     // ones column -- with a workgroup prefix count; workgroup j sorts those numbered j mod the role's
@@ -890,6 +893,18 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
       val_out[s + p] = __uint_as_float(bi);
     }
   }
+  // the entries of every column of 9..64 entries, loaded at once (lane i: entry i of column k), so
+  // the one-column-at-a-time loop below waits for no load of them
+  int pr[kSortCols];
+  unsigned pb[kSortCols];
+#pragma unroll
+  for (int k = 0; k < kSortCols; ++k) {
+    const int s = __builtin_amdgcn_readlane(cs, k), n = __builtin_amdgcn_readlane(cn, k);
+    const bool own = n > kSortSmall && n <= 64 && lane < n;
+    pr[k] = own ? row_in[s + lane] : 0;
+    pb[k] = own ? __float_as_uint(val_in[s + lane]) : 0u;
+  }
+#pragma unroll
   for (int k = 0; k < kSortCols; ++k) {  // the longer ones, one at a time (wave-uniform bounds)
     const int s = __builtin_amdgcn_readlane(cs, k), n = __builtin_amdgcn_readlane(cn, k);
     const int e = s + n;
@@ -899,8 +914,8 @@ __global__ __launch_bounds__(kSortNT) void k_csc_sort_rows(const int* __restrict
     if ((DSSM_SORT_DIAG & 8) && n > kSortWaveMax) continue;
     if (n <= 64) {
       const bool own = lane < n;
-      const int ri = own ? row_in[s + lane] : 0;
-      const unsigned bi = own ? __float_as_uint(val_in[s + lane]) : 0u;
+      const int ri = pr[k];
+      const unsigned bi = pb[k];
       int p = 0;
       for (int j = 0; j < n; ++j) {
         const int rj = __builtin_amdgcn_readlane(ri, j);
@@ -1316,9 +1331,9 @@ hipError_t launch_csc_build(const int* indptr, const int* indices, const float* 
     hipLaunchKernelGGL(k_csc_fill_global, dim3(cdiv(rows, 4)), dim3(256), 0, s, indptr, indices,
                        values, rows, D, cursor, col_ptr, out_row, out_val, csc_col);
   }
-  if (sort_row)
-    hipLaunchKernelGGL(k_csc_sort_rows, dim3(csc_sort_grid(D)), dim3(kSortNT), 0, s, col_ptr,
-                       D, rows, sort_row, sort_val, csc_row, csc_val, nullptr, nullptr, csc_sort_grid(D));
+  if (sort_row)  // the rank path's scan listed the heavy columns: the long ones get their own role
+    return launch_csc_sort(col_ptr, rows, D, sort_row, sort_val, csc_row, csc_val, s,
+                           rank_path && csc_rank_supported(D) ? scratch : nullptr, max_nnz);
   return hipGetLastError();
 }
 
