@@ -1,7 +1,7 @@
 """Diagnostics (not collected by pytest): where the bf16 step with the last layer's BN backward
 folded into the pair launch (BNB_IN_PAIR, default) differs from the apply-launch schedule, per
 buffer and gradient tensor, on one step from the same state (tests/test_gpu_schedules.py case 1).
-    python tests/diag_bnb.py"""
+    python tools/diag_bnb.py"""
 import os
 import sys
 

@@ -1,6 +1,6 @@
 """Diagnostics (not collected by pytest): tests/test_gpu_dp_bow.py's state and shard, single
 process: the unfused backward's gradients with and without BNB_IN_PAIR, bitwise and against the
-bf16-emulating oracle.   python tests/diag_fold_dp.py"""
+bf16-emulating oracle.   python tools/diag_fold_dp.py"""
 import os
 import sys
 

@@ -1,7 +1,7 @@
 """Diagnostics (not collected by pytest): the bf16 step's gradients against the bf16-emulating
 float64 oracle at the C3 shard shape of tests/test_gpu_dp_bow.py, with the BN backward folded into
 the pairs (BNB_IN_PAIR = 1, default) and with the apply launches (0): relative L2 error per weight.
-    python tests/diag_fold_grads.py"""
+    python tools/diag_fold_grads.py"""
 import os
 import sys
 

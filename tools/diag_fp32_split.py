@@ -1,8 +1,8 @@
 """Diagnostics (not collected by pytest): the fp32 parity mode's end-to-end C2 step against the
 float64 oracle, per layer (Z, A, dA, dZ) and per gradient, for the library named by DSSM_LIB_PATH
 (the split-product tiles, DSSM_G32_SPLIT=1, or the exact FMA-chain tiles, =0).  Usage, on a GPU:
-    DSSM_LIB_PATH=dssm_amd/libdssm.so python tests/diag_fp32_split.py
-    python tests/diag_fp32_split.py both      # both libraries, each in a child process"""
+    DSSM_LIB_PATH=dssm_amd/libdssm.so python tools/diag_fp32_split.py
+    python tools/diag_fp32_split.py both      # both libraries, each in a child process"""
 import os
 import subprocess
 import sys
