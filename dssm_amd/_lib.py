@@ -215,7 +215,18 @@ _SIGS = {
     "dssm_rows_pack_u16": (C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P]),
     "dssm_rows_unpack_u16": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _P, _P]),
     "dssm_comm_destroy": (C.c_int, []),
+    # peer-store exchange (csrc/peer.hip)
+    "dssm_peer_alloc": (C.c_int, [C.c_int64, _P]),
+    "dssm_peer_free": (C.c_int, [_P]),
+    "dssm_ipc_handle": (C.c_int, [_P, _P]),
+    "dssm_ipc_open": (C.c_int, [_P, _P]),
+    "dssm_ipc_close": (C.c_int, [_P]),
+    "dssm_plan_set_dp_peers": (C.c_int, [_P, C.c_int, _P, _P, _P, _P]),
+    "dssm_plan_set_peer_timeout": (C.c_int, [_P, C.c_double]),
+    "dssm_plan_peer_exchange": (C.c_int, [_P, C.c_int, _P]),
+    "dssm_plan_peer_status": (C.c_int, [_P, _P]),
 }
+PEER_FLAG_BYTES = 4096  # include/dssm.h DSSM_PEER_FLAG_BYTES
 
 _lib = None
 

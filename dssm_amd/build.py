@@ -15,7 +15,7 @@ CSRC = os.environ.get("DSSM_CSRC_DIR", os.path.join(PKG, "csrc"))  # side builds
 TAG = os.environ.get("DSSM_BUILD_TAG", "")
 OBJ = os.path.join(PKG, "_build" + TAG)
 LIB = os.path.join(PKG, f"libdssm{TAG}.so")
-SOURCES = ["spmm.hip", "gemm.hip", "gemm32.hip", "bn.hip", "cosine.hip", "adam.hip", "plan.hip", "feed.hip", "rnn.hip", "rnn_mfma.hip", "ops.hip"]
+SOURCES = ["spmm.hip", "gemm.hip", "gemm32.hip", "bn.hip", "cosine.hip", "adam.hip", "plan.hip", "feed.hip", "rnn.hip", "rnn_mfma.hip", "ops.hip", "peer.hip"]
 HEADERS = ["common.h", "launch.h", "gather.h", "bnfuse.h", "flat.h", "tn.h", "csc.h", "g32.h"]
 ARCH = os.environ.get("DSSM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

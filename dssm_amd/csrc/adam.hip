@@ -152,6 +152,13 @@ __device__ __forceinline__ RowEntries row_entries(const AdamStep& a, int s, int 
   return r;
 }
 
+// gradient pass: where W1 row c's bf16 gradient goes -- this rank's gradient wire, or (peer exchange,
+// one wire chunk) the block of this rank in the stage of the row's owner j = c / geo.ws
+__device__ __forceinline__ u16* grad_row(const AdamStep& a, int c) {
+  if (a.npeer) return a.gpeer[c / a.geo.ws] + wire_row_off(a.geo, c);
+  return a.gout + wire_row_off(a.geo, c);
+}
+
 template <typename TZ, bool WIRE>
 __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, float alpha,
                                        const RowEntries* pre = nullptr) {
@@ -193,16 +200,19 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
     if (WIRE && nvalid > 0 && a.gout) {  // gradient pass: the row leaves as bf16 (bias row: fp32)
       const int k = nvalid >= 8 ? 8 : 4;
       if (c < a.D) {
-        u16* q = a.gout + wire_row_off(a.geo, c) + cc;
+        u16* q = grad_row(a, c) + cc;
         uint2 lo;
         lo.x = pack2bf(G[0], G[1]);
         lo.y = pack2bf(G[2], G[3]);
-        *reinterpret_cast<uint2*>(q) = lo;
-        if (k == 8) {
-          uint2 hi;
-          hi.x = pack2bf(G[4], G[5]);
-          hi.y = pack2bf(G[6], G[7]);
-          *reinterpret_cast<uint2*>(q + 4) = hi;
+        uint2 hi;
+        hi.x = pack2bf(G[4], G[5]);
+        hi.y = pack2bf(G[6], G[7]);
+        if (a.npeer) {  // peer exchange: system-scope stores into the owner's stage
+          st_sys8(q, lo);
+          if (k == 8) st_sys8(q + 4, hi);
+        } else {
+          *reinterpret_cast<uint2*>(q) = lo;
+          if (k == 8) *reinterpret_cast<uint2*>(q + 4) = hi;
         }
       } else {
         *reinterpret_cast<float4*>(a.g + o) = make_float4(G[0], G[1], G[2], G[3]);
@@ -241,6 +251,11 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
 // Adam over one W1 row c whose gradient row sits in LDS (heavy-item workgroups).
 template <bool WIRE>
 __device__ __forceinline__ void w1_row_from(const AdamStep& a, int c, const float* grow, float alpha) {
+  if (WIRE && a.gout && a.npeer && c < a.D) {  // peer exchange: 4-B stores into the owner's stage
+    unsigned* q = reinterpret_cast<unsigned*>(grad_row(a, c));
+    for (int j = threadIdx.x; j < a.n / 2; j += blockDim.x) st_sys4(q + j, pack2bf(grow[2 * j], grow[2 * j + 1]));
+    return;
+  }
   if (WIRE && a.gout) {  // gradient pass
     const int64_t wo = c < a.D ? wire_row_off(a.geo, c) : 0;
     for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
@@ -487,7 +502,9 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
         const int vr = (int)(i / q);
         const int c = w1_role_row(a, vr);
         if (c < 0 || c >= a.D || a.col_ptr[c + 1] != a.col_ptr[c]) continue;
-        reinterpret_cast<uint2*>(a.gout + wire_row_off(a.geo, c))[i - (int64_t)vr * q] = make_uint2(0u, 0u);
+        uint2* z = reinterpret_cast<uint2*>(grad_row(a, c)) + (i - (int64_t)vr * q);
+        if (a.npeer) st_sys8(z, make_uint2(0u, 0u));
+        else *z = make_uint2(0u, 0u);
       }
     } else if (a.w1_flat) {
       // untouched W1 rows (no CSC entry, g = 0): float4 streaming, every lane busy
@@ -498,6 +515,10 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
 #endif
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
+    if (WIRE && a.peer_sync && a.gstage) {  // peer exchange: the stage was stored by other agents
+      if (threadIdx.x == 0) peer_acquire();
+      __syncthreads();
+    }
     if (WIRE && a.slab_to_g) {  // gradient pass: g = the deferred split-K slabs' sums (fixed order)
       for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < nt; j += (int64_t)a.dense_blocks * blockDim.x) {
         const int64_t i = a.t4_begin + j;
@@ -516,7 +537,7 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
         gg = make_float4(0.f, 0.f, 0.f, 0.f);
         const uint2* st = reinterpret_cast<const uint2*>(a.gstage) + (i - a.gbase4);
         for (int k = 0; k < a.gparts; ++k) {
-          const uint2 q = st[(int64_t)k * (a.gstride / 4)];
+          const uint2 q = a.npeer ? ld_sys8(st + (int64_t)k * (a.gstride / 4)) : st[(int64_t)k * (a.gstride / 4)];
           gg.x += __uint_as_float(q.x << 16);
           gg.y += __uint_as_float(q.x & 0xffff0000u);
           gg.z += __uint_as_float(q.y << 16);
@@ -544,7 +565,11 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
         uint2 q;
         q.x = pack2bf(pp.x, pp.y);
         q.y = pack2bf(pp.z, pp.w);
-        reinterpret_cast<uint2*>(a.pwire)[i + a.pwire_off4] = q;
+        if (a.npeer) {
+          for (int k = 0; k < a.npeer; ++k) st_sys8(reinterpret_cast<uint2*>(a.ppeer[k]) + (i + a.pwire_off4), q);
+        } else {
+          reinterpret_cast<uint2*>(a.pwire)[i + a.pwire_off4] = q;
+        }
       } else if (a.sh.count) {
         write_shadow4(a.sh, i * 4, pp);
       }
@@ -553,7 +578,9 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+  if (WIRE && a.peer_sync) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
   __syncthreads();
+  if (WIRE && a.peer_sync && threadIdx.x == 0) peer_release();  // before any later flag (peer.hip)
   ADAM_TL(1);
   if (threadIdx.x == 0 && a.ticket) {
     // Two-level ticket: same-address atomics serialise (~6 ns each; one counter for ~8k blocks
@@ -738,6 +765,10 @@ static hipError_t prepare_adam_step(AdamStep& a) {
   // rows with no entry this step stream through the flat role instead of a wave per row
   a.w1_flat = (a.w1_blocks > 0 && a.item_blocks > 0 && (a.n % 4) == 0) ? 1 : 0;
   if (a.t4_end < a.t4_begin || (a.wire4 > 0 && (!a.gwire || !a.pwire))) return hipErrorInvalidValue;
+  if (a.npeer < 0 || a.npeer > kPeerMax) return hipErrorInvalidValue;
+  if (a.npeer && a.gout && (a.geo.wp != 1 || a.geo.ww != a.npeer || (a.n % 2))) return hipErrorInvalidValue;
+  for (int k = 0; k < a.npeer; ++k)
+    if ((a.gout && !a.gpeer[k]) || (!a.gout && !a.ppeer[k])) return hipErrorInvalidValue;
   const int64_t flat_rows = a.wchunk < 0 ? (int64_t)a.D + 1 : (int64_t)a.geo.ww * a.geo.ws;
 #ifdef DSSM_ADAM_SKIP_UNTOUCHED
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + 0 * flat_rows;
@@ -753,7 +784,8 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   const hipError_t pe = prepare_adam_step(a);
   if (pe != hipSuccess) return pe;
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
-  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g;
+  const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g ||
+                    a.npeer || a.peer_sync;
 #define DSSM_ADAM_LAUNCH(TZ)                                                         \
   if (wire) hipLaunchKernelGGL((k_adam_step<TZ, true>), grid, block, 0, s, a);       \
   else hipLaunchKernelGGL((k_adam_step<TZ, false>), grid, block, 0, s, a)

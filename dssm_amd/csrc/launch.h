@@ -304,6 +304,48 @@ __host__ __device__ inline int wire_chunk_row(const WireGeo& g, int chunk, int v
   return c < D ? c : -1;
 }
 
+// Peer-store exchange (peer.hip): flag words of each rank's flags buffer (one 256-B line each group)
+constexpr int kPeerMax = 8;  // ranks
+constexpr int kPeerGrad = 0, kPeerParam = 64, kPeerSeq = 128, kPeerTicket = 192, kPeerErr = 256;
+constexpr int kPeerFlagWords = 320;
+// SYSTEM-scope release / acquire (fine-grained buffers shared with other agents); the explicit wait
+// keeps the compiler from dropping the drain after the write-back (MI355X_MICROARCH.md, compiler hazard)
+__device__ __forceinline__ void peer_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void peer_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// payload accesses of the peer exchange: system-scope relaxed atomics (global_load / store ... sc0 sc1,
+// the same access the flags use), so every byte moves coherently whatever MTYPE the IPC-imported
+// mapping of a buffer carries; 8-B aligned
+__device__ __forceinline__ void st_sys8(void* p, uint2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys4(void* p, unsigned v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint2 ld_sys8(const void* p) {
+  const unsigned long long u = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<void*>(p)),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint2((unsigned)u, (unsigned)(u >> 32));
+}
+struct PeerArgs {
+  int world, rank;
+  unsigned* flags;            // this rank's flags
+  unsigned* rflags[kPeerMax]; // every rank's flags (rflags[rank] == flags)
+  float* rtail[kPeerMax];     // every rank's tail stage ([world][tailn] fp32)
+  const float* tail_src;      // this rank's tail gradient (the arena's [extent, param_count))
+  float* tail_dst;            // the same range: the rank-order sum is written back into it
+  int64_t tailn;
+};
+hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s);
+hipError_t launch_peer_after_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s);
+
 struct AdamStep {
   float* p;
   float* g;
@@ -373,6 +415,15 @@ struct AdamStep {
   // gradient pass: the dense role sums the deferred split-K slabs (slabs) of [t4_begin, t4_end) into
   // the gradient arena instead of updating parameters (the tail's all-reduce then sends the sums)
   int slab_to_g;
+  // peer-store exchange (peer.hip; wire chunks == 1): npeer ranks.  Gradient pass: row c's bf16
+  // gradient goes to gpeer[c / geo.ws] + wire_row_off(geo, c) (owner j's stage, block of this rank)
+  // instead of gout.  Adam: bf16(p) of the shard goes to every ppeer[k] at the wire offset instead of
+  // pwire.  peer_sync: the stage-reading workgroups acquire (system scope) first and every workgroup
+  // releases its stores (system scope) last.
+  int npeer;
+  int peer_sync;
+  uint16_t* gpeer[kPeerMax];
+  uint16_t* ppeer[kPeerMax];
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);
@@ -394,6 +445,8 @@ hipError_t launch_adam_flat_shadow(float* p, const float* g, float* m, float* v,
 // only, -1: all)
 hipError_t launch_wire_pack(const float* g, uint16_t* wire, int D, WireGeo geo, hipStream_t s);
 hipError_t launch_wire_shadow(const uint16_t* wire, ShadowSeg seg, WireGeo geo, int chunk, hipStream_t s);
+// the peer exchange's shadow rebuild (tight rows, chunks == 1) behind a system-scope acquire per workgroup
+hipError_t launch_peer_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s);
 // one workgroup spinning for `ns` nanoseconds (the data-parallel rehearsal's modelled collective)
 hipError_t launch_spin(double ns, hipStream_t s);
 // device-to-device copy as a kernel (captured graphs: ordered like the neighbouring kernel nodes)

@@ -1,0 +1,228 @@
+// Peer-store data-parallel exchange (include/dssm.h dssm_plan_set_dp_peers; DESIGN.md §6 "peer
+// exchange").  The bf16-wire schedule's two collectives (the gradient all-to-all and the parameter
+// all-gather, new_dssm.py:215-217's optimizer over a sharded batch) become stores into the peers'
+// buffers, mapped into every rank through HIP IPC:
+//   * the gradient pass (k_adam_step, gradient-pass mode) stores rank i's bf16 W1 gradient rows of
+//     owner j's shard straight into owner j's stage at block i -- the layout the all-to-all delivers --
+//     while it computes them, so the link traffic runs under the pass instead of after it;
+//   * the fp32 tail (b1, W2.., BN: 0.5 MB) is pushed to every rank's tail stage (k_peer_tail_push),
+//     whose last workgroup raises this step's GRAD flag on every rank;
+//   * each rank waits for every rank's GRAD flag (k_peer_wait, one workgroup), sums the world's tails
+//     in rank order (k_peer_tail_sum: the replicated tail stays bit-identical on every rank), and its
+//     Adam shard sums the stage's partials in rank order as the all-to-all schedule does, storing
+//     bf16(W1) of its shard into EVERY rank's parameter wire;
+//   * k_peer_signal raises this step's PARAM flag on every rank; each rank waits for every PARAM
+//     flag and rebuilds W1's bf16 shadow from its parameter wire (k_peer_shadow).
+// No collective library runs on the data path.  Steps are numbered by a per-rank epoch (flags[SEQ],
+// advanced by the tail push) and flags only grow, so nothing is re-armed between steps, graph
+// replays or regions.  Reuse is ordered by the flags themselves: rank i overwrites owner j's stage
+// (or tail slot) for step t+1 only after its PARAM wait of step t saw owner j's Adam of step t done,
+// and owner j overwrites rank i's parameter wire for step t+1 only after its GRAD wait saw rank i's
+// gradient pass of step t+1, which follows rank i's shadow rebuild of step t on rank i's stream.
+//
+// Memory: the stage, the parameter wire, the tail stage and the flags are fine-grained device
+// allocations (hipDeviceMallocFinegrained: coherent across agents while kernels run), exported with
+// hipIpcGetMemHandle.  Every producing workgroup drains its stores (s_waitcnt vmcnt(0)), joins a
+// barrier and issues a SYSTEM-scope release (the flag is raised by a later kernel or workgroup that
+// observed it); flags are system-scope atomics; the poll is a system-scope atomic read-modify-write
+// (never a cached load); every consuming workgroup issues a system-scope acquire before its loads.
+// Waits are bounded (a timeout sets flags[ERR]; later waits return at once; the host reads it with
+// dssm_plan_peer_status), so a peer that never arrives cannot hang the GPU.
+#include <cstring>
+#include <string>
+
+#include "../../include/dssm.h"
+#include "common.h"
+#include "launch.h"
+
+namespace dssm {
+int report_error(int code, const char* msg);  // plan.hip: sets dssm_last_error()
+
+namespace {
+
+__device__ __forceinline__ unsigned sys_poll(unsigned* p) {
+  return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The tail's partial of this rank into slot `rank` of every rank's tail stage; the last workgroup
+// advances the epoch and raises this rank's GRAD flag on every rank.
+__global__ __launch_bounds__(256) void k_peer_tail_push(PeerArgs a) {
+  const int64_t n4 = a.tailn / 4;
+  const float4* src = reinterpret_cast<const float4*>(a.tail_src);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = src[i];
+    const uint2 lo = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
+    const uint2 hi = make_uint2(__float_as_uint(v.z), __float_as_uint(v.w));
+    for (int k = 0; k < a.world; ++k) {
+      float* d = a.rtail[k] + a.rank * a.tailn + 4 * i;
+      st_sys8(d, lo);
+      st_sys8(d + 2, hi);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  peer_release();
+  const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != gridDim.x - 1) return;
+  __hip_atomic_store(a.flags + kPeerTicket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  peer_acquire();  // every workgroup's release (the ticket's RMW chain) before ...
+  const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __hip_atomic_store(a.flags + kPeerSeq, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  peer_release();  // ... this workgroup's flags
+  for (int k = 0; k < a.world; ++k)
+    __hip_atomic_store(a.rflags[k] + kPeerGrad + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One wave: lane k < world waits until flags[base + k] has reached this rank's epoch (bounded by
+// `ticks` of the 100 MHz counter; a timeout records 1 + base + k in flags[ERR]).
+__global__ __launch_bounds__(64) void k_peer_wait(unsigned* flags, int base, int world, unsigned long long ticks) {
+  const int k = threadIdx.x;
+  if (k >= world) return;
+  if (__hip_atomic_load(flags + kPeerErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const unsigned e = __hip_atomic_load(flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(sys_poll(flags + base + k) - e) < 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      __hip_atomic_store(flags + kPeerErr, (unsigned)(1 + base + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// The world's tail partials summed in rank order into the gradient arena's tail (the Adam shard
+// consumes and clears it).
+__global__ __launch_bounds__(256) void k_peer_tail_sum(PeerArgs a) {
+  if (threadIdx.x == 0) peer_acquire();
+  __syncthreads();
+  const int64_t n4 = a.tailn / 4;
+  const float* t = a.rtail[a.rank];
+  auto ld4 = [](const float* p) {
+    const uint2 lo = ld_sys8(p), hi = ld_sys8(p + 2);
+    return make_float4(__uint_as_float(lo.x), __uint_as_float(lo.y), __uint_as_float(hi.x), __uint_as_float(hi.y));
+  };
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 s = ld4(t + 4 * i);
+    for (int k = 1; k < a.world; ++k) {
+      const float4 v = ld4(t + (int64_t)k * a.tailn + 4 * i);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(a.tail_dst)[i] = s;
+  }
+}
+
+// After this rank's Adam shard (every workgroup of which released its parameter-wire stores):
+// this step's PARAM flag on every rank.
+__global__ __launch_bounds__(64) void k_peer_signal(PeerArgs a) {
+  const int k = threadIdx.x;
+  peer_release();
+  if (k >= a.world) return;
+  const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.rflags[k] + kPeerParam + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// W1's bf16 shadow from the parameter wire (tight rows of stride geo.n, chunks == 1), behind an
+// acquire in every workgroup.
+__global__ __launch_bounds__(256) void k_peer_shadow(const u16* __restrict__ w, ShadowSeg g) {
+  if (threadIdx.x == 0) peer_acquire();
+  __syncthreads();
+  const int q = g.cols / 4;
+  const int64_t n4 = g.rows * q;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / q;
+    const int c = (int)(i - r * q) * 4;
+    *reinterpret_cast<uint2*>(g.ptr + r * g.ld + c) = ld_sys8(w + r * g.cols + c);
+  }
+}
+
+int grid_of(int64_t n4) {
+  const int64_t b = (n4 + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+}  // namespace
+
+hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
+  if (a.world < 1 || a.world > kPeerMax || a.tailn % 4) return hipErrorInvalidValue;
+  const int g = grid_of(a.tailn / 4);
+  hipLaunchKernelGGL(k_peer_tail_push, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerGrad, a.world, ticks);
+  hipLaunchKernelGGL(k_peer_tail_sum, dim3(g), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_after_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
+  if (a.world < 1 || a.world > kPeerMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerParam, a.world, ticks);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_shadow(const uint16_t* wire, ShadowSeg seg, hipStream_t s) {
+  if (seg.cols % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_peer_shadow, dim3(grid_of(seg.rows * seg.cols / 4)), dim3(256), 0, s, wire, seg);
+  return hipGetLastError();
+}
+
+}  // namespace dssm
+
+// ---- C-ABI: fine-grained buffers and their IPC handles ------------------------------------------
+namespace {
+int perr(int code, const std::string& m) { return dssm::report_error(code, m.c_str()); }
+}  // namespace
+
+extern "C" {
+
+int dssm_peer_alloc(int64_t bytes, void** out) {
+  if (!out || bytes <= 0) return perr(DSSM_E_INVALID, "dssm_peer_alloc: bytes > 0 and an output pointer");
+  *out = nullptr;
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained);
+  if (e != hipSuccess) return perr(DSSM_E_HIP, std::string("hipExtMallocWithFlags(fine-grained): ") + hipGetErrorString(e));
+  e = hipMemset(*out, 0, (size_t)bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    (void)hipFree(*out);
+    *out = nullptr;
+    return perr(DSSM_E_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  }
+  return DSSM_OK;
+}
+
+int dssm_peer_free(void* p) {
+  if (!p) return DSSM_OK;
+  hipError_t e = hipFree(p);
+  return e == hipSuccess ? DSSM_OK : perr(DSSM_E_HIP, std::string("hipFree: ") + hipGetErrorString(e));
+}
+
+int dssm_ipc_handle(void* p, void* out64) {
+  if (!p || !out64) return perr(DSSM_E_INVALID, "dssm_ipc_handle: null argument");
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle larger than 64 bytes");
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return perr(DSSM_E_HIP, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+  memset(out64, 0, 64);
+  memcpy(out64, &h, sizeof(h));
+  return DSSM_OK;
+}
+
+int dssm_ipc_open(const void* in64, void** out) {
+  if (!in64 || !out) return perr(DSSM_E_INVALID, "dssm_ipc_open: null argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, in64, sizeof(h));
+  *out = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) return perr(DSSM_E_HIP, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+  return DSSM_OK;
+}
+
+int dssm_ipc_close(void* p) {
+  if (!p) return DSSM_OK;
+  hipError_t e = hipIpcCloseMemHandle(p);
+  return e == hipSuccess ? DSSM_OK : perr(DSSM_E_HIP, std::string("hipIpcCloseMemHandle: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -219,6 +219,17 @@ struct dssm_plan {
   const uint16_t* w1_wire = nullptr;
   dssm::WireGeo geo{};
   int dp_rank = 0;
+  // peer-store exchange (dssm_plan_set_dp_peers, peer.hip): every rank's stage / parameter wire /
+  // tail stage / flags mapped into this process; world 0: off
+  struct PeerSet {
+    int world = 0;
+    uint16_t* stage[dssm::kPeerMax] = {};
+    uint16_t* pwire[dssm::kPeerMax] = {};
+    float* tail[dssm::kPeerMax] = {};
+    unsigned* flags[dssm::kPeerMax] = {};
+    unsigned long long wait_ticks = 2000000000ull;  // 20 s of the 100 MHz counter
+  } peer;
+  bool peer_on() const { return peer.world > 0 && pwire != nullptr; }
   bool dp_defer_gradpass = false;  // the data-parallel graph builder launches the chunks itself
   // the data-parallel graph builder's hook after each Adam chunk launch (that chunk's all-gather)
   std::function<int(int)> dp_hook;
@@ -1037,6 +1048,14 @@ static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s, int chunk) {
   a.gout = P->gwire;
   a.geo = P->geo;
   a.wchunk = P->geo.wp > 1 ? chunk : -1;
+  if (P->peer_on()) {  // rank i's rows of owner j: block i of j's stage (the all-to-all's layout)
+    const int64_t sub = P->sub_elems();
+    a.npeer = P->peer.world;
+    a.peer_sync = 1;
+    for (int j = 0; j < a.npeer; ++j)
+      a.gpeer[j] = reinterpret_cast<uint16_t*>(reinterpret_cast<intptr_t>(P->peer.stage[j]) +
+                                               (intptr_t)((int64_t)(P->dp_rank - j) * sub * 2));
+  }
   // the pass of b1's row (the last chunk) also sums the deferred dW_l split-K slabs into the
   // gradient arena (no separate reduce launches; the tail's all-reduce follows this launch)
   if (chunk < 0 || chunk == P->geo.wp - 1) {
@@ -1080,6 +1099,11 @@ static int dp_adam_chunk(dssm_plan* P, const dssm::AdamStep& base, int c, hipStr
   a.gstage = P->gstage + (int64_t)c * P->geo.ww * sub;
   a.gbase4 = a.d4_begin;
   a.pwire_off4 = ((int64_t)c * P->geo.ww + P->dp_rank) * sub / 4 - a.d4_begin;
+  if (P->peer_on()) {  // bf16(W1) of the shard into every rank's parameter wire
+    a.npeer = P->peer.world;
+    a.peer_sync = 1;
+    for (int k = 0; k < a.npeer; ++k) a.ppeer[k] = P->peer.pwire[k];
+  }
   if (!last) {
     a.t4_begin = a.t4_end = 0;
     a.no_advance = 1;
@@ -1225,6 +1249,11 @@ int dssm_plan_set_dp_wire(dssm_plan* P, int world, int rank, int chunks, uint16_
                           const uint16_t* stage, uint16_t* param_wire, int64_t count) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (P->capturing) return fail(DSSM_E_INVALID, "the wire cannot change during a graph capture");
+  {  // a new wire drops the peer set (dssm_plan_set_dp_peers maps the new buffers)
+    const unsigned long long t = P->peer.wait_ticks;
+    P->peer = dssm_plan::PeerSet{};
+    P->peer.wait_ticks = t;
+  }
   if (!grad_wire && !param_wire && !stage) {
     P->gwire = P->pwire = nullptr;
     P->gstage = nullptr;
@@ -1272,7 +1301,82 @@ int dssm_plan_dp_geometry(const dssm_plan* P, int64_t* out) {
 int dssm_plan_wire_shadows(dssm_plan* P, void* stream) {
   if (!P) return fail(DSSM_E_INVALID, "null plan");
   if (!P->pwire) return fail(DSSM_E_INVALID, "no wire set (dssm_plan_set_dp_wire)");
-  HIP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, -1, (hipStream_t)stream));
+  if (P->peer_on()) HIP_TRY(dssm::launch_peer_shadow(P->pwire, P->shadows().seg[0], (hipStream_t)stream));
+  else HIP_TRY(dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, -1, (hipStream_t)stream));
+  return DSSM_OK;
+}
+
+static dssm::PeerArgs peer_args(const dssm_plan* P) {
+  dssm::PeerArgs a{};
+  a.world = P->peer.world;
+  a.rank = P->dp_rank;
+  a.flags = P->peer.flags[P->dp_rank];
+  for (int k = 0; k < a.world; ++k) {
+    a.rflags[k] = P->peer.flags[k];
+    a.rtail[k] = P->peer.tail[k];
+  }
+  const int64_t we = P->wire_end();
+  a.tail_src = P->g + we;
+  a.tail_dst = P->g + we;
+  a.tailn = P->Lt.total - we;
+  return a;
+}
+
+int dssm_plan_set_dp_peers(dssm_plan* P, int world, uint16_t* const* stages, uint16_t* const* param_wires,
+                           float* const* tails, unsigned* const* flags) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (P->capturing) return fail(DSSM_E_INVALID, "the peers cannot change during a graph capture");
+  if (!stages && !param_wires && !tails && !flags) {
+    P->peer = dssm_plan::PeerSet{};
+    return DSSM_OK;
+  }
+  if (!stages || !param_wires || !tails || !flags) return fail(DSSM_E_INVALID, "stages, param_wires, tails and flags, or none");
+  if (!P->pwire) return fail(DSSM_E_INVALID, "set the bf16 wire first (dssm_plan_set_dp_wire)");
+  if (world < 1 || world > dssm::kPeerMax || world != P->geo.ww)
+    return fail(DSSM_E_INVALID, "peer exchange: world must be the wire's world size, at most 8");
+  if (P->geo.wp != 1) return fail(DSSM_E_UNSUPPORTED, "peer exchange: one wire chunk");
+  if (!wire_gradient_pass(P)) return fail(DSSM_E_UNSUPPORTED, "peer exchange: needs the wire gradient pass");
+  if ((P->Lt.total - P->wire_end()) % 4) return fail(DSSM_E_UNSUPPORTED, "peer exchange: tail not a multiple of 4");
+  for (int k = 0; k < world; ++k)
+    if (!stages[k] || !param_wires[k] || !tails[k] || !flags[k]) return fail(DSSM_E_INVALID, "null peer buffer");
+  if (stages[P->dp_rank] != P->gstage || param_wires[P->dp_rank] != P->pwire)
+    return fail(DSSM_E_INVALID, "this rank's stage and parameter wire must be the wire's (dssm_plan_set_dp_wire)");
+  dssm_plan::PeerSet ps;
+  ps.world = world;
+  ps.wait_ticks = P->peer.wait_ticks;
+  for (int k = 0; k < world; ++k) {
+    ps.stage[k] = stages[k];
+    ps.pwire[k] = param_wires[k];
+    ps.tail[k] = tails[k];
+    ps.flags[k] = flags[k];
+  }
+  P->peer = ps;
+  return DSSM_OK;
+}
+
+int dssm_plan_set_peer_timeout(dssm_plan* P, double ms) {
+  if (!P || !(ms > 0.0)) return fail(DSSM_E_INVALID, "null plan or timeout <= 0");
+  P->peer.wait_ticks = (unsigned long long)(ms * 1e5);  // 100 MHz counter
+  return DSSM_OK;
+}
+
+int dssm_plan_peer_exchange(dssm_plan* P, int phase, void* stream) {
+  if (!P) return fail(DSSM_E_INVALID, "null plan");
+  if (!P->peer_on()) return fail(DSSM_E_INVALID, "no peer exchange set (dssm_plan_set_dp_peers)");
+  hipStream_t s = (hipStream_t)stream;
+  const dssm::PeerArgs a = peer_args(P);
+  if (phase == 0) HIP_TRY(dssm::launch_peer_before_adam(a, P->peer.wait_ticks, s));
+  else if (phase == 1) HIP_TRY(dssm::launch_peer_after_adam(a, P->peer.wait_ticks, s));
+  else return fail(DSSM_E_INVALID, "phase: 0 (before Adam) or 1 (after Adam)");
+  return DSSM_OK;
+}
+
+int dssm_plan_peer_status(const dssm_plan* P, unsigned* out2) {
+  if (!P || !out2) return fail(DSSM_E_INVALID, "null argument");
+  if (!P->peer_on()) return fail(DSSM_E_INVALID, "no peer exchange set (dssm_plan_set_dp_peers)");
+  unsigned* f = P->peer.flags[P->dp_rank];
+  HIP_TRY(hipMemcpy(&out2[0], f + dssm::kPeerErr, sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&out2[1], f + dssm::kPeerSeq, sizeof(unsigned), hipMemcpyDeviceToHost));
   return DSSM_OK;
 }
 
@@ -1923,6 +2027,12 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
     HIP_TRY(dssm::launch_spin(k.latency_ns + bytes / k.gbps, cs));
     return DSSM_OK;
   }
+  if (k.mode == 3) {  // peer stores: the all-to-all happened inside the gradient pass (peer.hip)
+    const dssm::PeerArgs a = peer_args(P);
+    if (kind == 0) HIP_TRY(dssm::launch_peer_before_adam(a, P->peer.wait_ticks, cs));
+    if (kind == 1) HIP_TRY(dssm::launch_peer_after_adam(a, P->peer.wait_ticks, cs));
+    return DSSM_OK;  // kind 2: the tail rode in the push
+  }
   uint16_t* gw = P->gwire + chunk * blk;
   uint16_t* st = const_cast<uint16_t*>(P->gstage) + chunk * blk;
   uint16_t* pw = P->pwire + chunk * blk;
@@ -1952,8 +2062,10 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
   if (overlap)
     return fail(DSSM_E_INVALID, "overlap: removed (the two-stream variant measured slower than the one-stream "
                                 "graph and its captured RCCL steps raced at world 1; DESIGN 6)");
-  if (comm < 0 || comm > 2 || (comm == 2 && !(link_gbps > 0.f)))
-    return fail(DSSM_E_INVALID, "comm: 0 RCCL, 1 device copies, 2 modelled (link_gbps > 0)");
+  if (comm < 0 || comm > 3 || (comm == 2 && !(link_gbps > 0.f)))
+    return fail(DSSM_E_INVALID, "comm: 0 RCCL, 1 device copies, 2 modelled (link_gbps > 0), 3 peer stores");
+  if ((comm == 3) != P->peer_on())
+    return fail(DSSM_E_INVALID, "comm 3 (peer stores) if and only if dssm_plan_set_dp_peers is set");
   if (comm == 0 && (!g_comm || g_world != P->geo.ww || g_rank != P->dp_rank))
     return fail(DSSM_E_INVALID, "comm 0 needs dssm_comm_init with the wire's world and rank");
   if (comm == 0 && P->geo.ww > 1 && P->gstage == P->gwire)
@@ -2007,7 +2119,7 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
       if (c == 0) P->probe_end(DSSM_PROBE_DP_ALL_TO_ALL, s);
     }
     P->probe_begin(DSSM_PROBE_DP_TAIL, s);
-    if (!rc && !P->on(DSSM_OPT_TAIL_IN_A2A))  // the fp32 tail (b1's row: the last chunk's pass)
+    if (!rc && !P->on(DSSM_OPT_TAIL_IN_A2A) && comm != 3)  // the fp32 tail (b1's row: the last chunk's pass)
       rc = dp_collective(P, k, 2, 0, s);
     P->probe_end(DSSM_PROBE_DP_TAIL, s);
     // Adam chunk by chunk, each chunk's all-gather behind its Adam
@@ -2022,9 +2134,14 @@ int dssm_plan_graph_build_dp_steps(dssm_plan* P, const int32_t* const* indptrs, 
     // one chunk the wire already holds W1 row-major: the region's next step reads it directly
     // (w1_wire, tight rows of stride n: RawRow8<u16t>) and only the last step rebuilds the shadow,
     // which the next region's first step and the eval forward read.
-    const bool direct = C == 1 && P->geo.n == P->Lt.n[0] && i + 1 < nsteps;
+    // (peer stores: the shadow is rebuilt every step, behind the acquire of k_peer_shadow)
+    const bool direct = C == 1 && P->geo.n == P->Lt.n[0] && i + 1 < nsteps && comm != 3;
     P->probe_begin(DSSM_PROBE_DP_SHADOW, s);
-    for (int c = 0; c < C && !rc && !direct; ++c) {
+    if (!rc && comm == 3) {
+      hipError_t e_ = dssm::launch_peer_shadow(P->pwire, P->shadows().seg[0], s);
+      if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string("launch_peer_shadow: ") + hipGetErrorString(e_));
+    }
+    for (int c = 0; c < C && !rc && !direct && comm != 3; ++c) {
       hipError_t e_ = dssm::launch_wire_shadow(P->pwire, P->shadows().seg[0], P->geo, C > 1 ? c : -1, s);
       if (e_ != hipSuccess) rc = fail(DSSM_E_HIP, std::string("launch_wire_shadow: ") + hipGetErrorString(e_));
     }

@@ -29,6 +29,13 @@ Transports for the same collectives:
   through torch.distributed once (bootstrap only);
 * "torch": torch.distributed (gloo on the CPU tests; the "nccl" backend = RCCL as a fallback).
 
+exchange="peer" (bf16 wire, one chunk; PeerBuffers below, csrc/peer.hip): no collective on the data
+path at all.  The gradient pass stores each owner's bf16 W1 rows straight into that owner's stage
+(HIP IPC-mapped fine-grained buffers), the fp32 tail is pushed to every rank and summed there in
+rank order, and each Adam shard stores its bf16 rows into every rank's parameter wire; per-step
+epoch flags order the hand-offs (DESIGN §6 "peer exchange").  The transport is then used only for
+bootstrap (the IPC handles) and gather_state().
+
 Every collective the chosen schedule uses (SCHEDULE_OPS) is self-tested at start-up on small exact
 patterns and every rank must agree.  With comm="auto" a failing library transport falls back to
 torch.distributed and a failing zero schedule (mode="auto") is demoted to "allreduce"; each such
@@ -311,6 +318,87 @@ def select_transport(rank: int, world: int, device, comm: str, ops) -> "tuple":
     return None, notes
 
 
+class _DeviceArray:
+    """__cuda_array_interface__ of library-allocated device memory (for a torch view of it)."""
+
+    def __init__(self, addr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(addr), False),
+                                         "version": 2}
+
+
+def device_view(addr: int, n: int, dtype, device) -> torch.Tensor:
+    """A torch tensor over n elements at device address addr (not owned: keep the allocation alive)."""
+    ts = {torch.bfloat16: "<i2", torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+    t = torch.as_tensor(_DeviceArray(addr, n, ts), device=device)
+    return t.view(torch.bfloat16) if dtype == torch.bfloat16 else t
+
+
+class PeerBuffers:
+    """The peer-store exchange's buffers (include/dssm.h dssm_peer_alloc / dssm_ipc_*): this rank's
+    fine-grained stage, parameter wire, tail stage and flags, and every other rank's, mapped through
+    HIP IPC with handles exchanged once over torch.distributed (all_gather_object).  addr[kind][r]
+    is rank r's buffer as seen from this process.  A barrier follows, so every rank's zeroed flags
+    exist before any rank's first step."""
+
+    KINDS = ("stage", "pwire", "tail", "flags")
+
+    def __init__(self, world: int, rank: int, wire_n: int, tail_n: int, device):
+        self.lib = _lib.load()
+        self.world, self.rank = world, rank
+        sizes = {"stage": 2 * wire_n, "pwire": 2 * wire_n, "tail": 4 * world * tail_n,
+                 "flags": _lib.PEER_FLAG_BYTES}
+        self.own, self.opened = {}, []
+        try:
+            for k in self.KINDS:
+                p = C.c_void_p()
+                check(self.lib.dssm_peer_alloc(sizes[k], C.byref(p)), f"peer_alloc {k}")
+                self.own[k] = int(p.value)
+            handles = {}
+            for k in self.KINDS:
+                h = C.create_string_buffer(64)
+                check(self.lib.dssm_ipc_handle(C.c_void_p(self.own[k]), h), f"ipc_handle {k}")
+                handles[k] = h.raw
+            allh = [None] * world
+            if world > 1:
+                dist.all_gather_object(allh, handles)
+            else:
+                allh[0] = handles
+            self.addr = {k: [0] * world for k in self.KINDS}
+            for r in range(world):
+                for k in self.KINDS:
+                    if r == rank:
+                        self.addr[k][r] = self.own[k]
+                        continue
+                    p = C.c_void_p()
+                    check(self.lib.dssm_ipc_open(C.create_string_buffer(allh[r][k], 64), C.byref(p)),
+                          f"ipc_open rank {r} {k}")
+                    self.opened.append(int(p.value))
+                    self.addr[k][r] = int(p.value)
+        except Exception:
+            self._release()
+            raise
+        self.stage = device_view(self.own["stage"], wire_n, torch.bfloat16, device)
+        self.param_wire = device_view(self.own["pwire"], wire_n, torch.bfloat16, device)
+
+    def _release(self):
+        for a in self.opened:
+            self.lib.dssm_ipc_close(C.c_void_p(a))
+        self.opened = []
+        for a in self.own.values():
+            self.lib.dssm_peer_free(C.c_void_p(a))
+        self.own = {}
+
+    def close(self):
+        """Unmap the peers' buffers and free this rank's, after every rank is done with them."""
+        if not self.own:
+            return
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        self.stage = self.param_wire = None
+        self._release()
+
+
 def shard_bounds(n_pad: int, n: int, rank: int, world: int):
     """Rank's optimizer shard of an arena of n elements padded to n_pad (equal shards)."""
     s = n_pad // world
@@ -321,7 +409,8 @@ class DataParallel:
     """Wraps a DSSM model: step = forward + backward + gradient exchange + Adam (see module doc)."""
 
     def __init__(self, model, comm: str = "auto", mode: str = "auto", wire: str = "auto", chunks: int = 1,
-                 overlap: bool = False, sparse: bool = False, tail_in_a2a="auto", verify_sparse: bool = True):
+                 overlap: bool = False, sparse: bool = False, tail_in_a2a="auto", verify_sparse: bool = True,
+                 exchange: str = "collective", peer_timeout_ms: float = 0.0):
         """comm: "auto" (the library's RCCL communicator on GPUs, torch.distributed as the
         self-tested fallback), "rccl" (strict: no fallback) or "torch".  mode / wire: "auto" picks
         zero + bf16 wire for bf16 models; an explicit "zero" is strict (never demoted).  Every
@@ -339,12 +428,26 @@ class DataParallel:
         is recorded in .fallbacks; True: strict (a failing self-test raises); False: off.
         verify_sparse: before the first step, one exchange of a synthetic gradient through the
         sparse path and the dense all-to-all; the stages must be bit-identical on every rank, or the
-        sparse path is turned off (recorded in .fallbacks)."""
+        sparse path is turned off (recorded in .fallbacks).
+        exchange: "collective" (the schedules above) or "peer" (the peer-store exchange: zero / bf16
+        wire in one chunk, HIP-engine models on GPUs, world <= 8; no fallback: a failure raises).
+        peer_timeout_ms: the peer waits' bound (0: the library's default, 20 s)."""
         if overlap:  # removed in round 3 (DESIGN §6): slower; refused before any side effect
             raise ValueError("overlap is no longer supported: the exchange runs on one captured stream")
+        if exchange not in ("collective", "peer"):
+            raise ValueError("exchange: 'collective' or 'peer'")
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.peer = None
+        if exchange == "peer":
+            if mode not in ("auto", "zero") or wire not in ("auto", "bf16") or int(chunks) != 1 or sparse:
+                raise ValueError("the peer exchange is the zero schedule on the bf16 wire in one chunk")
+            if getattr(model, "dtype", "fp32") != "bf16" or not hasattr(model, "set_dp_peers"):
+                raise ValueError("the peer exchange needs a bf16 HIP-engine model")
+            if self.world > 8:
+                raise ValueError("the peer exchange supports at most 8 ranks")
+            mode, wire, tail_in_a2a = "zero", "bf16", False
         npad = model.params.numel()
         strict_mode = mode == "zero"
         if mode == "auto":
@@ -353,7 +456,7 @@ class DataParallel:
             raise ValueError("the zero schedule needs 64-float aligned equal shards")
         if mode not in ("zero", "allreduce"):
             raise ValueError("mode: 'zero', 'allreduce' or 'auto'")
-        self.mode = mode if self.world > 1 else "allreduce"
+        self.mode = mode if (self.world > 1 or exchange == "peer") else "allreduce"
         if wire == "auto":
             wire = "bf16" if getattr(model, "dtype", "fp32") == "bf16" else "fp32"
         if wire not in ("bf16", "fp32"):
@@ -361,8 +464,9 @@ class DataParallel:
         self.wire = wire if self.mode == "zero" else "fp32"
         self.tx = None
         self.fallbacks = []
-        if self.world > 1:
+        if self.world > 1 or exchange == "peer":
             model.set_fused_w1_adam(False)  # the exchange needs the materialized dW1
+        if self.world > 1:
             self.tx = self._transport(comm, strict_mode)
         self.grad_wire = self.param_wire = self.stage = None
         self.chunks, self.overlap = 1, False
@@ -373,9 +477,24 @@ class DataParallel:
             n = model.dp_wire_size(self.world, self.chunks)
             dev = model.params.device
             self.grad_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
-            self.param_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
-            self.stage = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+            if exchange == "peer":  # the stage and parameter wire are the fine-grained, IPC-shared ones
+                model.set_dp_wire(self.world, self.rank, 1, self.grad_wire,
+                                  torch.zeros(n, dtype=torch.bfloat16, device=dev), self.grad_wire.clone())
+                geo0 = model.dp_geometry()
+                self.peer = PeerBuffers(self.world, self.rank, n, geo0["n_params"] - geo0["extent"], dev)
+                self.param_wire, self.stage = self.peer.param_wire, self.peer.stage
+            else:
+                self.param_wire = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+                self.stage = torch.zeros(n, dtype=torch.bfloat16, device=dev)
             model.set_dp_wire(self.world, self.rank, self.chunks, self.grad_wire, self.stage, self.param_wire)
+            if self.peer is not None:
+                a = self.peer.addr
+                model.set_dp_peers(self.world, a["stage"], a["pwire"], a["tail"], a["flags"])
+                if peer_timeout_ms > 0:
+                    model.set_peer_timeout(peer_timeout_ms)
+                torch.cuda.synchronize()
+                if self.world > 1:
+                    dist.barrier()  # every rank's zeroed flags attached before any rank's first step
             geo = model.dp_geometry()
             self.extent, self.sub = geo["extent"], geo["sub"]
             self.begin, self.end = geo["shard_begin"], geo["shard_end"]
@@ -422,6 +541,8 @@ class DataParallel:
     def schedule(self) -> str:
         """What the exchange runs, e.g. "zero/bf16 via rccl" (bench.py's config.dp_exchange)."""
         s = f"{self.mode}/{self.wire}" if self.mode == "zero" else self.mode
+        if getattr(self, "peer", None) is not None:
+            return f"{s} via peer stores"
         if getattr(self, "sparse", False):
             s += " sparse"
         if getattr(self, "tail_group", False):
@@ -524,6 +645,9 @@ class DataParallel:
             warnings.warn(f"DataParallel: {note}", RuntimeWarning, stacklevel=3)
 
     def exchange_before_adam(self):
+        if self.peer is not None:  # the rows went out in the gradient pass: tail push, wait, tail sum
+            self.model.peer_exchange(0)
+            return
         if self.world == 1:
             return
         g = self.model.grads
@@ -547,6 +671,9 @@ class DataParallel:
             self.tx.reduce_scatter_(g, self.shard)
 
     def exchange_after_adam(self):
+        if self.peer is not None:  # the shard's rows went out in Adam: this rank's flag, wait for all
+            self.model.peer_exchange(1)
+            return
         if self.mode == "zero" and self.wire == "bf16":
             blk = self.world * self.sub
             for p in range(self.chunks):
@@ -563,7 +690,7 @@ class DataParallel:
     def gather_state(self):
         """Full parameters and Adam m / v on every rank (the zero schedule keeps W1's sharded):
         before a checkpoint."""
-        if self.mode != "zero":
+        if self.mode != "zero" or self.world == 1:
             return
         if self.wire == "bf16":
             # W1's fp32 rows (parameters too: other ranks' shards are stale on this one) through
@@ -593,6 +720,8 @@ class DataParallel:
     def capturable(self) -> bool:
         """Whole steps, collectives included, can be captured into one graph: the library's RCCL
         transport with the zero / bf16-wire schedule (dssm_plan_graph_build_dp_steps)."""
+        if self.peer is not None:
+            return True
         return (getattr(self.tx, "capturable", False) and self.mode == "zero" and self.wire == "bf16"
                 and not self.sparse)
 
@@ -605,8 +734,8 @@ class DataParallel:
         Adam.  Replay: model.graph_launch."""
         if not self.capturable:
             raise RuntimeError(f"the {self.schedule} exchange cannot be captured (needs zero/bf16 via rccl)")
-        return self.model.graph_build_dp_steps(batches, 1.0 / self.world, comm=0, overlap=self.overlap,
-                                               probes=probes)
+        return self.model.graph_build_dp_steps(batches, 1.0 / self.world, comm=3 if self.peer is not None else 0,
+                                               overlap=self.overlap, probes=probes)
 
     def build_graphs(self, staged, probe_batch=None):
         """Capture, per staged device batch (indptr, indices, values), the forward + backward as a
@@ -668,7 +797,18 @@ class DataParallel:
         """(plain fwd+bwd graphs, merged graphs, Adam graph): for reading the timing probes."""
         return self._g_plain, self._g_merged, self._g_adam
 
+    def peer_check(self):
+        """Raise if a peer wait timed out (dssm_plan_peer_status); returns the exchanged step count."""
+        st = self.model.peer_status()
+        if st["error"]:
+            raise RuntimeError(f"peer exchange: a wait timed out (flag {st['error'] - 1}) after {st['steps']} steps")
+        return st["steps"]
+
     def close(self):
+        if self.peer is not None:
+            self.model.set_dp_peers(0, None, None, None, None)
+            self.peer.close()
+            self.peer = None
         if self.tx is not None:
             self.tx.destroy()
             self.tx = None

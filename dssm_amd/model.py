@@ -295,6 +295,29 @@ class DSSM:
         keys = ("world", "chunks", "rows", "sub", "shard_begin", "shard_end", "extent", "n_params")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def set_dp_peers(self, world: int, stages, param_wires, tails, flags):
+        """The peer-store exchange (dssm_plan_set_dp_peers): every rank's stage / parameter wire /
+        tail stage / flags as device addresses (ints) indexed by rank, this rank's own included (its
+        stage and parameter wire the ones set_dp_wire attached).  All None: off."""
+        if stages is None:
+            check(self.lib.dssm_plan_set_dp_peers(self._plan, 0, None, None, None, None), "set_dp_peers")
+            return
+        arr = [(C.c_void_p * world)(*[int(x) for x in lst]) for lst in (stages, param_wires, tails, flags)]
+        check(self.lib.dssm_plan_set_dp_peers(self._plan, int(world), *arr), "set_dp_peers")
+
+    def set_peer_timeout(self, ms: float):
+        check(self.lib.dssm_plan_set_peer_timeout(self._plan, float(ms)), "set_peer_timeout")
+
+    def peer_exchange(self, phase: int, stream=None):
+        """dssm_plan_peer_exchange: phase 0 between backward and Adam, 1 after Adam."""
+        check(self.lib.dssm_plan_peer_exchange(self._plan, int(phase), stream_ptr(stream)), "peer_exchange")
+
+    def peer_status(self) -> Dict[str, int]:
+        """{error: 0 or 1 + the flag index a wait timed out on, steps: exchanged steps} (synchronous)."""
+        out = (C.c_uint * 2)()
+        check(self.lib.dssm_plan_peer_status(self._plan, out), "peer_status")
+        return {"error": int(out[0]), "steps": int(out[1])}
+
     def wire_shadows(self, stream=None):
         check(self.lib.dssm_plan_wire_shadows(self._plan, stream_ptr(stream)), "wire_shadows")
 

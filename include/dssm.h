@@ -224,7 +224,8 @@ int dssm_plan_wire_shadows(dssm_plan* plan, void* stream);
  * comm: 0 = the library's RCCL communicator (dssm_comm_init; world / rank must match the wire's);
  * 1 = rehearsal on one GPU, each collective replaced by a device copy of its bytes; 2 = rehearsal,
  * each collective replaced by a kernel that holds its stream for latency_us + (bytes this rank
- * sends) / link_gbps (GB/s) -- the exchange's modelled time on the links.  with_probes: the Adam
+ * sends) / link_gbps (GB/s) -- the exchange's modelled time on the links; 3 = the peer-store
+ * exchange (dssm_plan_set_dp_peers, below): no collectives, the shadow rebuilt every step.  with_probes: the Adam
  * probe brackets the last step's Adam launches. */
 int dssm_plan_graph_build_dp_steps(dssm_plan* plan, const int32_t* const* indptrs,
                                    const int32_t* const* indices, const float* const* values,
@@ -540,6 +541,39 @@ int dssm_all_to_all_tail(const void* send, void* recv, int64_t count, int dtype,
 int dssm_all_to_allv(const void* send, const int64_t* send_counts, void* recv, const int64_t* recv_counts,
                      int dtype, void* tail, int64_t tail_count, int tail_dtype, void* stream);
 int dssm_comm_destroy(void);
+
+/* Peer-store exchange (DESIGN.md §6 "peer exchange"; dssm_amd/csrc/peer.hip): the bf16-wire
+ * schedule with no collective library on the data path, replacing the gradient all-to-all, the
+ * fp32 tail all-reduce and the parameter all-gather that stand in for the reference's fp32 gradient
+ * reduction (new_dssm.py:215-217 over a sharded batch).  Each rank allocates its stage and parameter
+ * wire (dssm_plan_dp_wire_size elements of bf16 each), its tail stage (world * (param_count -
+ * extent) floats) and its flags (DSSM_PEER_FLAG_BYTES) with dssm_peer_alloc (fine-grained device
+ * memory, zeroed), shares dssm_ipc_handle of each with every rank, maps the others' with
+ * dssm_ipc_open, attaches its own stage / parameter wire with dssm_plan_set_dp_wire (one chunk) and
+ * then the world's buffers, indexed by rank, with dssm_plan_set_dp_peers.  All ranks must attach
+ * zeroed flags before any rank's first step (a host barrier).  Then:
+ *   - dssm_plan_backward's gradient pass stores this rank's bf16 W1 gradient rows straight into each
+ *     owner's stage (block `rank`), as the all-to-all would have delivered them;
+ *   - dssm_plan_peer_exchange(phase 0), between backward and adam: the fp32 tail pushed to every
+ *     rank, a wait for every rank's gradient pass of this step, the tails summed in rank order;
+ *   - dssm_plan_adam stores bf16(W1) of the shard into every rank's parameter wire;
+ *   - dssm_plan_peer_exchange(phase 1), after adam: this rank's "parameters ready" flag on every
+ *     rank, a wait for every rank's;
+ *   - dssm_plan_wire_shadows rebuilds W1's shadow from the parameter wire (behind an acquire).
+ * dssm_plan_graph_build_dp_steps with comm 3 captures the same sequence.  Waits are bounded
+ * (dssm_plan_set_peer_timeout, default 20 s): a timeout is recorded, later waits return at once, and
+ * dssm_plan_peer_status reports {error (0: none, else 1 + flag index), steps exchanged}. */
+#define DSSM_PEER_FLAG_BYTES 4096
+int dssm_peer_alloc(int64_t bytes, void** out);
+int dssm_peer_free(void* ptr);
+int dssm_ipc_handle(void* ptr, void* out64);
+int dssm_ipc_open(const void* handle64, void** out);
+int dssm_ipc_close(void* ptr);
+int dssm_plan_set_dp_peers(dssm_plan* plan, int world, uint16_t* const* stages, uint16_t* const* param_wires,
+                           float* const* tails, unsigned* const* flags);
+int dssm_plan_set_peer_timeout(dssm_plan* plan, double ms);
+int dssm_plan_peer_exchange(dssm_plan* plan, int phase, void* stream);
+int dssm_plan_peer_status(const dssm_plan* plan, unsigned* out2);
 /* Packed rows of the sparse exchange, stride n + 4 u16: [row id int32][pad][n u16 of src row id].
  * pack: packed row k from src row rows[k] (n % 4 == 0); unpack: dst row (id - row_base) = packed row
  * k's data for ids in [row_base, row_base + nrows) (others skipped). */
