@@ -67,7 +67,7 @@ def parse():
                     help="analysis only (N=1): rank 0's share of a W-rank zero/bf16-wire step (the data-"
                          "parallel step graph, chunked gradient pass / Adam / shadow rebuild) with each "
                          "collective replaced per --rehearse-comm")
-    ap.add_argument("--rehearse-comm", default="model", choices=["model", "copy"],
+    ap.add_argument("--rehearse-comm", default="model", choices=["model", "copy", "peer"],
                     help="rehearsal collectives: model = a kernel holding the comm stream for the modelled "
                          "link time (--link-latency-us + bytes sent / --link-gbps); copy = a device copy of "
                          "the same bytes")
@@ -126,6 +126,13 @@ def parse():
     ap.add_argument("--dp-alt-sparse", type=int, default=1,
                     help="N>1 started as a plain process: also run the --dp-sparse 1 exchange as a third child "
                          "and report it as dp_alt_sparse")
+    ap.add_argument("--dp-exchange", default="collective", choices=["collective", "peer"],
+                    help="N>1 zero/bf16 schedule: the library's RCCL collectives (default) or the peer-store "
+                         "exchange (DataParallel(exchange='peer'): gradient rows stored into the owners' stages "
+                         "by the gradient pass, parameters into every rank's wire, epoch flags; DESIGN §6)")
+    ap.add_argument("--dp-alt-peer", type=int, default=1,
+                    help="N>1 started as a plain process: also run the --dp-exchange peer step as a child and "
+                         "report it as dp_alt_peer")
     ap.add_argument("--dp-check", type=int, default=1,
                     help="N>1: after the timed region, gather the sharded optimizer state and compare a "
                          "digest of every rank's parameters / Adam m / v (reported as dp_check)")
@@ -199,6 +206,7 @@ def spawn_ranks(args) -> int:
     argv = sys.argv[1:]
     alt = args.dp_alt and args.model == "bow" and args.dp_mode != "allreduce"
     alt_sparse = alt and args.dp_alt_sparse and not args.dp_sparse
+    alt_peer = alt and args.dp_alt_peer and args.dp_exchange == "collective" and args.gpus <= 8
     t_head = time.perf_counter()
     rc, lines = _run_ranks(args, argv, capture=alt)
     if not alt:
@@ -211,21 +219,23 @@ def spawn_ranks(args) -> int:
     legs = [("dp_alt", ["--dp-mode", "allreduce", "--wire", "fp32"])]
     if alt_sparse:
         legs.append(("dp_alt_sparse", ["--dp-sparse", "1"]))
+    if alt_peer:
+        legs.append(("dp_alt_peer", ["--dp-exchange", "peer"]))
     # each alternative leg gets a wall-clock limit from the headline child's own time
     limit = max(180.0, 3.0 * (time.perf_counter() - t_head))
     for key, extra in legs:
         t0 = time.perf_counter()
-        arc, alines = _run_ranks(args, argv + extra + ["--dp-alt", "0", "--dp-alt-sparse", "0"], capture=True,
-                                 limit=limit)
+        arc, alines = _run_ranks(args, argv + extra + ["--dp-alt", "0", "--dp-alt-sparse", "0", "--dp-alt-peer", "0"],
+                                 capture=True, limit=limit)
         if arc != 0 or not alines:
             late = time.perf_counter() - t0 >= limit
             out[key] = {"error": f"timed out after {limit:.0f} s" if late else f"exit {arc}, no line"}
             continue
         a = json.loads(alines[-1])
-        out[key] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")}
+        out[key] = {k: a.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup", "final_loss")}
         out[key].update({k: a["config"].get(k) for k in ("dp_exchange", "dp_launch", "comm", "dp_sparse")
                          if k in a.get("config", {})})
-        for k in ("dp_kernels_ms", "dp_check"):
+        for k in ("dp_kernels_ms", "dp_check", "peer_status"):
             if k in a:
                 out[key][k] = a[k]
     print(json.dumps(out), flush=True)
@@ -838,7 +848,7 @@ def main():
     if world > 1:
         from dssm_amd.dist import DataParallel
         dp = DataParallel(model, comm=args.comm, mode=args.dp_mode, wire=args.wire, chunks=args.dp_chunks,
-                          sparse=bool(args.dp_sparse))
+                          sparse=bool(args.dp_sparse), exchange=args.dp_exchange)
     rehearse = args.rehearse_world if world == 1 else 1
     if rehearse > 1:
         # rank 0's kernels of a W-rank bf16-wire step in the data-parallel step graph, each
@@ -847,6 +857,15 @@ def main():
         nw = model.dp_wire_size(rehearse, args.dp_chunks)
         wires = [torch.zeros(nw, dtype=torch.bfloat16, device=dev) for _ in range(3)]
         model.set_dp_wire(rehearse, 0, args.dp_chunks, *wires)
+        if args.rehearse_comm == "peer":  # rank 0 of the peer-store exchange, the peers' buffers local
+            from dssm_amd.dist import RehearsalPeers
+            if args.dp_chunks != 1:
+                raise SystemExit("--rehearse-comm peer: one wire chunk")
+            geo = model.dp_geometry()
+            rehearsal_peers = RehearsalPeers(rehearse, nw, geo["n_params"] - geo["extent"], dev)
+            model.set_dp_wire(rehearse, 0, 1, wires[0], rehearsal_peers.stage, rehearsal_peers.param_wire)
+            a = rehearsal_peers.addr
+            model.set_dp_peers(rehearse, a["stage"], a["pwire"], a["tail"], a["flags"])
 
     cols = ZipfColumns(D, uniform=args.columns == "uniform")
     staged = []
@@ -873,7 +892,7 @@ def main():
     dp_events = []  # split-graph data parallel: (phase, start, end) events of the last timed step
     if args.graph and args.feed == "device" and (rehearse > 1 or (dp is not None and dp.capturable)):
         MAX_REGION_STEPS = 256
-        comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2}[args.rehearse_comm]
+        comm_mode = 0 if rehearse == 1 else {"copy": 1, "model": 2, "peer": 3}[args.rehearse_comm]
 
         def dp_graph(batches, probes=False):
             if rehearse == 1:
@@ -1177,8 +1196,14 @@ def main():
         out["rehearsal"] = {"world": rehearse, "chunks": args.dp_chunks,
                             "collectives": ({"model": f"modelled: {args.link_latency_us} us + bytes sent / "
                                                       f"{args.link_gbps} GB/s per collective",
-                                             "copy": "device copies of the same bytes"}[args.rehearse_comm]),
+                                             "copy": "device copies of the same bytes",
+                                             "peer": "peer-store exchange, the peers' buffers local and their "
+                                                     "flags raised in advance (no link time)"}[args.rehearse_comm]),
                             "note": "rank 0 of an N-rank bf16-wire step on one GPU; not a headline number"}
+    if (dp is not None and dp.peer is not None) or (rehearse > 1 and args.rehearse_comm == "peer"):
+        out["peer_status"] = model.peer_status()
+        if out["peer_status"]["error"]:
+            raise SystemExit(f"bench: the peer exchange timed out: {out['peer_status']}")
     if dp is not None:
         out["config"]["dp_chunks"] = dp.chunks
         try:

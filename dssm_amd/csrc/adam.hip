@@ -515,10 +515,6 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
 #endif
     }
     const int64_t na = a.d4_end - a.d4_begin, nt = a.t4_end - a.t4_begin;
-    if (WIRE && a.peer_sync && a.gstage) {  // peer exchange: the stage was stored by other agents
-      if (threadIdx.x == 0) peer_acquire();
-      __syncthreads();
-    }
     if (WIRE && a.slab_to_g) {  // gradient pass: g = the deferred split-K slabs' sums (fixed order)
       for (int64_t j = (int64_t)bi * blockDim.x + threadIdx.x; j < nt; j += (int64_t)a.dense_blocks * blockDim.x) {
         const int64_t i = a.t4_begin + j;
@@ -578,9 +574,7 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
 #ifdef DSSM_WG_TL
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-  if (WIRE && a.peer_sync) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
   __syncthreads();
-  if (WIRE && a.peer_sync && threadIdx.x == 0) peer_release();  // before any later flag (peer.hip)
   ADAM_TL(1);
   if (threadIdx.x == 0 && a.ticket) {
     // Two-level ticket: same-address atomics serialise (~6 ns each; one counter for ~8k blocks
@@ -785,7 +779,7 @@ hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s) {
   if (pe != hipSuccess) return pe;
   dim3 grid(a.rank.nblocks + a.item_blocks + a.w1_blocks + a.dense_blocks), block(256);
   const bool wire = a.gout || a.wchunk >= 0 || a.wire4 > 0 || a.gstage || a.gwire || a.pwire || a.slab_to_g ||
-                    a.npeer || a.peer_sync;
+                    a.npeer;
 #define DSSM_ADAM_LAUNCH(TZ)                                                         \
   if (wire) hipLaunchKernelGGL((k_adam_step<TZ, true>), grid, block, 0, s, a);       \
   else hipLaunchKernelGGL((k_adam_step<TZ, false>), grid, block, 0, s, a)

@@ -306,7 +306,7 @@ __host__ __device__ inline int wire_chunk_row(const WireGeo& g, int chunk, int v
 
 // Peer-store exchange (peer.hip): flag words of each rank's flags buffer (one 256-B line each group)
 constexpr int kPeerMax = 8;  // ranks
-constexpr int kPeerGrad = 0, kPeerParam = 64, kPeerSeq = 128, kPeerTicket = 192, kPeerErr = 256;
+constexpr int kPeerGrad = 0, kPeerParam = 64, kPeerSeq = 128, kPeerTicket = 192, kPeerTicket2 = 224, kPeerErr = 256;
 constexpr int kPeerFlagWords = 320;
 // SYSTEM-scope release / acquire (fine-grained buffers shared with other agents); the explicit wait
 // keeps the compiler from dropping the drain after the write-back (MI355X_MICROARCH.md, compiler hazard)
@@ -318,21 +318,42 @@ __device__ __forceinline__ void peer_acquire() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-// payload accesses of the peer exchange: system-scope relaxed atomics (global_load / store ... sc0 sc1,
-// the same access the flags use), so every byte moves coherently whatever MTYPE the IPC-imported
-// mapping of a buffer carries; 8-B aligned
+// payload accesses of the peer exchange, 8-B aligned.  Loads: system-scope relaxed atomic loads
+// (global_load ... sc0 sc1, as the flag polls): measured necessary -- with plain loads behind a
+// system-scope acquire the second process read stale stage rows through its IPC-shared buffers
+// (DESIGN §6).  Stores: plain (measured sufficient; the signalling launches write back every XCD's
+// L2 at system scope before the flag).  Build knobs (measurement): DSSM_PEER_ST 1 makes the stores
+// system-scope atomics too, DSSM_PEER_LD 0 makes the loads plain.
+#ifndef DSSM_PEER_ST
+#define DSSM_PEER_ST 0
+#endif
+#ifndef DSSM_PEER_LD
+#define DSSM_PEER_LD 1
+#endif
 __device__ __forceinline__ void st_sys8(void* p, uint2 v) {
+#if DSSM_PEER_ST
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
                      (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  *reinterpret_cast<uint2*>(p) = v;
+#endif
 }
 __device__ __forceinline__ void st_sys4(void* p, unsigned v) {
+#if DSSM_PEER_ST
   __hip_atomic_store(reinterpret_cast<unsigned*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  *reinterpret_cast<unsigned*>(p) = v;
+#endif
 }
 __device__ __forceinline__ uint2 ld_sys8(const void* p) {
+#if DSSM_PEER_LD
   const unsigned long long u = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<void*>(p)),
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return make_uint2((unsigned)u, (unsigned)(u >> 32));
+#else
+  return *reinterpret_cast<const uint2*>(p);
+#endif
 }
 struct PeerArgs {
   int world, rank;
@@ -418,10 +439,9 @@ struct AdamStep {
   // peer-store exchange (peer.hip; wire chunks == 1): npeer ranks.  Gradient pass: row c's bf16
   // gradient goes to gpeer[c / geo.ws] + wire_row_off(geo, c) (owner j's stage, block of this rank)
   // instead of gout.  Adam: bf16(p) of the shard goes to every ppeer[k] at the wire offset instead of
-  // pwire.  peer_sync: the stage-reading workgroups acquire (system scope) first and every workgroup
-  // releases its stores (system scope) last.
+  // pwire; the stage is read with system-scope loads.  (The stores are plain: the signalling
+  // launches after this one write back every XCD's L2 at system scope before raising a flag.)
   int npeer;
-  int peer_sync;
   uint16_t* gpeer[kPeerMax];
   uint16_t* ppeer[kPeerMax];
 };

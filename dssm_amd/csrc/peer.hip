@@ -22,10 +22,12 @@
 //
 // Memory: the stage, the parameter wire, the tail stage and the flags are fine-grained device
 // allocations (hipDeviceMallocFinegrained: coherent across agents while kernels run), exported with
-// hipIpcGetMemHandle.  Every producing workgroup drains its stores (s_waitcnt vmcnt(0)), joins a
-// barrier and issues a SYSTEM-scope release (the flag is raised by a later kernel or workgroup that
-// observed it); flags are system-scope atomics; the poll is a system-scope atomic read-modify-write
-// (never a cached load); every consuming workgroup issues a system-scope acquire before its loads.
+// hipIpcGetMemHandle.  Producers store plainly; a flag is raised only by a later launch whose
+// workgroups (at least one per XCD) each issue a SYSTEM-scope release -- the write-back of that
+// XCD's L2 -- and whose last workgroup then stores the flags (system-scope atomics).  The wait
+// polls with system-scope atomic loads, and every consumer reads the payload with system-scope
+// loads (launch.h ld_sys8): measured on one GPU across two processes, plain loads behind a
+// system-scope acquire read stale rows, system-scope loads did not.
 // Waits are bounded (a timeout sets flags[ERR]; later waits return at once; the host reads it with
 // dssm_plan_peer_status), so a peer that never arrives cannot hang the GPU.
 #include <cstring>
@@ -44,8 +46,10 @@ __device__ __forceinline__ unsigned sys_poll(unsigned* p) {
   return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The tail's partial of this rank into slot `rank` of every rank's tail stage; the last workgroup
-// advances the epoch and raises this rank's GRAD flag on every rank.
+// The tail's partial of this rank into slot `rank` of every rank's tail stage; every workgroup then
+// writes back its XCD's L2 at system scope (at least kSignalBlocks workgroups: every XCD's, so the
+// gradient pass's rows stored in the launch before leave too), and the last workgroup advances the
+// epoch and raises this rank's GRAD flag on every rank.
 __global__ __launch_bounds__(256) void k_peer_tail_push(PeerArgs a) {
   const int64_t n4 = a.tailn / 4;
   const float4* src = reinterpret_cast<const float4*>(a.tail_src);
@@ -92,10 +96,8 @@ __global__ __launch_bounds__(64) void k_peer_wait(unsigned* flags, int base, int
 }
 
 // The world's tail partials summed in rank order into the gradient arena's tail (the Adam shard
-// consumes and clears it).
+// consumes and clears it); system-scope loads.
 __global__ __launch_bounds__(256) void k_peer_tail_sum(PeerArgs a) {
-  if (threadIdx.x == 0) peer_acquire();
-  __syncthreads();
   const int64_t n4 = a.tailn / 4;
   const float* t = a.rtail[a.rank];
   auto ld4 = [](const float* p) {
@@ -115,21 +117,26 @@ __global__ __launch_bounds__(256) void k_peer_tail_sum(PeerArgs a) {
   }
 }
 
-// After this rank's Adam shard (every workgroup of which released its parameter-wire stores):
-// this step's PARAM flag on every rank.
+// After this rank's Adam shard: every XCD's L2 written back at system scope (kSignalBlocks one-wave
+// workgroups, dispatched round-robin over the 8 XCDs, each releasing its XCD's dirty lines -- the
+// parameter-wire rows Adam stored there), then the last of them raises this step's PARAM flag on
+// every rank.
+constexpr int kSignalBlocks = 64;
 __global__ __launch_bounds__(64) void k_peer_signal(PeerArgs a) {
-  const int k = threadIdx.x;
+  if (threadIdx.x != 0) return;
   peer_release();
-  if (k >= a.world) return;
+  const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != gridDim.x - 1) return;
+  __hip_atomic_store(a.flags + kPeerTicket2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  peer_acquire();
+  peer_release();
   const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(a.rflags[k] + kPeerParam + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int k = 0; k < a.world; ++k)
+    __hip_atomic_store(a.rflags[k] + kPeerParam + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// W1's bf16 shadow from the parameter wire (tight rows of stride geo.n, chunks == 1), behind an
-// acquire in every workgroup.
+// W1's bf16 shadow from the parameter wire (tight rows of stride geo.n, chunks == 1); system-scope loads.
 __global__ __launch_bounds__(256) void k_peer_shadow(const u16* __restrict__ w, ShadowSeg g) {
-  if (threadIdx.x == 0) peer_acquire();
-  __syncthreads();
   const int q = g.cols / 4;
   const int64_t n4 = g.rows * q;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
@@ -149,7 +156,7 @@ int grid_of(int64_t n4) {
 hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
   if (a.world < 1 || a.world > kPeerMax || a.tailn % 4) return hipErrorInvalidValue;
   const int g = grid_of(a.tailn / 4);
-  hipLaunchKernelGGL(k_peer_tail_push, dim3(g), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_peer_tail_push, dim3(g < kSignalBlocks ? kSignalBlocks : g), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerGrad, a.world, ticks);
   hipLaunchKernelGGL(k_peer_tail_sum, dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -157,7 +164,7 @@ hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, 
 
 hipError_t launch_peer_after_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
   if (a.world < 1 || a.world > kPeerMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_peer_signal, dim3(kSignalBlocks), dim3(64), 0, s, a);
   hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerParam, a.world, ticks);
   return hipGetLastError();
 }
@@ -180,7 +187,12 @@ extern "C" {
 int dssm_peer_alloc(int64_t bytes, void** out) {
   if (!out || bytes <= 0) return perr(DSSM_E_INVALID, "dssm_peer_alloc: bytes > 0 and an output pointer");
   *out = nullptr;
+#ifdef DSSM_PEER_COARSE  // measurement: coarse-grained payload buffers (the flags buffer stays fine-grained)
+  hipError_t e = bytes == DSSM_PEER_FLAG_BYTES ? hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained)
+                                               : hipMalloc(out, (size_t)bytes);
+#else
   hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained);
+#endif
   if (e != hipSuccess) return perr(DSSM_E_HIP, std::string("hipExtMallocWithFlags(fine-grained): ") + hipGetErrorString(e));
   e = hipMemset(*out, 0, (size_t)bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();

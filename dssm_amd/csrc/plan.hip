@@ -1051,7 +1051,6 @@ static int launch_wire_gradient_pass(dssm_plan* P, hipStream_t s, int chunk) {
   if (P->peer_on()) {  // rank i's rows of owner j: block i of j's stage (the all-to-all's layout)
     const int64_t sub = P->sub_elems();
     a.npeer = P->peer.world;
-    a.peer_sync = 1;
     for (int j = 0; j < a.npeer; ++j)
       a.gpeer[j] = reinterpret_cast<uint16_t*>(reinterpret_cast<intptr_t>(P->peer.stage[j]) +
                                                (intptr_t)((int64_t)(P->dp_rank - j) * sub * 2));
@@ -1101,7 +1100,6 @@ static int dp_adam_chunk(dssm_plan* P, const dssm::AdamStep& base, int c, hipStr
   a.pwire_off4 = ((int64_t)c * P->geo.ww + P->dp_rank) * sub / 4 - a.d4_begin;
   if (P->peer_on()) {  // bf16(W1) of the shard into every rank's parameter wire
     a.npeer = P->peer.world;
-    a.peer_sync = 1;
     for (int k = 0; k < a.npeer; ++k) a.ppeer[k] = P->peer.pwire[k];
   }
   if (!last) {

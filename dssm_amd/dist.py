@@ -399,6 +399,39 @@ class PeerBuffers:
         self._release()
 
 
+class RehearsalPeers:
+    """bench.py --rehearse-world W --rehearse-comm peer: rank 0 of a W-rank peer exchange on ONE GPU.
+    Every rank's buffers are local allocations (so rank 0's kernels store the same bytes into W
+    stages / parameter wires / tail slots as on W GPUs, at HBM instead of xGMI speed), and the other
+    ranks' flags in rank 0's flags buffer are raised in advance, so its waits pass at once: the
+    compute share of the per-rank step, to which DESIGN §6 adds the link time."""
+
+    def __init__(self, world: int, wire_n: int, tail_n: int, device):
+        self.lib = _lib.load()
+        self.addr = {k: [] for k in PeerBuffers.KINDS}
+        sizes = {"stage": 2 * wire_n, "pwire": 2 * wire_n, "tail": 4 * world * tail_n,
+                 "flags": _lib.PEER_FLAG_BYTES}
+        for _ in range(world):
+            for k in PeerBuffers.KINDS:
+                p = C.c_void_p()
+                check(self.lib.dssm_peer_alloc(sizes[k], C.byref(p)), f"peer_alloc {k}")
+                self.addr[k].append(int(p.value))
+        self.stage = device_view(self.addr["stage"][0], wire_n, torch.bfloat16, device)
+        self.param_wire = device_view(self.addr["pwire"][0], wire_n, torch.bfloat16, device)
+        flags = device_view(self.addr["flags"][0], _lib.PEER_FLAG_BYTES // 4, torch.int32, device)
+        for base in (0, 64):  # DSSM peer flags GRAD / PARAM (csrc/launch.h kPeerGrad / kPeerParam)
+            flags[base + 1:base + world].fill_(0x7FFFFFFF)
+        torch.cuda.synchronize()
+
+    def close(self):
+        torch.cuda.synchronize()
+        self.stage = self.param_wire = None
+        for lst in self.addr.values():
+            for a in lst:
+                self.lib.dssm_peer_free(C.c_void_p(a))
+        self.addr = {}
+
+
 def shard_bounds(n_pad: int, n: int, rank: int, world: int):
     """Rank's optimizer shard of an arena of n elements padded to n_pad (equal shards)."""
     s = n_pad // world

@@ -74,7 +74,8 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     class FakeChild:
         def __init__(self, cmd, env=None, stdout=None, text=None, **kw):
             seen.append((cmd, env))
-            exch = {1: "zero/bf16 via rccl", 2: "allreduce via rccl"}.get(len(seen), "zero/bf16 sparse via rccl")
+            exch = {1: "zero/bf16 via rccl", 2: "allreduce via rccl", 3: "zero/bf16 sparse via rccl"}.get(
+                len(seen), "zero/bf16 via peer stores")
             head = {"value": 1.0, "ms_per_step": 2.0, "steps": 20, "warmup": 5, "unit": "pairs/s",
                     "config": {"dp_exchange": exch}, "dp_kernels_ms": {"adam": 0.05}}
             self.stdout = io.StringIO("progress\n" + json.dumps(head) + "\n") if stdout is not None else None
@@ -102,16 +103,19 @@ def test_gpus_n_spawns_its_own_ranks(monkeypatch, capsys):
     capsys.readouterr()
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
     assert bench.spawn_ranks(bench.parse()) == 0
-    assert len(seen) == 3
+    assert len(seen) == 4
+    off = ["--dp-alt", "0", "--dp-alt-sparse", "0", "--dp-alt-peer", "0"]
     assert seen[0][0][-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
-    assert seen[1][0][-8:] == ["--dp-mode", "allreduce", "--wire", "fp32", "--dp-alt", "0", "--dp-alt-sparse", "0"]
-    assert seen[2][0][-6:] == ["--dp-sparse", "1", "--dp-alt", "0", "--dp-alt-sparse", "0"]
+    assert seen[1][0][-10:] == ["--dp-mode", "allreduce", "--wire", "fp32"] + off
+    assert seen[2][0][-8:] == ["--dp-sparse", "1"] + off
+    assert seen[3][0][-8:] == ["--dp-exchange", "peer"] + off
     lines = [x for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["config"]["dp_exchange"] == "zero/bf16 via rccl"
     assert d["dp_alt"]["dp_exchange"] == "allreduce via rccl" and d["dp_alt"]["dp_kernels_ms"] == {"adam": 0.05}
     assert d["dp_alt_sparse"]["dp_exchange"] == "zero/bf16 sparse via rccl"
+    assert d["dp_alt_peer"]["dp_exchange"] == "zero/bf16 via peer stores"
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--backend", "gloo"])
     assert bench.parse().comm == "torch"
 

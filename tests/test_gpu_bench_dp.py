@@ -56,6 +56,14 @@ def test_bench_gpus2_spawns_ranks_and_checks_them():
     assert sp["dp_exchange"] == "zero/bf16 sparse tail-in-a2a via torch" and sp["value"] > 0
     assert sp["dp_check"]["ranks_identical"] is True and sp["dp_check"]["world"] == 2
     assert 0 < sp["dp_sparse"]["rows_sent_frac"] < 1 and sp["dp_sparse"]["steps"] >= 4
+    # the fourth child: the peer-store exchange (DataParallel(exchange="peer"), IPC-mapped buffers,
+    # one captured graph per region), its ranks bit-identical and no wait timed out
+    pe = d["dp_alt_peer"]
+    assert "error" not in pe, pe
+    assert pe["dp_exchange"] == "zero/bf16 via peer stores" and pe["value"] > 0
+    assert pe["dp_launch"] == "one graph per region, collectives captured"
+    assert pe["dp_check"]["ranks_identical"] is True and pe["dp_check"]["world"] == 2
+    assert pe["peer_status"]["error"] == 0 and pe["peer_status"]["steps"] >= 5, pe["peer_status"]
 
 
 @pytest.mark.gpu
@@ -68,13 +76,15 @@ def test_bench_multiview_gpus2_spawns_ranks_and_checks_them():
 
 
 @pytest.mark.gpu
-def test_bench_rehearsal_reports_dp_phases():
+@pytest.mark.parametrize("comm", ["copy", "peer"])
+def test_bench_rehearsal_reports_dp_phases(comm):
     """The captured data-parallel step graph (the one the RCCL ranks time) rehearsed on one GPU with
-    its collectives as device copies: the last step's phase probes are all recorded."""
+    its collectives as device copies, or as rank 0 of the peer-store exchange with the peers' buffers
+    local: the last step's phase probes are all recorded."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse-world", "8", "--rehearse-comm", "copy",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse-world", "8", "--rehearse-comm", comm,
            "--steps", "4", "--warmup", "2", "--cpu-baseline", "0", "--fp32-line", "0", "--det-line", "0",
            "--fwd-only", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
@@ -85,5 +95,8 @@ def test_bench_rehearsal_reports_dp_phases():
         assert k in ph, (k, ph)
     for k in ("fwd_bwd", "grad_pass", "all_to_all", "adam", "all_gather", "shadow_rebuild"):
         assert ph[k] > 0, (k, ph)
+    assert d["rehearsal"]["world"] == 8
+    if comm == "peer":
+        assert d["peer_status"]["error"] == 0 and d["peer_status"]["steps"] >= 6, d["peer_status"]
     # the step's phases fit inside its measured time
     assert sum(v for k, v in ph.items() if k != "source") <= 1.2 * d["ms_per_step"], (ph, d["ms_per_step"])
