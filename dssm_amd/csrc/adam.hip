@@ -543,6 +543,18 @@ __device__ __forceinline__ void adam_step_body(const AdamStep& a, const int blk,
         const uint2 q = reinterpret_cast<const uint2*>(a.gwire)[i];
         gg = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                          __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+      } else if (WIRE && a.ptail) {  // peer exchange: the world's tail partials, rank order
+        const float* t = a.ptail + (i * 4 - a.tail0);
+        uint2 lo = ld_sys8(t), hi = ld_sys8(t + 2);
+        gg = make_float4(__uint_as_float(lo.x), __uint_as_float(lo.y), __uint_as_float(hi.x), __uint_as_float(hi.y));
+        for (int k = 1; k < a.npeer; ++k) {
+          lo = ld_sys8(t + k * a.tailn);
+          hi = ld_sys8(t + k * a.tailn + 2);
+          gg.x += __uint_as_float(lo.x);
+          gg.y += __uint_as_float(lo.y);
+          gg.z += __uint_as_float(hi.x);
+          gg.w += __uint_as_float(hi.y);
+        }
       } else {
         gg = slab_grad4(a.slabs, i * 4, a.g);
       }
@@ -763,6 +775,8 @@ static hipError_t prepare_adam_step(AdamStep& a) {
   if (a.npeer && a.gout && (a.geo.wp != 1 || a.geo.ww != a.npeer || (a.n % 2))) return hipErrorInvalidValue;
   for (int k = 0; k < a.npeer; ++k)
     if ((a.gout && !a.gpeer[k]) || (!a.gout && !a.ppeer[k])) return hipErrorInvalidValue;
+  if (a.ptail && (!a.npeer || a.gout || a.tailn < 4 * (a.t4_end - a.t4_begin) || a.tail0 != 4 * a.t4_begin))
+    return hipErrorInvalidValue;
   const int64_t flat_rows = a.wchunk < 0 ? (int64_t)a.D + 1 : (int64_t)a.geo.ww * a.geo.ws;
 #ifdef DSSM_ADAM_SKIP_UNTOUCHED
   const int64_t n4 = a.d4_end - a.d4_begin + (a.t4_end - a.t4_begin) + 0 * flat_rows;

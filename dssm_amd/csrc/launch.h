@@ -361,11 +361,11 @@ struct PeerArgs {
   unsigned* rflags[kPeerMax]; // every rank's flags (rflags[rank] == flags)
   float* rtail[kPeerMax];     // every rank's tail stage ([world][tailn] fp32)
   const float* tail_src;      // this rank's tail gradient (the arena's [extent, param_count))
-  float* tail_dst;            // the same range: the rank-order sum is written back into it
   int64_t tailn;
+  unsigned long long ticks;   // wait bound (100 MHz counter)
 };
-hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s);
-hipError_t launch_peer_after_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s);
+hipError_t launch_peer_before_adam(const PeerArgs& a, hipStream_t s);
+hipError_t launch_peer_after_adam(const PeerArgs& a, hipStream_t s);
 
 struct AdamStep {
   float* p;
@@ -444,6 +444,10 @@ struct AdamStep {
   int npeer;
   uint16_t* gpeer[kPeerMax];
   uint16_t* ppeer[kPeerMax];
+  // Adam: the tail's gradient (float4 i in [t4_begin, t4_end)) is the rank-order sum of the npeer fp32
+  // partials ptail[k * tailn + 4 * i - tail0] (system-scope loads) instead of g
+  const float* ptail;
+  int64_t tailn, tail0;
 };
 constexpr int kAdamItemBlocks = DSSM_ADAM_ITEMS;  // persistent workgroups for the heavy W1 columns
 hipError_t launch_adam_step(AdamStep a, bool dz_bf16, hipStream_t s);

@@ -7,12 +7,14 @@
 //     while it computes them, so the link traffic runs under the pass instead of after it;
 //   * the fp32 tail (b1, W2.., BN: 0.5 MB) is pushed to every rank's tail stage (k_peer_tail_push),
 //     whose last workgroup raises this step's GRAD flag on every rank;
-//   * each rank waits for every rank's GRAD flag (k_peer_wait, one workgroup), sums the world's tails
-//     in rank order (k_peer_tail_sum: the replicated tail stays bit-identical on every rank), and its
-//     Adam shard sums the stage's partials in rank order as the all-to-all schedule does, storing
-//     bf16(W1) of its shard into EVERY rank's parameter wire;
-//   * k_peer_signal raises this step's PARAM flag on every rank; each rank waits for every PARAM
-//     flag and rebuilds W1's bf16 shadow from its parameter wire (k_peer_shadow).
+//   * the push's last workgroup then waits for every rank's GRAD flag; the Adam shard sums the
+//     world's tails in rank order (the replicated tail stays bit-identical on every rank) and the
+//     stage's partials in rank order as the all-to-all schedule does, storing bf16(W1) of its shard
+//     into EVERY rank's parameter wire;
+//   * k_peer_signal raises this step's PARAM flag on every rank and its last workgroup waits for
+//     every rank's; W1's bf16 shadow is then rebuilt from the parameter wire (k_peer_shadow).
+// Per step: two launches of their own (push + wait, signal + wait) and the shadow rebuild; a wait
+// is one wave of the launch's last workgroup, so it never holds more than one CU.
 // No collective library runs on the data path.  Steps are numbered by a per-rank epoch (flags[SEQ],
 // advanced by the tail push) and flags only grow, so nothing is re-armed between steps, graph
 // replays or regions.  Reuse is ordered by the flags themselves: rank i overwrites owner j's stage
@@ -46,6 +48,23 @@ __device__ __forceinline__ unsigned sys_poll(unsigned* p) {
   return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Lane k < world of the calling wave waits until flags[base + k] has reached epoch e (bounded by
+// `ticks` of the 100 MHz counter; a timeout records 1 + base + k in flags[ERR]; after any timeout
+// no wait waits again).
+__device__ void wait_flags(unsigned* flags, int base, int world, unsigned e, unsigned long long ticks) {
+  const int k = threadIdx.x;
+  if (k >= world) return;
+  if (__hip_atomic_load(flags + kPeerErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(sys_poll(flags + base + k) - e) < 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      __hip_atomic_store(flags + kPeerErr, (unsigned)(1 + base + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 // The tail's partial of this rank into slot `rank` of every rank's tail stage; every workgroup then
 // writes back its XCD's L2 at system scope (at least kSignalBlocks workgroups: every XCD's, so the
 // gradient pass's rows stored in the launch before leave too), and the last workgroup advances the
@@ -65,56 +84,26 @@ __global__ __launch_bounds__(256) void k_peer_tail_push(PeerArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  peer_release();
-  const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t != gridDim.x - 1) return;
-  __hip_atomic_store(a.flags + kPeerTicket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  peer_acquire();  // every workgroup's release (the ticket's RMW chain) before ...
-  const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  __hip_atomic_store(a.flags + kPeerSeq, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  peer_release();  // ... this workgroup's flags
-  for (int k = 0; k < a.world; ++k)
-    __hip_atomic_store(a.rflags[k] + kPeerGrad + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// One wave: lane k < world waits until flags[base + k] has reached this rank's epoch (bounded by
-// `ticks` of the 100 MHz counter; a timeout records 1 + base + k in flags[ERR]).
-__global__ __launch_bounds__(64) void k_peer_wait(unsigned* flags, int base, int world, unsigned long long ticks) {
-  const int k = threadIdx.x;
-  if (k >= world) return;
-  if (__hip_atomic_load(flags + kPeerErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const unsigned e = __hip_atomic_load(flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((int)(sys_poll(flags + base + k) - e) < 0) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-      __hip_atomic_store(flags + kPeerErr, (unsigned)(1 + base + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
+  __shared__ unsigned s_last;
+  if (threadIdx.x == 0) {
+    peer_release();
+    const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == gridDim.x - 1;
+    if (s_last) {
+      __hip_atomic_store(a.flags + kPeerTicket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      peer_acquire();  // every workgroup's release (the ticket's RMW chain) before ...
+      const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      __hip_atomic_store(a.flags + kPeerSeq, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      peer_release();  // ... this workgroup's flags
+      for (int k = 0; k < a.world; ++k)
+        __hip_atomic_store(a.rflags[k] + kPeerGrad + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_last = e;
     }
-    __builtin_amdgcn_s_sleep(8);
   }
-}
-
-// The world's tail partials summed in rank order into the gradient arena's tail (the Adam shard
-// consumes and clears it); system-scope loads.
-__global__ __launch_bounds__(256) void k_peer_tail_sum(PeerArgs a) {
-  const int64_t n4 = a.tailn / 4;
-  const float* t = a.rtail[a.rank];
-  auto ld4 = [](const float* p) {
-    const uint2 lo = ld_sys8(p), hi = ld_sys8(p + 2);
-    return make_float4(__uint_as_float(lo.x), __uint_as_float(lo.y), __uint_as_float(hi.x), __uint_as_float(hi.y));
-  };
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = ld4(t + 4 * i);
-    for (int k = 1; k < a.world; ++k) {
-      const float4 v = ld4(t + (int64_t)k * a.tailn + 4 * i);
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    reinterpret_cast<float4*>(a.tail_dst)[i] = s;
-  }
+  __syncthreads();
+  // the last workgroup stays for every rank's gradient pass of this step (the next launch, Adam,
+  // reads their rows)
+  if (s_last && threadIdx.x < 64) wait_flags(a.flags, kPeerGrad, a.world, s_last, a.ticks);
 }
 
 // After this rank's Adam shard: every XCD's L2 written back at system scope (kSignalBlocks one-wave
@@ -123,16 +112,25 @@ __global__ __launch_bounds__(256) void k_peer_tail_sum(PeerArgs a) {
 // every rank.
 constexpr int kSignalBlocks = 64;
 __global__ __launch_bounds__(64) void k_peer_signal(PeerArgs a) {
-  if (threadIdx.x != 0) return;
-  peer_release();
-  const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t != gridDim.x - 1) return;
-  __hip_atomic_store(a.flags + kPeerTicket2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  peer_acquire();
-  peer_release();
-  const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int k = 0; k < a.world; ++k)
-    __hip_atomic_store(a.rflags[k] + kPeerParam + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __shared__ unsigned s_e;
+  if (threadIdx.x == 0) {
+    peer_release();
+    const unsigned t = __hip_atomic_fetch_add(a.flags + kPeerTicket2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_e = 0;
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(a.flags + kPeerTicket2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      peer_acquire();
+      peer_release();
+      const unsigned e = __hip_atomic_load(a.flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < a.world; ++k)
+        __hip_atomic_store(a.rflags[k] + kPeerParam + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_e = e;
+    }
+  }
+  __syncthreads();
+  // the last workgroup stays for every rank's Adam shard of this step (the next launch rebuilds the
+  // shadow from the parameter wire they stored)
+  if (s_e) wait_flags(a.flags, kPeerParam, a.world, s_e, a.ticks);
 }
 
 // W1's bf16 shadow from the parameter wire (tight rows of stride geo.n, chunks == 1); system-scope loads.
@@ -153,19 +151,16 @@ int grid_of(int64_t n4) {
 
 }  // namespace
 
-hipError_t launch_peer_before_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
+hipError_t launch_peer_before_adam(const PeerArgs& a, hipStream_t s) {
   if (a.world < 1 || a.world > kPeerMax || a.tailn % 4) return hipErrorInvalidValue;
   const int g = grid_of(a.tailn / 4);
   hipLaunchKernelGGL(k_peer_tail_push, dim3(g < kSignalBlocks ? kSignalBlocks : g), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerGrad, a.world, ticks);
-  hipLaunchKernelGGL(k_peer_tail_sum, dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_peer_after_adam(const PeerArgs& a, unsigned long long ticks, hipStream_t s) {
+hipError_t launch_peer_after_adam(const PeerArgs& a, hipStream_t s) {
   if (a.world < 1 || a.world > kPeerMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_peer_signal, dim3(kSignalBlocks), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, s, a.flags, kPeerParam, a.world, ticks);
   return hipGetLastError();
 }
 

@@ -1101,6 +1101,11 @@ static int dp_adam_chunk(dssm_plan* P, const dssm::AdamStep& base, int c, hipStr
   if (P->peer_on()) {  // bf16(W1) of the shard into every rank's parameter wire
     a.npeer = P->peer.world;
     for (int k = 0; k < a.npeer; ++k) a.ppeer[k] = P->peer.pwire[k];
+    if (last) {  // the replicated tail's gradient: the world's pushed partials, summed in rank order
+      a.ptail = P->peer.tail[P->dp_rank];
+      a.tailn = P->Lt.total - P->wire_end();
+      a.tail0 = P->wire_end();
+    }
   }
   if (!last) {
     a.t4_begin = a.t4_end = 0;
@@ -1315,8 +1320,8 @@ static dssm::PeerArgs peer_args(const dssm_plan* P) {
   }
   const int64_t we = P->wire_end();
   a.tail_src = P->g + we;
-  a.tail_dst = P->g + we;
   a.tailn = P->Lt.total - we;
+  a.ticks = P->peer.wait_ticks;
   return a;
 }
 
@@ -1363,8 +1368,8 @@ int dssm_plan_peer_exchange(dssm_plan* P, int phase, void* stream) {
   if (!P->peer_on()) return fail(DSSM_E_INVALID, "no peer exchange set (dssm_plan_set_dp_peers)");
   hipStream_t s = (hipStream_t)stream;
   const dssm::PeerArgs a = peer_args(P);
-  if (phase == 0) HIP_TRY(dssm::launch_peer_before_adam(a, P->peer.wait_ticks, s));
-  else if (phase == 1) HIP_TRY(dssm::launch_peer_after_adam(a, P->peer.wait_ticks, s));
+  if (phase == 0) HIP_TRY(dssm::launch_peer_before_adam(a, s));
+  else if (phase == 1) HIP_TRY(dssm::launch_peer_after_adam(a, s));
   else return fail(DSSM_E_INVALID, "phase: 0 (before Adam) or 1 (after Adam)");
   return DSSM_OK;
 }
@@ -2027,8 +2032,8 @@ static int dp_collective(dssm_plan* P, const DpComm& k, int kind, int chunk, hip
   }
   if (k.mode == 3) {  // peer stores: the all-to-all happened inside the gradient pass (peer.hip)
     const dssm::PeerArgs a = peer_args(P);
-    if (kind == 0) HIP_TRY(dssm::launch_peer_before_adam(a, P->peer.wait_ticks, cs));
-    if (kind == 1) HIP_TRY(dssm::launch_peer_after_adam(a, P->peer.wait_ticks, cs));
+    if (kind == 0) HIP_TRY(dssm::launch_peer_before_adam(a, cs));
+    if (kind == 1) HIP_TRY(dssm::launch_peer_after_adam(a, cs));
     return DSSM_OK;  // kind 2: the tail rode in the push
   }
   uint16_t* gw = P->gwire + chunk * blk;
