@@ -259,7 +259,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, steps):
+def _worker(rank, world, port, out_dir, steps, delay_rank=-1):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -274,7 +274,11 @@ def _worker(rank, world, port, out_dir, steps):
         diag = []
         try:
             geo = m.dp_geometry()
+            import time
             for i in range(steps):  # eager steps, then the last as a captured one-step region
+                if rank == delay_rank:  # uneven arrival: the other rank's waits spin for ~50 ms
+                    torch.cuda.synchronize()
+                    time.sleep(0.05)
                 if i < steps - 1:
                     ip, ix, vv = batches[rank][i]
                     m.set_batch(indptr=ip, indices=ix, values=vv)
@@ -299,12 +303,15 @@ def _worker(rank, world, port, out_dir, steps):
         dist.destroy_process_group()
 
 
-def test_peer_world2_two_processes_ipc():
+@pytest.mark.parametrize("delay_rank", [-1, 0, 1])
+def test_peer_world2_two_processes_ipc(delay_rank):
+    """delay_rank: that rank sleeps 50 ms (idle GPU) before each of its steps, so the other rank's
+    waits spin until its flags arrive late (uneven load on the hand-offs)."""
     import torch.multiprocessing as mp
     W, steps = 2, 3
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(functools.partial(_worker), args=(W, _free_port(), d, steps), nprocs=W,
+        mp.start_processes(functools.partial(_worker), args=(W, _free_port(), d, steps, delay_rank), nprocs=W,
                            start_method="spawn", join=True)
         z = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(W)]
     for r in range(W):
