@@ -280,3 +280,24 @@ def test_data_parallel_gloo(mode, wire, chunks, world):
         well = np.abs(gmean[k]) > 1e-3 * np.abs(gmean[k]).max()
         assert diff[well].max(initial=0.0) <= 1e-5, (k, diff[well].max(initial=0.0))
         assert diff.max() <= 2 * 0.01, k
+
+
+@pytest.mark.parametrize("kw", [dict(chunks=3), dict(sparse=True), dict(wire="fp32"), dict(mode="allreduce"),
+                                dict(exchange="rings")])
+def test_peer_exchange_arguments_refused(kw):
+    """DataParallel(exchange="peer") is the zero schedule on the bf16 wire in one chunk with a bf16
+    HIP-engine model; anything else is refused before any buffer is allocated (the CPU engine,
+    an fp32 model without dssm_plan_set_dp_peers, is refused too)."""
+    from dssm_amd.dist import DataParallel
+    eng = CpuEngine(O.init_params(O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS, neg=NEG), seed=3), 1)
+    args = dict(exchange="peer")
+    args.update(kw)
+    with pytest.raises(ValueError):
+        DataParallel(eng, **args)
+
+
+def test_peer_exchange_needs_a_hip_model():
+    from dssm_amd.dist import DataParallel
+    eng = CpuEngine(O.init_params(O.OracleConfig(trigram_d=D, widths=WIDTHS, query_bs=BS, neg=NEG), seed=3), 1)
+    with pytest.raises(ValueError, match="bf16 HIP-engine"):
+        DataParallel(eng, exchange="peer")
