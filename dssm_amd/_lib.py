@@ -218,6 +218,7 @@ _SIGS = {
     # peer-store exchange (csrc/peer.hip)
     "dssm_peer_alloc": (C.c_int, [C.c_int64, _P]),
     "dssm_peer_free": (C.c_int, [_P]),
+    "dssm_peer_can_access": (C.c_int, [C.c_int, _P]),
     "dssm_ipc_handle": (C.c_int, [_P, _P]),
     "dssm_ipc_open": (C.c_int, [_P, _P]),
     "dssm_ipc_close": (C.c_int, [_P]),

@@ -205,6 +205,19 @@ int dssm_peer_free(void* p) {
   return e == hipSuccess ? DSSM_OK : perr(DSSM_E_HIP, std::string("hipFree: ") + hipGetErrorString(e));
 }
 
+int dssm_peer_can_access(int peer_device, int* out) {
+  if (!out) return perr(DSSM_E_INVALID, "dssm_peer_can_access: null output");
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess && dev == peer_device) {  // the same device (ranks sharing one GPU)
+    *out = 1;
+    return DSSM_OK;
+  }
+  if (e == hipSuccess) e = hipDeviceCanAccessPeer(out, dev, peer_device);
+  if (e != hipSuccess) return perr(DSSM_E_HIP, std::string("hipDeviceCanAccessPeer: ") + hipGetErrorString(e));
+  return DSSM_OK;
+}
+
 int dssm_ipc_handle(void* p, void* out64) {
   if (!p || !out64) return perr(DSSM_E_INVALID, "dssm_ipc_handle: null argument");
   static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle larger than 64 bytes");

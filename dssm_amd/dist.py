@@ -358,11 +358,25 @@ class PeerBuffers:
                 h = C.create_string_buffer(64)
                 check(self.lib.dssm_ipc_handle(C.c_void_p(self.own[k]), h), f"ipc_handle {k}")
                 handles[k] = h.raw
+            handles["device"] = torch.cuda.current_device()
             allh = [None] * world
             if world > 1:
                 dist.all_gather_object(allh, handles)
             else:
                 allh[0] = handles
+            # every rank's device must be able to map every other rank's (hipDeviceCanAccessPeer)
+            # before any handle is opened: an unsupported pair raises here, not as a GPU fault
+            ok = C.c_int(0)
+            bad = []
+            for r in range(world):
+                check(self.lib.dssm_peer_can_access(int(allh[r]["device"]), C.byref(ok)), "peer_can_access")
+                if not ok.value:
+                    bad.append(r)
+            dev = torch.device("cuda", torch.cuda.current_device())
+            all_ok = agree(not bad, dev) if world > 1 else not bad
+            if not all_ok:
+                raise RuntimeError(f"peer exchange: this device cannot access the devices of ranks {bad} "
+                                   "(or another rank's cannot): use the collective exchange")
             self.addr = {k: [0] * world for k in self.KINDS}
             for r in range(world):
                 for k in self.KINDS:

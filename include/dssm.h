@@ -566,6 +566,9 @@ int dssm_comm_destroy(void);
 #define DSSM_PEER_FLAG_BYTES 4096
 int dssm_peer_alloc(int64_t bytes, void** out);
 int dssm_peer_free(void* ptr);
+/* *out = 1 when the current device can map peer_device's memory (hipDeviceCanAccessPeer; the same
+ * device: 1): DataParallel checks every pair before opening any peer's handle. */
+int dssm_peer_can_access(int peer_device, int* out);
 int dssm_ipc_handle(void* ptr, void* out64);
 int dssm_ipc_open(const void* handle64, void** out);
 int dssm_ipc_close(void* ptr);

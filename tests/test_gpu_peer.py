@@ -229,6 +229,15 @@ def test_peer_world2_in_process_equal_emulated_collectives():
         free()
 
 
+def test_peer_can_access_same_device():
+    """dssm_peer_can_access: the same device is always mappable (ranks sharing one GPU)."""
+    from dssm_amd import _lib
+    lib = _lib.load()
+    ok = _lib.C.c_int(0)
+    _lib.check(lib.dssm_peer_can_access(torch.cuda.current_device(), _lib.C.byref(ok)), "peer_can_access")
+    assert ok.value == 1
+
+
 def test_peer_timeout_is_bounded_and_reported():
     """Rank 1 never runs: rank 0's first wait times out after the bound, records the flag it waited
     on (GRAD of rank 1 = 1 + 0 + 1), and every later wait returns at once."""
