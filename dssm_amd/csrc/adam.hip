@@ -207,7 +207,7 @@ __device__ __forceinline__ void w1_row(const AdamStep& a, int c, int s, int e, f
         uint2 hi;
         hi.x = pack2bf(G[4], G[5]);
         hi.y = pack2bf(G[6], G[7]);
-        if (a.npeer) {  // peer exchange: system-scope stores into the owner's stage
+        if (a.npeer) {  // peer exchange: into the owner's stage (launch.h st_sys8)
           st_sys8(q, lo);
           if (k == 8) st_sys8(q + 4, hi);
         } else {
