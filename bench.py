@@ -1202,6 +1202,8 @@ def main():
                             "note": "rank 0 of an N-rank bf16-wire step on one GPU; not a headline number"}
     if (dp is not None and dp.peer is not None) or (rehearse > 1 and args.rehearse_comm == "peer"):
         out["peer_status"] = model.peer_status()
+        if dp is not None:
+            out["peer_status"]["selftest_mismatches"] = dp.peer_selftest
         if out["peer_status"]["error"]:
             raise SystemExit(f"bench: the peer exchange timed out: {out['peer_status']}")
     if dp is not None:

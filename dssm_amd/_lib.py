@@ -226,6 +226,7 @@ _SIGS = {
     "dssm_plan_set_peer_timeout": (C.c_int, [_P, C.c_double]),
     "dssm_plan_peer_exchange": (C.c_int, [_P, C.c_int, _P]),
     "dssm_plan_peer_status": (C.c_int, [_P, _P]),
+    "dssm_plan_peer_selftest": (C.c_int, [_P, _P, _P]),
 }
 PEER_FLAG_BYTES = 4096  # include/dssm.h DSSM_PEER_FLAG_BYTES
 

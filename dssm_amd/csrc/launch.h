@@ -366,6 +366,11 @@ struct PeerArgs {
 };
 hipError_t launch_peer_before_adam(const PeerArgs& a, hipStream_t s);
 hipError_t launch_peer_after_adam(const PeerArgs& a, hipStream_t s);
+// start-up self-test: patterns into every rank's tail slot / parameter-wire shard block, released,
+// flagged and read back with system-scope loads; mismatches added to *bad (pw_dev: a device array of
+// the world's parameter-wire pointers)
+hipError_t launch_peer_selftest(const PeerArgs& a, uint16_t* const* pw_dev, const uint16_t* pw_local, int64_t sub,
+                                unsigned* bad, hipStream_t s);
 
 struct AdamStep {
   float* p;

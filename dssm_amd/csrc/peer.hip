@@ -133,6 +133,44 @@ __global__ __launch_bounds__(64) void k_peer_signal(PeerArgs a) {
   if (s_e) wait_flags(a.flags, kPeerParam, a.world, s_e, a.ticks);
 }
 
+// ---- start-up self-test (dssm_plan_peer_selftest) -------------------------------------------------
+// Synthetic patterns through the exchange's own store / release / flag / load path: every rank stores
+// pattern(rank, j) plainly into its slot of every rank's tail stage and into its shard block of every
+// rank's parameter wire; k_peer_signal writes back every XCD's L2, raises the flags and waits; then
+// every rank reads all W slots and blocks back with system-scope loads and counts mismatches.
+__device__ __forceinline__ float tail_pattern(int r, int64_t j) { return (float)((r + 1) * 4096 + (int)(j & 4095)); }
+__device__ __forceinline__ unsigned short wire_pattern(int r, int64_t j) {
+  return (unsigned short)((r * 40503u + (unsigned)j * 2654435761u) >> 16);
+}
+__global__ void k_peer_seq_bump(unsigned* flags) {
+  const unsigned e = __hip_atomic_load(flags + kPeerSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(flags + kPeerSeq, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(256) void k_peer_fill(PeerArgs a, uint16_t* const* pw, int64_t sub) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.tailn; j += stride)
+    for (int k = 0; k < a.world; ++k) a.rtail[k][a.rank * a.tailn + j] = tail_pattern(a.rank, j);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < sub; j += stride)
+    for (int k = 0; k < a.world; ++k) pw[k][a.rank * sub + j] = wire_pattern(a.rank, j);
+}
+__global__ __launch_bounds__(256) void k_peer_check(PeerArgs a, const uint16_t* pw, int64_t sub, unsigned* bad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned nb = 0;
+  const float* t = a.rtail[a.rank];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.world * a.tailn / 2; i += stride) {
+    const int64_t e = 2 * i, r = e / a.tailn, j = e - r * a.tailn;  // tailn is even: a pair never straddles
+    const uint2 q = ld_sys8(t + e);
+    nb += (__uint_as_float(q.x) != tail_pattern((int)r, j)) + (__uint_as_float(q.y) != tail_pattern((int)r, j + 1));
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.world * sub / 4; i += stride) {
+    const int64_t e = 4 * i, r = e / sub, j = e - r * sub;  // sub is a multiple of 4
+    const uint2 q = ld_sys8(pw + e);
+    nb += ((q.x & 0xffffu) != wire_pattern((int)r, j)) + ((q.x >> 16) != wire_pattern((int)r, j + 1)) +
+          ((q.y & 0xffffu) != wire_pattern((int)r, j + 2)) + ((q.y >> 16) != wire_pattern((int)r, j + 3));
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+
 // W1's bf16 shadow from the parameter wire (tight rows of stride geo.n, chunks == 1); system-scope loads.
 __global__ __launch_bounds__(256) void k_peer_shadow(const u16* __restrict__ w, ShadowSeg g) {
   const int q = g.cols / 4;
@@ -161,6 +199,16 @@ hipError_t launch_peer_before_adam(const PeerArgs& a, hipStream_t s) {
 hipError_t launch_peer_after_adam(const PeerArgs& a, hipStream_t s) {
   if (a.world < 1 || a.world > kPeerMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_peer_signal, dim3(kSignalBlocks), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_selftest(const PeerArgs& a, uint16_t* const* pw_dev, const uint16_t* pw_local, int64_t sub,
+                                unsigned* bad, hipStream_t s) {
+  if (a.world < 1 || a.world > kPeerMax || (a.tailn % 2) || (sub % 4)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_peer_seq_bump, dim3(1), dim3(1), 0, s, a.flags);
+  hipLaunchKernelGGL(k_peer_fill, dim3(512), dim3(256), 0, s, a, pw_dev, sub);
+  hipLaunchKernelGGL(k_peer_signal, dim3(kSignalBlocks), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_peer_check, dim3(512), dim3(256), 0, s, a, pw_local, sub, bad);
   return hipGetLastError();
 }
 

@@ -229,6 +229,10 @@ struct dssm_plan {
     unsigned* flags[dssm::kPeerMax] = {};
     unsigned long long wait_ticks = 2000000000ull;  // 20 s of the 100 MHz counter
   } peer;
+  // the peer self-test's device scratch ([kPeerMax] parameter-wire pointers + a counter), allocated
+  // once by dssm_plan_set_dp_peers (no allocation, hence no device-wide synchronisation, inside the
+  // self-test: ranks sharing a GPU run theirs concurrently)
+  void* peer_scratch = nullptr;
   bool peer_on() const { return peer.world > 0 && pwire != nullptr; }
   bool dp_defer_gradpass = false;  // the data-parallel graph builder launches the chunks itself
   // the data-parallel graph builder's hook after each Adam chunk launch (that chunk's all-gather)
@@ -542,6 +546,7 @@ int dssm_plan_create(const dssm_config* cfg, void* workspace, size_t workspace_b
 
 int dssm_plan_destroy(dssm_plan* plan) {
   if (plan) {
+    if (plan->peer_scratch) (void)hipFree(plan->peer_scratch);
     for (auto& p : plan->probe)
       for (hipEvent_t e : p.ev) hipEventDestroy(e);
     for (auto* g : plan->graphs) {
@@ -1344,6 +1349,7 @@ int dssm_plan_set_dp_peers(dssm_plan* P, int world, uint16_t* const* stages, uin
     if (!stages[k] || !param_wires[k] || !tails[k] || !flags[k]) return fail(DSSM_E_INVALID, "null peer buffer");
   if (stages[P->dp_rank] != P->gstage || param_wires[P->dp_rank] != P->pwire)
     return fail(DSSM_E_INVALID, "this rank's stage and parameter wire must be the wire's (dssm_plan_set_dp_wire)");
+  if (!P->peer_scratch) HIP_TRY(hipMalloc(&P->peer_scratch, sizeof(uint16_t*) * dssm::kPeerMax + 64));
   dssm_plan::PeerSet ps;
   ps.world = world;
   ps.wait_ticks = P->peer.wait_ticks;
@@ -1371,6 +1377,28 @@ int dssm_plan_peer_exchange(dssm_plan* P, int phase, void* stream) {
   if (phase == 0) HIP_TRY(dssm::launch_peer_before_adam(a, s));
   else if (phase == 1) HIP_TRY(dssm::launch_peer_after_adam(a, s));
   else return fail(DSSM_E_INVALID, "phase: 0 (before Adam) or 1 (after Adam)");
+  return DSSM_OK;
+}
+
+int dssm_plan_peer_selftest(dssm_plan* P, int64_t* mismatches, void* stream) {
+  if (!P || !mismatches) return fail(DSSM_E_INVALID, "null argument");
+  if (!P->peer_on()) return fail(DSSM_E_INVALID, "no peer exchange set (dssm_plan_set_dp_peers)");
+  if (P->capturing) return fail(DSSM_E_INVALID, "the self-test cannot be captured");
+  hipStream_t s = (hipStream_t)stream;
+  const dssm::PeerArgs a = peer_args(P);
+  const int W = P->peer.world;
+  void* dev = P->peer_scratch;  // [W] parameter-wire pointers + the mismatch counter
+  uint16_t** pw = static_cast<uint16_t**>(dev);
+  unsigned* bad = reinterpret_cast<unsigned*>(static_cast<char*>(dev) + sizeof(uint16_t*) * dssm::kPeerMax);
+  hipError_t e = hipMemcpyAsync(pw, P->peer.pwire, sizeof(uint16_t*) * W, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(unsigned), s);
+  if (e == hipSuccess) e = dssm::launch_peer_selftest(a, pw, P->pwire, P->sub_elems(), bad, s);
+  unsigned nb = 0, err = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&nb, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(&err, a.flags + dssm::kPeerErr, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(DSSM_E_HIP, std::string("peer self-test: ") + hipGetErrorString(e));
+  *mismatches = err ? -1 : (int64_t)nb;  // -1: a wait timed out
   return DSSM_OK;
 }
 

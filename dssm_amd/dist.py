@@ -542,6 +542,13 @@ class DataParallel:
                 torch.cuda.synchronize()
                 if self.world > 1:
                     dist.barrier()  # every rank's zeroed flags attached before any rank's first step
+                # the exchange's store / release / flag / load path checked at the real world size with
+                # synthetic patterns (dssm_plan_peer_selftest); any mismatch on any rank raises
+                self.peer_selftest = model.peer_selftest()
+                ok = self.peer_selftest == 0
+                if not (agree(ok, dev) if self.world > 1 else ok):
+                    raise RuntimeError(f"peer exchange self-test failed on some rank (this rank: "
+                                       f"{self.peer_selftest} mismatching elements, -1 = timed out)")
             geo = model.dp_geometry()
             self.extent, self.sub = geo["extent"], geo["sub"]
             self.begin, self.end = geo["shard_begin"], geo["shard_end"]

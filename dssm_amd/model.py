@@ -312,6 +312,12 @@ class DSSM:
         """dssm_plan_peer_exchange: phase 0 between backward and Adam, 1 after Adam."""
         check(self.lib.dssm_plan_peer_exchange(self._plan, int(phase), stream_ptr(stream)), "peer_exchange")
 
+    def peer_selftest(self, stream=None) -> int:
+        """dssm_plan_peer_selftest: mismatching elements of the synthetic exchange (-1: timed out)."""
+        out = C.c_int64(0)
+        check(self.lib.dssm_plan_peer_selftest(self._plan, C.byref(out), stream_ptr(stream)), "peer_selftest")
+        return int(out.value)
+
     def peer_status(self) -> Dict[str, int]:
         """{error: 0 or 1 + the flag index a wait timed out on, steps: exchanged steps} (synchronous)."""
         out = (C.c_uint * 2)()

@@ -577,6 +577,12 @@ int dssm_plan_set_dp_peers(dssm_plan* plan, int world, uint16_t* const* stages, 
 int dssm_plan_set_peer_timeout(dssm_plan* plan, double ms);
 int dssm_plan_peer_exchange(dssm_plan* plan, int phase, void* stream);
 int dssm_plan_peer_status(const dssm_plan* plan, unsigned* out2);
+/* Start-up self-test at the real world size (every rank calls it once, together, before its first
+ * step): each rank stores a synthetic pattern into its slot of every rank's tail stage and its shard
+ * block of every rank's parameter wire, releases and flags as a step does, and reads all slots and
+ * blocks back with the consumers' system-scope loads.  *mismatches = elements that differ (0: pass;
+ * -1: a wait timed out).  Synchronous; the buffers it writes are overwritten by the next step. */
+int dssm_plan_peer_selftest(dssm_plan* plan, int64_t* mismatches, void* stream);
 /* Packed rows of the sparse exchange, stride n + 4 u16: [row id int32][pad][n u16 of src row id].
  * pack: packed row k from src row rows[k] (n % 4 == 0); unpack: dst row (id - row_base) = packed row
  * k's data for ids in [row_base, row_base + nrows) (others skipped). */

@@ -173,6 +173,7 @@ def test_peer_world1_eager_and_graph_equal_wire_schedule():
     dp = DataParallel(m, exchange="peer", peer_timeout_ms=TIMEOUT_MS)
     try:
         assert dp.schedule == "zero/bf16 via peer stores" and dp.capturable
+        assert dp.peer_selftest == 0
         batches = _batches(steps, 500)
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
@@ -229,6 +230,41 @@ def test_peer_world2_in_process_equal_emulated_collectives():
         free()
 
 
+def test_peer_selftest_in_process_and_after_steps():
+    """dssm_plan_peer_selftest at world 2 in one process (the two ranks' self-tests on two streams,
+    each waiting for the other's flags), before and between steps: 0 mismatches, and the steps
+    around it still equal the emulated collectives bit for bit."""
+    import threading
+    W, steps = 2, 2
+    e = Emulated(W)
+    models, bufs, free = _peer_in_process(W)
+    try:
+        streams = [torch.cuda.Stream() for _ in range(W)]
+        per_rank = [_batches(steps, 1300, r) for r in range(W)]
+        out = [None] * W
+
+        def st(r):  # the self-test synchronizes its stream: the ranks run it from two host threads
+            with torch.cuda.stream(streams[r]):
+                out[r] = models[r].peer_selftest()
+        for i in range(steps):
+            th = [threading.Thread(target=st, args=(r,)) for r in range(W)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(60)
+            assert out == [0] * W, out
+            for r in range(W):
+                with torch.cuda.stream(streams[r]):
+                    _peer_step(models[r], per_rank[r][i], W)
+            e.step([per_rank[r][i] for r in range(W)])
+        torch.cuda.synchronize()
+        for r in range(W):
+            assert models[r].peer_status()["error"] == 0
+            _compare(models[r], e.models[r], bufs[r]["pwire_t"], e.wires[r][2])
+    finally:
+        free()
+
+
 def test_peer_can_access_same_device():
     """dssm_peer_can_access: the same device is always mappable (ranks sharing one GPU)."""
     from dssm_amd import _lib
@@ -279,6 +315,7 @@ def _worker(rank, world, port, out_dir, steps, delay_rank=-1):
         batches = [_batches(steps, 1100, r) for r in range(world)]  # every rank's shard (for the emulation)
         m = _model()
         dp = DataParallel(m, comm="torch", exchange="peer", peer_timeout_ms=TIMEOUT_MS)
+        assert dp.peer_selftest == 0  # the synthetic exchange across the two processes
         e = Emulated(world)
         diag = []
         try:
