@@ -319,10 +319,10 @@ __device__ __forceinline__ void peer_acquire() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 // payload accesses of the peer exchange, 8-B aligned.  Loads: system-scope relaxed atomic loads
-// (global_load ... sc0 sc1, as the flag polls): measured necessary -- with plain loads behind a
-// system-scope acquire the second process read stale stage rows through its IPC-shared buffers
-// (DESIGN §6).  Stores: plain (measured sufficient; the signalling launches write back every XCD's
-// L2 at system scope before the flag).  Build knobs (measurement): DSSM_PEER_ST 1 makes the stores
+// (global_load ... sc0 sc1, as the flag polls) -- coherent whatever the reader's L2 holds; in the
+// exchange's first design, plain loads behind a system-scope acquire read stale stage rows in the
+// second of two processes sharing IPC buffers.  Stores: plain (the signalling launches
+// write back every XCD's L2 at system scope before the flag).  Build knobs (measurement): DSSM_PEER_ST 1 makes the stores
 // system-scope atomics too, DSSM_PEER_LD 0 makes the loads plain.
 #ifndef DSSM_PEER_ST
 #define DSSM_PEER_ST 0

@@ -28,8 +28,9 @@
 // workgroups (at least one per XCD) each issue a SYSTEM-scope release -- the write-back of that
 // XCD's L2 -- and whose last workgroup then stores the flags (system-scope atomics).  The wait
 // polls with system-scope atomic loads, and every consumer reads the payload with system-scope
-// loads (launch.h ld_sys8): measured on one GPU across two processes, plain loads behind a
-// system-scope acquire read stale rows, system-scope loads did not.
+// loads (launch.h ld_sys8; in the first design, plain loads behind a system-scope acquire read stale
+// rows across two processes on one GPU).  Before the first step every rank runs the
+// self-test below through the same path with synthetic patterns (dssm_plan_peer_selftest).
 // Waits are bounded (a timeout sets flags[ERR]; later waits return at once; the host reads it with
 // dssm_plan_peer_status), so a peer that never arrives cannot hang the GPU.
 #include <cstring>
