@@ -861,6 +861,8 @@ class DataParallel:
     def close(self):
         if self.peer is not None:
             self.model.set_dp_peers(0, None, None, None, None)
+            self.model.set_dp_wire()  # detach: the stage / parameter wire are about to be freed
+            self.stage = self.param_wire = None  # views of the freed buffers
             self.peer.close()
             self.peer = None
         if self.tx is not None:
